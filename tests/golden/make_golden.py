@@ -1,0 +1,213 @@
+"""Generate the golden vectors under tests/golden/ by importing the reference (``/root/reference/nof``) on CPU.
+
+Run in the build container only (the reference does not travel to the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What it pins: Embedding + NOF eval/train forward, render_rays_val, render_rays_train in the
+PC-NeRF / OriginalNeRF configurations (child losses on/off, segmented sampling on/off, per-child divide on/off,
+perturbation with recorded RNG draws), sample_pdf incl. the denom<1e-5 branch, the two-step
+render_rays_view_0525_2_2 (methods 0 and 2), and the range loss of ``train_kitti.py:121-155`` computed with the
+reference's own ``nof.criteria`` loss classes.
+
+Only one shim is applied: ``nof/render.py:397`` moves ``u`` to ``"cuda:0"``; on this CPU-only container that
+device move is turned into a no-op so the identical arithmetic runs on CPU.
+
+Inputs are synthetic (checkpoints and child-AABB clouds are absent from the reference): weights come from
+``nof.synthetic.init_nof_params(seed)`` and rays from ``nof.synthetic.make_rays`` -- both reproducible from the
+seeds stored in each fixture; the rays themselves are also stored so the fixtures stand alone.
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+
+# our synthetic-data module, loaded by path (our package is also called ``nof``)
+_spec = importlib.util.spec_from_file_location("pcnerf_synthetic", os.path.join(REPO, "pc-nerf_amd", "nof", "synthetic.py"))
+syn = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(syn)
+
+sys.path.insert(0, REF)
+import nof.render as R  # noqa: E402  (the reference)
+from nof.networks import Embedding, NOF_coarse, NOF_fine  # noqa: E402
+from nof.criteria import nof_loss  # noqa: E402
+
+_orig_to = torch.Tensor.to
+
+
+def _to_shim(self, *a, **k):  # render.py:397 ``u.to("cuda:0")`` -> stay on CPU
+    if a and isinstance(a[0], str) and a[0].startswith("cuda"):
+        return self
+    return _orig_to(self, *a, **k)
+
+
+torch.Tensor.to = _to_shim
+torch.set_num_threads(1)
+
+SEED_C, SEED_F = 1234, 5678
+
+
+def models(train):
+    emb = Embedding(3, 10)
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(SEED_C))
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(SEED_F))
+    mc.train(train)
+    mf.train(train)
+    return emb, mc, mf
+
+
+def running_stats(m):
+    out = []
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm1d):
+            out.append(torch.stack([mod.running_mean, mod.running_var]))
+    return torch.stack(out).numpy()
+
+
+def save(name, **arrs):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
+    print("wrote", path, sum(np.asarray(v).nbytes for v in arrs.values()), "bytes raw")
+
+
+def t(x):
+    return x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+
+
+def gen_nof():
+    rng = np.random.default_rng(7)
+    pts = rng.uniform(syn.PARENT_LO, syn.PARENT_HI, size=(2048, 3)).astype(np.float32)
+    emb, mc, _ = models(train=False)
+    with torch.no_grad():
+        e = emb(torch.from_numpy(pts))
+        p = mc(e)
+    save("nof_eval", points=pts, embedding=t(e), p=t(p), seed=SEED_C)
+
+    pts = rng.uniform(syn.PARENT_LO, syn.PARENT_HI, size=(4096, 3)).astype(np.float32)
+    emb, mc, _ = models(train=True)
+    chunk = 1000
+    out = []
+    with torch.no_grad():
+        for i in range(0, len(pts), chunk):  # render.py:47-50 chunk loop
+            out.append(mc(emb(torch.from_numpy(pts[i:i + chunk]))))
+    save("nof_train", points=pts, p=t(torch.cat(out)), chunk=chunk, running=running_stats(mc), seed=SEED_C)
+
+
+def gen_val():
+    for S, I, nr in ((64, 128, 256), (128, 256, 96)):
+        rays = syn.make_rays(nr, seed=11)
+        emb, mc, mf = models(train=False)
+        with torch.no_grad():
+            res = R.render_rays_val(mc, mf, emb, torch.from_numpy(rays), N_samples=S, N_importance=I,
+                                    perturb=0, noise_std=0, chunk=4096)
+        save(f"render_val_s{S}", rays=rays, N_samples=S, N_importance=I, chunk=4096,
+             depth=t(res["depth"]), depth_fine=t(res["depth_fine"]))
+
+
+TRAIN_CASES = {
+    # name: (use_child_nerf_loss, issegmentated, use_child_nerf_divide, perturb, S, I, ratio)
+    "pcnerf": (1, 1, 0, 0, 64, 128, 0.1),
+    "pcnerf_noseg": (1, 0, 0, 0, 64, 128, 0.1),
+    "pcnerf_divide": (1, 1, 1, 0, 64, 128, 0.1),
+    "original": (0, 0, 0, 0, 64, 128, 0.1),
+    "pcnerf_perturb": (1, 1, 0, 1, 64, 128, 0.1),
+    "pcnerf_s128": (1, 1, 0, 0, 128, 256, 0.1),
+}
+
+
+def range_losses(depth, depth_fine, gt, rays, divide, sub_num, lam=1.0, lam_fine=1.0):
+    """train_kitti.py:121-146 restated with the reference's own loss class (nof/criteria/loss.py:42-50)."""
+    loss = nof_loss["smoothl1"]()
+    if divide:
+        lr = torch.tensor([0])
+        lrf = torch.tensor([0])
+        sub = rays[:, 9]
+        for i in range(sub_num):
+            m = torch.logical_and(sub > (i + 0.5), sub < (i + 1.5))
+            if m.sum() >= 1:
+                lr = lr + 1e-1 * lam * loss(1e1 * depth[m], 1e1 * gt[m])
+                lrf = lrf + 1e-1 * lam_fine * loss(1e1 * depth_fine[m], 1e1 * gt[m])
+        return lr, lrf
+    return 1e-1 * lam * loss(1e1 * depth, 1e1 * gt), 1e-1 * lam * loss(1e1 * depth_fine, 1e1 * gt)
+
+
+def gen_train():
+    for name, (cl, seg, div, pert, S, I, ratio) in TRAIN_CASES.items():
+        nr = 256 if S == 64 else 64
+        rays = syn.make_rays(nr, seed=21)
+        if name == "pcnerf_noseg":
+            # shrink child intervals so some contain no coarse sample: exercises render.py:82-84 expand loop
+            mid = 0.5 * (rays[:, 10] + rays[:, 11])
+            rays[::3, 10] = mid[::3] - 0.02
+            rays[::3, 11] = mid[::3] + 0.02
+        emb, mc, mf = models(train=True)
+        torch.manual_seed(99)
+        # record the RNG draws in the order the reference consumes them (render.py:453,57,383,57)
+        F = S + I
+        g = torch.Generator().manual_seed(99)
+        draws = {}
+        if pert > 0:
+            draws["perturb_rand"] = torch.rand((nr, S), generator=g).numpy()
+            torch.randn((nr, S), generator=g)
+            draws["u"] = torch.rand((nr, I), generator=g).numpy()
+            torch.randn((nr, F), generator=g)
+        with torch.no_grad():
+            res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=32, N_samples=S,
+                                      N_importance=I, perturb=pert, noise_std=0, chunk=4096, issegmentated=seg,
+                                      childnerf_ratio=ratio, use_child_nerf_divide=div, use_child_nerf_loss=cl)
+            gt = torch.from_numpy(rays[:, 14])
+            lr, lrf = range_losses(res["depth"], res["depth_fine"], gt, torch.from_numpy(rays), div, 32)
+            total = lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"] + \
+                1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"]
+        save(f"render_train_{name}", rays=rays, N_samples=S, N_importance=I, chunk=4096, sub_nerf_test_num=32,
+             use_child_nerf_loss=cl, issegmentated=seg, use_child_nerf_divide=div, perturb=pert,
+             childnerf_ratio=ratio, depth=t(res["depth"]), depth_fine=t(res["depth_fine"]),
+             child_free_loss=t(res["child_free_loss"]), child_depth_loss=t(res["child_depth_loss"]),
+             child_free_loss_fine=t(res["child_free_loss_fine"]),
+             child_depth_loss_fine=t(res["child_depth_loss_fine"]),
+             loss_range=t(lr), loss_range_fine=t(lrf), loss_total=t(total),
+             running_c=running_stats(mc), running_f=running_stats(mf), **draws)
+
+
+def gen_pdf():
+    rng = np.random.default_rng(31)
+    nr, nb = 64, 33
+    bins = np.sort(rng.uniform(0, 30, size=(nr, nb)), axis=1).astype(np.float32)
+    w = rng.uniform(0, 1, size=(nr, nb - 1)).astype(np.float32) ** 8
+    w[::4, 5:20] = 0.0      # flat cdf runs: denom < 1e-5 branch (render.py:408)
+    w[1::8] = 0.0           # all-zero rows
+    w = (w / (w.sum(1, keepdims=True) + 1e-10)).astype(np.float32)
+    with torch.no_grad():
+        det = R.sample_pdf(torch.from_numpy(bins), torch.from_numpy(w), 96, det=True)
+        torch.manual_seed(5)
+        u = torch.rand((nr, 96))
+        torch.manual_seed(5)
+        rnd = R.sample_pdf(torch.from_numpy(bins), torch.from_numpy(w), 96, det=False)
+    save("sample_pdf", bins=bins, weights=w, samples_det=t(det), u=t(u), samples_rand=t(rnd))
+
+
+def gen_view():
+    rows, other, ranges = syn.make_view_rows(48, seed=41)
+    for method in (0, 2):
+        emb, mc, mf = models(train=False)
+        with torch.no_grad():
+            res = R.render_rays_view_0525_2_2(mc, mf, emb, torch.from_numpy(rows), torch.from_numpy(other),
+                                              N_samples=64, N_importance=128, perturb=0, noise_std=0,
+                                              chunk=4096, depth_inference_method=method)
+        save(f"render_view_m{method}", rows=rows, other=other, ranges=ranges, N_samples=64, N_importance=128,
+             depth_inference_method=method,
+             **{k: t(v) for k, v in res.items()})
+
+
+if __name__ == "__main__":
+    gen_nof()
+    gen_pdf()
+    gen_val()
+    gen_train()
+    gen_view()

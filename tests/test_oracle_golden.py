@@ -1,0 +1,99 @@
+"""Pin the CPU oracle (oracle/ref_cpu.py) against golden vectors made by importing the reference."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from nof import synthetic as syn
+from oracle import ref_cpu as O
+
+SEED_C, SEED_F = 1234, 5678
+torch.set_num_threads(1)  # goldens were made single-threaded: keep reduction orders identical
+
+
+def P(seed):
+    return O.params_from_numpy(syn.init_nof_params(seed))
+
+
+def close(a, b, rtol=1e-6, atol=1e-7):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol)
+
+
+def running(Pm):
+    return np.stack([np.stack([Pm[b + ".running_mean"].numpy(), Pm[b + ".running_var"].numpy()]) for b in O.BN])
+
+
+def test_embedding_and_nof_eval():
+    g = golden("nof_eval")
+    x = torch.from_numpy(g["points"])
+    e = O.embed(x)
+    close(e, g["embedding"], 0, 0)
+    close(O.nof_forward(P(SEED_C), e, False), g["p"])
+
+
+def test_nof_train_chunks_and_running_stats():
+    g = golden("nof_train")
+    Pm = P(SEED_C)
+    x = torch.from_numpy(g["points"])
+    c = int(g["chunk"])
+    p = torch.cat([O.nof_forward(Pm, O.embed(x[i:i + c]), True) for i in range(0, len(x), c)])
+    close(p, g["p"])
+    close(running(Pm), g["running"])
+
+
+def test_sample_pdf():
+    g = golden("sample_pdf")
+    b, w = torch.from_numpy(g["bins"]), torch.from_numpy(g["weights"])
+    close(O.sample_pdf(b, w, 96, det=True), g["samples_det"], 0, 0)
+    close(O.sample_pdf(b, w, 96, det=False, u=torch.from_numpy(g["u"])), g["samples_rand"], 0, 0)
+
+
+@pytest.mark.parametrize("S", [64, 128])
+def test_render_val(S):
+    g = golden(f"render_val_s{S}")
+    res = O.render_rays_val(P(SEED_C), P(SEED_F), torch.from_numpy(g["rays"]), N_samples=S,
+                            N_importance=int(g["N_importance"]), perturb=0, noise_std=0, chunk=int(g["chunk"]))
+    close(res["depth"], g["depth"])
+    close(res["depth_fine"], g["depth_fine"])
+
+
+TRAIN = ["pcnerf", "pcnerf_noseg", "pcnerf_divide", "original", "pcnerf_perturb", "pcnerf_s128"]
+
+
+@pytest.mark.parametrize("name", TRAIN)
+def test_render_train(name):
+    g = golden(f"render_train_{name}")
+    rays = torch.from_numpy(g["rays"])
+    Pc, Pf = P(SEED_C), P(SEED_F)
+    draws = {k: torch.from_numpy(g[k]) for k in ("perturb_rand", "u") if k in g}
+    res = O.render_rays_train(Pc, Pf, rays, sub_nerf_test_num=int(g["sub_nerf_test_num"]),
+                              N_samples=int(g["N_samples"]), N_importance=int(g["N_importance"]),
+                              perturb=int(g["perturb"]), noise_std=0, chunk=int(g["chunk"]),
+                              issegmentated=int(g["issegmentated"]), childnerf_ratio=float(g["childnerf_ratio"]),
+                              use_child_nerf_divide=int(g["use_child_nerf_divide"]),
+                              use_child_nerf_loss=int(g["use_child_nerf_loss"]), draws=draws)
+    for k in ("depth", "depth_fine", "child_free_loss", "child_depth_loss", "child_free_loss_fine",
+              "child_depth_loss_fine"):
+        close(res[k], g[k], 1e-5, 1e-9)
+    lr, lrf = O.range_losses(res["depth"], res["depth_fine"], rays[:, 14], rays,
+                             int(g["use_child_nerf_divide"]), int(g["sub_nerf_test_num"]))
+    close(lr, g["loss_range"], 1e-5)
+    close(lrf, g["loss_range_fine"], 1e-5)
+    close(O.total_loss(res, lr, lrf), g["loss_total"], 1e-5)
+    close(running(Pc), g["running_c"])
+    close(running(Pf), g["running_f"])
+
+
+@pytest.mark.parametrize("method", [0, 2])
+def test_render_view(method):
+    g = golden(f"render_view_m{method}")
+    res = O.render_rays_view(P(SEED_C), P(SEED_F), torch.from_numpy(g["rows"]), torch.from_numpy(g["other"]),
+                             N_samples=int(g["N_samples"]), N_importance=int(g["N_importance"]), chunk=4096,
+                             method=method)
+    for k in ("depth", "depth_fine", "weights", "z_vals", "opacity", "opacity_fine", "points_inference",
+              "points_inference_fine"):
+        close(res[k], g[k], 1e-5, 1e-9)
+    for k in ("rays_effective_flag", "rays_effective_flag_fine"):
+        assert np.array_equal(res[k].numpy(), g[k])
