@@ -1,0 +1,227 @@
+"""Benchmark: LiDAR rays/s (render + loss) at 128 samples/ray on MI355X -- BASELINE.json config 2.
+
+One step = the reference training step's forward on one batch (train_kitti.py:117-155 without backward):
+``render_rays_train`` (train-mode BatchNorm over 262,144-sample chunks, segmented sampling ratio 0.1, child
+free/depth losses, perturb 1, noise_std 0) over 65,536 synthetic rays of one parent block with 32 child AABBs at
+N_samples=128 / N_importance=256 (512 MLP samples per ray), plus the SmoothL1 range losses and the weighted total
+loss.  Inputs are resident in HBM before timing starts.
+
+Multi-GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``): one process per GPU, each
+rank renders its own parent block (own rays, own NOF weights) -- weak scaling with no collective
+inside the timed region; the only collectives are the barrier around it and the max-over-ranks of the time.
+
+Prints ONE JSON line (rank 0) with the throughput, the dominant kernel's roofline (HIP events over the timed
+region, on the kernels' own stream) and a CPU baseline (the CPU oracle on a bounded sample, rank 0 only).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "pc-nerf_amd"))
+sys.path.insert(0, HERE)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # /opt/skills/guides/MI355X_MICROARCH.md (F32 MFMA = vector peak, no xf32)
+HBM_PEAK_GBS = 8000.0          # same guide (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rays", type=int, default=65536)
+    ap.add_argument("--samples", type=int, default=128)
+    ap.add_argument("--importance", type=int, default=256)
+    ap.add_argument("--chunk", type=int, default=262144)
+    ap.add_argument("--mode", choices=["train_fwd", "val"], default="train_fwd")
+    ap.add_argument("--cpu-rays", type=int, default=1024, help="bounded CPU-baseline sample (rays)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def prof_read(L, tag):
+    t, n, f, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+    rc = L.pcnerf_prof_read(tag, ctypes.byref(t), ctypes.byref(n), ctypes.byref(f), ctypes.byref(b))
+    if rc:
+        raise RuntimeError(L.pcnerf_last_error().decode())
+    return t.value, n.value, f.value, b.value
+
+
+def pmc_traffic(kernel_name: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary (profiles/), or None."""
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get(kernel_name, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from nof import _hip, synthetic as syn
+    from nof.criteria import nof_loss
+    from nof.networks import Embedding, NOF_coarse, NOF_fine
+    from nof.render import render_rays_train, render_rays_val
+
+    # this rank's parent block: its own child layout, rays and weights
+    rays = torch.from_numpy(syn.make_rays(a.rays, n_children=32, seed=1000 * rank)).to(dev)
+    train = a.mode == "train_fwd"
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234 + rank)).to(dev).train(train)
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678 + rank)).to(dev).train(train)
+    emb = Embedding(3, 10)
+    loss_fn = nof_loss["smoothl1"]()
+    gt = rays[:, 14].contiguous()
+
+    def step():
+        if train:
+            res = render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=32, N_samples=a.samples,
+                                    N_importance=a.importance, perturb=1, noise_std=0, chunk=a.chunk,
+                                    issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0,
+                                    use_child_nerf_loss=1)
+            lr = 1e-1 * loss_fn(1e1 * res["depth"], 1e1 * gt)           # train_kitti.py:145-146
+            lrf = 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
+            return (lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"]
+                    + 1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"])
+        res = render_rays_val(mc, mf, emb, rays, N_samples=a.samples, N_importance=a.importance, perturb=0,
+                              noise_std=0, chunk=a.chunk)
+        return 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
+
+    L = _hip.lib()
+    with torch.no_grad():
+        for _ in range(a.warmup):
+            loss = step()
+        torch.cuda.synchronize(dev)
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize(dev)
+        L.pcnerf_prof_enable(1)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            loss = step()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        if dist:
+            tdist.barrier()
+        loss_val = float(loss)
+    if not np.isfinite(loss_val):
+        raise RuntimeError(f"non-finite loss {loss_val}")
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+    elapsed = float(el)
+
+    # dominant kernel: the 256 -> 256 pre-BN Linear of train mode (6 of 9 GEMMs per chunk), or the fused eval query
+    tag = 1 if train else 0
+    kname = "k_train_layer<false,true>" if train else "k_nof_eval"
+    ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)
+    kernels = {}
+    for t, nm in ((0, "eval_query"), (1, "train_hidden"), (2, "train_first"), (3, "train_skip"), (4, "train_out"),
+                  (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample")):
+        tm, n, f, b = prof_read(L, t)
+        if n:
+            kernels[nm] = {"ms_per_step": round(tm / a.steps, 3), "launches_per_step": n // a.steps,
+                           "avg_us": round(1e3 * tm / n, 2),
+                           "TFLOP/s": round(f / (tm * 1e-3) / 1e12, 2) if f else None,
+                           "GB/s": round(b / (tm * 1e-3) / 1e9, 1) if b else None}
+    L.pcnerf_prof_enable(0)
+    avg_s = ktime_ms * 1e-3 / max(klaunch, 1)
+    achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
+    traffic = pmc_traffic(kname)
+
+    cpu = None
+    if rank == 0 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a, syn)
+
+    if rank != 0:
+        if dist:
+            tdist.destroy_process_group()
+        return
+    rays_total = a.rays * world * a.steps
+    value = rays_total / elapsed
+    out = {
+        "metric": "LiDAR rays/s (render+loss) at 128 samples/ray",
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)",
+        "config": {"workload": "render_rays_train fwd + range/child losses" if train else "render_rays_val fwd",
+                   "rays_per_gpu": a.rays, "N_samples": a.samples, "N_importance": a.importance,
+                   "mlp_samples_per_ray": a.samples + a.samples + a.importance, "chunk": a.chunk,
+                   "batchnorm": "train (batch stats per chunk)" if train else "eval (folded)",
+                   "segmented_ratio": 0.1 if train else None, "perturb": 1 if train else 0,
+                   "parallelism": f"blocks{world}"},
+        "roofline": {"kernel": kname, "bound": "mfma", "achieved": round(achieved, 2),
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 2),
+                     "algorithmic_flop_per_launch": kflops / max(klaunch, 1)},
+        "cpu_baseline": cpu,
+        "loss": loss_val,
+        "kernels": kernels,
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+def cpu_baseline(a, syn):
+    """The CPU oracle (oracle/ref_cpu.py, the reference's arithmetic on torch CPU) on a bounded sample of the
+    same workload: ``--cpu-rays`` rays of the same block, same settings, forward + losses."""
+    from oracle import ref_cpu as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    rays = torch.from_numpy(syn.make_rays(a.cpu_rays, n_children=32, seed=0))
+    Pc = O.params_from_numpy(syn.init_nof_params(1234))
+    Pf = O.params_from_numpy(syn.init_nof_params(5678))
+    train = a.mode == "train_fwd"
+
+    def run(r):
+        if train:
+            res = O.render_rays_train(Pc, Pf, r, sub_nerf_test_num=32, N_samples=a.samples, N_importance=a.importance,
+                                      perturb=1, noise_std=0, chunk=a.chunk, issegmentated=1, childnerf_ratio=0.1,
+                                      use_child_nerf_loss=1, training=True)
+            lr, lrf = O.range_losses(res["depth"], res["depth_fine"], r[:, 14])
+            return O.total_loss(res, lr, lrf)
+        res = O.render_rays_val(Pc, Pf, r, N_samples=a.samples, N_importance=a.importance, perturb=0, noise_std=0,
+                                chunk=a.chunk)
+        return res["depth_fine"].sum()
+
+    with torch.no_grad():
+        run(rays[:64])  # warm-up
+        t0 = time.perf_counter()
+        run(rays)
+        dt = time.perf_counter() - t0
+    return {"value": round(a.cpu_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{a.cpu_rays} rays of the same workload ({a.mode}, {a.samples}/{a.importance} samples, "
+                      f"chunk {a.chunk}) through oracle/ref_cpu.py on torch CPU, {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,134 @@
+/* pcnerf_hip.h -- C ABI of the MI355X (gfx950) PC-NeRF render + loss path.
+ *
+ * The reference (biter0088/pc-nerf) has no FFI: its hot path is eager PyTorch called from Python
+ * (nof/render.py, nof/networks/models.py, nof/criteria/loss.py).  This library is what that Python
+ * boundary binds to: the drop-in modules under pc-nerf_amd/nof/ keep the reference's names and signatures
+ * and call these entry points through ctypes.  Every entry point below names the
+ * reference code it replaces.
+ *
+ * Conventions
+ *   - every pointer is a device pointer (hipMalloc'd / torch CUDA tensor) unless stated otherwise;
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); all work is enqueued asynchronously on it;
+ *   - arrays are contiguous, fp32 unless stated; "rays" rows are `ray_stride` floats apart;
+ *   - return value 0 = success; nonzero = failure, with a message from pcnerf_last_error()
+ *     (argument errors are detected on the host before anything is launched).
+ */
+#ifndef PCNERF_HIP_H
+#define PCNERF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCNERF_ABI_VERSION 1
+#define PCNERF_FEATURES 256 /* NOF feature_size supported by the kernels (models.py:45 default) */
+#define PCNERF_IN_CH 63     /* 3 + 3*2*L_pos with L_pos = 10 (train_kitti.py:25-28)            */
+
+int pcnerf_abi_version(void);
+const char* pcnerf_last_error(void);
+
+/* ---------------------------------------------------------------- NOF network (models.py:44-359)
+ * Parameters in reference state_dict order: Linear weights [256,63],[256,256]x3,[256,319],[256,256]x3
+ * (layer1.{0,3,6,9}, layer2.{0,2,4,6}), BatchNorm1d gamma/beta/running_mean/running_var
+ * (layer1.{1,4,7,10}, layer2.{1,3,5,7}), occ_out.0 weight [1,256] and bias [1]. */
+typedef struct pcnerf_nof_params {
+  const float* lin_w[8];
+  const float* lin_b[8];
+  const float* bn_w[8];
+  const float* bn_b[8];
+  float* bn_rm[8]; /* running_mean: read in eval mode, updated in place in train mode */
+  float* bn_rv[8]; /* running_var:  idem */
+  const float* out_w;
+  const float* out_b;
+} pcnerf_nof_params;
+
+/* Eval-mode network image: BatchNorm (running stats) folded into each Linear, weights repacked into the
+ * MFMA operand order of the fused query kernel.  Replaces the per-call nn.Module forward in eval mode. */
+size_t pcnerf_nof_eval_packed_floats(void);
+int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* packed, void* stream);
+
+/* Fused eval-mode query: for every flattened sample g = ray*n_samples + s computes
+ *   p_out[g] = NOF(Embedding(o + d*z[g]))        (render.py:18-25 chunk loop, models.py:27-41, :183-203)
+ * with o = rays[ray, 0:3], d = rays[ray, 3:6]. */
+int pcnerf_nof_query_eval(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
+                          const float* packed, float* p_out, void* stream);
+
+/* NOF.forward on an already embedded batch: p_out[i] = NOF(emb[i, 0:63]) (eval mode, packed image). */
+int pcnerf_nof_forward_eval(const float* emb, int64_t n, const float* packed, float* p_out, void* stream);
+
+/* Embedding(3, 10).forward (models.py:27-41): out[i, 0:63] = [x, sin(2^k x), cos(2^k x)]_k for x = pts[i, 0:3]. */
+int pcnerf_embed(const float* pts, int64_t n, float* out, void* stream);
+
+/* Train-mode query (BatchNorm batch statistics per chunk of `chunk` flattened ray-major samples, running
+ * stats updated once per chunk with `momentum`; render.py:47-50 + nn.BatchNorm1d train semantics).
+ * `workspace` must hold pcnerf_nof_train_workspace_bytes(chunk) bytes. */
+size_t pcnerf_nof_train_workspace_bytes(int64_t chunk);
+int pcnerf_nof_query_train(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
+                           int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
+                           void* workspace, size_t workspace_bytes, float* p_out, void* stream);
+
+/* NOF.forward in train mode on an embedded batch of n rows (one BatchNorm chunk; running stats updated). */
+int pcnerf_nof_forward_train(const float* emb, int64_t n, const pcnerf_nof_params* params, float momentum,
+                             float eps, void* workspace, size_t workspace_bytes, float* p_out, void* stream);
+
+/* ---------------------------------------------------------------- sampling (render.py:429-454, :497-511)
+ * z[ray, :] = linspace sampling of [rays[near_col], rays[far_col]] with n_samples points; if
+ * n_parent < n_samples the segmented scheme is used: n_parent points over [near, far] and
+ * n_samples - n_parent over [rays[child_near_col], rays[child_far_col]], merged by sort. */
+int pcnerf_sample_coarse(const float* rays, int64_t n_rays, int ray_stride, int near_col, int far_col,
+                         int child_near_col, int child_far_col, int n_samples, int n_parent, float* z,
+                         void* stream);
+/* Stratified perturbation z' = lower + (upper - lower) * (perturb * rand) (render.py:449-454). */
+int pcnerf_perturb(const float* z, int64_t n_rays, int n_samples, float perturb, const float* rand, float* z_out,
+                   void* stream);
+
+/* ---------------------------------------------------------------- compositing + child losses
+ * (render.py:51-61 and :75-159).  Per ray: w = p * cumprod(1-p) (+ noise_std*noise if noise != NULL),
+ * w /= sum(w) + eps; depth = sum(w z).  If `rays` != NULL, also the child masks (inclusive, expansion
+ * from 0 and from 2 m by 0.01 steps) and the per-ray loss terms:
+ *   free_ray[r] = sum_s (w * !M0)^2,   sl1_ray[r] = SmoothL1(10 * depth_child, 10 * range). */
+int pcnerf_composite(const float* p, const float* z, int64_t n_rays, int n_samples, const float* noise,
+                     float noise_std, float eps, const float* rays, int ray_stride, int child_near_col,
+                     int child_far_col, int range_col, float* weights, float* depth, float* free_ray,
+                     float* sl1_ray, void* stream);
+
+/* ---------------------------------------------------------------- importance resampling
+ * z_fine[ray, :] = sort(cat(z, sample_pdf(mid(z), weights[:, 1:-1], n_importance, det = (u == NULL))))
+ * (render.py:371-412, :463-467).  `u` [n_rays, n_importance] replaces torch.rand when not NULL. */
+int pcnerf_resample(const float* z, const float* weights, int64_t n_rays, int n_samples, int n_importance,
+                    const float* u, float* z_fine, void* stream);
+
+/* Standalone sample_pdf(bins (R, n_bins), weights (R, n_bins-1), n_samples, det = (u == NULL)) -> out
+ * (R, n_samples), unsorted (render.py:371-412). */
+int pcnerf_sample_pdf(const float* bins, const float* weights, int64_t n_rays, int n_bins, int n_samples,
+                      const float* u, float* out, void* stream);
+
+/* ---------------------------------------------------------------- losses
+ * Child free / depth losses from the per-ray terms (render.py:102-159).  sub_nerf_test_num == 0 selects
+ * the plain branch (sum / n_rays, 0.1/n_rays * mean); > 0 the per-child "divide" branch over child ids
+ * 1..sub_nerf_test_num read from child_id[r * id_stride].  out[0] = free loss, out[1] = depth loss.
+ * `workspace` needs pcnerf_child_loss_workspace_bytes(sub_nerf_test_num) bytes. */
+size_t pcnerf_child_loss_workspace_bytes(int sub_nerf_test_num);
+int pcnerf_child_loss_reduce(const float* free_ray, const float* sl1_ray, int64_t n_rays, const float* child_id,
+                             int id_stride, int sub_nerf_test_num, void* workspace, float* out, void* stream);
+
+/* mean(loss(pred, target)) over elements where mask != 0 (mask may be NULL); kind 0 = MSE, 1 = L1,
+ * 2 = SmoothL1(beta 1) (nof/criteria/loss.py:12-50 with nn.*Loss(reduction='mean')).  out: one float. */
+int pcnerf_pointwise_loss(const float* pred, const float* target, const uint8_t* mask, int64_t n, int kind,
+                          float* out, void* stream);
+
+/* ---------------------------------------------------------------- kernel timing (bench / profiling)
+ * pcnerf_prof_enable(1) makes every subsequent launch record a HIP event pair on its stream; tags:
+ * 0 eval query, 1 train hidden Linear, 2 train first Linear, 3 train skip Linear, 4 train occ_out,
+ * 5 BN fold, 6 composite, 7 resample, 8 sampling.  pcnerf_prof_read synchronises the tag's events and returns
+ * the summed duration, launch count and algorithmic FLOPs / bytes of those launches. */
+int pcnerf_prof_enable(int on);
+int pcnerf_prof_read(int tag, double* total_ms, int64_t* launches, double* flops, double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCNERF_HIP_H */

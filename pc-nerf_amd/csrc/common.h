@@ -1,0 +1,59 @@
+// Shared device helpers for the PC-NeRF render path (gfx950 / CDNA4, wave64).
+//
+// Compiled with -ffp-contract=off: the reference rounds every eager torch op separately
+// (nof/render.py:432,458), and the positional encoding reaches sin(512 x) (nof/networks/models.py:23), so a
+// fused multiply-add in z = near*(1-s)+far*s or p = o+d*z would move sample features by ~1e-3.  Where an FMA
+// *is* the reference's arithmetic (torch.linspace's upper half) it is written explicitly with fmaf().
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PCN_WAVE 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace pcn {
+
+// torch.linspace(0, 1, n) on CPU, value i (verified bit-exact for n in 2..8192):
+// step = 1/(n-1); lower half i*step, upper half fma(-(n-1-i), step, 1).
+__device__ __forceinline__ float linspace01(int i, int n) {
+  if (n == 1) return 0.0f;
+  const float step = 1.0f / (float)(n - 1);
+  if (i < n / 2) return (float)i * step;
+  return fmaf(-(float)(n - 1 - i), step, 1.0f);
+}
+
+// z = near*(1-s) + far*s, rounded op by op (render.py:432).
+__device__ __forceinline__ float lerp_z(float near, float far, float s) {
+  const float a = near * (1.0f - s);
+  const float b = far * s;
+  return a + b;
+}
+
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// torch sigmoid on CPU: 1 / (1 + exp(-x)).
+__device__ __forceinline__ float sigmoid_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// nn.SmoothL1Loss(beta=1) element term on already-scaled inputs.
+__device__ __forceinline__ float smooth_l1(float a, float b) {
+  const float d = fabsf(a - b);
+  return d < 1.0f ? 0.5f * d * d : d - 0.5f;
+}
+
+}  // namespace pcn

@@ -1,0 +1,247 @@
+// Eval-mode NOF query: positional encoding + the full 9-Linear network + sigmoid, fused in one kernel with
+// every activation held in registers (nof/networks/models.py:27-41 Embedding, :183-203 NOF_coarse.forward;
+// render.py:18-25 chunk loop).  BatchNorm1d in eval mode is an affine map per feature, folded into the
+// Linear that produces it when the network image is packed (pcnerf_nof_pack_eval).
+//
+// MFMA mapping (v_mfma_f32_32x32x2_f32, exact fp32 fmaf chain).  One wave owns a tile of 32 samples and
+// computes every layer transposed, out^T[neuron][sample] = W[neuron][:] . act^T[:][sample]:
+//   A operand (lane l) = W[32*ob + (l&31)][feature(t, l>>5)]      -- packed weights, 1 VGPR per k-step
+//   B operand (lane l) = act[feature(t, l>>5)][sample l&31]      -- register-resident activations
+//   D (block ob, reg r, lane l) = out[32*ob + (r&3) + 8*(r>>2) + 4*(l>>5)][sample l&31]
+// so accumulator register R = 16*ob + r of a layer IS the B operand of k-step t = R of the next layer
+// (feature map FEAT_H below): the whole chain runs without LDS or lane shuffles.  The encoding feeds layer 1
+// (and the skip half of layer 5) with feature(t, h) = 2t + h.
+#include "common.h"
+#include "pcnerf_internal.h"
+#include "prof.h"
+
+namespace pcn {
+
+// ---------------------------------------------------------------------------------- eval network image
+// [L1e][L2h][L3h][L4h][L5e][L5h][L6h][L7h][L8h][bias 8x256][w_out 256][b_out 4]
+// e-part: KG_E = 8 groups of 4 k-steps (64 features, the 64th is zero padding); h-part: KG_H = 32 groups.
+// Within a part: [kg][ob(8)][lane(64)][q(4)], value = W'[32*ob + (lane&31)][feature(4*kg+q, lane>>5)].
+constexpr int KG_E = 8, KG_H = 32;
+constexpr size_t SZ_E = (size_t)KG_E * 8 * 64 * 4;  // 16384
+constexpr size_t SZ_H = (size_t)KG_H * 8 * 64 * 4;  // 65536
+__host__ __device__ constexpr size_t off_w(int layer, bool epart) {
+  // layer 0..7
+  return layer == 0 ? 0
+       : layer <= 3 ? SZ_E + (size_t)(layer - 1) * SZ_H
+       : layer == 4 ? (epart ? SZ_E + 3 * SZ_H : 2 * SZ_E + 3 * SZ_H)
+                    : 2 * SZ_E + (size_t)(layer - 1) * SZ_H;
+}
+constexpr size_t OFF_BIAS = 2 * SZ_E + 7 * SZ_H;
+constexpr size_t OFF_WOUT = OFF_BIAS + 8 * 256;
+constexpr size_t OFF_BOUT = OFF_WOUT + 256;
+constexpr size_t EVAL_FLOATS = OFF_BOUT + 4;
+
+__device__ __forceinline__ int feat_h(int t, int h) {  // accumulator register -> neuron
+  return 32 * (t >> 4) + (t & 3) + 8 * ((t & 15) >> 2) + 4 * h;
+}
+
+// one thread per packed float of the weight parts
+__global__ void k_pack_eval_weights(NofParamsDev P, float* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= OFF_BIAS) return;
+  int layer;
+  bool epart;
+  size_t base;
+  if (idx < SZ_E) { layer = 0; epart = true; base = 0; }
+  else if (idx < SZ_E + 3 * SZ_H) { layer = 1 + (int)((idx - SZ_E) / SZ_H); epart = false; base = off_w(layer, false); }
+  else if (idx < 2 * SZ_E + 3 * SZ_H) { layer = 4; epart = true; base = off_w(4, true); }
+  else if (idx < 2 * SZ_E + 4 * SZ_H) { layer = 4; epart = false; base = off_w(4, false); }
+  else { layer = 5 + (int)((idx - (2 * SZ_E + 4 * SZ_H)) / SZ_H); epart = false; base = off_w(layer, false); }
+  const size_t j = idx - base;
+  const int q = (int)(j & 3), lane = (int)((j >> 2) & 63), ob = (int)((j >> 8) & 7), kg = (int)(j >> 11);
+  const int t = 4 * kg + q, h = lane >> 5, n = 32 * ob + (lane & 31);
+  const int in_f = layer == 0 ? 63 : layer == 4 ? 319 : 256;
+  int col;
+  if (epart) {
+    const int f = 2 * t + h;
+    col = f < 63 ? f : -1;
+  } else {
+    col = (layer == 4 ? 63 : 0) + feat_h(t, h);
+  }
+  // BatchNorm eval: alpha = gamma / sqrt(rv + eps) (ATen batch_norm_cpu_transform_input: invstd * weight)
+  const float alpha = (1.0f / sqrtf(P.bn_rv[layer][n] + P.eps)) * P.bn_w[layer][n];
+  out[idx] = col < 0 ? 0.0f : alpha * P.lin_w[layer][(size_t)n * in_f + col];
+}
+
+__global__ void k_pack_eval_vectors(NofParamsDev P, float* __restrict__ out) {
+  const int n = threadIdx.x;  // 256 threads
+  for (int layer = 0; layer < 8; ++layer) {
+    const float alpha = (1.0f / sqrtf(P.bn_rv[layer][n] + P.eps)) * P.bn_w[layer][n];
+    const float beta = P.bn_b[layer][n] - P.bn_rm[layer][n] * alpha;
+    out[OFF_BIAS + layer * 256 + n] = alpha * P.lin_b[layer][n] + beta;
+  }
+  out[OFF_WOUT + n] = P.out_w[n];
+  if (n == 0) {
+    out[OFF_BOUT] = P.out_b[0];
+    out[OFF_BOUT + 1] = out[OFF_BOUT + 2] = out[OFF_BOUT + 3] = 0.0f;
+  }
+}
+
+// ---------------------------------------------------------------------------------- fused query kernel
+template <int KG, int NX>
+__device__ __forceinline__ void gemm_t(f32x16 (&acc)[8], const float (&x)[NX], const float* __restrict__ wp,
+                                       int lane) {
+  static_assert(NX == 4 * KG, "operand count");
+  const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(wp) + lane;
+  f32x4 wa[8];
+#pragma unroll
+  for (int ob = 0; ob < 8; ++ob) wa[ob] = w4[ob * 64];
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) {
+    f32x4 wb[8];
+    if (kg + 1 < KG) {
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob) wb[ob] = w4[((kg + 1) * 8 + ob) * 64];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob)
+        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[ob][q], x[4 * kg + q], acc[ob], 0, 0, 0);
+    }
+    if (kg + 1 < KG) {
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob) wa[ob] = wb[ob];
+    }
+  }
+}
+
+__device__ __forceinline__ void init_bias_t(f32x16 (&acc)[8], const float* __restrict__ b, int h) {
+#pragma unroll
+  for (int ob = 0; ob < 8; ++ob) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(b + 32 * ob + 8 * g + 4 * h);
+      acc[ob][4 * g + 0] = v[0];
+      acc[ob][4 * g + 1] = v[1];
+      acc[ob][4 * g + 2] = v[2];
+      acc[ob][4 * g + 3] = v[3];
+    }
+  }
+}
+
+// ein != NULL: the (total, 63) embedding is read from memory instead (NOF.forward on embedded input).
+__global__ __launch_bounds__(256) void k_nof_eval(const float* __restrict__ rays, int stride,
+                                                  const float* __restrict__ z, int64_t total, int S,
+                                                  const float* __restrict__ ein, const float* __restrict__ W,
+                                                  float* __restrict__ p_out) {
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t g = tile * 32 + (lane & 31);
+  const int64_t gc = g < total ? g : total - 1;
+  float e[32];
+  if (ein) {
+    load_embedding<0>(ein + gc * 63, h, e);
+  } else {
+    const float* r = rays + (gc / S) * stride;
+    float p[3];
+    sample_point(r, z[gc], p);
+    encode_half(p, h, e);
+  }
+
+  f32x16 acc[8];
+  float act[128];
+#pragma unroll 1
+  for (int L = 0; L < 8; ++L) {
+    init_bias_t(acc, W + OFF_BIAS + 256 * L, h);
+    if (L == 0 || L == 4) gemm_t<KG_E>(acc, e, W + off_w(L, true), lane);
+    if (L != 0) gemm_t<KG_H>(acc, act, W + off_w(L, false), lane);
+#pragma unroll
+    for (int R = 0; R < 128; ++R) act[R] = acc[R >> 4][R & 15];
+  }
+  // occ_out: Linear(256, 1) + Sigmoid; each lane holds half the features of its sample
+  float part = 0.0f;
+#pragma unroll
+  for (int ob = 0; ob < 8; ++ob) {
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(W + OFF_WOUT + 32 * ob + 8 * gq + 4 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part = fmaf(wv[q], act[16 * ob + 4 * gq + q], part);
+    }
+  }
+  const float logit = part + __shfl_xor(part, 32, 64) + W[OFF_BOUT];
+  if (lane < 32 && g < total) p_out[g] = sigmoid_ref(logit);
+}
+
+__global__ void k_embed(const float* __restrict__ pts, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float p[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+  float e0[32], e1[32];
+  encode_half(p, 0, e0);
+  encode_half(p, 1, e1);
+  float* o = out + 63 * i;
+#pragma unroll
+  for (int t = 0; t < 32; ++t) {
+    o[2 * t] = e0[t];
+    if (2 * t + 1 < 63) o[2 * t + 1] = e1[t];
+  }
+}
+
+}  // namespace pcn
+
+using namespace pcn;
+
+extern "C" int pcnerf_embed(const float* pts, int64_t n, float* out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(pts && out, "pcnerf_embed: null argument");
+  PCN_CHECK(n > 0, "pcnerf_embed: empty input");
+  hipLaunchKernelGGL(k_embed, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, pts, n, out);
+  PCN_LAUNCH_CHECK("pcnerf_embed");
+  PCN_API_END
+}
+
+extern "C" size_t pcnerf_nof_eval_packed_floats(void) { return EVAL_FLOATS; }
+
+extern "C" int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* packed, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(params && packed, "pcnerf_nof_pack_eval: null argument");
+  NofParamsDev P;
+  PCN_CHECK(to_dev_params(params, 1e-5f, &P), "pcnerf_nof_pack_eval: null parameter pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned nb = (unsigned)((OFF_BIAS + 255) / 256);
+  hipLaunchKernelGGL(k_pack_eval_weights, dim3(nb), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(k_pack_eval_vectors, dim3(1), dim3(256), 0, s, P, packed);
+  PCN_LAUNCH_CHECK("pcnerf_nof_pack_eval");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_query_eval(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                     int n_samples, const float* packed, float* p_out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && packed && p_out, "pcnerf_nof_query_eval: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_nof_query_eval: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_eval: ray_stride < 6");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  const int64_t tiles = (total + 31) / 32;
+  const int64_t blocks = (tiles + 3) / 4;
+  PCN_CHECK(blocks < (int64_t)1 << 31, "pcnerf_nof_query_eval: too many samples for one launch");
+  {
+    // algorithmic work: 982,528 FLOP per sample (9 Linear layers); bytes: z in, p out, ray rows, network image
+    ProfScope ps((hipStream_t)stream, PT_EVAL_QUERY, 982528.0 * (double)total,
+                 8.0 * (double)total + 4.0 * ray_stride * (double)n_rays + 4.0 * EVAL_FLOATS);
+    hipLaunchKernelGGL(k_nof_eval, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rays, ray_stride, z,
+                       total, n_samples, (const float*)nullptr, packed, p_out);
+  }
+  PCN_LAUNCH_CHECK("pcnerf_nof_query_eval");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_forward_eval(const float* emb, int64_t n, const float* packed, float* p_out,
+                                       void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(emb && packed && p_out, "pcnerf_nof_forward_eval: null argument");
+  PCN_CHECK(n > 0, "pcnerf_nof_forward_eval: empty input");
+  const int64_t blocks = ((n + 31) / 32 + 3) / 4;
+  PCN_CHECK(blocks < (int64_t)1 << 31, "pcnerf_nof_forward_eval: too many samples for one launch");
+  hipLaunchKernelGGL(k_nof_eval, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const float*)nullptr, 0,
+                     (const float*)nullptr, n, 1, emb, packed, p_out);
+  PCN_LAUNCH_CHECK("pcnerf_nof_forward_eval");
+  PCN_API_END
+}

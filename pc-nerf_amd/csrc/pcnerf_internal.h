@@ -1,0 +1,97 @@
+// Internal glue shared by the translation units: error reporting, the device-side parameter struct and the
+// per-sample front end (sample position + positional encoding) used by every NOF query kernel.
+#pragma once
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "pcnerf_hip.h"
+
+namespace pcn {
+
+struct NofParamsDev {
+  const float* lin_w[8];
+  const float* lin_b[8];
+  const float* bn_w[8];
+  const float* bn_b[8];
+  float* bn_rm[8];
+  float* bn_rv[8];
+  const float* out_w;
+  const float* out_b;
+  float eps;
+};
+
+bool to_dev_params(const pcnerf_nof_params* p, float eps, NofParamsDev* d);
+void set_error(const std::string& msg);
+
+// p = o + d*z, one rounding per op (render.py:458; built with -ffp-contract=off).
+__device__ __forceinline__ void sample_point(const float* __restrict__ r, float z, float (&p)[3]) {
+  p[0] = r[0] + r[3] * z;
+  p[1] = r[1] + r[4] * z;
+  p[2] = r[2] + r[5] * z;
+}
+
+// Embedding(3, 10) (models.py:27-41): feature f of [x(3), sin(2^0 x)(3), cos(2^0 x)(3), ..., cos(2^9 x)(3)],
+// f = 63 is zero padding.  freq_bands = 2**linspace(0,9,10) are exact powers of two, so 2^k * x is exact
+// and only sinf/cosf rounding remains (full-range ocml sincosf, never the __sinf fast path).
+// Lane half h receives, for k-step t = 0..31, feature 2t + h (MAP 0: eval chain) or 8(t>>2) + 4h + (t&3)
+// (MAP 1: train-mode layer kernels, whose memory-resident activations use 16-byte feature groups).
+template <int MAP = 0>
+__device__ __forceinline__ void encode_half(const float (&p)[3], int h, float (&e)[32]) {
+  float f[64];
+  f[0] = p[0];
+  f[1] = p[1];
+  f[2] = p[2];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const float sc = (float)(1 << k);
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      float s, c;
+      sincosf(sc * p[m], &s, &c);
+      f[3 + 6 * k + m] = s;
+      f[6 + 6 * k + m] = c;
+    }
+  }
+  f[63] = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 32; ++t) {
+    if (MAP == 0) e[t] = h ? f[2 * t + 1] : f[2 * t];
+    else e[t] = h ? f[8 * (t >> 2) + 4 + (t & 3)] : f[8 * (t >> 2) + (t & 3)];
+  }
+}
+
+// The same operand selection from a stored (., 63) embedding row.
+template <int MAP = 0>
+__device__ __forceinline__ void load_embedding(const float* __restrict__ row, int h, float (&e)[32]) {
+#pragma unroll
+  for (int t = 0; t < 32; ++t) {
+    const int f = MAP == 0 ? 2 * t + h : 8 * (t >> 2) + 4 * h + (t & 3);
+    e[t] = f < 63 ? row[f] : 0.0f;
+  }
+}
+
+}  // namespace pcn
+
+#define PCN_API_BEGIN try {
+#define PCN_API_END                                       \
+  return 0;                                               \
+  }                                                       \
+  catch (const std::exception& ex__) {                    \
+    pcn::set_error(ex__.what());                          \
+    return 1;                                             \
+  }
+#define PCN_CHECK(cond, msg)                              \
+  do {                                                    \
+    if (!(cond)) throw std::runtime_error(msg);           \
+  } while (0)
+#define PCN_LAUNCH_CHECK(name)                                                                 \
+  do {                                                                                         \
+    hipError_t e__ = hipGetLastError();                                                        \
+    if (e__ != hipSuccess) throw std::runtime_error(std::string(name) + ": " + hipGetErrorString(e__)); \
+  } while (0)
+#define PCN_HIP(call)                                                                          \
+  do {                                                                                         \
+    hipError_t e__ = (call);                                                                   \
+    if (e__ != hipSuccess) throw std::runtime_error(std::string(#call) + ": " + hipGetErrorString(e__)); \
+  } while (0)

@@ -1,0 +1,28 @@
+// Kernel timing scope: records a HIP event pair around the enclosed launch when profiling is enabled.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace pcn {
+// tags reported by pcnerf_prof_read
+enum ProfTag {
+  PT_EVAL_QUERY = 0,   // k_nof_eval: fused 9-layer eval query
+  PT_TRAIN_HIDDEN = 1, // k_train_layer<false,true>: 256 -> 256 pre-BN Linear (6 per chunk)
+  PT_TRAIN_FIRST = 2,  // k_train_layer<true,false>: encoding -> 256
+  PT_TRAIN_SKIP = 3,   // k_train_layer<true,true>: [encoding, 256] -> 256
+  PT_TRAIN_OUT = 4,    // k_train_out
+  PT_BN_FOLD = 5,      // k_bn_fold
+  PT_COMPOSITE = 6,    // k_composite
+  PT_RESAMPLE = 7,     // k_resample
+  PT_SAMPLE = 8,       // k_sample_coarse / k_perturb
+};
+extern bool g_prof_on;
+class ProfScope {
+ public:
+  ProfScope(hipStream_t s, int tag, double flops, double bytes);
+  ~ProfScope();
+
+ private:
+  hipStream_t s_;
+  int idx_;
+};
+}  // namespace pcn

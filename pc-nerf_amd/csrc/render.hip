@@ -1,0 +1,576 @@
+// Per-ray stages of the render path: coarse sampling, perturbation, occupancy compositing with the child
+// masks and loss terms, importance resampling + merge, and the loss reductions (nof/render.py).
+// These stages read/write a few bytes per sample and are bound by HBM, not by arithmetic: one wave per ray,
+// samples of a ray in contiguous per-lane blocks, scans in registers + cross-lane shuffles, no atomics on
+// the per-ray path.
+#include <stdio.h>
+
+#include <mutex>
+#include <string>
+
+#include "common.h"
+#include "pcnerf_internal.h"
+#include "prof.h"
+
+namespace pcn {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+bool to_dev_params(const pcnerf_nof_params* p, float eps, NofParamsDev* d) {
+  for (int i = 0; i < 8; ++i) {
+    if (!p->lin_w[i] || !p->lin_b[i] || !p->bn_w[i] || !p->bn_b[i] || !p->bn_rm[i] || !p->bn_rv[i]) return false;
+    d->lin_w[i] = p->lin_w[i];
+    d->lin_b[i] = p->lin_b[i];
+    d->bn_w[i] = p->bn_w[i];
+    d->bn_b[i] = p->bn_b[i];
+    d->bn_rm[i] = p->bn_rm[i];
+    d->bn_rv[i] = p->bn_rv[i];
+  }
+  if (!p->out_w || !p->out_b) return false;
+  d->out_w = p->out_w;
+  d->out_b = p->out_b;
+  d->eps = eps;
+  return true;
+}
+
+// ------------------------------------------------------------------------------- coarse sampling
+// render.py:429-442.  One wave per ray; segmented sampling merges the parent and child linspace lists by
+// rank (count of smaller values + equal values with a lower index), which is the sorted order for any input.
+__device__ __forceinline__ float seg_value(int a, int sp, int sc, float near, float far, float cn, float cf) {
+  return a < sp ? lerp_z(near, far, linspace01(a, sp)) : lerp_z(cn, cf, linspace01(a - sp, sc));
+}
+
+__global__ __launch_bounds__(256) void k_sample_coarse(const float* __restrict__ rays, int64_t n_rays, int stride,
+                                                       int near_col, int far_col, int cn_col, int cf_col, int S,
+                                                       int sp, float* __restrict__ z) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ray >= n_rays) return;
+  const float* r = rays + ray * stride;
+  const float near = r[near_col], far = r[far_col];
+  float* zr = z + ray * S;
+  if (sp >= S) {
+    for (int i = lane; i < S; i += 64) zr[i] = lerp_z(near, far, linspace01(i, S));
+    return;
+  }
+  const float cn = r[cn_col], cf = r[cf_col];
+  const int sc = S - sp;
+  for (int a = lane; a < S; a += 64) {
+    const float va = seg_value(a, sp, sc, near, far, cn, cf);
+    int rank = 0;
+    for (int b = 0; b < S; ++b) {
+      const float vb = seg_value(b, sp, sc, near, far, cn, cf);
+      rank += (vb < va) || (vb == va && b < a);
+    }
+    zr[rank] = va;
+  }
+}
+
+// render.py:449-454 (and :506-511): z' = lower + (upper - lower) * (perturb * rand)
+__global__ void k_perturb(const float* __restrict__ z, int64_t total, int S, float perturb,
+                          const float* __restrict__ rnd, float* __restrict__ zo) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  const int i = (int)(g % S);
+  const float zi = z[g];
+  const float lower = i == 0 ? zi : 0.5f * (z[g - 1] + zi);
+  const float upper = i == S - 1 ? zi : 0.5f * (zi + z[g + 1]);
+  const float pr = perturb * rnd[g];
+  zo[g] = lower + (upper - lower) * pr;
+}
+
+// ------------------------------------------------------------------------------- compositing
+// Exclusive multiplicative scan of one double per lane across the wave.
+__device__ __forceinline__ double wave_excl_prod(double v, int lane) {
+  double incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double n = __shfl_up(incl, o, 64);
+    if (lane >= o) incl *= n;
+  }
+  const double ex = __shfl_up(incl, 1, 64);
+  return lane == 0 ? 1.0 : ex;
+}
+__device__ __forceinline__ double wave_excl_sum(double v, int lane) {
+  double incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double n = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += n;
+  }
+  const double ex = __shfl_up(incl, 1, 64);
+  return lane == 0 ? 0.0 : ex;
+}
+
+// Smallest thr = thr0 + k*0.01 (Python float64 accumulation) for which a sample of the ray lies in
+// [fl32(near - fl32(thr)), fl32(far + fl32(thr))] (inclusive: render.py:80-84,94-97) or the open interval
+// (strict: render.py:255-263).  Returns fl32 bounds.
+template <bool STRICT, int MAXB>
+__device__ __forceinline__ void expand_bounds(const float (&zv)[MAXB], int nb, float near, float far, double thr0,
+                                              float& lo, float& hi, int* err) {
+  double thr = thr0;
+  for (int it = 0; it < 4000000; ++it) {
+    const float t32 = (float)thr;
+    lo = near - t32;
+    hi = far + t32;
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j)
+      if (j < nb) any |= STRICT ? (lo < zv[j] && zv[j] < hi) : (lo <= zv[j] && zv[j] <= hi);
+    if (__any(any)) return;
+    thr = thr + 0.01;
+  }
+  if (err) *err = 1;
+}
+
+template <int MAXB>
+__global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, const float* __restrict__ Z,
+                                                   int64_t n_rays, int S, const float* __restrict__ noise,
+                                                   float noise_std, float eps, const float* __restrict__ rays,
+                                                   int stride, int cn_col, int cf_col, int rg_col,
+                                                   float* __restrict__ Wout, float* __restrict__ depth,
+                                                   float* __restrict__ free_ray, float* __restrict__ sl1_ray,
+                                                   int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ray >= n_rays) return;
+  const int B = (S + 63) / 64;
+  const int i0 = lane * B;
+  const int nb = max(0, min(B, S - i0));
+  const float* pr = P + ray * S + i0;
+  const float* zr = Z + ray * S + i0;
+  float pv[MAXB], zv[MAXB], wv[MAXB];
+  double loc = 1.0;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    if (j < nb) {
+      pv[j] = pr[j];
+      zv[j] = zr[j];
+      loc *= (double)(1.0f - pv[j]);
+    } else {
+      pv[j] = 0.0f;
+      zv[j] = 0.0f;
+    }
+  }
+  // transmittance: cumprod of [1, 1-p] in float64, each prefix rounded to fp32 (render.py:52-55)
+  double T = wave_excl_prod(loc, lane);
+  double sw = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    if (j < nb) {
+      float w = (float)T * pv[j];
+      if (noise) w = w + noise[ray * S + i0 + j] * noise_std;
+      wv[j] = w;
+      sw += (double)w;
+      T *= (double)(1.0f - pv[j]);
+    } else {
+      wv[j] = 0.0f;
+    }
+  }
+  const float den = (float)wave_sum_d(sw) + eps;  // render.py:60
+  double sd = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    if (j < nb) {
+      wv[j] = wv[j] / den;
+      sd += (double)(wv[j] * zv[j]);
+    }
+  }
+  const float d = (float)wave_sum_d(sd);
+  if (Wout) {
+    float* wr = Wout + ray * S + i0;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j)
+      if (j < nb) wr[j] = wv[j];
+  }
+  if (lane == 0) depth[ray] = d;
+  if (!rays) return;
+
+  // child masks and loss terms (render.py:75-159)
+  const float* r = rays + ray * stride;
+  const float cn = r[cn_col], cf = r[cf_col], rg = r[rg_col];
+  float lo0, hi0, lo2, hi2;
+  expand_bounds<false, MAXB>(zv, nb, cn, cf, 0.0, lo0, hi0, err);
+  expand_bounds<false, MAXB>(zv, nb, cn, cf, 2.0, lo2, hi2, err);
+  double fr = 0.0, sc = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    if (j < nb) {
+      const bool m0 = lo0 <= zv[j] && zv[j] <= hi0;
+      const float wf = wv[j] * (m0 ? 0.0f : 1.0f);
+      fr += (double)(wf * wf);
+      const bool m2 = lo2 <= zv[j] && zv[j] <= hi2;
+      sc += (double)(wv[j] * (m2 ? 1.0f : 0.0f));
+    }
+  }
+  const float denc = (float)wave_sum_d(sc) + eps;  // render.py:129
+  double dcs = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    if (j < nb) {
+      const float m2 = (lo2 <= zv[j] && zv[j] <= hi2) ? 1.0f : 0.0f;
+      const float wc = (wv[j] * m2) / denc;
+      dcs += (double)(wc * (zv[j] * m2));
+    }
+  }
+  const float dc = (float)wave_sum_d(dcs);
+  const float frs = (float)wave_sum_d(fr);
+  if (lane == 0) {
+    free_ray[ray] = frs;
+    sl1_ray[ray] = smooth_l1(10.0f * dc, 10.0f * rg);
+  }
+}
+
+// ------------------------------------------------------------------------------- importance resampling
+// sample_pdf (render.py:371-412) for one ray by one wave: bins[0..nb), weights w[0..nb-1) (already sliced),
+// cdf scratch of nb floats in LDS, n draws -> out[k] (unsorted).  Sums run in float64: every pdf value is
+// >= 1e-5/sum, so all partial sums are exact in float64 and the cdf equals the reference's cumsum (which
+// accumulates in float64 on CPU) bit for bit; the normaliser is the float64 sum rounded once.
+__device__ void pdf_samples(const float* bins, const float* w, int nb, float* cdf, int n, const float* u_row,
+                            float* out, int lane) {
+  const int npdf = nb - 1;
+  const int B = (npdf + 63) / 64;
+  const int i0 = lane * B;
+  double ls = 0.0;
+  for (int j = 0; j < B; ++j) {
+    const int i = i0 + j;
+    if (i < npdf) ls += (double)(w[i] + 1e-5f);
+  }
+  const float tot = (float)wave_sum_d(ls);
+  double lp = 0.0;
+  for (int j = 0; j < B; ++j) {
+    const int i = i0 + j;
+    if (i < npdf) lp += (double)((w[i] + 1e-5f) / tot);
+  }
+  double run = wave_excl_sum(lp, lane);
+  if (lane == 0) cdf[0] = 0.0f;
+  for (int j = 0; j < B; ++j) {
+    const int i = i0 + j;
+    if (i < npdf) {
+      run += (double)((w[i] + 1e-5f) / tot);
+      cdf[i + 1] = (float)run;
+    }
+  }
+  __syncthreads();
+  for (int k = lane; k < n; k += 64) {
+    const float u = u_row ? u_row[k] : linspace01(k, n);
+    int lo = 0, hi = nb;  // first index with cdf > u  (searchsorted right=True)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
+    }
+    const int below = max(lo - 1, 0), above = min(lo, nb - 1);
+    const float c0 = cdf[below], c1 = cdf[above];
+    float denom = c1 - c0;
+    if (denom < 1e-5f) denom = 1.0f;
+    const float t = (u - c0) / denom;
+    const float b0 = bins[below], b1 = bins[above];
+    out[k] = b0 + t * (b1 - b0);
+  }
+}
+
+// standalone sample_pdf(bins (R,nb), weights (R,nb-1)) -> (R,n), one wave per ray; LDS: bins | w | cdf
+__global__ __launch_bounds__(256) void k_sample_pdf(const float* __restrict__ bins_g, const float* __restrict__ w_g,
+                                                    int64_t n_rays, int nb, int n, const float* __restrict__ U,
+                                                    float* __restrict__ out) {
+  extern __shared__ float lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int64_t ray0 = (int64_t)blockIdx.x * nw + wid;
+  const bool active = ray0 < n_rays;
+  const int64_t ray = active ? ray0 : n_rays - 1;
+  float* bins = lds + (size_t)wid * 3 * nb;
+  float* w = bins + nb;
+  float* cdf = w + nb;
+  for (int i = lane; i < nb; i += 64) bins[i] = bins_g[ray * nb + i];
+  for (int i = lane; i < nb - 1; i += 64) w[i] = w_g[ray * (nb - 1) + i];
+  __syncthreads();
+  if (active) {
+    pdf_samples(bins, w, nb, cdf, n, U ? U + ray * n : nullptr, out + ray * n, lane);
+  } else {
+    pdf_samples(bins, w, nb, cdf, 0, nullptr, nullptr, lane);
+  }
+}
+
+// render.py:371-412 + :463-467.  One wave per ray; per-wave LDS: z (S) | w (S) | bins (S) | cdf (S) | sort (P2).
+__global__ __launch_bounds__(256) void k_resample(const float* __restrict__ Z, const float* __restrict__ Wt,
+                                                  int64_t n_rays, int S, int I, int P2,
+                                                  const float* __restrict__ U, float* __restrict__ ZF) {
+  extern __shared__ float lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  const int64_t ray0 = (int64_t)blockIdx.x * nw + wid;
+  const bool active = ray0 < n_rays;
+  const int64_t ray = active ? ray0 : n_rays - 1;
+  float* zs = lds + (size_t)wid * (4 * S + P2);
+  float* ws = zs + S;
+  float* bins = ws + S;
+  float* cdf = bins + S;
+  float* sb = cdf + S;
+  for (int i = lane; i < S; i += 64) {
+    zs[i] = Z[ray * S + i];
+    ws[i] = Wt[ray * S + i];
+  }
+  __syncthreads();
+  const int nbin = S - 1;
+  for (int i = lane; i < nbin; i += 64) bins[i] = 0.5f * (zs[i + 1] + zs[i]);
+  pdf_samples(bins, ws + 1, nbin, cdf, I, U ? U + ray * I : nullptr, sb + S, lane);
+  for (int i = lane; i < S; i += 64) sb[i] = zs[i];
+  for (int i = S + I + lane; i < P2; i += 64) sb[i] = __builtin_inff();
+  __syncthreads();
+  // bitonic sort of P2 values (ascending); every wave of the block runs the same trip counts
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = lane; i < P2; i += 64) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const float a = sb[i], b = sb[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            sb[i] = b;
+            sb[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (active) {
+    const int F = S + I;
+    for (int i = lane; i < F; i += 64) ZF[ray * F + i] = sb[i];
+  }
+}
+
+// ------------------------------------------------------------------------------- loss reductions
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+  v = wave_sum_d(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+    sh[0] = t;
+  }
+  __syncthreads();
+  t = sh[0];
+  __syncthreads();
+  return t;
+}
+
+// plain branch: free = fl32(sum) / R (render.py:121); depth = fl32((1/R)*0.1) * mean(SmoothL1) (render.py:155)
+__global__ void k_child_loss_plain(const float* __restrict__ fr, const float* __restrict__ sl, int64_t n,
+                                   float* __restrict__ out) {
+  __shared__ double sh[16];
+  double a = 0.0, b = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    a += (double)fr[i];
+    b += (double)sl[i];
+  }
+  a = block_sum_d(a, sh);
+  b = block_sum_d(b, sh);
+  if (threadIdx.x == 0) {
+    const float nf = (float)n;
+    out[0] = (float)a / nf;
+    const float mean = (float)b / nf;
+    out[1] = (float)((1.0 / (double)n) * 0.1) * mean;
+  }
+}
+
+// divide branch: per child id c in 1..N (render.py:111-119, :140-152)
+__global__ void k_child_loss_scatter(const float* __restrict__ fr, const float* __restrict__ sl, int64_t n,
+                                     const float* __restrict__ cid, int stride, int N, double* __restrict__ acc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float c = cid[i * stride];
+  const int k = (int)floorf(c - 0.5f);  // candidate child slot: c in (k+0.5, k+1.5)
+  if (k < 0 || k >= N) return;
+  if (!(c > (float)k + 0.5f && c < (float)k + 1.5f)) return;
+  atomicAdd(acc + 3 * k + 0, (double)fr[i]);
+  atomicAdd(acc + 3 * k + 1, (double)sl[i]);
+  atomicAdd(acc + 3 * k + 2, 1.0);
+}
+
+__global__ void k_child_loss_divide(const double* __restrict__ acc, int N, float* __restrict__ out) {
+  __shared__ double sh[16];
+  double a = 0.0, b = 0.0;
+  for (int k = threadIdx.x; k < N; k += blockDim.x) {
+    const double cnt = acc[3 * k + 2];
+    if (cnt >= 1.0) {
+      const float c32 = (float)cnt;
+      a += (double)((float)acc[3 * k + 0] / c32);
+      const float inv = 1.0f / c32;
+      b += (double)((inv * 0.1f) * ((float)acc[3 * k + 1] / c32));
+    }
+  }
+  a = block_sum_d(a, sh);
+  b = block_sum_d(b, sh);
+  if (threadIdx.x == 0) {
+    out[0] = (float)a;
+    out[1] = (float)b;
+  }
+}
+
+__global__ void k_pointwise_loss(const float* __restrict__ a, const float* __restrict__ b,
+                                 const uint8_t* __restrict__ m, int64_t n, int kind, float* __restrict__ out) {
+  __shared__ double sh[16];
+  double s = 0.0, c = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (m && !m[i]) continue;
+    const float d = a[i] - b[i];
+    float v;
+    if (kind == 0) v = d * d;
+    else if (kind == 1) v = fabsf(d);
+    else v = smooth_l1(a[i], b[i]);
+    s += (double)v;
+    c += 1.0;
+  }
+  s = block_sum_d(s, sh);
+  c = block_sum_d(c, sh);
+  if (threadIdx.x == 0) out[0] = (float)s / (float)c;  // mean of an empty selection is nan, like torch
+}
+
+}  // namespace pcn
+
+using namespace pcn;
+
+extern "C" int pcnerf_abi_version(void) { return PCNERF_ABI_VERSION; }
+extern "C" const char* pcnerf_last_error(void) { return g_last_error.c_str(); }
+
+static inline unsigned nblk(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+extern "C" int pcnerf_sample_coarse(const float* rays, int64_t n_rays, int ray_stride, int near_col, int far_col,
+                                    int child_near_col, int child_far_col, int n_samples, int n_parent, float* z,
+                                    void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z, "pcnerf_sample_coarse: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_sample_coarse: empty input");
+  PCN_CHECK(n_parent >= 1 && n_parent <= n_samples, "pcnerf_sample_coarse: n_parent out of range");
+  const int maxc = near_col > far_col ? near_col : far_col;
+  PCN_CHECK(maxc < ray_stride && child_near_col < ray_stride && child_far_col < ray_stride,
+            "pcnerf_sample_coarse: column outside ray row");
+  ProfScope ps((hipStream_t)stream, PT_SAMPLE, 0.0, (double)n_rays * (4.0 * ray_stride + 4.0 * n_samples));
+  hipLaunchKernelGGL(k_sample_coarse, dim3(nblk(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, rays, n_rays,
+                     ray_stride, near_col, far_col, child_near_col, child_far_col, n_samples, n_parent, z);
+  PCN_LAUNCH_CHECK("pcnerf_sample_coarse");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_perturb(const float* z, int64_t n_rays, int n_samples, float perturb, const float* rand,
+                              float* z_out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(z && rand && z_out && z != z_out, "pcnerf_perturb: null or aliased argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_perturb: empty input");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  hipLaunchKernelGGL(k_perturb, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream, z, total, n_samples,
+                     perturb, rand, z_out);
+  PCN_LAUNCH_CHECK("pcnerf_perturb");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, int n_samples, const float* noise,
+                                float noise_std, float eps, const float* rays, int ray_stride, int child_near_col,
+                                int child_far_col, int range_col, float* weights, float* depth, float* free_ray,
+                                float* sl1_ray, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(p && z && depth, "pcnerf_composite: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_composite: empty input");
+  if (rays) {
+    PCN_CHECK(free_ray && sl1_ray, "pcnerf_composite: child losses need free_ray and sl1_ray");
+    PCN_CHECK(child_near_col < ray_stride && child_far_col < ray_stride && range_col < ray_stride,
+              "pcnerf_composite: column outside ray row");
+  }
+  const int B = (n_samples + 63) / 64;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(nblk(n_rays, 4)), b(256);
+  const double ns = (double)n_rays * n_samples;
+  ProfScope ps(s, PT_COMPOSITE, 0.0, ns * (weights ? 12.0 : 8.0) + (rays ? 60.0 * n_rays : 0.0) + 12.0 * n_rays);
+#define PCN_COMP(MB)                                                                                          \
+  hipLaunchKernelGGL(k_composite<MB>, g, b, 0, s, p, z, n_rays, n_samples, noise, noise_std, eps, rays,      \
+                     ray_stride, child_near_col, child_far_col, range_col, weights, depth, free_ray, sl1_ray, \
+                     (int*)nullptr)
+  if (B <= 2) PCN_COMP(2);
+  else if (B <= 6) PCN_COMP(6);
+  else if (B <= 16) PCN_COMP(16);
+  else if (B <= 64) PCN_COMP(64);
+  else if (B <= 256) PCN_COMP(256);
+  else PCN_CHECK(false, "pcnerf_composite: more than 16384 samples per ray");
+#undef PCN_COMP
+  PCN_LAUNCH_CHECK("pcnerf_composite");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_resample(const float* z, const float* weights, int64_t n_rays, int n_samples, int n_importance,
+                               const float* u, float* z_fine, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(z && weights && z_fine, "pcnerf_resample: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples >= 3 && n_importance > 0, "pcnerf_resample: need n_samples >= 3");
+  const int F = n_samples + n_importance;
+  int P2 = 1;
+  while (P2 < F) P2 <<= 1;
+  const size_t per_wave = (size_t)(4 * n_samples + P2) * sizeof(float);
+  const size_t lds_max = 160 * 1024;
+  PCN_CHECK(per_wave <= lds_max, "pcnerf_resample: n_samples + n_importance too large for one wave's LDS");
+  int nw = (int)(lds_max / per_wave);
+  if (nw > 4) nw = 4;
+  if (nw > 1 && per_wave * nw > 64 * 1024) nw = (int)((64 * 1024) / per_wave) > 0 ? (int)((64 * 1024) / per_wave) : 1;
+  if (per_wave * nw > 64 * 1024)
+    PCN_HIP(hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(per_wave * nw)));
+  ProfScope ps((hipStream_t)stream, PT_RESAMPLE, 0.0,
+               (double)n_rays * (8.0 * n_samples + 4.0 * F + (u ? 4.0 * n_importance : 0.0)));
+  hipLaunchKernelGGL(k_resample, dim3(nblk(n_rays, nw)), dim3(64 * nw), per_wave * nw, (hipStream_t)stream, z,
+                     weights, n_rays, n_samples, n_importance, P2, u, z_fine);
+  PCN_LAUNCH_CHECK("pcnerf_resample");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_sample_pdf(const float* bins, const float* weights, int64_t n_rays, int n_bins, int n_samples,
+                                 const float* u, float* out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(bins && weights && out, "pcnerf_sample_pdf: null argument");
+  PCN_CHECK(n_rays > 0 && n_bins >= 2 && n_samples > 0, "pcnerf_sample_pdf: need n_bins >= 2");
+  const size_t per_wave = (size_t)3 * n_bins * sizeof(float);
+  PCN_CHECK(per_wave <= 64 * 1024, "pcnerf_sample_pdf: too many bins");
+  int nw = (int)((64 * 1024) / per_wave);
+  if (nw > 4) nw = 4;
+  hipLaunchKernelGGL(k_sample_pdf, dim3(nblk(n_rays, nw)), dim3(64 * nw), per_wave * nw, (hipStream_t)stream, bins,
+                     weights, n_rays, n_bins, n_samples, u, out);
+  PCN_LAUNCH_CHECK("pcnerf_sample_pdf");
+  PCN_API_END
+}
+
+extern "C" size_t pcnerf_child_loss_workspace_bytes(int n) { return (size_t)(n > 0 ? n : 1) * 3 * sizeof(double); }
+
+extern "C" int pcnerf_child_loss_reduce(const float* free_ray, const float* sl1_ray, int64_t n_rays,
+                                        const float* child_id, int id_stride, int sub_nerf_test_num, void* workspace,
+                                        float* out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(free_ray && sl1_ray && out, "pcnerf_child_loss_reduce: null argument");
+  PCN_CHECK(n_rays > 0, "pcnerf_child_loss_reduce: empty input");
+  hipStream_t s = (hipStream_t)stream;
+  if (sub_nerf_test_num <= 0) {
+    hipLaunchKernelGGL(k_child_loss_plain, dim3(1), dim3(1024), 0, s, free_ray, sl1_ray, n_rays, out);
+  } else {
+    PCN_CHECK(child_id && workspace, "pcnerf_child_loss_reduce: divide branch needs child ids and workspace");
+    PCN_HIP(hipMemsetAsync(workspace, 0, pcnerf_child_loss_workspace_bytes(sub_nerf_test_num), s));
+    hipLaunchKernelGGL(k_child_loss_scatter, dim3(nblk(n_rays, 256)), dim3(256), 0, s, free_ray, sl1_ray, n_rays,
+                       child_id, id_stride, sub_nerf_test_num, (double*)workspace);
+    hipLaunchKernelGGL(k_child_loss_divide, dim3(1), dim3(1024), 0, s, (const double*)workspace, sub_nerf_test_num,
+                       out);
+  }
+  PCN_LAUNCH_CHECK("pcnerf_child_loss_reduce");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_pointwise_loss(const float* pred, const float* target, const uint8_t* mask, int64_t n,
+                                     int kind, float* out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(pred && target && out, "pcnerf_pointwise_loss: null argument");
+  PCN_CHECK(n > 0, "pcnerf_pointwise_loss: empty input");
+  PCN_CHECK(kind >= 0 && kind <= 2, "pcnerf_pointwise_loss: kind must be 0 (mse), 1 (l1) or 2 (smoothl1)");
+  hipLaunchKernelGGL(k_pointwise_loss, dim3(1), dim3(1024), 0, (hipStream_t)stream, pred, target, mask, n, kind,
+                     out);
+  PCN_LAUNCH_CHECK("pcnerf_pointwise_loss");
+  PCN_API_END
+}

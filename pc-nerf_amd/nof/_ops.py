@@ -1,0 +1,246 @@
+"""Tensor-level wrappers over the C ABI (include/pcnerf_hip.h).
+
+Every function takes ROCm device tensors, allocates its outputs with torch (memory only), and enqueues the HIP
+kernels on the current stream.  Nothing here computes on the host.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _hip as H
+
+# ----------------------------------------------------------------------------------------------- utilities
+_ws_cache: dict = {}
+
+
+def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """Grow-only scratch buffer per device (torch caching allocator memory)."""
+    key = (device.type, device.index)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    H.require_device(t)
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _bn_config(model):
+    norms = model.norms()
+    mom, eps = norms[0].momentum, norms[0].eps
+    for bn in norms:
+        if bn.momentum != mom or bn.eps != eps or not bn.track_running_stats or not bn.affine:
+            raise NotImplementedError("HIP NOF kernels need identical affine BatchNorm1d layers with running stats")
+    if mom is None:
+        raise NotImplementedError("BatchNorm1d(momentum=None) (cumulative averaging) is not supported")
+    return float(mom), float(eps)
+
+
+def _params(model) -> tuple[H.NofParams, list]:
+    """Device pointers of a NOF module's parameters in reference state_dict order."""
+    keep = []
+    s = H.NofParams()
+
+    def p(t):
+        H.require_device(t)
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError("NOF parameters must be contiguous float32 device tensors")
+        keep.append(t)
+        return t.data_ptr()
+
+    for i, lin in enumerate(model.linears()):
+        s.lin_w[i] = p(lin.weight)
+        s.lin_b[i] = p(lin.bias)
+    for i, bn in enumerate(model.norms()):
+        s.bn_w[i] = p(bn.weight)
+        s.bn_b[i] = p(bn.bias)
+        s.bn_rm[i] = p(bn.running_mean)
+        s.bn_rv[i] = p(bn.running_var)
+    s.out_w = p(model.occ_out[0].weight)
+    s.out_b = p(model.occ_out[0].bias)
+    return s, keep
+
+
+def _stream(t: torch.Tensor):
+    return H.stream_of(t)
+
+
+# ----------------------------------------------------------------------------------------------- network
+def pack_eval(model, device) -> torch.Tensor:
+    """Eval-mode network image (BN folded, MFMA operand order); rebuilt per call (weights may change)."""
+    L = H.lib()
+    out = torch.empty(L.pcnerf_nof_eval_packed_floats(), dtype=torch.float32, device=device)
+    s, keep = _params(model)
+    _bn_config(model)
+    H.check(L.pcnerf_nof_pack_eval(ctypes.byref(s), out.data_ptr(), _stream(out)))
+    return out
+
+
+def _track_batches(model, n_chunks: int) -> None:
+    for bn in model.norms():
+        if bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(n_chunks)
+
+
+def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int) -> torch.Tensor:
+    """Occupancy p (R, S) of the samples o + d*z through Embedding + NOF (render.py:18-25 / 44-51)."""
+    L = H.lib()
+    R, S = z.shape
+    p = torch.empty((R, S), dtype=torch.float32, device=z.device)
+    st = _stream(z)
+    if model.training:
+        mom, eps = _bn_config(model)
+        s, keep = _params(model)
+        nbytes = L.pcnerf_nof_train_workspace_bytes(int(chunk))
+        ws = _workspace(z.device, nbytes)
+        H.check(L.pcnerf_nof_query_train(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                         ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(), p.data_ptr(), st))
+        _track_batches(model, -(-R * S // int(chunk)))
+    else:
+        packed = pack_eval(model, z.device)
+        H.check(L.pcnerf_nof_query_eval(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, packed.data_ptr(),
+                                        p.data_ptr(), st))
+    return p
+
+
+def nof_forward_embedded(model, x: torch.Tensor) -> torch.Tensor:
+    """NOF.forward on a (B, 63) embedded batch (one BatchNorm batch in train mode)."""
+    L = H.lib()
+    x = _f32(x)
+    if x.dim() != 2 or x.shape[1] != 63:
+        raise RuntimeError(f"expected (B, 63) embedded input, got {tuple(x.shape)}")
+    B = x.shape[0]
+    out = torch.empty((B, 1), dtype=torch.float32, device=x.device)
+    st = _stream(x)
+    if model.training:
+        if B <= 1:
+            raise ValueError("Expected more than 1 value per channel when training")
+        mom, eps = _bn_config(model)
+        s, keep = _params(model)
+        ws = _workspace(x.device, L.pcnerf_nof_train_workspace_bytes(B))
+        H.check(L.pcnerf_nof_forward_train(x.data_ptr(), B, ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(),
+                                           out.data_ptr(), st))
+        _track_batches(model, 1)
+    else:
+        packed = pack_eval(model, x.device)
+        H.check(L.pcnerf_nof_forward_eval(x.data_ptr(), B, packed.data_ptr(), out.data_ptr(), st))
+    return out
+
+
+def embed(x: torch.Tensor) -> torch.Tensor:
+    x = _f32(x)
+    if x.shape[-1] != 3:
+        raise RuntimeError("Embedding(3, 10) expects (..., 3) input")
+    flat = x.reshape(-1, 3)
+    out = torch.empty((flat.shape[0], 63), dtype=torch.float32, device=x.device)
+    H.check(H.lib().pcnerf_embed(flat.data_ptr(), flat.shape[0], out.data_ptr(), _stream(x)))
+    return out.reshape(*x.shape[:-1], 63)
+
+
+# ----------------------------------------------------------------------------------------------- render stages
+def sample_coarse(rays, n_samples, n_parent, near_col, far_col, cn_col=0, cf_col=0) -> torch.Tensor:
+    R = rays.shape[0]
+    z = torch.empty((R, n_samples), dtype=torch.float32, device=rays.device)
+    H.check(H.lib().pcnerf_sample_coarse(rays.data_ptr(), R, rays.shape[1], near_col, far_col, cn_col, cf_col,
+                                         n_samples, n_parent, z.data_ptr(), _stream(rays)))
+    return z
+
+
+def perturb(z, amount: float, rand: torch.Tensor) -> torch.Tensor:
+    rand = _f32(rand)
+    if rand.shape != z.shape:
+        raise RuntimeError(f"perturbation draws {tuple(rand.shape)} != z {tuple(z.shape)}")
+    out = torch.empty_like(z)
+    H.check(H.lib().pcnerf_perturb(z.data_ptr(), z.shape[0], z.shape[1], float(amount), rand.data_ptr(),
+                                   out.data_ptr(), _stream(z)))
+    return out
+
+
+def composite(p, z, noise=None, noise_std=0.0, eps=1e-10, rays=None, cn_col=10, cf_col=11, range_col=14,
+              want_weights=True):
+    """-> (weights or None, depth (R,), free_ray (R,) or None, sl1_ray (R,) or None)."""
+    R, S = z.shape
+    dev = z.device
+    w = torch.empty((R, S), dtype=torch.float32, device=dev) if want_weights else None
+    depth = torch.empty((R,), dtype=torch.float32, device=dev)
+    fr = sl = None
+    if rays is not None:
+        fr = torch.empty((R,), dtype=torch.float32, device=dev)
+        sl = torch.empty((R,), dtype=torch.float32, device=dev)
+    if noise is not None:
+        noise = _f32(noise)
+        if noise.shape != z.shape:
+            raise RuntimeError("noise draws must have the shape of the samples")
+    H.check(H.lib().pcnerf_composite(p.data_ptr(), z.data_ptr(), R, S, H.ptr(noise), float(noise_std), float(eps),
+                                     H.ptr(rays), rays.shape[1] if rays is not None else 0, cn_col, cf_col, range_col,
+                                     H.ptr(w), depth.data_ptr(), H.ptr(fr), H.ptr(sl), _stream(z)))
+    return w, depth, fr, sl
+
+
+def resample(z, w, n_importance: int, u=None) -> torch.Tensor:
+    R, S = z.shape
+    if u is not None:
+        u = _f32(u)
+        if u.shape != (R, n_importance):
+            raise RuntimeError(f"u draws {tuple(u.shape)} != ({R}, {n_importance})")
+    zf = torch.empty((R, S + n_importance), dtype=torch.float32, device=z.device)
+    H.check(H.lib().pcnerf_resample(z.data_ptr(), w.data_ptr(), R, S, int(n_importance), H.ptr(u), zf.data_ptr(),
+                                    _stream(z)))
+    return zf
+
+
+def sample_pdf_standalone(bins, weights, n_samples: int, det: bool, u=None) -> torch.Tensor:
+    bins, weights = _f32(bins), _f32(weights)
+    R, nb = bins.shape
+    if weights.shape != (R, nb - 1):
+        raise RuntimeError(f"weights {tuple(weights.shape)} must be (R, n_bins - 1) = ({R}, {nb - 1})")
+    if not det and u is None:
+        u = torch.rand((R, n_samples), device=bins.device)
+    if u is not None:
+        u = _f32(u)
+    out = torch.empty((R, n_samples), dtype=torch.float32, device=bins.device)
+    H.check(H.lib().pcnerf_sample_pdf(bins.data_ptr(), weights.data_ptr(), R, nb, int(n_samples),
+                                      H.ptr(None if det else u), out.data_ptr(), _stream(bins)))
+    return out
+
+
+def child_losses(free_ray, sl1_ray, rays, divide: bool, sub_nerf_test_num: int):
+    """-> (child_free_loss, child_depth_loss) device tensors; shape (1,) in the divide branch (render.py:109,138
+    start from torch.tensor([0])), () otherwise."""
+    L = H.lib()
+    R = free_ray.shape[0]
+    out = torch.empty((2,), dtype=torch.float32, device=free_ray.device)
+    n = int(sub_nerf_test_num) if divide else 0
+    ws = _workspace(free_ray.device, L.pcnerf_child_loss_workspace_bytes(n)) if n > 0 else None
+    H.check(L.pcnerf_child_loss_reduce(free_ray.data_ptr(), sl1_ray.data_ptr(), R,
+                                       rays.data_ptr() + 9 * 4 if n > 0 else None, rays.shape[1], n,
+                                       H.ptr(ws), out.data_ptr(), _stream(free_ray)))
+    if n > 0:
+        return out[0:1], out[1:2]
+    return out[0], out[1]
+
+
+_KIND = {"mse": 0, "l1": 1, "smoothl1": 2}
+
+
+def pointwise_loss(pred, target, kind: str, valid_mask=None) -> torch.Tensor:
+    pred, target = _f32(pred), _f32(target)
+    if pred.shape != target.shape:
+        raise RuntimeError(f"loss inputs differ in shape: {tuple(pred.shape)} vs {tuple(target.shape)}")
+    m = None
+    if valid_mask is not None:
+        H.require_device(valid_mask)
+        m = valid_mask.to(torch.uint8).contiguous()
+        if m.numel() != pred.numel():
+            raise RuntimeError("valid_mask must match the loss inputs")
+    out = torch.empty((), dtype=torch.float32, device=pred.device)
+    H.check(H.lib().pcnerf_pointwise_loss(pred.data_ptr(), target.data_ptr(), H.ptr(m), pred.numel(), _KIND[kind],
+                                          out.data_ptr(), _stream(pred)))
+    return out

@@ -1,0 +1,125 @@
+"""PC-NeRF LiDAR volume rendering -- drop-in for ``nof/render.py`` of the reference, on MI355X HIP kernels.
+
+Same function names, signatures, result keys, shapes and dtypes as the reference.  Each stage is a kernel of
+lib/libpcnerf_hip.so (see include/pcnerf_hip.h):
+
+    coarse z sampling (+segmented merge)  pcnerf_sample_coarse      render.py:429-442
+    stratified perturbation               pcnerf_perturb            render.py:449-454
+    Embedding + NOF query (chunked BN)    pcnerf_nof_query_*        render.py:18-25 / 44-51, models.py
+    compositing, child masks, loss terms  pcnerf_composite          render.py:51-61, 75-159
+    sample_pdf + sort(cat(z, samples))    pcnerf_resample           render.py:371-412, 463-467
+    child loss reductions                 pcnerf_child_loss_reduce  render.py:102-159
+
+Differences from the reference, all deliberate:
+  * everything stays on ``rays.device`` (the reference pins ``u`` to ``cuda:0``, render.py:397);
+  * RNG: draws are taken from torch's generator on the device, and only when used (the reference also draws
+    ``randn`` noise when ``noise_std == 0``).  Parity tests inject the draws with the keyword-only ``rng``
+    dict: ``perturb_rand`` (R,S), ``noise`` (R,S), ``u`` (R,I), ``noise_fine`` (R,S+I);
+  * gradients: this round ships the forward path; calling with autograd enabled on parameters that require
+    grad raises (run under ``torch.no_grad()``).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _ops
+from .networks import NOF, Embedding, NOF_coarse, NOF_fine, NOF_plusfine  # noqa: F401  (reference exports)
+
+__all__ = ['render_rays']
+
+EPSILON = 1e-10  # render.py:456, :514, :656
+
+
+def _check_inputs(model, model_fine, embedding_xy, rays, n_cols):
+    if not rays.is_cuda:
+        raise RuntimeError("nof.render (HIP) renders device-resident rays; move them with rays.to('cuda') -- there "
+                           "is no CPU path")
+    if rays.dim() != 2 or rays.shape[1] < n_cols:
+        raise RuntimeError(f"rays must be (N_rays, >={n_cols}); got {tuple(rays.shape)}")
+    if embedding_xy is not None and not embedding_xy.supported():
+        raise NotImplementedError("HIP render supports Embedding(3, 10) (L_pos = 10)")
+    for m in (model, model_fine):
+        if not m.supported():
+            raise NotImplementedError("HIP render supports NOF(feature_size=256, in_channels_xy=63, use_skip=True)")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in m.parameters()):
+            raise NotImplementedError("the HIP render path is forward-only in this release; call it under "
+                                      "torch.no_grad()")
+    return rays.float().contiguous()
+
+
+def _draw(rng, key, shape, device, fn):
+    if rng is not None and key in rng:
+        t = rng[key]
+        return t.to(device=device, dtype=torch.float32).contiguous()
+    return fn(shape, device=device)
+
+
+def _coarse(rays, N_samples, segmented, ratio, perturb, rng):
+    """render.py:429-454."""
+    R = rays.shape[0]
+    n_parent = int(N_samples * (1 - ratio)) if segmented else N_samples
+    z = _ops.sample_coarse(rays, N_samples, n_parent, 6, 7, 10, 11)
+    if perturb > 0:
+        z = _ops.perturb(z, perturb, _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
+    return z
+
+
+def _noise(rng, key, z, noise_std):
+    if noise_std == 0:
+        return None
+    return _draw(rng, key, tuple(z.shape), z.device, torch.randn)
+
+
+def sample_pdf(bins, weights, N_samples, det=False, pytest=False, *, u=None):
+    """render.py:371-412: inverse-CDF samples, unsorted, ``bins`` (R, B), ``weights`` (R, B-1) -> (R, N).
+    ``u`` (keyword-only) injects the uniform draws when ``det`` is False."""
+    if pytest:
+        raise NotImplementedError("sample_pdf(pytest=True) (numpy-seeded draws) is not supported on the device")
+    return _ops.sample_pdf_standalone(bins, weights, N_samples, det, u)
+
+
+def render_rays_train(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: torch.Tensor, sub_nerf_test_num=4,
+                      N_samples=64, N_importance=128, use_disp=False, perturb=0, noise_std=1, chunk=1024 * 3,
+                      isval=False, issegmentated=0, childnerf_ratio=0.5, use_child_nerf_divide=0,
+                      use_child_nerf_loss=0, *, rng=None):
+    """render.py:416-482 -> {'child_free_loss_fine', 'child_depth_loss_fine', 'depth_fine', 'child_free_loss',
+    'child_depth_loss', 'depth'}."""
+    rays = _check_inputs(model, model_fine, embedding_xy, rays, 15)
+    R = rays.shape[0]
+    z = _coarse(rays, N_samples, issegmentated, childnerf_ratio, perturb, rng)
+    with_losses = use_child_nerf_loss == 1
+
+    def one_pass(m, z, noise_key):
+        p = _ops.query(m, rays, z, chunk)
+        w, depth, fr, sl = _ops.composite(p, z, _noise(rng, noise_key, z, noise_std), noise_std, EPSILON,
+                                          rays if with_losses else None)
+        if with_losses:
+            free, dl = _ops.child_losses(fr, sl, rays, use_child_nerf_divide == 1, sub_nerf_test_num)
+        else:
+            free, dl = torch.tensor(0.0), torch.tensor(0.0)   # render.py:123-125, 157-159 (CPU scalars)
+        return w, depth, free, dl
+
+    w, depth, free, dl = one_pass(model, z, "noise")
+    u = None if perturb == 0 else _draw(rng, "u", (R, N_importance), rays.device, torch.rand)
+    zf = _ops.resample(z, w, N_importance, u)
+    _, depth_f, free_f, dl_f = one_pass(model_fine, zf, "noise_fine")
+    return {'child_free_loss_fine': free_f, 'child_depth_loss_fine': dl_f, "depth_fine": depth_f,
+            'child_free_loss': free, 'child_depth_loss': dl, 'depth': depth}
+
+
+def render_rays_val(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: torch.Tensor, sub_nerf_test_num=4,
+                    N_samples=64, N_importance=128, use_disp=False, perturb=0, noise_std=1, chunk=1024 * 3,
+                    isval=False, *, rng=None):
+    """render.py:485-536 -> {'depth_fine', 'depth'}."""
+    rays = _check_inputs(model, model_fine, embedding_xy, rays, 8)
+    R = rays.shape[0]
+    z = _coarse(rays, N_samples, False, 0.0, perturb, rng)
+    p = _ops.query(model, rays, z, chunk)
+    w, depth, _, _ = _ops.composite(p, z, _noise(rng, "noise", z, noise_std), noise_std, EPSILON)
+    u = None if perturb == 0 else _draw(rng, "u", (R, N_importance), rays.device, torch.rand)
+    zf = _ops.resample(z, w, N_importance, u)
+    pf = _ops.query(model_fine, rays, zf, chunk)
+    _, depth_f, _, _ = _ops.composite(pf, zf, _noise(rng, "noise_fine", zf, noise_std), noise_std, EPSILON,
+                                      want_weights=False)
+    return {"depth_fine": depth_f, 'depth': depth}

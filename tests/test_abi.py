@@ -1,0 +1,56 @@
+"""C-ABI library: loads on a machine without a GPU and exports every entry point include/pcnerf_hip.h declares."""
+import os
+import re
+
+from conftest import REPO
+
+
+def declared_functions():
+    txt = open(os.path.join(REPO, "include", "pcnerf_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(pcnerf_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_loads_and_exports_header_symbols():
+    from nof import _hip
+    L = _hip.lib()
+    names = declared_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_hip.exported_symbols()), set(names) ^ set(_hip.exported_symbols())
+    assert L.pcnerf_abi_version() == 1
+
+
+def test_size_queries_without_gpu():
+    from nof import _hip
+    L = _hip.lib()
+    assert L.pcnerf_nof_eval_packed_floats() == 2 * 16384 + 7 * 65536 + 8 * 256 + 256 + 4
+    # two chunk-sized activation buffers dominate the train workspace
+    assert L.pcnerf_nof_train_workspace_bytes(262144) >= 2 * 262144 * 256 * 4
+    assert L.pcnerf_child_loss_workspace_bytes(15333) == 15333 * 3 * 8
+
+
+def test_argument_errors_are_reported_before_launch():
+    from nof import _hip
+    L = _hip.lib()
+    rc = L.pcnerf_composite(None, None, 0, 0, None, 0.0, 0.0, None, 0, 0, 0, 0, None, None, None, None, None)
+    assert rc != 0
+    assert b"null" in L.pcnerf_last_error()
+
+
+def test_render_refuses_cpu_tensors():
+    import pytest
+    import torch
+    from nof.networks import Embedding, NOF_coarse, NOF_fine
+    from nof.render import render_rays_val
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        with torch.no_grad():
+            render_rays_val(NOF_coarse(), NOF_fine(), Embedding(3, 10), torch.zeros(4, 15))
+
+
+def test_state_dict_keys_match_reference_layout():
+    from nof import synthetic as syn
+    from nof.networks import NOF_coarse
+    keys = set(NOF_coarse().state_dict())
+    assert keys == set(syn.init_nof_params(0))

@@ -1,0 +1,181 @@
+"""HIP path vs the reference: golden vectors (made by importing the reference) and the CPU oracle.
+
+Tolerances (north star: depth and losses within 1e-4 relative fp32 of the reference PyTorch path):
+  depth / depth_fine / losses: rtol 1e-4 (atol 1e-6 for values near zero);
+  network outputs p: rtol 2e-5; embeddings: atol 2e-6 (sinf/cosf differ from torch CPU by <= 1-2 ulp);
+  BatchNorm running stats: rtol 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from nof import synthetic as syn
+from nof.networks import Embedding, NOF_coarse, NOF_fine
+from nof import render as R
+from oracle import ref_cpu as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SEED_C, SEED_F = 1234, 5678
+RTOL = 1e-4
+
+
+def models(train):
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(SEED_C)).to(DEV).train(train)
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(SEED_F)).to(DEV).train(train)
+    return Embedding(3, 10), mc, mf
+
+
+def close(a, b, rtol=RTOL, atol=1e-6, what=""):
+    a = a.detach().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    np.testing.assert_allclose(a.astype(np.float64), b.astype(np.float64), rtol=rtol, atol=atol, err_msg=what)
+
+
+def running(m):
+    return np.stack([np.stack([bn.running_mean.cpu().numpy(), bn.running_var.cpu().numpy()]) for bn in m.norms()])
+
+
+def test_embedding():
+    g = golden("nof_eval")
+    e = Embedding(3, 10)(torch.from_numpy(g["points"]).to(DEV))
+    close(e, g["embedding"], 0, 2e-6, "embedding")
+
+
+def test_nof_eval_forward():
+    g = golden("nof_eval")
+    _, mc, _ = models(False)
+    with torch.no_grad():
+        p = mc(torch.from_numpy(g["embedding"]).to(DEV))
+    close(p, g["p"], 2e-5, 1e-7, "p eval")
+
+
+def test_nof_train_forward_chunks_and_running_stats():
+    g = golden("nof_train")
+    _, mc, _ = models(True)
+    emb = Embedding(3, 10)
+    x = torch.from_numpy(g["points"]).to(DEV)
+    c = int(g["chunk"])
+    with torch.no_grad():
+        p = torch.cat([mc(emb(x[i:i + c])) for i in range(0, len(x), c)])
+    close(p, g["p"], 2e-5, 1e-7, "p train")
+    close(running(mc), g["running"], RTOL, 1e-7, "running stats")
+    assert int(mc.norms()[0].num_batches_tracked) == -(-len(x) // c)
+
+
+def test_sample_pdf():
+    g = golden("sample_pdf")
+    b, w = torch.from_numpy(g["bins"]).to(DEV), torch.from_numpy(g["weights"]).to(DEV)
+    close(R.sample_pdf(b, w, 96, det=True), g["samples_det"], 1e-5, 1e-5, "det")
+    u = torch.from_numpy(g["u"]).to(DEV)
+    close(R.sample_pdf(b, w, 96, det=False, u=u), g["samples_rand"], 1e-5, 1e-5, "rand")
+
+
+@pytest.mark.parametrize("S", [64, 128])
+def test_render_val(S):
+    g = golden(f"render_val_s{S}")
+    emb, mc, mf = models(False)
+    with torch.no_grad():
+        res = R.render_rays_val(mc, mf, emb, torch.from_numpy(g["rays"]).to(DEV), N_samples=S,
+                                N_importance=int(g["N_importance"]), perturb=0, noise_std=0, chunk=int(g["chunk"]))
+    assert set(res) == {"depth", "depth_fine"}
+    close(res["depth"], g["depth"], what="depth")
+    close(res["depth_fine"], g["depth_fine"], what="depth_fine")
+
+
+TRAIN = ["pcnerf", "pcnerf_noseg", "pcnerf_divide", "original", "pcnerf_perturb", "pcnerf_s128"]
+
+
+@pytest.mark.parametrize("name", TRAIN)
+def test_render_train(name):
+    g = golden(f"render_train_{name}")
+    emb, mc, mf = models(True)
+    rng = {k: torch.from_numpy(g[k]).to(DEV) for k in ("perturb_rand", "u") if k in g}
+    rays = torch.from_numpy(g["rays"]).to(DEV)
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=int(g["sub_nerf_test_num"]),
+                                  N_samples=int(g["N_samples"]), N_importance=int(g["N_importance"]),
+                                  perturb=int(g["perturb"]), noise_std=0, chunk=int(g["chunk"]),
+                                  issegmentated=int(g["issegmentated"]),
+                                  childnerf_ratio=float(g["childnerf_ratio"]),
+                                  use_child_nerf_divide=int(g["use_child_nerf_divide"]),
+                                  use_child_nerf_loss=int(g["use_child_nerf_loss"]), rng=rng)
+    assert set(res) == {"child_free_loss_fine", "child_depth_loss_fine", "depth_fine", "child_free_loss",
+                        "child_depth_loss", "depth"}
+    close(res["depth"], g["depth"], what="depth")
+    close(res["depth_fine"], g["depth_fine"], what="depth_fine")
+    for k in ("child_free_loss", "child_depth_loss", "child_free_loss_fine", "child_depth_loss_fine"):
+        close(res[k], g[k], RTOL, 1e-9, k)
+    # range losses through the drop-in criteria (train_kitti.py:121-155)
+    from nof.criteria import nof_loss
+    loss = nof_loss["smoothl1"]()
+    gt = rays[:, 14]
+    if int(g["use_child_nerf_divide"]):
+        lr = torch.zeros(1, device=DEV)
+        lrf = torch.zeros(1, device=DEV)
+        sub = rays[:, 9]
+        for i in range(int(g["sub_nerf_test_num"])):
+            m = torch.logical_and(sub > (i + 0.5), sub < (i + 1.5))
+            if int(m.sum()) >= 1:
+                lr = lr + 1e-1 * loss(1e1 * res["depth"][m], 1e1 * gt[m])
+                lrf = lrf + 1e-1 * loss(1e1 * res["depth_fine"][m], 1e1 * gt[m])
+    else:
+        lr = 1e-1 * loss(1e1 * res["depth"], 1e1 * gt)
+        lrf = 1e-1 * loss(1e1 * res["depth_fine"], 1e1 * gt)
+    close(lr, g["loss_range"], what="loss_range")
+    close(lrf, g["loss_range_fine"], what="loss_range_fine")
+    total = lr + lrf + 1e6 * res["child_free_loss_fine"].to(DEV) + 1e6 * res["child_free_loss"].to(DEV) + \
+        1e5 * res["child_depth_loss_fine"].to(DEV) + 1e5 * res["child_depth_loss"].to(DEV)
+    close(total, g["loss_total"], what="loss_total")
+    close(running(mc), g["running_c"], RTOL, 1e-6, "running coarse")
+    close(running(mf), g["running_f"], RTOL, 1e-6, "running fine")
+
+
+def test_render_train_vs_oracle_config2_subset():
+    """Config-2 rays at S=128/I=256 with several BatchNorm chunks, against the CPU oracle."""
+    rays = syn.make_rays(192, seed=3)
+    emb, mc, mf = models(True)
+    kw = dict(sub_nerf_test_num=32, N_samples=128, N_importance=256, perturb=0, noise_std=0, chunk=16384,
+              issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0, use_child_nerf_loss=1)
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays).to(DEV), **kw)
+    ref = O.render_rays_train(O.params_from_numpy(syn.init_nof_params(SEED_C)),
+                              O.params_from_numpy(syn.init_nof_params(SEED_F)), torch.from_numpy(rays), **kw)
+    for k in ("depth", "depth_fine", "child_free_loss", "child_depth_loss", "child_free_loss_fine",
+              "child_depth_loss_fine"):
+        close(res[k], ref[k].numpy(), RTOL, 1e-9, k)
+
+
+def test_eval_query_is_per_sample():
+    """Eval mode: a ray rendered alone equals the same ray rendered inside a large batch (bitwise)."""
+    rays = torch.from_numpy(syn.make_rays(4096, seed=5)).to(DEV)
+    emb, mc, mf = models(False)
+    with torch.no_grad():
+        full = R.render_rays_val(mc, mf, emb, rays, N_samples=128, N_importance=256, perturb=0, noise_std=0)
+        part = R.render_rays_val(mc, mf, emb, rays[1000:1037], N_samples=128, N_importance=256, perturb=0,
+                                 noise_std=0)
+    assert torch.equal(full["depth"][1000:1037], part["depth"])
+    assert torch.equal(full["depth_fine"][1000:1037], part["depth_fine"])
+
+
+def test_full_size_properties():
+    """Config 2 at full size (65,536 rays, 128/256 samples, train mode, chunk 262,144): every depth is finite
+    and lies in [0, parent far]; losses are finite and non-negative; train-mode BatchNorm stats moved."""
+    rays = torch.from_numpy(syn.make_rays(65536, seed=0)).to(DEV)
+    emb, mc, mf = models(True)
+    rm0 = mc.norms()[0].running_mean.clone()
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=32, N_samples=128, N_importance=256,
+                                  perturb=1, noise_std=0, chunk=262144, issegmentated=1, childnerf_ratio=0.1,
+                                  use_child_nerf_loss=1)
+    far = rays[:, 7]
+    for k in ("depth", "depth_fine"):
+        d = res[k]
+        assert torch.isfinite(d).all()
+        assert (d >= -1e-4).all() and (d <= far * (1 + 1e-5) + 1e-4).all()
+    for k in ("child_free_loss", "child_depth_loss", "child_free_loss_fine", "child_depth_loss_fine"):
+        v = float(res[k])
+        assert np.isfinite(v) and v >= 0
+    assert not torch.equal(rm0, mc.norms()[0].running_mean)
