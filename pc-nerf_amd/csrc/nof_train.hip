@@ -2,13 +2,14 @@
 // samples (nof/render.py:47-50 chunk loop; nn.BatchNorm1d train semantics; models.py:183-203).
 //
 // Every BatchNorm needs the statistics of its whole chunk before the next Linear may run, so the network is
-// evaluated layer by layer per chunk:
-//   k_train_layer  : h_L = W'_L x + b'_L on MFMA for the chunk, written raw (pre-BN) to HBM, with per-neuron
-//                    sums of (h - c) and (h - c)^2 (shift c = the expected mean) reduced in the epilogue;
-//   k_bn_fold      : mean / biased var -> alpha = gamma/sqrt(var+eps), beta' = beta - mean*alpha; running
-//                    stats updated (momentum, unbiased var); the BN is folded into the NEXT Linear:
-//                    W'_{L+1} = W_{L+1} diag(alpha), b'_{L+1} = b_{L+1} + W_{L+1} beta' (packed for MFMA);
-//   k_train_out    : occ_out Linear(256,1) on the folded last BN + sigmoid.
+// evaluated layer by layer per chunk, one launch per Linear:
+//   k_train_layer<EP,HP> : prologue: BatchNorm L-1's coefficients from the chunk statistics of h_{L-1},
+//                          alpha = gamma/sqrt(var+eps), beta' = beta - mean*alpha (ATen's transform form; block 0
+//                          also updates running_mean/var with momentum and the unbiased variance);
+//                          body: h_L = W_L (alpha*h_{L-1} + beta') + b_L on MFMA, the BatchNorm applied as the
+//                          activations are loaded; h_L written raw (pre-BN) to HBM with per-neuron sums of
+//                          (h - b) and (h - b)^2 reduced in the epilogue;
+//   k_train_out          : the same prologue for BatchNorm 8, occ_out Linear(256,1) + sigmoid.
 // The activations LeakyReLU(True) are identities (negative_slope == 1) and are not applied.
 //
 // MFMA mapping (v_mfma_f32_32x32x2_f32), samples on rows: out[sample][neuron] = act[sample][:] . W^T[:][neuron]
@@ -23,16 +24,23 @@
 
 namespace pcn {
 
+// tuning knobs (variant builds for A/B timing; defaults are the shipped configuration)
+#ifndef PCN_TRAIN_WAVES
+#define PCN_TRAIN_WAVES 1  // waves per SIMD the layer kernel is compiled for (launch bounds)
+#endif
+#ifndef PCN_XD
+#define PCN_XD 4  // activation prefetch depth in k-groups (divides 32)
+#endif
+#ifndef PCN_WD
+#define PCN_WD 2  // weight prefetch depth in k-groups (divides 32)
+#endif
+
 constexpr int KG_E = 8, KG_H = 32;
 constexpr size_t SZ_E = (size_t)KG_E * 8 * 64 * 4;
 constexpr size_t SZ_H = (size_t)KG_H * 8 * 64 * 4;
 constexpr size_t TILE_FLOATS = 32 * 256;
+constexpr int LDS_ROW = 260;
 
-__host__ __device__ inline size_t packed_index(int n, int f) {
-  // neuron n, input feature f (0..255 or 0..63) -> position in a [kg][ob][lane][q] part
-  const int ob = n >> 5, i = n & 31, g = f >> 3, hh = (f >> 2) & 1, q = f & 3;
-  return (((size_t)g * 8 + ob) * 64 + (i + 32 * hh)) * 4 + q;
-}
 
 template <int KG, int NX>
 __device__ __forceinline__ void gemm_n_regs(f32x16 (&acc)[8], const float (&x)[NX], const float* __restrict__ wp,
@@ -49,12 +57,14 @@ __device__ __forceinline__ void gemm_n_regs(f32x16 (&acc)[8], const float (&x)[N
 #pragma unroll
       for (int ob = 0; ob < 8; ++ob) wb[ob] = w4[((kg + 1) * 8 + ob) * 64];
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int ob = 0; ob < 8; ++ob)
         acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[4 * kg + q], wa[ob][q], acc[ob], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
     if (kg + 1 < KG) {
 #pragma unroll
       for (int ob = 0; ob < 8; ++ob) wa[ob] = wb[ob];
@@ -62,60 +72,157 @@ __device__ __forceinline__ void gemm_n_regs(f32x16 (&acc)[8], const float (&x)[N
   }
 }
 
-template <int KG>
-__device__ __forceinline__ void gemm_n_mem(f32x16 (&acc)[8], const float* __restrict__ xt,
-                                           const float* __restrict__ wp, int lane) {
-  const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(wp) + lane;
-  const f32x4* __restrict__ x4 = reinterpret_cast<const f32x4*>(xt) + lane;
-  f32x4 wa[8];
-  f32x4 xa = x4[0];
+// Packed train-mode weights: the eval image's layout (off_w) with raw weights (no BatchNorm folding) in the
+// samples-on-rows operand order, feature(t, h) = 8*(t>>2) + 4*h + (t&3).
+__host__ __device__ constexpr size_t off_w(int layer, bool epart) {
+  return layer == 0 ? 0
+       : layer <= 3 ? SZ_E + (size_t)(layer - 1) * SZ_H
+       : layer == 4 ? (epart ? SZ_E + 3 * SZ_H : 2 * SZ_E + 3 * SZ_H)
+                    : 2 * SZ_E + (size_t)(layer - 1) * SZ_H;
+}
+constexpr size_t TRAIN_W_FLOATS = 2 * SZ_E + 7 * SZ_H;
+
+__global__ void k_pack_train(NofParamsDev P, float* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= TRAIN_W_FLOATS) return;
+  int layer;
+  bool epart;
+  size_t base;
+  if (idx < SZ_E) { layer = 0; epart = true; base = 0; }
+  else if (idx < SZ_E + 3 * SZ_H) { layer = 1 + (int)((idx - SZ_E) / SZ_H); epart = false; base = off_w(layer, false); }
+  else if (idx < 2 * SZ_E + 3 * SZ_H) { layer = 4; epart = true; base = off_w(4, true); }
+  else if (idx < 2 * SZ_E + 4 * SZ_H) { layer = 4; epart = false; base = off_w(4, false); }
+  else { layer = 5 + (int)((idx - (2 * SZ_E + 4 * SZ_H)) / SZ_H); epart = false; base = off_w(layer, false); }
+  const size_t j = idx - base;
+  const int q = (int)(j & 3), lane = (int)((j >> 2) & 63), ob = (int)((j >> 8) & 7), kg = (int)(j >> 11);
+  const int f = 8 * kg + 4 * (lane >> 5) + q, nn = 32 * ob + (lane & 31);
+  const int in_f = layer == 0 ? 63 : layer == 4 ? 319 : 256;
+  int col;
+  if (epart) col = f < 63 ? f : -1;
+  else col = (layer == 4 ? 63 : 0) + f;
+  out[idx] = col < 0 ? 0.0f : P.lin_w[layer][(size_t)nn * in_f + col];
+}
+
+struct BnPrev {  // the BatchNorm whose output a layer consumes
+  const float* gamma;
+  const float* beta;
+  float* rm;
+  float* rv;
+  const float* lin_bias;   // bias of the Linear that produced the statistics (the stats are of h - bias)
+  const double* stats;     // [256][2]: sum(h - bias), sum((h - bias)^2) over the chunk
+};
+
+// alpha/beta' of one BatchNorm for feature k = threadIdx.x (256 threads); block 0 updates the running stats.
+// ATen batch_norm_cpu_update_stats/transform: mean and biased var in float64, invstd = 1/sqrt(var+eps) stored as
+// float, alpha = invstd*gamma, beta' = beta - mean*alpha; running = momentum*x + (1-momentum)*running with the
+// unbiased variance.
+__device__ __forceinline__ void bn_coeffs(const BnPrev& B, int64_t n, float momentum, float eps, float* al,
+                                          float* be) {
+  const int k = threadIdx.x;
+  const double s1 = B.stats[2 * k], s2 = B.stats[2 * k + 1];
+  const double m = s1 / (double)n;
+  double var = s2 / (double)n - m * m;
+  if (var < 0.0) var = 0.0;
+  const double mean = (double)B.lin_bias[k] + m;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float a = invstd * B.gamma[k];
+  al[k] = a;
+  be[k] = B.beta[k] - (float)mean * a;
+  if (blockIdx.x == 0) {
+    const double mom = (double)momentum;
+    B.rm[k] = (float)(mom * mean + (1.0 - mom) * (double)B.rm[k]);
+    const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+    B.rv[k] = (float)(mom * unb + (1.0 - mom) * (double)B.rv[k]);
+  }
+}
+
+// 256-wide input streamed from HBM with the previous BatchNorm applied on load (x*alpha + beta').
+// Software pipeline (one wave per SIMD has no partner to hide latency, so every load is issued ahead):
+//   activations: ring of XD k-groups, weights: ring of WD k-groups, alpha/beta': one group ahead (LDS).
+// Both rings are carried across tiles -- their last loads of a tile fetch the first groups of the next tile
+// (the weights' addresses repeat), so a tile starts with its operands in flight.  KG_H % XD == KG_H % WD == 0
+// keeps the ring slot of group g equal to g % depth in every tile.  sched_barrier pins the loads where they
+// are issued (otherwise the scheduler sinks them next to their first use).
+constexpr int XD = PCN_XD;
+constexpr int WD = PCN_WD;
+static_assert(KG_H % XD == 0 && KG_H % WD == 0, "ring depths must divide the k-group count");
+
+struct HRing {
+  f32x4 x[XD];
+  f32x4 w[WD][8];
+  f32x4 a, b;  // alpha/beta' of the next group
+};
+
+__device__ __forceinline__ void ring_fill(HRing& R, const f32x4* __restrict__ x4, const f32x4* __restrict__ w4,
+                                          const float* __restrict__ al, const float* __restrict__ be, int h4) {
 #pragma unroll
-  for (int ob = 0; ob < 8; ++ob) wa[ob] = w4[ob * 64];
+  for (int d = 0; d < XD; ++d) R.x[d] = x4[d * 64];
 #pragma unroll
-  for (int kg = 0; kg < KG; ++kg) {
-    f32x4 wb[8];
-    f32x4 xb;
-    if (kg + 1 < KG) {
-      xb = x4[(kg + 1) * 64];
+  for (int d = 0; d < WD; ++d)
 #pragma unroll
-      for (int ob = 0; ob < 8; ++ob) wb[ob] = w4[((kg + 1) * 8 + ob) * 64];
-    }
+    for (int ob = 0; ob < 8; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
+  R.a = *reinterpret_cast<const f32x4*>(al + h4);
+  R.b = *reinterpret_cast<const f32x4*>(be + h4);
+}
+
+__device__ __forceinline__ void gemm_n_mem(f32x16 (&acc)[8], HRing& R, const f32x4* __restrict__ x4,
+                                           const f32x4* __restrict__ x4_next, const f32x4* __restrict__ w4,
+                                           const float* __restrict__ al, const float* __restrict__ be, int h4) {
+#pragma unroll
+  for (int kg = 0; kg < KG_H; ++kg) {
+    f32x4 xa;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xa[q] = R.x[kg % XD][q] * R.a[q] + R.b[q];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int ob = 0; ob < 8; ++ob)
-        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[q], wa[ob][q], acc[ob], 0, 0, 0);
+        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[q], R.w[kg % WD][ob][q], acc[ob], 0, 0, 0);
     }
-    if (kg + 1 < KG) {
-      xa = xb;
+    __builtin_amdgcn_sched_barrier(0);
+    const int gw = (kg + WD) % KG_H;  // group kg+WD of this tile, or the first groups of the next tile
 #pragma unroll
-      for (int ob = 0; ob < 8; ++ob) wa[ob] = wb[ob];
-    }
+    for (int ob = 0; ob < 8; ++ob) R.w[kg % WD][ob] = w4[(gw * 8 + ob) * 64];
+    R.x[kg % XD] = kg + XD < KG_H ? x4[(kg + XD) * 64] : x4_next[(kg + XD - KG_H) * 64];
+    const int ga = (kg + 1) % KG_H;
+    R.a = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
+    R.b = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-// One pre-BN Linear over a chunk [c0, c0 + n) of flattened samples.  EP: the encoding half (layer 1 and the
-// skip half of layer 5) computed from positions; HP: the 256 BN'd features read from `hin`.
+// One Linear over a chunk [c0, c0 + n) of flattened samples.  EP: the encoding half (layer 1, skip half of
+// layer 5) computed from positions (or read from `ein`); HP: the 256 BatchNorm'd features of the previous layer.
 template <bool EP, bool HP>
-__global__ __launch_bounds__(256, 2) void k_train_layer(const float* __restrict__ rays, int stride,
-                                                        const float* __restrict__ z, int S, int64_t c0, int64_t n,
-                                                        const float* __restrict__ ein, const float* __restrict__ hin, const float* __restrict__ Wp,
-                                                        const float* __restrict__ bias,
-                                                        const float* __restrict__ shift, float* __restrict__ hout,
-                                                        double* __restrict__ stats) {
+__global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_train_layer(
+    const float* __restrict__ rays, int stride, const float* __restrict__ z, int S, int64_t c0, int64_t n,
+    const float* __restrict__ ein, const float* __restrict__ hin, const float* __restrict__ Wp,
+    const float* __restrict__ bias, BnPrev prev, float momentum, float eps, float* __restrict__ hout,
+    double* __restrict__ stats) {
   __shared__ double st[512];
+  __shared__ __attribute__((aligned(16))) float al[256];
+  __shared__ __attribute__((aligned(16))) float be[256];
+  // per-wave output staging: 32 samples x 256 neurons, rows padded to 260 floats (conflict-free writes by
+  // neuron, conflict-free 16-byte reads by sample)
+  __shared__ __attribute__((aligned(16))) float stage[4][32 * LDS_ROW];
   for (int i = threadIdx.x; i < 512; i += blockDim.x) st[i] = 0.0;
+  if (HP) bn_coeffs(prev, n, momentum, eps, al, be);
   __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, wv = threadIdx.x >> 6;
-  const int64_t ntiles = (n + 31) / 32;
-  // activation tile offset of this lane's neuron column (see the [tile][g][lane][4] layout above)
   const int li = lane & 31;
-  const int lane_off = ((li >> 3) * 64 + 32 * ((li >> 2) & 1) + 4 * h) * 4 + (li & 3);
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wv; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
-    // opaque per-iteration copy of the weight pointer: without it the compiler hoists all 256 weight
-    // float4s of the layer out of the tile loop (loop-invariant) and spills them to scratch
-    const float* wpt = Wp;
-    asm volatile("" : "+s"(wpt));
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t tstride = (int64_t)gridDim.x * 4;
+  const int64_t tile0 = (int64_t)blockIdx.x * 4 + wv;
+  const f32x4* __restrict__ wh4 = reinterpret_cast<const f32x4*>(Wp + (EP ? SZ_E : 0)) + lane;
+  HRing ring;
+  if (HP && tile0 < ntiles)
+    ring_fill(ring, reinterpret_cast<const f32x4*>(hin + tile0 * TILE_FLOATS) + lane, wh4, al, be, 4 * h);
+  for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
+    // opaque per-iteration offset: keeps the compiler from hoisting all of the layer's weight loads out of the
+    // tile loop (an integer, not the pointer: a laundered pointer loses its global address space -> flat loads)
+    int wofs = 0;
+    asm volatile("" : "+s"(wofs));
+    const float* wpt = Wp + wofs;
     f32x16 acc[8];
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob)
@@ -136,22 +243,25 @@ __global__ __launch_bounds__(256, 2) void k_train_layer(const float* __restrict_
       }
       gemm_n_regs<KG_E>(acc, e, wpt, lane);
     }
-    if (HP) gemm_n_mem<KG_H>(acc, hin + tile * TILE_FLOATS, wpt + (EP ? SZ_E : 0), lane);
-    // epilogue: + bias, raw h to the next layer's tile layout, shifted statistics of the valid samples
-    float* ho = hout + tile * TILE_FLOATS + lane_off;
+    if (HP) {
+      const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
+      gemm_n_mem(acc, ring, reinterpret_cast<const f32x4*>(hin + tile * TILE_FLOATS) + lane,
+                 reinterpret_cast<const f32x4*>(hin + nxt * TILE_FLOATS) + lane, wh4 + wofs, al, be, 4 * h);
+    }
+    // epilogue: + bias -> LDS stage [sample][neuron]; statistics of (h - bias) over valid samples
+    float* lt = stage[wv];
     const int64_t base = tile * 32;
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) {
       const int nn = 32 * ob + li;
-      const float bo = bias[nn], so = shift[nn];
+      const float bo = bias[nn];
       float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int s = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float v = acc[ob][r] + bo;
-        ho[1024 * ob + 4 * ((r & 3) + 8 * (r >> 2))] = v;
+        const float d = acc[ob][r];
+        lt[s * LDS_ROW + nn] = d + bo;
         if (base + s < n) {
-          const float d = v - so;
           s1 += d;
           s2 += d * d;
         }
@@ -159,80 +269,30 @@ __global__ __launch_bounds__(256, 2) void k_train_layer(const float* __restrict_
       atomicAdd(&st[2 * nn], (double)s1);
       atomicAdd(&st[2 * nn + 1], (double)s2);
     }
+    // raw h to the next layer's [g][lane][4] tile: one 1 KiB dwordx4 store per wave-instruction
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f32x4* ho4 = reinterpret_cast<f32x4*>(hout + tile * TILE_FLOATS) + lane;
+    const float* lrow = lt + li * LDS_ROW + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 32; ++g) ho4[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 512; i += blockDim.x) atomicAdd(&stats[i], st[i]);
 }
 
-// BatchNorm L's statistics -> folded next layer (L < 7) or folded occ_out (L == 7).
-// grid: 256 blocks (one per neuron of layer L+1), or 1 block for L == 7; block: 256 threads (one per feature).
-__global__ __launch_bounds__(256) void k_bn_fold(NofParamsDev P, int L, const double* __restrict__ stats,
-                                                 const float* __restrict__ shift, int64_t n, float momentum,
-                                                 float* __restrict__ Wp, float* __restrict__ bias_next,
-                                                 float* __restrict__ shift_next) {
-  __shared__ double red[2][4];
-  const int k = threadIdx.x;
-  const double s1 = stats[2 * k], s2 = stats[2 * k + 1];
-  const double m = s1 / (double)n;
-  const double mean = (double)shift[k] + m;
-  double var = s2 / (double)n - m * m;
-  if (var < 0.0) var = 0.0;
-  // ATen batch_norm_cpu_update_stats: invstd = 1/sqrt(var + eps) in double, stored as float;
-  // transform: alpha = invstd * gamma, beta' = beta - mean * alpha (float)
-  const float invstd = (float)(1.0 / sqrt(var + (double)P.eps));
-  const float a = invstd * P.bn_w[L][k];
-  const float bp = P.bn_b[L][k] - (float)mean * a;
-  if (blockIdx.x == 0) {
-    const double mom = (double)momentum;
-    P.bn_rm[L][k] = (float)(mom * mean + (1.0 - mom) * (double)P.bn_rm[L][k]);
-    const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
-    P.bn_rv[L][k] = (float)(mom * unb + (1.0 - mom) * (double)P.bn_rv[L][k]);
-  }
-  const int lane = k & 63, wid = k >> 6;
-  if (L == 7) {
-    const float w = P.out_w[k];
-    Wp[k] = w * a;
-    double dp = wave_sum_d((double)w * (double)bp);
-    if (lane == 0) red[0][wid] = dp;
-    __syncthreads();
-    if (k == 0) bias_next[0] = (float)((double)P.out_b[0] + red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    return;
-  }
-  const int nxt = L + 1;
-  const int nn = blockIdx.x;
-  const int in_f = nxt == 4 ? 319 : 256;
-  const int hc0 = nxt == 4 ? 63 : 0;
-  const float* Wn = P.lin_w[nxt] + (size_t)nn * in_f;
-  const float w = Wn[hc0 + k];
-  Wp[(nxt == 4 ? SZ_E : 0) + packed_index(nn, k)] = w * a;
-  if (nxt == 4 && k < 64) Wp[packed_index(nn, k)] = k < 63 ? Wn[k] : 0.0f;
-  const double dp = wave_sum_d((double)w * (double)bp);
-  const double dc = wave_sum_d((double)w * (double)P.bn_b[L][k]);
-  if (lane == 0) {
-    red[0][wid] = dp;
-    red[1][wid] = dc;
-  }
+// occ_out on BatchNorm 8 (applied on load) + sigmoid; one wave per 32-sample tile.
+__global__ __launch_bounds__(256) void k_train_out(const float* __restrict__ hin, int64_t n, BnPrev prev,
+                                                   float momentum, float eps, const float* __restrict__ wout,
+                                                   const float* __restrict__ bout, float* __restrict__ p_out) {
+  __shared__ __attribute__((aligned(16))) float al[256];
+  __shared__ __attribute__((aligned(16))) float be[256];
+  bn_coeffs(prev, n, momentum, eps, al, be);
   __syncthreads();
-  if (k == 0) {
-    const double b = (double)P.lin_b[nxt][nn];
-    bias_next[nn] = (float)(b + red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    shift_next[nn] = (float)(b + red[1][0] + red[1][1] + red[1][2] + red[1][3]);
-  }
-}
-
-// Layer 1's raw weights in the train-mode operand order (encoding features, feature 63 = zero padding).
-__global__ void k_pack_train_first(const float* __restrict__ W1, float* __restrict__ Wp) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int)SZ_E) return;
-  const int q = idx & 3, lane = (idx >> 2) & 63, ob = (idx >> 8) & 7, kg = idx >> 11;
-  const int f = 8 * kg + 4 * (lane >> 5) + q, nn = 32 * ob + (lane & 31);
-  Wp[idx] = f < 63 ? W1[nn * 63 + f] : 0.0f;
-}
-
-// occ_out on the folded last BatchNorm + sigmoid; one wave per 32-sample tile.
-__global__ __launch_bounds__(256) void k_train_out(const float* __restrict__ hin, int64_t n,
-                                                   const float* __restrict__ wout, const float* __restrict__ bout,
-                                                   float* __restrict__ p_out) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t ntiles = (n + 31) / 32;
@@ -242,11 +302,12 @@ __global__ __launch_bounds__(256) void k_train_out(const float* __restrict__ hin
 #pragma unroll 8
   for (int g = 0; g < 32; ++g) {
     const f32x4 x = x4[g * 64];
-    const f32x4 w = *reinterpret_cast<const f32x4*>(wout + 8 * g + 4 * h);
-    part = fmaf(x[0], w[0], part);
-    part = fmaf(x[1], w[1], part);
-    part = fmaf(x[2], w[2], part);
-    part = fmaf(x[3], w[3], part);
+    const int f = 8 * g + 4 * h;
+    const f32x4 w = *reinterpret_cast<const f32x4*>(wout + f);
+    const f32x4 a = *reinterpret_cast<const f32x4*>(al + f);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(be + f);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) part = fmaf(x[q] * a[q] + b[q], w[q], part);
   }
   const float logit = part + __shfl_xor(part, 32, 64) + bout[0];
   const int64_t s = tile * 32 + (lane & 31);
@@ -256,12 +317,7 @@ __global__ __launch_bounds__(256) void k_train_out(const float* __restrict__ hin
 struct TrainWs {
   float* bufA;
   float* bufB;
-  float* wp1;
   float* wp;
-  float* bias;
-  float* shift[2];  // c_L and c_{L+1} ping-pong: k_bn_fold reads one and writes the other
-  float* wout;
-  float* bout;
   double* stats;
   size_t bytes;
 };
@@ -275,19 +331,12 @@ static TrainWs carve(void* base, int64_t chunk) {
     return o;
   };
   const size_t oA = take(tiles * TILE_FLOATS * 4), oB = take(tiles * TILE_FLOATS * 4);
-  const size_t o1 = take(SZ_E * 4), ow = take((SZ_E + SZ_H) * 4), ob = take(256 * 4), os = take(2 * 256 * 4);
-  const size_t owo = take(256 * 4), obo = take(16), ost = take(8 * 512 * 8);
+  const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
   char* b = (char*)base;
   TrainWs w;
   w.bufA = (float*)(b + oA);
   w.bufB = (float*)(b + oB);
-  w.wp1 = (float*)(b + o1);
   w.wp = (float*)(b + ow);
-  w.bias = (float*)(b + ob);
-  w.shift[0] = (float*)(b + os);
-  w.shift[1] = (float*)(b + os) + 256;
-  w.wout = (float*)(b + owo);
-  w.bout = (float*)(b + obo);
   w.stats = (double*)(b + ost);
   w.bytes = off;
   return w;
@@ -309,49 +358,47 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
   // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_pack_train_first, dim3((unsigned)((SZ_E + 255) / 256)), dim3(256), 0, s, P.lin_w[0], ws.wp1);
+  hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wp);
   for (int64_t c0 = 0; c0 < total; c0 += chunk) {
     const int64_t n = total - c0 < chunk ? total - c0 : chunk;
     const int64_t ntiles = (n + 31) / 32;
-    const unsigned grid = (unsigned)(ntiles / 4 + 1 < 512 ? ntiles / 4 + 1 : 512);
+    const unsigned maxg = 256u * PCN_TRAIN_WAVES;
+    const unsigned grid = (unsigned)(ntiles / 4 + 1 < maxg ? ntiles / 4 + 1 : maxg);
+    const double dn = (double)n;
     PCN_HIP(hipMemsetAsync(ws.stats, 0, 8 * 512 * sizeof(double), s));
     float* hin = ws.bufA;
     float* hout = ws.bufB;
-    // layer 1: encoding -> h1
-    const double dn = (double)n;
     {
+      const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
       hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
-                         c0, n, ein, (const float*)nullptr, ws.wp1, P.lin_b[0], P.lin_b[0], hin, ws.stats);
+                         c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps,
+                         hin, ws.stats);
     }
-    for (int L = 0; L < 7; ++L) {
-      const float* c_cur = L == 0 ? P.lin_b[0] : ws.shift[L & 1];
-      float* c_next = ws.shift[(L + 1) & 1];
-      {
-        ProfScope ps(s, PT_BN_FOLD, 0.0, 4.0 * 256 * 320);
-        hipLaunchKernelGGL(k_bn_fold, dim3(256), dim3(256), 0, s, P, L, ws.stats + 512 * L, c_cur, n, momentum,
-                           ws.wp, ws.bias, c_next);
-      }
-      if (L + 1 == 4) {
+    for (int L = 1; L < 8; ++L) {
+      const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], P.bn_rm[L - 1], P.bn_rv[L - 1], P.lin_b[L - 1],
+                        ws.stats + 512 * (L - 1)};
+      if (L == 4) {
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
         hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
-                           c0, n, ein, hin, ws.wp, ws.bias, c_next, hout, ws.stats + 512 * (L + 1));
+                           c0, n, ein, hin, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
+                           ws.stats + 512 * L);
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
         hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                           n_samples, c0, n, ein, hin, ws.wp, ws.bias, c_next, hout, ws.stats + 512 * (L + 1));
+                           n_samples, c0, n, ein, hin, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps,
+                           hout, ws.stats + 512 * L);
       }
       float* t = hin;
       hin = hout;
       hout = t;
     }
-    hipLaunchKernelGGL(k_bn_fold, dim3(1), dim3(256), 0, s, P, 7, ws.stats + 512 * 7, ws.shift[7 & 1], n, momentum,
-                       ws.wout, ws.bout, (float*)nullptr);
     {
+      const BnPrev prev{P.bn_w[7], P.bn_b[7], P.bn_rm[7], P.bn_rv[7], P.lin_b[7], ws.stats + 512 * 7};
       ProfScope ps(s, PT_TRAIN_OUT, 2.0 * 256 * dn, 1028.0 * dn);
-      hipLaunchKernelGGL(k_train_out, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, hin, n, ws.wout, ws.bout,
-                         p_out + c0);
+      hipLaunchKernelGGL(k_train_out, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, hin, n, prev, momentum,
+                         eps, P.out_w, P.out_b, p_out + c0);
     }
   }
   PCN_LAUNCH_CHECK("pcnerf_nof_query_train");

@@ -1,0 +1,76 @@
+"""A/B timing of kernel variant libraries (pc-nerf_amd/lib/variants/*.so) in ONE process, interleaved rounds
+(cdna_hip_programming.md 5.4 rule 24).  Times the train-mode query (all chunks) and the eval query on the same
+inputs; prints per-variant median kernel times per tag."""
+import ctypes
+import glob
+import json
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(HERE, "pc-nerf_amd"), HERE]
+from nof import _hip as H  # noqa: E402
+from nof import _ops, synthetic as syn  # noqa: E402
+from nof.networks import NOF_coarse  # noqa: E402
+
+TAGS = {0: "eval", 1: "hidden", 2: "first", 3: "skip", 4: "out", 5: "fold"}
+
+
+def load(path):
+    L = ctypes.CDLL(path)
+    for name, (res, args) in H._SIGS.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    return L
+
+
+def read(L, tag):
+    t, n, f, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+    L.pcnerf_prof_read(tag, ctypes.byref(t), ctypes.byref(n), ctypes.byref(f), ctypes.byref(b))
+    return t.value, n.value, f.value
+
+
+def main():
+    rays_n = int(os.environ.get("VB_RAYS", "16384"))
+    S = int(os.environ.get("VB_S", "384"))
+    libs = sorted(glob.glob(os.path.join(HERE, "pc-nerf_amd", "lib", "variants", "*.so")))
+    dev = torch.device("cuda")
+    rays = torch.from_numpy(syn.make_rays(rays_n, seed=0)).to(dev)
+    z = (torch.linspace(0, 1, S, device=dev)[None] * rays[:, 7:8]).contiguous()
+    m = syn.load_into(NOF_coarse(), syn.init_nof_params(1)).to(dev).train()
+    s, keep = _ops._params(m)
+    p = torch.empty_like(z)
+    Ls = {os.path.basename(l)[10:-3]: load(l) for l in libs}
+    ws = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_train_workspace_bytes(262144), dtype=torch.uint8, device=dev)
+    packed = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_eval_packed_floats(), device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    res = {k: {t: [] for t in TAGS} for k in Ls}
+    for rnd in range(4):
+        for name, L in Ls.items():
+            L.pcnerf_prof_enable(1)
+            rc = L.pcnerf_nof_query_train(rays.data_ptr(), rays_n, 15, z.data_ptr(), S, 262144, ctypes.byref(s),
+                                          0.1, 1e-5, ws.data_ptr(), ws.numel(), p.data_ptr(), st)
+            assert rc == 0, L.pcnerf_last_error()
+            m.eval()
+            L.pcnerf_nof_pack_eval(ctypes.byref(s), packed.data_ptr(), st)
+            L.pcnerf_nof_query_eval(rays.data_ptr(), rays_n, 15, z.data_ptr(), S, packed.data_ptr(), p.data_ptr(), st)
+            m.train()
+            torch.cuda.synchronize()
+            if rnd == 0:
+                continue  # warm-up round
+            for t in TAGS:
+                tm, n, f = read(L, t)
+                if n:
+                    res[name][t].append((tm / n * 1e3, f / (tm * 1e-3) / 1e12))
+            L.pcnerf_prof_enable(0)
+    out = {}
+    for name in Ls:
+        out[name] = {TAGS[t]: {"us": round(sorted(v)[len(v) // 2][0], 1), "TF": round(sorted(v)[len(v) // 2][1], 1)}
+                     for t, v in res[name].items() if v}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
