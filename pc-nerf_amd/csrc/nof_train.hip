@@ -165,9 +165,13 @@ __device__ __forceinline__ void ring_fill(HRing& R, const f32x4* __restrict__ x4
   R.b = *reinterpret_cast<const f32x4*>(be + h4);
 }
 
+// `prev_out` (nullable): the previous tile's output, staged in LDS rows `stage_row`, is written to HBM one
+// 1 KiB group per k-group (vmcnt retires in issue order: a burst of 32 stores at the end of a tile would hold
+// back the waits of the next tile's first loads until the whole burst is acknowledged).
 __device__ __forceinline__ void gemm_n_mem(f32x16 (&acc)[8], HRing& R, const f32x4* __restrict__ x4,
                                            const f32x4* __restrict__ x4_next, const f32x4* __restrict__ w4,
-                                           const float* __restrict__ al, const float* __restrict__ be, int h4) {
+                                           const float* __restrict__ al, const float* __restrict__ be, int h4,
+                                           f32x4* __restrict__ prev_out, const float* __restrict__ stage_row) {
 #pragma unroll
   for (int kg = 0; kg < KG_H; ++kg) {
     f32x4 xa;
@@ -187,6 +191,7 @@ __device__ __forceinline__ void gemm_n_mem(f32x16 (&acc)[8], HRing& R, const f32
     const int ga = (kg + 1) % KG_H;
     R.a = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
     R.b = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
+    if (prev_out) prev_out[kg * 64] = *reinterpret_cast<const f32x4*>(stage_row + 8 * kg);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -217,6 +222,7 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_train_layer(
   HRing ring;
   if (HP && tile0 < ntiles)
     ring_fill(ring, reinterpret_cast<const f32x4*>(hin + tile0 * TILE_FLOATS) + lane, wh4, al, be, 4 * h);
+  f32x4* prev_out = nullptr;  // previous tile's output, still staged in LDS
   for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
     // opaque per-iteration offset: keeps the compiler from hoisting all of the layer's weight loads out of the
     // tile loop (an integer, not the pointer: a laundered pointer loses its global address space -> flat loads)
@@ -243,13 +249,23 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_train_layer(
       }
       gemm_n_regs<KG_E>(acc, e, wpt, lane);
     }
+    float* lt = stage[wv];
+    const float* lrow = lt + li * LDS_ROW + 4 * h;
     if (HP) {
       const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
       gemm_n_mem(acc, ring, reinterpret_cast<const f32x4*>(hin + tile * TILE_FLOATS) + lane,
-                 reinterpret_cast<const f32x4*>(hin + nxt * TILE_FLOATS) + lane, wh4 + wofs, al, be, 4 * h);
+                 reinterpret_cast<const f32x4*>(hin + nxt * TILE_FLOATS) + lane, wh4 + wofs, al, be, 4 * h,
+                 prev_out, lrow);
+      prev_out = nullptr;
     }
+    if (prev_out) {  // EP-only layer: no k-group loop to hide the stores in
+#pragma unroll
+      for (int g = 0; g < 32; ++g) prev_out[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // epilogue: + bias -> LDS stage [sample][neuron]; statistics of (h - bias) over valid samples
-    float* lt = stage[wv];
     const int64_t base = tile * 32;
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) {
@@ -269,17 +285,17 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_train_layer(
       atomicAdd(&st[2 * nn], (double)s1);
       atomicAdd(&st[2 * nn + 1], (double)s2);
     }
-    // raw h to the next layer's [g][lane][4] tile: one 1 KiB dwordx4 store per wave-instruction
+    // the raw h of this tile goes to the next layer's [g][lane][4] layout (1 KiB dwordx4 stores) during the
+    // next tile's k-group loop, or below after the last tile
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    f32x4* ho4 = reinterpret_cast<f32x4*>(hout + tile * TILE_FLOATS) + lane;
-    const float* lrow = lt + li * LDS_ROW + 4 * h;
+    prev_out = reinterpret_cast<f32x4*>(hout + tile * TILE_FLOATS) + lane;
+  }
+  if (prev_out) {
+    const float* lrow = stage[wv] + li * LDS_ROW + 4 * h;
 #pragma unroll
-    for (int g = 0; g < 32; ++g) ho4[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int g = 0; g < 32; ++g) prev_out[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 512; i += blockDim.x) atomicAdd(&stats[i], st[i]);
