@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--mode", choices=["train_fwd", "val"], default="train_fwd")
     ap.add_argument("--cpu-rays", type=int, default=1024, help="bounded CPU-baseline sample (rays)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="gather every rank's depth_fine to rank 0 inside each step (eval-driver output path)")
     return ap.parse_args()
 
 
@@ -80,15 +82,17 @@ def main():
     dev = torch.device("cuda", local)
 
     from nof import _hip, synthetic as syn
+    from nof.blocks import blocks_of_rank, gather_rows, max_over_ranks
     from nof.criteria import nof_loss
     from nof.networks import Embedding, NOF_coarse, NOF_fine
     from nof.render import render_rays_train, render_rays_val
 
-    # this rank's parent block: its own child layout, rays and weights
-    rays = torch.from_numpy(syn.make_rays(a.rays, n_children=32, seed=1000 * rank)).to(dev)
+    # this rank's parent block (one per GPU): its own child layout, rays and coarse/fine weights
+    (block,) = blocks_of_rank(rank, world, world)
+    rays = torch.from_numpy(syn.make_rays(a.rays, n_children=32, seed=1000 * block)).to(dev)
     train = a.mode == "train_fwd"
-    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234 + rank)).to(dev).train(train)
-    mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678 + rank)).to(dev).train(train)
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234 + block)).to(dev).train(train)
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678 + block)).to(dev).train(train)
     emb = Embedding(3, 10)
     loss_fn = nof_loss["smoothl1"]()
     gt = rays[:, 14].contiguous()
@@ -101,11 +105,15 @@ def main():
                                     use_child_nerf_loss=1)
             lr = 1e-1 * loss_fn(1e1 * res["depth"], 1e1 * gt)           # train_kitti.py:145-146
             lrf = 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
-            return (lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"]
+            loss = (lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"]
                     + 1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"])
-        res = render_rays_val(mc, mf, emb, rays, N_samples=a.samples, N_importance=a.importance, perturb=0,
-                              noise_std=0, chunk=a.chunk)
-        return 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
+        else:
+            res = render_rays_val(mc, mf, emb, rays, N_samples=a.samples, N_importance=a.importance, perturb=0,
+                                  noise_std=0, chunk=a.chunk)
+            loss = 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
+        if a.gather:
+            gather_rows(res["depth_fine"][:, None], dst=0)
+        return loss
 
     L = _hip.lib()
     with torch.no_grad():
@@ -126,10 +134,7 @@ def main():
         loss_val = float(loss)
     if not np.isfinite(loss_val):
         raise RuntimeError(f"non-finite loss {loss_val}")
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist:
-        tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
-    elapsed = float(el)
+    elapsed = max_over_ranks(elapsed, device=dev)
 
     # dominant kernel: the 256 -> 256 pre-BN Linear of train mode (6 of 9 GEMMs per chunk), or the fused eval query
     tag = 1 if train else 0
@@ -177,7 +182,7 @@ def main():
                    "mlp_samples_per_ray": a.samples + a.samples + a.importance, "chunk": a.chunk,
                    "batchnorm": "train (batch stats per chunk)" if train else "eval (folded)",
                    "segmented_ratio": 0.1 if train else None, "perturb": 1 if train else 0,
-                   "parallelism": f"blocks{world}"},
+                   "parallelism": f"blocks{world}", "gather": bool(a.gather)},
         "roofline": {"kernel": kname, "bound": "mfma", "achieved": round(achieved, 2),
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                      "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 2),
