@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--importance", type=int, default=256)
     ap.add_argument("--chunk", type=int, default=262144)
     ap.add_argument("--mode", choices=["train_fwd", "val"], default="train_fwd")
-    ap.add_argument("--cpu-rays", type=int, default=1024, help="bounded CPU-baseline sample (rays)")
+    ap.add_argument("--cpu-rays", type=int, default=4096, help="bounded CPU-baseline sample (rays)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="gather every rank's depth_fine to rank 0 inside each step (eval-driver output path)")
