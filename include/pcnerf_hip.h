@@ -120,6 +120,23 @@ int pcnerf_child_loss_reduce(const float* free_ray, const float* sl1_ray, int64_
 int pcnerf_pointwise_loss(const float* pred, const float* target, const uint8_t* mask, int64_t n, int kind,
                           float* out, void* stream);
 
+/* ---------------------------------------------------------------- two-step inference (render_rays_view_0525_2_2)
+ * Per row (render.py:241-354 after the query): weights = composite(p) normalised with eps, the strict child
+ * mask [rows[child_near_col], rows[child_far_col]] expanded from 0.01 by 0.01, the argmax of the weights
+ * smoothed by `gauss` (2*radius+1 float64 taps = scipy gaussian_filter(sigma=5), reflect), at_peak = mask at
+ * that argmax, child_sum = sum(w * mask), depth (method 2: child re-normalised, else sum(w z)), the per-row
+ * opacity sum and points = o + depth * d (points may be NULL, weights may be NULL). */
+int pcnerf_view_rows(const float* p, const float* z, int64_t n_rows, int n_samples, const float* rows, int row_stride,
+                     int child_near_col, int child_far_col, int method, float eps, const double* gauss, int radius,
+                     float* weights, float* depth, uint8_t* at_peak, float* child_sum, double* opac_row,
+                     float* points, void* stream);
+/* Ray-group walk (render.py:317-340) over other_interest_sub_nerf_number (int64, k-1 on a group's first row):
+ * flags[r] = 1 for the effective row of every group; *opacity = mean opacity term over n_rows * n_samples. */
+size_t pcnerf_view_walk_workspace_bytes(int64_t n_rows);
+int pcnerf_view_walk(const int64_t* other, int64_t n_rows, const uint8_t* at_peak, const float* child_sum,
+                     const double* opac_row, int n_samples, void* workspace, uint8_t* flags, float* opacity,
+                     void* stream);
+
 /* ---------------------------------------------------------------- kernel timing (bench / profiling)
  * pcnerf_prof_enable(1) makes every subsequent launch record a HIP event pair on its stream; tags:
  * 0 eval query, 1 train hidden Linear, 2 train first Linear, 3 train skip Linear, 4 train occ_out,

@@ -49,6 +49,10 @@ _SIGS = {
     "pcnerf_child_loss_reduce": (c_int, [vp, vp, i64, vp, c_int, c_int, vp, vp, vp]),
     "pcnerf_pointwise_loss": (c_int, [vp, vp, vp, i64, c_int, vp, vp]),
     "pcnerf_embed": (c_int, [vp, i64, vp, vp]),
+    "pcnerf_view_rows": (c_int, [vp, vp, i64, c_int, vp, c_int, c_int, c_int, c_int, c_float, vp, c_int, vp, vp, vp,
+                                 vp, vp, vp, vp]),
+    "pcnerf_view_walk_workspace_bytes": (c_size, [i64]),
+    "pcnerf_view_walk": (c_int, [vp, i64, vp, vp, vp, c_int, vp, vp, vp, vp]),
     "pcnerf_prof_enable": (c_int, [c_int]),
     "pcnerf_prof_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),

@@ -227,6 +227,57 @@ def child_losses(free_ray, sl1_ray, rays, divide: bool, sub_nerf_test_num: int):
     return out[0], out[1]
 
 
+_GAUSS = {}
+
+
+def _gauss_taps(device, sigma=5.0, truncate=4.0):
+    """scipy.ndimage.gaussian_filter's kernel (render.py:306, sigma 5): radius int(truncate*sigma + 0.5),
+    exp(-0.5 x^2 / sigma^2) normalised by its float64 sum -- a 41-entry host-side constant table."""
+    key = (device.type, device.index, sigma, truncate)
+    if key not in _GAUSS:
+        import numpy as np
+        radius = int(truncate * float(sigma) + 0.5)
+        x = np.arange(-radius, radius + 1)
+        phi = np.exp(-0.5 / (sigma * sigma) * x ** 2)
+        phi = phi / phi.sum()
+        _GAUSS[key] = (torch.from_numpy(phi[::-1].copy()).to(device), radius)
+    return _GAUSS[key]
+
+
+def view_rows(p, z, rows, method: int, eps: float, want_points=True):
+    """-> weights (R,S), depth (R,), at_peak (R,) uint8, child_sum (R,), opac_row (R,) float64, points (R,3)."""
+    R, S = z.shape
+    dev = z.device
+    g, radius = _gauss_taps(dev)
+    w = torch.empty((R, S), dtype=torch.float32, device=dev)
+    depth = torch.empty((R,), dtype=torch.float32, device=dev)
+    at_peak = torch.empty((R,), dtype=torch.uint8, device=dev)
+    csum = torch.empty((R,), dtype=torch.float32, device=dev)
+    opac = torch.empty((R,), dtype=torch.float64, device=dev)
+    pts = torch.empty((R, 3), dtype=torch.float32, device=dev) if want_points else None
+    H.check(H.lib().pcnerf_view_rows(p.data_ptr(), z.data_ptr(), R, S, rows.data_ptr(), rows.shape[1], 6, 7,
+                                     int(method), float(eps), g.data_ptr(), radius, w.data_ptr(), depth.data_ptr(),
+                                     at_peak.data_ptr(), csum.data_ptr(), opac.data_ptr(), H.ptr(pts), _stream(z)))
+    return w, depth, at_peak, csum, opac, pts
+
+
+def view_walk(other, at_peak, child_sum, opac_row, n_samples: int):
+    """-> flags (R, 1) bool, opacity () float32."""
+    L = H.lib()
+    R = at_peak.shape[0]
+    H.require_device(other)
+    other = other.to(torch.int64).contiguous()
+    if other.numel() != R:
+        raise RuntimeError(f"other_interest_sub_nerf_number has {other.numel()} entries for {R} rows")
+    flags = torch.empty((R, 1), dtype=torch.bool, device=at_peak.device)
+    opacity = torch.empty((), dtype=torch.float32, device=at_peak.device)
+    ws = _workspace(at_peak.device, L.pcnerf_view_walk_workspace_bytes(R))
+    H.check(L.pcnerf_view_walk(other.data_ptr(), R, at_peak.data_ptr(), child_sum.data_ptr(), opac_row.data_ptr(),
+                               int(n_samples), ws.data_ptr(), flags.data_ptr(), opacity.data_ptr(),
+                               _stream(at_peak)))
+    return flags, opacity
+
+
 _KIND = {"mse": 0, "l1": 1, "smoothl1": 2}
 
 

@@ -123,3 +123,38 @@ def render_rays_val(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: 
     _, depth_f, _, _ = _ops.composite(pf, zf, _noise(rng, "noise_fine", zf, noise_std), noise_std, EPSILON,
                                       want_weights=False)
     return {"depth_fine": depth_f, 'depth': depth}
+
+
+def _inference_view(model, rays, z, other, chunk, method):
+    """inference_0525_2 (render.py:229-368) on the HIP kernels: query, per-row compositing / peak / child sums,
+    then the ray-group walk."""
+    p = _ops.query(model, rays, z, chunk)
+    w, depth, at_peak, csum, opac_row, pts = _ops.view_rows(p, z, rays, method, EPSILON)
+    flags, opacity = _ops.view_walk(other, at_peak, csum, opac_row, z.shape[1])
+    return depth, w, opacity, flags, pts
+
+
+def render_rays_view_0525_2_2(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: torch.Tensor,
+                              other_interest_sub_nerf_number: torch.Tensor, N_samples=64, N_importance=128,
+                              use_disp=False, perturb=0, noise_std=1, chunk=1024 * 3, isval=False,
+                              depth_inference_method=0, *, rng=None):
+    """render.py:614-699: two-step inference on 13-column rows grouped per ray.  Returns {'depth_fine', 'weights',
+    'opacity', 'z_vals', 'depth', 'opacity_fine', 'points_inference_fine', 'points_inference',
+    'rays_effective_flag', 'rays_effective_flag_fine'} (the reference's debug prints are not reproduced)."""
+    rays = _check_inputs(model, model_fine, embedding_xy, rays, 11)
+    other = other_interest_sub_nerf_number
+    if not torch.is_tensor(other):
+        other = torch.as_tensor(other)
+    other = other.to(rays.device)
+    R = rays.shape[0]
+    z = _ops.sample_coarse(rays, N_samples, N_samples, 9, 10)          # parent bounds, render.py:622-628
+    if perturb > 0:
+        z = _ops.perturb(z, perturb, _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
+    method = int(depth_inference_method)
+    depth, w, opacity, flags, pts = _inference_view(model, rays, z, other, chunk, method)
+    u = None if perturb == 0 else _draw(rng, "u", (R, N_importance), rays.device, torch.rand)
+    zf = _ops.resample(z, w, N_importance, u)
+    depth_f, wf, opacity_f, flags_f, pts_f = _inference_view(model_fine, rays, zf, other, chunk, method)
+    return {'depth_fine': depth_f, 'weights': wf, 'opacity': opacity, 'z_vals': zf, "depth": depth,
+            "opacity_fine": opacity_f, "points_inference_fine": pts_f, "points_inference": pts,
+            "rays_effective_flag": flags, "rays_effective_flag_fine": flags_f}

@@ -152,6 +152,44 @@ def test_render_train(name):
     close(running(mf), g["running_f"], RTOL, 1e-6, "running fine")
 
 
+@pytest.mark.parametrize("method", [0, 2])
+def test_render_view(method):
+    g = golden(f"render_view_m{method}")
+    emb, mc, mf = models(False)
+    with torch.no_grad():
+        res = R.render_rays_view_0525_2_2(mc, mf, emb, torch.from_numpy(g["rows"]).to(DEV),
+                                          torch.from_numpy(g["other"]).to(DEV), N_samples=int(g["N_samples"]),
+                                          N_importance=int(g["N_importance"]), perturb=0, noise_std=0, chunk=4096,
+                                          depth_inference_method=method)
+    assert set(res) == {"depth_fine", "weights", "opacity", "z_vals", "depth", "opacity_fine",
+                        "points_inference_fine", "points_inference", "rays_effective_flag",
+                        "rays_effective_flag_fine"}
+    for k in ("depth", "depth_fine", "points_inference", "points_inference_fine", "opacity", "opacity_fine"):
+        close(res[k], g[k], RTOL, 1e-6, k)
+    close(res["z_vals"], g["z_vals"], RTOL, 1e-5, "z_vals")
+    close(res["weights"], g["weights"], 1e-3, 1e-7, "weights")
+    for k in ("rays_effective_flag", "rays_effective_flag_fine"):
+        got = res[k].cpu().numpy()
+        assert got.dtype == np.bool_ and got.shape == g[k].shape
+        assert np.array_equal(got, g[k]), k
+
+
+def test_view_walk_fallback_matches_parallel():
+    """Malformed group lists take the literal sequential walk; well-formed ones the parallel path."""
+    from nof import _ops
+    R = 12
+    at_peak = torch.tensor([0, 0, 1, 0, 0, 0, 1, 0, 0, 0, 0, 0], dtype=torch.uint8, device=DEV)
+    csum = torch.arange(R, dtype=torch.float32, device=DEV).flip(0)
+    op = torch.ones(R, dtype=torch.float64, device=DEV)
+    good = torch.tensor([2, 0, 0, 0, 3, 0, 0, 0, 1, 0, 0, 0], device=DEV)
+    flags, opac = _ops.view_walk(good, at_peak, csum, op, 4)
+    assert flags[:, 0].nonzero().flatten().tolist() == [2, 3, 6, 8, 10, 11]
+    assert abs(float(opac) - 0.25) < 1e-7
+    bad = torch.tensor([2, 1, 0, 0, 3, 0, -1, 0, 0, 0, 0, 0], device=DEV)   # nested head + negative inner row
+    flags, _ = _ops.view_walk(bad, at_peak, csum, op, 4)
+    assert flags[:, 0].nonzero().flatten().tolist() == [2, 3, 6, 8, 9, 10, 11]
+
+
 def test_render_train_vs_oracle_config2_subset():
     """Config-2 rays at S=128/I=256 with several BatchNorm chunks, against the CPU oracle."""
     rays = syn.make_rays(192, seed=3)
