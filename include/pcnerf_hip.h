@@ -77,9 +77,10 @@ int pcnerf_nof_forward_train(const float* emb, int64_t n, const pcnerf_nof_param
 /* ---------------------------------------------------------------- sampling (render.py:429-454, :497-511)
  * z[ray, :] = linspace sampling of [rays[near_col], rays[far_col]] with n_samples points; if
  * n_parent < n_samples the segmented scheme is used: n_parent points over [near, far] and
- * n_samples - n_parent over [rays[child_near_col], rays[child_far_col]], merged by sort. */
+ * n_samples - n_parent over [rays[child_near_col], rays[child_far_col]], merged by sort.  disparity != 0:
+ * linear in inverse depth, z = 1/(1/near*(1-s) + 1/far*s) (render.py:565-567, use_disp). */
 int pcnerf_sample_coarse(const float* rays, int64_t n_rays, int ray_stride, int near_col, int far_col,
-                         int child_near_col, int child_far_col, int n_samples, int n_parent, float* z,
+                         int child_near_col, int child_far_col, int n_samples, int n_parent, int disparity, float* z,
                          void* stream);
 /* Stratified perturbation z' = lower + (upper - lower) * (perturb * rand) (render.py:449-454). */
 int pcnerf_perturb(const float* z, int64_t n_rays, int n_samples, float perturb, const float* rand, float* z_out,
@@ -93,7 +94,11 @@ int pcnerf_perturb(const float* z, int64_t n_rays, int n_samples, float perturb,
 int pcnerf_composite(const float* p, const float* z, int64_t n_rays, int n_samples, const float* noise,
                      float noise_std, float eps, const float* rays, int ray_stride, int child_near_col,
                      int child_far_col, int range_col, float* weights, float* depth, float* free_ray,
-                     float* sl1_ray, void* stream);
+                     float* sl1_ray, double* opac_row, float* depth2, void* stream);
+/* (opac_row, nullable: per-ray sum of log(0.1+p)+log(1.1-p)+2.20727, render.py:224; depth2, nullable: z at the
+ * rank of the last sample in the descending weight order, render.py:598-600.) */
+/* mean = sum(x[0:n]) / denom, one float written to out (used for the opacity means). */
+int pcnerf_mean_f64(const double* x, int64_t n, double denom, float* out, void* stream);
 
 /* ---------------------------------------------------------------- importance resampling
  * z_fine[ray, :] = sort(cat(z, sample_pdf(mid(z), weights[:, 1:-1], n_importance, det = (u == NULL))))

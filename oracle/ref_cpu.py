@@ -293,6 +293,36 @@ def inference_view(p, z, other, near_far_child, method, eps=1e-10):
     return depth, w, opacity, flag
 
 
+def render_rays(Pc, Pf, rays, N_samples=64, N_importance=128, use_disp=False, perturb=0, noise_std=1, chunk=3072,
+                isval=False, draws=None):
+    """render.py:538-611 with inference (:166-226).  The call at render.py:585/596 passes ``isval`` positionally
+    into inference's ``epsilon`` slot, so weights are always normalised, by sum + float(isval), and inference's
+    own ``isval`` stays False.  depth2 = z at the position where sample F-1 appears in the descending argsort of
+    the fine weights (render.py:598-600)."""
+    draws = draws or {}
+    near, far = rays[:, 6:7], rays[:, 7:8]
+    s = torch.linspace(0, 1, N_samples).expand(rays.shape[0], N_samples)
+    z = 1 / (1 / near * (1 - s) + 1 / far * s) if use_disp else near * (1 - s) + far * s
+    if perturb > 0:
+        z = perturb_z(z, perturb, draws["perturb_rand"] if "perturb_rand" in draws else torch.rand(z.shape))
+    eps = float(isval)
+
+    def inf(P, z, noise):
+        p = query(P, points(rays, z), False, chunk)
+        w, depth = composite(p, z, eps, None if noise_std == 0 else noise * noise_std)
+        opac = torch.mean(torch.log(0.1 + p) + torch.log(0.1 + (1 - p)) + 2.20727)
+        return depth, w, opac
+
+    depth, w, opac = inf(Pc, z, draws.get("noise"))
+    zmid = .5 * (z[..., 1:] + z[..., :-1])
+    zs = sample_pdf(zmid, w[..., 1:-1], N_importance, det=(perturb == 0.), u=draws.get("u"))
+    zf = torch.sort(torch.cat([z, zs], -1), -1)[0]
+    depth_f, wf, opac_f = inf(Pf, zf, draws.get("noise_fine"))
+    mask = wf.argsort(dim=-1, descending=True).eq(wf.shape[1] - 1)
+    return {"depth_fine": depth_f, "weights": wf, "opacity": opac, "z_vals": zf, "depth": depth,
+            "depth2": zf[mask], "opacity_fine": opac_f}
+
+
 def render_rays_view(Pc, Pf, rows, other, N_samples=64, N_importance=128, chunk=3072, method=0):
     """render.py:614-699: parent bounds from cols 9/10, child bounds cols 6:8, coarse + fine inference_view,
     points o + depth*d."""

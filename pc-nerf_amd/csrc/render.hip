@@ -43,13 +43,23 @@ __device__ __forceinline__ float seg_value(int a, int sp, int sc, float near, fl
 
 __global__ __launch_bounds__(256) void k_sample_coarse(const float* __restrict__ rays, int64_t n_rays, int stride,
                                                        int near_col, int far_col, int cn_col, int cf_col, int S,
-                                                       int sp, float* __restrict__ z) {
+                                                       int sp, int disparity, float* __restrict__ z) {
   const int lane = threadIdx.x & 63;
   const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (ray >= n_rays) return;
   const float* r = rays + ray * stride;
   const float near = r[near_col], far = r[far_col];
   float* zr = z + ray * S;
+  if (disparity) {  // render.py:565-567: z = 1 / (1/near*(1-s) + 1/far*s)
+    const float in = 1.0f / near, inf_ = 1.0f / far;
+    for (int i = lane; i < S; i += 64) {
+      const float sv = linspace01(i, S);
+      const float a = in * (1.0f - sv);
+      const float b = inf_ * sv;
+      zr[i] = 1.0f / (a + b);
+    }
+    return;
+  }
   if (sp >= S) {
     for (int i = lane; i < S; i += 64) zr[i] = lerp_z(near, far, linspace01(i, S));
     return;
@@ -131,6 +141,7 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
                                                    int stride, int cn_col, int cf_col, int rg_col,
                                                    float* __restrict__ Wout, float* __restrict__ depth,
                                                    float* __restrict__ free_ray, float* __restrict__ sl1_ray,
+                                                   double* __restrict__ opac_row, float* __restrict__ depth2,
                                                    int* __restrict__ err) {
   const int lane = threadIdx.x & 63;
   const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -185,6 +196,29 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
       if (j < nb) wr[j] = wv[j];
   }
   if (lane == 0) depth[ray] = d;
+  if (opac_row) {  // render.py:224: log(0.1 + p) + log(0.1 + (1 - p)) + 2.20727, summed per ray
+    double op = 0.0;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j)
+      if (j < nb) op += (double)((logf(0.1f + pv[j]) + logf(0.1f + (1.0f - pv[j]))) + 2.20727f);
+    op = wave_sum_d(op);
+    if (lane == 0) opac_row[ray] = op;
+  }
+  if (depth2) {  // render.py:598-600: z at the rank of sample S-1 in the (stable) descending weight order
+    const int last_lane = (S - 1) / B, last_j = (S - 1) % B;
+    float wl = 0.0f;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j)
+      if (j == last_j) wl = wv[j];
+    wl = __shfl(wl, last_lane, 64);
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j)
+      if (j < nb) cnt += (wv[j] > wl) || (wv[j] == wl && i0 + j < S - 1);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if (lane == 0) depth2[ray] = Z[ray * S + cnt];
+  }
   if (!rays) return;
 
   // child masks and loss terms (render.py:75-159)
@@ -411,6 +445,14 @@ __global__ void k_child_loss_divide(const double* __restrict__ acc, int N, float
   }
 }
 
+__global__ void k_sum_f64(const double* __restrict__ x, int64_t n, double denom, float* __restrict__ out) {
+  __shared__ double sh[16];
+  double a = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) a += x[i];
+  a = block_sum_d(a, sh);
+  if (threadIdx.x == 0) out[0] = (float)(a / denom);
+}
+
 __global__ void k_pointwise_loss(const float* __restrict__ a, const float* __restrict__ b,
                                  const uint8_t* __restrict__ m, int64_t n, int kind, float* __restrict__ out) {
   __shared__ double sh[16];
@@ -440,8 +482,8 @@ extern "C" const char* pcnerf_last_error(void) { return g_last_error.c_str(); }
 static inline unsigned nblk(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
 extern "C" int pcnerf_sample_coarse(const float* rays, int64_t n_rays, int ray_stride, int near_col, int far_col,
-                                    int child_near_col, int child_far_col, int n_samples, int n_parent, float* z,
-                                    void* stream) {
+                                    int child_near_col, int child_far_col, int n_samples, int n_parent,
+                                    int disparity, float* z, void* stream) {
   PCN_API_BEGIN
   PCN_CHECK(rays && z, "pcnerf_sample_coarse: null argument");
   PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_sample_coarse: empty input");
@@ -451,7 +493,8 @@ extern "C" int pcnerf_sample_coarse(const float* rays, int64_t n_rays, int ray_s
             "pcnerf_sample_coarse: column outside ray row");
   ProfScope ps((hipStream_t)stream, PT_SAMPLE, 0.0, (double)n_rays * (4.0 * ray_stride + 4.0 * n_samples));
   hipLaunchKernelGGL(k_sample_coarse, dim3(nblk(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, rays, n_rays,
-                     ray_stride, near_col, far_col, child_near_col, child_far_col, n_samples, n_parent, z);
+                     ray_stride, near_col, far_col, child_near_col, child_far_col, n_samples, n_parent, disparity,
+                     z);
   PCN_LAUNCH_CHECK("pcnerf_sample_coarse");
   PCN_API_END
 }
@@ -471,7 +514,7 @@ extern "C" int pcnerf_perturb(const float* z, int64_t n_rays, int n_samples, flo
 extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, int n_samples, const float* noise,
                                 float noise_std, float eps, const float* rays, int ray_stride, int child_near_col,
                                 int child_far_col, int range_col, float* weights, float* depth, float* free_ray,
-                                float* sl1_ray, void* stream) {
+                                float* sl1_ray, double* opac_row, float* depth2, void* stream) {
   PCN_API_BEGIN
   PCN_CHECK(p && z && depth, "pcnerf_composite: null argument");
   PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_composite: empty input");
@@ -488,7 +531,7 @@ extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, 
 #define PCN_COMP(MB)                                                                                          \
   hipLaunchKernelGGL(k_composite<MB>, g, b, 0, s, p, z, n_rays, n_samples, noise, noise_std, eps, rays,      \
                      ray_stride, child_near_col, child_far_col, range_col, weights, depth, free_ray, sl1_ray, \
-                     (int*)nullptr)
+                     opac_row, depth2, (int*)nullptr)
   if (B <= 2) PCN_COMP(2);
   else if (B <= 6) PCN_COMP(6);
   else if (B <= 16) PCN_COMP(16);
@@ -560,6 +603,14 @@ extern "C" int pcnerf_child_loss_reduce(const float* free_ray, const float* sl1_
                        out);
   }
   PCN_LAUNCH_CHECK("pcnerf_child_loss_reduce");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_mean_f64(const double* x, int64_t n, double denom, float* out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(x && out && n > 0, "pcnerf_mean_f64: bad argument");
+  hipLaunchKernelGGL(k_sum_f64, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, n, denom, out);
+  PCN_LAUNCH_CHECK("pcnerf_mean_f64");
   PCN_API_END
 }
 

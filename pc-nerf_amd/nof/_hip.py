@@ -39,10 +39,11 @@ _SIGS = {
     "pcnerf_nof_train_workspace_bytes": (c_size, [i64]),
     "pcnerf_nof_query_train": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams), c_float, c_float,
                                        vp, c_size, vp, vp]),
-    "pcnerf_sample_coarse": (c_int, [vp, i64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, vp, vp]),
+    "pcnerf_sample_coarse": (c_int, [vp, i64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, vp, vp]),
     "pcnerf_perturb": (c_int, [vp, i64, c_int, c_float, vp, vp, vp]),
     "pcnerf_composite": (c_int, [vp, vp, i64, c_int, vp, c_float, c_float, vp, c_int, c_int, c_int, c_int, vp, vp,
-                                 vp, vp, vp]),
+                                 vp, vp, vp, vp, vp]),
+    "pcnerf_mean_f64": (c_int, [vp, i64, ctypes.c_double, vp, vp]),
     "pcnerf_resample": (c_int, [vp, vp, i64, c_int, c_int, vp, vp, vp]),
     "pcnerf_sample_pdf": (c_int, [vp, vp, i64, c_int, c_int, vp, vp, vp]),
     "pcnerf_child_loss_workspace_bytes": (c_size, [c_int]),

@@ -145,11 +145,11 @@ def embed(x: torch.Tensor) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------------------------- render stages
-def sample_coarse(rays, n_samples, n_parent, near_col, far_col, cn_col=0, cf_col=0) -> torch.Tensor:
+def sample_coarse(rays, n_samples, n_parent, near_col, far_col, cn_col=0, cf_col=0, disparity=False) -> torch.Tensor:
     R = rays.shape[0]
     z = torch.empty((R, n_samples), dtype=torch.float32, device=rays.device)
     H.check(H.lib().pcnerf_sample_coarse(rays.data_ptr(), R, rays.shape[1], near_col, far_col, cn_col, cf_col,
-                                         n_samples, n_parent, z.data_ptr(), _stream(rays)))
+                                         n_samples, n_parent, int(bool(disparity)), z.data_ptr(), _stream(rays)))
     return z
 
 
@@ -164,8 +164,9 @@ def perturb(z, amount: float, rand: torch.Tensor) -> torch.Tensor:
 
 
 def composite(p, z, noise=None, noise_std=0.0, eps=1e-10, rays=None, cn_col=10, cf_col=11, range_col=14,
-              want_weights=True):
-    """-> (weights or None, depth (R,), free_ray (R,) or None, sl1_ray (R,) or None)."""
+              want_weights=True, extras=False):
+    """-> (weights or None, depth (R,), free_ray (R,) or None, sl1_ray (R,) or None)
+    [+ (opacity mean (), depth2 (R,)) when ``extras``]."""
     R, S = z.shape
     dev = z.device
     w = torch.empty((R, S), dtype=torch.float32, device=dev) if want_weights else None
@@ -178,10 +179,19 @@ def composite(p, z, noise=None, noise_std=0.0, eps=1e-10, rays=None, cn_col=10, 
         noise = _f32(noise)
         if noise.shape != z.shape:
             raise RuntimeError("noise draws must have the shape of the samples")
+    opac = depth2 = None
+    if extras:
+        opac = torch.empty((R,), dtype=torch.float64, device=dev)
+        depth2 = torch.empty((R,), dtype=torch.float32, device=dev)
     H.check(H.lib().pcnerf_composite(p.data_ptr(), z.data_ptr(), R, S, H.ptr(noise), float(noise_std), float(eps),
                                      H.ptr(rays), rays.shape[1] if rays is not None else 0, cn_col, cf_col, range_col,
-                                     H.ptr(w), depth.data_ptr(), H.ptr(fr), H.ptr(sl), _stream(z)))
-    return w, depth, fr, sl
+                                     H.ptr(w), depth.data_ptr(), H.ptr(fr), H.ptr(sl), H.ptr(opac), H.ptr(depth2),
+                                     _stream(z)))
+    if not extras:
+        return w, depth, fr, sl
+    om = torch.empty((), dtype=torch.float32, device=dev)
+    H.check(H.lib().pcnerf_mean_f64(opac.data_ptr(), R, float(R * S), om.data_ptr(), _stream(z)))
+    return w, depth, fr, sl, om, depth2
 
 
 def resample(z, w, n_importance: int, u=None) -> torch.Tensor:

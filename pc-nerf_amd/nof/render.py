@@ -125,6 +125,30 @@ def render_rays_val(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: 
     return {"depth_fine": depth_f, 'depth': depth}
 
 
+def render_rays(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: torch.Tensor, N_samples=64,
+                N_importance=128, use_disp=False, perturb=0, noise_std=1, chunk=1024 * 3, isval=False, *, rng=None):
+    """render.py:538-611 (the generic NOF renderer, exported in the reference's __all__).  Reproduces the
+    reference's call ``inference(..., chunk, noise_std, isval)``, which lands ``isval`` in inference's
+    ``epsilon`` slot: weights are always normalised, by sum(w) + float(isval).  Returns {'depth_fine',
+    'weights', 'opacity', 'z_vals', 'depth', 'depth2', 'opacity_fine'}; depth2 is the z at the position where
+    the last sample falls in the descending weight order (render.py:598-600; ties broken stably)."""
+    rays = _check_inputs(model, model_fine, embedding_xy, rays, 8)
+    R = rays.shape[0]
+    z = _ops.sample_coarse(rays, N_samples, N_samples, 6, 7, disparity=use_disp)
+    if perturb > 0:
+        z = _ops.perturb(z, perturb, _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
+    eps = float(isval)
+    p = _ops.query(model, rays, z, chunk)
+    w, depth, _, _, opac, _ = _ops.composite(p, z, _noise(rng, "noise", z, noise_std), noise_std, eps, extras=True)
+    u = None if perturb == 0 else _draw(rng, "u", (R, N_importance), rays.device, torch.rand)
+    zf = _ops.resample(z, w, N_importance, u)
+    pf = _ops.query(model_fine, rays, zf, chunk)
+    wf, depth_f, _, _, opac_f, depth2 = _ops.composite(pf, zf, _noise(rng, "noise_fine", zf, noise_std), noise_std,
+                                                       eps, extras=True)
+    return {'depth_fine': depth_f, 'weights': wf, 'opacity': opac, 'z_vals': zf, "depth": depth, "depth2": depth2,
+            "opacity_fine": opac_f}
+
+
 def _inference_view(model, rays, z, other, chunk, method):
     """inference_0525_2 (render.py:229-368) on the HIP kernels: query, per-row compositing / peak / child sums,
     then the ray-group walk."""
@@ -147,7 +171,7 @@ def render_rays_view_0525_2_2(model: NOF, model_fine: NOF, embedding_xy: Embeddi
         other = torch.as_tensor(other)
     other = other.to(rays.device)
     R = rays.shape[0]
-    z = _ops.sample_coarse(rays, N_samples, N_samples, 9, 10)          # parent bounds, render.py:622-628
+    z = _ops.sample_coarse(rays, N_samples, N_samples, 9, 10)   # parent bounds, render.py:622-628
     if perturb > 0:
         z = _ops.perturb(z, perturb, _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
     method = int(depth_inference_method)

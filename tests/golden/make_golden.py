@@ -205,7 +205,19 @@ def gen_view():
              **{k: t(v) for k, v in res.items()})
 
 
+def gen_render_rays():
+    rays = syn.make_rays(128, seed=51)
+    for isval in (False, True):
+        emb, mc, mf = models(train=False)
+        with torch.no_grad():
+            res = R.render_rays(mc, mf, emb, torch.from_numpy(rays[:, :8].copy()), N_samples=64, N_importance=128,
+                                perturb=0, noise_std=0, chunk=4096, isval=isval)
+        save(f"render_rays_isval{int(isval)}", rays=rays[:, :8].copy(), N_samples=64, N_importance=128,
+             **{k: t(v) for k, v in res.items()})
+
+
 if __name__ == "__main__":
+    gen_render_rays()
     gen_nof()
     gen_pdf()
     gen_val()

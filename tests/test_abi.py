@@ -34,7 +34,8 @@ def test_size_queries_without_gpu():
 def test_argument_errors_are_reported_before_launch():
     from nof import _hip
     L = _hip.lib()
-    rc = L.pcnerf_composite(None, None, 0, 0, None, 0.0, 0.0, None, 0, 0, 0, 0, None, None, None, None, None)
+    rc = L.pcnerf_composite(None, None, 0, 0, None, 0.0, 0.0, None, 0, 0, 0, 0, None, None, None, None, None, None,
+                            None)
     assert rc != 0
     assert b"null" in L.pcnerf_last_error()
 

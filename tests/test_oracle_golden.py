@@ -97,3 +97,12 @@ def test_render_view(method):
         close(res[k], g[k], 1e-5, 1e-9)
     for k in ("rays_effective_flag", "rays_effective_flag_fine"):
         assert np.array_equal(res[k].numpy(), g[k])
+
+
+@pytest.mark.parametrize("isval", [0, 1])
+def test_render_rays(isval):
+    g = golden(f"render_rays_isval{isval}")
+    res = O.render_rays(P(SEED_C), P(SEED_F), torch.from_numpy(g["rays"]), N_samples=int(g["N_samples"]),
+                        N_importance=int(g["N_importance"]), perturb=0, noise_std=0, chunk=4096, isval=bool(isval))
+    for k in ("depth", "depth_fine", "weights", "z_vals", "depth2", "opacity", "opacity_fine"):
+        close(res[k], g[k], 1e-5, 1e-9)
