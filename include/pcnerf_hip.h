@@ -142,6 +142,25 @@ int pcnerf_view_walk(const int64_t* other, int64_t n_rows, const uint8_t* at_pea
                      const double* opac_row, int n_samples, void* workspace, uint8_t* flags, float* opacity,
                      void* stream);
 
+/* ---------------------------------------------------------------- ray tables (ray/AABB intersection)
+ * float64 inputs: points (n,3) and origin (3) of one LiDAR frame in the block frame, child boxes as bounds6
+ * (C,6) = [xmin,ymin,zmin,xmax,ymax,zmax] (already grown by 0.025), centers (C,3), parent6 (6) the parent block.
+ * Train/val 15-column rows (nof/dataset/ipb2dmapping.py:736-768): rows needs n_points*15 floats; the row count
+ * (points in a child box whose box the ray enters) is written to *n_rows (device int64). */
+size_t pcnerf_rays_workspace_bytes(int64_t n_points);
+int pcnerf_build_train_rays(const double* points, int64_t n_points, const double* origin, const double* centers,
+                            const double* bounds6, int64_t n_children, const double* parent6, double surface_expand,
+                            void* workspace, float* rows, int64_t* n_rows, void* stream);
+/* Two-step 13-column rows grouped per ray (eval_kitti_render.py:675-803; method 2 = every child hit, method 1 =
+ * first hit with parent bounds): count pass (writes *n_rows, device int64) then emit pass with the same workspace;
+ * ranges (M), other_interest_sub_nerf_number (M, int64), true_in (M, bool). */
+int pcnerf_count_view_rows(const double* points, int64_t n_points, const double* origin, const double* bounds6,
+                           int64_t n_children, const double* parent6, int method, void* workspace, int64_t* n_rows,
+                           void* stream);
+int pcnerf_emit_view_rows(const double* points, int64_t n_points, const double* origin, const double* bounds6,
+                          int64_t n_children, const double* parent6, int method, void* workspace, float* rows,
+                          float* ranges, int64_t* other, uint8_t* true_in, void* stream);
+
 /* ---------------------------------------------------------------- kernel timing (bench / profiling)
  * pcnerf_prof_enable(1) makes every subsequent launch record a HIP event pair on its stream; tags:
  * 0 eval query, 1 train hidden Linear, 2 train first Linear, 3 train skip Linear, 4 train occ_out,

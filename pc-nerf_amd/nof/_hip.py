@@ -54,6 +54,10 @@ _SIGS = {
                                  vp, vp, vp, vp]),
     "pcnerf_view_walk_workspace_bytes": (c_size, [i64]),
     "pcnerf_view_walk": (c_int, [vp, i64, vp, vp, vp, c_int, vp, vp, vp, vp]),
+    "pcnerf_rays_workspace_bytes": (c_size, [i64]),
+    "pcnerf_build_train_rays": (c_int, [vp, i64, vp, vp, vp, i64, vp, ctypes.c_double, vp, vp, vp, vp]),
+    "pcnerf_count_view_rows": (c_int, [vp, i64, vp, vp, i64, vp, c_int, vp, vp, vp]),
+    "pcnerf_emit_view_rows": (c_int, [vp, i64, vp, vp, i64, vp, c_int, vp, vp, vp, vp, vp, vp]),
     "pcnerf_prof_enable": (c_int, [c_int]),
     "pcnerf_prof_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
@@ -100,7 +104,7 @@ def require_device(*ts: torch.Tensor) -> None:
     for t in ts:
         if t is None:
             continue
-        if not (t.is_cuda and t.dtype in (torch.float32, torch.uint8, torch.bool, torch.int64)):
+        if not (t.is_cuda and t.dtype in (torch.float32, torch.float64, torch.uint8, torch.bool, torch.int64)):
             raise RuntimeError("pcnerf_hip kernels take ROCm device tensors (got %s on %s); this package has no "
                                "CPU path" % (t.dtype, t.device))
 

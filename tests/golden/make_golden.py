@@ -216,7 +216,73 @@ def gen_render_rays():
              **{k: t(v) for k, v in res.items()})
 
 
+def reference_functions():
+    """The reference's ray/AABB primitives, executed from its own source text: the modules that define them
+    (nof/dataset/ipb2dmapping.py, eval_kitti_render.py) import open3d/pcl at top level, which this image lacks,
+    but the functions themselves only use numpy and sklearn's KDTree."""
+    import ast
+    from sklearn.neighbors import KDTree
+    ns = {"np": np, "KDTree": KDTree}
+    want = {"nof/dataset/ipb2dmapping.py": ("compute_far_bound", "compute_far_bound0406", "compute_far_bound0606",
+                                            "find_aabb_box"),
+            "eval_kitti_render.py": ("compute_far_bound0429", "ray_aabb_distances", "distance_to_ray")}
+    for rel, names in want.items():
+        src = open(os.path.join(REF, rel)).read()
+        for node in ast.parse(src).body:
+            if isinstance(node, ast.FunctionDef) and node.name in names:
+                code = ast.get_source_segment(src, node).replace('    print("here")\n', "")
+                exec(compile(code, rel, "exec"), ns)
+    return ns
+
+
+def gen_aabb():
+    """Ray/AABB primitives on synthetic scenes: points on/inside child boxes seen from an origin, plus boxes the
+    rays graze (edge/corner hits, the eval path's exactly-two-hits rule) and misses."""
+    F = reference_functions()
+    rng = np.random.default_rng(61)
+    boxes = syn.make_children(200, seed=62, min_center_dist=2.0)
+    lo = boxes[:, 0] - syn.AABB_GROW
+    hi = boxes[:, 1] + syn.AABB_GROW
+    centers = 0.5 * (boxes[:, 0] + boxes[:, 1])
+    origin = np.array([0.3, -0.2, 0.1])
+    n = 600
+    cid = rng.integers(0, len(boxes), size=n)
+    pts = rng.uniform(boxes[cid, 0] - 0.3, boxes[cid, 1] + 0.3)          # some outside every box
+    pts[::7] = np.where(rng.random((len(pts[::7]), 3)) < 0.5, boxes[cid[::7], 0], boxes[cid[::7], 1])  # corners
+    vec = pts - origin
+    rng_ = np.linalg.norm(vec, axis=1)
+    dirs = vec / rng_[:, None]
+    bounds6 = np.concatenate([lo, hi], 1)
+    inside, idx = [], []
+    for q in pts:
+        ok, k = F["find_aabb_box"](centers, bounds6, q)
+        inside.append(ok)
+        idx.append(-1 if k is None else k)
+    pb = (syn.PARENT_LO, syn.PARENT_HI)
+    parent_far = []
+    for d in dirs:
+        t = F["compute_far_bound"](origin, d, pb[1][0], pb[0][0], pb[1][1], pb[0][1], pb[1][2], pb[0][2])
+        parent_far.append(np.nan if t is None else t)
+    # face-hit tests against the point's own box and a random box
+    other_box = rng.integers(0, len(boxes), size=n)
+    f0606, f0429 = [], []
+    for i in range(n):
+        row = []
+        for b in (cid[i], other_box[i]):
+            hit, a, z = F["compute_far_bound0606"](origin, dirs[i], lo[b], hi[b])
+            row += [float(hit), a, z]
+            hit2, a2, z2 = F["compute_far_bound0429"](origin, dirs[i], lo[b], hi[b])
+            f0429.append([float(hit2), a2, z2])
+        f0606.append(row)
+    slab = F["ray_aabb_distances"](origin, dirs, np.array(syn.PARENT_LO), np.array(syn.PARENT_HI))
+    d2r = np.stack([F["distance_to_ray"](torch.from_numpy(origin), dirs[i], centers) for i in range(0, n, 37)])
+    save("aabb_primitives", boxes=boxes, lo=lo, hi=hi, centers=centers, origin=origin, points=pts, cid=cid,
+         other_box=other_box, find_inside=np.array(inside), find_idx=np.array(idx), parent_far=np.array(parent_far),
+         f0606=np.array(f0606), f0429=np.array(f0429), slab=slab, d2r=d2r)
+
+
 if __name__ == "__main__":
+    gen_aabb()
     gen_render_rays()
     gen_nof()
     gen_pdf()

@@ -256,3 +256,37 @@ def test_full_size_properties():
         v = float(res[k])
         assert np.isfinite(v) and v >= 0
     assert not torch.equal(rm0, mc.norms()[0].running_mean)
+
+
+def _aabb_scene():
+    g = golden("aabb_primitives")
+    bounds6 = np.concatenate([g["lo"], g["hi"]], 1)
+    parent6 = np.concatenate([syn.PARENT_LO, syn.PARENT_HI])
+    return g, bounds6, parent6
+
+
+def test_build_train_rays_vs_oracle():
+    from nof.raytable import build_train_rays
+    from oracle import rays_cpu as RC
+    g, bounds6, parent6 = _aabb_scene()
+    ref = RC.build_train_rays(g["points"], g["origin"], g["centers"], bounds6, syn.PARENT_LO, syn.PARENT_HI)
+    t = lambda a: torch.from_numpy(np.asarray(a, dtype=np.float64)).to(DEV)
+    got = build_train_rays(t(g["points"]), t(g["origin"]), t(g["centers"]), t(bounds6), t(parent6)).cpu().numpy()
+    assert got.shape == ref.shape
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("method", [2, 1])
+def test_build_view_rows_vs_oracle(method):
+    from nof.raytable import build_view_rows
+    from oracle import rays_cpu as RC
+    g, bounds6, parent6 = _aabb_scene()
+    rows, rng, other, tin = RC.build_view_rows(g["points"], g["origin"], bounds6, syn.PARENT_LO, syn.PARENT_HI,
+                                               method=method)
+    t = lambda a: torch.from_numpy(np.asarray(a, dtype=np.float64)).to(DEV)
+    r2, g2, o2, t2 = build_view_rows(t(g["points"]), t(g["origin"]), t(bounds6), t(parent6), method=method)
+    assert r2.shape == rows.shape
+    np.testing.assert_array_equal(r2.cpu().numpy(), rows)
+    np.testing.assert_array_equal(g2.cpu().numpy(), rng)
+    np.testing.assert_array_equal(o2.cpu().numpy(), other)
+    np.testing.assert_array_equal(t2.cpu().numpy(), tin)
