@@ -218,7 +218,7 @@ def render_rays_train(Pc, Pf, rays, sub_nerf_test_num=4, N_samples=64, N_importa
 
     w, depth, fl, dl = pass_(Pc, z, draws.get("noise"))
     zmid = .5 * (z[..., 1:] + z[..., :-1])
-    zs = sample_pdf(zmid, w[..., 1:-1], N_importance, det=(perturb == 0.), u=draws.get("u"))
+    zs = sample_pdf(zmid, w[..., 1:-1], N_importance, det=(perturb == 0.), u=draws.get("u")).detach()  # :466
     zf = torch.sort(torch.cat([z, zs], -1), -1)[0]
     wf, depth_f, flf, dlf = pass_(Pf, zf, draws.get("noise_fine"))
     return {"child_free_loss_fine": flf, "child_depth_loss_fine": dlf, "depth_fine": depth_f,

@@ -281,7 +281,47 @@ def gen_aabb():
          f0606=np.array(f0606), f0429=np.array(f0429), slab=slab, d2r=d2r)
 
 
+GRAD_CASES = {"pcnerf": (1, 1, 0), "divide": (1, 1, 1), "original": (0, 0, 0)}
+
+
+def grad_summary(m, seed):
+    """Full gradients of the small tensors; norm + 2048 fixed entries of each weight matrix."""
+    out = {}
+    rng = np.random.default_rng(seed)
+    for k, p_ in m.named_parameters():
+        gr = p_.grad.detach().numpy()
+        if gr.size <= 512:
+            out[k] = gr
+        else:
+            idx = rng.choice(gr.size, size=2048, replace=False)
+            out[k + "@idx"] = idx
+            out[k + "@val"] = gr.reshape(-1)[idx]
+            out[k + "@norm"] = np.linalg.norm(gr.astype(np.float64))
+    return out
+
+
+def gen_grads():
+    """Parameter gradients of the train_kitti.py:117-155 loss through render_rays_train (train-mode BN, several
+    chunks), i.e. what loss.backward() produces in the reference's training step."""
+    for name, (cl, seg, div) in GRAD_CASES.items():
+        rays = syn.make_rays(96, seed=71)
+        emb, mc, mf = models(train=True)
+        res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=32, N_samples=64,
+                                  N_importance=128, perturb=0, noise_std=0, chunk=4096, issegmentated=seg,
+                                  childnerf_ratio=0.1, use_child_nerf_divide=div, use_child_nerf_loss=cl)
+        gt = torch.from_numpy(rays[:, 14])
+        lr, lrf = range_losses(res["depth"], res["depth_fine"], gt, torch.from_numpy(rays), div, 32)
+        total = lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"] + \
+            1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"]
+        total.sum().backward()
+        gc = {"c:" + k: v for k, v in grad_summary(mc, 81).items()}
+        gf = {"f:" + k: v for k, v in grad_summary(mf, 82).items()}
+        save(f"grads_{name}", rays=rays, use_child_nerf_loss=cl, issegmentated=seg, use_child_nerf_divide=div,
+             loss_total=t(total), **gc, **gf)
+
+
 if __name__ == "__main__":
+    gen_grads()
     gen_aabb()
     gen_render_rays()
     gen_nof()

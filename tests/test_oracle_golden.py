@@ -106,3 +106,66 @@ def test_render_rays(isval):
                         N_importance=int(g["N_importance"]), perturb=0, noise_std=0, chunk=4096, isval=bool(isval))
     for k in ("depth", "depth_fine", "weights", "z_vals", "depth2", "opacity", "opacity_fine"):
         close(res[k], g[k], 1e-5, 1e-9)
+
+
+def grad_leaves(Pm):
+    keys = [k for k in Pm if k.endswith(".weight") or k.endswith(".bias")]
+    for k in keys:
+        Pm[k].requires_grad_(True)
+    return keys
+
+
+def noise_level_grads():
+    """Gradients that are mathematically zero: the bias of every Linear that feeds a BatchNorm (BN removes the
+    mean) and the shift of every BN followed by Linear->BN (its gradient is W^T sum(dL/dh) = 0).  Their values
+    are pure rounding noise, so they are checked to be at noise level against the BN scale gradient."""
+    out = {}
+    for i, (lin, bn) in enumerate(zip(O.LIN, O.BN)):
+        out[lin + ".bias"] = bn + ".weight"
+        if i < 7:
+            out[bn + ".bias"] = bn + ".weight"
+    return out
+
+
+def check_grads(get, keys, g, prefix, rtol, noise=1e-5):
+    """Golden gradients: small tensors in full, weight matrices by norm + 2048 fixed entries."""
+    bad = []
+    nz = noise_level_grads()
+    for k in keys:
+        gr = np.asarray(get(k), dtype=np.float64)
+        try:
+            if k in nz:
+                ref_scale = np.abs(g[prefix + nz[k]]).max()
+                assert np.abs(gr).max() <= noise * ref_scale, (np.abs(gr).max(), ref_scale)
+                assert np.abs(g[prefix + k]).max() <= noise * ref_scale
+            elif prefix + k in g:
+                ref = g[prefix + k]
+                np.testing.assert_allclose(gr, ref, rtol=rtol, atol=rtol * np.abs(ref).max(), err_msg=k)
+            else:
+                idx = g[prefix + k + "@idx"]
+                ref = g[prefix + k + "@val"]
+                np.testing.assert_allclose(gr.reshape(-1)[idx], ref, rtol=rtol, atol=rtol * np.abs(ref).max(),
+                                           err_msg=k)
+                np.testing.assert_allclose(np.linalg.norm(gr), g[prefix + k + "@norm"], rtol=rtol)
+        except AssertionError as e:
+            bad.append(prefix + k + ": " + " ".join(str(e).split())[:300])
+    assert not bad, "\n".join(bad)
+
+
+@pytest.mark.parametrize("name", ["pcnerf", "divide", "original"])
+def test_train_grads(name):
+    """loss.backward() of train_kitti.py:117-155 through render_rays_train: oracle autograd == reference."""
+    g = golden(f"grads_{name}")
+    Pc, Pf = P(SEED_C), P(SEED_F)
+    kc, kf = grad_leaves(Pc), grad_leaves(Pf)
+    rays = torch.from_numpy(g["rays"])
+    div = int(g["use_child_nerf_divide"])
+    res = O.render_rays_train(Pc, Pf, rays, sub_nerf_test_num=32, N_samples=64, N_importance=128, perturb=0,
+                              noise_std=0, chunk=4096, issegmentated=int(g["issegmentated"]), childnerf_ratio=0.1,
+                              use_child_nerf_divide=div, use_child_nerf_loss=int(g["use_child_nerf_loss"]))
+    lr, lrf = O.range_losses(res["depth"], res["depth_fine"], rays[:, 14], rays, div, 32)
+    tot = O.total_loss(res, lr, lrf)
+    close(tot.detach().reshape(-1), g["loss_total"].reshape(-1), 1e-6, 0)
+    tot.sum().backward()
+    check_grads(lambda k: Pc[k].grad.numpy(), kc, g, "c:", 1e-5)
+    check_grads(lambda k: Pf[k].grad.numpy(), kf, g, "f:", 1e-5)
