@@ -74,6 +74,31 @@ int pcnerf_nof_query_train(const float* rays, int64_t n_rays, int ray_stride, co
 int pcnerf_nof_forward_train(const float* emb, int64_t n, const pcnerf_nof_params* params, float momentum,
                              float eps, void* workspace, size_t workspace_bytes, float* p_out, void* stream);
 
+/* ---------------------------------------------------------------- training backward (loss.backward())
+ * Parameter gradients of the train-mode query, i.e. what autograd produces through render.py:47-50 and
+ * models.py:183-203 (Linear -> BatchNorm1d(train) x 8, skip concat, occ_out, sigmoid) in the reference's
+ * training step (train_kitti.py:155 `loss` returned to Lightning, which calls backward).  The chunks are
+ * recomputed (same BatchNorm batches as the forward, running stats untouched).  Gradients are ADDED to the
+ * non-NULL buffers of `grads` (torch .grad accumulation semantics); each has the shape of its parameter. */
+typedef struct pcnerf_nof_grads {
+  float* lin_w[8];
+  float* lin_b[8];
+  float* bn_w[8];
+  float* bn_b[8];
+  float* out_w;
+  float* out_b;
+} pcnerf_nof_grads;
+size_t pcnerf_nof_backward_workspace_bytes(int64_t chunk);
+/* grad_logit[g] = dL/d(occupancy logit) of flattened sample g (pcnerf_composite_backward's output). */
+int pcnerf_nof_query_train_backward(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                    int n_samples, int64_t chunk, const pcnerf_nof_params* params, float eps,
+                                    const float* grad_logit, void* workspace, size_t workspace_bytes,
+                                    const pcnerf_nof_grads* grads, void* stream);
+/* NOF.forward(emb) in train mode (one batch): grad_p = dL/dp for p = the forward's output. */
+int pcnerf_nof_forward_train_backward(const float* emb, int64_t n, const pcnerf_nof_params* params, float eps,
+                                      const float* p, const float* grad_p, void* workspace, size_t workspace_bytes,
+                                      const pcnerf_nof_grads* grads, void* stream);
+
 /* ---------------------------------------------------------------- sampling (render.py:429-454, :497-511)
  * z[ray, :] = linspace sampling of [rays[near_col], rays[far_col]] with n_samples points; if
  * n_parent < n_samples the segmented scheme is used: n_parent points over [near, far] and
@@ -100,6 +125,19 @@ int pcnerf_composite(const float* p, const float* z, int64_t n_rays, int n_sampl
 /* mean = sum(x[0:n]) / denom, one float written to out (used for the opacity means). */
 int pcnerf_mean_f64(const double* x, int64_t n, double denom, float* out, void* stream);
 
+/* Backward of pcnerf_composite + the child losses (render.py:51-61, 75-159) to the occupancy logits:
+ * grad_logit[r, s] = dL/d logit(p[r, s]) given grad_depth[r] = dL/d depth[r] (nullable = 0) and the device
+ * scalars grad_free_loss = dL/d child_free_loss, grad_depth_loss = dL/d child_depth_loss (nullable = 0;
+ * ignored when rays == NULL).  sub_nerf_test_num > 0 selects the divide branch (child ids in
+ * rays[:, child_id_col]); `workspace` then needs pcnerf_composite_backward_workspace_bytes(sub_nerf_test_num).
+ * The weights are not differentiated through sample_pdf (render.py:466 detaches the fine samples). */
+size_t pcnerf_composite_backward_workspace_bytes(int sub_nerf_test_num);
+int pcnerf_composite_backward(const float* p, const float* z, int64_t n_rays, int n_samples, const float* noise,
+                              float noise_std, float eps, const float* rays, int ray_stride, int child_near_col,
+                              int child_far_col, int range_col, int child_id_col, int sub_nerf_test_num,
+                              const float* grad_depth, const float* grad_free_loss, const float* grad_depth_loss,
+                              void* workspace, float* grad_logit, void* stream);
+
 /* ---------------------------------------------------------------- importance resampling
  * z_fine[ray, :] = sort(cat(z, sample_pdf(mid(z), weights[:, 1:-1], n_importance, det = (u == NULL))))
  * (render.py:371-412, :463-467).  `u` [n_rays, n_importance] replaces torch.rand when not NULL. */
@@ -124,6 +162,10 @@ int pcnerf_child_loss_reduce(const float* free_ray, const float* sl1_ray, int64_
  * 2 = SmoothL1(beta 1) (nof/criteria/loss.py:12-50 with nn.*Loss(reduction='mean')).  out: one float. */
 int pcnerf_pointwise_loss(const float* pred, const float* target, const uint8_t* mask, int64_t n, int kind,
                           float* out, void* stream);
+/* Its backward: grad_pred[i] = grad_out * d loss_i / d pred_i / count (0 where mask == 0); grad_out is a
+ * device scalar. */
+int pcnerf_pointwise_loss_backward(const float* pred, const float* target, const uint8_t* mask, int64_t n, int kind,
+                                   const float* grad_out, float* grad_pred, void* stream);
 
 /* ---------------------------------------------------------------- two-step inference (render_rays_view_0525_2_2)
  * Per row (render.py:241-354 after the query): weights = composite(p) normalised with eps, the strict child
@@ -164,7 +206,8 @@ int pcnerf_emit_view_rows(const double* points, int64_t n_points, const double* 
 /* ---------------------------------------------------------------- kernel timing (bench / profiling)
  * pcnerf_prof_enable(1) makes every subsequent launch record a HIP event pair on its stream; tags:
  * 0 eval query, 1 train hidden Linear, 2 train first Linear, 3 train skip Linear, 4 train occ_out,
- * 5 BN fold, 6 composite, 7 resample, 8 sampling.  pcnerf_prof_read synchronises the tag's events and returns
+ * 5 BN fold, 6 composite, 7 resample, 8 sampling, 9 composite backward, 10 weight-gradient GEMM,
+ * 11 data-gradient GEMM, 12 other backward kernels.  pcnerf_prof_read synchronises the tag's events and returns
  * the summed duration, launch count and algorithmic FLOPs / bytes of those launches. */
 int pcnerf_prof_enable(int on);
 int pcnerf_prof_read(int tag, double* total_ms, int64_t* launches, double* flops, double* bytes);

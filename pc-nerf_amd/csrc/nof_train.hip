@@ -128,7 +128,7 @@ __device__ __forceinline__ void bn_coeffs(const BnPrev& B, int64_t n, float mome
   const float a = invstd * B.gamma[k];
   al[k] = a;
   be[k] = B.beta[k] - (float)mean * a;
-  if (blockIdx.x == 0) {
+  if (blockIdx.x == 0 && B.rm) {  // (the backward's forward recomputation passes no running stats)
     const double mom = (double)momentum;
     B.rm[k] = (float)(mom * mean + (1.0 - mom) * (double)B.rm[k]);
     const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
@@ -440,5 +440,674 @@ extern "C" int pcnerf_nof_forward_train(const float* emb, int64_t n, const pcner
   PCN_CHECK(emb && params && workspace && p_out, "pcnerf_nof_forward_train: null argument");
   PCN_CHECK(n > 0, "pcnerf_nof_forward_train: empty input");
   query_train(nullptr, 0, nullptr, 1, emb, n, n, params, momentum, eps, workspace, workspace_bytes, p_out, stream);
+  PCN_API_END
+}
+
+// =============================================================================================== backward
+// dL/dparams of the train-mode query (loss.backward() through render.py:47-50 and models.py:183-203), given
+// dL/dlogit per sample (or dL/dp with p).  Per chunk:
+//   1. forward recomputation with k_train_layer, the raw h_L of all 8 layers kept (1 KiB/sample each) and the
+//      chunk statistics re-derived (running stats untouched); k_bn_save stores mean/invstd/alpha/beta;
+//   2. occ_out + BatchNorm 8 backward (k_out_bwd_stats, k_out_bwd_grad) -> dL/dh_7;
+//   3. for L = 7..1: k_wgrad: G_L = sum_s dL/dh_L[s] (x) (h_{L-1}[s] - mean_{L-1})   (+ the encoding part at L=4)
+//                    on MFMA, partials per block;  k_wgrad_reduce: dW_L = alpha*G + beta (x) db, db_L, and the
+//                    statistics BatchNorm L-1's backward needs, which are algebraic in G and db:
+//                      sum_s dL/dy = W^T db,   sum_s dL/dy (h - mean) = colsum(W o G);
+//                    k_dgrad: dL/dh_{L-1} = BN_back(W_L^T dL/dh_L) on MFMA, the BatchNorm backward fused into
+//                    the epilogue (ATen's formula: (dy - mean(dy) - (h - mean) * k) * invstd * gamma);
+//   4. k_wgrad / k_wgrad_reduce for layer 0 on the recomputed encoding.
+// Parameter gradients accumulate in float64 across chunks and are added to the caller's fp32 buffers at the
+// end (k_grad_emit).
+namespace pcn {
+
+constexpr size_t DGRAD_W_FLOATS = 7 * SZ_H;
+constexpr int WG_BLOCKS = 256;  // weight-gradient partials per chunk (one 8-wave block per CU)
+
+__host__ __device__ constexpr int in_features(int L) { return L == 0 ? 63 : L == 4 ? 319 : 256; }
+
+// transposed weights for the data-gradient GEMM (neurons of layer L-1 on MFMA rows, samples on columns):
+//   A (k-group kg, block ob, lane l, component q) = W_L[m = 8kg + 4(l>>5) + q][col0 + 32 ob + (l&31)]
+__global__ void k_pack_dgrad(NofParamsDev P, float* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= DGRAD_W_FLOATS) return;
+  const int L = 1 + (int)(idx / SZ_H);
+  const size_t j = idx % SZ_H;
+  const int q = (int)(j & 3), lane = (int)((j >> 2) & 63), ob = (int)((j >> 8) & 7), kg = (int)(j >> 11);
+  const int m = 8 * kg + 4 * (lane >> 5) + q, nn = 32 * ob + (lane & 31);
+  out[idx] = P.lin_w[L][(size_t)m * in_features(L) + (L == 4 ? 63 : 0) + nn];
+}
+
+// per layer: [mean(256), invstd(256), alpha = invstd*gamma (256), beta (256)] -- bn_coeffs' arithmetic
+__global__ void k_bn_save(NofParamsDev P, const double* __restrict__ stats, int64_t n, float eps,
+                          float* __restrict__ coef) {
+  const int L = blockIdx.x, k = threadIdx.x;
+  const double s1 = stats[512 * L + 2 * k], s2 = stats[512 * L + 2 * k + 1];
+  const double m = s1 / (double)n;
+  double var = s2 / (double)n - m * m;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  float* c = coef + 1024 * L;
+  c[k] = (float)((double)P.lin_b[L][k] + m);
+  c[256 + k] = invstd;
+  c[512 + k] = invstd * P.bn_w[L][k];
+  c[768 + k] = P.bn_b[L][k];
+}
+
+__device__ __forceinline__ float logit_grad(const float* __restrict__ g, const float* __restrict__ p, int64_t i) {
+  if (!p) return g[i];
+  const float pv = p[i];
+  return g[i] * (1.0f - pv) * pv;  // sigmoid backward
+}
+
+// acc[f] += sum_s g_s (h7[s][f] - mean7[f]), acc[256] += sum_s g_s.  Each lane accumulates its 128 features over
+// its tiles; one LDS transpose-reduction per block at the end.
+__global__ __launch_bounds__(256) void k_out_bwd_stats(const float* __restrict__ g, const float* __restrict__ pin,
+                                                       const float* __restrict__ h7, int64_t n,
+                                                       const float* __restrict__ coef7, double* __restrict__ acc) {
+  __shared__ float red[64 * 129];
+  __shared__ __attribute__((aligned(16))) float mu[256];
+  const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31, wv = t >> 6;
+  mu[t] = coef7[t];
+  __syncthreads();
+  float a[128];
+#pragma unroll
+  for (int i = 0; i < 128; ++i) a[i] = 0.0f;
+  float gs = 0.0f;
+  const int64_t ntiles = (n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wv; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t s = tile * 32 + li;
+    const float gv = s < n ? logit_grad(g, pin, s) : 0.0f;
+    if (h == 0) gs += gv;
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(h7 + tile * TILE_FLOATS) + lane;
+#pragma unroll
+    for (int gq = 0; gq < 32; ++gq) {
+      const f32x4 x = x4[gq * 64];
+      const f32x4 m = *reinterpret_cast<const f32x4*>(mu + 8 * gq + 4 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[4 * gq + q] += gv * (x[q] - m[q]);
+    }
+  }
+  const int hb = (t >> 2) & 1, idx = (t >> 3) * 4 + (t & 3);
+  double tot = 0.0;
+  for (int w = 0; w < 4; ++w) {
+    __syncthreads();
+    if (wv == w) {
+#pragma unroll
+      for (int i = 0; i < 128; ++i) red[lane * 129 + i] = a[i];
+    }
+    __syncthreads();
+    float s = 0.0f;
+    for (int l = 0; l < 32; ++l) s += red[(l + 32 * hb) * 129 + idx];
+    tot += (double)s;
+  }
+  atomicAdd(&acc[t], tot);
+  gs = wave_sum_f(gs);
+  if (lane == 0) atomicAdd(&acc[256], (double)gs);
+}
+
+// dL/dh_7 = BN8_back(g_s * w_out); block 0 also accumulates d gamma_8, d beta_8, d w_out, d b_out.
+__global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ g, const float* __restrict__ pin,
+                                                      const float* __restrict__ h7, int64_t n,
+                                                      const float* __restrict__ coef7, const float* __restrict__ gamma,
+                                                      const float* __restrict__ wout, const double* __restrict__ acc,
+                                                      double* __restrict__ d_gamma, double* __restrict__ d_beta,
+                                                      double* __restrict__ d_wout, double* __restrict__ d_bout,
+                                                      float* __restrict__ gout) {
+  __shared__ __attribute__((aligned(16))) float cgm[256];
+  __shared__ __attribute__((aligned(16))) float ckk[256];
+  __shared__ __attribute__((aligned(16))) float cmu[256];
+  __shared__ __attribute__((aligned(16))) float cis[256];
+  __shared__ __attribute__((aligned(16))) float cga[256];
+  __shared__ __attribute__((aligned(16))) float cwo[256];
+  {
+    const int k = threadIdx.x;
+    const double A = acc[k], G0 = acc[256];
+    const float wo = wout[k], invstd = coef7[256 + k];
+    const double S1 = (double)wo * G0, dotp = (double)wo * A;
+    cgm[k] = (float)(S1 / (double)n);
+    ckk[k] = (((float)dotp * invstd) * invstd) / (float)n;
+    cmu[k] = coef7[k];
+    cis[k] = invstd;
+    cga[k] = gamma[k];
+    cwo[k] = wo;
+    if (blockIdx.x == 0) {
+      d_gamma[k] += dotp * (double)invstd;
+      d_beta[k] += S1;
+      d_wout[k] += (double)coef7[512 + k] * A + (double)coef7[768 + k] * G0;
+      if (k == 0) d_bout[0] += G0;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
+  const int64_t ntiles = (n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t s = tile * 32 + li;
+    const bool valid = s < n;
+    const float gv = valid ? logit_grad(g, pin, s) : 0.0f;
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(h7 + tile * TILE_FLOATS) + lane;
+    f32x4* o4 = reinterpret_cast<f32x4*>(gout + tile * TILE_FLOATS) + lane;
+#pragma unroll 8
+    for (int gq = 0; gq < 32; ++gq) {
+      const f32x4 x = x4[gq * 64];
+      const int f0 = 8 * gq + 4 * h;
+      f32x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = f0 + q;
+        o[q] = valid ? ((gv * cwo[f] - cgm[f]) - (x[q] - cmu[f]) * ckk[f]) * cis[f] * cga[f] : 0.0f;
+      }
+      o4[gq * 64] = o;
+    }
+  }
+}
+
+// ---- weight gradient: G[m][n] = sum_s dL/dh_L[s][m] * X[s][n] over one chunk, partials per block.
+// 8 waves per block, wave w owns rows m in [32w, 32w+32).  Per 32-sample tile both operands are staged in LDS
+// as [sample][feature] (rows padded to 260 floats) so the MFMA reads contract over samples:
+//   A (lane l, k-step t) = dL/dh[2t + (l>>5)][32w + (l&31)],  B (lane l) = X[2t + (l>>5)][32nb + (l&31)]
+// X = h_{L-1} - mean_{L-1} (MODE 0), the encoding (MODE 1, 64 columns), or both (MODE 2, layer 4).  The next
+// tile's operands are loaded into registers while the current one is multiplied (double-buffered LDS, one
+// barrier per tile).  db[m] = sum_s dL/dh[s][m] comes free from the A reads.
+constexpr int ES_ROW = 68;
+
+template <int MODE>
+struct WgradCfg {
+  static constexpr bool HX = MODE != 1, EX = MODE != 0;
+  static constexpr int C = (EX ? 64 : 0) + (HX ? 256 : 0);
+  static constexpr int GS = 32 * LDS_ROW;
+  static constexpr int BUF = GS + (HX ? GS : 0) + (EX ? 32 * ES_ROW : 0);
+  static constexpr size_t LDS_BYTES = (size_t)(2 * BUF + 256) * sizeof(float);
+  static constexpr size_t PART = (size_t)256 * C + 256;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays, int stride,
+                                                  const float* __restrict__ z, int S, int64_t c0, int64_t n,
+                                                  const float* __restrict__ ein, const float* __restrict__ gin,
+                                                  const float* __restrict__ hprev, const float* __restrict__ mu,
+                                                  float* __restrict__ part) {
+  using Cfg = WgradCfg<MODE>;
+  constexpr bool HX = Cfg::HX, EX = Cfg::EX;
+  constexpr int GS = Cfg::GS, BUF = Cfg::BUF, C = Cfg::C;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* mus = lds + 2 * BUF;
+  const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31, wv = t >> 6;
+  if (HX && t < 256) mus[t] = mu[t];
+  __syncthreads();
+  const int64_t ntiles = (n + 31) / 32;
+  f32x16 ah[8], ae[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) ah[b][r] = 0.0f;
+    ae[0][r] = 0.0f;
+    ae[1][r] = 0.0f;
+  }
+  float dbacc = 0.0f;
+  f32x4 rg[4], rx[4];
+  auto gload = [&](int64_t tile) {
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(gin + tile * TILE_FLOATS);
+    const f32x4* x4 = reinterpret_cast<const f32x4*>((HX ? hprev : gin) + tile * TILE_FLOATS);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      rg[j] = g4[t + 512 * j];
+      if (HX) rx[j] = x4[t + 512 * j];
+    }
+  };
+  auto lstore = [&](float* buf, int64_t tile) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = t + 512 * j, g = i >> 6, lp = i & 63;
+      const int off = (lp & 31) * LDS_ROW + 8 * g + 4 * (lp >> 5);
+      *reinterpret_cast<f32x4*>(buf + off) = rg[j];
+      if (HX) {
+        const f32x4 m = *reinterpret_cast<const f32x4*>(mus + 8 * g + 4 * (lp >> 5));
+        f32x4 x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = rx[j][q] - m[q];
+        *reinterpret_cast<f32x4*>(buf + GS + off) = x;
+      }
+    }
+    if (EX) {
+      float* row = buf + GS + (HX ? GS : 0) + (t >> 4) * ES_ROW;
+      const int jj = t & 15;
+      int64_t sl = tile * 32 + (t >> 4);
+      if (sl >= n) sl = n - 1;
+      const int64_t gi = c0 + sl;
+      if (ein) {
+        const float* er = ein + gi * 63;
+        for (int f = jj; f < 64; f += 16) row[f] = f < 63 ? er[f] : 0.0f;
+      } else {
+        float p[3];
+        sample_point(rays + (gi / S) * stride, z[gi], p);
+        if (jj == 0) {
+          row[0] = p[0];
+          row[1] = p[1];
+          row[2] = p[2];
+          row[63] = 0.0f;
+        }
+        for (int q = jj; q < 30; q += 16) {
+          const int k = q / 3, m = q - 3 * k;
+          float sv, cv;
+          sincosf((float)(1 << k) * p[m], &sv, &cv);  // encode_half's arithmetic
+          row[3 + 6 * k + m] = sv;
+          row[6 + 6 * k + m] = cv;
+        }
+      }
+    }
+  };
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) gload(tile);
+  int bsel = 0;
+  for (; tile < ntiles; tile += gridDim.x) {
+    float* buf = lds + bsel * BUF;
+    lstore(buf, tile);
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) gload(tile + gridDim.x);
+    const float* xs = buf + GS;
+    const float* xe = buf + GS + (HX ? GS : 0);
+#pragma unroll
+    for (int kt = 0; kt < 16; ++kt) {
+      const int s = 2 * kt + h;
+      const float a = buf[s * LDS_ROW + 32 * wv + li];
+      dbacc += a;
+      if (HX) {
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb)
+          ah[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xs[s * LDS_ROW + 32 * nb + li], ah[nb], 0, 0, 0);
+      }
+      if (EX) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          ae[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xe[s * ES_ROW + 32 * nb + li], ae[nb], 0, 0, 0);
+      }
+    }
+    bsel ^= 1;
+  }
+  float* pb = part + (size_t)blockIdx.x * Cfg::PART;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = 32 * wv + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (EX) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) pb[(size_t)m * C + 32 * nb + li] = ae[nb][r];
+    }
+    if (HX) {
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) pb[(size_t)m * C + (EX ? 64 : 0) + 32 * nb + li] = ah[nb][r];
+    }
+  }
+  dbacc += __shfl_xor(dbacc, 32, 64);
+  if (h == 0) pb[(size_t)256 * C + 32 * wv + li] = dbacc;
+}
+
+// Sum the partials of row m (block m, thread = column), accumulate dW/db in float64 and the statistics of the
+// BatchNorm below: s12[n] = (sum_m W[m][n] db[m], sum_m W[m][n] G[m][n]).
+template <int MODE>
+__global__ void k_wgrad_reduce(const float* __restrict__ part, int nblk, const float* __restrict__ W,
+                               const float* __restrict__ coefp, double* __restrict__ dW, double* __restrict__ db,
+                               double* __restrict__ s12) {
+  using Cfg = WgradCfg<MODE>;
+  constexpr int C = Cfg::C;
+  constexpr int in_f = MODE == 0 ? 256 : MODE == 1 ? 63 : 319;
+  constexpr int wcol_h = MODE == 2 ? 63 : 0, col_h = Cfg::EX ? 64 : 0;
+  __shared__ double red[C];
+  const int m = blockIdx.x, t = threadIdx.x;
+  double d = 0.0;
+  for (int b = t; b < nblk; b += C) d += (double)part[(size_t)b * Cfg::PART + (size_t)256 * C + m];
+  red[t] = d;
+  __syncthreads();
+  double dbm = 0.0;
+  for (int i = 0; i < C; ++i) dbm += red[i];
+  double G = 0.0;
+  for (int b = 0; b < nblk; ++b) G += (double)part[(size_t)b * Cfg::PART + (size_t)m * C + t];
+  if (Cfg::EX && t < 64) {
+    if (t < 63) dW[(size_t)m * in_f + t] += G;
+  } else {
+    const int nn = t - col_h;
+    const size_t wi = (size_t)m * in_f + wcol_h + nn;
+    dW[wi] += (double)coefp[512 + nn] * G + (double)coefp[768 + nn] * dbm;
+    const double w = (double)W[wi];
+    atomicAdd(&s12[2 * nn], w * dbm);
+    atomicAdd(&s12[2 * nn + 1], w * G);
+  }
+  if (t == 0) db[m] += dbm;
+}
+
+// ---- data gradient: dL/dh_{L-1} = BN_{L-1}_back(W_L^T dL/dh_L), samples on MFMA columns:
+//   A = packed W_L^T (k_pack_dgrad), B (lane l, k-step t) = dL/dh_L[sample l&31][feature(t, l>>5)]
+//   D (block ob, reg r, lane l) = dL/dy[sample l&31][neuron 32 ob + (r&3) + 8 (r>>2) + 4 (l>>5)]
+// so registers 4gq..4gq+3 of block ob are exactly the float4 at [g = 4 ob + gq][lane] of the tile layout: the
+// h_{L-1} operand of the BatchNorm backward and the result move as coalesced 1 KiB wave accesses.
+struct TRing {
+  f32x4 x[XD];
+  f32x4 w[WD][8];
+};
+
+__device__ __forceinline__ void tring_fill(TRing& R, const f32x4* __restrict__ x4, const f32x4* __restrict__ w4) {
+#pragma unroll
+  for (int d = 0; d < XD; ++d) R.x[d] = x4[d * 64];
+#pragma unroll
+  for (int d = 0; d < WD; ++d)
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
+}
+
+__device__ __forceinline__ void gemm_t_mem(f32x16 (&acc)[8], TRing& R, const f32x4* __restrict__ x4,
+                                           const f32x4* __restrict__ x4_next, const f32x4* __restrict__ w4) {
+#pragma unroll
+  for (int kg = 0; kg < KG_H; ++kg) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob)
+        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(R.w[kg % WD][ob][q], R.x[kg % XD][q], acc[ob], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int gw = (kg + WD) % KG_H;
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) R.w[kg % WD][ob] = w4[(gw * 8 + ob) * 64];
+    R.x[kg % XD] = kg + XD < KG_H ? x4[(kg + XD) * 64] : x4_next[(kg + XD - KG_H) * 64];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_dgrad(
+    const float* __restrict__ gin, const float* __restrict__ Wt, const float* __restrict__ hprev, int64_t n,
+    const double* __restrict__ s12, const float* __restrict__ coefp, const float* __restrict__ gamma,
+    double* __restrict__ d_gamma, double* __restrict__ d_beta, float* __restrict__ gout) {
+  __shared__ __attribute__((aligned(16))) float cgm[256];
+  __shared__ __attribute__((aligned(16))) float ckk[256];
+  __shared__ __attribute__((aligned(16))) float cmu[256];
+  __shared__ __attribute__((aligned(16))) float cis[256];
+  __shared__ __attribute__((aligned(16))) float cga[256];
+  {
+    const int k = threadIdx.x;
+    const double S1 = s12[2 * k], dotp = s12[2 * k + 1];
+    const float invstd = coefp[256 + k];
+    cgm[k] = (float)(S1 / (double)n);
+    ckk[k] = (((float)dotp * invstd) * invstd) / (float)n;
+    cmu[k] = coefp[k];
+    cis[k] = invstd;
+    cga[k] = gamma[k];
+    if (blockIdx.x == 0) {
+      d_gamma[k] += dotp * (double)invstd;
+      d_beta[k] += S1;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, wv = threadIdx.x >> 6, li = lane & 31;
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t tstride = (int64_t)gridDim.x * 4;
+  const int64_t tile0 = (int64_t)blockIdx.x * 4 + wv;
+  const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wt) + lane;
+  TRing ring;
+  if (tile0 < ntiles) tring_fill(ring, reinterpret_cast<const f32x4*>(gin + tile0 * TILE_FLOATS) + lane, w4);
+  for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
+    int wofs = 0;
+    asm volatile("" : "+s"(wofs));
+    f32x16 acc[8];
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ob][r] = 0.0f;
+    const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
+    gemm_t_mem(acc, ring, reinterpret_cast<const f32x4*>(gin + tile * TILE_FLOATS) + lane,
+               reinterpret_cast<const f32x4*>(gin + nxt * TILE_FLOATS) + lane, w4 + wofs);
+    const bool valid = tile * 32 + li < n;
+    const f32x4* hp4 = reinterpret_cast<const f32x4*>(hprev + tile * TILE_FLOATS) + lane;
+    f32x4* go4 = reinterpret_cast<f32x4*>(gout + tile * TILE_FLOATS) + lane;
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {
+      f32x4 hx[4];
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) hx[gq] = hp4[(4 * ob + gq) * 64];
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int f0 = 32 * ob + 8 * gq + 4 * h;
+        f32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int f = f0 + q;
+          o[q] = valid ? ((acc[ob][4 * gq + q] - cgm[f]) - (hx[gq][q] - cmu[f]) * ckk[f]) * cis[f] * cga[f] : 0.0f;
+        }
+        go4[(4 * ob + gq) * 64] = o;
+      }
+    }
+  }
+}
+
+struct GradTable {
+  float* dst[34];
+  int64_t off[34];
+  int len[34];
+};
+
+__global__ void k_grad_emit(GradTable T, const double* __restrict__ acc) {
+  const int k = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (T.dst[k] && i < T.len[k]) T.dst[k][i] += (float)acc[T.off[k] + i];
+}
+
+struct GaccLayout {
+  int64_t w[8], b[8], g[8], be[8], wo, bo, total;
+};
+
+static GaccLayout gacc_layout() {
+  GaccLayout G;
+  int64_t o = 0;
+  for (int L = 0; L < 8; ++L) {
+    G.w[L] = o;
+    o += 256 * (int64_t)in_features(L);
+    G.b[L] = o;
+    o += 256;
+    G.g[L] = o;
+    o += 256;
+    G.be[L] = o;
+    o += 256;
+  }
+  G.wo = o;
+  o += 256;
+  G.bo = o;
+  o += 1;
+  G.total = o;
+  return G;
+}
+
+struct BwdWs {
+  float* h[8];
+  float* g[2];
+  float* wp;
+  float* wt;
+  double* stats;
+  float* coef;
+  float* part;
+  double* s12;
+  double* ostat;
+  double* gacc;
+  size_t bytes;
+};
+
+static BwdWs carve_bwd(void* base, int64_t chunk) {
+  const size_t tiles = (size_t)((chunk + 31) / 32);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  size_t oh[8], og[2];
+  for (int L = 0; L < 8; ++L) oh[L] = take(tiles * TILE_FLOATS * 4);
+  for (int i = 0; i < 2; ++i) og[i] = take(tiles * TILE_FLOATS * 4);
+  const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
+  const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4), os = take(512 * 8);
+  const size_t oo = take(257 * 8), oa = take((size_t)gacc_layout().total * 8);
+  char* b = (char*)base;
+  BwdWs w;
+  for (int L = 0; L < 8; ++L) w.h[L] = (float*)(b + oh[L]);
+  for (int i = 0; i < 2; ++i) w.g[i] = (float*)(b + og[i]);
+  w.wp = (float*)(b + ow);
+  w.wt = (float*)(b + ot);
+  w.stats = (double*)(b + ost);
+  w.coef = (float*)(b + oc);
+  w.part = (float*)(b + op);
+  w.s12 = (double*)(b + os);
+  w.ostat = (double*)(b + oo);
+  w.gacc = (double*)(b + oa);
+  w.bytes = off;
+  return w;
+}
+
+template <int MODE>
+static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
+                         int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
+                         const float* mu, float* part) {
+  static bool attr = false;
+  const size_t lds = WgradCfg<MODE>::LDS_BYTES;
+  if (!attr) {
+    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_wgrad<MODE>, dim3(blocks), dim3(512), lds, s, rays, stride, z, S, c0, n, ein, gin, hprev,
+                     mu, part);
+}
+
+}  // namespace pcn
+
+extern "C" size_t pcnerf_nof_backward_workspace_bytes(int64_t chunk) { return carve_bwd(nullptr, chunk).bytes; }
+
+static void backward_train(const float* rays, int ray_stride, const float* z, int n_samples, const float* ein,
+                           int64_t total, int64_t chunk, const pcnerf_nof_params* params, float eps,
+                           const float* grad, const float* p, void* workspace, size_t workspace_bytes,
+                           const pcnerf_nof_grads* grads, hipStream_t s) {
+  const BwdWs ws = carve_bwd(workspace, chunk);
+  PCN_CHECK(workspace_bytes >= ws.bytes, "pcnerf_nof_backward: workspace too small");
+  NofParamsDev P;
+  PCN_CHECK(to_dev_params(params, eps, &P), "pcnerf_nof_backward: null parameter pointer");
+  PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
+  const GaccLayout G = gacc_layout();
+  hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wp);
+  hipLaunchKernelGGL(k_pack_dgrad, dim3((unsigned)((DGRAD_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wt);
+  PCN_HIP(hipMemsetAsync(ws.gacc, 0, (size_t)G.total * 8, s));
+  const float mom = 0.0f;  // unused: the recomputation passes no running stats
+  for (int64_t c0 = 0; c0 < total; c0 += chunk) {
+    const int64_t n = total - c0 < chunk ? total - c0 : chunk;
+    const int64_t ntiles = (n + 31) / 32;
+    const double dn = (double)n;
+    const unsigned maxg = 256u * PCN_TRAIN_WAVES;
+    const unsigned grid = (unsigned)(ntiles / 4 + 1 < maxg ? ntiles / 4 + 1 : maxg);
+    const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
+    const unsigned wblocks = (unsigned)(ntiles < WG_BLOCKS ? ntiles : WG_BLOCKS);
+    PCN_HIP(hipMemsetAsync(ws.stats, 0, 8 * 512 * sizeof(double), s));
+    // 1. forward recomputation, every layer's raw h kept
+    {
+      const BnPrev none{};
+      ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
+      hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
+                         c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps,
+                         ws.h[0], ws.stats);
+    }
+    for (int L = 1; L < 8; ++L) {
+      const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], nullptr, nullptr, P.lin_b[L - 1], ws.stats + 512 * (L - 1)};
+      if (L == 4) {
+        ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
+        hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
+                           c0, n, ein, ws.h[3], ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps, ws.h[4],
+                           ws.stats + 512 * 4);
+      } else {
+        ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
+        hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
+                           n_samples, c0, n, ein, ws.h[L - 1], ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps,
+                           ws.h[L], ws.stats + 512 * L);
+      }
+    }
+    {
+      ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
+      hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, ws.stats, n, eps, ws.coef);
+      // 2. occ_out + BatchNorm 8
+      PCN_HIP(hipMemsetAsync(ws.ostat, 0, 257 * sizeof(double), s));
+      hipLaunchKernelGGL(k_out_bwd_stats, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, ws.h[7], n,
+                         ws.coef + 7 * 1024, ws.ostat);
+      hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, ws.h[7], n,
+                         ws.coef + 7 * 1024, P.bn_w[7], P.out_w, ws.ostat, ws.gacc + G.g[7], ws.gacc + G.be[7],
+                         ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0]);
+    }
+    // 3. layers 7..1
+    int cur = 0;
+    for (int L = 7; L >= 1; --L) {
+      const float* coefp = ws.coef + 1024 * (L - 1);
+      {
+        ProfScope ps(s, PT_BWD_WGRAD, 2.0 * 256.0 * (L == 4 ? 320 : 256) * dn, (L == 4 ? 2048.0 : 2048.0) * dn);
+        if (L == 4)
+          launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], ws.h[3], coefp, ws.part);
+        else
+          launch_wgrad<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], ws.h[L - 1], coefp,
+                          ws.part);
+      }
+      {
+        ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<0>::PART * 4.0);
+        PCN_HIP(hipMemsetAsync(ws.s12, 0, 512 * sizeof(double), s));
+        if (L == 4)
+          hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::C), 0, s, ws.part, (int)wblocks,
+                             P.lin_w[4], coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12);
+        else
+          hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::C), 0, s, ws.part, (int)wblocks,
+                             P.lin_w[L], coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12);
+      }
+      {
+        ProfScope ps(s, PT_BWD_DGRAD, 2.0 * 256 * 256 * dn, 3072.0 * dn);
+        hipLaunchKernelGGL(k_dgrad, dim3(grid), dim3(256), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
+                           ws.h[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
+                           ws.gacc + G.be[L - 1], ws.g[cur ^ 1]);
+      }
+      cur ^= 1;
+    }
+    // 4. layer 0 on the encoding
+    {
+      ProfScope ps(s, PT_BWD_WGRAD, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
+      launch_wgrad<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr, ws.part);
+    }
+    {
+      ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<1>::PART * 4.0);
+      hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::C), 0, s, ws.part, (int)wblocks,
+                         P.lin_w[0], (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr);
+    }
+  }
+  GradTable T;
+  int k = 0;
+  for (int L = 0; L < 8; ++L) {
+    T.dst[k] = grads->lin_w[L], T.off[k] = G.w[L], T.len[k++] = 256 * in_features(L);
+    T.dst[k] = grads->lin_b[L], T.off[k] = G.b[L], T.len[k++] = 256;
+    T.dst[k] = grads->bn_w[L], T.off[k] = G.g[L], T.len[k++] = 256;
+    T.dst[k] = grads->bn_b[L], T.off[k] = G.be[L], T.len[k++] = 256;
+  }
+  T.dst[k] = grads->out_w, T.off[k] = G.wo, T.len[k++] = 256;
+  T.dst[k] = grads->out_b, T.off[k] = G.bo, T.len[k++] = 1;
+  hipLaunchKernelGGL(k_grad_emit, dim3((256 * 319 + 255) / 256, 34), dim3(256), 0, s, T, ws.gacc);
+  PCN_LAUNCH_CHECK("pcnerf_nof_backward");
+}
+
+extern "C" int pcnerf_nof_query_train_backward(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                               int n_samples, int64_t chunk, const pcnerf_nof_params* params,
+                                               float eps, const float* grad_logit, void* workspace,
+                                               size_t workspace_bytes, const pcnerf_nof_grads* grads, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && grad_logit && workspace && grads, "pcnerf_nof_query_train_backward: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_backward: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_backward: ray_stride < 6");
+  backward_train(rays, ray_stride, z, n_samples, nullptr, n_rays * (int64_t)n_samples, chunk, params, eps,
+                 grad_logit, nullptr, workspace, workspace_bytes, grads, (hipStream_t)stream);
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_forward_train_backward(const float* emb, int64_t n, const pcnerf_nof_params* params,
+                                                 float eps, const float* p, const float* grad_p, void* workspace,
+                                                 size_t workspace_bytes, const pcnerf_nof_grads* grads,
+                                                 void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(emb && params && p && grad_p && workspace && grads, "pcnerf_nof_forward_train_backward: null argument");
+  PCN_CHECK(n > 0, "pcnerf_nof_forward_train_backward: empty input");
+  backward_train(nullptr, 0, nullptr, 1, emb, n, n, params, eps, grad_p, p, workspace, workspace_bytes, grads,
+                 (hipStream_t)stream);
   PCN_API_END
 }

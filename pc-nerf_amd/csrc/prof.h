@@ -14,6 +14,10 @@ enum ProfTag {
   PT_COMPOSITE = 6,    // k_composite
   PT_RESAMPLE = 7,     // k_resample
   PT_SAMPLE = 8,       // k_sample_coarse / k_perturb
+  PT_COMPOSITE_BWD = 9,// k_composite_bwd
+  PT_BWD_WGRAD = 10,   // k_wgrad: weight-gradient GEMM partials (sum over samples on MFMA)
+  PT_BWD_DGRAD = 11,   // k_dgrad: data-gradient GEMM + BatchNorm backward
+  PT_BWD_MISC = 12,    // output-layer backward, partial reduction, BN statistics
 };
 extern bool g_prof_on;
 class ProfScope {

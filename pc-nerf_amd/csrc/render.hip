@@ -472,6 +472,203 @@ __global__ void k_pointwise_loss(const float* __restrict__ a, const float* __res
   if (threadIdx.x == 0) out[0] = (float)s / (float)c;  // mean of an empty selection is nan, like torch
 }
 
+// d mean(loss(pred, target)) / d pred, scaled by the upstream scalar gradient; zero outside the mask
+// (torch's backward of index-select + mean: grad / count at the selected elements).
+__global__ void k_pointwise_loss_bwd(const float* __restrict__ a, const float* __restrict__ b,
+                                     const uint8_t* __restrict__ m, int64_t n, int kind,
+                                     const float* __restrict__ gout, float* __restrict__ ga) {
+  __shared__ double sh[16];
+  double c = 0.0;
+  if (m) {
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c += m[i] ? 1.0 : 0.0;
+    c = block_sum_d(c, sh);
+  } else {
+    c = (double)n;
+  }
+  const float scale = gout[0] / (float)c;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (m && !m[i]) {
+      ga[i] = 0.0f;
+      continue;
+    }
+    const float d = a[i] - b[i];
+    const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+    const float g = kind == 0 ? 2.0f * d : kind == 1 ? sg : (fabsf(d) < 1.0f ? d : sg);
+    ga[i] = g * scale;
+  }
+}
+
+
+// ------------------------------------------------------------------------------- compositing backward
+// Gradient of the compositing + child-loss terms (render.py:51-61, 75-159) with respect to the occupancy
+// logits, from the upstream gradients autograd hands the render step: dL/ddepth per ray and dL/d(free loss),
+// dL/d(child depth loss) as scalars.  One wave per ray, the forward values recomputed exactly as k_composite
+// does.  All backward arithmetic runs in float64 and rounds once, so the result is the exact derivative of the
+// fp32 forward up to that final rounding (torch's autograd rounds each backward op in fp32).
+//   w~_j = T_j p_j (+ noise),  W = sum w~ + eps,  w_j = w~_j / W,  depth = sum w_j z_j
+//   dL/dw~_j = (dL/dw_j - sum_k dL/dw_k w_k) / W
+//   dL/dp_j  = T_j (dL/dw~_j - U_j),  U_j = sum_{k>j} dL/dw~_k p_k prod_{j<i<k}(1-p_i)
+// U is the reverse affine recurrence U_{j-1} = g~_j p_j + (1-p_j) U_j (no division by 1-p, exact when
+// p saturates at 1): each lane composes the map over its block, a wave suffix scan composes the lanes.
+// Child terms: free = sum (w*!M0)^2 / R (or per child / count), depth loss c * mean SL1(10 dc, 10 range),
+// dc = sum_j w_j M2_j z_j / (sum w M2 + eps).
+template <int MAXB>
+__global__ __launch_bounds__(256) void k_composite_bwd(
+    const float* __restrict__ P, const float* __restrict__ Z, int64_t n_rays, int S, const float* __restrict__ noise,
+    float noise_std, float eps, const float* __restrict__ rays, int stride, int cn_col, int cf_col, int rg_col,
+    int cid_col, int n_child, const double* __restrict__ counts, const float* __restrict__ g_depth,
+    const float* __restrict__ g_free, const float* __restrict__ g_dl, float* __restrict__ g_logit,
+    int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ray >= n_rays) return;
+  const int B = (S + 63) / 64;
+  const int i0 = lane * B;
+  const int nb = max(0, min(B, S - i0));
+  const float* pr = P + ray * S + i0;
+  const float* zr = Z + ray * S + i0;
+  float pv[MAXB], zv[MAXB], wv[MAXB], tv[MAXB];
+  double loc = 1.0;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    if (j < nb) {
+      pv[j] = pr[j];
+      zv[j] = zr[j];
+      loc *= (double)(1.0f - pv[j]);
+    } else {
+      pv[j] = 0.0f;
+      zv[j] = 0.0f;
+    }
+  }
+  double T = wave_excl_prod(loc, lane);
+  double sw = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    tv[j] = 0.0f;
+    wv[j] = 0.0f;
+    if (j < nb) {
+      tv[j] = (float)T;
+      float w = tv[j] * pv[j];
+      if (noise) w = w + noise[ray * S + i0 + j] * noise_std;
+      wv[j] = w;
+      sw += (double)w;
+      T *= (double)(1.0f - pv[j]);
+    }
+  }
+  const float den = (float)wave_sum_d(sw) + eps;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j)
+    if (j < nb) wv[j] = wv[j] / den;
+
+  // dL/dw_j
+  const double gd = g_depth ? (double)g_depth[ray] : 0.0;
+  double gw[MAXB];
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) gw[j] = gd * (double)zv[j];
+  if (rays) {
+    const float* r = rays + ray * stride;
+    const float cn = r[cn_col], cf = r[cf_col], rg = r[rg_col];
+    double kf = 0.0, kd = 0.0;  // d loss / d (w_j^2 summand) and d loss / d dc
+    const double gf = g_free ? (double)g_free[0] : 0.0, gl = g_dl ? (double)g_dl[0] : 0.0;
+    if (n_child <= 0) {
+      kf = gf / (double)(float)n_rays;
+      kd = gl * (double)(float)((1.0 / (double)n_rays) * 0.1) / (double)(float)n_rays * 10.0;
+    } else {
+      const float c = r[cid_col];
+      const int k = (int)floorf(c - 0.5f);
+      if (k >= 0 && k < n_child && c > (float)k + 0.5f && c < (float)k + 1.5f && counts[k] >= 1.0) {
+        const float c32 = (float)counts[k];
+        kf = gf / (double)c32;
+        kd = gl * (double)((1.0f / c32) * 0.1f) / (double)c32 * 10.0;
+      }
+    }
+    float lo0, hi0, lo2, hi2;
+    expand_bounds<false, MAXB>(zv, nb, cn, cf, 0.0, lo0, hi0, err);
+    expand_bounds<false, MAXB>(zv, nb, cn, cf, 2.0, lo2, hi2, err);
+    double sc = 0.0;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+      if (j < nb) {
+        const bool m2 = lo2 <= zv[j] && zv[j] <= hi2;
+        sc += (double)(wv[j] * (m2 ? 1.0f : 0.0f));
+      }
+    }
+    const float denc = (float)wave_sum_d(sc) + eps;
+    double dcs = 0.0;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+      if (j < nb) {
+        const float m2 = (lo2 <= zv[j] && zv[j] <= hi2) ? 1.0f : 0.0f;
+        const float wc = (wv[j] * m2) / denc;
+        dcs += (double)(wc * (zv[j] * m2));
+      }
+    }
+    const float dc = (float)wave_sum_d(dcs);
+    const float x = 10.0f * dc - 10.0f * rg;
+    const double sl1g = fabsf(x) < 1.0f ? (double)x : (x > 0.0f ? 1.0 : -1.0);  // SmoothL1 (beta 1) derivative
+    const double gdc = kd * sl1g;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+      if (j < nb) {
+        const bool m0 = lo0 <= zv[j] && zv[j] <= hi0;
+        const bool m2 = lo2 <= zv[j] && zv[j] <= hi2;
+        if (!m0) gw[j] += 2.0 * kf * (double)wv[j];
+        if (m2) gw[j] += gdc * ((double)zv[j] - (double)dc) / (double)denc;
+      }
+    }
+  }
+  // normalisation backward
+  double dot = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j)
+    if (j < nb) dot += gw[j] * (double)wv[j];
+  dot = wave_sum_d(dot);
+  const double rden = 1.0 / (double)den;
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) gw[j] = (gw[j] - dot) * rden;  // now dL/dw~
+  // this lane's affine map U_{end} -> U_{i0 - 1}: U_{j-1} = a_j + b_j U_j
+  double A = 0.0, Bm = 1.0;
+#pragma unroll
+  for (int j = MAXB - 1; j >= 0; --j) {
+    if (j < nb) {
+      const double a = gw[j] * (double)pv[j], b = (double)(1.0f - pv[j]);
+      A = a + b * A;
+      Bm = b * Bm;
+    }
+  }
+  // suffix composition over lanes: Y_L = A_L + B_L * Y_{L+1}
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double An = __shfl_down(A, o, 64), Bn = __shfl_down(Bm, o, 64);
+    if (lane + o < 64) {
+      A = A + Bm * An;
+      Bm = Bm * Bn;
+    }
+  }
+  double U = __shfl_down(A, 1, 64);
+  if (lane == 63) U = 0.0;
+  float* go = g_logit + ray * S + i0;
+#pragma unroll
+  for (int j = MAXB - 1; j >= 0; --j) {
+    if (j < nb) {
+      const double gp = (double)tv[j] * (gw[j] - U);
+      U = gw[j] * (double)pv[j] + (double)(1.0f - pv[j]) * U;
+      go[j] = (float)(gp * (double)(1.0f - pv[j]) * (double)pv[j]);  // sigmoid backward
+    }
+  }
+}
+
+// rays per child id c in 1..N (the divide branch's sub_nerf_tmp.sum(), render.py:111-119)
+__global__ void k_child_counts(const float* __restrict__ cid, int stride, int64_t n, int N, double* __restrict__ acc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float c = cid[i * stride];
+  const int k = (int)floorf(c - 0.5f);
+  if (k < 0 || k >= N) return;
+  if (!(c > (float)k + 0.5f && c < (float)k + 1.5f)) return;
+  atomicAdd(acc + k, 1.0);
+}
+
 }  // namespace pcn
 
 using namespace pcn;
@@ -623,5 +820,57 @@ extern "C" int pcnerf_pointwise_loss(const float* pred, const float* target, con
   hipLaunchKernelGGL(k_pointwise_loss, dim3(1), dim3(1024), 0, (hipStream_t)stream, pred, target, mask, n, kind,
                      out);
   PCN_LAUNCH_CHECK("pcnerf_pointwise_loss");
+  PCN_API_END
+}
+
+extern "C" size_t pcnerf_composite_backward_workspace_bytes(int sub_nerf_test_num) {
+  return (size_t)(sub_nerf_test_num > 0 ? sub_nerf_test_num : 1) * sizeof(double);
+}
+
+extern "C" int pcnerf_composite_backward(const float* p, const float* z, int64_t n_rays, int n_samples,
+                                         const float* noise, float noise_std, float eps, const float* rays,
+                                         int ray_stride, int child_near_col, int child_far_col, int range_col,
+                                         int child_id_col, int sub_nerf_test_num, const float* grad_depth,
+                                         const float* grad_free_loss, const float* grad_depth_loss, void* workspace,
+                                         float* grad_logit, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(p && z && grad_logit, "pcnerf_composite_backward: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_composite_backward: empty input");
+  hipStream_t s = (hipStream_t)stream;
+  const double* counts = nullptr;
+  if (rays && sub_nerf_test_num > 0) {
+    PCN_CHECK(workspace, "pcnerf_composite_backward: divide branch needs a workspace");
+    PCN_HIP(hipMemsetAsync(workspace, 0, pcnerf_composite_backward_workspace_bytes(sub_nerf_test_num), s));
+    hipLaunchKernelGGL(k_child_counts, dim3(nblk(n_rays, 256)), dim3(256), 0, s, rays + child_id_col, ray_stride,
+                       n_rays, sub_nerf_test_num, (double*)workspace);
+    counts = (const double*)workspace;
+  }
+  const int B = (n_samples + 63) / 64;
+  const dim3 g(nblk(n_rays, 4)), b(256);
+  ProfScope ps(s, PT_COMPOSITE_BWD, 0.0, (double)n_rays * n_samples * (12.0 + (noise ? 4.0 : 0.0)));
+#define PCN_CB(MB)                                                                                           \
+  hipLaunchKernelGGL(k_composite_bwd<MB>, g, b, 0, s, p, z, n_rays, n_samples, noise, noise_std, eps, rays,  \
+                     ray_stride, child_near_col, child_far_col, range_col, child_id_col,                    \
+                     rays ? sub_nerf_test_num : 0, counts, grad_depth, grad_free_loss, grad_depth_loss,      \
+                     grad_logit, (int*)nullptr)
+  if (B <= 2) PCN_CB(2);
+  else if (B <= 6) PCN_CB(6);
+  else if (B <= 16) PCN_CB(16);
+  else if (B <= 64) PCN_CB(64);
+  else PCN_CHECK(false, "pcnerf_composite_backward: more than 4096 samples per ray");
+#undef PCN_CB
+  PCN_LAUNCH_CHECK("pcnerf_composite_backward");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_pointwise_loss_backward(const float* pred, const float* target, const uint8_t* mask, int64_t n,
+                                              int kind, const float* grad_out, float* grad_pred, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(pred && target && grad_out && grad_pred, "pcnerf_pointwise_loss_backward: null argument");
+  PCN_CHECK(n > 0, "pcnerf_pointwise_loss_backward: empty input");
+  PCN_CHECK(kind >= 0 && kind <= 2, "pcnerf_pointwise_loss_backward: kind must be 0, 1 or 2");
+  hipLaunchKernelGGL(k_pointwise_loss_bwd, dim3(1), dim3(1024), 0, (hipStream_t)stream, pred, target, mask, n, kind,
+                     grad_out, grad_pred);
+  PCN_LAUNCH_CHECK("pcnerf_pointwise_loss_backward");
   PCN_API_END
 }

@@ -29,6 +29,11 @@ class NofParams(ctypes.Structure):
                 ("bn_rv", vp * 8), ("out_w", vp), ("out_b", vp)]
 
 
+class NofGrads(ctypes.Structure):
+    _fields_ = [("lin_w", vp * 8), ("lin_b", vp * 8), ("bn_w", vp * 8), ("bn_b", vp * 8), ("out_w", vp),
+                ("out_b", vp)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "pcnerf_abi_version": (c_int, []),
@@ -49,6 +54,7 @@ _SIGS = {
     "pcnerf_child_loss_workspace_bytes": (c_size, [c_int]),
     "pcnerf_child_loss_reduce": (c_int, [vp, vp, i64, vp, c_int, c_int, vp, vp, vp]),
     "pcnerf_pointwise_loss": (c_int, [vp, vp, vp, i64, c_int, vp, vp]),
+    "pcnerf_pointwise_loss_backward": (c_int, [vp, vp, vp, i64, c_int, vp, vp, vp]),
     "pcnerf_embed": (c_int, [vp, i64, vp, vp]),
     "pcnerf_view_rows": (c_int, [vp, vp, i64, c_int, vp, c_int, c_int, c_int, c_int, c_float, vp, c_int, vp, vp, vp,
                                  vp, vp, vp, vp]),
@@ -63,6 +69,14 @@ _SIGS = {
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "pcnerf_nof_forward_eval": (c_int, [vp, i64, vp, vp, vp]),
     "pcnerf_nof_forward_train": (c_int, [vp, i64, ctypes.POINTER(NofParams), c_float, c_float, vp, c_size, vp, vp]),
+    "pcnerf_nof_backward_workspace_bytes": (c_size, [i64]),
+    "pcnerf_nof_query_train_backward": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams), c_float,
+                                                vp, vp, c_size, ctypes.POINTER(NofGrads), vp]),
+    "pcnerf_nof_forward_train_backward": (c_int, [vp, i64, ctypes.POINTER(NofParams), c_float, vp, vp, vp, c_size,
+                                                  ctypes.POINTER(NofGrads), vp]),
+    "pcnerf_composite_backward_workspace_bytes": (c_size, [c_int]),
+    "pcnerf_composite_backward": (c_int, [vp, vp, i64, c_int, vp, c_float, c_float, vp, c_int, c_int, c_int, c_int,
+                                          c_int, c_int, vp, vp, vp, vp, vp, vp]),
 }
 
 

@@ -291,6 +291,26 @@ def view_walk(other, at_peak, child_sum, opac_row, n_samples: int):
 _KIND = {"mse": 0, "l1": 1, "smoothl1": 2}
 
 
+def _loss_mask(pred, valid_mask):
+    if valid_mask is None:
+        return None
+    H.require_device(valid_mask)
+    m = valid_mask.to(torch.uint8).contiguous()
+    if m.numel() != pred.numel():
+        raise RuntimeError("valid_mask must match the loss inputs")
+    return m
+
+
+def pointwise_loss_backward(pred, target, kind: str, valid_mask, grad_out) -> torch.Tensor:
+    pred, target = _f32(pred), _f32(target)
+    m = _loss_mask(pred, valid_mask)
+    g = torch.empty_like(pred)
+    H.check(H.lib().pcnerf_pointwise_loss_backward(pred.data_ptr(), target.data_ptr(), H.ptr(m), pred.numel(),
+                                                   _KIND[kind], _f32(grad_out).data_ptr(), g.data_ptr(),
+                                                   _stream(pred)))
+    return g
+
+
 def pointwise_loss(pred, target, kind: str, valid_mask=None) -> torch.Tensor:
     pred, target = _f32(pred), _f32(target)
     if pred.shape != target.shape:
@@ -304,4 +324,80 @@ def pointwise_loss(pred, target, kind: str, valid_mask=None) -> torch.Tensor:
     out = torch.empty((), dtype=torch.float32, device=pred.device)
     H.check(H.lib().pcnerf_pointwise_loss(pred.data_ptr(), target.data_ptr(), H.ptr(m), pred.numel(), _KIND[kind],
                                           out.data_ptr(), _stream(pred)))
+    return out
+
+
+# ----------------------------------------------------------------------------------------------- backward
+def grad_params(model) -> list:
+    """The 34 trainable tensors of a NOF in pcnerf_nof_grads order (lin_w, lin_b, bn_w, bn_b, out_w, out_b)."""
+    lins, norms = model.linears(), model.norms()
+    return ([l.weight for l in lins] + [l.bias for l in lins] + [b.weight for b in norms] + [b.bias for b in norms]
+            + [model.occ_out[0].weight, model.occ_out[0].bias])
+
+
+def _grads_struct(model, device):
+    out = [torch.zeros_like(t, device=device) for t in grad_params(model)]
+    s = H.NofGrads()
+    for i in range(8):
+        s.lin_w[i] = out[i].data_ptr()
+        s.lin_b[i] = out[8 + i].data_ptr()
+        s.bn_w[i] = out[16 + i].data_ptr()
+        s.bn_b[i] = out[24 + i].data_ptr()
+    s.out_w = out[32].data_ptr()
+    s.out_b = out[33].data_ptr()
+    return s, out
+
+
+def _opt_scalar(g):
+    if g is None:
+        return None
+    g = _f32(g)
+    if g.numel() != 1:
+        raise RuntimeError("loss gradients must be scalars")
+    return g
+
+
+def composite_backward(p, z, noise, noise_std, eps, rays, sub_nerf_test_num, g_depth, g_free, g_dl,
+                       cn_col=10, cf_col=11, range_col=14, cid_col=9) -> torch.Tensor:
+    """dL/dlogit (R, S) of the compositing + child-loss terms (pcnerf_composite_backward)."""
+    L = H.lib()
+    R, S = z.shape
+    out = torch.empty((R, S), dtype=torch.float32, device=z.device)
+    gd = None if g_depth is None else _f32(g_depth).reshape(-1)
+    if gd is not None and gd.numel() != R:
+        raise RuntimeError("depth gradient must have one entry per ray")
+    n = int(sub_nerf_test_num) if rays is not None else 0
+    ws = _workspace(z.device, L.pcnerf_composite_backward_workspace_bytes(n)) if n > 0 else None
+    H.check(L.pcnerf_composite_backward(p.data_ptr(), z.data_ptr(), R, S, H.ptr(noise), float(noise_std), float(eps),
+                                        H.ptr(rays), rays.shape[1] if rays is not None else 0, cn_col, cf_col,
+                                        range_col, cid_col, n, H.ptr(gd), H.ptr(_opt_scalar(g_free)),
+                                        H.ptr(_opt_scalar(g_dl)), H.ptr(ws), out.data_ptr(), _stream(z)))
+    return out
+
+
+def nof_query_backward(model, rays, z, chunk: int, g_logit) -> list:
+    """Parameter gradients (grad_params order) of the train-mode query given dL/dlogit per sample."""
+    L = H.lib()
+    R, S = z.shape
+    _, eps = _bn_config(model)
+    s, keep = _params(model)
+    gs, out = _grads_struct(model, z.device)
+    ws = _workspace(z.device, L.pcnerf_nof_backward_workspace_bytes(int(chunk)))
+    H.check(L.pcnerf_nof_query_train_backward(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                              ctypes.byref(s), eps, _f32(g_logit).data_ptr(), ws.data_ptr(),
+                                              ws.numel(), ctypes.byref(gs), _stream(z)))
+    return out
+
+
+def nof_forward_backward(model, x, p, g_p) -> list:
+    """Parameter gradients of NOF.forward(x) (train mode, one batch) given dL/dp."""
+    L = H.lib()
+    B = x.shape[0]
+    _, eps = _bn_config(model)
+    s, keep = _params(model)
+    gs, out = _grads_struct(model, x.device)
+    ws = _workspace(x.device, L.pcnerf_nof_backward_workspace_bytes(B))
+    H.check(L.pcnerf_nof_forward_train_backward(x.data_ptr(), B, ctypes.byref(s), eps, _f32(p).data_ptr(),
+                                                _f32(g_p).data_ptr(), ws.data_ptr(), ws.numel(), ctypes.byref(gs),
+                                                _stream(x)))
     return out

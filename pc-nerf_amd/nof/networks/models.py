@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .. import _ops
+from .. import _autograd, _ops
 
 
 class Embedding(nn.Module):
@@ -81,6 +81,9 @@ class _NOFBase(nn.Module):
         """x: (B, 63) embedded positions -> (B, 1) occupancy probability (models.py:183-203)."""
         if not self.supported():
             raise NotImplementedError("HIP NOF kernels support feature_size=256, in_channels_xy=63, use_skip=True")
+        if _autograd.needs_grad(self):
+            _autograd.check_trainable(self)
+            return _autograd.NofForward.apply(self, x, *_ops.grad_params(self))
         return _ops.nof_forward_embedded(self, x)
 
 

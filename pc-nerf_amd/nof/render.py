@@ -15,15 +15,17 @@ Differences from the reference, all deliberate:
   * RNG: draws are taken from torch's generator on the device, and only when used (the reference also draws
     ``randn`` noise when ``noise_std == 0``).  Parity tests inject the draws with the keyword-only ``rng``
     dict: ``perturb_rand`` (R,S), ``noise`` (R,S), ``u`` (R,I), ``noise_fine`` (R,S+I);
-  * gradients: this round ships the forward path; calling with autograd enabled on parameters that require
-    grad raises (run under ``torch.no_grad()``).
+  * gradients: ``render_rays_train`` is differentiable (train-mode networks): with autograd enabled and
+    parameters requiring grad, each pass runs as ``nof._autograd.TrainPass`` whose backward is the HIP
+    compositing backward + the NOF backward (chunks recomputed), so ``loss.backward()`` of train_kitti.py:155
+    fills ``.grad`` of both networks.  The inference renderers stay forward-only (they raise under autograd).
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
 
-from . import _ops
+from . import _autograd, _ops
 from .networks import NOF, Embedding, NOF_coarse, NOF_fine, NOF_plusfine  # noqa: F401  (reference exports)
 
 __all__ = ['render_rays']
@@ -31,7 +33,7 @@ __all__ = ['render_rays']
 EPSILON = 1e-10  # render.py:456, :514, :656
 
 
-def _check_inputs(model, model_fine, embedding_xy, rays, n_cols):
+def _check_inputs(model, model_fine, embedding_xy, rays, n_cols, differentiable=False):
     if not rays.is_cuda:
         raise RuntimeError("nof.render (HIP) renders device-resident rays; move them with rays.to('cuda') -- there "
                            "is no CPU path")
@@ -42,9 +44,11 @@ def _check_inputs(model, model_fine, embedding_xy, rays, n_cols):
     for m in (model, model_fine):
         if not m.supported():
             raise NotImplementedError("HIP render supports NOF(feature_size=256, in_channels_xy=63, use_skip=True)")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in m.parameters()):
-            raise NotImplementedError("the HIP render path is forward-only in this release; call it under "
-                                      "torch.no_grad()")
+        if _autograd.needs_grad(m):
+            if not differentiable:
+                raise NotImplementedError("this HIP renderer is forward-only (inference); call it under "
+                                          "torch.no_grad()")
+            _autograd.check_trainable(m)
     return rays.float().contiguous()
 
 
@@ -85,12 +89,20 @@ def render_rays_train(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays
                       use_child_nerf_loss=0, *, rng=None):
     """render.py:416-482 -> {'child_free_loss_fine', 'child_depth_loss_fine', 'depth_fine', 'child_free_loss',
     'child_depth_loss', 'depth'}."""
-    rays = _check_inputs(model, model_fine, embedding_xy, rays, 15)
+    rays = _check_inputs(model, model_fine, embedding_xy, rays, 15, differentiable=True)
     R = rays.shape[0]
     z = _coarse(rays, N_samples, issegmentated, childnerf_ratio, perturb, rng)
     with_losses = use_child_nerf_loss == 1
 
     def one_pass(m, z, noise_key):
+        if _autograd.needs_grad(m):
+            noise = _noise(rng, noise_key, z, noise_std)
+            sub = int(sub_nerf_test_num) if use_child_nerf_divide == 1 else 0
+            w, depth, free, dl = _autograd.TrainPass.apply(m, rays, z, noise, float(noise_std), EPSILON, int(chunk),
+                                                           with_losses, sub, *_ops.grad_params(m))
+            if not with_losses:
+                free, dl = torch.tensor(0.0), torch.tensor(0.0)
+            return w, depth, free, dl
         p = _ops.query(m, rays, z, chunk)
         w, depth, fr, sl = _ops.composite(p, z, _noise(rng, noise_key, z, noise_std), noise_std, EPSILON,
                                           rays if with_losses else None)

@@ -1,0 +1,180 @@
+"""Training gradients (loss.backward() of train_kitti.py:117-155) through the HIP backward kernels.
+
+Pinned two ways:
+  * against the reference itself: tests/golden/grads_*.npz hold the parameter gradients the reference's
+    render_rays_train + range/child losses produce on CPU (three loss configurations, several BN chunks);
+  * against the CPU oracle's torch autograd on larger cases (perturbation and noise draws injected, a ragged
+    last chunk whose tail tile is padded).
+Tolerance: gradients of the weight matrices and the non-degenerate vectors within rtol 2e-4 of the tensor's
+largest entry (GPU and CPU sum ~10^4-10^5 terms per entry in different orders); the mathematically-zero
+gradients (Linear biases before BN, BN shifts before Linear->BN) only at noise level (gradcheck.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from gradcheck import check_grads
+from nof import synthetic as syn
+from nof.criteria import nof_loss
+from nof.networks import Embedding, NOF_coarse, NOF_fine
+from nof import render as R
+from oracle import ref_cpu as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SEED_C, SEED_F = 1234, 5678
+GRTOL = 2e-4
+NOISE = 1e-4
+
+
+def models():
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(SEED_C)).to(DEV).train(True)
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(SEED_F)).to(DEV).train(True)
+    return Embedding(3, 10), mc, mf
+
+
+def range_losses(depth, depth_f, gt, rays, divide, sub_num):
+    """train_kitti.py:121-146 with this package's criteria (differentiable HIP SmoothL1)."""
+    loss = nof_loss["smoothl1"]()
+    if not divide:
+        return 1e-1 * loss(1e1 * depth, 1e1 * gt), 1e-1 * loss(1e1 * depth_f, 1e1 * gt)
+    lr = lrf = 0
+    sub = rays[:, 9]
+    for i in range(sub_num):
+        m = torch.logical_and(sub > (i + 0.5), sub < (i + 1.5))
+        if m.sum() >= 1:
+            lr = lr + 1e-1 * loss(1e1 * depth[m], 1e1 * gt[m])
+            lrf = lrf + 1e-1 * loss(1e1 * depth_f[m], 1e1 * gt[m])
+    return lr, lrf
+
+
+def total(res, lr, lrf):
+    return (lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"]
+            + 1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"])
+
+
+def named(m):
+    return dict(m.named_parameters())
+
+
+@pytest.mark.parametrize("name", ["pcnerf", "divide", "original"])
+def test_train_grads_vs_reference(name):
+    g = golden(f"grads_{name}")
+    emb, mc, mf = models()
+    rays = torch.from_numpy(g["rays"]).to(DEV)
+    div = int(g["use_child_nerf_divide"])
+    res = R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=32, N_samples=64, N_importance=128, perturb=0,
+                              noise_std=0, chunk=4096, issegmentated=int(g["issegmentated"]), childnerf_ratio=0.1,
+                              use_child_nerf_divide=div, use_child_nerf_loss=int(g["use_child_nerf_loss"]))
+    lr, lrf = range_losses(res["depth"], res["depth_fine"], rays[:, 14], rays, div, 32)
+    tot = total(res, lr, lrf)
+    np.testing.assert_allclose(float(tot.detach().sum()), float(g["loss_total"].sum()), rtol=1e-4)
+    tot.sum().backward()
+    pc, pf = named(mc), named(mf)
+    check_grads(lambda k: pc[k].grad.cpu().numpy(), list(pc), g, "c:", GRTOL, NOISE)
+    check_grads(lambda k: pf[k].grad.cpu().numpy(), list(pf), g, "f:", GRTOL, NOISE)
+
+
+def oracle_params(seed):
+    P = O.params_from_numpy(syn.init_nof_params(seed))
+    for k in P:
+        if k.endswith(".weight") or k.endswith(".bias"):
+            P[k].requires_grad_(True)
+    return P
+
+
+def oracle_summary(P, seed):
+    """Same layout as the golden files, from oracle autograd."""
+    out = {}
+    rng = np.random.default_rng(seed)
+    for k, t in P.items():
+        if not (k.endswith(".weight") or k.endswith(".bias")):
+            continue
+        gr = t.grad.numpy()
+        if gr.size <= 512:
+            out[k] = gr
+        else:
+            idx = rng.choice(gr.size, size=2048, replace=False)
+            out[k + "@idx"], out[k + "@val"] = idx, gr.reshape(-1)[idx]
+            out[k + "@norm"] = np.linalg.norm(gr.astype(np.float64))
+    return out
+
+
+@pytest.mark.parametrize("divide,noise_std", [(0, 0.0), (1, 1e-3)])
+def test_train_grads_vs_oracle_ragged_chunks_with_draws(divide, noise_std):
+    """512 rays, 64 + 128 samples, chunk 30000 (the fine pass's last chunk is 8304 samples: a padded tail tile),
+    stratified perturbation and importance draws (the reference's training runs perturb=1, noise_std=0,
+    logs/*/hparams.yaml) plus a small weight noise, injected identically into both paths.  (Noise of the order
+    of the weights themselves makes sum(w) + eps arbitrarily small and the gradient ill-conditioned.)"""
+    torch.manual_seed(3)
+    R_, S, I = 512, 64, 128
+    rays_np = syn.make_rays(R_, seed=17)
+    draws = {"perturb_rand": torch.rand(R_, S), "noise": torch.randn(R_, S), "u": torch.rand(R_, I),
+             "noise_fine": torch.randn(R_, S + I)}
+    kw = dict(sub_nerf_test_num=16, N_samples=S, N_importance=I, perturb=1.0, noise_std=noise_std, chunk=30000,
+              issegmentated=1, childnerf_ratio=0.2, use_child_nerf_divide=divide, use_child_nerf_loss=1)
+    Pc, Pf = oracle_params(SEED_C), oracle_params(SEED_F)
+    rays_c = torch.from_numpy(rays_np)
+    ro = O.render_rays_train(Pc, Pf, rays_c, draws=draws, **kw)
+    lr, lrf = O.range_losses(ro["depth"], ro["depth_fine"], rays_c[:, 14], rays_c, divide, 16)
+    O.total_loss(ro, lr, lrf).sum().backward()
+    gc, gf = oracle_summary(Pc, 5), oracle_summary(Pf, 6)
+
+    emb, mc, mf = models()
+    rays = torch.from_numpy(rays_np).to(DEV)
+    res = R.render_rays_train(mc, mf, emb, rays, rng={k: v.to(DEV) for k, v in draws.items()}, **kw)
+    lr, lrf = range_losses(res["depth"], res["depth_fine"], rays[:, 14], rays, divide, 16)
+    total(res, lr, lrf).sum().backward()
+    pc, pf = named(mc), named(mf)
+    check_grads(lambda k: pc[k].grad.cpu().numpy(), list(pc), gc, "", GRTOL, NOISE)
+    check_grads(lambda k: pf[k].grad.cpu().numpy(), list(pf), gf, "", GRTOL, NOISE)
+
+
+def test_nof_forward_backward_embedded():
+    """NOF.forward on an embedded batch (one BN batch of 1000 rows, not a multiple of 32) under autograd."""
+    torch.manual_seed(5)
+    x = torch.rand(1000, 3) * 20 - 10
+    e = O.embed(x)
+    wgt = torch.randn(1000, 1)
+    P = oracle_params(SEED_C)
+    (O.nof_forward(P, e, True).reshape(-1, 1) * wgt).sum().backward()
+    ref = oracle_summary(P, 9)
+    _, mc, _ = models()
+    p = mc(e.to(DEV))
+    (p * wgt.to(DEV)).sum().backward()
+    pc = named(mc)
+    check_grads(lambda k: pc[k].grad.cpu().numpy(), list(pc), ref, "", GRTOL, NOISE)
+
+
+@pytest.mark.parametrize("kind", ["mse", "l1", "smoothl1"])
+def test_criteria_backward(kind):
+    torch.manual_seed(1)
+    a = torch.randn(777) * 2
+    b = torch.randn(777) * 2
+    m = torch.rand(777) > 0.3
+    fn = {"mse": torch.nn.MSELoss(), "l1": torch.nn.L1Loss(), "smoothl1": torch.nn.SmoothL1Loss()}[kind]
+    ac = a.clone().requires_grad_(True)
+    (3.0 * fn(ac[m], b[m])).backward()
+    ad = a.to(DEV).requires_grad_(True)
+    (3.0 * nof_loss[kind]()(ad, b.to(DEV), m.to(DEV))).backward()
+    np.testing.assert_allclose(ad.grad.cpu().numpy(), ac.grad.numpy(), rtol=1e-6, atol=1e-8)
+
+
+def test_grad_accumulates_and_running_stats_once():
+    """Two backward calls add into .grad (torch semantics); the recomputation leaves running stats alone."""
+    g = golden("grads_original")
+    emb, mc, mf = models()
+    rays = torch.from_numpy(g["rays"]).to(DEV)
+    kw = dict(N_samples=64, N_importance=128, perturb=0, noise_std=0, chunk=4096)
+    outs = []
+    for _ in range(2):
+        res = R.render_rays_train(mc, mf, emb, rays, **kw)
+        outs.append([bn.running_mean.clone() for bn in mc.norms()])
+        (res["depth"].sum() + res["depth_fine"].sum()).backward()
+        after = [bn.running_mean.clone() for bn in mc.norms()]
+        assert all(torch.equal(x, y) for x, y in zip(outs[-1], after))
+        if _ == 0:
+            first = mc.layer2[6].weight.grad.clone()
+    np.testing.assert_allclose(mc.layer2[6].weight.grad.cpu().numpy(), 2 * first.cpu().numpy(), rtol=1e-5,
+                               atol=1e-6 * float(first.abs().max()))
