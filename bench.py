@@ -1,10 +1,14 @@
 """Benchmark: LiDAR rays/s (render + loss) at 128 samples/ray on MI355X -- BASELINE.json config 2.
 
-One step = the reference training step's forward on one batch (train_kitti.py:117-155 without backward):
+Default (--mode train_fwd): one step = the reference training step's forward on one batch
+(train_kitti.py:117-155 without backward):
 ``render_rays_train`` (train-mode BatchNorm over 262,144-sample chunks, segmented sampling ratio 0.1, child
 free/depth losses, perturb 1, noise_std 0) over 65,536 synthetic rays of one parent block with 32 child AABBs at
 N_samples=128 / N_importance=256 (512 MLP samples per ray), plus the SmoothL1 range losses and the weighted total
 loss.  Inputs are resident in HBM before timing starts.
+--mode train_step adds what Lightning does with that loss: loss.backward() through the HIP backward kernels and
+the reference's optimizer step (Adam lr 5e-4, eps 1e-8, weight_decay 1e-3 over both networks, nof_utils.py:162-173)
+-- the end-to-end training iteration of config 3 on config 2's batch.  --mode val: render_rays_val (eval BN).
 
 Multi-GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``): one process per GPU, each
 rank renders its own parent block (own rays, own NOF weights) -- weak scaling with no collective
@@ -42,8 +46,9 @@ def parse():
     ap.add_argument("--samples", type=int, default=128)
     ap.add_argument("--importance", type=int, default=256)
     ap.add_argument("--chunk", type=int, default=262144)
-    ap.add_argument("--mode", choices=["train_fwd", "val"], default="train_fwd")
-    ap.add_argument("--cpu-rays", type=int, default=4096, help="bounded CPU-baseline sample (rays)")
+    ap.add_argument("--mode", choices=["train_fwd", "train_step", "val"], default="train_fwd")
+    ap.add_argument("--cpu-rays", type=int, default=None,
+                    help="bounded CPU-baseline sample (rays; default 4096, 1024 for train_step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="gather every rank's depth_fine to rank 0 inside each step (eval-driver output path)")
@@ -90,14 +95,21 @@ def main():
     # this rank's parent block (one per GPU): its own child layout, rays and coarse/fine weights
     (block,) = blocks_of_rank(rank, world, world)
     rays = torch.from_numpy(syn.make_rays(a.rays, n_children=32, seed=1000 * block)).to(dev)
-    train = a.mode == "train_fwd"
+    train = a.mode in ("train_fwd", "train_step")
+    grad = a.mode == "train_step"
     mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234 + block)).to(dev).train(train)
     mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678 + block)).to(dev).train(train)
     emb = Embedding(3, 10)
     loss_fn = nof_loss["smoothl1"]()
     gt = rays[:, 14].contiguous()
+    opt = None
+    if grad:
+        params = list(mc.parameters()) + list(mf.parameters())
+        opt = torch.optim.Adam(params, lr=5e-4, eps=1e-8, weight_decay=1e-3)   # nof_utils.py:167-169
 
     def step():
+        if grad:
+            opt.zero_grad(set_to_none=True)
         if train:
             res = render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=32, N_samples=a.samples,
                                     N_importance=a.importance, perturb=1, noise_std=0, chunk=a.chunk,
@@ -113,10 +125,13 @@ def main():
             loss = 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
         if a.gather:
             gather_rows(res["depth_fine"][:, None], dst=0)
-        return loss
+        if grad:
+            loss.backward()
+            opt.step()
+        return loss.detach()
 
     L = _hip.lib()
-    with torch.no_grad():
+    with (torch.enable_grad() if grad else torch.no_grad()):
         for _ in range(a.warmup):
             loss = step()
         torch.cuda.synchronize(dev)
@@ -136,13 +151,17 @@ def main():
         raise RuntimeError(f"non-finite loss {loss_val}")
     elapsed = max_over_ranks(elapsed, device=dev)
 
-    # dominant kernel: the 256 -> 256 pre-BN Linear of train mode (6 of 9 GEMMs per chunk), or the fused eval query
-    tag = 1 if train else 0
-    kname = "k_train_layer<false,true>" if train else "k_nof_eval"
+    # dominant kernel: the MFMA kernel with the most time per step -- the 256 -> 256 pre-BN Linear of train mode
+    # (6 of 9 GEMMs per chunk, also run by the backward's recomputation), or the fused eval query
+    knames = {0: "k_nof_eval", 1: "k_train_layer<false,true>", 2: "k_train_layer<true,false>",
+              3: "k_train_layer<true,true>", 10: "k_wgrad", 11: "k_dgrad"}
+    tag = max(knames, key=lambda t: prof_read(L, t)[0])
+    kname = knames[tag]
     ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)
     kernels = {}
     for t, nm in ((0, "eval_query"), (1, "train_hidden"), (2, "train_first"), (3, "train_skip"), (4, "train_out"),
-                  (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample")):
+                  (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
+                  (10, "wgrad"), (11, "dgrad"), (12, "bwd_other")):
         tm, n, f, b = prof_read(L, t)
         if n:
             kernels[nm] = {"ms_per_step": round(tm / a.steps, 3), "launches_per_step": n // a.steps,
@@ -156,6 +175,8 @@ def main():
 
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
+        if a.cpu_rays is None:
+            a.cpu_rays = 1024 if grad else 4096
         cpu = cpu_baseline(a, syn)
 
     if rank != 0:
@@ -177,7 +198,9 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)",
-        "config": {"workload": "render_rays_train fwd + range/child losses" if train else "render_rays_val fwd",
+        "config": {"workload": {"train_fwd": "render_rays_train fwd + range/child losses",
+                                "train_step": "render_rays_train fwd + losses + backward + Adam step",
+                                "val": "render_rays_val fwd"}[a.mode],
                    "rays_per_gpu": a.rays, "N_samples": a.samples, "N_importance": a.importance,
                    "mlp_samples_per_ray": a.samples + a.samples + a.importance, "chunk": a.chunk,
                    "batchnorm": "train (batch stats per chunk)" if train else "eval (folded)",
@@ -205,7 +228,15 @@ def cpu_baseline(a, syn):
     rays = torch.from_numpy(syn.make_rays(a.cpu_rays, n_children=32, seed=0))
     Pc = O.params_from_numpy(syn.init_nof_params(1234))
     Pf = O.params_from_numpy(syn.init_nof_params(5678))
-    train = a.mode == "train_fwd"
+    train = a.mode in ("train_fwd", "train_step")
+    grad = a.mode == "train_step"
+    leaves = []
+    if grad:
+        for P in (Pc, Pf):
+            for k in P:
+                if k.endswith(".weight") or k.endswith(".bias"):
+                    leaves.append(P[k].requires_grad_(True))
+        opt = torch.optim.Adam(leaves, lr=5e-4, eps=1e-8, weight_decay=1e-3)
 
     def run(r):
         if train:
@@ -213,12 +244,17 @@ def cpu_baseline(a, syn):
                                       perturb=1, noise_std=0, chunk=a.chunk, issegmentated=1, childnerf_ratio=0.1,
                                       use_child_nerf_loss=1, training=True)
             lr, lrf = O.range_losses(res["depth"], res["depth_fine"], r[:, 14])
-            return O.total_loss(res, lr, lrf)
+            loss = O.total_loss(res, lr, lrf)
+            if grad:
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+            return loss
         res = O.render_rays_val(Pc, Pf, r, N_samples=a.samples, N_importance=a.importance, perturb=0, noise_std=0,
                                 chunk=a.chunk)
         return res["depth_fine"].sum()
 
-    with torch.no_grad():
+    with (torch.enable_grad() if grad else torch.no_grad()):
         run(rays[:64])  # warm-up
         t0 = time.perf_counter()
         run(rays)

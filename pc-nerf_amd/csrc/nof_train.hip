@@ -499,48 +499,56 @@ __device__ __forceinline__ float logit_grad(const float* __restrict__ g, const f
   return g[i] * (1.0f - pv) * pv;  // sigmoid backward
 }
 
-// acc[f] += sum_s g_s (h7[s][f] - mean7[f]), acc[256] += sum_s g_s.  Each lane accumulates its 128 features over
-// its tiles; one LDS transpose-reduction per block at the end.
+// acc[f] += sum_s g_s (h7[s][f] - mean7[f]), acc[256] += sum_s g_s.  Four passes over quarters of the feature
+// groups (32 accumulators per lane over its tiles), each followed by an LDS transpose-reduction across lanes.
 __global__ __launch_bounds__(256) void k_out_bwd_stats(const float* __restrict__ g, const float* __restrict__ pin,
                                                        const float* __restrict__ h7, int64_t n,
                                                        const float* __restrict__ coef7, double* __restrict__ acc) {
-  __shared__ float red[64 * 129];
+  __shared__ float red[4][64 * 33];
   __shared__ __attribute__((aligned(16))) float mu[256];
   const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31, wv = t >> 6;
   mu[t] = coef7[t];
   __syncthreads();
-  float a[128];
-#pragma unroll
-  for (int i = 0; i < 128; ++i) a[i] = 0.0f;
-  float gs = 0.0f;
   const int64_t ntiles = (n + 31) / 32;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wv; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+  const int64_t t0 = (int64_t)blockIdx.x * 4 + wv, ts = (int64_t)gridDim.x * 4;
+  float gs = 0.0f;
+  for (int64_t tile = t0; tile < ntiles; tile += ts) {
     const int64_t s = tile * 32 + li;
-    const float gv = s < n ? logit_grad(g, pin, s) : 0.0f;
-    if (h == 0) gs += gv;
-    const f32x4* x4 = reinterpret_cast<const f32x4*>(h7 + tile * TILE_FLOATS) + lane;
-#pragma unroll
-    for (int gq = 0; gq < 32; ++gq) {
-      const f32x4 x = x4[gq * 64];
-      const f32x4 m = *reinterpret_cast<const f32x4*>(mu + 8 * gq + 4 * h);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[4 * gq + q] += gv * (x[q] - m[q]);
-    }
+    if (h == 0 && s < n) gs += logit_grad(g, pin, s);
   }
-  const int hb = (t >> 2) & 1, idx = (t >> 3) * 4 + (t & 3);
-  double tot = 0.0;
-  for (int w = 0; w < 4; ++w) {
-    __syncthreads();
-    if (wv == w) {
+  // thread t reduces feature f = 64*pass + (t & 63) over the 32 lanes of its half, one wave-slice per t>>6
+  for (int pass = 0; pass < 4; ++pass) {
+    float a[32];
 #pragma unroll
-      for (int i = 0; i < 128; ++i) red[lane * 129 + i] = a[i];
+    for (int i = 0; i < 32; ++i) a[i] = 0.0f;
+    for (int64_t tile = t0; tile < ntiles; tile += ts) {
+      const int64_t s = tile * 32 + li;
+      const float gv = s < n ? logit_grad(g, pin, s) : 0.0f;
+      const f32x4* x4 = reinterpret_cast<const f32x4*>(h7 + tile * TILE_FLOATS) + 8 * pass * 64 + lane;
+#pragma unroll
+      for (int gq = 0; gq < 8; ++gq) {
+        const f32x4 x = x4[gq * 64];
+        const f32x4 m = *reinterpret_cast<const f32x4*>(mu + 8 * (8 * pass + gq) + 4 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[4 * gq + q] += gv * (x[q] - m[q]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) red[wv][lane * 33 + i] = a[i];
+    __syncthreads();
+    if (t < 64) {
+      const int f = 64 * pass + t;  // feature within this pass: group gq = (f>>3)&7, half (f>>2)&1, q = f&3
+      const int fl = f - 64 * pass, hb = (fl >> 2) & 1, idx = (fl >> 3) * 4 + (fl & 3);
+      double tot = 0.0;
+      for (int w = 0; w < 4; ++w) {
+        float sw = 0.0f;
+        for (int l = 0; l < 32; ++l) sw += red[w][(l + 32 * hb) * 33 + idx];
+        tot += (double)sw;
+      }
+      atomicAdd(&acc[f], tot);
     }
     __syncthreads();
-    float s = 0.0f;
-    for (int l = 0; l < 32; ++l) s += red[(l + 32 * hb) * 129 + idx];
-    tot += (double)s;
   }
-  atomicAdd(&acc[t], tot);
   gs = wave_sum_f(gs);
   if (lane == 0) atomicAdd(&acc[256], (double)gs);
 }
@@ -741,7 +749,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
   if (h == 0) pb[(size_t)256 * C + 32 * wv + li] = dbacc;
 }
 
-// Sum the partials of row m (block m, thread = column), accumulate dW/db in float64 and the statistics of the
+// Sum the partials of row m (block m; thread = column + C * slice, SPLIT slices of the partial list so narrow
+// layers still put 256 threads on the latency-bound sum), accumulate dW/db in float64 and the statistics of the
 // BatchNorm below: s12[n] = (sum_m W[m][n] db[m], sum_m W[m][n] G[m][n]).
 template <int MODE>
 __global__ void k_wgrad_reduce(const float* __restrict__ part, int nblk, const float* __restrict__ W,
@@ -749,18 +758,35 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int nblk, const f
                                double* __restrict__ s12) {
   using Cfg = WgradCfg<MODE>;
   constexpr int C = Cfg::C;
+  constexpr int SPLIT = C >= 256 ? 1 : 256 / C;
   constexpr int in_f = MODE == 0 ? 256 : MODE == 1 ? 63 : 319;
   constexpr int wcol_h = MODE == 2 ? 63 : 0, col_h = Cfg::EX ? 64 : 0;
-  __shared__ double red[C];
-  const int m = blockIdx.x, t = threadIdx.x;
+  __shared__ double red[C * SPLIT];
+  const int m = blockIdx.x, tt = threadIdx.x, t = tt % C, sl = tt / C;
   double d = 0.0;
-  for (int b = t; b < nblk; b += C) d += (double)part[(size_t)b * Cfg::PART + (size_t)256 * C + m];
-  red[t] = d;
+  for (int b = tt; b < nblk; b += C * SPLIT) d += (double)part[(size_t)b * Cfg::PART + (size_t)256 * C + m];
+  red[tt] = d;
   __syncthreads();
   double dbm = 0.0;
-  for (int i = 0; i < C; ++i) dbm += red[i];
-  double G = 0.0;
-  for (int b = 0; b < nblk; ++b) G += (double)part[(size_t)b * Cfg::PART + (size_t)m * C + t];
+  for (int i = 0; i < C * SPLIT; ++i) dbm += red[i];
+  __syncthreads();
+  // 8 independent loads in flight per thread (the sum is latency-bound otherwise)
+  double Gp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  const float* pc = part + (size_t)m * C + t;
+  const int b0 = sl * ((nblk + SPLIT - 1) / SPLIT), b1 = min(nblk, b0 + (nblk + SPLIT - 1) / SPLIT);
+  int b = b0;
+  for (; b + 8 <= b1; b += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Gp[j] += (double)pc[(size_t)(b + j) * Cfg::PART];
+  }
+  for (; b < b1; ++b) Gp[0] += (double)pc[(size_t)b * Cfg::PART];
+  double G = ((Gp[0] + Gp[1]) + (Gp[2] + Gp[3])) + ((Gp[4] + Gp[5]) + (Gp[6] + Gp[7]));
+  if (SPLIT > 1) {
+    red[tt] = G;
+    __syncthreads();
+    if (sl != 0) return;
+    for (int k = 1; k < SPLIT; ++k) G += red[t + C * k];
+  }
   if (Cfg::EX && t < 64) {
     if (t < 63) dW[(size_t)m * in_f + t] += G;
   } else {
@@ -793,8 +819,11 @@ __device__ __forceinline__ void tring_fill(TRing& R, const f32x4* __restrict__ x
     for (int ob = 0; ob < 8; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
 }
 
+// `prev_out` (nullable): the previous tile's dL/dh, staged in LDS as [g][lane] float4s, is written one 1 KiB
+// group per k-group (the store burst would otherwise hold back the vmcnt waits of the next loads).
 __device__ __forceinline__ void gemm_t_mem(f32x16 (&acc)[8], TRing& R, const f32x4* __restrict__ x4,
-                                           const f32x4* __restrict__ x4_next, const f32x4* __restrict__ w4) {
+                                           const f32x4* __restrict__ x4_next, const f32x4* __restrict__ w4,
+                                           f32x4* __restrict__ prev_out, const f32x4* __restrict__ stage) {
 #pragma unroll
   for (int kg = 0; kg < KG_H; ++kg) {
 #pragma unroll
@@ -808,6 +837,7 @@ __device__ __forceinline__ void gemm_t_mem(f32x16 (&acc)[8], TRing& R, const f32
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) R.w[kg % WD][ob] = w4[(gw * 8 + ob) * 64];
     R.x[kg % XD] = kg + XD < KG_H ? x4[(kg + XD) * 64] : x4_next[(kg + XD - KG_H) * 64];
+    if (prev_out) prev_out[kg * 64] = stage[kg * 64];
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -821,6 +851,7 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_dgrad(
   __shared__ __attribute__((aligned(16))) float cmu[256];
   __shared__ __attribute__((aligned(16))) float cis[256];
   __shared__ __attribute__((aligned(16))) float cga[256];
+  __shared__ f32x4 stage[4][32 * 64];  // per-wave output tile in the [g][lane] layout (32 KiB)
   {
     const int k = threadIdx.x;
     const double S1 = s12[2 * k], dotp = s12[2 * k + 1];
@@ -841,8 +872,10 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_dgrad(
   const int64_t tstride = (int64_t)gridDim.x * 4;
   const int64_t tile0 = (int64_t)blockIdx.x * 4 + wv;
   const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wt) + lane;
+  f32x4* st = stage[wv] + lane;
   TRing ring;
   if (tile0 < ntiles) tring_fill(ring, reinterpret_cast<const f32x4*>(gin + tile0 * TILE_FLOATS) + lane, w4);
+  f32x4* prev_out = nullptr;
   for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
     int wofs = 0;
     asm volatile("" : "+s"(wofs));
@@ -853,27 +886,38 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_dgrad(
       for (int r = 0; r < 16; ++r) acc[ob][r] = 0.0f;
     const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
     gemm_t_mem(acc, ring, reinterpret_cast<const f32x4*>(gin + tile * TILE_FLOATS) + lane,
-               reinterpret_cast<const f32x4*>(gin + nxt * TILE_FLOATS) + lane, w4 + wofs);
+               reinterpret_cast<const f32x4*>(gin + nxt * TILE_FLOATS) + lane, w4 + wofs, prev_out, st);
     const bool valid = tile * 32 + li < n;
     const f32x4* hp4 = reinterpret_cast<const f32x4*>(hprev + tile * TILE_FLOATS) + lane;
-    f32x4* go4 = reinterpret_cast<f32x4*>(gout + tile * TILE_FLOATS) + lane;
+    f32x4 hx[32];
+#pragma unroll
+    for (int g = 0; g < 32; ++g) hx[g] = hp4[g * 64];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) {
-      f32x4 hx[4];
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) hx[gq] = hp4[(4 * ob + gq) * 64];
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
-        const int f0 = 32 * ob + 8 * gq + 4 * h;
+        const int g = 4 * ob + gq, f0 = 8 * g + 4 * h;
+        const f32x4 gm = *reinterpret_cast<const f32x4*>(cgm + f0), kk = *reinterpret_cast<const f32x4*>(ckk + f0);
+        const f32x4 mu = *reinterpret_cast<const f32x4*>(cmu + f0), is = *reinterpret_cast<const f32x4*>(cis + f0);
+        const f32x4 ga = *reinterpret_cast<const f32x4*>(cga + f0);
         f32x4 o;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int f = f0 + q;
-          o[q] = valid ? ((acc[ob][4 * gq + q] - cgm[f]) - (hx[gq][q] - cmu[f]) * ckk[f]) * cis[f] * cga[f] : 0.0f;
-        }
-        go4[(4 * ob + gq) * 64] = o;
+        for (int q = 0; q < 4; ++q)
+          o[q] = valid ? ((acc[ob][4 * gq + q] - gm[q]) - (hx[g][q] - mu[q]) * kk[q]) * is[q] * ga[q] : 0.0f;
+        st[g * 64] = o;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    prev_out = reinterpret_cast<f32x4*>(gout + tile * TILE_FLOATS) + lane;
+  }
+  if (prev_out) {
+#pragma unroll
+    for (int g = 0; g < 32; ++g) prev_out[g * 64] = st[g * 64];
   }
 }
 
@@ -1069,7 +1113,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     }
     {
       ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<1>::PART * 4.0);
-      hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::C), 0, s, ws.part, (int)wblocks,
+      hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(256), 0, s, ws.part, (int)wblocks,
                          P.lin_w[0], (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr);
     }
   }
