@@ -173,11 +173,12 @@ def main():
     achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
     traffic = pmc_traffic(kname)
 
-    cpu = None
+    cpu = cdref = None
     if rank == 0 and not a.no_cpu_baseline:
         if a.cpu_rays is None:
             a.cpu_rays = 1024 if grad else 4096
-        cpu = cpu_baseline(a, syn)
+        cpu, ext = cpu_baseline(a, syn)
+        cdref = cd_vs_ref(a, syn, ext, dev)
 
     if rank != 0:
         if dist:
@@ -186,7 +187,7 @@ def main():
     rays_total = a.rays * world * a.steps
     value = rays_total / elapsed
     out = {
-        "metric": "LiDAR rays/s (render+loss) at 128 samples/ray",
+        "metric": "LiDAR rays/s (render+loss) at 128 samples/ray; CD vs ref depth",
         "value": round(value, 1),
         "unit": "rays/s",
         "n_gpus": world,
@@ -211,6 +212,7 @@ def main():
                      "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 2),
                      "algorithmic_flop_per_launch": kflops / max(klaunch, 1)},
         "cpu_baseline": cpu,
+        "cd_vs_ref": cdref,
         "loss": loss_val,
         "kernels": kernels,
     }
@@ -221,7 +223,9 @@ def main():
 
 def cpu_baseline(a, syn):
     """The CPU oracle (oracle/ref_cpu.py, the reference's arithmetic on torch CPU) on a bounded sample of the
-    same workload: ``--cpu-rays`` rays of the same block, same settings, forward + losses."""
+    same workload: ``--cpu-rays`` rays of the same block, same settings, forward + losses (+ backward + Adam in
+    train_step mode).  The RNG draws are generated here and returned with the oracle's depths, so the HIP path can
+    be run on the identical inputs for the "CD vs ref depth" half of the metric."""
     from oracle import ref_cpu as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
@@ -230,6 +234,10 @@ def cpu_baseline(a, syn):
     Pf = O.params_from_numpy(syn.init_nof_params(5678))
     train = a.mode in ("train_fwd", "train_step")
     grad = a.mode == "train_step"
+    gen = torch.Generator().manual_seed(7)
+    R = rays.shape[0]
+    draws = {"perturb_rand": torch.rand(R, a.samples, generator=gen),
+             "u": torch.rand(R, a.importance, generator=gen)} if train else {}
     leaves = []
     if grad:
         for P in (Pc, Pf):
@@ -238,30 +246,59 @@ def cpu_baseline(a, syn):
                     leaves.append(P[k].requires_grad_(True))
         opt = torch.optim.Adam(leaves, lr=5e-4, eps=1e-8, weight_decay=1e-3)
 
-    def run(r):
+    def run(r, dr, step):
         if train:
             res = O.render_rays_train(Pc, Pf, r, sub_nerf_test_num=32, N_samples=a.samples, N_importance=a.importance,
                                       perturb=1, noise_std=0, chunk=a.chunk, issegmentated=1, childnerf_ratio=0.1,
-                                      use_child_nerf_loss=1, training=True)
+                                      use_child_nerf_loss=1, training=True, draws=dr)
             lr, lrf = O.range_losses(res["depth"], res["depth_fine"], r[:, 14])
             loss = O.total_loss(res, lr, lrf)
-            if grad:
+            if grad and step:
                 opt.zero_grad()
                 loss.backward()
                 opt.step()
-            return loss
-        res = O.render_rays_val(Pc, Pf, r, N_samples=a.samples, N_importance=a.importance, perturb=0, noise_std=0,
-                                chunk=a.chunk)
-        return res["depth_fine"].sum()
+            return res
+        return O.render_rays_val(Pc, Pf, r, N_samples=a.samples, N_importance=a.importance, perturb=0, noise_std=0,
+                                 chunk=a.chunk)
 
     with (torch.enable_grad() if grad else torch.no_grad()):
-        run(rays[:64])  # warm-up
+        run(rays[:64], {k: v[:64] for k, v in draws.items()}, False)  # warm-up (no parameter update)
         t0 = time.perf_counter()
-        run(rays)
+        res = run(rays, draws, True)
         dt = time.perf_counter() - t0
-    return {"value": round(a.cpu_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+    base = {"value": round(a.cpu_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
             "sample": f"{a.cpu_rays} rays of the same workload ({a.mode}, {a.samples}/{a.importance} samples, "
                       f"chunk {a.chunk}) through oracle/ref_cpu.py on torch CPU, {dt:.1f} s"}
+    return base, {"rays": rays, "draws": draws, "depth_fine": res["depth_fine"].detach()}
+
+
+def cd_vs_ref(a, syn, ext, dev):
+    """The HIP path on the CPU sample's rays and draws (fresh weights of the same seeds) vs the oracle's depths:
+    Chamfer distance / F-score (0.2 m) of the rendered points o + d * depth_fine (nof.metrics on the GPU) and the
+    largest relative depth error."""
+    from nof import metrics as NM
+    from nof.networks import Embedding, NOF_coarse, NOF_fine
+    from nof.render import render_rays_train, render_rays_val
+    train = a.mode in ("train_fwd", "train_step")
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234)).to(dev).train(train)
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678)).to(dev).train(train)
+    rays = ext["rays"].to(dev)
+    with torch.no_grad():
+        if train:
+            res = render_rays_train(mc, mf, Embedding(3, 10), rays, sub_nerf_test_num=32, N_samples=a.samples,
+                                    N_importance=a.importance, perturb=1, noise_std=0, chunk=a.chunk,
+                                    issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0,
+                                    use_child_nerf_loss=1, rng={k: v.to(dev) for k, v in ext["draws"].items()})
+        else:
+            res = render_rays_val(mc, mf, Embedding(3, 10), rays, N_samples=a.samples, N_importance=a.importance,
+                                  perturb=0, noise_std=0, chunk=a.chunk)
+    d_hip, d_ref = res["depth_fine"], ext["depth_fine"].to(dev)
+    p_hip = rays[:, 0:3] + rays[:, 3:6] * d_hip[:, None]
+    p_ref = rays[:, 0:3] + rays[:, 3:6] * d_ref[:, None]
+    cd, f = NM.eval_pts(p_hip, p_ref, 0.2)
+    rel = float(((d_hip - d_ref).abs() / d_ref.abs().clamp_min(1e-6)).max())
+    return {"cd_m": cd, "fscore": f, "max_rel_depth_err": rel, "rays": int(rays.shape[0]),
+            "vs": "oracle depth_fine on the cpu_baseline sample (same rays, draws and initial weights)"}
 
 
 if __name__ == "__main__":

@@ -203,6 +203,23 @@ int pcnerf_emit_view_rows(const double* points, int64_t n_points, const double* 
                           int64_t n_children, const double* parent6, int method, void* workspace, float* rows,
                           float* ranges, int64_t* other, uint8_t* true_in, void* stream);
 
+/* ---------------------------------------------------------------- evaluation metrics
+ * (nof/criteria/pointcloud_metrics.py:5-49, logs/.../render_result/print_metrics.py:31-133; exhaustive float64
+ * nearest-neighbour search instead of open3d's KD-tree).  Clouds are (n, 3) float32 rows.
+ * pcnerf_nn_distance: dist[i] = min_j |query[i] - ref[j]| (float64).
+ * pcnerf_eval_pts: out = {cd, fscore, precision, recall} of eval_pts(pred, gt, threshold): precision over the
+ *   gt points' nearest-pred distances, recall over the pred points' nearest-gt distances, cd = sum of the two
+ *   means; `workspace` needs pcnerf_eval_pts_workspace_bytes(n_pred, n_gt) bytes.  out is device memory.
+ * pcnerf_range_metrics: out = {sum |r_pred - r_gt|, count(|.| < threshold)} with ranges from `origin` (3 floats)
+ *   over n aligned points (abs_error / acc_thres before the division by n). */
+int pcnerf_nn_distance(const float* ref, int64_t n_ref, const float* query, int64_t n_query, double* dist,
+                       void* stream);
+size_t pcnerf_eval_pts_workspace_bytes(int64_t n_pred, int64_t n_gt);
+int pcnerf_eval_pts(const float* pred, int64_t n_pred, const float* gt, int64_t n_gt, double threshold,
+                    void* workspace, double* out, void* stream);
+int pcnerf_range_metrics(const float* pred, const float* gt, const float* origin, int64_t n, double threshold,
+                         double* out, void* stream);
+
 /* ---------------------------------------------------------------- kernel timing (bench / profiling)
  * pcnerf_prof_enable(1) makes every subsequent launch record a HIP event pair on its stream; tags:
  * 0 eval query, 1 train hidden Linear, 2 train first Linear, 3 train skip Linear, 4 train occ_out,

@@ -74,6 +74,10 @@ _SIGS = {
                                                 vp, vp, c_size, ctypes.POINTER(NofGrads), vp]),
     "pcnerf_nof_forward_train_backward": (c_int, [vp, i64, ctypes.POINTER(NofParams), c_float, vp, vp, vp, c_size,
                                                   ctypes.POINTER(NofGrads), vp]),
+    "pcnerf_nn_distance": (c_int, [vp, i64, vp, i64, vp, vp]),
+    "pcnerf_eval_pts_workspace_bytes": (c_size, [i64, i64]),
+    "pcnerf_eval_pts": (c_int, [vp, i64, vp, i64, ctypes.c_double, vp, vp, vp]),
+    "pcnerf_range_metrics": (c_int, [vp, vp, vp, i64, ctypes.c_double, vp, vp]),
     "pcnerf_composite_backward_workspace_bytes": (c_size, [c_int]),
     "pcnerf_composite_backward": (c_int, [vp, vp, i64, c_int, vp, c_float, c_float, vp, c_int, c_int, c_int, c_int,
                                           c_int, c_int, vp, vp, vp, vp, vp, vp]),

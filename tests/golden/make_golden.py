@@ -21,6 +21,7 @@ import importlib.util
 import os
 import sys
 
+import json
 import numpy as np
 import torch
 
@@ -320,7 +321,52 @@ def gen_grads():
              loss_total=t(total), **gc, **gf)
 
 
+METRIC_SCENES = {"kitti": ("logs/kitti00/1151_1200_view/render_result", range(1150, 1200)),
+                 "maicity": ("logs/maicity00/maicity_00_1/render_result", range(0, 50))}
+
+
+def raw_pcd(path):
+    """Independent minimal reader for the reference's binary xyz float32 PCDs (checks nof.io.read_pcd)."""
+    b = open(path, "rb").read()
+    i = b.index(b"DATA binary\n") + len(b"DATA binary\n")
+    n = int([ln for ln in b[:i].decode().splitlines() if ln.startswith("POINTS")][0].split()[1])
+    return np.frombuffer(b[i:i + 12 * n], dtype="<f4").reshape(n, 3).copy()
+
+
+def gen_metrics():
+    """print_metrics.py:54-133 over the reference's committed rendered / source PCDs (two versions x one/two-step
+    x every test frame, both scenes), computed by the cKDTree oracle; plus one KITTI frame's clouds as the GPU
+    fixture."""
+    sys.path.append(REPO)
+    from oracle import metrics_cpu as M
+    out = {}
+    for scene, (rel, frames) in METRIC_SCENES.items():
+        base = os.path.join(REF, rel)
+        for ver in ("version_0", "version_1"):
+            for kind in ("one_step", "two_step"):
+                rows = {}
+                for j in frames:
+                    if (j + 1 - 3) % 5 != 0:
+                        continue
+                    f = j + 1
+                    gt = raw_pcd(f"{base}/source/{f}_source.pcd")
+                    org = raw_pcd(f"{base}/source/{f}_pose.pcd").reshape(-1)
+                    pred = raw_pcd(f"{base}/infer/{ver}_{f}_{kind}.pcd")
+                    rows[str(f)] = M.frame_metrics(pred, gt, org, 0.2)
+                avg = np.mean(np.array(list(rows.values())), 0).tolist()
+                out[f"{scene}/{ver}/{kind}"] = {"frames": rows, "mean": avg}
+    with open(os.path.join(HERE, "metrics_reference.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    base = os.path.join(REF, METRIC_SCENES["kitti"][0])
+    save("metrics_frame", gt=raw_pcd(f"{base}/source/1153_source.pcd"),
+         origin=raw_pcd(f"{base}/source/1153_pose.pcd").reshape(-1),
+         pred=raw_pcd(f"{base}/infer/version_1_1153_two_step.pcd"),
+         expected=np.array(out["kitti/version_1/two_step"]["frames"]["1153"]))
+    print("metrics", {k: [round(x, 4) for x in v["mean"]] for k, v in out.items()})
+
+
 if __name__ == "__main__":
+    gen_metrics()
     gen_grads()
     gen_aabb()
     gen_render_rays()
