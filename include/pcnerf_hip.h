@@ -167,6 +167,19 @@ int pcnerf_pointwise_loss(const float* pred, const float* target, const uint8_t*
 int pcnerf_pointwise_loss_backward(const float* pred, const float* target, const uint8_t* mask, int64_t n, int kind,
                                    const float* grad_out, float* grad_pred, void* stream);
 
+/* Per-child range loss, the use_child_nerf_divide branch of train_kitti.py:125-142 (replaces its Python loop over
+ * sub_nerf_test_num children): out = sum over child ids c in 1..N owning >= 1 ray of
+ * post_scale * mean_{i in c} loss(pre_scale*pred_i, pre_scale*target_i) (the reference: pre 10, post 0.1*lambda).
+ * Child ids are read from child_id[i * id_stride] (ray column 9).  The backward needs the forward's workspace
+ * (per-child sums and counts, pcnerf_child_range_loss_workspace_bytes) unchanged; grad_out is a device scalar. */
+size_t pcnerf_child_range_loss_workspace_bytes(int sub_nerf_test_num);
+int pcnerf_child_range_loss(const float* pred, const float* target, int64_t n, const float* child_id, int id_stride,
+                            int sub_nerf_test_num, int kind, float pre_scale, float post_scale, void* workspace,
+                            float* out, void* stream);
+int pcnerf_child_range_loss_backward(const float* pred, const float* target, int64_t n, const float* child_id,
+                                     int id_stride, int sub_nerf_test_num, int kind, float pre_scale, float post_scale,
+                                     const void* workspace, const float* grad_out, float* grad_pred, void* stream);
+
 /* ---------------------------------------------------------------- two-step inference (render_rays_view_0525_2_2)
  * Per row (render.py:241-354 after the query): weights = composite(p) normalised with eps, the strict child
  * mask [rows[child_near_col], rows[child_far_col]] expanded from 0.01 by 0.01, the argmax of the weights

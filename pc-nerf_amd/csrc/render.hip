@@ -445,6 +445,59 @@ __global__ void k_child_loss_divide(const double* __restrict__ acc, int N, float
   }
 }
 
+// Per-child range loss (train_kitti.py:125-142, use_child_nerf_divide == 1): for each child id c in 1..N,
+// post * mean_c loss(pre*pred, pre*target); the reference sums these over the children that own >= 1 ray.
+// Scatter: per-child float64 sums of the element losses and counts (child slot as in k_child_loss_scatter).
+__device__ __forceinline__ int child_slot(const float* cid, int64_t i, int stride, int N) {
+  const float c = cid[i * stride];
+  const int k = (int)floorf(c - 0.5f);
+  if (k < 0 || k >= N) return -1;
+  return (c > (float)k + 0.5f && c < (float)k + 1.5f) ? k : -1;
+}
+
+__global__ void k_child_range_scatter(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                                      const float* __restrict__ cid, int stride, int N, int kind, float pre,
+                                      double* __restrict__ acc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int k = child_slot(cid, i, stride, N);
+  if (k < 0) return;
+  const float x = pre * a[i], y = pre * b[i];
+  const float d = x - y;
+  const float v = kind == 0 ? d * d : kind == 1 ? fabsf(d) : smooth_l1(x, y);
+  atomicAdd(acc + 2 * k + 0, (double)v);
+  atomicAdd(acc + 2 * k + 1, 1.0);
+}
+
+__global__ void k_child_range_reduce(const double* __restrict__ acc, int N, float post, float* __restrict__ out) {
+  __shared__ double sh[16];
+  double a = 0.0;
+  for (int k = threadIdx.x; k < N; k += blockDim.x) {
+    const double cnt = acc[2 * k + 1];
+    if (cnt >= 1.0) a += (double)(post * ((float)acc[2 * k + 0] / (float)cnt));
+  }
+  a = block_sum_d(a, sh);
+  if (threadIdx.x == 0) out[0] = (float)a;
+}
+
+// d/dpred_i = gout * post * pre * loss'(pre*pred - pre*target) / count_c(i); 0 for rays of no child slot.
+__global__ void k_child_range_bwd(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                                  const float* __restrict__ cid, int stride, int N, int kind, float pre, float post,
+                                  const double* __restrict__ acc, const float* __restrict__ gout,
+                                  float* __restrict__ ga) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int k = child_slot(cid, i, stride, N);
+  if (k < 0) {
+    ga[i] = 0.0f;
+    return;
+  }
+  const float d = pre * a[i] - pre * b[i];
+  const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+  const float g = kind == 0 ? 2.0f * d : kind == 1 ? sg : (fabsf(d) < 1.0f ? d : sg);
+  ga[i] = ((gout[0] * post) / (float)acc[2 * k + 1]) * g * pre;
+}
+
 __global__ void k_sum_f64(const double* __restrict__ x, int64_t n, double denom, float* __restrict__ out) {
   __shared__ double sh[16];
   double a = 0.0;
@@ -800,6 +853,41 @@ extern "C" int pcnerf_child_loss_reduce(const float* free_ray, const float* sl1_
                        out);
   }
   PCN_LAUNCH_CHECK("pcnerf_child_loss_reduce");
+  PCN_API_END
+}
+
+extern "C" size_t pcnerf_child_range_loss_workspace_bytes(int n) { return (size_t)(n > 0 ? n : 1) * 2 * sizeof(double); }
+
+extern "C" int pcnerf_child_range_loss(const float* pred, const float* target, int64_t n, const float* child_id,
+                                       int id_stride, int sub_nerf_test_num, int kind, float pre_scale,
+                                       float post_scale, void* workspace, float* out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(pred && target && child_id && workspace && out, "pcnerf_child_range_loss: null argument");
+  PCN_CHECK(n > 0 && sub_nerf_test_num > 0, "pcnerf_child_range_loss: empty input or no children");
+  PCN_CHECK(kind >= 0 && kind <= 2, "pcnerf_child_range_loss: kind must be 0, 1 or 2");
+  hipStream_t s = (hipStream_t)stream;
+  PCN_HIP(hipMemsetAsync(workspace, 0, pcnerf_child_range_loss_workspace_bytes(sub_nerf_test_num), s));
+  hipLaunchKernelGGL(k_child_range_scatter, dim3(nblk(n, 256)), dim3(256), 0, s, pred, target, n, child_id, id_stride,
+                     sub_nerf_test_num, kind, pre_scale, (double*)workspace);
+  hipLaunchKernelGGL(k_child_range_reduce, dim3(1), dim3(1024), 0, s, (const double*)workspace, sub_nerf_test_num,
+                     post_scale, out);
+  PCN_LAUNCH_CHECK("pcnerf_child_range_loss");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_child_range_loss_backward(const float* pred, const float* target, int64_t n,
+                                                const float* child_id, int id_stride, int sub_nerf_test_num, int kind,
+                                                float pre_scale, float post_scale, const void* workspace,
+                                                const float* grad_out, float* grad_pred, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(pred && target && child_id && workspace && grad_out && grad_pred,
+            "pcnerf_child_range_loss_backward: null argument");
+  PCN_CHECK(n > 0 && sub_nerf_test_num > 0, "pcnerf_child_range_loss_backward: empty input or no children");
+  PCN_CHECK(kind >= 0 && kind <= 2, "pcnerf_child_range_loss_backward: kind must be 0, 1 or 2");
+  hipLaunchKernelGGL(k_child_range_bwd, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, pred, target, n,
+                     child_id, id_stride, sub_nerf_test_num, kind, pre_scale, post_scale, (const double*)workspace,
+                     grad_out, grad_pred);
+  PCN_LAUNCH_CHECK("pcnerf_child_range_loss_backward");
   PCN_API_END
 }
 

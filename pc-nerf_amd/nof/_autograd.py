@@ -74,6 +74,23 @@ class PointwiseLoss(torch.autograd.Function):
         return gp.reshape(pred.shape), None, None, None
 
 
+class ChildRangeLoss(torch.autograd.Function):
+    """Per-child range loss of train_kitti.py:125-142 (divide branch) with d/dpred."""
+
+    @staticmethod
+    def forward(ctx, pred, target, rays, sub_num, kind, pre, post):
+        out, ws = _ops.child_range_loss(pred, target, rays, sub_num, kind, pre, post)
+        ctx.args = (sub_num, kind, pre, post)
+        ctx.save_for_backward(pred, target, rays, ws)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, target, rays, ws = ctx.saved_tensors
+        gp = _ops.child_range_loss_backward(pred, target, rays, *ctx.args, ws, g.contiguous())
+        return (gp.reshape(pred.shape),) + (None,) * 6
+
+
 def needs_grad(model) -> bool:
     return torch.is_grad_enabled() and any(t.requires_grad for t in model.parameters())
 

@@ -55,6 +55,10 @@ _SIGS = {
     "pcnerf_child_loss_reduce": (c_int, [vp, vp, i64, vp, c_int, c_int, vp, vp, vp]),
     "pcnerf_pointwise_loss": (c_int, [vp, vp, vp, i64, c_int, vp, vp]),
     "pcnerf_pointwise_loss_backward": (c_int, [vp, vp, vp, i64, c_int, vp, vp, vp]),
+    "pcnerf_child_range_loss_workspace_bytes": (c_size, [c_int]),
+    "pcnerf_child_range_loss": (c_int, [vp, vp, i64, vp, c_int, c_int, c_int, c_float, c_float, vp, vp, vp]),
+    "pcnerf_child_range_loss_backward": (c_int, [vp, vp, i64, vp, c_int, c_int, c_int, c_float, c_float, vp, vp, vp,
+                                                 vp]),
     "pcnerf_embed": (c_int, [vp, i64, vp, vp]),
     "pcnerf_view_rows": (c_int, [vp, vp, i64, c_int, vp, c_int, c_int, c_int, c_int, c_float, vp, c_int, vp, vp, vp,
                                  vp, vp, vp, vp]),

@@ -327,6 +327,41 @@ def pointwise_loss(pred, target, kind: str, valid_mask=None) -> torch.Tensor:
     return out
 
 
+def _child_ids(rays, n):
+    H.require_device(rays)
+    if rays.dtype != torch.float32 or rays.dim() != 2 or rays.shape[1] < 10 or rays.shape[0] != n \
+            or rays.stride(1) != 1:
+        raise RuntimeError("child range loss: rays must be a float32 (N, >=10) row-major table matching pred")
+    return rays.data_ptr() + 9 * 4, rays.stride(0)
+
+
+def child_range_loss(pred, target, rays, sub_nerf_test_num: int, kind: str, pre: float, post: float):
+    """-> (loss (1,) device tensor, workspace holding per-child sums/counts for the backward)."""
+    pred, target = _f32(pred).reshape(-1), _f32(target).reshape(-1)
+    n = pred.numel()
+    if target.numel() != n:
+        raise RuntimeError("child range loss: pred and target differ in size")
+    cid, stride = _child_ids(rays, n)
+    L = H.lib()
+    ws = _workspace(pred.device, L.pcnerf_child_range_loss_workspace_bytes(int(sub_nerf_test_num)))
+    out = torch.empty((1,), dtype=torch.float32, device=pred.device)
+    H.check(L.pcnerf_child_range_loss(pred.data_ptr(), target.data_ptr(), n, cid, stride, int(sub_nerf_test_num),
+                                      _KIND[kind], float(pre), float(post), ws.data_ptr(), out.data_ptr(),
+                                      _stream(pred)))
+    return out, ws
+
+
+def child_range_loss_backward(pred, target, rays, sub_nerf_test_num, kind, pre, post, ws, grad_out):
+    pred, target = _f32(pred).reshape(-1), _f32(target).reshape(-1)
+    cid, stride = _child_ids(rays, pred.numel())
+    g = torch.empty_like(pred)
+    H.check(H.lib().pcnerf_child_range_loss_backward(pred.data_ptr(), target.data_ptr(), pred.numel(), cid, stride,
+                                                     int(sub_nerf_test_num), _KIND[kind], float(pre), float(post),
+                                                     ws.data_ptr(), _f32(grad_out).data_ptr(), g.data_ptr(),
+                                                     _stream(pred)))
+    return g
+
+
 # ----------------------------------------------------------------------------------------------- backward
 def grad_params(model) -> list:
     """The 34 trainable tensors of a NOF in pcnerf_nof_grads order (lin_w, lin_b, bn_w, bn_b, out_w, out_b)."""

@@ -10,7 +10,7 @@ import torch
 
 from .. import _autograd, _ops
 
-__all__ = ["NOFLoss", "NOFMSELoss", "NOFL1Loss", "NOFSmoothL1Loss"]
+__all__ = ["NOFLoss", "NOFMSELoss", "NOFL1Loss", "NOFSmoothL1Loss", "child_range_loss"]
 
 
 class NOFLoss(nn.Module):
@@ -38,3 +38,14 @@ class NOFL1Loss(NOFLoss):
 class NOFSmoothL1Loss(NOFLoss):
     """SmoothL1 (beta 1): squared below 1, absolute above."""
     kind = "smoothl1"
+
+
+def child_range_loss(pred, target, rays, sub_nerf_test_num, lambda_loss=1.0, kind="smoothl1", pre=1e1, post=None):
+    """The use_child_nerf_divide == 1 range loss of train_kitti.py:125-142 in one kernel pair instead of a Python
+    loop over sub_nerf_test_num children: sum over child ids c = 1..N (ray column 9) that own >= 1 ray of
+    ``0.1 * lambda_loss * loss(10 * pred_c, 10 * target_c)`` (mean over the child's rays).  Shape (1,) like the
+    reference's ``torch.tensor([0]) + ...`` accumulator; differentiable in ``pred``."""
+    post = 1e-1 * lambda_loss if post is None else post
+    if torch.is_grad_enabled() and pred.requires_grad:
+        return _autograd.ChildRangeLoss.apply(pred, target, rays, int(sub_nerf_test_num), kind, pre, post)
+    return _ops.child_range_loss(pred, target, rays, int(sub_nerf_test_num), kind, pre, post)[0]

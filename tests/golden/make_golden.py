@@ -365,7 +365,19 @@ def gen_metrics():
     print("metrics", {k: [round(x, 4) for x in v["mean"]] for k, v in out.items()})
 
 
+def gen_kitti_frames(step=40):
+    """Scene fixture for the dataset pipeline (nof/dataset.py): KITTI-00 scans 1151..1156 of the reference's
+    data/kitti/00/pcd_remove_dynamic (every ``step``-th point, float32 as stored) and poses.txt rows 1150..1156."""
+    frames = {f"f{f}": raw_pcd(os.path.join(REF, f"data/kitti/00/pcd_remove_dynamic/{f}.pcd"))[::step]
+              for f in range(1151, 1157)}
+    with open(os.path.join(REF, "data/kitti/00/poses.txt")) as fh:
+        rows = [ln.strip() for ln in fh if ln.strip()]
+    poses = np.array([[float(v) for v in rows[i].split(" ")] for i in range(1150, 1157)])
+    save("kitti_frames", poses=poses, pose_first=np.array(1150), **frames)
+
+
 if __name__ == "__main__":
+    gen_kitti_frames()
     gen_metrics()
     gen_grads()
     gen_aabb()

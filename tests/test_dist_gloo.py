@@ -63,3 +63,64 @@ def test_gather_and_max_world2():
     assert [row[1] for row in out0] == [0, 0, 0, 1, 1, 1, 1]
     assert t0 == res[1][1] == 2.0
     assert b0 == [0, 1] and res[1][2] == [2, 3]
+
+
+def test_shard_batch_partition():
+    from nof.blocks import shard_batch
+    for n in (0, 1, 5, 256, 257):
+        idx = torch.randperm(n)
+        for world in (1, 2, 3, 8):
+            parts = [shard_batch(idx, r, world) for r in range(world)]
+            assert torch.equal(torch.cat(parts), idx)
+            sizes = [p.numel() for p in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _dp_worker(rank, world, port, q):
+    """Data-parallel step of train_kitti.fit on CPU: each rank's shard of one global batch, mean loss per rank,
+    gradients averaged by allreduce_grads -> must equal the single-process gradient of the whole batch (equal
+    shards), and every rank must end with identical parameters after the optimizer step."""
+    from nof.blocks import allreduce_grads, shard_batch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Linear(16, 1))
+        unused = torch.nn.Parameter(torch.ones(3))          # never receives a gradient
+        x, y = torch.randn(64, 7), torch.randn(64, 1)
+        idx = shard_batch(torch.arange(64), rank, world)
+        loss = torch.nn.functional.mse_loss(net(x[idx]), y[idx])
+        loss.backward()
+        params = list(net.parameters()) + [unused]
+        allreduce_grads(params)
+        g = torch.cat([p.grad.reshape(-1) for p in params]).clone()
+        opt = torch.optim.Adam(params, lr=1e-2)
+        opt.step()
+        w = torch.cat([p.detach().reshape(-1) for p in params])
+        q.put((rank, g.tolist(), w.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_data_parallel_gradients_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        rank, g, w = q.get(timeout=90)
+        res[rank] = (torch.tensor(g), torch.tensor(w))
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Linear(16, 1))
+    x, y = torch.randn(64, 7), torch.randn(64, 1)
+    torch.nn.functional.mse_loss(net(x), y).backward()
+    full = torch.cat([p.grad.reshape(-1) for p in net.parameters()] + [torch.zeros(3)])
+    torch.testing.assert_close(res[0][0], full, rtol=1e-5, atol=1e-7)
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
