@@ -18,14 +18,16 @@ import math
 import numpy as np
 
 
-def filter_scan(pts32, range_delete, over_height, over_low):
+def filter_scan(pts32, range_delete, over_height, over_low, strict_range=False):
+    """ipb2dmapping.py:650-664 (dist <= 120); strict_range: eval_kitti_render.py:621-641 (dist < 120)."""
     out = []
     dx, dy, dz = range_delete
     for p in np.asarray(pts32, dtype=np.float32):
         if abs(p[0]) < dx and abs(p[1]) < dy and abs(p[2]) < dz:
             continue
         sq = p * p
-        if np.sqrt((sq[0] + sq[1]) + sq[2]) > np.float32(120):
+        dist = np.sqrt((sq[0] + sq[1]) + sq[2])
+        if dist > np.float32(120) or (strict_range and dist == np.float32(120)):
             continue
         if p[2] > over_height or p[2] < over_low:
             continue
@@ -90,3 +92,25 @@ def val_index(n_rays, cloud_size_val):
     import torch
     sel = torch.linspace(1, n_rays - 2, steps=cloud_size_val, dtype=torch.float32)
     return np.array([math.floor(float(s)) for s in sel], dtype=np.int64)
+
+
+def batch_slices(rows_last_col, batch_size_set):
+    """eval_kitti_render.py:1120-1143, the reference's loop verbatim in structure (float column compared < -0.5)."""
+    n = len(rows_last_col)
+    out = []
+    i = 0
+    while i < n:
+        if i == n - 1:
+            break
+        if i + batch_size_set < n - 0.5 * batch_size_set:
+            other_ray_number = 0
+            while rows_last_col[i + batch_size_set + other_ray_number] < -0.5:
+                other_ray_number = other_ray_number + 1
+                if i + batch_size_set + other_ray_number == n:
+                    break
+            out.append((i, i + batch_size_set + other_ray_number))
+            i = i + batch_size_set + other_ray_number
+        else:
+            out.append((i, n))
+            i = n
+    return out

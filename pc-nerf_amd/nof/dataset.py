@@ -82,14 +82,16 @@ def frame_ids(data_start: int, data_end: int, split: str, sparsity: int = 20) ->
 
 
 def filter_scan(pts: torch.Tensor, range_delete=(3.0, 2.0, 1.25), over_height=0.168, over_low=-2.0,
-                max_range=120.0) -> torch.Tensor:
+                max_range=120.0, strict_range=False) -> torch.Tensor:
     """ipb2dmapping.py:650-664: drop the ego box (|x|<dx and |y|<dy and |z|<dz), points beyond 120 m (norm in
-    float32, like np.linalg.norm of the float32 scan) and points outside [over_low, over_height] in z."""
+    float32, like np.linalg.norm of the float32 scan) and points outside [over_low, over_height] in z.
+    ``strict_range``: the test-frame variant keeps only norms < 120 (eval_kitti_render.py:637)."""
     p = pts.to(torch.float32)
     dx, dy, dz = (float(v) for v in range_delete)
     keep = (p[:, 0].abs() >= dx) | (p[:, 1].abs() >= dy) | (p[:, 2].abs() >= dz)
     sq = p * p
-    keep &= torch.sqrt((sq[:, 0] + sq[:, 1]) + sq[:, 2]) <= max_range
+    nrm = torch.sqrt((sq[:, 0] + sq[:, 1]) + sq[:, 2])
+    keep &= (nrm < max_range) if strict_range else (nrm <= max_range)
     keep &= (p[:, 2] <= over_height) & (p[:, 2] >= over_low)
     return p[keep]
 
