@@ -34,6 +34,39 @@ namespace pcn {
 #ifndef PCN_WD
 #define PCN_WD 2  // weight prefetch depth in k-groups (divides 32)
 #endif
+#ifndef PCN_WD2
+#define PCN_WD2 2  // weight prefetch depth of k_train_hidden (k-groups of one half: 4 float4 each)
+#endif
+#ifndef PCN_HIDDEN_PP
+#define PCN_HIDDEN_PP 1  // 1: hidden layers run k_train_hidden (epilogue overlapped), 0: k_train_layer<false,true>
+#endif
+#ifndef PCN_PP_SCHED
+#define PCN_PP_SCHED 0  // k_train_hidden: sched_group_barrier interleave per k-group (measured 2.7 % slower: off)
+#endif
+#ifndef PCN_PP_XREG
+#define PCN_PP_XREG 1  // k_train_hidden: the tile's activations register-resident across its two passes
+#endif
+#ifndef PCN_DGRAD_PF
+#define PCN_DGRAD_PF 1  // k_dgrad: prefetch the BatchNorm-backward operand tile during the GEMM
+#endif
+#ifndef PCN_ABL_PLDS
+#define PCN_ABL_PLDS 0
+#endif
+#ifndef PCN_ABL_PSTAT
+#define PCN_ABL_PSTAT 0
+#endif
+#ifndef PCN_ABL_PSTORE
+#define PCN_ABL_PSTORE 0
+#endif
+#ifndef PCN_ABL_WLOAD
+#define PCN_ABL_WLOAD 0
+#endif
+#ifndef PCN_ABL_XLOAD
+#define PCN_ABL_XLOAD 0
+#endif
+#ifndef PCN_ABL_EPI
+#define PCN_ABL_EPI 0
+#endif
 
 constexpr int KG_E = 8, KG_H = 32;
 constexpr size_t SZ_E = (size_t)KG_E * 8 * 64 * 4;
@@ -150,7 +183,7 @@ static_assert(KG_H % XD == 0 && KG_H % WD == 0, "ring depths must divide the k-g
 struct HRing {
   f32x4 x[XD];
   f32x4 w[WD][8];
-  f32x4 a, b;  // alpha/beta' of the next group
+  f32x4 a[2], b[2];  // alpha/beta' of groups kg, kg+1 (read from LDS two groups ahead)
 };
 
 __device__ __forceinline__ void ring_fill(HRing& R, const f32x4* __restrict__ x4, const f32x4* __restrict__ w4,
@@ -161,8 +194,11 @@ __device__ __forceinline__ void ring_fill(HRing& R, const f32x4* __restrict__ x4
   for (int d = 0; d < WD; ++d)
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
-  R.a = *reinterpret_cast<const f32x4*>(al + h4);
-  R.b = *reinterpret_cast<const f32x4*>(be + h4);
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    R.a[d] = *reinterpret_cast<const f32x4*>(al + 8 * d + h4);
+    R.b[d] = *reinterpret_cast<const f32x4*>(be + 8 * d + h4);
+  }
 }
 
 // `prev_out` (nullable): the previous tile's output, staged in LDS rows `stage_row`, is written to HBM one
@@ -176,7 +212,7 @@ __device__ __forceinline__ void gemm_n_mem(f32x16 (&acc)[8], HRing& R, const f32
   for (int kg = 0; kg < KG_H; ++kg) {
     f32x4 xa;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) xa[q] = R.x[kg % XD][q] * R.a[q] + R.b[q];
+    for (int q = 0; q < 4; ++q) xa[q] = R.x[kg % XD][q] * R.a[kg & 1][q] + R.b[kg & 1][q];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -185,12 +221,16 @@ __device__ __forceinline__ void gemm_n_mem(f32x16 (&acc)[8], HRing& R, const f32
     }
     __builtin_amdgcn_sched_barrier(0);
     const int gw = (kg + WD) % KG_H;  // group kg+WD of this tile, or the first groups of the next tile
+#if !PCN_ABL_WLOAD  // ablation builds (timing only, wrong results): PCN_ABL_WLOAD / _XLOAD skip the reloads
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) R.w[kg % WD][ob] = w4[(gw * 8 + ob) * 64];
+#endif
+#if !PCN_ABL_XLOAD
     R.x[kg % XD] = kg + XD < KG_H ? x4[(kg + XD) * 64] : x4_next[(kg + XD - KG_H) * 64];
-    const int ga = (kg + 1) % KG_H;
-    R.a = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
-    R.b = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
+#endif
+    const int ga = (kg + 2) % KG_H;
+    R.a[kg & 1] = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
+    R.b[kg & 1] = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
     if (prev_out) prev_out[kg * 64] = *reinterpret_cast<const f32x4*>(stage_row + 8 * kg);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -267,6 +307,17 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_train_layer(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // epilogue: + bias -> LDS stage [sample][neuron]; statistics of (h - bias) over valid samples
     const int64_t base = tile * 32;
+#if PCN_ABL_EPI  // ablation (timing only): no epilogue, the accumulators kept live by one store
+    {
+      float t = 0.0f;
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[ob][r];
+      hout[tile * TILE_FLOATS + lane] = t;
+      continue;
+    }
+#endif
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) {
       const int nn = 32 * ob + li;
@@ -296,6 +347,348 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_train_layer(
     const float* lrow = stage[wv] + li * LDS_ROW + 4 * h;
 #pragma unroll
     for (int g = 0; g < 32; ++g) prev_out[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) atomicAdd(&stats[i], st[i]);
+}
+
+// ---- k_train_hidden: k_train_layer<false,true> with the epilogue hidden behind the MFMA stream.
+// Each 32-sample tile is computed in two passes over K (neurons 0-127, then 128-255), each into its own 64
+// accumulators.  While a pass runs its 512 MFMAs, the epilogue of the PREVIOUS pass (the other accumulator set:
+// + bias, LDS staging, BatchNorm statistics) and the HBM stores of the pass before that (LDS -> 1 KiB dwordx4 per
+// k-group) are interleaved between the MFMA groups, two values and half a store per k-group, so the matrix pipe
+// never idles for the epilogue (it cost 14 % of k_train_layer's time, measured by an ablation build).
+// Stage regions: pass (t, half E)'s epilogue writes neurons [128E, 128E+128) of the stage, the stores of that
+// region are issued during pass (t+1, E) and the region is rewritten during pass (t+1, 1-E) -- program order of
+// one wave's LDS operations keeps the three apart.  Statistics: same per-(lane, neuron) fp32 partial sums over
+// the tile's 16 rows, in the same order, as k_train_layer.
+constexpr int PXD = PCN_XD;
+constexpr int PWD = PCN_WD2;
+static_assert(KG_H % PXD == 0 && KG_H % PWD == 0, "ring depths must divide the k-group count");
+
+struct PRing {
+  f32x4 x[PXD];
+  f32x4 w[PWD][4];
+  f32x4 a[2], b[2];  // BatchNorm alpha/beta' of k-groups kg, kg+1 (read from LDS two groups ahead)
+  f32x4 xa;          // BatchNorm'd activations of the current k-group
+};
+
+struct PEpi {            // epilogue of the previous pass
+  float* lt;             // this wave's stage
+  int64_t base;          // first sample of its tile
+  float on;              // 0 when there is no previous pass (statistics multiplied by it)
+};
+
+// Per k-group interleave of the 16 MFMAs with the pass's other instructions: at most 2 VALU and one memory
+// operation per MFMA gap (cdna_hip_programming.md T19; MI355X_MICROARCH issue costs: a 64-cycle f32 MFMA hides
+// a handful of 4-cycle issues, a block of them between two MFMAs stalls the matrix pipe).
+__device__ __forceinline__ void pp_interleave() {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU
+    if (i < 10 && (i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+    if (i == 1 || i == 5 || i == 9) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    if (i == 3 || i == 11) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+    if (i == 13) __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // VMEM write
+  }
+}
+
+template <int H>
+__device__ __forceinline__ void pp_pass(f32x16 (&acc)[4], const f32x16 (&eacc)[4], PRing& R,
+                                        const f32x4* __restrict__ x4, const f32x4* __restrict__ x4_next,
+                                        const f32x4* __restrict__ w4, const float* __restrict__ al,
+                                        const float* __restrict__ be, const float* __restrict__ bias, int lane,
+                                        const PEpi& E, int64_t n, double* st, f32x4* __restrict__ sout) {
+  constexpr int EH = 1 - H;  // half of the previous pass
+  const int li = lane & 31, h = lane >> 5, h4 = 4 * h;
+  float ebias[4];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) ebias[ob] = bias[32 * (4 * EH + ob) + li];
+  const float* srow = E.lt + li * LDS_ROW + h4;
+  // rows of the previous pass's tile that hold samples < n, as a per-lane bound on the register row
+  const int64_t nv64 = n - E.base;
+  const int lim = (nv64 >= 32 ? 32 : (int)nv64) - h4;
+  float s1 = 0.0f, s2 = 0.0f;
+  f32x4 sv;
+#pragma unroll
+  for (int kg = 0; kg < KG_H; ++kg) {
+    const f32x4 xa = R.xa;   // BatchNorm'd activations of this k-group (computed during the previous one)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        const f32x16 c = (kg == 0 && q == 0) ? f32x16{} : acc[ob];
+        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[q], R.w[kg % PWD][ob][q], c, 0, 0, 0);
+      }
+    }
+    // epilogue values v = 2 kg, 2 kg + 1 of the previous pass
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int v = 2 * kg + u, ob = v >> 4, r = v & 15;
+      const int sr = (r & 3) + 8 * (r >> 2);   // sample row of register r (lane half adds 4)
+      const int nn = 32 * (4 * EH + ob) + li;
+      const float d = eacc[ob][r];
+#if !PCN_ABL_PLDS
+      E.lt[(sr + h4) * LDS_ROW + nn] = d + ebias[ob];
+#endif
+#if !PCN_ABL_PSTAT
+      const float dv = sr < lim ? d : 0.0f;
+      s1 += dv;
+      s2 += dv * dv;
+#endif
+      if (r == 15) {
+        atomicAdd(&st[2 * nn], (double)(s1 * E.on));
+        atomicAdd(&st[2 * nn + 1], (double)(s2 * E.on));
+        s1 = 0.0f;
+        s2 = 0.0f;
+      }
+    }
+    // staged output of the pass before (half H of the previous tile): LDS read on even k-groups, store on odd
+#if !PCN_ABL_PSTORE
+    {
+      const int g = 16 * H + (kg >> 1);
+      if ((kg & 1) == 0) sv = *reinterpret_cast<const f32x4*>(srow + 8 * g);
+      else sout[g * 64] = sv;
+    }
+#endif
+    // prefetch: stream position kg + depth (the next pass: same tile's other half for H = 0, next tile for H = 1)
+    const int gw = kg + PWD;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      const int gg = gw < KG_H ? gw : gw - KG_H;
+      const int hh = gw < KG_H ? H : 1 - H;
+      R.w[kg % PWD][ob] = w4[(gg * 8 + 4 * hh + ob) * 64];
+    }
+    {
+      const int gx = kg + PXD;
+      if (gx < KG_H) R.x[kg % PXD] = x4[gx * 64];
+      else R.x[kg % PXD] = (H == 0 ? x4 : x4_next)[(gx - KG_H) * 64];
+    }
+    // BatchNorm of the next k-group's activations (ring slots hold group kg + 1 already)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) R.xa[q] = R.x[(kg + 1) % PXD][q] * R.a[(kg + 1) & 1][q] + R.b[(kg + 1) & 1][q];
+    const int ga = (kg + 2) % KG_H;
+    R.a[kg & 1] = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
+    R.b[kg & 1] = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
+#if PCN_PP_SCHED
+    pp_interleave();
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Variant with the tile's 32 activation groups register-resident (128 VGPRs): pass A loads nothing for x (the
+// raw groups were loaded during the previous tile's pass B), applies the BatchNorm in place one group ahead, and
+// pass B reuses the BatchNorm'd groups -- no second read of the tile, no second BatchNorm -- and refills each
+// group with the next tile's raw values right after its last use.
+struct XRing {
+  f32x4 w[PWD][4];
+  f32x4 a[2], b[2];  // alpha/beta' ring (pass A reads group kg + 2 into slot kg & 1)
+};
+
+template <int H>
+__device__ __forceinline__ void pp_pass_x(f32x16 (&acc)[4], const f32x16 (&eacc)[4], f32x4 (&X)[KG_H], XRing& R,
+                                          const f32x4* __restrict__ xn4, const f32x4* __restrict__ w4,
+                                          const float* __restrict__ al, const float* __restrict__ be,
+                                          const float* __restrict__ bias, int lane, const PEpi& E, int64_t n,
+                                          double* st, f32x4* __restrict__ sout) {
+  constexpr int EH = 1 - H;
+  const int li = lane & 31, h = lane >> 5, h4 = 4 * h;
+  float ebias[4];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) ebias[ob] = bias[32 * (4 * EH + ob) + li];
+  const float* srow = E.lt + li * LDS_ROW + h4;
+  const int64_t nv64 = n - E.base;
+  const int lim = (nv64 >= 32 ? 32 : (int)nv64) - h4;
+  float s1 = 0.0f, s2 = 0.0f;
+  f32x4 sv;
+#pragma unroll
+  for (int kg = 0; kg < KG_H; ++kg) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        const f32x16 c = (kg == 0 && q == 0) ? f32x16{} : acc[ob];
+        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(X[kg][q], R.w[kg % PWD][ob][q], c, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int v = 2 * kg + u, ob = v >> 4, r = v & 15;
+      const int sr = (r & 3) + 8 * (r >> 2);
+      const int nn = 32 * (4 * EH + ob) + li;
+      const float d = eacc[ob][r];
+      E.lt[(sr + h4) * LDS_ROW + nn] = d + ebias[ob];
+      const float dv = sr < lim ? d : 0.0f;
+      s1 += dv;
+      s2 += dv * dv;
+      if (r == 15) {
+        atomicAdd(&st[2 * nn], (double)(s1 * E.on));
+        atomicAdd(&st[2 * nn + 1], (double)(s2 * E.on));
+        s1 = 0.0f;
+        s2 = 0.0f;
+      }
+    }
+    {
+      const int g = 16 * H + (kg >> 1);
+      if ((kg & 1) == 0) sv = *reinterpret_cast<const f32x4*>(srow + 8 * g);
+      else sout[g * 64] = sv;
+    }
+    const int gw = kg + PWD;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      const int gg = gw < KG_H ? gw : gw - KG_H;
+      const int hh = gw < KG_H ? H : 1 - H;
+      R.w[kg % PWD][ob] = w4[(gg * 8 + 4 * hh + ob) * 64];
+    }
+    if (H == 0) {
+      // BatchNorm of the next group in place (its alpha/beta' sit in slot (kg+1)&1), then refill slot kg&1
+      if (kg + 1 < KG_H) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X[kg + 1][q] = X[kg + 1][q] * R.a[(kg + 1) & 1][q] + R.b[(kg + 1) & 1][q];
+      }
+      const int ga = (kg + 2) % KG_H;
+      R.a[kg & 1] = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
+      R.b[kg & 1] = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
+    } else {
+      X[kg] = xn4[kg * 64];   // next tile's raw group kg
+      if (kg == KG_H - 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X[0][q] = X[0][q] * R.a[0][q] + R.b[0][q];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void k_train_hidden(const float* __restrict__ hin, int64_t n,
+                                                         const float* __restrict__ Wp,
+                                                         const float* __restrict__ bias, BnPrev prev,
+                                                         float momentum, float eps, float* __restrict__ hout,
+                                                         float* __restrict__ trash, double* __restrict__ stats) {
+  __shared__ double st[512];
+  __shared__ __attribute__((aligned(16))) float al[256];
+  __shared__ __attribute__((aligned(16))) float be[256];
+  __shared__ __attribute__((aligned(16))) float stage[4][32 * LDS_ROW];
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) st[i] = 0.0;
+  bn_coeffs(prev, n, momentum, eps, al, be);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar tile bookkeeping
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t tstride = (int64_t)gridDim.x * 4;
+  const int64_t tile0 = (int64_t)blockIdx.x * 4 + wv;
+#if PCN_PP_XREG
+  if (tile0 < ntiles) {
+    const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wp) + lane;
+    float* lt = stage[wv];
+    XRing R;
+    f32x4 X[KG_H];
+    {
+      const f32x4* x0 = reinterpret_cast<const f32x4*>(hin + tile0 * TILE_FLOATS) + lane;
+#pragma unroll
+      for (int g = 0; g < KG_H; ++g) X[g] = x0[g * 64];
+#pragma unroll
+      for (int d = 0; d < PWD; ++d)
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        R.a[d] = *reinterpret_cast<const f32x4*>(al + 8 * d + 4 * h);
+        R.b[d] = *reinterpret_cast<const f32x4*>(be + 8 * d + 4 * h);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) X[0][q] = X[0][q] * R.a[0][q] + R.b[0][q];
+    }
+    f32x16 accA[4], accB[4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) accB[ob] = f32x16{};
+    int64_t prev_tile = -1;
+    for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
+      int wofs = 0;
+      asm volatile("" : "+s"(wofs));
+      const f32x4* wt = w4 + wofs;
+      const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
+      const f32x4* x4n = reinterpret_cast<const f32x4*>(hin + nxt * TILE_FLOATS) + lane;
+      f32x4* pout = reinterpret_cast<f32x4*>(prev_tile >= 0 ? hout + prev_tile * TILE_FLOATS : trash) + lane;
+      const PEpi ea{lt, prev_tile >= 0 ? prev_tile * 32 : 0, prev_tile >= 0 ? 1.0f : 0.0f};
+      pp_pass_x<0>(accA, accB, X, R, x4n, wt, al, be, bias, lane, ea, n, st, pout);
+      const PEpi eb{lt, tile * 32, 1.0f};
+      pp_pass_x<1>(accB, accA, X, R, x4n, wt, al, be, bias, lane, eb, n, st, pout);
+      prev_tile = tile;
+    }
+#else
+  if (tile0 < ntiles) {
+    const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wp) + lane;
+    float* lt = stage[wv];
+    PRing R;
+    {
+      const f32x4* x0 = reinterpret_cast<const f32x4*>(hin + tile0 * TILE_FLOATS) + lane;
+#pragma unroll
+      for (int d = 0; d < PXD; ++d) R.x[d] = x0[d * 64];
+#pragma unroll
+      for (int d = 0; d < PWD; ++d)
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        R.a[d] = *reinterpret_cast<const f32x4*>(al + 8 * d + 4 * h);
+        R.b[d] = *reinterpret_cast<const f32x4*>(be + 8 * d + 4 * h);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) R.xa[q] = R.x[0][q] * R.a[0][q] + R.b[0][q];
+    }
+    f32x16 accA[4], accB[4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) accB[ob] = f32x16{};
+    int64_t prev_tile = -1;
+    for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
+      int wofs = 0;  // opaque offset: keeps the weight loads inside the tile loop (see k_train_layer)
+      asm volatile("" : "+s"(wofs));
+      const f32x4* wt = w4 + wofs;
+      const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
+      const f32x4* x4 = reinterpret_cast<const f32x4*>(hin + tile * TILE_FLOATS) + lane;
+      const f32x4* x4n = reinterpret_cast<const f32x4*>(hin + nxt * TILE_FLOATS) + lane;
+      // first tile: there is no previous tile, its (meaningless) stores go to a scratch tile nobody reads
+      f32x4* pout = reinterpret_cast<f32x4*>(prev_tile >= 0 ? hout + prev_tile * TILE_FLOATS : trash) + lane;
+      const PEpi ea{lt, prev_tile >= 0 ? prev_tile * 32 : 0, prev_tile >= 0 ? 1.0f : 0.0f};
+      pp_pass<0>(accA, accB, R, x4, x4n, wt, al, be, bias, lane, ea, n, st, pout);
+      const PEpi eb{lt, tile * 32, 1.0f};
+      pp_pass<1>(accB, accA, R, x4, x4n, wt, al, be, bias, lane, eb, n, st, pout);
+      prev_tile = tile;
+    }
+#endif
+    // drain: epilogue of the last tile's second half, then all of its stores
+    {
+      const int li = lane & 31;
+      float s1, s2;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        const int nn = 32 * (4 + ob) + li;
+        const float bo = bias[nn];
+        s1 = 0.0f;
+        s2 = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int smp = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float d = accB[ob][r];
+          lt[smp * LDS_ROW + nn] = d + bo;
+          const float dv = (prev_tile * 32 + smp < n) ? d : 0.0f;
+          s1 += dv;
+          s2 += dv * dv;
+        }
+        atomicAdd(&st[2 * nn], (double)s1);
+        atomicAdd(&st[2 * nn + 1], (double)s2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      f32x4* out = reinterpret_cast<f32x4*>(hout + prev_tile * TILE_FLOATS) + lane;
+      const float* lrow = lt + li * LDS_ROW + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 32; ++g) out[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 512; i += blockDim.x) atomicAdd(&stats[i], st[i]);
@@ -346,7 +739,8 @@ static TrainWs carve(void* base, int64_t chunk) {
     off += (bytes + 255) & ~(size_t)255;
     return o;
   };
-  const size_t oA = take(tiles * TILE_FLOATS * 4), oB = take(tiles * TILE_FLOATS * 4);
+  // one extra tile per activation buffer: the scratch target of k_train_hidden's first-tile stores
+  const size_t oA = take((tiles + 1) * TILE_FLOATS * 4), oB = take((tiles + 1) * TILE_FLOATS * 4);
   const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
   char* b = (char*)base;
   TrainWs w;
@@ -402,9 +796,14 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                           n_samples, c0, n, ein, hin, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps,
-                           hout, ws.stats + 512 * L);
+        if (PCN_HIDDEN_PP)
+          hipLaunchKernelGGL(k_train_hidden, dim3(grid), dim3(256), 0, s, hin, n, ws.wp + off_w(L, false),
+                             P.lin_b[L], prev, momentum, eps, hout,
+                             hout + (size_t)((chunk + 31) / 32) * TILE_FLOATS, ws.stats + 512 * L);
+        else
+          hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
+                             n_samples, c0, n, ein, hin, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps,
+                             hout, ws.stats + 512 * L);
       }
       float* t = hin;
       hin = hout;
@@ -821,9 +1220,12 @@ __device__ __forceinline__ void tring_fill(TRing& R, const f32x4* __restrict__ x
 
 // `prev_out` (nullable): the previous tile's dL/dh, staged in LDS as [g][lane] float4s, is written one 1 KiB
 // group per k-group (the store burst would otherwise hold back the vmcnt waits of the next loads).
+// `hp4` / `hx`: the BatchNorm backward's h_{L-1} tile is prefetched during the first 16 k-groups (two 1 KiB loads
+// each) instead of as a 32-load burst after the GEMM, so its latency hides behind the MFMAs.
 __device__ __forceinline__ void gemm_t_mem(f32x16 (&acc)[8], TRing& R, const f32x4* __restrict__ x4,
                                            const f32x4* __restrict__ x4_next, const f32x4* __restrict__ w4,
-                                           f32x4* __restrict__ prev_out, const f32x4* __restrict__ stage) {
+                                           f32x4* __restrict__ prev_out, const f32x4* __restrict__ stage,
+                                           const f32x4* __restrict__ hp4, f32x4 (&hx)[32]) {
 #pragma unroll
   for (int kg = 0; kg < KG_H; ++kg) {
 #pragma unroll
@@ -834,10 +1236,20 @@ __device__ __forceinline__ void gemm_t_mem(f32x16 (&acc)[8], TRing& R, const f32
     }
     __builtin_amdgcn_sched_barrier(0);
     const int gw = (kg + WD) % KG_H;
+#if !PCN_ABL_WLOAD  // ablation builds (timing only, wrong results): PCN_ABL_WLOAD / _XLOAD skip the reloads
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) R.w[kg % WD][ob] = w4[(gw * 8 + ob) * 64];
+#endif
+#if !PCN_ABL_XLOAD
     R.x[kg % XD] = kg + XD < KG_H ? x4[(kg + XD) * 64] : x4_next[(kg + XD - KG_H) * 64];
+#endif
     if (prev_out) prev_out[kg * 64] = stage[kg * 64];
+#if PCN_DGRAD_PF
+    if (kg < 16) {
+      hx[2 * kg] = hp4[(2 * kg) * 64];
+      hx[2 * kg + 1] = hp4[(2 * kg + 1) * 64];
+    }
+#endif
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -885,13 +1297,15 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_dgrad(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[ob][r] = 0.0f;
     const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
-    gemm_t_mem(acc, ring, reinterpret_cast<const f32x4*>(gin + tile * TILE_FLOATS) + lane,
-               reinterpret_cast<const f32x4*>(gin + nxt * TILE_FLOATS) + lane, w4 + wofs, prev_out, st);
-    const bool valid = tile * 32 + li < n;
     const f32x4* hp4 = reinterpret_cast<const f32x4*>(hprev + tile * TILE_FLOATS) + lane;
     f32x4 hx[32];
+    gemm_t_mem(acc, ring, reinterpret_cast<const f32x4*>(gin + tile * TILE_FLOATS) + lane,
+               reinterpret_cast<const f32x4*>(gin + nxt * TILE_FLOATS) + lane, w4 + wofs, prev_out, st, hp4, hx);
+    const bool valid = tile * 32 + li < n;
+#if !PCN_DGRAD_PF
 #pragma unroll
     for (int g = 0; g < 32; ++g) hx[g] = hp4[g * 64];
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -15,7 +15,8 @@ from nof import _hip as H  # noqa: E402
 from nof import _ops, synthetic as syn  # noqa: E402
 from nof.networks import NOF_coarse  # noqa: E402
 
-TAGS = {0: "eval", 1: "hidden", 2: "first", 3: "skip", 4: "out", 5: "fold"}
+TAGS = {0: "eval", 1: "hidden", 2: "first", 3: "skip", 4: "out", 5: "fold", 10: "wgrad", 11: "dgrad",
+        12: "bwd_other"}
 
 
 def load(path):
@@ -47,12 +48,29 @@ def main():
     packed = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_eval_packed_floats(), device=dev)
     st = torch.cuda.current_stream().cuda_stream
     res = {k: {t: [] for t in TAGS} for k in Ls}
+    outs, gouts = {}, {}
+    bwd = os.environ.get("VB_BWD", "1") == "1"
+    if bwd:   # backward on a quarter of the rays (its workspace holds all 8 layers of a chunk)
+        rays_b, z_b = rays[: rays_n // 4].contiguous(), z[: rays_n // 4].contiguous()
+        g_logit = torch.randn(z_b.shape, generator=torch.Generator().manual_seed(3)).to(dev) * 1e-3
+        wsb = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_backward_workspace_bytes(262144), dtype=torch.uint8,
+                          device=dev)
     for rnd in range(4):
         for name, L in Ls.items():
             L.pcnerf_prof_enable(1)
             rc = L.pcnerf_nof_query_train(rays.data_ptr(), rays_n, 15, z.data_ptr(), S, 262144, ctypes.byref(s),
-                                          0.1, 1e-5, ws.data_ptr(), ws.numel(), p.data_ptr(), st)
+                                          0.0, 1e-5, ws.data_ptr(), ws.numel(), p.data_ptr(), st)
             assert rc == 0, L.pcnerf_last_error()
+            if rnd == 0:
+                outs[name] = p.clone()   # train-mode query output of this variant (checked against 'base')
+            if bwd:
+                gs, gout = _ops._grads_struct(m, dev)
+                rc = L.pcnerf_nof_query_train_backward(rays_b.data_ptr(), rays_b.shape[0], 15, z_b.data_ptr(), S,
+                                                       262144, ctypes.byref(s), 1e-5, g_logit.data_ptr(),
+                                                       wsb.data_ptr(), wsb.numel(), ctypes.byref(gs), st)
+                assert rc == 0, L.pcnerf_last_error()
+                if rnd == 0:
+                    gouts[name] = gout[3].clone()   # weight gradient of a hidden layer
             m.eval()
             L.pcnerf_nof_pack_eval(ctypes.byref(s), packed.data_ptr(), st)
             L.pcnerf_nof_query_eval(rays.data_ptr(), rays_n, 15, z.data_ptr(), S, packed.data_ptr(), p.data_ptr(), st)
@@ -69,6 +87,14 @@ def main():
     for name in Ls:
         out[name] = {TAGS[t]: {"us": round(sorted(v)[len(v) // 2][0], 1), "TF": round(sorted(v)[len(v) // 2][1], 1)}
                      for t, v in res[name].items() if v}
+    ref = outs.get("base")
+    if ref is not None:
+        for name in Ls:
+            d = (outs[name] - ref).abs() / ref.abs().clamp_min(1e-12)
+            out[name]["max_rel_diff_vs_base"] = float(d.max())
+            if name in gouts:
+                gr = gouts["base"]
+                out[name]["grad_max_rel_diff_vs_base"] = float(((gouts[name] - gr).abs().max() / gr.abs().max()))
     print(json.dumps(out, indent=1))
 
 

@@ -44,8 +44,14 @@ def test_batch_slices_edges():
 def test_view_rows_and_render_on_fixture(tmp_path):
     from test_dataset import write_scene, oracle_poses, DS, DE, KW, INTEREST
     from oracle import rays_cpu as RC
+    from nof import io as nio
+    from nof import synthetic as syn
+    from nof.networks import NOF_coarse, NOF_fine
     root, pose_path, g = write_scene(str(tmp_path))
-    args = f"""--dataset kitti --root_dir {root} --pose_path {pose_path} --data_start {DS} --data_end {DE}
+    ckpt = str(tmp_path / "seeded.ckpt")   # fixed weights for every main() call (a fresh NOF is randomly initialised)
+    nio.save_ckpt(ckpt, nof_coarse=syn.load_into(NOF_coarse(), syn.init_nof_params(11)),
+                  nof_fine=syn.load_into(NOF_fine(), syn.init_nof_params(12)))
+    args = f"""--dataset kitti --root_dir {root} --pose_path {pose_path} --data_start {DS} --data_end {DE} --ckpt_path {ckpt}
      --test_data_create 1 --depth_inference_method 2 --result_path {tmp_path}/res --pcd_path {tmp_path}/pcd/v1_
      --N_samples 32 --N_importance 64 --chunk 8192 --range_delete_x 3 --range_delete_y 2 --range_delete_z 1.25
      --over_height 0.168 --over_low -2.0 --interest_x {INTEREST} --interest_y {INTEREST} --use_skip"""
@@ -79,7 +85,6 @@ def test_view_rows_and_render_on_fixture(tmp_path):
     h0 = args.replace("--test_data_create 1", "--test_data_create 0").replace("v1_", "v0_")
     rep0 = E.main(h0.split())
     assert [r["points"] for r in rep] == [r["points"] for r in rep0]
-    from nof import io as nio
     for r in rep:
         x = nio.read_pcd(f"{tmp_path}/pcd/v1_{r['frame']}_two_step.pcd")
         y = nio.read_pcd(f"{tmp_path}/pcd/v0_{r['frame']}_two_step.pcd")
