@@ -9,6 +9,8 @@ loss.  Inputs are resident in HBM before timing starts.
 --mode train_step adds what Lightning does with that loss: loss.backward() through the HIP backward kernels and
 the reference's optimizer step (Adam lr 5e-4, eps 1e-8, weight_decay 1e-3 over both networks, nof_utils.py:162-173)
 -- the end-to-end training iteration of config 3 on config 2's batch.  --mode val: render_rays_val (eval BN).
+--mode view: config 5's two-step coarse-to-fine inference (render_rays_view_0525_2_2, method 2) on 13-column rows
+grouped per LiDAR ray; value counts LiDAR rays (groups), rows_per_gpu the rendered rows.
 
 Multi-GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``): one process per GPU, each
 rank renders its own parent block (own rays, own NOF weights) -- weak scaling with no collective
@@ -42,11 +44,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rays", type=int, default=65536)
+    ap.add_argument("--rays", type=int, default=None,
+                    help="LiDAR rays per GPU (default 65,536; 16,384 ray groups = ~52k two-step rows for --mode view)")
     ap.add_argument("--samples", type=int, default=128)
     ap.add_argument("--importance", type=int, default=256)
     ap.add_argument("--chunk", type=int, default=262144)
-    ap.add_argument("--mode", choices=["train_fwd", "train_step", "val"], default="train_fwd")
+    ap.add_argument("--mode", choices=["train_fwd", "train_step", "val", "view"], default="train_fwd")
     ap.add_argument("--cpu-rays", type=int, default=None,
                     help="bounded CPU-baseline sample (rays; default 4096, 1024 for train_step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -90,18 +93,28 @@ def main():
     from nof.blocks import blocks_of_rank, gather_rows, max_over_ranks
     from nof.criteria import nof_loss
     from nof.networks import Embedding, NOF_coarse, NOF_fine
-    from nof.render import render_rays_train, render_rays_val
+    from nof.render import render_rays_train, render_rays_val, render_rays_view_0525_2_2
 
     # this rank's parent block (one per GPU): its own child layout, rays and coarse/fine weights
     (block,) = blocks_of_rank(rank, world, world)
-    rays = torch.from_numpy(syn.make_rays(a.rays, n_children=32, seed=1000 * block)).to(dev)
+    view = a.mode == "view"
+    if a.rays is None:
+        a.rays = 16384 if view else 65536
+    if view:   # config 5: two-step rows grouped per ray (group sizes of the reference's KITTI test frames)
+        vr, vo, vg = syn.make_view_rows(a.rays, n_children=32, seed=1000 * block)
+        rays = torch.from_numpy(vr).to(dev)
+        other = torch.from_numpy(vo).to(dev)
+        gt = torch.from_numpy(vg).to(dev)
+    else:
+        rays = torch.from_numpy(syn.make_rays(a.rays, n_children=32, seed=1000 * block)).to(dev)
     train = a.mode in ("train_fwd", "train_step")
     grad = a.mode == "train_step"
     mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234 + block)).to(dev).train(train)
     mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678 + block)).to(dev).train(train)
     emb = Embedding(3, 10)
     loss_fn = nof_loss["smoothl1"]()
-    gt = rays[:, 14].contiguous()
+    if not view:
+        gt = rays[:, 14].contiguous()
     opt = None
     if grad:
         params = list(mc.parameters()) + list(mf.parameters())
@@ -119,6 +132,13 @@ def main():
             lrf = 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
             loss = (lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"]
                     + 1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"])
+        elif view:   # eval_kitti_render.py:1147-1161: two-step inference, effective rows' points kept
+            res = render_rays_view_0525_2_2(mc, mf, emb, rays, other, N_samples=a.samples,
+                                            N_importance=a.importance, perturb=0, noise_std=0, chunk=a.chunk,
+                                            depth_inference_method=2)
+            keep = res["rays_effective_flag_fine"].reshape(-1)
+            pts = res["points_inference_fine"][keep]
+            loss = pts.abs().mean()
         else:
             res = render_rays_val(mc, mf, emb, rays, N_samples=a.samples, N_importance=a.importance, perturb=0,
                                   noise_std=0, chunk=a.chunk)
@@ -176,9 +196,9 @@ def main():
     cpu = cdref = None
     if rank == 0 and not a.no_cpu_baseline:
         if a.cpu_rays is None:
-            a.cpu_rays = 1024 if grad else 4096
+            a.cpu_rays = 1024 if grad else 512 if view else 4096
         cpu, ext = cpu_baseline(a, syn)
-        cdref = cd_vs_ref(a, syn, ext, dev)
+        cdref = (cd_vs_ref_view if view else cd_vs_ref)(a, syn, ext, dev)
 
     if rank != 0:
         if dist:
@@ -198,11 +218,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)",
+        "data": ("synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)"
+                 + ("; ray groups with the group-size histogram of the reference's KITTI test frames" if view
+                    else "")),
         "config": {"workload": {"train_fwd": "render_rays_train fwd + range/child losses",
                                 "train_step": "render_rays_train fwd + losses + backward + Adam step",
-                                "val": "render_rays_val fwd"}[a.mode],
+                                "val": "render_rays_val fwd",
+                                "view": "render_rays_view_0525_2_2 two-step inference (method 2) + effective points"
+                                }[a.mode],
                    "rays_per_gpu": a.rays, "N_samples": a.samples, "N_importance": a.importance,
+                   "rows_per_gpu": int(rays.shape[0]),
                    "mlp_samples_per_ray": a.samples + a.samples + a.importance, "chunk": a.chunk,
                    "batchnorm": "train (batch stats per chunk)" if train else "eval (folded)",
                    "segmented_ratio": 0.1 if train else None, "perturb": 1 if train else 0,
@@ -229,6 +254,8 @@ def cpu_baseline(a, syn):
     from oracle import ref_cpu as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
+    if a.mode == "view":
+        return cpu_baseline_view(a, syn, O, threads)
     rays = torch.from_numpy(syn.make_rays(a.cpu_rays, n_children=32, seed=0))
     Pc = O.params_from_numpy(syn.init_nof_params(1234))
     Pf = O.params_from_numpy(syn.init_nof_params(5678))
@@ -270,6 +297,48 @@ def cpu_baseline(a, syn):
             "sample": f"{a.cpu_rays} rays of the same workload ({a.mode}, {a.samples}/{a.importance} samples, "
                       f"chunk {a.chunk}) through oracle/ref_cpu.py on torch CPU, {dt:.1f} s"}
     return base, {"rays": rays, "draws": draws, "depth_fine": res["depth_fine"].detach()}
+
+
+def cpu_baseline_view(a, syn, O, threads):
+    """Two-step inference (render.py:614-699 restated in oracle/ref_cpu.py) on ``--cpu-rays`` ray groups."""
+    vr, vo, _ = syn.make_view_rows(a.cpu_rays, n_children=32, seed=0)
+    rows, other = torch.from_numpy(vr), torch.from_numpy(vo)
+    Pc = O.params_from_numpy(syn.init_nof_params(1234))
+    Pf = O.params_from_numpy(syn.init_nof_params(5678))
+    with torch.no_grad():
+        O.render_rays_view(Pc, Pf, rows[:16], torch.zeros(16, dtype=torch.int64), a.samples, a.importance, a.chunk,
+                           method=2)   # warm-up
+        t0 = time.perf_counter()
+        res = O.render_rays_view(Pc, Pf, rows, other, a.samples, a.importance, a.chunk, method=2)
+        dt = time.perf_counter() - t0
+    base = {"value": round(a.cpu_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{a.cpu_rays} ray groups ({rows.shape[0]} two-step rows, {a.samples}/{a.importance} samples, "
+                      f"method 2) through oracle/ref_cpu.py on torch CPU, {dt:.1f} s"}
+    return base, {"rows": rows, "other": other, "res": res}
+
+
+def cd_vs_ref_view(a, syn, ext, dev):
+    """HIP two-step inference on the CPU sample's rows vs the oracle: effective-row flags must agree; CD / F-score
+    of the effective rows' fine points (what eval_kitti_render.py writes to the PCD)."""
+    from nof import metrics as NM
+    from nof.networks import Embedding, NOF_coarse, NOF_fine
+    from nof.render import render_rays_view_0525_2_2
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234)).to(dev).eval()
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678)).to(dev).eval()
+    rows, other, ref = ext["rows"].to(dev), ext["other"].to(dev), ext["res"]
+    with torch.no_grad():
+        res = render_rays_view_0525_2_2(mc, mf, Embedding(3, 10), rows, other, N_samples=a.samples,
+                                        N_importance=a.importance, perturb=0, noise_std=0, chunk=a.chunk,
+                                        depth_inference_method=2)
+    fh = res["rays_effective_flag_fine"].reshape(-1).cpu()
+    fr = ref["rays_effective_flag_fine"].reshape(-1)
+    p_hip = res["points_inference_fine"][fh.to(dev)]
+    p_ref = ref["points_inference_fine"][fr].to(dev)
+    cd, f = NM.eval_pts(p_hip, p_ref, 0.2)
+    d_hip, d_ref = res["depth_fine"].cpu(), ref["depth_fine"]
+    rel = float(((d_hip - d_ref).abs() / d_ref.abs().clamp_min(1e-6)).max())
+    return {"cd_m": cd, "fscore": f, "max_rel_depth_err": rel, "flags_equal": bool(torch.equal(fh, fr)),
+            "rays": int(rows.shape[0]), "vs": "oracle two-step points of the effective rows (same rows and weights)"}
 
 
 def cd_vs_ref(a, syn, ext, dev):
