@@ -201,11 +201,15 @@ int pcnerf_view_walk(const int64_t* other, int64_t n_rows, const uint8_t* at_pea
  * float64 inputs: points (n,3) and origin (3) of one LiDAR frame in the block frame, child boxes as bounds6
  * (C,6) = [xmin,ymin,zmin,xmax,ymax,zmax] (already grown by 0.025), centers (C,3), parent6 (6) the parent block.
  * Train/val 15-column rows (nof/dataset/ipb2dmapping.py:736-768): rows needs n_points*15 floats; the row count
- * (points in a child box whose box the ray enters) is written to *n_rows (device int64). */
+ * is written to *n_rows (device int64).  face_rule 0 = compute_far_bound0606 (KITTI, :119-172: min/max of every
+ * face hit, rays that hit no face are dropped); 1 = compute_far_bound0406 (MaiCity, :82-114, :383-395: the first
+ * two hits, every point in a child box yields a row; rays with fewer than two hits -- the reference's IndexError
+ * -- are counted in *n_short, a device int, so the caller can raise). */
 size_t pcnerf_rays_workspace_bytes(int64_t n_points);
 int pcnerf_build_train_rays(const double* points, int64_t n_points, const double* origin, const double* centers,
                             const double* bounds6, int64_t n_children, const double* parent6, double surface_expand,
-                            void* workspace, float* rows, int64_t* n_rows, void* stream);
+                            int face_rule, void* workspace, float* rows, int64_t* n_rows, int* n_short,
+                            void* stream);
 /* Two-step 13-column rows grouped per ray (eval_kitti_render.py:675-803; method 2 = every child hit, method 1 =
  * first hit with parent bounds): count pass (writes *n_rows, device int64) then emit pass with the same workspace;
  * ranges (M), other_interest_sub_nerf_number (M, int64), true_in (M, bool). */

@@ -114,3 +114,23 @@ def batch_slices(rows_last_col, batch_size_set):
             out.append((i, n))
             i = n
     return out
+
+
+def filter_scan_maicity(pts32, range_delete):
+    """ipb2dmapping.py:318-330 (MaiCity): ego box, norm < 120 (strict); no height filter."""
+    out = []
+    dx, dy, dz = range_delete
+    for p in np.asarray(pts32, dtype=np.float32):
+        if abs(p[0]) < dx and abs(p[1]) < dy and abs(p[2]) < dz:
+            continue
+        sq = p * p
+        if not np.sqrt((sq[0] + sq[1]) + sq[2]) < np.float32(120):
+            continue
+        out.append(p)
+    return np.asarray(out, dtype=np.float32).reshape(-1, 3)
+
+
+def in_parent_box(pts, lo, hi):
+    """ipb2dmapping.py:336-338 (MaiCity): inclusive box test."""
+    keep = [p for p in pts if all(lo[a] <= p[a] <= hi[a] for a in range(3))]
+    return np.asarray(keep, dtype=np.float64).reshape(-1, 3)

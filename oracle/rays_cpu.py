@@ -38,6 +38,16 @@ def far_bound_0606(p, d, lo, hi):
     return True, min(h), max(h)
 
 
+def far_bound_0406(p, d, lo, hi):
+    """ipb2dmapping.py:82-114 (MaiCity): the FIRST two face hits in face order, swapped if needed; fewer than
+    two hits make the reference raise IndexError -> (False, 0, 0) here."""
+    h = face_hits(p, d, lo, hi)
+    if len(h) < 2:
+        return False, 0.0, 0.0
+    a, b = h[0], h[1]
+    return True, min(a, b), max(a, b)
+
+
 def far_bound_0429(p, d, lo, hi):
     """eval_kitti_render.py:170-211: exactly two face hits or no intersection."""
     h = face_hits(p, d, lo, hi)
@@ -101,9 +111,10 @@ def rays_of(points, origin):
     return dirs, rng
 
 
-def build_train_rays(points, origin, centers, bounds6, parent_lo, parent_hi, surface_expand=0.05):
+def build_train_rays(points, origin, centers, bounds6, parent_lo, parent_hi, surface_expand=0.05, rule="0606"):
     """ipb2dmapping.py:736-768 + 819-824 for one frame: float32 (N', 15) rows of the points that fall in a
-    child box (KD-tree lookup) whose box the ray enters."""
+    child box (KD-tree lookup) whose box the ray enters.  rule "0406" (MaiCity, :383-395): every point in a child
+    box yields a row, near/far from the first two face hits (a ray with fewer raises, as the reference does)."""
     tree = KDTree(centers)
     dirs, rng = rays_of(points, origin)
     rows = []
@@ -112,9 +123,14 @@ def build_train_rays(points, origin, centers, bounds6, parent_lo, parent_hi, sur
         if k is None:
             continue
         d = dirs[i]
-        hit, near, far = far_bound_0606(origin, d, bounds6[k][:3], bounds6[k][3:6])
-        if not hit:
-            continue
+        if rule == "0406":
+            hit, near, far = far_bound_0406(origin, d, bounds6[k][:3], bounds6[k][3:6])
+            if not hit:
+                raise IndexError("compute_far_bound0406: fewer than two face hits")
+        else:
+            hit, near, far = far_bound_0606(origin, d, bounds6[k][:3], bounds6[k][3:6])
+            if not hit:
+                continue
         near, far = near - surface_expand, far + surface_expand
         pf = far_bound_parent(origin, d, parent_lo, parent_hi)
         pf = np.nan if pf is None else pf

@@ -75,9 +75,9 @@ __device__ __forceinline__ void ray_of(const double* q, const double (&o)[3], do
 __global__ __launch_bounds__(256) void k_train_rays(int pass, const double* __restrict__ pts, int64_t n,
                                                     const double* __restrict__ origin, const double* __restrict__ ctr,
                                                     const double* __restrict__ b6, int64_t C,
-                                                    const double* __restrict__ P6, double se,
+                                                    const double* __restrict__ P6, double se, int rule,
                                                     int* __restrict__ cnt, const int64_t* __restrict__ off,
-                                                    float* __restrict__ rows) {
+                                                    float* __restrict__ rows, int* __restrict__ nshort) {
   __shared__ double sc[CTILE * 3];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < n;
@@ -139,7 +139,17 @@ __global__ __launch_bounds__(256) void k_train_rays(int pass, const double* __re
   if (child >= 0) {
     double h[6];
     const int nh = face_hits(o, d, b6 + 6 * child, b6 + 6 * child + 3, h);
-    if (nh > 0) {
+    if (rule == 1) {
+      // compute_far_bound0406 (MaiCity, ipb2dmapping.py:82-114): the first two hits in face order; every point in a
+      // child box yields a row; fewer than two hits is the reference's IndexError (counted, the caller raises)
+      ok = 1;
+      if (nh >= 2) {
+        near = h[0] < h[1] ? h[0] : h[1];
+        far = h[0] < h[1] ? h[1] : h[0];
+      } else if (pass == 0) {
+        atomicAdd(nshort, 1);
+      }
+    } else if (nh > 0) {  // compute_far_bound0606 (KITTI, :119-172): min / max over all hits, none -> dropped
       ok = 1;
       near = h[0];
       far = h[0];
@@ -335,21 +345,24 @@ extern "C" size_t pcnerf_rays_workspace_bytes(int64_t n_points) {
 
 extern "C" int pcnerf_build_train_rays(const double* points, int64_t n_points, const double* origin,
                                        const double* centers, const double* bounds6, int64_t n_children,
-                                       const double* parent6, double surface_expand, void* workspace, float* rows,
-                                       int64_t* n_rows, void* stream) {
+                                       const double* parent6, double surface_expand, int face_rule, void* workspace,
+                                       float* rows, int64_t* n_rows, int* n_short, void* stream) {
   PCN_API_BEGIN
   PCN_CHECK(points && origin && centers && bounds6 && parent6 && workspace && rows && n_rows,
             "pcnerf_build_train_rays: null argument");
   PCN_CHECK(n_points > 0 && n_children >= KNN, "pcnerf_build_train_rays: need points and >= 10 child boxes");
+  PCN_CHECK(face_rule == 0 || (face_rule == 1 && n_short),
+            "pcnerf_build_train_rays: face_rule must be 0 (0606) or 1 (0406, with n_short)");
   hipStream_t s = (hipStream_t)stream;
   int64_t* off = (int64_t*)workspace;
   int* cnt = (int*)(off + n_points + 1);
   const dim3 g((unsigned)((n_points + 255) / 256)), b(256);
+  if (n_short) PCN_HIP(hipMemsetAsync(n_short, 0, sizeof(int), s));
   hipLaunchKernelGGL(k_train_rays, g, b, 0, s, 0, points, n_points, origin, centers, bounds6, n_children, parent6,
-                     surface_expand, cnt, (const int64_t*)nullptr, rows);
+                     surface_expand, face_rule, cnt, (const int64_t*)nullptr, rows, n_short);
   hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, cnt, n_points, off);
   hipLaunchKernelGGL(k_train_rays, g, b, 0, s, 1, points, n_points, origin, centers, bounds6, n_children, parent6,
-                     surface_expand, cnt, off, rows);
+                     surface_expand, face_rule, cnt, off, rows, n_short);
   PCN_HIP(hipMemcpyAsync(n_rows, off + n_points, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
   PCN_LAUNCH_CHECK("pcnerf_build_train_rays");
   PCN_API_END

@@ -65,7 +65,7 @@ _SIGS = {
     "pcnerf_view_walk_workspace_bytes": (c_size, [i64]),
     "pcnerf_view_walk": (c_int, [vp, i64, vp, vp, vp, c_int, vp, vp, vp, vp]),
     "pcnerf_rays_workspace_bytes": (c_size, [i64]),
-    "pcnerf_build_train_rays": (c_int, [vp, i64, vp, vp, vp, i64, vp, ctypes.c_double, vp, vp, vp, vp]),
+    "pcnerf_build_train_rays": (c_int, [vp, i64, vp, vp, vp, i64, vp, ctypes.c_double, c_int, vp, vp, vp, vp, vp]),
     "pcnerf_count_view_rows": (c_int, [vp, i64, vp, vp, i64, vp, c_int, vp, vp, vp]),
     "pcnerf_emit_view_rows": (c_int, [vp, i64, vp, vp, i64, vp, c_int, vp, vp, vp, vp, vp, vp]),
     "pcnerf_prof_enable": (c_int, [c_int]),

@@ -1,4 +1,5 @@
-"""Scene datasets -- drop-in for ``nof/dataset`` (``nof_dataset`` registry, ``kitti_dataload``), built on the GPU.
+"""Scene datasets -- drop-in for ``nof/dataset`` (``nof_dataset`` registry: ``kitti_dataload``,
+``maicity_dataload``), built on the GPU.
 
 The reference builds its training rays in ``nof/dataset/ipb2dmapping.py`` with open3d / python-pcl and per-point
 Python loops (minutes per frame).  Here every stage is a device tensor op or a HIP kernel:
@@ -266,4 +267,102 @@ class kitti_dataload(torch.utils.data.Dataset):
         return {'rays': self.rays[i], 'ranges': self.ranges[i]}
 
 
-nof_dataset = {'kitti_dataload': kitti_dataload}
+def read_poses_raw(pose_path: str) -> np.ndarray:
+    """MaiCity poses.txt -> (N, 4, 4) float64 absolute poses, no calibration (ipb2dmapping.py:236-246)."""
+    out = []
+    with open(pose_path, "r", encoding="utf-8") as fh:
+        for line in fh:
+            s = line.strip()
+            if s:
+                out.append(np.vstack([np.array([float(v) for v in s.split(" ")]).reshape(3, 4), [[0.0, 0.0, 0.0, 1.0]]]))
+    return np.asarray(out)
+
+
+def filter_scan_maicity(pts: torch.Tensor, range_delete=(2.0, 1.0, 0.5), max_range=120.0) -> torch.Tensor:
+    """ipb2dmapping.py:318-330: the ego box and norms >= 120 m (strict) go; no height filter."""
+    p = pts.to(torch.float32)
+    dx, dy, dz = (float(v) for v in range_delete)
+    keep = (p[:, 0].abs() >= dx) | (p[:, 1].abs() >= dy) | (p[:, 2].abs() >= dz)
+    sq = p * p
+    keep &= torch.sqrt((sq[:, 0] + sq[:, 1]) + sq[:, 2]) < max_range
+    return p[keep]
+
+
+def in_box(pts: torch.Tensor, lo, hi) -> torch.Tensor:
+    """ipb2dmapping.py:336-338: inclusive parent-box test in float64."""
+    lo = torch.as_tensor(lo, dtype=torch.float64, device=pts.device)
+    hi = torch.as_tensor(hi, dtype=torch.float64, device=pts.device)
+    return ((pts >= lo) & (pts <= hi)).all(1)
+
+
+class maicity_dataload(torch.utils.data.Dataset):
+    """ipb2dmapping.py:200-507 with the reference's constructor keywords: absolute poses (pose j for file j+1, no
+    calibration), the parent block given by nerf_{length,width,height}_{min,max}, scans cut to that block, child
+    near/far by compute_far_bound0406 (face_rule "0406": every point in a child box yields a row; a ray with fewer
+    than two face hits raises IndexError, as in the reference).  val frames: (j+1-3-data_start) % 5 == 0.
+    Extra keywords as kitti_dataload (``device``, ``sparsity``, ``children``)."""
+
+    def __init__(self, root_dir, split='train', data_start=0, data_end=36, cloud_size_val=2048, range_delete_x=2,
+                 range_delete_y=1, range_delete_z=0.5, sub_nerf_test_num=3, surface_expand=0.1, nerf_length_min=-4.5,
+                 nerf_length_max=25.5, nerf_width_min=-12, nerf_width_max=12, nerf_height_min=-2, nerf_height_max=0.5,
+                 pose_path=None, subnerf_path=None, re_loaddata=0, result_path=None, *, device="cuda", sparsity=20,
+                 children=None):
+        super().__init__()
+        self.split, self.cloud_size_val = split, cloud_size_val
+        self.device = torch.device(device)
+        cache = os.path.join(result_path, "save_npy", "split_child_nerf2_3") if result_path else None
+        if not re_loaddata:
+            if cache is None:
+                raise ValueError("re_loaddata=0 needs result_path holding save_npy/split_child_nerf2_3")
+            rays, ranges = nio.load_rays(cache, split)
+            self.rays = torch.from_numpy(rays).to(self.device)
+            self.ranges = torch.from_numpy(ranges.reshape(-1)).to(self.device)
+            return
+        rd = (range_delete_x, range_delete_y, range_delete_z)
+        lo = (nerf_length_min, nerf_width_min, nerf_height_min)
+        hi = (nerf_length_max, nerf_width_max, nerf_height_max)
+        parent6 = torch.tensor([*lo, *hi], dtype=torch.float64, device=self.device)
+        P64 = read_poses_raw(pose_path)
+        self.poses = torch.tensor(P64, dtype=torch.float32)      # torch.Tensor(poses), ipb2dmapping.py:247
+        positions = P64[:, :3, 3]                                 # float64 (numpy), ipb2dmapping.py:245
+
+        def frame(j):
+            p = filter_scan_maicity(torch.from_numpy(load_frame(root_dir, j + 1)).to(self.device), rd)
+            w = to_block(p, self.poses[j])
+            return w[in_box(w, lo, hi)]
+
+        if split == "train":
+            rule = SPARSITY_RULES[int(sparsity)]
+            frames = [j for j in range(data_start, data_end) if rule(j, data_start)]
+        elif split == "val":
+            frames = [j for j in range(data_start, data_end) if (j + 1 - 3 - data_start) % 5 == 0]
+        else:
+            raise ValueError(f"split must be 'train' or 'val', got {split!r}")
+        if children is None:
+            if subnerf_path and os.path.isdir(subnerf_path):
+                children = load_children(subnerf_path, sub_nerf_test_num, self.device)
+            else:   # the block's training frames, split like split_child_nerf_xyz.py (child clouds not shipped)
+                rule = SPARSITY_RULES[int(sparsity)]
+                cloud = torch.cat([frame(j) for j in range(data_start, data_end) if rule(j, data_start)])
+                self.parent_cloud = cloud.to(torch.float32)
+                children = split_children(self.parent_cloud)
+        self.bounds6, self.centers = child_boxes(*(torch.as_tensor(c, dtype=torch.float64).to(self.device)
+                                                   for c in children))
+        self.sub_nerf_test_num = self.bounds6.shape[0]
+        from .raytable import build_train_rays
+        rays = []
+        for j in frames:
+            origin = torch.tensor(positions[j], dtype=torch.float64, device=self.device)
+            rays.append(build_train_rays(frame(j), origin, self.centers, self.bounds6, parent6, surface_expand,
+                                         face_rule="0406"))
+        self.rays = torch.cat(rays) if rays else torch.zeros((0, 15), device=self.device)
+        self.ranges = self.rays[:, 14].clone()
+        if cache is not None:
+            nio.save_rays(cache, self.rays.cpu().numpy(), self.ranges.cpu().numpy(), split)
+
+    val_index = kitti_dataload.val_index
+    __len__ = kitti_dataload.__len__
+    __getitem__ = kitti_dataload.__getitem__
+
+
+nof_dataset = {'kitti_dataload': kitti_dataload, 'maicity_dataload': maicity_dataload}

@@ -20,16 +20,27 @@ def _f64(t):
     return t.to(torch.float64).contiguous()
 
 
-def build_train_rays(points, origin, centers, bounds6, parent6, surface_expand=0.05) -> torch.Tensor:
+FACE_RULES = {"0606": 0, "0406": 1}   # compute_far_bound0606 (KITTI) / compute_far_bound0406 (MaiCity)
+
+
+def build_train_rays(points, origin, centers, bounds6, parent6, surface_expand=0.05, face_rule="0606") -> torch.Tensor:
+    """15-column rows of one frame.  face_rule "0606" (kitti_dataload) drops rays that hit no face of their child
+    box; "0406" (maicity_dataload) keeps every point in a child box and, like the reference's IndexError, raises
+    when a ray hits fewer than two faces."""
     points, origin, centers, bounds6, parent6 = map(_f64, (points, origin, centers, bounds6, parent6))
     n, C = points.shape[0], bounds6.shape[0]
     L = H.lib()
     rows = torch.empty((n, 15), dtype=torch.float32, device=points.device)
     cnt = torch.empty((1,), dtype=torch.int64, device=points.device)
+    short = torch.zeros((1,), dtype=torch.int32, device=points.device)
     ws = _workspace(points.device, L.pcnerf_rays_workspace_bytes(n))
     H.check(L.pcnerf_build_train_rays(points.data_ptr(), n, origin.data_ptr(), centers.data_ptr(), bounds6.data_ptr(),
-                                      C, parent6.data_ptr(), float(surface_expand), ws.data_ptr(), rows.data_ptr(),
-                                      cnt.data_ptr(), H.stream_of(points)))
+                                      C, parent6.data_ptr(), float(surface_expand), FACE_RULES[face_rule],
+                                      ws.data_ptr(), rows.data_ptr(), cnt.data_ptr(), short.data_ptr(),
+                                      H.stream_of(points)))
+    if face_rule == "0406" and int(short):
+        raise IndexError(f"compute_far_bound0406: {int(short)} ray(s) hit fewer than two faces of their child box "
+                         "(the reference raises IndexError here)")
     return rows[:int(cnt)]
 
 

@@ -71,16 +71,21 @@ class NOFSystem:
         h = self.hparams
         if self.train_dataset is not None:
             return
-        if h.datasettype != "kitti_dataload":
-            raise NotImplementedError(f"datasettype {h.datasettype!r}: this build implements kitti_dataload")
-        kwargs = dict(root_dir=h.root_dir, data_start=h.data_start, data_end=h.data_end,
+        common = dict(root_dir=h.root_dir, data_start=h.data_start, data_end=h.data_end,
                       cloud_size_val=h.cloud_size_val, range_delete_x=h.range_delete_x,
                       range_delete_y=h.range_delete_y, range_delete_z=h.range_delete_z,
-                      sub_nerf_test_num=h.sub_nerf_test_num, parentnerf_path=h.parentnerf_path,
-                      pose_path=h.pose_path, subnerf_path=h.subnerf_path, surface_expand=h.surface_expand,
-                      interest_x=h.interest_x, interest_y=h.interest_y, over_height=h.over_height,
-                      over_low=h.over_low, re_loaddata=h.re_loaddata, result_path=h.result_path,
+                      sub_nerf_test_num=h.sub_nerf_test_num, pose_path=h.pose_path, subnerf_path=h.subnerf_path,
+                      surface_expand=h.surface_expand, re_loaddata=h.re_loaddata, result_path=h.result_path,
                       device=self.device, sparsity=h.frame_sparsity)
+        if h.datasettype == "kitti_dataload":
+            kwargs = dict(common, parentnerf_path=h.parentnerf_path, interest_x=h.interest_x,
+                          interest_y=h.interest_y, over_height=h.over_height, over_low=h.over_low)
+        elif h.datasettype == "maicity_dataload":
+            kwargs = dict(common, nerf_length_min=h.nerf_length_min, nerf_length_max=h.nerf_length_max,
+                          nerf_width_min=h.nerf_width_min, nerf_width_max=h.nerf_width_max,
+                          nerf_height_min=h.nerf_height_min, nerf_height_max=h.nerf_height_max)
+        else:
+            raise NotImplementedError(f"datasettype {h.datasettype!r}: kitti_dataload or maicity_dataload")
         ds = nof_dataset[h.datasettype]
         self.train_dataset = ds(split='train', **kwargs)
         self.val_dataset = ds(split='val', **kwargs)

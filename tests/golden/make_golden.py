@@ -266,8 +266,13 @@ def gen_aabb():
         parent_far.append(np.nan if t is None else t)
     # face-hit tests against the point's own box and a random box
     other_box = rng.integers(0, len(boxes), size=n)
-    f0606, f0429 = [], []
+    f0606, f0429, f0406 = [], [], []
     for i in range(n):
+        try:   # MaiCity's rule: the first two face hits; fewer than two raise IndexError in the reference
+            a4, z4 = F["compute_far_bound0406"](origin, dirs[i], lo[cid[i]], hi[cid[i]])
+            f0406.append([1.0, a4, z4])
+        except IndexError:
+            f0406.append([0.0, 0.0, 0.0])
         row = []
         for b in (cid[i], other_box[i]):
             hit, a, z = F["compute_far_bound0606"](origin, dirs[i], lo[b], hi[b])
@@ -279,7 +284,7 @@ def gen_aabb():
     d2r = np.stack([F["distance_to_ray"](torch.from_numpy(origin), dirs[i], centers) for i in range(0, n, 37)])
     save("aabb_primitives", boxes=boxes, lo=lo, hi=hi, centers=centers, origin=origin, points=pts, cid=cid,
          other_box=other_box, find_inside=np.array(inside), find_idx=np.array(idx), parent_far=np.array(parent_far),
-         f0606=np.array(f0606), f0429=np.array(f0429), slab=slab, d2r=d2r)
+         f0606=np.array(f0606), f0429=np.array(f0429), f0406=np.array(f0406), slab=slab, d2r=d2r)
 
 
 GRAD_CASES = {"pcnerf": (1, 1, 0), "divide": (1, 1, 1), "original": (0, 0, 0)}
@@ -376,7 +381,18 @@ def gen_kitti_frames(step=40):
     save("kitti_frames", poses=poses, pose_first=np.array(1150), **frames)
 
 
+def gen_maicity_frames(step=40):
+    """MaiCity-00 scans 1..6 of the reference's data/maicity/00/pcd (every ``step``-th point) and poses.txt rows
+    0..6, for maicity_dataload."""
+    frames = {f"f{f}": raw_pcd(os.path.join(REF, f"data/maicity/00/pcd/{f}.pcd"))[::step] for f in range(1, 7)}
+    with open(os.path.join(REF, "data/maicity/00/poses.txt")) as fh:
+        rows = [ln.strip() for ln in fh if ln.strip()]
+    poses = np.array([[float(v) for v in rows[i].split(" ")] for i in range(0, 7)])
+    save("maicity_frames", poses=poses, **frames)
+
+
 if __name__ == "__main__":
+    gen_maicity_frames()
     gen_kitti_frames()
     gen_metrics()
     gen_grads()

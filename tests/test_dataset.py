@@ -141,3 +141,72 @@ def test_kitti_dataload_rays_match_oracle(tmp_path):
     np.testing.assert_array_equal(b["rays"].cpu().numpy(), va.rays.cpu().numpy()[OD.val_index(len(va.rays), 64)])
     again = D.kitti_dataload(root, split="train", **{**kw, "re_loaddata": 0})
     assert torch.equal(again.rays, tr.rays)
+
+
+# ----------------------------------------------------------------------------------------------- MaiCity
+M_LO, M_HI = (-12.0, -12.0, -2.0), (61.0, 12.0, 0.5)     # shells/pretraining/MaiCity00_pcnerf_train.bash
+M_RD = (2.0, 1.0, 0.5)
+
+
+def write_maicity(tmp):
+    g = golden("maicity_frames")
+    os.makedirs(os.path.join(tmp, "pcd"), exist_ok=True)
+    for k, v in g.items():
+        if k.startswith("f"):
+            nio.write_pcd(os.path.join(tmp, "pcd", f"{k[1:]}.pcd"), v)
+    with open(os.path.join(tmp, "poses.txt"), "w") as fh:
+        for row in g["poses"]:
+            fh.write(" ".join(repr(float(v)) for v in row) + "\n")
+    return os.path.join(tmp, "pcd"), os.path.join(tmp, "poses.txt"), g
+
+
+def test_maicity_host_stages_match_oracle(tmp_path):
+    _, pose_path, g = write_maicity(str(tmp_path))
+    P = D.read_poses_raw(pose_path)
+    np.testing.assert_array_equal(P[:, :3, :].reshape(len(P), 12), g["poses"])
+    P32 = torch.tensor(P, dtype=torch.float32)
+    for j in (0, 2, 4):
+        raw = g[f"f{j + 1}"]
+        got = D.filter_scan_maicity(torch.from_numpy(raw), M_RD)
+        want = OD.filter_scan_maicity(raw, M_RD)
+        np.testing.assert_array_equal(got.numpy(), want)
+        w = D.to_block(got, P32[j])
+        kept = w[D.in_box(w, M_LO, M_HI)].numpy()
+        np.testing.assert_array_equal(kept, OD.in_parent_box(w.numpy(), M_LO, M_HI))
+        assert 0 < len(kept) < len(got)
+
+
+@pytest.mark.gpu
+def test_maicity_dataload_rays_match_oracle(tmp_path):
+    root, pose_path, g = write_maicity(str(tmp_path))
+    kw = dict(data_start=0, data_end=6, cloud_size_val=32, range_delete_x=M_RD[0], range_delete_y=M_RD[1],
+              range_delete_z=M_RD[2], sub_nerf_test_num=0, surface_expand=0.05, nerf_length_min=M_LO[0],
+              nerf_length_max=M_HI[0], nerf_width_min=M_LO[1], nerf_width_max=M_HI[1], nerf_height_min=M_LO[2],
+              nerf_height_max=M_HI[2], pose_path=pose_path, re_loaddata=1, result_path=str(tmp_path / "out"),
+              device="cuda")
+    P = D.read_poses_raw(pose_path)
+    P32 = torch.tensor(P, dtype=torch.float32)
+
+    def oracle_frame(j):
+        p = OD.filter_scan_maicity(g[f"f{j + 1}"], M_RD)
+        return OD.in_parent_box(D.to_block(torch.from_numpy(p), P32[j]).numpy(), M_LO, M_HI)
+
+    frames = [j for j in range(6) if (j + 1 - 3) % 5 != 0]
+    cells = OD.split_children(np.concatenate([oracle_frame(j) for j in frames]).astype(np.float32))
+    b6, cen = OD.child_boxes(cells)
+    want, err = [], None
+    try:
+        for j in frames:
+            want.append(RC.build_train_rays(oracle_frame(j), P[j][:3, 3], cen, b6, np.array(M_LO), np.array(M_HI),
+                                            0.05, rule="0406"))
+    except IndexError as e:       # the reference raises here too; the GPU path must as well
+        err = e
+    if err is not None:
+        with pytest.raises(IndexError):
+            D.maicity_dataload(root, split="train", **kw)
+        return
+    tr = D.maicity_dataload(root, split="train", **kw)
+    got = tr.rays.cpu().numpy()
+    want = np.concatenate(want)
+    assert got.shape == want.shape and len(got) > 100
+    np.testing.assert_array_equal(got, want)

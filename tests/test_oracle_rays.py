@@ -23,6 +23,8 @@ def test_primitives_match_reference():
             row += [float(h), a, z]
             row2.append(list(map(float, RC.far_bound_0429(o, dirs[i], lo[b], hi[b]))))
         np.testing.assert_array_equal(np.array(row), g["f0606"][i])
+        np.testing.assert_array_equal(np.array(list(map(float, RC.far_bound_0406(o, dirs[i], lo[g["cid"][i]],
+                                                                                  hi[g["cid"][i]])))), g["f0406"][i])
         np.testing.assert_array_equal(np.array(row2), g["f0429"][2 * i:2 * i + 2])
     np.testing.assert_array_equal(RC.slab_far(o, dirs, *(np.asarray(x) for x in _parent())), g["slab"])
     d2r = np.stack([RC.distance_to_ray(o, dirs[i], g["centers"]) for i in range(0, len(pts), 37)])
