@@ -212,13 +212,15 @@ int pcnerf_build_train_rays(const double* points, int64_t n_points, const double
                             void* stream);
 /* Two-step 13-column rows grouped per ray (eval_kitti_render.py:675-803; method 2 = every child hit, method 1 =
  * first hit with parent bounds): count pass (writes *n_rows, device int64) then emit pass with the same workspace;
+ * rule 0 = KITTI (expansion step 0.05, column 10 = max(parent far, child far)), 1 = MaiCity (multi_frame_maicity,
+ * eval_kitti_render.py:344-431: step 0.005, column 10 = parent far; pass its child boxes grown by 0.025);
  * ranges (M), other_interest_sub_nerf_number (M, int64), true_in (M, bool). */
 int pcnerf_count_view_rows(const double* points, int64_t n_points, const double* origin, const double* bounds6,
-                           int64_t n_children, const double* parent6, int method, void* workspace, int64_t* n_rows,
-                           void* stream);
+                           int64_t n_children, const double* parent6, int method, int rule, void* workspace,
+                           int64_t* n_rows, void* stream);
 int pcnerf_emit_view_rows(const double* points, int64_t n_points, const double* origin, const double* bounds6,
-                          int64_t n_children, const double* parent6, int method, void* workspace, float* rows,
-                          float* ranges, int64_t* other, uint8_t* true_in, void* stream);
+                          int64_t n_children, const double* parent6, int method, int rule, void* workspace,
+                          float* rows, float* ranges, int64_t* other, uint8_t* true_in, void* stream);
 
 /* ---------------------------------------------------------------- evaluation metrics
  * (nof/criteria/pointcloud_metrics.py:5-49, logs/.../render_result/print_metrics.py:31-133; exhaustive float64

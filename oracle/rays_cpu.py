@@ -140,9 +140,11 @@ def build_train_rays(points, origin, centers, bounds6, parent_lo, parent_hi, sur
     return np.asarray(rows, dtype=np.float64).reshape(-1, 15).astype(np.float32)
 
 
-def build_view_rows(points, origin, bounds6, parent_lo, parent_hi, method=2, radius=0.65):
+def build_view_rows(points, origin, bounds6, parent_lo, parent_hi, method=2, radius=0.65, rule="kitti"):
     """eval_kitti_render.py:675-803 for one frame -> (rows (M, 13) float32, ranges (M,) float32,
-    other (M,) int64, true_in (M,) bool)."""
+    other (M,) int64, true_in (M,) bool).  rule "maicity" (multi_frame_maicity, :344-431): expansion step 0.005
+    instead of 0.05 and column 10 the parent far bound itself (KITTI: max(parent far, child far))."""
+    step = 0.005 if rule == "maicity" else 0.05
     dirs, rng = rays_of(points, origin)
     pfar_all = slab_far(origin, dirs, parent_lo, parent_hi)
     center = (bounds6[:, :3] + bounds6[:, 3:]) / 2
@@ -160,7 +162,7 @@ def build_view_rows(points, origin, bounds6, parent_lo, parent_hi, method=2, rad
                     q = points[i]
                     inside = bool(filt[k][0] <= q[0] <= filt[k][3] and filt[k][1] <= q[1] <= filt[k][4]
                                   and filt[k][2] <= q[2] <= filt[k][5])
-                    adj = b if pfar < b else pfar
+                    adj = pfar if rule == "maicity" else (b if pfar < b else pfar)
                     if method == 1:
                         hits.append([pnear, pfar, adj, inside])
                         return True
@@ -173,7 +175,7 @@ def build_view_rows(points, origin, bounds6, parent_lo, parent_hi, method=2, rad
             if ext > 0.5:
                 drop = True
                 break
-            ext = ext + 0.05
+            ext = ext + step
             filt[:, :3] = filt[:, :3] - ext
             filt[:, 3:6] = filt[:, 3:6] + ext
             found = scan()

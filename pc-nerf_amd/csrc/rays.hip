@@ -194,7 +194,7 @@ struct ViewHit {
 
 __global__ __launch_bounds__(256) void k_view_rays(int pass, const double* __restrict__ pts, int64_t n,
                                                    const double* __restrict__ origin, const double* __restrict__ b6,
-                                                   int64_t C, const double* __restrict__ P6, int method,
+                                                   int64_t C, const double* __restrict__ P6, int method, int rule,
                                                    double radius, int* __restrict__ cnt,
                                                    const int64_t* __restrict__ off, float* __restrict__ rows,
                                                    float* __restrict__ ranges, int64_t* __restrict__ other,
@@ -227,10 +227,10 @@ __global__ __launch_bounds__(256) void k_view_rays(int pass, const double* __res
   const double pnear = 0.0;
   ViewHit hits[HIT_MAX];
   int nh = 0;
-  // expansion rounds: ext_r = ext_{r-1} + 0.05 (float64), the filtered boxes grow by ext_1, then ext_2, ...
-  double ext[12];
-  ext[0] = 0.0;
-  for (int r = 1; r < 12; ++r) ext[r] = ext[r - 1] + 0.05;
+  // expansion rounds: ext_r = ext_{r-1} + step (float64; KITTI 0.05, MaiCity 0.005), the filtered boxes grow by
+  // ext_1, then ext_2, ... (the reference updates them in place); give up once ext > 0.5
+  const double step = rule == 1 ? 0.005 : 0.05;
+  double ext_now = 0.0;
   int rounds = 0;
   bool drop = false;
   for (;;) {
@@ -244,11 +244,14 @@ __global__ __launch_bounds__(256) void k_view_rays(int pass, const double* __res
       const double dr = dist * sqrt(1 - cs * cs);
       if (!(dr <= radius)) continue;
       double lo[3] = {b[0], b[1], b[2]}, hi[3] = {b[3], b[4], b[5]};
-      for (int r = 1; r <= rounds; ++r)
+      double e = 0.0;
+      for (int r = 1; r <= rounds; ++r) {
+        e = e + step;
         for (int a = 0; a < 3; ++a) {
-          lo[a] = lo[a] - ext[r];
-          hi[a] = hi[a] + ext[r];
+          lo[a] = lo[a] - e;
+          hi[a] = hi[a] + e;
         }
+      }
       double h[6];
       if (face_hits(o, d, lo, hi, h) != 2) continue;
       const double a0 = h[0] < h[1] ? h[0] : h[1], a1 = h[0] < h[1] ? h[1] : h[0];
@@ -259,14 +262,15 @@ __global__ __launch_bounds__(256) void k_view_rays(int pass, const double* __res
       ViewHit& H = hits[nh++];
       H.near = method == 1 ? pnear : a0;
       H.far = method == 1 ? pfar : a1;
-      H.col7 = pfar < a1 ? a1 : pfar;
+      H.col7 = rule == 1 ? pfar : (pfar < a1 ? a1 : pfar);   // MaiCity keeps the parent far bound as is
       H.tin = (q[0] >= lo[0] && q[0] <= hi[0] && q[1] >= lo[1] && q[1] <= hi[1] && q[2] >= lo[2] && q[2] <= hi[2]);
     }
     if (nh > 0) break;
-    if (ext[rounds] > 0.5 || rounds >= 11) {
+    if (ext_now > 0.5) {
       drop = true;
       break;
     }
+    ext_now = ext_now + step;
     ++rounds;
   }
   const int k = drop ? 0 : nh;
@@ -370,17 +374,18 @@ extern "C" int pcnerf_build_train_rays(const double* points, int64_t n_points, c
 
 extern "C" int pcnerf_count_view_rows(const double* points, int64_t n_points, const double* origin,
                                       const double* bounds6, int64_t n_children, const double* parent6, int method,
-                                      void* workspace, int64_t* n_rows, void* stream) {
+                                      int rule, void* workspace, int64_t* n_rows, void* stream) {
   PCN_API_BEGIN
   PCN_CHECK(points && origin && bounds6 && parent6 && workspace && n_rows, "pcnerf_count_view_rows: null argument");
   PCN_CHECK(n_points > 0 && n_children > 0, "pcnerf_count_view_rows: empty input");
+  PCN_CHECK(rule == 0 || rule == 1, "pcnerf_count_view_rows: rule must be 0 (KITTI) or 1 (MaiCity)");
   hipStream_t s = (hipStream_t)stream;
   int64_t* off = (int64_t*)workspace;
   int* cnt = (int*)(off + n_points + 1);
   int* ovf = (int*)(cnt + n_points);
   PCN_HIP(hipMemsetAsync(ovf, 0, sizeof(int), s));
   hipLaunchKernelGGL(k_view_rays, dim3((unsigned)((n_points + 255) / 256)), dim3(256), 0, s, 0, points, n_points,
-                     origin, bounds6, n_children, parent6, method, 0.65, cnt, (const int64_t*)nullptr,
+                     origin, bounds6, n_children, parent6, method, rule, 0.65, cnt, (const int64_t*)nullptr,
                      (float*)nullptr, (float*)nullptr, (int64_t*)nullptr, (uint8_t*)nullptr, ovf);
   hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, cnt, n_points, off);
   PCN_HIP(hipMemcpyAsync(n_rows, off + n_points, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
@@ -390,8 +395,8 @@ extern "C" int pcnerf_count_view_rows(const double* points, int64_t n_points, co
 
 extern "C" int pcnerf_emit_view_rows(const double* points, int64_t n_points, const double* origin,
                                      const double* bounds6, int64_t n_children, const double* parent6, int method,
-                                     void* workspace, float* rows, float* ranges, int64_t* other, uint8_t* true_in,
-                                     void* stream) {
+                                     int rule, void* workspace, float* rows, float* ranges, int64_t* other,
+                                     uint8_t* true_in, void* stream) {
   PCN_API_BEGIN
   PCN_CHECK(points && origin && bounds6 && parent6 && workspace && rows && ranges && other && true_in,
             "pcnerf_emit_view_rows: null argument");
@@ -399,7 +404,7 @@ extern "C" int pcnerf_emit_view_rows(const double* points, int64_t n_points, con
   int* cnt = (int*)(off + n_points + 1);
   int* ovf = (int*)(cnt + n_points);
   hipLaunchKernelGGL(k_view_rays, dim3((unsigned)((n_points + 255) / 256)), dim3(256), 0, (hipStream_t)stream, 1,
-                     points, n_points, origin, bounds6, n_children, parent6, method, 0.65, cnt,
+                     points, n_points, origin, bounds6, n_children, parent6, method, rule, 0.65, cnt,
                      (const int64_t*)off, rows, ranges, other, true_in, ovf);
   PCN_LAUNCH_CHECK("pcnerf_emit_view_rows");
   PCN_API_END

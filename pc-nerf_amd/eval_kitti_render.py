@@ -108,10 +108,17 @@ def batch_slices(group_col: np.ndarray, batch_rows: int):
 
 
 class Scene:
-    """Parent box, child boxes (raw, no growth: eval_kitti_render.py:590-603) and poses of one sequence."""
+    """Parent box, child boxes and poses of one sequence.  KITTI (multi_frame_kitti, eval_kitti_render.py:538-881):
+    relative calibrated poses, parent box of the parent cloud, raw child boxes (no growth, :590-603).  MaiCity
+    (multi_frame_maicity, :246-535): absolute poses (pose j for file j+1), the parent box from the command line,
+    child boxes grown by 0.025 (:277-291), scans cut to the parent box."""
 
     def __init__(self, h, device):
         self.h, self.device = h, torch.device(device)
+        self.maicity = h.dataset == "maicity"
+        if self.maicity:
+            self._init_maicity(h)
+            return
         self.poses = D.relative_poses(D.read_poses(h.pose_path), h.data_start)
         rd = (h.range_delete_x, h.range_delete_y, h.range_delete_z)
         if h.parentnerf_path and os.path.exists(h.parentnerf_path):
@@ -127,9 +134,27 @@ class Scene:
             mn, mx = D.split_children(parent)
         self.bounds6 = torch.cat([mn, mx], 1)
 
+    def _init_maicity(self, h):
+        self.lo = (h.nerf_length_min, h.nerf_width_min, h.nerf_height_min)
+        self.hi = (h.nerf_length_max, h.nerf_width_max, h.nerf_height_max)
+        self.parent6 = torch.tensor([*self.lo, *self.hi], dtype=torch.float64, device=self.device)
+        self.poses = torch.tensor(D.read_poses_raw(h.pose_path), dtype=torch.float32)
+        if h.subnerf_path and os.path.isdir(h.subnerf_path):
+            mn, mx = D.load_children(h.subnerf_path, h.sub_nerf_test_num, self.device)
+        else:   # the training frames' cells, as maicity_dataload builds them
+            train = [f for f in range(h.data_start + 1, h.data_end + 1) if (f - 3 - h.data_start) % 5 != 0]
+            mn, mx = D.split_children(torch.cat([self.frame_points(f) for f in train]).to(torch.float32))
+        self.bounds6 = torch.cat([mn - D.CHILD_GROW, mx + D.CHILD_GROW], 1)
+
     def frame_points(self, f):
-        """eval_kitti_render.py:621-660: filtered (strict < 120 m) scan of file f in the block frame."""
+        """eval_kitti_render.py:621-660 (KITTI: filtered, strict < 120 m, interest region) or :315-340 (MaiCity: ego
+        box, < 120 m, cut to the parent box) -- scan of file f in the block frame."""
         h = self.h
+        if self.maicity:
+            raw = torch.from_numpy(D.load_frame(h.root_dir, f)).to(self.device)
+            p = D.filter_scan_maicity(raw, (h.range_delete_x, h.range_delete_y, h.range_delete_z))
+            w = D.to_block(p, self.poses[f - 1])
+            return w[D.in_box(w, self.lo, self.hi)]
         raw = torch.from_numpy(D.load_frame(h.root_dir, f)).to(self.device)
         p = D.filter_scan(raw, (h.range_delete_x, h.range_delete_y, h.range_delete_z), h.over_height, h.over_low,
                           strict_range=True)
@@ -138,8 +163,10 @@ class Scene:
         return w[D.interest_mask(w, pos, h.interest_x, h.interest_y)]
 
     def view_rows(self, f, method):
-        origin = self.poses[f][:3, 3].to(device=self.device, dtype=torch.float64)
-        return build_view_rows(self.frame_points(f), origin, self.bounds6, self.parent6, method=method)
+        pose = self.poses[f - 1] if self.maicity else self.poses[f]
+        origin = pose[:3, 3].to(device=self.device, dtype=torch.float64)
+        return build_view_rows(self.frame_points(f), origin, self.bounds6, self.parent6, method=method,
+                               rule="maicity" if self.maicity else "kitti")
 
 
 def cache_dir(h, f):

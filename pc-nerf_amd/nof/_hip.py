@@ -66,8 +66,8 @@ _SIGS = {
     "pcnerf_view_walk": (c_int, [vp, i64, vp, vp, vp, c_int, vp, vp, vp, vp]),
     "pcnerf_rays_workspace_bytes": (c_size, [i64]),
     "pcnerf_build_train_rays": (c_int, [vp, i64, vp, vp, vp, i64, vp, ctypes.c_double, c_int, vp, vp, vp, vp, vp]),
-    "pcnerf_count_view_rows": (c_int, [vp, i64, vp, vp, i64, vp, c_int, vp, vp, vp]),
-    "pcnerf_emit_view_rows": (c_int, [vp, i64, vp, vp, i64, vp, c_int, vp, vp, vp, vp, vp, vp]),
+    "pcnerf_count_view_rows": (c_int, [vp, i64, vp, vp, i64, vp, c_int, c_int, vp, vp, vp]),
+    "pcnerf_emit_view_rows": (c_int, [vp, i64, vp, vp, i64, vp, c_int, c_int, vp, vp, vp, vp, vp, vp]),
     "pcnerf_prof_enable": (c_int, [c_int]),
     "pcnerf_prof_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),

@@ -44,8 +44,12 @@ def build_train_rays(points, origin, centers, bounds6, parent6, surface_expand=0
     return rows[:int(cnt)]
 
 
-def build_view_rows(points, origin, bounds6, parent6, method=2):
-    """-> (rows (M,13) float32, ranges (M,) float32, other (M,) int64, true_in (M,) bool)."""
+VIEW_RULES = {"kitti": 0, "maicity": 1}
+
+
+def build_view_rows(points, origin, bounds6, parent6, method=2, rule="kitti"):
+    """-> (rows (M,13) float32, ranges (M,) float32, other (M,) int64, true_in (M,) bool).  rule "maicity":
+    multi_frame_maicity's expansion step (0.005) and parent-far column."""
     points, origin, bounds6, parent6 = map(_f64, (points, origin, bounds6, parent6))
     n, C = points.shape[0], bounds6.shape[0]
     L = H.lib()
@@ -54,7 +58,8 @@ def build_view_rows(points, origin, bounds6, parent6, method=2):
     ws = _workspace(dev, L.pcnerf_rays_workspace_bytes(n))
     st = H.stream_of(points)
     H.check(L.pcnerf_count_view_rows(points.data_ptr(), n, origin.data_ptr(), bounds6.data_ptr(), C,
-                                     parent6.data_ptr(), int(method), ws.data_ptr(), cnt.data_ptr(), st))
+                                     parent6.data_ptr(), int(method), VIEW_RULES[rule], ws.data_ptr(), cnt.data_ptr(),
+                                     st))
     m = int(cnt)
     rows = torch.empty((m, 13), dtype=torch.float32, device=dev)
     ranges = torch.empty((m,), dtype=torch.float32, device=dev)
@@ -62,6 +67,7 @@ def build_view_rows(points, origin, bounds6, parent6, method=2):
     tin = torch.empty((m,), dtype=torch.bool, device=dev)
     if m:
         H.check(L.pcnerf_emit_view_rows(points.data_ptr(), n, origin.data_ptr(), bounds6.data_ptr(), C,
-                                        parent6.data_ptr(), int(method), ws.data_ptr(), rows.data_ptr(),
+                                        parent6.data_ptr(), int(method), VIEW_RULES[rule], ws.data_ptr(),
+                                        rows.data_ptr(),
                                         ranges.data_ptr(), other.data_ptr(), tin.data_ptr(), st))
     return rows, ranges, other, tin

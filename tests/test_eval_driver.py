@@ -89,3 +89,30 @@ def test_view_rows_and_render_on_fixture(tmp_path):
         x = nio.read_pcd(f"{tmp_path}/pcd/v1_{r['frame']}_two_step.pcd")
         y = nio.read_pcd(f"{tmp_path}/pcd/v0_{r['frame']}_two_step.pcd")
         assert x.shape == (r["points"], 3) and np.array_equal(x, y)
+
+
+@pytest.mark.gpu
+def test_view_rows_maicity_on_fixture(tmp_path):
+    """MaiCity two-step rows (multi_frame_maicity): expansion step 0.005, parent-far column, boxes grown 0.025."""
+    from test_dataset import write_maicity, M_LO, M_HI, M_RD
+    from oracle import rays_cpu as RC
+    import nof.dataset as D
+    root, pose_path, g = write_maicity(str(tmp_path))
+    args = f"""--dataset maicity --root_dir {root} --pose_path {pose_path} --data_start 0 --data_end 6
+     --range_delete_x {M_RD[0]} --range_delete_y {M_RD[1]} --range_delete_z {M_RD[2]}
+     --nerf_length_min {M_LO[0]} --nerf_length_max {M_HI[0]} --nerf_width_min {M_LO[1]} --nerf_width_max {M_HI[1]}
+     --nerf_height_min {M_LO[2]} --nerf_height_max {M_HI[2]}"""
+    h = E.get_opts(args.split())
+    scene = E.Scene(h, "cuda")
+    f = E.test_frame_ids(0, 6)[0]
+    rows, ranges, other, tin = scene.view_rows(f, 2)
+    P32 = torch.tensor(D.read_poses_raw(pose_path), dtype=torch.float32)
+    pts = OD.in_parent_box(D.to_block(torch.from_numpy(OD.filter_scan_maicity(g[f"f{f}"], M_RD)),
+                                      P32[f - 1]).numpy(), M_LO, M_HI)
+    b6 = scene.bounds6.cpu().numpy()
+    orows, orng, ooth, _ = RC.build_view_rows(pts, P32[f - 1][:3, 3].double().numpy(), b6, np.array(M_LO),
+                                              np.array(M_HI), 2, rule="maicity")
+    assert rows.shape[0] == orows.shape[0] > 50
+    np.testing.assert_array_equal(rows.cpu().numpy(), orows)
+    np.testing.assert_array_equal(other.cpu().numpy(), ooth)
+    np.testing.assert_array_equal(ranges.cpu().numpy(), orng)
