@@ -94,6 +94,21 @@ int pcnerf_nof_query_train_backward(const float* rays, int64_t n_rays, int ray_s
                                     int n_samples, int64_t chunk, const pcnerf_nof_params* params, float eps,
                                     const float* grad_logit, void* workspace, size_t workspace_bytes,
                                     const pcnerf_nof_grads* grads, void* stream);
+/* Activation store (the training step without the backward's recomputation): pcnerf_nof_store_bytes(chunk) bytes
+ * per chunk hold that chunk's raw layer outputs h_1..h_8 and BatchNorm statistics.  The _store forward writes
+ * chunks 0..store_chunks-1 into `store` (results otherwise identical to pcnerf_nof_query_train); the _store
+ * backward reads them instead of recomputing those chunks (the rest are recomputed).  The caller sizes
+ * store_chunks to the HBM it can spare (nof._autograd: what is free after the backward workspace). */
+size_t pcnerf_nof_store_bytes(int64_t chunk);
+int pcnerf_nof_query_train_store(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
+                                 int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
+                                 void* workspace, size_t workspace_bytes, float* p_out, void* store,
+                                 int64_t store_chunks, void* stream);
+int pcnerf_nof_query_train_backward_store(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                          int n_samples, int64_t chunk, const pcnerf_nof_params* params, float eps,
+                                          const float* grad_logit, void* workspace, size_t workspace_bytes,
+                                          const pcnerf_nof_grads* grads, const void* store, int64_t store_chunks,
+                                          void* stream);
 /* NOF.forward(emb) in train mode (one batch): grad_p = dL/dp for p = the forward's output. */
 int pcnerf_nof_forward_train_backward(const float* emb, int64_t n, const pcnerf_nof_params* params, float eps,
                                       const float* p, const float* grad_p, void* workspace, size_t workspace_bytes,

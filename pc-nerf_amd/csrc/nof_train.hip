@@ -758,9 +758,33 @@ using namespace pcn;
 
 extern "C" size_t pcnerf_nof_train_workspace_bytes(int64_t chunk) { return carve(nullptr, chunk).bytes; }
 
+// Activation store of the training step: per chunk the raw h of all 8 layers (the tile layout the backward
+// consumes) and the chunk's BatchNorm statistics, written by the forward so the backward need not recompute.
+struct StoreChunk {
+  float* h[8];
+  double* stats;
+};
+
+static size_t store_layer_bytes(int64_t chunk) {
+  return ((size_t)((chunk + 31) / 32) * TILE_FLOATS * 4 + 255) & ~(size_t)255;
+}
+
+extern "C" size_t pcnerf_nof_store_bytes(int64_t chunk) {
+  return 8 * store_layer_bytes(chunk) + ((8 * 512 * 8 + 255) & ~(size_t)255);
+}
+
+static StoreChunk store_chunk(const void* store, int64_t chunk, int64_t ci) {
+  char* b = (char*)store + (size_t)ci * pcnerf_nof_store_bytes(chunk);
+  StoreChunk c;
+  for (int L = 0; L < 8; ++L) c.h[L] = (float*)(b + L * store_layer_bytes(chunk));
+  c.stats = (double*)(b + 8 * store_layer_bytes(chunk));
+  return c;
+}
+
 static void query_train(const float* rays, int ray_stride, const float* z, int n_samples, const float* ein,
                         int64_t total, int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
-                        void* workspace, size_t workspace_bytes, float* p_out, void* stream) {
+                        void* workspace, size_t workspace_bytes, float* p_out, void* stream,
+                        void* store = nullptr, int64_t store_chunks = 0) {
   const TrainWs ws = carve(workspace, chunk);
   PCN_CHECK(workspace_bytes >= ws.bytes, "pcnerf_nof_query_train: workspace too small");
   NofParamsDev P;
@@ -775,42 +799,51 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     const unsigned maxg = 256u * PCN_TRAIN_WAVES;
     const unsigned grid = (unsigned)(ntiles / 4 + 1 < maxg ? ntiles / 4 + 1 : maxg);
     const double dn = (double)n;
-    PCN_HIP(hipMemsetAsync(ws.stats, 0, 8 * 512 * sizeof(double), s));
-    float* hin = ws.bufA;
-    float* hout = ws.bufB;
+    // stored chunk: every layer writes its own buffer of the store (kept for the backward); else ping-pong
+    const int64_t ci = c0 / chunk;
+    const bool keep = store && ci < store_chunks;
+    const StoreChunk sc = keep ? store_chunk(store, chunk, ci) : StoreChunk{};
+    double* stats = keep ? sc.stats : ws.stats;
+    float* trash = ws.bufA + (size_t)((chunk + 31) / 32) * TILE_FLOATS;
+    PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));
+    float* hin = keep ? sc.h[0] : ws.bufA;
+    float* hout = keep ? sc.h[1] : ws.bufB;
     {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
       hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
                          c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps,
-                         hin, ws.stats);
+                         hin, stats);
     }
     for (int L = 1; L < 8; ++L) {
+      if (keep) {
+        hin = sc.h[L - 1];
+        hout = sc.h[L];
+      }
       const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], P.bn_rm[L - 1], P.bn_rv[L - 1], P.lin_b[L - 1],
-                        ws.stats + 512 * (L - 1)};
+                        stats + 512 * (L - 1)};
       if (L == 4) {
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
         hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
                            c0, n, ein, hin, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
-                           ws.stats + 512 * L);
+                           stats + 512 * L);
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
         if (PCN_HIDDEN_PP)
           hipLaunchKernelGGL(k_train_hidden, dim3(grid), dim3(256), 0, s, hin, n, ws.wp + off_w(L, false),
-                             P.lin_b[L], prev, momentum, eps, hout,
-                             hout + (size_t)((chunk + 31) / 32) * TILE_FLOATS, ws.stats + 512 * L);
+                             P.lin_b[L], prev, momentum, eps, hout, trash, stats + 512 * L);
         else
           hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
                              n_samples, c0, n, ein, hin, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps,
-                             hout, ws.stats + 512 * L);
+                             hout, stats + 512 * L);
       }
       float* t = hin;
       hin = hout;
       hout = t;
     }
     {
-      const BnPrev prev{P.bn_w[7], P.bn_b[7], P.bn_rm[7], P.bn_rv[7], P.lin_b[7], ws.stats + 512 * 7};
+      const BnPrev prev{P.bn_w[7], P.bn_b[7], P.bn_rm[7], P.bn_rv[7], P.lin_b[7], stats + 512 * 7};
       ProfScope ps(s, PT_TRAIN_OUT, 2.0 * 256 * dn, 1028.0 * dn);
       hipLaunchKernelGGL(k_train_out, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, hin, n, prev, momentum,
                          eps, P.out_w, P.out_b, p_out + c0);
@@ -829,6 +862,20 @@ extern "C" int pcnerf_nof_query_train(const float* rays, int64_t n_rays, int ray
   PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train: ray_stride < 6");
   query_train(rays, ray_stride, z, n_samples, nullptr, n_rays * (int64_t)n_samples, chunk, params, momentum, eps,
               workspace, workspace_bytes, p_out, stream);
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_query_train_store(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                            int n_samples, int64_t chunk, const pcnerf_nof_params* params,
+                                            float momentum, float eps, void* workspace, size_t workspace_bytes,
+                                            float* p_out, void* store, int64_t store_chunks, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && workspace && p_out, "pcnerf_nof_query_train_store: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_store: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_store: ray_stride < 6");
+  PCN_CHECK(store_chunks == 0 || store, "pcnerf_nof_query_train_store: store_chunks > 0 needs a store");
+  query_train(rays, ray_stride, z, n_samples, nullptr, n_rays * (int64_t)n_samples, chunk, params, momentum, eps,
+              workspace, workspace_bytes, p_out, stream, store, store_chunks);
   PCN_API_END
 }
 
@@ -1437,7 +1484,8 @@ extern "C" size_t pcnerf_nof_backward_workspace_bytes(int64_t chunk) { return ca
 static void backward_train(const float* rays, int ray_stride, const float* z, int n_samples, const float* ein,
                            int64_t total, int64_t chunk, const pcnerf_nof_params* params, float eps,
                            const float* grad, const float* p, void* workspace, size_t workspace_bytes,
-                           const pcnerf_nof_grads* grads, hipStream_t s) {
+                           const pcnerf_nof_grads* grads, hipStream_t s, const void* store = nullptr,
+                           int64_t store_chunks = 0) {
   const BwdWs ws = carve_bwd(workspace, chunk);
   PCN_CHECK(workspace_bytes >= ws.bytes, "pcnerf_nof_backward: workspace too small");
   NofParamsDev P;
@@ -1456,16 +1504,22 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     const unsigned grid = (unsigned)(ntiles / 4 + 1 < maxg ? ntiles / 4 + 1 : maxg);
     const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
     const unsigned wblocks = (unsigned)(ntiles < WG_BLOCKS ? ntiles : WG_BLOCKS);
-    PCN_HIP(hipMemsetAsync(ws.stats, 0, 8 * 512 * sizeof(double), s));
-    // 1. forward recomputation, every layer's raw h kept
-    {
+    // 1. the forward's layer outputs and statistics: from the activation store, or recomputed here
+    const int64_t ci = c0 / chunk;
+    const bool kept = store && ci < store_chunks;
+    const StoreChunk sc = kept ? store_chunk(store, chunk, ci) : StoreChunk{};
+    float* hh[8];
+    for (int L = 0; L < 8; ++L) hh[L] = kept ? sc.h[L] : ws.h[L];
+    const double* stats = kept ? sc.stats : ws.stats;
+    if (!kept) PCN_HIP(hipMemsetAsync(ws.stats, 0, 8 * 512 * sizeof(double), s));
+    if (!kept) {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
       hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
                          c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps,
                          ws.h[0], ws.stats);
     }
-    for (int L = 1; L < 8; ++L) {
+    for (int L = 1; L < 8 && !kept; ++L) {
       const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], nullptr, nullptr, P.lin_b[L - 1], ws.stats + 512 * (L - 1)};
       if (L == 4) {
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
@@ -1481,12 +1535,12 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     }
     {
       ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
-      hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, ws.stats, n, eps, ws.coef);
+      hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
       // 2. occ_out + BatchNorm 8
       PCN_HIP(hipMemsetAsync(ws.ostat, 0, 257 * sizeof(double), s));
-      hipLaunchKernelGGL(k_out_bwd_stats, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, ws.h[7], n,
+      hipLaunchKernelGGL(k_out_bwd_stats, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, ws.ostat);
-      hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, ws.h[7], n,
+      hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, P.bn_w[7], P.out_w, ws.ostat, ws.gacc + G.g[7], ws.gacc + G.be[7],
                          ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0]);
     }
@@ -1497,9 +1551,9 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       {
         ProfScope ps(s, PT_BWD_WGRAD, 2.0 * 256.0 * (L == 4 ? 320 : 256) * dn, (L == 4 ? 2048.0 : 2048.0) * dn);
         if (L == 4)
-          launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], ws.h[3], coefp, ws.part);
+          launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
         else
-          launch_wgrad<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], ws.h[L - 1], coefp,
+          launch_wgrad<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
                           ws.part);
       }
       {
@@ -1515,7 +1569,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       {
         ProfScope ps(s, PT_BWD_DGRAD, 2.0 * 256 * 256 * dn, 3072.0 * dn);
         hipLaunchKernelGGL(k_dgrad, dim3(grid), dim3(256), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
-                           ws.h[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
+                           hh[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
                            ws.gacc + G.be[L - 1], ws.g[cur ^ 1]);
       }
       cur ^= 1;
@@ -1543,6 +1597,23 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
   T.dst[k] = grads->out_b, T.off[k] = G.bo, T.len[k++] = 1;
   hipLaunchKernelGGL(k_grad_emit, dim3((256 * 319 + 255) / 256, 34), dim3(256), 0, s, T, ws.gacc);
   PCN_LAUNCH_CHECK("pcnerf_nof_backward");
+}
+
+extern "C" int pcnerf_nof_query_train_backward_store(const float* rays, int64_t n_rays, int ray_stride,
+                                                     const float* z, int n_samples, int64_t chunk,
+                                                     const pcnerf_nof_params* params, float eps,
+                                                     const float* grad_logit, void* workspace,
+                                                     size_t workspace_bytes, const pcnerf_nof_grads* grads,
+                                                     const void* store, int64_t store_chunks, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && grad_logit && workspace && grads,
+            "pcnerf_nof_query_train_backward_store: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_backward_store: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_backward_store: ray_stride < 6");
+  PCN_CHECK(store_chunks == 0 || store, "pcnerf_nof_query_train_backward_store: store_chunks > 0 needs a store");
+  backward_train(rays, ray_stride, z, n_samples, nullptr, n_rays * (int64_t)n_samples, chunk, params, eps,
+                 grad_logit, nullptr, workspace, workspace_bytes, grads, (hipStream_t)stream, store, store_chunks);
+  PCN_API_END
 }
 
 extern "C" int pcnerf_nof_query_train_backward(const float* rays, int64_t n_rays, int ray_stride, const float* z,

@@ -20,7 +20,12 @@ from . import _ops
 class TrainPass(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, rays, z, noise, noise_std, eps, chunk, with_losses, sub_num, *params):
-        p = _ops.query(model, rays, z, chunk)
+        # keep the chunks' layer outputs for the backward in the HBM left after its workspace (+ 4 GiB margin)
+        L = _ops.H.lib()
+        reserve = int(L.pcnerf_nof_backward_workspace_bytes(int(chunk))) + (4 << 30)
+        store = _ops.ActivationStore(z.device, z.numel(), chunk, reserve)
+        p = _ops.query(model, rays, z, chunk, store)
+        ctx.store = store
         w, depth, fr, sl = _ops.composite(p, z, noise, noise_std, eps, rays if with_losses else None)
         if with_losses:
             free, dl = _ops.child_losses(fr, sl, rays, sub_num > 0, sub_num)
@@ -39,7 +44,8 @@ class TrainPass(torch.autograd.Function):
             g_free = g_dl = None
         g_logit = _ops.composite_backward(p, z, noise, ctx.noise_std, ctx.eps, rays if ctx.with_losses else None,
                                           ctx.sub_num, g_depth, g_free, g_dl)
-        grads = _ops.nof_query_backward(ctx.model, rays, z, ctx.chunk, g_logit)
+        grads = _ops.nof_query_backward(ctx.model, rays, z, ctx.chunk, g_logit, ctx.store)
+        ctx.store.release()
         return (None,) * 9 + tuple(grads)
 
 

@@ -89,8 +89,9 @@ def _track_batches(model, n_chunks: int) -> None:
             bn.num_batches_tracked.add_(n_chunks)
 
 
-def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int) -> torch.Tensor:
-    """Occupancy p (R, S) of the samples o + d*z through Embedding + NOF (render.py:18-25 / 44-51)."""
+def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None) -> torch.Tensor:
+    """Occupancy p (R, S) of the samples o + d*z through Embedding + NOF (render.py:18-25 / 44-51).
+    ``store`` (train mode): an ActivationStore whose chunks keep the layer outputs for the backward."""
     L = H.lib()
     R, S = z.shape
     p = torch.empty((R, S), dtype=torch.float32, device=z.device)
@@ -100,8 +101,13 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int) -> torch.Tenso
         s, keep = _params(model)
         nbytes = L.pcnerf_nof_train_workspace_bytes(int(chunk))
         ws = _workspace(z.device, nbytes)
-        H.check(L.pcnerf_nof_query_train(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
-                                         ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(), p.data_ptr(), st))
+        if store is not None and store.n_chunks > 0:
+            H.check(L.pcnerf_nof_query_train_store(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                                   ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(),
+                                                   p.data_ptr(), store.buf.data_ptr(), store.n_chunks, st))
+        else:
+            H.check(L.pcnerf_nof_query_train(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                             ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(), p.data_ptr(), st))
         _track_batches(model, -(-R * S // int(chunk)))
     else:
         packed = pack_eval(model, z.device)
@@ -410,17 +416,57 @@ def composite_backward(p, z, noise, noise_std, eps, rays, sub_nerf_test_num, g_d
     return out
 
 
-def nof_query_backward(model, rays, z, chunk: int, g_logit) -> list:
-    """Parameter gradients (grad_params order) of the train-mode query given dL/dlogit per sample."""
+class ActivationStore:
+    """Device buffer for the first ``n_chunks`` chunks' layer outputs + BatchNorm statistics of one train-mode
+    query (pcnerf_nof_store_bytes per chunk), so its backward skips their recomputation.  Sized to the HBM that is
+    free (driver-free + torch's cached-but-unused) after ``reserve`` bytes; ``PCNERF_ACT_STORE=0`` disables it,
+    ``PCNERF_ACT_STORE_GB`` caps it."""
+
+    def __init__(self, device, total_samples: int, chunk: int, reserve: int):
+        import os
+        L = H.lib()
+        self.per_chunk = int(L.pcnerf_nof_store_bytes(int(chunk)))
+        n_chunks = -(-int(total_samples) // int(chunk))
+        budget = 0
+        if os.environ.get("PCNERF_ACT_STORE", "1") != "0" and n_chunks > 0:
+            free, _ = torch.cuda.mem_get_info(device)
+            free += torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+            budget = max(0, free - int(reserve))
+            cap = os.environ.get("PCNERF_ACT_STORE_GB")
+            if cap is not None:
+                budget = min(budget, int(float(cap) * (1 << 30)))
+        self.n_chunks = min(n_chunks, budget // self.per_chunk)
+        self.buf = None
+        while self.n_chunks > 0:
+            try:
+                self.buf = torch.empty((self.n_chunks * self.per_chunk,), dtype=torch.uint8, device=device)
+                break
+            except torch.cuda.OutOfMemoryError:   # fragmented cache: keep fewer chunks (the rest is recomputed)
+                self.n_chunks //= 2
+
+    def release(self):
+        self.buf = None
+        self.n_chunks = 0
+
+
+def nof_query_backward(model, rays, z, chunk: int, g_logit, store=None) -> list:
+    """Parameter gradients (grad_params order) of the train-mode query given dL/dlogit per sample; chunks held in
+    ``store`` (the forward's layer outputs) are not recomputed."""
     L = H.lib()
     R, S = z.shape
     _, eps = _bn_config(model)
     s, keep = _params(model)
     gs, out = _grads_struct(model, z.device)
     ws = _workspace(z.device, L.pcnerf_nof_backward_workspace_bytes(int(chunk)))
-    H.check(L.pcnerf_nof_query_train_backward(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
-                                              ctypes.byref(s), eps, _f32(g_logit).data_ptr(), ws.data_ptr(),
-                                              ws.numel(), ctypes.byref(gs), _stream(z)))
+    if store is not None and store.n_chunks > 0:
+        H.check(L.pcnerf_nof_query_train_backward_store(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S,
+                                                        int(chunk), ctypes.byref(s), eps, _f32(g_logit).data_ptr(),
+                                                        ws.data_ptr(), ws.numel(), ctypes.byref(gs),
+                                                        store.buf.data_ptr(), store.n_chunks, _stream(z)))
+    else:
+        H.check(L.pcnerf_nof_query_train_backward(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                                  ctypes.byref(s), eps, _f32(g_logit).data_ptr(), ws.data_ptr(),
+                                                  ws.numel(), ctypes.byref(gs), _stream(z)))
     return out
 
 

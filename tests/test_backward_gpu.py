@@ -101,12 +101,19 @@ def oracle_summary(P, seed):
     return out
 
 
-@pytest.mark.parametrize("divide,noise_std", [(0, 0.0), (1, 1e-3)])
-def test_train_grads_vs_oracle_ragged_chunks_with_draws(divide, noise_std):
+@pytest.mark.parametrize("divide,noise_std,store", [(0, 0.0, "all"), (1, 1e-3, "all"), (0, 0.0, "part"),
+                                                     (1, 1e-3, "none")])
+def test_train_grads_vs_oracle_ragged_chunks_with_draws(divide, noise_std, store, monkeypatch):
     """512 rays, 64 + 128 samples, chunk 30000 (the fine pass's last chunk is 8304 samples: a padded tail tile),
     stratified perturbation and importance draws (the reference's training runs perturb=1, noise_std=0,
     logs/*/hparams.yaml) plus a small weight noise, injected identically into both paths.  (Noise of the order
-    of the weights themselves makes sum(w) + eps arbitrarily small and the gradient ill-conditioned.)"""
+    of the weights themselves makes sum(w) + eps arbitrarily small and the gradient ill-conditioned.)
+    ``store``: the activation store keeps every chunk's layer outputs ("all"), only the first chunk's (a 0.3 GB
+    cap: the rest recomputed in the backward), or none (PCNERF_ACT_STORE=0)."""
+    if store == "none":
+        monkeypatch.setenv("PCNERF_ACT_STORE", "0")
+    elif store == "part":
+        monkeypatch.setenv("PCNERF_ACT_STORE_GB", "0.3")
     torch.manual_seed(3)
     R_, S, I = 512, 64, 128
     rays_np = syn.make_rays(R_, seed=17)
