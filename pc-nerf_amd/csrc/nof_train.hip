@@ -18,6 +18,9 @@
 // so each lane owns one neuron per block and the per-neuron statistics are register sums (no cross-lane
 // reduction).  feature(t, h) = 8*(t>>2) + 4*h + (t&3): k-steps 4g..4g+3 read one float4 per lane from the
 // activation tile stored as [tile][g][lane][4] (1 KiB per wave-instruction).
+#include <algorithm>
+#include <vector>
+
 #include "common.h"
 #include "pcnerf_internal.h"
 #include "prof.h"
@@ -36,6 +39,12 @@ namespace pcn {
 #endif
 #ifndef PCN_WD2
 #define PCN_WD2 2  // weight prefetch depth of k_train_hidden (k-groups of one half: 4 float4 each)
+#endif
+#ifndef PCN_HIDDEN_WS
+#define PCN_HIDDEN_WS 1  // 1: hidden layers run k_train_hidden_ws (weight-stationary, samples on columns)
+#endif
+#ifndef PCN_WS_XD
+#define PCN_WS_XD 4  // k_train_hidden_ws: LDS read ring depth in k-groups
 #endif
 #ifndef PCN_HIDDEN_PP
 #define PCN_HIDDEN_PP 1  // 1: hidden layers run k_train_hidden (epilogue overlapped), 0: k_train_layer<false,true>
@@ -66,6 +75,40 @@ namespace pcn {
 #endif
 #ifndef PCN_ABL_EPI
 #define PCN_ABL_EPI 0
+#endif
+
+#ifndef PCN_CLOCK_STAMP
+#define PCN_CLOCK_STAMP 0  // diagnostic builds only: in-kernel clock of the hidden-layer kernels (see pcnerf_debug_clock)
+#endif
+#if PCN_CLOCK_STAMP
+// per workgroup: s_memrealtime (100 MHz, global) at entry / loop begin / loop end / exit (after its atomics
+// completed), s_memtime (shader clock) at loop begin / end
+__device__ unsigned long long g_clk[4096][6];
+#define CLK_ENTRY unsigned long long clk_e = __builtin_amdgcn_s_memrealtime();
+#define CLK_BEGIN                                                   \
+  unsigned long long clk_t0 = __builtin_amdgcn_s_memtime();         \
+  unsigned long long clk_r0 = __builtin_amdgcn_s_memrealtime();
+#define CLK_END                                                     \
+  unsigned long long clk_t1 = __builtin_amdgcn_s_memtime();         \
+  unsigned long long clk_r1 = __builtin_amdgcn_s_memrealtime();
+#define CLK_VARS unsigned long long clk_t0 = 0, clk_r0 = 0, clk_t1 = 0, clk_r1 = 0;
+#define CLK_BEGIN_ST clk_t0 = __builtin_amdgcn_s_memtime(); clk_r0 = __builtin_amdgcn_s_memrealtime();
+#define CLK_END_ST clk_t1 = __builtin_amdgcn_s_memtime(); clk_r1 = __builtin_amdgcn_s_memrealtime();
+#define CLK_EXIT                                                                  \
+  __builtin_amdgcn_s_waitcnt(0);                                                  \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                    \
+    unsigned long long* g = g_clk[blockIdx.x];                                    \
+    g[0] = clk_e; g[1] = clk_r0; g[2] = clk_r1; g[3] = __builtin_amdgcn_s_memrealtime(); \
+    g[4] = clk_t0; g[5] = clk_t1;                                                 \
+  }
+#else
+#define CLK_ENTRY
+#define CLK_BEGIN
+#define CLK_END
+#define CLK_EXIT
+#define CLK_VARS
+#define CLK_BEGIN_ST
+#define CLK_END_ST
 #endif
 
 constexpr int KG_E = 8, KG_H = 32;
@@ -567,6 +610,8 @@ __global__ __launch_bounds__(256, 1) void k_train_hidden(const float* __restrict
                                                          const float* __restrict__ bias, BnPrev prev,
                                                          float momentum, float eps, float* __restrict__ hout,
                                                          float* __restrict__ trash, double* __restrict__ stats) {
+  CLK_ENTRY
+  CLK_VARS
   __shared__ double st[512];
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
@@ -605,6 +650,7 @@ __global__ __launch_bounds__(256, 1) void k_train_hidden(const float* __restrict
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) accB[ob] = f32x16{};
     int64_t prev_tile = -1;
+    CLK_BEGIN_ST
     for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
       int wofs = 0;
       asm volatile("" : "+s"(wofs));
@@ -659,6 +705,7 @@ __global__ __launch_bounds__(256, 1) void k_train_hidden(const float* __restrict
       prev_tile = tile;
     }
 #endif
+    CLK_END_ST
     // drain: epilogue of the last tile's second half, then all of its stores
     {
       const int li = lane & 31;
@@ -692,6 +739,191 @@ __global__ __launch_bounds__(256, 1) void k_train_hidden(const float* __restrict
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 512; i += blockDim.x) atomicAdd(&stats[i], st[i]);
+  CLK_EXIT
+}
+
+// ---- k_train_hidden_ws: weight-stationary hidden layer, samples on COLUMNS (D = W x^T).
+// A workgroup of 8 waves (two per SIMD) computes all 256 neurons of one 32-sample tile at a time; wave b owns
+// neurons 32b..32b+31, whose weights are its MFMA A operand, loaded ONCE per launch into 128 registers (the
+// packed B-operand image of the samples-on-rows kernels has exactly the per-lane content the A operand of the
+// transposed product wants).  The B operand is the activation tile's [g][lane][4] float4 itself, staged once
+// per workgroup in LDS (double buffered, BatchNorm applied while staging, next tile's HBM loads in flight
+// during the current tile's MFMAs).  In this orientation accumulator registers 4j..4j+3 of wave b ARE the
+// output tile's float4 at group 4b+j, so the raw h goes to HBM straight from registers (no LDS transpose), and
+// each lane owns one sample: the per-neuron statistics are per-lane running sums (kept in an LDS slot of the
+// lane's own) across all the workgroup's tiles, reduced across lanes once at the end -- one coalesced float64
+// atomic per (neuron, moment) and workgroup.  No weight traffic inside the tile loop at all.
+// Two waves per SIMD (8 per workgroup, 256 registers each) measured 267 us per chunk of 262,144 samples against
+// 295 us for one wave per SIMD owning 64 neurons (k_train_hidden: 299 us).
+constexpr int WS_XD = PCN_WS_XD;
+__global__ __launch_bounds__(512, 1) void k_train_hidden_ws(const float* __restrict__ hin, int64_t n,
+                                                            const float* __restrict__ Wp,
+                                                            const float* __restrict__ bias, BnPrev prev,
+                                                            float momentum, float eps, float* __restrict__ hout,
+                                                            double* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) float al[256];
+  __shared__ __attribute__((aligned(16))) float be[256];
+  __shared__ __attribute__((aligned(16))) float bs[256];
+  __shared__ f32x4 xs[2][KG_H * 64];   // 2 x 32 KiB
+  // per-lane running statistics (its sample's d and d^2 summed over the launch's tiles) for the wave's 16
+  // neurons of its half: [wave][lane][8 float4 chunks], chunk 2j = sum d, 2j+1 = sum d^2 of registers 4j..4j+3,
+  // stored at position chunk ^ ((lane >> 1) & 7) (conflict-free 16-byte accesses)
+  __shared__ f32x4 sred[8 * 64 * 8];   // 64 KiB
+  CLK_ENTRY
+  const int t = threadIdx.x;
+  if (t < 256) {
+    bn_coeffs(prev, n, momentum, eps, al, be);
+    bs[t] = bias[t];
+  }
+  const int64_t ntiles = (n + 31) / 32;
+  const int lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
+  f32x4 wr[KG_H];
+  {
+    const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wp) + lane;
+#pragma unroll
+    for (int kg = 0; kg < KG_H; ++kg) wr[kg] = w4[(kg * 8 + blk) * 64];
+  }
+  __syncthreads();
+  // all weights resident before the tile loop: otherwise the waitcnt pass cannot tell them from the loop's own
+  // loads and waits on the next tile's activations inside the k-loop
+  __builtin_amdgcn_s_waitcnt(0);
+  // staging: thread t owns the float4s t + 512 m (m = 0..3) of a tile: group (t >> 6) + 8 m, lane t & 63
+  if ((int64_t)blockIdx.x < ntiles) {
+    f32x4 v[4];
+    const f32x4* src = reinterpret_cast<const f32x4*>(hin + (int64_t)blockIdx.x * TILE_FLOATS) + t;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) v[m] = src[512 * m];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int g = (t >> 6) + 8 * m;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
+      f32x4 x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + b[q];
+      xs[0][t + 512 * m] = x;
+    }
+  }
+  __syncthreads();
+  f32x4* const my_st = sred + (blk * 64 + lane) * 8;
+  const int st_sw = (lane >> 1) & 7;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) my_st[c] = f32x4{};
+  int buf = 0;
+  CLK_BEGIN
+  // Software pipeline over tiles: tile t's MFMAs run into one accumulator set while the other set's epilogue
+  // (tile t-1: + bias, statistics, 4 x 1 KiB stores) goes out at k-groups 1-2 and tile t+1's staging (its HBM
+  // loads issued at k-group 3, BatchNorm'd into the other LDS buffer at k-groups 22-23) -- so the only thing
+  // left between two tiles' MFMA streams is the barrier.  Two tiles per loop iteration keep the sets' names fixed.
+  // Tile indices are wave-uniform 32-bit scalars, so every address is an SGPR base + the lane's 32-bit offset.
+  const int nt = (int)ntiles;
+  const int gstride = (int)gridDim.x;
+  auto epi = [&](const f32x16& pacc, int ptile, int j) {
+    const bool valid = (int64_t)ptile * 32 + li < n;
+    const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
+    f32x4 s1 = my_st[(2 * j) ^ st_sw], s2 = my_st[(2 * j + 1) ^ st_sw];
+    f32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float d = pacc[4 * j + q];
+      o[q] = d + bj[q];
+      const float dv = valid ? d : 0.0f;
+      s1[q] += dv;
+      s2[q] += dv * dv;
+    }
+    my_st[(2 * j) ^ st_sw] = s1;
+    my_st[(2 * j + 1) ^ st_sw] = s2;
+    float* base = hout + (size_t)ptile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
+    reinterpret_cast<f32x4*>(base)[lane] = o;
+  };
+  auto stage = [&](const f32x4 (&v)[4], int m) {
+    const int g = (t >> 6) + 8 * m;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
+    f32x4 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + b[q];
+    xs[buf ^ 1][t + 512 * m] = x;
+  };
+  auto body = [&](f32x16& acc, const f32x16& pacc, int tl, int ptile) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
+    const bool more = nxt < nt;
+    const f32x4* xb = &xs[buf][lane];
+    f32x4 xr[WS_XD];
+    f32x4 v[4];   // the next tile's raw activations, k-groups 3 to 23 only
+#pragma unroll
+    for (int d = 0; d < WS_XD - 1; ++d) xr[d] = xb[d * 64];
+#pragma unroll
+    for (int kg = 0; kg < KG_H; ++kg) {
+      if (kg + WS_XD - 1 < KG_H) xr[(kg + WS_XD - 1) % WS_XD] = xb[(kg + WS_XD - 1) * 64];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x16 c = (kg == 0 && q == 0) ? f32x16{} : acc;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[kg][q], xr[kg % WS_XD][q], c, 0, 0, 0);
+      }
+      if (kg == 1 && ptile >= 0) {
+        epi(pacc, ptile, 0);
+        epi(pacc, ptile, 1);
+      }
+      if (kg == 2 && ptile >= 0) {
+        epi(pacc, ptile, 2);
+        epi(pacc, ptile, 3);
+      }
+      if (kg == 3 && more) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)nxt * TILE_FLOATS + (size_t)m * 2048)[t];
+      }
+      if (kg == 22 && more) {
+        stage(v, 0);
+        stage(v, 1);
+      }
+      if (kg == 23 && more) {
+        stage(v, 2);
+        stage(v, 3);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    buf ^= 1;
+  };
+  f32x16 accA, accB;
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  int ptile = -1;
+  while (tl < nt) {
+    body(accA, accB, tl, ptile);
+    ptile = tl;
+    tl = __builtin_amdgcn_readfirstlane(tl + gstride);
+    if (tl >= nt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epi(accA, ptile, j);
+      break;
+    }
+    body(accB, accA, tl, ptile);
+    ptile = tl;
+    tl = __builtin_amdgcn_readfirstlane(tl + gstride);
+    if (tl >= nt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epi(accB, ptile, j);
+    }
+  }
+  CLK_END
+  // per-neuron sums, once per launch: thread t = 2 n + moment sums its (neuron, moment) over the 32 lanes of the
+  // half that holds neuron n, in float64, and adds it with one coalesced atomic
+  __syncthreads();
+  {
+    const int nn = t >> 1, mo = t & 1, ib = nn & 31, wb = nn >> 5;
+    const int hh = (ib >> 2) & 1, jj = ib >> 3, qq = ib & 3;
+    double a = 0.0;
+#pragma unroll 8
+    for (int l = 0; l < 32; ++l) {
+      const int ln = 32 * hh + l;
+      a += (double)sred[(wb * 64 + ln) * 8 + ((2 * jj + mo) ^ ((ln >> 1) & 7))][qq];
+    }
+    atomicAdd(&stats[t], a);
+  }
+  CLK_EXIT
 }
 
 // occ_out on BatchNorm 8 (applied on load) + sigmoid; one wave per 32-sample tile.
@@ -757,6 +989,35 @@ static TrainWs carve(void* base, int64_t chunk) {
 using namespace pcn;
 
 extern "C" size_t pcnerf_nof_train_workspace_bytes(int64_t chunk) { return carve(nullptr, chunk).bytes; }
+
+#if PCN_CLOCK_STAMP
+// diagnostic builds: median over workgroups of the last hidden-layer launch's in-kernel clock (MHz) and cycles
+extern "C" int pcnerf_debug_clock(double* out) {
+  // out: [0] loop clock MHz, [1] kernel span us (last exit - first entry), median [2] prologue, [3] loop,
+  // [4] epilogue us; [5] entry spread, [6] exit spread, [7] loop-end spread (us)
+  static unsigned long long h[4096][6];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_clk), sizeof(h)) != hipSuccess) return 1;
+  std::vector<double> f, pro, loop, epi, en, ex, le;
+  for (int i = 0; i < 4096; ++i)
+    if (h[i][3] > h[i][0] && h[i][2] > h[i][1]) {
+      f.push_back((double)(h[i][5] - h[i][4]) / (double)(h[i][2] - h[i][1]) * 100.0);
+      pro.push_back((h[i][1] - h[i][0]) * 0.01);
+      loop.push_back((h[i][2] - h[i][1]) * 0.01);
+      epi.push_back((h[i][3] - h[i][2]) * 0.01);
+      en.push_back((double)h[i][0]);
+      ex.push_back((double)h[i][3]);
+      le.push_back((double)h[i][2]);
+    }
+  if (f.empty()) return 2;
+  auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+  const double e0 = *std::min_element(en.begin(), en.end()), e1 = *std::max_element(en.begin(), en.end());
+  const double x0 = *std::min_element(ex.begin(), ex.end()), x1 = *std::max_element(ex.begin(), ex.end());
+  const double l0 = *std::min_element(le.begin(), le.end()), l1 = *std::max_element(le.begin(), le.end());
+  out[0] = med(f); out[1] = (x1 - e0) * 0.01; out[2] = med(pro); out[3] = med(loop); out[4] = med(epi);
+  out[5] = (e1 - e0) * 0.01; out[6] = (x1 - x0) * 0.01; out[7] = (l1 - l0) * 0.01;
+  return 0;
+}
+#endif
 
 // Activation store of the training step: per chunk the raw h of all 8 layers (the tile layout the backward
 // consumes) and the chunk's BatchNorm statistics, written by the forward so the backward need not recompute.
@@ -830,7 +1091,11 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        if (PCN_HIDDEN_PP)
+        if (PCN_HIDDEN_WS)
+          hipLaunchKernelGGL(k_train_hidden_ws, dim3((unsigned)(ntiles < 256 ? ntiles : 256)), dim3(512), 0, s,
+                             hin, n, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps, hout,
+                             stats + 512 * L);
+        else if (PCN_HIDDEN_PP)
           hipLaunchKernelGGL(k_train_hidden, dim3(grid), dim3(256), 0, s, hin, n, ws.wp + off_w(L, false),
                              P.lin_b[L], prev, momentum, eps, hout, trash, stats + 512 * L);
         else
@@ -1528,9 +1793,14 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
                            ws.stats + 512 * 4);
       } else {
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                           n_samples, c0, n, ein, ws.h[L - 1], ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps,
-                           ws.h[L], ws.stats + 512 * L);
+        if (PCN_HIDDEN_WS)
+          hipLaunchKernelGGL(k_train_hidden_ws, dim3((unsigned)(ntiles < 256 ? ntiles : 256)), dim3(512), 0, s,
+                             ws.h[L - 1], n, ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps, ws.h[L],
+                             ws.stats + 512 * L);
+        else
+          hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
+                             n_samples, c0, n, ein, ws.h[L - 1], ws.wp + off_w(L, false), P.lin_b[L], prev, mom,
+                             eps, ws.h[L], ws.stats + 512 * L);
       }
     }
     {

@@ -36,7 +36,11 @@ def read(L, tag):
 def main():
     rays_n = int(os.environ.get("VB_RAYS", "16384"))
     S = int(os.environ.get("VB_S", "384"))
+    chunk = int(os.environ.get("VB_CHUNK", "262144"))
     libs = sorted(glob.glob(os.path.join(HERE, "pc-nerf_amd", "lib", "variants", "*.so")))
+    only = os.environ.get("VB_ONLY")
+    if only:
+        libs = [l for l in libs if os.path.basename(l)[10:-3] in only.split(",")]
     dev = torch.device("cuda")
     rays = torch.from_numpy(syn.make_rays(rays_n, seed=0)).to(dev)
     z = (torch.linspace(0, 1, S, device=dev)[None] * rays[:, 7:8]).contiguous()
@@ -44,7 +48,7 @@ def main():
     s, keep = _ops._params(m)
     p = torch.empty_like(z)
     Ls = {os.path.basename(l)[10:-3]: load(l) for l in libs}
-    ws = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_train_workspace_bytes(262144), dtype=torch.uint8, device=dev)
+    ws = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_train_workspace_bytes(chunk), dtype=torch.uint8, device=dev)
     packed = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_eval_packed_floats(), device=dev)
     st = torch.cuda.current_stream().cuda_stream
     res = {k: {t: [] for t in TAGS} for k in Ls}
@@ -53,12 +57,12 @@ def main():
     if bwd:   # backward on a quarter of the rays (its workspace holds all 8 layers of a chunk)
         rays_b, z_b = rays[: rays_n // 4].contiguous(), z[: rays_n // 4].contiguous()
         g_logit = torch.randn(z_b.shape, generator=torch.Generator().manual_seed(3)).to(dev) * 1e-3
-        wsb = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_backward_workspace_bytes(262144), dtype=torch.uint8,
+        wsb = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_backward_workspace_bytes(chunk), dtype=torch.uint8,
                           device=dev)
     for rnd in range(4):
         for name, L in Ls.items():
             L.pcnerf_prof_enable(1)
-            rc = L.pcnerf_nof_query_train(rays.data_ptr(), rays_n, 15, z.data_ptr(), S, 262144, ctypes.byref(s),
+            rc = L.pcnerf_nof_query_train(rays.data_ptr(), rays_n, 15, z.data_ptr(), S, chunk, ctypes.byref(s),
                                           0.0, 1e-5, ws.data_ptr(), ws.numel(), p.data_ptr(), st)
             assert rc == 0, L.pcnerf_last_error()
             if rnd == 0:
@@ -66,7 +70,7 @@ def main():
             if bwd:
                 gs, gout = _ops._grads_struct(m, dev)
                 rc = L.pcnerf_nof_query_train_backward(rays_b.data_ptr(), rays_b.shape[0], 15, z_b.data_ptr(), S,
-                                                       262144, ctypes.byref(s), 1e-5, g_logit.data_ptr(),
+                                                       chunk, ctypes.byref(s), 1e-5, g_logit.data_ptr(),
                                                        wsb.data_ptr(), wsb.numel(), ctypes.byref(gs), st)
                 assert rc == 0, L.pcnerf_last_error()
                 if rnd == 0:
@@ -84,6 +88,16 @@ def main():
                     res[name][t].append((tm / n * 1e3, f / (tm * 1e-3) / 1e12))
             L.pcnerf_prof_enable(0)
     out = {}
+    clk = {}
+    for name, L in Ls.items():
+        try:
+            f = L.pcnerf_debug_clock
+        except AttributeError:
+            continue
+        f.restype, f.argtypes = ctypes.c_int, [ctypes.POINTER(ctypes.c_double)]
+        buf = (ctypes.c_double * 8)()
+        if f(buf) == 0:
+            clk[name] = [round(x, 1) for x in buf]
     for name in Ls:
         out[name] = {TAGS[t]: {"us": round(sorted(v)[len(v) // 2][0], 1), "TF": round(sorted(v)[len(v) // 2][1], 1)}
                      for t, v in res[name].items() if v}
@@ -95,6 +109,9 @@ def main():
             if name in gouts:
                 gr = gouts["base"]
                 out[name]["grad_max_rel_diff_vs_base"] = float(((gouts[name] - gr).abs().max() / gr.abs().max()))
+    for name, c in clk.items():
+        out[name]["clock_stamps"] = dict(zip(["MHz", "span_us", "prologue_us", "loop_us", "epilogue_us",
+                                              "entry_spread_us", "exit_spread_us", "loopend_spread_us"], c))
     print(json.dumps(out, indent=1))
 
 
