@@ -40,8 +40,11 @@ namespace pcn {
 #ifndef PCN_WD2
 #define PCN_WD2 2  // weight prefetch depth of k_train_hidden (k-groups of one half: 4 float4 each)
 #endif
-#ifndef PCN_HIDDEN_WS
-#define PCN_HIDDEN_WS 1  // 1: hidden layers run k_train_hidden_ws (weight-stationary, samples on columns)
+#ifndef PCN_TRAIN_WS
+#define PCN_TRAIN_WS 7  // k_train_ws (weight-stationary, samples on columns) for: 1 hidden, 2 skip, 4 first layer
+#endif
+#ifndef PCN_WS_XD_SKIP
+#define PCN_WS_XD_SKIP 2  // the same for the skip layer
 #endif
 #ifndef PCN_WS_XD
 #define PCN_WS_XD 4  // k_train_hidden_ws: LDS read ring depth in k-groups
@@ -756,15 +759,71 @@ __global__ __launch_bounds__(256, 1) void k_train_hidden(const float* __restrict
 // Two waves per SIMD (8 per workgroup, 256 registers each) measured 267 us per chunk of 262,144 samples against
 // 295 us for one wave per SIMD owning 64 neurons (k_train_hidden: 299 us).
 constexpr int WS_XD = PCN_WS_XD;
-__global__ __launch_bounds__(512, 1) void k_train_hidden_ws(const float* __restrict__ hin, int64_t n,
-                                                            const float* __restrict__ Wp,
-                                                            const float* __restrict__ bias, BnPrev prev,
-                                                            float momentum, float eps, float* __restrict__ hout,
-                                                            double* __restrict__ stats) {
+
+// Encoding feature group g (features 8g + 4h + q, q = 0..3) of a sample at p for lane half h: Embedding(3, 10) as
+// in encode_half (2^k * x exact, full-range sincosf), computed per feature so one thread stages one float4.
+__device__ __forceinline__ f32x4 enc_feats(const float (&p)[3], int h, int g) {
+  f32x4 e;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int f = 8 * g + 4 * h + q;
+    const int fk = f < 3 ? 0 : (f - 3) / 6, fr = f < 3 ? 0 : (f - 3) - 6 * fk;
+    const int m = fr < 3 ? fr : fr - 3;
+    const float pm = m == 0 ? p[0] : m == 1 ? p[1] : p[2];
+    float sn, cs;
+    sincosf(__int_as_float((127 + fk) << 23) * pm, &sn, &cs);   // (float)(1 << fk) * p[m]
+    const float pf = f == 0 ? p[0] : f == 1 ? p[1] : p[2];
+    e[q] = f < 3 ? pf : f >= 63 ? 0.0f : fr < 3 ? sn : cs;
+  }
+  return e;
+}
+
+// The same group from a stored (., 63) embedding row.
+__device__ __forceinline__ f32x4 enc_feats_row(const float* __restrict__ row, int h, int g) {
+  f32x4 e;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int f = 8 * g + 4 * h + q;
+    e[q] = f < 63 ? row[f] : 0.0f;
+  }
+  return e;
+}
+
+// ---- k_train_ws<KE, HP>: weight-stationary train-mode Linear, samples on COLUMNS (D = W x^T).
+//   KE = 8: the 63 (+1 pad) encoding features are input k-groups 0..7 (computed from positions, or read from
+//   `ein`); HP: the 256 BatchNorm'd features of the previous layer are k-groups KE..KE+31.  Instances: first
+//   layer <8,false> (63 -> 256), hidden layers <0,true> (256 -> 256), skip layer 5 <8,true> ([e, h4] 319 -> 256).
+// A workgroup of 8 waves (two per SIMD) computes all 256 neurons of one 32-sample tile at a time; wave b owns
+// neurons 32b..32b+31, whose weights are its MFMA A operand, loaded ONCE per launch into registers (the packed
+// B-operand image of the samples-on-rows kernels has exactly the per-lane content the A operand of the
+// transposed product wants).  The B operand is the input tile's [g][lane][4] float4 itself, staged once per
+// workgroup in LDS (double buffered; previous BatchNorm applied while staging; encoding groups computed while
+// staging, one float4 per thread).  In this orientation accumulator registers 4j..4j+3 of wave b ARE the output
+// tile's float4 at group 4b+j, so the raw h goes to HBM straight from registers (no LDS transpose), and each lane
+// owns one sample: the per-neuron statistics are per-lane running sums (kept in an LDS slot of the lane's own)
+// across all the workgroup's tiles, reduced across lanes once at the end -- one coalesced float64 atomic per
+// (neuron, moment) and workgroup.  No weight traffic inside the tile loop at all.
+// Software pipeline over tiles: tile t's MFMAs run into one accumulator set while the other set's epilogue (tile
+// t-1: + bias, statistics, 4 x 1 KiB stores) goes out at k-groups 1-2 and tile t+1's input is staged into the
+// other LDS buffer (activation loads at k-group 3, BatchNorm'd at KGT-10/KGT-9; ray rows loaded at k-group KGT-8
+// (first layer: 0), encoding computed at the last k-group), so the only thing left between two tiles' MFMA
+// streams is the barrier.
+// Hidden layer: 265 us per chunk of 262,144 samples (the previous samples-on-rows kernel: 299 us); one wave per
+// SIMD owning 64 neurons measured 295 us.
+template <int KE, bool HP>
+__global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ rays, int stride,
+                                                     const float* __restrict__ z, int S, int64_t c0,
+                                                     const float* __restrict__ ein, const float* __restrict__ hin,
+                                                     int64_t n, const float* __restrict__ Wp,
+                                                     const float* __restrict__ bias, BnPrev prev, float momentum,
+                                                     float eps, float* __restrict__ hout,
+                                                     double* __restrict__ stats) {
+  constexpr int KGT = KE + (HP ? KG_H : 0);
+  constexpr int XD = (KE && HP) ? PCN_WS_XD_SKIP : WS_XD;   // the skip layer's 160 weight registers leave less
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
-  __shared__ f32x4 xs[2][KG_H * 64];   // 2 x 32 KiB
+  __shared__ f32x4 xs[2][KGT * 64];
   // per-lane running statistics (its sample's d and d^2 summed over the launch's tiles) for the wave's 16
   // neurons of its half: [wave][lane][8 float4 chunks], chunk 2j = sum d, 2j+1 = sum d^2 of registers 4j..4j+3,
   // stored at position chunk ^ ((lane >> 1) & 7) (conflict-free 16-byte accesses)
@@ -772,53 +831,67 @@ __global__ __launch_bounds__(512, 1) void k_train_hidden_ws(const float* __restr
   CLK_ENTRY
   const int t = threadIdx.x;
   if (t < 256) {
-    bn_coeffs(prev, n, momentum, eps, al, be);
+    if (HP) bn_coeffs(prev, n, momentum, eps, al, be);
     bs[t] = bias[t];
   }
-  const int64_t ntiles = (n + 31) / 32;
+  const int nt = (int)((n + 31) / 32);
+  const int gstride = (int)gridDim.x;
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
   const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
-  f32x4 wr[KG_H];
+  f32x4 wr[KGT];
   {
     const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wp) + lane;
 #pragma unroll
-    for (int kg = 0; kg < KG_H; ++kg) wr[kg] = w4[(kg * 8 + blk) * 64];
+    for (int kg = 0; kg < KGT; ++kg) wr[kg] = w4[(kg * 8 + blk) * 64];
   }
-  __syncthreads();
-  // all weights resident before the tile loop: otherwise the waitcnt pass cannot tell them from the loop's own
-  // loads and waits on the next tile's activations inside the k-loop
-  __builtin_amdgcn_s_waitcnt(0);
-  // staging: thread t owns the float4s t + 512 m (m = 0..3) of a tile: group (t >> 6) + 8 m, lane t & 63
-  if ((int64_t)blockIdx.x < ntiles) {
-    f32x4 v[4];
-    const f32x4* src = reinterpret_cast<const f32x4*>(hin + (int64_t)blockIdx.x * TILE_FLOATS) + t;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) v[m] = src[512 * m];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int g = (t >> 6) + 8 * m;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
-      f32x4 x;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + b[q];
-      xs[0][t + 512 * m] = x;
-    }
-  }
-  __syncthreads();
   f32x4* const my_st = sred + (blk * 64 + lane) * 8;
   const int st_sw = (lane >> 1) & 7;
 #pragma unroll
   for (int c = 0; c < 8; ++c) my_st[c] = f32x4{};
+  __syncthreads();
+  // all weights resident before the tile loop: otherwise the waitcnt pass cannot tell them from the loop's own
+  // loads and waits on the next tile's activations inside the k-loop
+  __builtin_amdgcn_s_waitcnt(0);
   int buf = 0;
+  // staging: thread t owns the activation float4s t + 512 m (m = 0..3) of a tile: group KE + (t >> 6) + 8 m,
+  // lane t & 63; and (KE) the encoding float4 of group t >> 6, lane t & 63
+  auto stage = [&](int b, const f32x4 (&v)[4], int m) {
+    const int g = (t >> 6) + 8 * m;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
+    const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
+    f32x4 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + c[q];
+    xs[b][KE * 64 + t + 512 * m] = x;
+  };
+  auto sample_of = [&](int tile) {
+    int64_t sl = (int64_t)tile * 32 + li;
+    if (sl >= n) sl = n - 1;
+    return c0 + sl;
+  };
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  if (tl < nt) {
+    if (HP) {
+      f32x4 v[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)tl * TILE_FLOATS + (size_t)m * 2048)[t];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) stage(0, v, m);
+    }
+    if (KE) {
+      const int64_t gs = sample_of(tl);
+      if (ein) {
+        xs[0][t] = enc_feats_row(ein + gs * 63, h, t >> 6);
+      } else {
+        float p[3];
+        sample_point(rays + (gs / S) * stride, z[gs], p);
+        xs[0][t] = enc_feats(p, h, t >> 6);
+      }
+    }
+  }
+  __syncthreads();
   CLK_BEGIN
-  // Software pipeline over tiles: tile t's MFMAs run into one accumulator set while the other set's epilogue
-  // (tile t-1: + bias, statistics, 4 x 1 KiB stores) goes out at k-groups 1-2 and tile t+1's staging (its HBM
-  // loads issued at k-group 3, BatchNorm'd into the other LDS buffer at k-groups 22-23) -- so the only thing
-  // left between two tiles' MFMA streams is the barrier.  Two tiles per loop iteration keep the sets' names fixed.
-  // Tile indices are wave-uniform 32-bit scalars, so every address is an SGPR base + the lane's 32-bit offset.
-  const int nt = (int)ntiles;
-  const int gstride = (int)gridDim.x;
   auto epi = [&](const f32x16& pacc, int ptile, int j) {
     const bool valid = (int64_t)ptile * 32 + li < n;
     const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
@@ -837,30 +910,29 @@ __global__ __launch_bounds__(512, 1) void k_train_hidden_ws(const float* __restr
     float* base = hout + (size_t)ptile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
     reinterpret_cast<f32x4*>(base)[lane] = o;
   };
-  auto stage = [&](const f32x4 (&v)[4], int m) {
-    const int g = (t >> 6) + 8 * m;
-    const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
-    const f32x4 b = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
-    f32x4 x;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + b[q];
-    xs[buf ^ 1][t + 512 * m] = x;
-  };
-  auto body = [&](f32x16& acc, const f32x16& pacc, int tl, int ptile) {
-    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
+  auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tile + gstride);
     const bool more = nxt < nt;
     const f32x4* xb = &xs[buf][lane];
-    f32x4 xr[WS_XD];
-    f32x4 v[4];   // the next tile's raw activations, k-groups 3 to 23 only
+    f32x4 xr[XD];
+    f32x4 v[4];    // HP: the next tile's raw activations, k-groups 3 to KGT-9 only
+    float rr[7];   // KE: the next tile's ray origin/direction and z for this lane's sample (last 8 k-groups)
 #pragma unroll
-    for (int d = 0; d < WS_XD - 1; ++d) xr[d] = xb[d * 64];
+    for (int d = 0; d < XD - 1; ++d) xr[d] = xb[d * 64];
 #pragma unroll
-    for (int kg = 0; kg < KG_H; ++kg) {
-      if (kg + WS_XD - 1 < KG_H) xr[(kg + WS_XD - 1) % WS_XD] = xb[(kg + WS_XD - 1) * 64];
+    for (int kg = 0; kg < KGT; ++kg) {
+      if (kg + XD - 1 < KGT) xr[(kg + XD - 1) % XD] = xb[(kg + XD - 1) * 64];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const f32x16 c = (kg == 0 && q == 0) ? f32x16{} : acc;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[kg][q], xr[kg % WS_XD][q], c, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[kg][q], xr[kg % XD][q], c, 0, 0, 0);
+      }
+      if (KE && kg == (HP ? KGT - 8 : 0) && more && !ein) {   // after the activations' registers are free
+        const int64_t gs = sample_of(nxt);
+        const float* r = rays + (gs / S) * stride;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) rr[c] = r[c];
+        rr[6] = z[gs];
       }
       if (kg == 1 && ptile >= 0) {
         epi(pacc, ptile, 0);
@@ -870,18 +942,30 @@ __global__ __launch_bounds__(512, 1) void k_train_hidden_ws(const float* __restr
         epi(pacc, ptile, 2);
         epi(pacc, ptile, 3);
       }
-      if (kg == 3 && more) {
+      if (HP && kg == 3 && more) {
 #pragma unroll
         for (int m = 0; m < 4; ++m)
           v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)nxt * TILE_FLOATS + (size_t)m * 2048)[t];
       }
-      if (kg == 22 && more) {
-        stage(v, 0);
-        stage(v, 1);
+      if (HP && kg == KGT - 10 && more) {
+        stage(buf ^ 1, v, 0);
+        stage(buf ^ 1, v, 1);
       }
-      if (kg == 23 && more) {
-        stage(v, 2);
-        stage(v, 3);
+      if (HP && kg == KGT - 9 && more) {
+        stage(buf ^ 1, v, 2);
+        stage(buf ^ 1, v, 3);
+      }
+      if (KE && kg == KGT - 1 && more) {
+        f32x4 e;
+        if (ein) {
+          e = enc_feats_row(ein + sample_of(nxt) * 63, h, t >> 6);
+        } else {   // sample_point on the prefetched ray row
+          float p[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) p[c] = rr[c] + rr[3 + c] * rr[6];
+          e = enc_feats(p, h, t >> 6);
+        }
+        xs[buf ^ 1][t] = e;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -889,7 +973,6 @@ __global__ __launch_bounds__(512, 1) void k_train_hidden_ws(const float* __restr
     buf ^= 1;
   };
   f32x16 accA, accB;
-  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
   int ptile = -1;
   while (tl < nt) {
     body(accA, accB, tl, ptile);
@@ -1059,6 +1142,7 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     const int64_t ntiles = (n + 31) / 32;
     const unsigned maxg = 256u * PCN_TRAIN_WAVES;
     const unsigned grid = (unsigned)(ntiles / 4 + 1 < maxg ? ntiles / 4 + 1 : maxg);
+    const unsigned gws = (unsigned)(ntiles < 256 ? ntiles : 256);   // k_train_ws: one workgroup per CU
     const double dn = (double)n;
     // stored chunk: every layer writes its own buffer of the store (kept for the backward); else ping-pong
     const int64_t ci = c0 / chunk;
@@ -1072,9 +1156,14 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
-      hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
-                         c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps,
-                         hin, stats);
+      if (PCN_TRAIN_WS & 4)
+        hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
+                           ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps,
+                           hin, stats);
+      else
+        hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
+                           n_samples, c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none,
+                           momentum, eps, hin, stats);
     }
     for (int L = 1; L < 8; ++L) {
       if (keep) {
@@ -1085,15 +1174,20 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
                         stats + 512 * (L - 1)};
       if (L == 4) {
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
-        hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
-                           c0, n, ein, hin, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
-                           stats + 512 * L);
+        if (PCN_TRAIN_WS & 2)
+          hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
+                             c0, ein, hin, n, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
+                             stats + 512 * L);
+        else
+          hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
+                             n_samples, c0, n, ein, hin, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps,
+                             hout, stats + 512 * L);
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        if (PCN_HIDDEN_WS)
-          hipLaunchKernelGGL(k_train_hidden_ws, dim3((unsigned)(ntiles < 256 ? ntiles : 256)), dim3(512), 0, s,
-                             hin, n, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps, hout,
+        if (PCN_TRAIN_WS & 1)
+          hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
+                             ein, hin, n, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps, hout,
                              stats + 512 * L);
         else if (PCN_HIDDEN_PP)
           hipLaunchKernelGGL(k_train_hidden, dim3(grid), dim3(256), 0, s, hin, n, ws.wp + off_w(L, false),
@@ -1767,6 +1861,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     const double dn = (double)n;
     const unsigned maxg = 256u * PCN_TRAIN_WAVES;
     const unsigned grid = (unsigned)(ntiles / 4 + 1 < maxg ? ntiles / 4 + 1 : maxg);
+    const unsigned gws = (unsigned)(ntiles < 256 ? ntiles : 256);
     const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
     const unsigned wblocks = (unsigned)(ntiles < WG_BLOCKS ? ntiles : WG_BLOCKS);
     // 1. the forward's layer outputs and statistics: from the activation store, or recomputed here
@@ -1780,22 +1875,32 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     if (!kept) {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
-      hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
-                         c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps,
-                         ws.h[0], ws.stats);
+      if (PCN_TRAIN_WS & 4)
+        hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
+                           ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps,
+                           ws.h[0], ws.stats);
+      else
+        hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
+                           n_samples, c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none,
+                           mom, eps, ws.h[0], ws.stats);
     }
     for (int L = 1; L < 8 && !kept; ++L) {
       const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], nullptr, nullptr, P.lin_b[L - 1], ws.stats + 512 * (L - 1)};
       if (L == 4) {
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
-        hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z, n_samples,
-                           c0, n, ein, ws.h[3], ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps, ws.h[4],
-                           ws.stats + 512 * 4);
+        if (PCN_TRAIN_WS & 2)
+          hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
+                             c0, ein, ws.h[3], n, ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps, ws.h[4],
+                             ws.stats + 512 * 4);
+        else
+          hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
+                             n_samples, c0, n, ein, ws.h[3], ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps,
+                             ws.h[4], ws.stats + 512 * 4);
       } else {
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        if (PCN_HIDDEN_WS)
-          hipLaunchKernelGGL(k_train_hidden_ws, dim3((unsigned)(ntiles < 256 ? ntiles : 256)), dim3(512), 0, s,
-                             ws.h[L - 1], n, ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps, ws.h[L],
+        if (PCN_TRAIN_WS & 1)
+          hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
+                             ein, ws.h[L - 1], n, ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps, ws.h[L],
                              ws.stats + 512 * L);
         else
           hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
