@@ -58,6 +58,9 @@ namespace pcn {
 #ifndef PCN_PP_XREG
 #define PCN_PP_XREG 1  // k_train_hidden: the tile's activations register-resident across its two passes
 #endif
+#ifndef PCN_DGRAD_WS
+#define PCN_DGRAD_WS 1  // backward data gradient: 1 weight-stationary k_dgrad_ws, 0 k_dgrad
+#endif
 #ifndef PCN_DGRAD_PF
 #define PCN_DGRAD_PF 1  // k_dgrad: prefetch the BatchNorm-backward operand tile during the GEMM
 #endif
@@ -1741,6 +1744,141 @@ __global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_dgrad(
   }
 }
 
+// ---- k_dgrad_ws: k_dgrad in the weight-stationary form of k_train_ws<0,true>.  A workgroup of 8 waves (two per
+// SIMD) computes all 256 input features of one 32-sample tile at a time; wave b holds the W^T rows of features
+// 32b..32b+31 (128 registers, loaded once per launch) as the A operand, the dL/dh tile is staged raw in LDS
+// (double buffered, next tile's loads in flight), and the BatchNorm backward runs on the accumulators: register
+// float4 4j..4j+3 of wave b is the output float4 at group 4b+j, whose h_{L-1} operand is the same [g][lane]
+// float4 of the h tile (one 16-byte load per lane, issued during the k-loop), and the result goes to HBM straight
+// from registers.  The previous tile's epilogue runs at k-groups 1-2 of the next tile's k-loop.
+__global__ __launch_bounds__(512, 1) void k_dgrad_ws(
+    const float* __restrict__ gin, const float* __restrict__ Wt, const float* __restrict__ hprev, int64_t n,
+    const double* __restrict__ s12, const float* __restrict__ coefp, const float* __restrict__ gamma,
+    double* __restrict__ d_gamma, double* __restrict__ d_beta, float* __restrict__ gout) {
+  __shared__ __attribute__((aligned(16))) float cgm[256];
+  __shared__ __attribute__((aligned(16))) float ckk[256];
+  __shared__ __attribute__((aligned(16))) float cmu[256];
+  __shared__ __attribute__((aligned(16))) float cis[256];
+  __shared__ __attribute__((aligned(16))) float cga[256];
+  __shared__ f32x4 xs[2][KG_H * 64];   // 2 x 32 KiB
+  const int t = threadIdx.x;
+  if (t < 256) {
+    const int k = t;
+    const double S1 = s12[2 * k], dotp = s12[2 * k + 1];
+    const float invstd = coefp[256 + k];
+    cgm[k] = (float)(S1 / (double)n);
+    ckk[k] = (((float)dotp * invstd) * invstd) / (float)n;
+    cmu[k] = coefp[k];
+    cis[k] = invstd;
+    cga[k] = gamma[k];
+    if (blockIdx.x == 0) {
+      d_gamma[k] += dotp * (double)invstd;
+      d_beta[k] += S1;
+    }
+  }
+  const int nt = (int)((n + 31) / 32);
+  const int gstride = (int)gridDim.x;
+  const int lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
+  f32x4 wr[KG_H];
+  {
+    const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wt) + lane;
+#pragma unroll
+    for (int kg = 0; kg < KG_H; ++kg) wr[kg] = w4[(kg * 8 + blk) * 64];
+  }
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  if (tl < nt) {
+    f32x4 v[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      v[m] = reinterpret_cast<const f32x4*>(gin + (size_t)tl * TILE_FLOATS + (size_t)m * 2048)[t];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) xs[0][t + 512 * m] = v[m];
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);   // weights resident before the tile loop (see k_train_ws)
+  int buf = 0;
+  auto epi = [&](const f32x16& pacc, const f32x4 (&hx)[4], int ptile, int j) {
+    const bool valid = (int64_t)ptile * 32 + li < n;
+    const int f0 = 8 * (4 * blk + j) + 4 * h;
+    const f32x4 gm = *reinterpret_cast<const f32x4*>(cgm + f0), kk = *reinterpret_cast<const f32x4*>(ckk + f0);
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(cmu + f0), is = *reinterpret_cast<const f32x4*>(cis + f0);
+    const f32x4 ga = *reinterpret_cast<const f32x4*>(cga + f0);
+    f32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      o[q] = valid ? ((pacc[4 * j + q] - gm[q]) - (hx[j][q] - mu[q]) * kk[q]) * is[q] * ga[q] : 0.0f;
+    reinterpret_cast<f32x4*>(gout + (size_t)ptile * TILE_FLOATS + (size_t)(4 * blk + j) * 256)[lane] = o;
+  };
+  auto body = [&](f32x16& acc, f32x4 (&hx)[4], const f32x16& pacc, const f32x4 (&phx)[4], int tile, int ptile) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tile + gstride);
+    const bool more = nxt < nt;
+    const f32x4* xb = &xs[buf][lane];
+    f32x4 xr[WS_XD];
+    f32x4 v[4];
+#pragma unroll
+    for (int d = 0; d < WS_XD - 1; ++d) xr[d] = xb[d * 64];
+#pragma unroll
+    for (int kg = 0; kg < KG_H; ++kg) {
+      if (kg + WS_XD - 1 < KG_H) xr[(kg + WS_XD - 1) % WS_XD] = xb[(kg + WS_XD - 1) * 64];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x16 c = (kg == 0 && q == 0) ? f32x16{} : acc;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[kg][q], xr[kg % WS_XD][q], c, 0, 0, 0);
+      }
+      if (kg == 1 && ptile >= 0) {
+        epi(pacc, phx, ptile, 0);
+        epi(pacc, phx, ptile, 1);
+      }
+      if (kg == 2 && ptile >= 0) {
+        epi(pacc, phx, ptile, 2);
+        epi(pacc, phx, ptile, 3);
+      }
+      if (kg == 3 && more) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          v[m] = reinterpret_cast<const f32x4*>(gin + (size_t)nxt * TILE_FLOATS + (size_t)m * 2048)[t];
+      }
+      if (kg == 22 && more) {
+        xs[buf ^ 1][t] = v[0];
+        xs[buf ^ 1][t + 512] = v[1];
+      }
+      if (kg == 23 && more) {
+        xs[buf ^ 1][t + 1024] = v[2];
+        xs[buf ^ 1][t + 1536] = v[3];
+      }
+      if (kg == 24) {   // this tile's h_{L-1} operand of the BatchNorm backward (epilogue at the next tile)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          hx[j] = reinterpret_cast<const f32x4*>(hprev + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256)[lane];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    buf ^= 1;
+  };
+  f32x16 accA, accB;
+  f32x4 hxA[4], hxB[4];
+  int ptile = -1;
+  while (tl < nt) {
+    body(accA, hxA, accB, hxB, tl, ptile);
+    ptile = tl;
+    tl = __builtin_amdgcn_readfirstlane(tl + gstride);
+    if (tl >= nt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epi(accA, hxA, ptile, j);
+      break;
+    }
+    body(accB, hxB, accA, hxA, tl, ptile);
+    ptile = tl;
+    tl = __builtin_amdgcn_readfirstlane(tl + gstride);
+    if (tl >= nt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epi(accB, hxB, ptile, j);
+    }
+  }
+}
+
 struct GradTable {
   float* dst[34];
   int64_t off[34];
@@ -1943,9 +2081,14 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       }
       {
         ProfScope ps(s, PT_BWD_DGRAD, 2.0 * 256 * 256 * dn, 3072.0 * dn);
-        hipLaunchKernelGGL(k_dgrad, dim3(grid), dim3(256), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
-                           hh[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
-                           ws.gacc + G.be[L - 1], ws.g[cur ^ 1]);
+        if (PCN_DGRAD_WS)
+          hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
+                             hh[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
+                             ws.gacc + G.be[L - 1], ws.g[cur ^ 1]);
+        else
+          hipLaunchKernelGGL(k_dgrad, dim3(grid), dim3(256), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
+                             hh[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
+                             ws.gacc + G.be[L - 1], ws.g[cur ^ 1]);
       }
       cur ^= 1;
     }
