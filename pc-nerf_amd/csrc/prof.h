@@ -6,9 +6,9 @@ namespace pcn {
 // tags reported by pcnerf_prof_read
 enum ProfTag {
   PT_EVAL_QUERY = 0,   // k_nof_eval: fused 9-layer eval query
-  PT_TRAIN_HIDDEN = 1, // k_train_layer<false,true>: 256 -> 256 pre-BN Linear (6 per chunk)
-  PT_TRAIN_FIRST = 2,  // k_train_layer<true,false>: encoding -> 256
-  PT_TRAIN_SKIP = 3,   // k_train_layer<true,true>: [encoding, 256] -> 256
+  PT_TRAIN_HIDDEN = 1, // k_train_ws<0,true>: 256 -> 256 pre-BN Linear (6 per chunk)
+  PT_TRAIN_FIRST = 2,  // k_train_ws<8,false>: encoding -> 256
+  PT_TRAIN_SKIP = 3,   // k_train_ws<8,true>: [encoding, 256] -> 256
   PT_TRAIN_OUT = 4,    // k_train_out
   PT_BN_FOLD = 5,      // k_bn_fold
   PT_COMPOSITE = 6,    // k_composite
@@ -16,7 +16,7 @@ enum ProfTag {
   PT_SAMPLE = 8,       // k_sample_coarse / k_perturb
   PT_COMPOSITE_BWD = 9,// k_composite_bwd
   PT_BWD_WGRAD = 10,   // k_wgrad: weight-gradient GEMM partials (sum over samples on MFMA)
-  PT_BWD_DGRAD = 11,   // k_dgrad: data-gradient GEMM + BatchNorm backward
+  PT_BWD_DGRAD = 11,   // k_dgrad_ws: data-gradient GEMM + BatchNorm backward
   PT_BWD_MISC = 12,    // output-layer backward, partial reduction, BN statistics
 };
 extern bool g_prof_on;
