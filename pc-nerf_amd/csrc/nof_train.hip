@@ -1,23 +1,20 @@
 // Train-mode NOF query: BatchNorm1d with batch statistics over each chunk of `chunk` flattened ray-major
-// samples (nof/render.py:47-50 chunk loop; nn.BatchNorm1d train semantics; models.py:183-203).
+// samples (nof/render.py:47-50 chunk loop; nn.BatchNorm1d train semantics; models.py:183-203), and its backward.
 //
 // Every BatchNorm needs the statistics of its whole chunk before the next Linear may run, so the network is
-// evaluated layer by layer per chunk, one launch per Linear:
-//   k_train_layer<EP,HP> : prologue: BatchNorm L-1's coefficients from the chunk statistics of h_{L-1},
-//                          alpha = gamma/sqrt(var+eps), beta' = beta - mean*alpha (ATen's transform form; block 0
-//                          also updates running_mean/var with momentum and the unbiased variance);
-//                          body: h_L = W_L (alpha*h_{L-1} + beta') + b_L on MFMA, the BatchNorm applied as the
-//                          activations are loaded; h_L written raw (pre-BN) to HBM with per-neuron sums of
-//                          (h - b) and (h - b)^2 reduced in the epilogue;
-//   k_train_out          : the same prologue for BatchNorm 8, occ_out Linear(256,1) + sigmoid.
+// evaluated layer by layer, one launch per Linear (k_train_ws, serving two chunks per launch), then k_train_out:
+//   prologue: BatchNorm L-1's coefficients from the chunk statistics of h_{L-1}, alpha = gamma/sqrt(var+eps),
+//             beta' = beta - mean*alpha (ATen's transform form; block 0 also updates running_mean/var with momentum
+//             and the unbiased variance);
+//   body:     h_L = W_L (alpha*h_{L-1} + beta') + b_L on MFMA, the BatchNorm applied while the input tile is
+//             staged; h_L written raw (pre-BN) to HBM with per-neuron sums of (h - b) and (h - b)^2.
 // The activations LeakyReLU(True) are identities (negative_slope == 1) and are not applied.
 //
-// MFMA mapping (v_mfma_f32_32x32x2_f32), samples on rows: out[sample][neuron] = act[sample][:] . W^T[:][neuron]
-//   A (lane l) = act[sample l&31][feature(t, l>>5)],  B (lane l) = W'[32*ob + (l&31)][feature(t, l>>5)]
-//   D (block ob, reg r, lane l) = out[sample (r&3) + 8*(r>>2) + 4*(l>>5)][neuron 32*ob + (l&31)]
-// so each lane owns one neuron per block and the per-neuron statistics are register sums (no cross-lane
-// reduction).  feature(t, h) = 8*(t>>2) + 4*h + (t&3): k-steps 4g..4g+3 read one float4 per lane from the
-// activation tile stored as [tile][g][lane][4] (1 KiB per wave-instruction).
+// Activation layout (HBM and LDS): tiles of 32 samples, [tile][g][lane][4] with lane = sample + 32 h holding
+// features 8g + 4h + q (1 KiB per wave-instruction).  MFMA v_mfma_f32_32x32x2_f32 with samples on COLUMNS
+// (D = W x^T): A (lane l) = W[neuron 32b + (l&31)][feature(t, l>>5)], B (lane l) = x[sample l&31][feature(t, l>>5)]
+// (the tile's float4 itself), D (reg r, lane l) = out[neuron 32b + (r&3) + 8(r>>2) + 4(l>>5)][sample l&31], so
+// registers 4j..4j+3 are the output tile's float4 at group 4b+j.  feature(t, h) = 8(t>>2) + 4h + (t&3).
 #include <algorithm>
 #include <vector>
 
@@ -28,63 +25,15 @@
 namespace pcn {
 
 // tuning knobs (variant builds for A/B timing; defaults are the shipped configuration)
-#ifndef PCN_TRAIN_WAVES
-#define PCN_TRAIN_WAVES 1  // waves per SIMD the layer kernel is compiled for (launch bounds)
-#endif
-#ifndef PCN_XD
-#define PCN_XD 4  // activation prefetch depth in k-groups (divides 32)
-#endif
-#ifndef PCN_WD
-#define PCN_WD 2  // weight prefetch depth in k-groups (divides 32)
-#endif
-#ifndef PCN_WD2
-#define PCN_WD2 2  // weight prefetch depth of k_train_hidden (k-groups of one half: 4 float4 each)
-#endif
-#ifndef PCN_TRAIN_WS
-#define PCN_TRAIN_WS 7  // k_train_ws (weight-stationary, samples on columns) for: 1 hidden, 2 skip, 4 first layer
-#endif
 #ifndef PCN_WS_XD_SKIP
 #define PCN_WS_XD_SKIP 2  // the same for the skip layer
 #endif
 #ifndef PCN_WS_XD
-#define PCN_WS_XD 4  // k_train_hidden_ws: LDS read ring depth in k-groups
-#endif
-#ifndef PCN_HIDDEN_PP
-#define PCN_HIDDEN_PP 1  // 1: hidden layers run k_train_hidden (epilogue overlapped), 0: k_train_layer<false,true>
-#endif
-#ifndef PCN_PP_SCHED
-#define PCN_PP_SCHED 0  // k_train_hidden: sched_group_barrier interleave per k-group (measured 2.7 % slower: off)
-#endif
-#ifndef PCN_PP_XREG
-#define PCN_PP_XREG 1  // k_train_hidden: the tile's activations register-resident across its two passes
-#endif
-#ifndef PCN_DGRAD_WS
-#define PCN_DGRAD_WS 1  // backward data gradient: 1 weight-stationary k_dgrad_ws, 0 k_dgrad
-#endif
-#ifndef PCN_DGRAD_PF
-#define PCN_DGRAD_PF 1  // k_dgrad: prefetch the BatchNorm-backward operand tile during the GEMM
-#endif
-#ifndef PCN_ABL_PLDS
-#define PCN_ABL_PLDS 0
-#endif
-#ifndef PCN_ABL_PSTAT
-#define PCN_ABL_PSTAT 0
-#endif
-#ifndef PCN_ABL_PSTORE
-#define PCN_ABL_PSTORE 0
-#endif
-#ifndef PCN_ABL_WLOAD
-#define PCN_ABL_WLOAD 0
-#endif
-#ifndef PCN_ABL_XLOAD
-#define PCN_ABL_XLOAD 0
-#endif
-#ifndef PCN_ABL_EPI
-#define PCN_ABL_EPI 0
+#define PCN_WS_XD 4  // k_train_ws / k_dgrad_ws: LDS read ring depth in k-groups
 #endif
 
 #ifndef PCN_CLOCK_STAMP
-#define PCN_CLOCK_STAMP 0  // diagnostic builds only: in-kernel clock of the hidden-layer kernels (see pcnerf_debug_clock)
+#define PCN_CLOCK_STAMP 0  // diagnostic builds only: in-kernel clock of k_train_ws (see pcnerf_debug_clock)
 #endif
 #if PCN_CLOCK_STAMP
 // per workgroup: s_memrealtime (100 MHz, global) at entry / loop begin / loop end / exit (after its atomics
@@ -97,9 +46,6 @@ __device__ unsigned long long g_clk[4096][6];
 #define CLK_END                                                     \
   unsigned long long clk_t1 = __builtin_amdgcn_s_memtime();         \
   unsigned long long clk_r1 = __builtin_amdgcn_s_memrealtime();
-#define CLK_VARS unsigned long long clk_t0 = 0, clk_r0 = 0, clk_t1 = 0, clk_r1 = 0;
-#define CLK_BEGIN_ST clk_t0 = __builtin_amdgcn_s_memtime(); clk_r0 = __builtin_amdgcn_s_memrealtime();
-#define CLK_END_ST clk_t1 = __builtin_amdgcn_s_memtime(); clk_r1 = __builtin_amdgcn_s_memrealtime();
 #define CLK_EXIT                                                                  \
   __builtin_amdgcn_s_waitcnt(0);                                                  \
   if (threadIdx.x == 0 && blockIdx.x < 4096) {                                    \
@@ -112,9 +58,6 @@ __device__ unsigned long long g_clk[4096][6];
 #define CLK_BEGIN
 #define CLK_END
 #define CLK_EXIT
-#define CLK_VARS
-#define CLK_BEGIN_ST
-#define CLK_END_ST
 #endif
 
 constexpr int KG_E = 8, KG_H = 32;
@@ -122,37 +65,6 @@ constexpr size_t SZ_E = (size_t)KG_E * 8 * 64 * 4;
 constexpr size_t SZ_H = (size_t)KG_H * 8 * 64 * 4;
 constexpr size_t TILE_FLOATS = 32 * 256;
 constexpr int LDS_ROW = 260;
-
-
-template <int KG, int NX>
-__device__ __forceinline__ void gemm_n_regs(f32x16 (&acc)[8], const float (&x)[NX], const float* __restrict__ wp,
-                                            int lane) {
-  static_assert(NX == 4 * KG, "operand count");
-  const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(wp) + lane;
-  f32x4 wa[8];
-#pragma unroll
-  for (int ob = 0; ob < 8; ++ob) wa[ob] = w4[ob * 64];
-#pragma unroll
-  for (int kg = 0; kg < KG; ++kg) {
-    f32x4 wb[8];
-    if (kg + 1 < KG) {
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob) wb[ob] = w4[((kg + 1) * 8 + ob) * 64];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob)
-        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[4 * kg + q], wa[ob][q], acc[ob], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (kg + 1 < KG) {
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob) wa[ob] = wb[ob];
-    }
-  }
-}
 
 // Packed train-mode weights: the eval image's layout (off_w) with raw weights (no BatchNorm folding) in the
 // samples-on-rows operand order, feature(t, h) = 8*(t>>2) + 4*h + (t&3).
@@ -218,549 +130,6 @@ __device__ __forceinline__ void bn_coeffs(const BnPrev& B, int64_t n, float mome
   }
 }
 
-// 256-wide input streamed from HBM with the previous BatchNorm applied on load (x*alpha + beta').
-// Software pipeline (one wave per SIMD has no partner to hide latency, so every load is issued ahead):
-//   activations: ring of XD k-groups, weights: ring of WD k-groups, alpha/beta': one group ahead (LDS).
-// Both rings are carried across tiles -- their last loads of a tile fetch the first groups of the next tile
-// (the weights' addresses repeat), so a tile starts with its operands in flight.  KG_H % XD == KG_H % WD == 0
-// keeps the ring slot of group g equal to g % depth in every tile.  sched_barrier pins the loads where they
-// are issued (otherwise the scheduler sinks them next to their first use).
-constexpr int XD = PCN_XD;
-constexpr int WD = PCN_WD;
-static_assert(KG_H % XD == 0 && KG_H % WD == 0, "ring depths must divide the k-group count");
-
-struct HRing {
-  f32x4 x[XD];
-  f32x4 w[WD][8];
-  f32x4 a[2], b[2];  // alpha/beta' of groups kg, kg+1 (read from LDS two groups ahead)
-};
-
-__device__ __forceinline__ void ring_fill(HRing& R, const f32x4* __restrict__ x4, const f32x4* __restrict__ w4,
-                                          const float* __restrict__ al, const float* __restrict__ be, int h4) {
-#pragma unroll
-  for (int d = 0; d < XD; ++d) R.x[d] = x4[d * 64];
-#pragma unroll
-  for (int d = 0; d < WD; ++d)
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
-#pragma unroll
-  for (int d = 0; d < 2; ++d) {
-    R.a[d] = *reinterpret_cast<const f32x4*>(al + 8 * d + h4);
-    R.b[d] = *reinterpret_cast<const f32x4*>(be + 8 * d + h4);
-  }
-}
-
-// `prev_out` (nullable): the previous tile's output, staged in LDS rows `stage_row`, is written to HBM one
-// 1 KiB group per k-group (vmcnt retires in issue order: a burst of 32 stores at the end of a tile would hold
-// back the waits of the next tile's first loads until the whole burst is acknowledged).
-__device__ __forceinline__ void gemm_n_mem(f32x16 (&acc)[8], HRing& R, const f32x4* __restrict__ x4,
-                                           const f32x4* __restrict__ x4_next, const f32x4* __restrict__ w4,
-                                           const float* __restrict__ al, const float* __restrict__ be, int h4,
-                                           f32x4* __restrict__ prev_out, const float* __restrict__ stage_row) {
-#pragma unroll
-  for (int kg = 0; kg < KG_H; ++kg) {
-    f32x4 xa;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xa[q] = R.x[kg % XD][q] * R.a[kg & 1][q] + R.b[kg & 1][q];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob)
-        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[q], R.w[kg % WD][ob][q], acc[ob], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int gw = (kg + WD) % KG_H;  // group kg+WD of this tile, or the first groups of the next tile
-#if !PCN_ABL_WLOAD  // ablation builds (timing only, wrong results): PCN_ABL_WLOAD / _XLOAD skip the reloads
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) R.w[kg % WD][ob] = w4[(gw * 8 + ob) * 64];
-#endif
-#if !PCN_ABL_XLOAD
-    R.x[kg % XD] = kg + XD < KG_H ? x4[(kg + XD) * 64] : x4_next[(kg + XD - KG_H) * 64];
-#endif
-    const int ga = (kg + 2) % KG_H;
-    R.a[kg & 1] = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
-    R.b[kg & 1] = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
-    if (prev_out) prev_out[kg * 64] = *reinterpret_cast<const f32x4*>(stage_row + 8 * kg);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// One Linear over a chunk [c0, c0 + n) of flattened samples.  EP: the encoding half (layer 1, skip half of
-// layer 5) computed from positions (or read from `ein`); HP: the 256 BatchNorm'd features of the previous layer.
-template <bool EP, bool HP>
-__global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_train_layer(
-    const float* __restrict__ rays, int stride, const float* __restrict__ z, int S, int64_t c0, int64_t n,
-    const float* __restrict__ ein, const float* __restrict__ hin, const float* __restrict__ Wp,
-    const float* __restrict__ bias, BnPrev prev, float momentum, float eps, float* __restrict__ hout,
-    double* __restrict__ stats) {
-  __shared__ double st[512];
-  __shared__ __attribute__((aligned(16))) float al[256];
-  __shared__ __attribute__((aligned(16))) float be[256];
-  // per-wave output staging: 32 samples x 256 neurons, rows padded to 260 floats (conflict-free writes by
-  // neuron, conflict-free 16-byte reads by sample)
-  __shared__ __attribute__((aligned(16))) float stage[4][32 * LDS_ROW];
-  for (int i = threadIdx.x; i < 512; i += blockDim.x) st[i] = 0.0;
-  if (HP) bn_coeffs(prev, n, momentum, eps, al, be);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, h = lane >> 5, wv = threadIdx.x >> 6;
-  const int li = lane & 31;
-  const int64_t ntiles = (n + 31) / 32;
-  const int64_t tstride = (int64_t)gridDim.x * 4;
-  const int64_t tile0 = (int64_t)blockIdx.x * 4 + wv;
-  const f32x4* __restrict__ wh4 = reinterpret_cast<const f32x4*>(Wp + (EP ? SZ_E : 0)) + lane;
-  HRing ring;
-  if (HP && tile0 < ntiles)
-    ring_fill(ring, reinterpret_cast<const f32x4*>(hin + tile0 * TILE_FLOATS) + lane, wh4, al, be, 4 * h);
-  f32x4* prev_out = nullptr;  // previous tile's output, still staged in LDS
-  for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
-    // opaque per-iteration offset: keeps the compiler from hoisting all of the layer's weight loads out of the
-    // tile loop (an integer, not the pointer: a laundered pointer loses its global address space -> flat loads)
-    int wofs = 0;
-    asm volatile("" : "+s"(wofs));
-    const float* wpt = Wp + wofs;
-    f32x16 acc[8];
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[ob][r] = 0.0f;
-    if (EP) {
-      int64_t sl = tile * 32 + li;
-      if (sl >= n) sl = n - 1;
-      const int64_t g = c0 + sl;
-      float e[32];
-      if (ein) {
-        load_embedding<1>(ein + g * 63, h, e);
-      } else {
-        const float* r = rays + (g / S) * stride;
-        float p[3];
-        sample_point(r, z[g], p);
-        encode_half<1>(p, h, e);
-      }
-      gemm_n_regs<KG_E>(acc, e, wpt, lane);
-    }
-    float* lt = stage[wv];
-    const float* lrow = lt + li * LDS_ROW + 4 * h;
-    if (HP) {
-      const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
-      gemm_n_mem(acc, ring, reinterpret_cast<const f32x4*>(hin + tile * TILE_FLOATS) + lane,
-                 reinterpret_cast<const f32x4*>(hin + nxt * TILE_FLOATS) + lane, wh4 + wofs, al, be, 4 * h,
-                 prev_out, lrow);
-      prev_out = nullptr;
-    }
-    if (prev_out) {  // EP-only layer: no k-group loop to hide the stores in
-#pragma unroll
-      for (int g = 0; g < 32; ++g) prev_out[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // epilogue: + bias -> LDS stage [sample][neuron]; statistics of (h - bias) over valid samples
-    const int64_t base = tile * 32;
-#if PCN_ABL_EPI  // ablation (timing only): no epilogue, the accumulators kept live by one store
-    {
-      float t = 0.0f;
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[ob][r];
-      hout[tile * TILE_FLOATS + lane] = t;
-      continue;
-    }
-#endif
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) {
-      const int nn = 32 * ob + li;
-      const float bo = bias[nn];
-      float s1 = 0.0f, s2 = 0.0f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int s = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float d = acc[ob][r];
-        lt[s * LDS_ROW + nn] = d + bo;
-        if (base + s < n) {
-          s1 += d;
-          s2 += d * d;
-        }
-      }
-      atomicAdd(&st[2 * nn], (double)s1);
-      atomicAdd(&st[2 * nn + 1], (double)s2);
-    }
-    // the raw h of this tile goes to the next layer's [g][lane][4] layout (1 KiB dwordx4 stores) during the
-    // next tile's k-group loop, or below after the last tile
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    prev_out = reinterpret_cast<f32x4*>(hout + tile * TILE_FLOATS) + lane;
-  }
-  if (prev_out) {
-    const float* lrow = stage[wv] + li * LDS_ROW + 4 * h;
-#pragma unroll
-    for (int g = 0; g < 32; ++g) prev_out[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 512; i += blockDim.x) atomicAdd(&stats[i], st[i]);
-}
-
-// ---- k_train_hidden: k_train_layer<false,true> with the epilogue hidden behind the MFMA stream.
-// Each 32-sample tile is computed in two passes over K (neurons 0-127, then 128-255), each into its own 64
-// accumulators.  While a pass runs its 512 MFMAs, the epilogue of the PREVIOUS pass (the other accumulator set:
-// + bias, LDS staging, BatchNorm statistics) and the HBM stores of the pass before that (LDS -> 1 KiB dwordx4 per
-// k-group) are interleaved between the MFMA groups, two values and half a store per k-group, so the matrix pipe
-// never idles for the epilogue (it cost 14 % of k_train_layer's time, measured by an ablation build).
-// Stage regions: pass (t, half E)'s epilogue writes neurons [128E, 128E+128) of the stage, the stores of that
-// region are issued during pass (t+1, E) and the region is rewritten during pass (t+1, 1-E) -- program order of
-// one wave's LDS operations keeps the three apart.  Statistics: same per-(lane, neuron) fp32 partial sums over
-// the tile's 16 rows, in the same order, as k_train_layer.
-constexpr int PXD = PCN_XD;
-constexpr int PWD = PCN_WD2;
-static_assert(KG_H % PXD == 0 && KG_H % PWD == 0, "ring depths must divide the k-group count");
-
-struct PRing {
-  f32x4 x[PXD];
-  f32x4 w[PWD][4];
-  f32x4 a[2], b[2];  // BatchNorm alpha/beta' of k-groups kg, kg+1 (read from LDS two groups ahead)
-  f32x4 xa;          // BatchNorm'd activations of the current k-group
-};
-
-struct PEpi {            // epilogue of the previous pass
-  float* lt;             // this wave's stage
-  int64_t base;          // first sample of its tile
-  float on;              // 0 when there is no previous pass (statistics multiplied by it)
-};
-
-// Per k-group interleave of the 16 MFMAs with the pass's other instructions: at most 2 VALU and one memory
-// operation per MFMA gap (cdna_hip_programming.md T19; MI355X_MICROARCH issue costs: a 64-cycle f32 MFMA hides
-// a handful of 4-cycle issues, a block of them between two MFMAs stalls the matrix pipe).
-__device__ __forceinline__ void pp_interleave() {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU
-    if (i < 10 && (i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
-    if (i == 1 || i == 5 || i == 9) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-    if (i == 3 || i == 11) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-    if (i == 13) __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // VMEM write
-  }
-}
-
-template <int H>
-__device__ __forceinline__ void pp_pass(f32x16 (&acc)[4], const f32x16 (&eacc)[4], PRing& R,
-                                        const f32x4* __restrict__ x4, const f32x4* __restrict__ x4_next,
-                                        const f32x4* __restrict__ w4, const float* __restrict__ al,
-                                        const float* __restrict__ be, const float* __restrict__ bias, int lane,
-                                        const PEpi& E, int64_t n, double* st, f32x4* __restrict__ sout) {
-  constexpr int EH = 1 - H;  // half of the previous pass
-  const int li = lane & 31, h = lane >> 5, h4 = 4 * h;
-  float ebias[4];
-#pragma unroll
-  for (int ob = 0; ob < 4; ++ob) ebias[ob] = bias[32 * (4 * EH + ob) + li];
-  const float* srow = E.lt + li * LDS_ROW + h4;
-  // rows of the previous pass's tile that hold samples < n, as a per-lane bound on the register row
-  const int64_t nv64 = n - E.base;
-  const int lim = (nv64 >= 32 ? 32 : (int)nv64) - h4;
-  float s1 = 0.0f, s2 = 0.0f;
-  f32x4 sv;
-#pragma unroll
-  for (int kg = 0; kg < KG_H; ++kg) {
-    const f32x4 xa = R.xa;   // BatchNorm'd activations of this k-group (computed during the previous one)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        const f32x16 c = (kg == 0 && q == 0) ? f32x16{} : acc[ob];
-        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[q], R.w[kg % PWD][ob][q], c, 0, 0, 0);
-      }
-    }
-    // epilogue values v = 2 kg, 2 kg + 1 of the previous pass
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int v = 2 * kg + u, ob = v >> 4, r = v & 15;
-      const int sr = (r & 3) + 8 * (r >> 2);   // sample row of register r (lane half adds 4)
-      const int nn = 32 * (4 * EH + ob) + li;
-      const float d = eacc[ob][r];
-#if !PCN_ABL_PLDS
-      E.lt[(sr + h4) * LDS_ROW + nn] = d + ebias[ob];
-#endif
-#if !PCN_ABL_PSTAT
-      const float dv = sr < lim ? d : 0.0f;
-      s1 += dv;
-      s2 += dv * dv;
-#endif
-      if (r == 15) {
-        atomicAdd(&st[2 * nn], (double)(s1 * E.on));
-        atomicAdd(&st[2 * nn + 1], (double)(s2 * E.on));
-        s1 = 0.0f;
-        s2 = 0.0f;
-      }
-    }
-    // staged output of the pass before (half H of the previous tile): LDS read on even k-groups, store on odd
-#if !PCN_ABL_PSTORE
-    {
-      const int g = 16 * H + (kg >> 1);
-      if ((kg & 1) == 0) sv = *reinterpret_cast<const f32x4*>(srow + 8 * g);
-      else sout[g * 64] = sv;
-    }
-#endif
-    // prefetch: stream position kg + depth (the next pass: same tile's other half for H = 0, next tile for H = 1)
-    const int gw = kg + PWD;
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      const int gg = gw < KG_H ? gw : gw - KG_H;
-      const int hh = gw < KG_H ? H : 1 - H;
-      R.w[kg % PWD][ob] = w4[(gg * 8 + 4 * hh + ob) * 64];
-    }
-    {
-      const int gx = kg + PXD;
-      if (gx < KG_H) R.x[kg % PXD] = x4[gx * 64];
-      else R.x[kg % PXD] = (H == 0 ? x4 : x4_next)[(gx - KG_H) * 64];
-    }
-    // BatchNorm of the next k-group's activations (ring slots hold group kg + 1 already)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) R.xa[q] = R.x[(kg + 1) % PXD][q] * R.a[(kg + 1) & 1][q] + R.b[(kg + 1) & 1][q];
-    const int ga = (kg + 2) % KG_H;
-    R.a[kg & 1] = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
-    R.b[kg & 1] = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
-#if PCN_PP_SCHED
-    pp_interleave();
-#endif
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// Variant with the tile's 32 activation groups register-resident (128 VGPRs): pass A loads nothing for x (the
-// raw groups were loaded during the previous tile's pass B), applies the BatchNorm in place one group ahead, and
-// pass B reuses the BatchNorm'd groups -- no second read of the tile, no second BatchNorm -- and refills each
-// group with the next tile's raw values right after its last use.
-struct XRing {
-  f32x4 w[PWD][4];
-  f32x4 a[2], b[2];  // alpha/beta' ring (pass A reads group kg + 2 into slot kg & 1)
-};
-
-template <int H>
-__device__ __forceinline__ void pp_pass_x(f32x16 (&acc)[4], const f32x16 (&eacc)[4], f32x4 (&X)[KG_H], XRing& R,
-                                          const f32x4* __restrict__ xn4, const f32x4* __restrict__ w4,
-                                          const float* __restrict__ al, const float* __restrict__ be,
-                                          const float* __restrict__ bias, int lane, const PEpi& E, int64_t n,
-                                          double* st, f32x4* __restrict__ sout) {
-  constexpr int EH = 1 - H;
-  const int li = lane & 31, h = lane >> 5, h4 = 4 * h;
-  float ebias[4];
-#pragma unroll
-  for (int ob = 0; ob < 4; ++ob) ebias[ob] = bias[32 * (4 * EH + ob) + li];
-  const float* srow = E.lt + li * LDS_ROW + h4;
-  const int64_t nv64 = n - E.base;
-  const int lim = (nv64 >= 32 ? 32 : (int)nv64) - h4;
-  float s1 = 0.0f, s2 = 0.0f;
-  f32x4 sv;
-#pragma unroll
-  for (int kg = 0; kg < KG_H; ++kg) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        const f32x16 c = (kg == 0 && q == 0) ? f32x16{} : acc[ob];
-        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(X[kg][q], R.w[kg % PWD][ob][q], c, 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int v = 2 * kg + u, ob = v >> 4, r = v & 15;
-      const int sr = (r & 3) + 8 * (r >> 2);
-      const int nn = 32 * (4 * EH + ob) + li;
-      const float d = eacc[ob][r];
-      E.lt[(sr + h4) * LDS_ROW + nn] = d + ebias[ob];
-      const float dv = sr < lim ? d : 0.0f;
-      s1 += dv;
-      s2 += dv * dv;
-      if (r == 15) {
-        atomicAdd(&st[2 * nn], (double)(s1 * E.on));
-        atomicAdd(&st[2 * nn + 1], (double)(s2 * E.on));
-        s1 = 0.0f;
-        s2 = 0.0f;
-      }
-    }
-    {
-      const int g = 16 * H + (kg >> 1);
-      if ((kg & 1) == 0) sv = *reinterpret_cast<const f32x4*>(srow + 8 * g);
-      else sout[g * 64] = sv;
-    }
-    const int gw = kg + PWD;
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      const int gg = gw < KG_H ? gw : gw - KG_H;
-      const int hh = gw < KG_H ? H : 1 - H;
-      R.w[kg % PWD][ob] = w4[(gg * 8 + 4 * hh + ob) * 64];
-    }
-    if (H == 0) {
-      // BatchNorm of the next group in place (its alpha/beta' sit in slot (kg+1)&1), then refill slot kg&1
-      if (kg + 1 < KG_H) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) X[kg + 1][q] = X[kg + 1][q] * R.a[(kg + 1) & 1][q] + R.b[(kg + 1) & 1][q];
-      }
-      const int ga = (kg + 2) % KG_H;
-      R.a[kg & 1] = *reinterpret_cast<const f32x4*>(al + 8 * ga + h4);
-      R.b[kg & 1] = *reinterpret_cast<const f32x4*>(be + 8 * ga + h4);
-    } else {
-      X[kg] = xn4[kg * 64];   // next tile's raw group kg
-      if (kg == KG_H - 1) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) X[0][q] = X[0][q] * R.a[0][q] + R.b[0][q];
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-__global__ __launch_bounds__(256, 1) void k_train_hidden(const float* __restrict__ hin, int64_t n,
-                                                         const float* __restrict__ Wp,
-                                                         const float* __restrict__ bias, BnPrev prev,
-                                                         float momentum, float eps, float* __restrict__ hout,
-                                                         float* __restrict__ trash, double* __restrict__ stats) {
-  CLK_ENTRY
-  CLK_VARS
-  __shared__ double st[512];
-  __shared__ __attribute__((aligned(16))) float al[256];
-  __shared__ __attribute__((aligned(16))) float be[256];
-  __shared__ __attribute__((aligned(16))) float stage[4][32 * LDS_ROW];
-  for (int i = threadIdx.x; i < 512; i += blockDim.x) st[i] = 0.0;
-  bn_coeffs(prev, n, momentum, eps, al, be);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, h = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar tile bookkeeping
-  const int64_t ntiles = (n + 31) / 32;
-  const int64_t tstride = (int64_t)gridDim.x * 4;
-  const int64_t tile0 = (int64_t)blockIdx.x * 4 + wv;
-#if PCN_PP_XREG
-  if (tile0 < ntiles) {
-    const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wp) + lane;
-    float* lt = stage[wv];
-    XRing R;
-    f32x4 X[KG_H];
-    {
-      const f32x4* x0 = reinterpret_cast<const f32x4*>(hin + tile0 * TILE_FLOATS) + lane;
-#pragma unroll
-      for (int g = 0; g < KG_H; ++g) X[g] = x0[g * 64];
-#pragma unroll
-      for (int d = 0; d < PWD; ++d)
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        R.a[d] = *reinterpret_cast<const f32x4*>(al + 8 * d + 4 * h);
-        R.b[d] = *reinterpret_cast<const f32x4*>(be + 8 * d + 4 * h);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) X[0][q] = X[0][q] * R.a[0][q] + R.b[0][q];
-    }
-    f32x16 accA[4], accB[4];
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) accB[ob] = f32x16{};
-    int64_t prev_tile = -1;
-    CLK_BEGIN_ST
-    for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
-      int wofs = 0;
-      asm volatile("" : "+s"(wofs));
-      const f32x4* wt = w4 + wofs;
-      const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
-      const f32x4* x4n = reinterpret_cast<const f32x4*>(hin + nxt * TILE_FLOATS) + lane;
-      f32x4* pout = reinterpret_cast<f32x4*>(prev_tile >= 0 ? hout + prev_tile * TILE_FLOATS : trash) + lane;
-      const PEpi ea{lt, prev_tile >= 0 ? prev_tile * 32 : 0, prev_tile >= 0 ? 1.0f : 0.0f};
-      pp_pass_x<0>(accA, accB, X, R, x4n, wt, al, be, bias, lane, ea, n, st, pout);
-      const PEpi eb{lt, tile * 32, 1.0f};
-      pp_pass_x<1>(accB, accA, X, R, x4n, wt, al, be, bias, lane, eb, n, st, pout);
-      prev_tile = tile;
-    }
-#else
-  if (tile0 < ntiles) {
-    const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wp) + lane;
-    float* lt = stage[wv];
-    PRing R;
-    {
-      const f32x4* x0 = reinterpret_cast<const f32x4*>(hin + tile0 * TILE_FLOATS) + lane;
-#pragma unroll
-      for (int d = 0; d < PXD; ++d) R.x[d] = x0[d * 64];
-#pragma unroll
-      for (int d = 0; d < PWD; ++d)
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        R.a[d] = *reinterpret_cast<const f32x4*>(al + 8 * d + 4 * h);
-        R.b[d] = *reinterpret_cast<const f32x4*>(be + 8 * d + 4 * h);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) R.xa[q] = R.x[0][q] * R.a[0][q] + R.b[0][q];
-    }
-    f32x16 accA[4], accB[4];
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) accB[ob] = f32x16{};
-    int64_t prev_tile = -1;
-    for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
-      int wofs = 0;  // opaque offset: keeps the weight loads inside the tile loop (see k_train_layer)
-      asm volatile("" : "+s"(wofs));
-      const f32x4* wt = w4 + wofs;
-      const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
-      const f32x4* x4 = reinterpret_cast<const f32x4*>(hin + tile * TILE_FLOATS) + lane;
-      const f32x4* x4n = reinterpret_cast<const f32x4*>(hin + nxt * TILE_FLOATS) + lane;
-      // first tile: there is no previous tile, its (meaningless) stores go to a scratch tile nobody reads
-      f32x4* pout = reinterpret_cast<f32x4*>(prev_tile >= 0 ? hout + prev_tile * TILE_FLOATS : trash) + lane;
-      const PEpi ea{lt, prev_tile >= 0 ? prev_tile * 32 : 0, prev_tile >= 0 ? 1.0f : 0.0f};
-      pp_pass<0>(accA, accB, R, x4, x4n, wt, al, be, bias, lane, ea, n, st, pout);
-      const PEpi eb{lt, tile * 32, 1.0f};
-      pp_pass<1>(accB, accA, R, x4, x4n, wt, al, be, bias, lane, eb, n, st, pout);
-      prev_tile = tile;
-    }
-#endif
-    CLK_END_ST
-    // drain: epilogue of the last tile's second half, then all of its stores
-    {
-      const int li = lane & 31;
-      float s1, s2;
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        const int nn = 32 * (4 + ob) + li;
-        const float bo = bias[nn];
-        s1 = 0.0f;
-        s2 = 0.0f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int smp = (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float d = accB[ob][r];
-          lt[smp * LDS_ROW + nn] = d + bo;
-          const float dv = (prev_tile * 32 + smp < n) ? d : 0.0f;
-          s1 += dv;
-          s2 += dv * dv;
-        }
-        atomicAdd(&st[2 * nn], (double)s1);
-        atomicAdd(&st[2 * nn + 1], (double)s2);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      f32x4* out = reinterpret_cast<f32x4*>(hout + prev_tile * TILE_FLOATS) + lane;
-      const float* lrow = lt + li * LDS_ROW + 4 * h;
-#pragma unroll
-      for (int g = 0; g < 32; ++g) out[g * 64] = *reinterpret_cast<const f32x4*>(lrow + 8 * g);
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 512; i += blockDim.x) atomicAdd(&stats[i], st[i]);
-  CLK_EXIT
-}
-
-// ---- k_train_hidden_ws: weight-stationary hidden layer, samples on COLUMNS (D = W x^T).
-// A workgroup of 8 waves (two per SIMD) computes all 256 neurons of one 32-sample tile at a time; wave b owns
-// neurons 32b..32b+31, whose weights are its MFMA A operand, loaded ONCE per launch into 128 registers (the
-// packed B-operand image of the samples-on-rows kernels has exactly the per-lane content the A operand of the
-// transposed product wants).  The B operand is the activation tile's [g][lane][4] float4 itself, staged once
-// per workgroup in LDS (double buffered, BatchNorm applied while staging, next tile's HBM loads in flight
-// during the current tile's MFMAs).  In this orientation accumulator registers 4j..4j+3 of wave b ARE the
-// output tile's float4 at group 4b+j, so the raw h goes to HBM straight from registers (no LDS transpose), and
-// each lane owns one sample: the per-neuron statistics are per-lane running sums (kept in an LDS slot of the
-// lane's own) across all the workgroup's tiles, reduced across lanes once at the end -- one coalesced float64
-// atomic per (neuron, moment) and workgroup.  No weight traffic inside the tile loop at all.
-// Two waves per SIMD (8 per workgroup, 256 registers each) measured 267 us per chunk of 262,144 samples against
-// 295 us for one wave per SIMD owning 64 neurons (k_train_hidden: 299 us).
 constexpr int WS_XD = PCN_WS_XD;
 
 // Encoding feature group g (features 8g + 4h + q, q = 0..3) of a sample at p for lane half h: Embedding(3, 10) as
@@ -1057,8 +426,7 @@ static TrainWs carve(void* base, int64_t chunk) {
     off += (bytes + 255) & ~(size_t)255;
     return o;
   };
-  // one extra tile per activation buffer: the scratch target of k_train_hidden's first-tile stores
-  const size_t oA = take((tiles + 1) * TILE_FLOATS * 4), oB = take((tiles + 1) * TILE_FLOATS * 4);
+  const size_t oA = take(tiles * TILE_FLOATS * 4), oB = take(tiles * TILE_FLOATS * 4);
   const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
   char* b = (char*)base;
   TrainWs w;
@@ -1143,8 +511,6 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
   for (int64_t c0 = 0; c0 < total; c0 += chunk) {
     const int64_t n = total - c0 < chunk ? total - c0 : chunk;
     const int64_t ntiles = (n + 31) / 32;
-    const unsigned maxg = 256u * PCN_TRAIN_WAVES;
-    const unsigned grid = (unsigned)(ntiles / 4 + 1 < maxg ? ntiles / 4 + 1 : maxg);
     const unsigned gws = (unsigned)(ntiles < 256 ? ntiles : 256);   // k_train_ws: one workgroup per CU
     const double dn = (double)n;
     // stored chunk: every layer writes its own buffer of the store (kept for the backward); else ping-pong
@@ -1152,21 +518,15 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     const bool keep = store && ci < store_chunks;
     const StoreChunk sc = keep ? store_chunk(store, chunk, ci) : StoreChunk{};
     double* stats = keep ? sc.stats : ws.stats;
-    float* trash = ws.bufA + (size_t)((chunk + 31) / 32) * TILE_FLOATS;
     PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));
     float* hin = keep ? sc.h[0] : ws.bufA;
     float* hout = keep ? sc.h[1] : ws.bufB;
     {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
-      if (PCN_TRAIN_WS & 4)
-        hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
-                           ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps,
-                           hin, stats);
-      else
-        hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                           n_samples, c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none,
-                           momentum, eps, hin, stats);
+      hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
+                         ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps, hin,
+                         stats);
     }
     for (int L = 1; L < 8; ++L) {
       if (keep) {
@@ -1177,28 +537,15 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
                         stats + 512 * (L - 1)};
       if (L == 4) {
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
-        if (PCN_TRAIN_WS & 2)
-          hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
-                             c0, ein, hin, n, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
-                             stats + 512 * L);
-        else
-          hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                             n_samples, c0, n, ein, hin, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps,
-                             hout, stats + 512 * L);
+        hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
+                           c0, ein, hin, n, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
+                           stats + 512 * L);
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        if (PCN_TRAIN_WS & 1)
-          hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
-                             ein, hin, n, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps, hout,
-                             stats + 512 * L);
-        else if (PCN_HIDDEN_PP)
-          hipLaunchKernelGGL(k_train_hidden, dim3(grid), dim3(256), 0, s, hin, n, ws.wp + off_w(L, false),
-                             P.lin_b[L], prev, momentum, eps, hout, trash, stats + 512 * L);
-        else
-          hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                             n_samples, c0, n, ein, hin, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps,
-                             hout, stats + 512 * L);
+        hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
+                           ein, hin, n, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps, hout,
+                           stats + 512 * L);
       }
       float* t = hin;
       hin = hout;
@@ -1254,14 +601,14 @@ extern "C" int pcnerf_nof_forward_train(const float* emb, int64_t n, const pcner
 // =============================================================================================== backward
 // dL/dparams of the train-mode query (loss.backward() through render.py:47-50 and models.py:183-203), given
 // dL/dlogit per sample (or dL/dp with p).  Per chunk:
-//   1. forward recomputation with k_train_layer, the raw h_L of all 8 layers kept (1 KiB/sample each) and the
-//      chunk statistics re-derived (running stats untouched); k_bn_save stores mean/invstd/alpha/beta;
+//   1. the forward's raw h_L of all 8 layers (1 KiB/sample each) and chunk statistics: from the activation store,
+//      or recomputed with k_train_ws (running stats untouched); k_bn_save stores mean/invstd/alpha/beta;
 //   2. occ_out + BatchNorm 8 backward (k_out_bwd_stats, k_out_bwd_grad) -> dL/dh_7;
 //   3. for L = 7..1: k_wgrad: G_L = sum_s dL/dh_L[s] (x) (h_{L-1}[s] - mean_{L-1})   (+ the encoding part at L=4)
 //                    on MFMA, partials per block;  k_wgrad_reduce: dW_L = alpha*G + beta (x) db, db_L, and the
 //                    statistics BatchNorm L-1's backward needs, which are algebraic in G and db:
 //                      sum_s dL/dy = W^T db,   sum_s dL/dy (h - mean) = colsum(W o G);
-//                    k_dgrad: dL/dh_{L-1} = BN_back(W_L^T dL/dh_L) on MFMA, the BatchNorm backward fused into
+//                    k_dgrad_ws: dL/dh_{L-1} = BN_back(W_L^T dL/dh_L) on MFMA, the BatchNorm backward fused into
 //                    the epilogue (ATen's formula: (dy - mean(dy) - (h - mean) * k) * invstd * gamma);
 //   4. k_wgrad / k_wgrad_reduce for layer 0 on the recomputed encoding.
 // Parameter gradients accumulate in float64 across chunks and are added to the caller's fp32 buffers at the
@@ -1608,143 +955,7 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int nblk, const f
   if (t == 0) db[m] += dbm;
 }
 
-// ---- data gradient: dL/dh_{L-1} = BN_{L-1}_back(W_L^T dL/dh_L), samples on MFMA columns:
-//   A = packed W_L^T (k_pack_dgrad), B (lane l, k-step t) = dL/dh_L[sample l&31][feature(t, l>>5)]
-//   D (block ob, reg r, lane l) = dL/dy[sample l&31][neuron 32 ob + (r&3) + 8 (r>>2) + 4 (l>>5)]
-// so registers 4gq..4gq+3 of block ob are exactly the float4 at [g = 4 ob + gq][lane] of the tile layout: the
-// h_{L-1} operand of the BatchNorm backward and the result move as coalesced 1 KiB wave accesses.
-struct TRing {
-  f32x4 x[XD];
-  f32x4 w[WD][8];
-};
-
-__device__ __forceinline__ void tring_fill(TRing& R, const f32x4* __restrict__ x4, const f32x4* __restrict__ w4) {
-#pragma unroll
-  for (int d = 0; d < XD; ++d) R.x[d] = x4[d * 64];
-#pragma unroll
-  for (int d = 0; d < WD; ++d)
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) R.w[d][ob] = w4[(d * 8 + ob) * 64];
-}
-
-// `prev_out` (nullable): the previous tile's dL/dh, staged in LDS as [g][lane] float4s, is written one 1 KiB
-// group per k-group (the store burst would otherwise hold back the vmcnt waits of the next loads).
-// `hp4` / `hx`: the BatchNorm backward's h_{L-1} tile is prefetched during the first 16 k-groups (two 1 KiB loads
-// each) instead of as a 32-load burst after the GEMM, so its latency hides behind the MFMAs.
-__device__ __forceinline__ void gemm_t_mem(f32x16 (&acc)[8], TRing& R, const f32x4* __restrict__ x4,
-                                           const f32x4* __restrict__ x4_next, const f32x4* __restrict__ w4,
-                                           f32x4* __restrict__ prev_out, const f32x4* __restrict__ stage,
-                                           const f32x4* __restrict__ hp4, f32x4 (&hx)[32]) {
-#pragma unroll
-  for (int kg = 0; kg < KG_H; ++kg) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob)
-        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(R.w[kg % WD][ob][q], R.x[kg % XD][q], acc[ob], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int gw = (kg + WD) % KG_H;
-#if !PCN_ABL_WLOAD  // ablation builds (timing only, wrong results): PCN_ABL_WLOAD / _XLOAD skip the reloads
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) R.w[kg % WD][ob] = w4[(gw * 8 + ob) * 64];
-#endif
-#if !PCN_ABL_XLOAD
-    R.x[kg % XD] = kg + XD < KG_H ? x4[(kg + XD) * 64] : x4_next[(kg + XD - KG_H) * 64];
-#endif
-    if (prev_out) prev_out[kg * 64] = stage[kg * 64];
-#if PCN_DGRAD_PF
-    if (kg < 16) {
-      hx[2 * kg] = hp4[(2 * kg) * 64];
-      hx[2 * kg + 1] = hp4[(2 * kg + 1) * 64];
-    }
-#endif
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-__global__ __launch_bounds__(256, PCN_TRAIN_WAVES) void k_dgrad(
-    const float* __restrict__ gin, const float* __restrict__ Wt, const float* __restrict__ hprev, int64_t n,
-    const double* __restrict__ s12, const float* __restrict__ coefp, const float* __restrict__ gamma,
-    double* __restrict__ d_gamma, double* __restrict__ d_beta, float* __restrict__ gout) {
-  __shared__ __attribute__((aligned(16))) float cgm[256];
-  __shared__ __attribute__((aligned(16))) float ckk[256];
-  __shared__ __attribute__((aligned(16))) float cmu[256];
-  __shared__ __attribute__((aligned(16))) float cis[256];
-  __shared__ __attribute__((aligned(16))) float cga[256];
-  __shared__ f32x4 stage[4][32 * 64];  // per-wave output tile in the [g][lane] layout (32 KiB)
-  {
-    const int k = threadIdx.x;
-    const double S1 = s12[2 * k], dotp = s12[2 * k + 1];
-    const float invstd = coefp[256 + k];
-    cgm[k] = (float)(S1 / (double)n);
-    ckk[k] = (((float)dotp * invstd) * invstd) / (float)n;
-    cmu[k] = coefp[k];
-    cis[k] = invstd;
-    cga[k] = gamma[k];
-    if (blockIdx.x == 0) {
-      d_gamma[k] += dotp * (double)invstd;
-      d_beta[k] += S1;
-    }
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, h = lane >> 5, wv = threadIdx.x >> 6, li = lane & 31;
-  const int64_t ntiles = (n + 31) / 32;
-  const int64_t tstride = (int64_t)gridDim.x * 4;
-  const int64_t tile0 = (int64_t)blockIdx.x * 4 + wv;
-  const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(Wt) + lane;
-  f32x4* st = stage[wv] + lane;
-  TRing ring;
-  if (tile0 < ntiles) tring_fill(ring, reinterpret_cast<const f32x4*>(gin + tile0 * TILE_FLOATS) + lane, w4);
-  f32x4* prev_out = nullptr;
-  for (int64_t tile = tile0; tile < ntiles; tile += tstride) {
-    int wofs = 0;
-    asm volatile("" : "+s"(wofs));
-    f32x16 acc[8];
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[ob][r] = 0.0f;
-    const int64_t nxt = tile + tstride < ntiles ? tile + tstride : tile;
-    const f32x4* hp4 = reinterpret_cast<const f32x4*>(hprev + tile * TILE_FLOATS) + lane;
-    f32x4 hx[32];
-    gemm_t_mem(acc, ring, reinterpret_cast<const f32x4*>(gin + tile * TILE_FLOATS) + lane,
-               reinterpret_cast<const f32x4*>(gin + nxt * TILE_FLOATS) + lane, w4 + wofs, prev_out, st, hp4, hx);
-    const bool valid = tile * 32 + li < n;
-#if !PCN_DGRAD_PF
-#pragma unroll
-    for (int g = 0; g < 32; ++g) hx[g] = hp4[g * 64];
-#endif
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) {
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int g = 4 * ob + gq, f0 = 8 * g + 4 * h;
-        const f32x4 gm = *reinterpret_cast<const f32x4*>(cgm + f0), kk = *reinterpret_cast<const f32x4*>(ckk + f0);
-        const f32x4 mu = *reinterpret_cast<const f32x4*>(cmu + f0), is = *reinterpret_cast<const f32x4*>(cis + f0);
-        const f32x4 ga = *reinterpret_cast<const f32x4*>(cga + f0);
-        f32x4 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          o[q] = valid ? ((acc[ob][4 * gq + q] - gm[q]) - (hx[g][q] - mu[q]) * kk[q]) * is[q] * ga[q] : 0.0f;
-        st[g * 64] = o;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    prev_out = reinterpret_cast<f32x4*>(gout + tile * TILE_FLOATS) + lane;
-  }
-  if (prev_out) {
-#pragma unroll
-    for (int g = 0; g < 32; ++g) prev_out[g * 64] = st[g * 64];
-  }
-}
-
-// ---- k_dgrad_ws: k_dgrad in the weight-stationary form of k_train_ws<0,true>.  A workgroup of 8 waves (two per
+// ---- k_dgrad_ws: the data gradient in the weight-stationary form of k_train_ws<0,true>.  A workgroup of 8 waves (two per
 // SIMD) computes all 256 input features of one 32-sample tile at a time; wave b holds the W^T rows of features
 // 32b..32b+31 (128 registers, loaded once per launch) as the A operand, the dL/dh tile is staged raw in LDS
 // (double buffered, next tile's loads in flight), and the BatchNorm backward runs on the accumulators: register
@@ -1997,9 +1208,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     const int64_t n = total - c0 < chunk ? total - c0 : chunk;
     const int64_t ntiles = (n + 31) / 32;
     const double dn = (double)n;
-    const unsigned maxg = 256u * PCN_TRAIN_WAVES;
-    const unsigned grid = (unsigned)(ntiles / 4 + 1 < maxg ? ntiles / 4 + 1 : maxg);
-    const unsigned gws = (unsigned)(ntiles < 256 ? ntiles : 256);
+    const unsigned gws = (unsigned)(ntiles < 256 ? ntiles : 256);   // k_train_ws / k_dgrad_ws
     const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
     const unsigned wblocks = (unsigned)(ntiles < WG_BLOCKS ? ntiles : WG_BLOCKS);
     // 1. the forward's layer outputs and statistics: from the activation store, or recomputed here
@@ -2013,37 +1222,22 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     if (!kept) {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
-      if (PCN_TRAIN_WS & 4)
-        hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
-                           ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps,
-                           ws.h[0], ws.stats);
-      else
-        hipLaunchKernelGGL((k_train_layer<true, false>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                           n_samples, c0, n, ein, (const float*)nullptr, ws.wp + off_w(0, true), P.lin_b[0], none,
-                           mom, eps, ws.h[0], ws.stats);
+      hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
+                         ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps, ws.h[0],
+                         ws.stats);
     }
     for (int L = 1; L < 8 && !kept; ++L) {
       const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], nullptr, nullptr, P.lin_b[L - 1], ws.stats + 512 * (L - 1)};
       if (L == 4) {
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
-        if (PCN_TRAIN_WS & 2)
-          hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
-                             c0, ein, ws.h[3], n, ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps, ws.h[4],
-                             ws.stats + 512 * 4);
-        else
-          hipLaunchKernelGGL((k_train_layer<true, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                             n_samples, c0, n, ein, ws.h[3], ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps,
-                             ws.h[4], ws.stats + 512 * 4);
+        hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
+                           c0, ein, ws.h[3], n, ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps, ws.h[4],
+                           ws.stats + 512 * 4);
       } else {
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        if (PCN_TRAIN_WS & 1)
-          hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
-                             ein, ws.h[L - 1], n, ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps, ws.h[L],
-                             ws.stats + 512 * L);
-        else
-          hipLaunchKernelGGL((k_train_layer<false, true>), dim3(grid), dim3(256), 0, s, rays, ray_stride, z,
-                             n_samples, c0, n, ein, ws.h[L - 1], ws.wp + off_w(L, false), P.lin_b[L], prev, mom,
-                             eps, ws.h[L], ws.stats + 512 * L);
+        hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
+                           ein, ws.h[L - 1], n, ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps, ws.h[L],
+                           ws.stats + 512 * L);
       }
     }
     {
@@ -2081,14 +1275,9 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       }
       {
         ProfScope ps(s, PT_BWD_DGRAD, 2.0 * 256 * 256 * dn, 3072.0 * dn);
-        if (PCN_DGRAD_WS)
-          hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
-                             hh[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
-                             ws.gacc + G.be[L - 1], ws.g[cur ^ 1]);
-        else
-          hipLaunchKernelGGL(k_dgrad, dim3(grid), dim3(256), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
-                             hh[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
-                             ws.gacc + G.be[L - 1], ws.g[cur ^ 1]);
+        hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
+                           hh[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1],
+                           ws.g[cur ^ 1]);
       }
       cur ^= 1;
     }
