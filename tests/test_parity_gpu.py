@@ -225,6 +225,27 @@ def test_render_train_vs_oracle_config2_subset():
         close(res[k], ref[k].numpy(), RTOL, 1e-9, k)
 
 
+@pytest.mark.parametrize("chunk", [50, 1000, 262144])
+def test_render_train_tiny_and_odd_chunks(chunk):
+    """BatchNorm chunks of 50 samples (two 32-sample tiles, the second partial: a 2-workgroup grid), 1000 and one
+    chunk covering everything, against the CPU oracle -- the train kernels' grid, tail-tile and statistics paths.
+    Checked on the coarse pass and its running statistics: with 16 coarse samples the fine pass's resampling is
+    ill-conditioned (the fp32 oracle itself differs from a float64 run of it by up to 1.5e-3 on depth_fine here)."""
+    rays = syn.make_rays(24, seed=11)
+    emb, mc, mf = models(True)
+    kw = dict(sub_nerf_test_num=32, N_samples=16, N_importance=32, perturb=0, noise_std=0, chunk=chunk,
+              issegmentated=1, childnerf_ratio=0.25, use_child_nerf_divide=0, use_child_nerf_loss=1)
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays).to(DEV), **kw)
+    Pc, Pf = O.params_from_numpy(syn.init_nof_params(SEED_C)), O.params_from_numpy(syn.init_nof_params(SEED_F))
+    ref = O.render_rays_train(Pc, Pf, torch.from_numpy(rays), **kw)
+    for k in ("depth", "child_free_loss", "child_depth_loss"):
+        close(res[k], ref[k].numpy(), RTOL, 1e-9, k)
+    # the coarse network's running statistics after every chunk's update, in chunk order
+    want = np.stack([np.stack([Pc[b + ".running_mean"].numpy(), Pc[b + ".running_var"].numpy()]) for b in O.BN])
+    close(running(mc), want, RTOL, 1e-7, "running stats")
+
+
 def test_eval_query_is_per_sample():
     """Eval mode: a ray rendered alone equals the same ray rendered inside a large batch (bitwise)."""
     rays = torch.from_numpy(syn.make_rays(4096, seed=5)).to(DEV)
