@@ -177,7 +177,7 @@ def main():
     # dominant kernel: the MFMA kernel with the most time per step -- the 256 -> 256 pre-BN Linear of train mode
     # (k_train_ws<0,true>: 6 of 9 GEMMs per chunk), or the fused eval query
     knames = {0: "k_nof_eval", 1: "k_train_ws<0,true>", 2: "k_train_ws<8,false>",
-              3: "k_train_ws<8,true>", 10: "k_wgrad", 11: "k_dgrad"}
+              3: "k_train_ws<8,true>", 10: "k_wgrad", 11: "k_dgrad_ws"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
     ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)

@@ -54,8 +54,7 @@ traffic_path = os.path.join(dst, "pmc_traffic.json")
 traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
 for k, e in summary.items():
     if "hbm_bytes_per_launch" in e:
-        name = k.replace("k_train_layer<false,true>", "k_train_layer<false,true>")
-        traffic[name] = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "avg_us": e["avg_us"], "profile": tag}
+        traffic[k] = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "avg_us": e["avg_us"], "profile": tag}
 with open(traffic_path, "w") as fh:
     json.dump(traffic, fh, indent=1)
 for k, e in list(summary.items())[:8]:
