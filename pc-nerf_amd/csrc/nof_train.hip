@@ -33,22 +33,23 @@ namespace pcn {
 #endif
 
 #ifndef PCN_CLOCK_STAMP
-#define PCN_CLOCK_STAMP 0  // diagnostic builds only: in-kernel clock of k_train_ws (see pcnerf_debug_clock)
+#define PCN_CLOCK_STAMP 0  // diagnostic builds only: phase stamps of 1 k_train_ws, 2 k_wgrad (pcnerf_debug_clock)
 #endif
 #if PCN_CLOCK_STAMP
 // per workgroup: s_memrealtime (100 MHz, global) at entry / loop begin / loop end / exit (after its atomics
 // completed), s_memtime (shader clock) at loop begin / end
 __device__ unsigned long long g_clk[4096][6];
 #define CLK_ENTRY unsigned long long clk_e = __builtin_amdgcn_s_memrealtime();
+#define CLK_ON(k) (PCN_CLOCK_STAMP == (k))
 #define CLK_BEGIN                                                   \
   unsigned long long clk_t0 = __builtin_amdgcn_s_memtime();         \
   unsigned long long clk_r0 = __builtin_amdgcn_s_memrealtime();
 #define CLK_END                                                     \
   unsigned long long clk_t1 = __builtin_amdgcn_s_memtime();         \
   unsigned long long clk_r1 = __builtin_amdgcn_s_memrealtime();
-#define CLK_EXIT                                                                  \
+#define CLK_EXIT(k)                                                               \
   __builtin_amdgcn_s_waitcnt(0);                                                  \
-  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                    \
+  if (CLK_ON(k) && threadIdx.x == 0 && blockIdx.x < 4096) {                       \
     unsigned long long* g = g_clk[blockIdx.x];                                    \
     g[0] = clk_e; g[1] = clk_r0; g[2] = clk_r1; g[3] = __builtin_amdgcn_s_memrealtime(); \
     g[4] = clk_t0; g[5] = clk_t1;                                                 \
@@ -57,7 +58,8 @@ __device__ unsigned long long g_clk[4096][6];
 #define CLK_ENTRY
 #define CLK_BEGIN
 #define CLK_END
-#define CLK_EXIT
+#define CLK_EXIT(k)
+#define CLK_ON(k) 0
 #endif
 
 constexpr int KG_E = 8, KG_H = 32;
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
     }
     atomicAdd(&stats[t], a);
   }
-  CLK_EXIT
+  CLK_EXIT(1)
 }
 
 // occ_out on BatchNorm 8 (applied on load) + sigmoid; one wave per 32-sample tile.
@@ -792,6 +794,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
   using Cfg = WgradCfg<MODE>;
   constexpr bool HX = Cfg::HX, EX = Cfg::EX;
   constexpr int GS = Cfg::GS, BUF = Cfg::BUF, C = Cfg::C;
+  CLK_ENTRY
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* mus = lds + 2 * BUF;
   const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31, wv = t >> 6;
@@ -862,6 +865,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
   int64_t tile = blockIdx.x;
   if (tile < ntiles) gload(tile);
   int bsel = 0;
+  CLK_BEGIN
   for (; tile < ntiles; tile += gridDim.x) {
     float* buf = lds + bsel * BUF;
     lstore(buf, tile);
@@ -887,6 +891,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
     }
     bsel ^= 1;
   }
+  CLK_END
   float* pb = part + (size_t)blockIdx.x * Cfg::PART;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -902,6 +907,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
   }
   dbacc += __shfl_xor(dbacc, 32, 64);
   if (h == 0) pb[(size_t)256 * C + 32 * wv + li] = dbacc;
+  CLK_EXIT(MODE == 0 ? 2 : -1)
 }
 
 // Sum the partials of row m (block m; thread = column + C * slice, SPLIT slices of the partial list so narrow
