@@ -83,6 +83,7 @@ __global__ void k_pack_eval_vectors(NofParamsDev P, float* __restrict__ out) {
 }
 
 // ---------------------------------------------------------------------------------- fused query kernel
+
 template <int KG, int NX>
 __device__ __forceinline__ void gemm_t(f32x16 (&acc)[8], const float (&x)[NX], const float* __restrict__ wp,
                                        int lane) {
@@ -144,11 +145,17 @@ __global__ __launch_bounds__(256) void k_nof_eval(const float* __restrict__ rays
     encode_half(p, h, e);
   }
 
+  // the 8 layers' biases in LDS (one 8 KiB copy per block): each layer's accumulator initialisation is then an
+  // LDS read instead of 32 global loads whose latency stalled the layer's first MFMA
+  __shared__ __attribute__((aligned(16))) float sbias[8 * 256];
+  for (int i = threadIdx.x; i < 8 * 256 / 4; i += blockDim.x)
+    reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
+  __syncthreads();
   f32x16 acc[8];
   float act[128];
 #pragma unroll 1
   for (int L = 0; L < 8; ++L) {
-    init_bias_t(acc, W + OFF_BIAS + 256 * L, h);
+    init_bias_t(acc, sbias + 256 * L, h);
     if (L == 0 || L == 4) gemm_t<KG_E>(acc, e, W + off_w(L, true), lane);
     if (L != 0) gemm_t<KG_H>(acc, act, W + off_w(L, false), lane);
 #pragma unroll
