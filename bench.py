@@ -197,7 +197,7 @@ def main():
     traffic = pmc_traffic(kname)
 
     cpu = cdref = None
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline belongs to the N=1 line only
         if a.cpu_rays is None:
             a.cpu_rays = 1024 if grad else 512 if view else 4096
         cpu, ext = cpu_baseline(a, syn)
