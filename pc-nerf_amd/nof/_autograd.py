@@ -20,6 +20,8 @@ from . import _ops
 class TrainPass(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, rays, z, noise, noise_std, eps, chunk, with_losses, sub_num, *params):
+        # a chunk larger than the pass is the same single BatchNorm chunk: size workspaces and store by the pass
+        chunk = max(1, min(int(chunk), z.numel()))
         # keep the chunks' layer outputs for the backward in the HBM left after its workspace (+ 4 GiB margin)
         L = _ops.H.lib()
         reserve = int(L.pcnerf_nof_backward_workspace_bytes(int(chunk))) + (4 << 30)
