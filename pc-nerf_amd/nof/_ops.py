@@ -97,6 +97,7 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None) ->
     p = torch.empty((R, S), dtype=torch.float32, device=z.device)
     st = _stream(z)
     if model.training:
+        chunk = max(1, min(int(chunk), R * S))   # a larger chunk is the same single BatchNorm chunk
         mom, eps = _bn_config(model)
         s, keep = _params(model)
         nbytes = L.pcnerf_nof_train_workspace_bytes(int(chunk))
