@@ -31,12 +31,6 @@ namespace pcn {
 #ifndef PCN_WS_XD
 #define PCN_WS_XD 4  // k_train_ws / k_dgrad_ws: LDS read ring depth in k-groups
 #endif
-#ifndef PCN_WS_FOLD
-#define PCN_WS_FOLD 0  // k_train_ws: previous BatchNorm folded into the resident weights (staging is a copy)
-#endif
-#ifndef PCN_WS_GLDS
-#define PCN_WS_GLDS 0  // k_train_ws (needs PCN_WS_FOLD): the copy as global_load_lds_dwordx4 (no VGPR round trip)
-#endif
 
 #ifndef PCN_CLOCK_STAMP
 #define PCN_CLOCK_STAMP 0  // diagnostic builds only: phase stamps of 1 k_train_ws, 2 k_wgrad (pcnerf_debug_clock)
@@ -200,12 +194,9 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
                                                      double* __restrict__ stats) {
   constexpr int KGT = KE + (HP ? KG_H : 0);
   constexpr int XD = (KE && HP) ? PCN_WS_XD_SKIP : WS_XD;   // the skip layer's 160 weight registers leave less
-  constexpr bool FOLD = HP && PCN_WS_FOLD;
-  constexpr bool GLDS = FOLD && PCN_WS_GLDS;
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
-  __shared__ __attribute__((aligned(16))) float cs[FOLD ? 256 : 4];
   __shared__ f32x4 xs[2][KGT * 64];
   // per-lane running statistics (its sample's d and d^2 summed over the launch's tiles) for the wave's 16
   // neurons of its half: [wave][lane][8 float4 chunks], chunk 2j = sum d, 2j+1 = sum d^2 of registers 4j..4j+3,
@@ -235,35 +226,10 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
   // all weights resident before the tile loop: otherwise the waitcnt pass cannot tell them from the loop's own
   // loads and waits on the next tile's activations inside the k-loop
   __builtin_amdgcn_s_waitcnt(0);
-  if (FOLD) {
-    // W (alpha x + beta') = (W alpha) x + W beta': the resident weights of input feature f = 8g + 4h + q scaled by
-    // alpha_f once per launch, and c = W beta' per neuron (float64, this lane's half of the features + the other
-    // half's by one exchange) added to the accumulator in the epilogue
-    double c = 0.0;
-#pragma unroll
-    for (int kg = KE; kg < KGT; ++kg) {
-      const int g = kg - KE;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        c += (double)wr[kg][q] * (double)b[q];
-        wr[kg][q] *= a[q];
-      }
-      asm volatile("" : "+v"(wr[kg]));   // the scaled weights materialised (not rematerialised from W and alpha)
-      __builtin_amdgcn_sched_barrier(0);   // one k-group's coefficients live at a time
-    }
-    c += __shfl_xor(c, 32, 64);
-    if (h == 0) cs[32 * blk + li] = (float)c;
-  }
   int buf = 0;
   // staging: thread t owns the activation float4s t + 512 m (m = 0..3) of a tile: group KE + (t >> 6) + 8 m,
   // lane t & 63; and (KE) the encoding float4 of group t >> 6, lane t & 63
   auto stage = [&](int b, const f32x4 (&v)[4], int m) {
-    if (FOLD) {
-      xs[b][KE * 64 + t + 512 * m] = v[m];
-      return;
-    }
     const int g = (t >> 6) + 8 * m;
     const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
     const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
@@ -303,18 +269,11 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
   auto epi = [&](const f32x16& pacc, int ptile, int j) {
     const bool valid = (int64_t)ptile * 32 + li < n;
     const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
-    f32x4 cj{};
-    if (FOLD) {   // read per epilogue (an opaque zero offset keeps the loop-invariant read from being hoisted
-                  // into 16 launch-long registers)
-      int z0;
-      asm volatile("s_mov_b32 %0, 0" : "=s"(z0));
-      cj = *reinterpret_cast<const f32x4*>(cs + z0 + 32 * blk + 8 * j + 4 * h);
-    }
     f32x4 s1 = my_st[(2 * j) ^ st_sw], s2 = my_st[(2 * j + 1) ^ st_sw];
     f32x4 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float d = FOLD ? pacc[4 * j + q] + cj[q] : pacc[4 * j + q];
+      const float d = pacc[4 * j + q];
       o[q] = d + bj[q];
       const float dv = valid ? d : 0.0f;
       s1[q] += dv;
@@ -357,24 +316,16 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
         epi(pacc, ptile, 2);
         epi(pacc, ptile, 3);
       }
-      if (GLDS && kg == 3 && more) {   // lane-linear 1 KiB per wave-instruction, straight into LDS
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-          __builtin_amdgcn_global_load_lds(
-              (const __attribute__((address_space(1))) void*)(reinterpret_cast<const f32x4*>(
-                  hin + (size_t)nxt * TILE_FLOATS + (size_t)m * 2048) + t),
-              (__attribute__((address_space(3))) void*)(&xs[buf ^ 1][KE * 64 + (t & ~63) + 512 * m]), 16, 0, 0);
-      }
-      if (!GLDS && HP && kg == 3 && more) {
+      if (HP && kg == 3 && more) {
 #pragma unroll
         for (int m = 0; m < 4; ++m)
           v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)nxt * TILE_FLOATS + (size_t)m * 2048)[t];
       }
-      if (!GLDS && HP && kg == KGT - 10 && more) {
+      if (HP && kg == KGT - 10 && more) {
         stage(buf ^ 1, v, 0);
         stage(buf ^ 1, v, 1);
       }
-      if (!GLDS && HP && kg == KGT - 9 && more) {
+      if (HP && kg == KGT - 9 && more) {
         stage(buf ^ 1, v, 2);
         stage(buf ^ 1, v, 3);
       }
@@ -392,7 +343,6 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (GLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA'd tile lands before the barrier
     __syncthreads();
     buf ^= 1;
   };
