@@ -783,6 +783,9 @@ struct WgradCfg {
   static constexpr int BUF = GS + (HX ? GS : 0) + (EX ? 32 * ES_ROW : 0);
   static constexpr size_t LDS_BYTES = (size_t)(2 * BUF + 256) * sizeof(float);
   static constexpr size_t PART = (size_t)256 * C + 256;
+  // k_wgrad_reduce: SPLIT slices of the partial list per column, RT threads per block
+  static constexpr int SPLIT = C >= 1024 ? 1 : 1024 / C;
+  static constexpr int RT = C * SPLIT;
 };
 
 template <int MODE>
@@ -910,16 +913,16 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
   CLK_EXIT(MODE == 0 ? 2 : -1)
 }
 
-// Sum the partials of row m (block m; thread = column + C * slice, SPLIT slices of the partial list so narrow
-// layers still put 256 threads on the latency-bound sum), accumulate dW/db in float64 and the statistics of the
-// BatchNorm below: s12[n] = (sum_m W[m][n] db[m], sum_m W[m][n] G[m][n]).
+// Sum the partials of row m (block m; thread = column + C * slice, SPLIT slices of the partial list so every
+// layer puts ~1024 threads, 8 loads each in flight, on the latency-bound sum), accumulate dW/db in float64 and the
+// statistics of the BatchNorm below: s12[n] = (sum_m W[m][n] db[m], sum_m W[m][n] G[m][n]).
 template <int MODE>
-__global__ void k_wgrad_reduce(const float* __restrict__ part, int nblk, const float* __restrict__ W,
+__global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__ part, int nblk, const float* __restrict__ W,
                                const float* __restrict__ coefp, double* __restrict__ dW, double* __restrict__ db,
                                double* __restrict__ s12) {
   using Cfg = WgradCfg<MODE>;
   constexpr int C = Cfg::C;
-  constexpr int SPLIT = C >= 256 ? 1 : 256 / C;
+  constexpr int SPLIT = Cfg::SPLIT;
   constexpr int in_f = MODE == 0 ? 256 : MODE == 1 ? 63 : 319;
   constexpr int wcol_h = MODE == 2 ? 63 : 0, col_h = Cfg::EX ? 64 : 0;
   __shared__ double red[C * SPLIT];
@@ -929,7 +932,8 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int nblk, const f
   red[tt] = d;
   __syncthreads();
   double dbm = 0.0;
-  for (int i = 0; i < C * SPLIT; ++i) dbm += red[i];
+  const int nred = nblk < C * SPLIT ? nblk : C * SPLIT;   // only the first nblk threads summed anything
+  for (int i = 0; i < nred; ++i) dbm += red[i];
   __syncthreads();
   // 8 independent loads in flight per thread (the sum is latency-bound otherwise)
   double Gp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -1159,8 +1163,8 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   for (int L = 0; L < 8; ++L) oh[L] = take(tiles * TILE_FLOATS * 4);
   for (int i = 0; i < 2; ++i) og[i] = take(tiles * TILE_FLOATS * 4);
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
-  const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4), os = take(512 * 8);
-  const size_t oo = take(257 * 8), oa = take((size_t)gacc_layout().total * 8);
+  const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
+  const size_t os = take((8 * 512 + 257) * 8), oa = take((size_t)gacc_layout().total * 8);
   char* b = (char*)base;
   BwdWs w;
   for (int L = 0; L < 8; ++L) w.h[L] = (float*)(b + oh[L]);
@@ -1171,7 +1175,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.coef = (float*)(b + oc);
   w.part = (float*)(b + op);
   w.s12 = (double*)(b + os);
-  w.ostat = (double*)(b + oo);
+  w.ostat = w.s12 + 8 * 512;   // s12 per layer [8][512], then the output layer's statistics: one memset per chunk
   w.gacc = (double*)(b + oa);
   w.bytes = off;
   return w;
@@ -1250,7 +1254,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
       hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
       // 2. occ_out + BatchNorm 8
-      PCN_HIP(hipMemsetAsync(ws.ostat, 0, 257 * sizeof(double), s));
+      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * 512 + 257) * sizeof(double), s));
       hipLaunchKernelGGL(k_out_bwd_stats, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, ws.ostat);
       hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
@@ -1271,18 +1275,17 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       }
       {
         ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<0>::PART * 4.0);
-        PCN_HIP(hipMemsetAsync(ws.s12, 0, 512 * sizeof(double), s));
         if (L == 4)
-          hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::C), 0, s, ws.part, (int)wblocks,
-                             P.lin_w[4], coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12);
+          hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::RT), 0, s, ws.part, (int)wblocks,
+                             P.lin_w[4], coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + 512 * L);
         else
-          hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::C), 0, s, ws.part, (int)wblocks,
-                             P.lin_w[L], coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12);
+          hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::RT), 0, s, ws.part, (int)wblocks,
+                             P.lin_w[L], coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12 + 512 * L);
       }
       {
         ProfScope ps(s, PT_BWD_DGRAD, 2.0 * 256 * 256 * dn, 3072.0 * dn);
         hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
-                           hh[L - 1], n, ws.s12, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1],
+                           hh[L - 1], n, ws.s12 + 512 * L, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1],
                            ws.g[cur ^ 1]);
       }
       cur ^= 1;
@@ -1294,7 +1297,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     }
     {
       ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<1>::PART * 4.0);
-      hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(256), 0, s, ws.part, (int)wblocks,
+      hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)wblocks,
                          P.lin_w[0], (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr);
     }
   }

@@ -48,7 +48,7 @@ def main():
     s, keep = _ops._params(m)
     p = torch.empty_like(z)
     Ls = {os.path.basename(l)[10:-3]: load(l) for l in libs}
-    ws = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_train_workspace_bytes(chunk), dtype=torch.uint8, device=dev)
+    ws = torch.empty(max(L.pcnerf_nof_train_workspace_bytes(chunk) for L in Ls.values()), dtype=torch.uint8, device=dev)
     packed = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_eval_packed_floats(), device=dev)
     st = torch.cuda.current_stream().cuda_stream
     res = {k: {t: [] for t in TAGS} for k in Ls}
@@ -57,7 +57,7 @@ def main():
     if bwd:   # backward on a quarter of the rays (its workspace holds all 8 layers of a chunk)
         rays_b, z_b = rays[: rays_n // 4].contiguous(), z[: rays_n // 4].contiguous()
         g_logit = torch.randn(z_b.shape, generator=torch.Generator().manual_seed(3)).to(dev) * 1e-3
-        wsb = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_backward_workspace_bytes(chunk), dtype=torch.uint8,
+        wsb = torch.empty(max(L.pcnerf_nof_backward_workspace_bytes(chunk) for L in Ls.values()), dtype=torch.uint8,
                           device=dev)
     for rnd in range(4):
         for name, L in Ls.items():
