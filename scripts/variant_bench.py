@@ -52,6 +52,7 @@ def main():
     packed = torch.empty(Ls[next(iter(Ls))].pcnerf_nof_eval_packed_floats(), device=dev)
     st = torch.cuda.current_stream().cuda_stream
     res = {k: {t: [] for t in TAGS} for k in Ls}
+    qt = {}
     outs, gouts = {}, {}
     bwd = os.environ.get("VB_BWD", "1") == "1"
     if bwd:   # backward on a quarter of the rays (its workspace holds all 8 layers of a chunk)
@@ -62,9 +63,12 @@ def main():
     for rnd in range(4):
         for name, L in Ls.items():
             L.pcnerf_prof_enable(1)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             rc = L.pcnerf_nof_query_train(rays.data_ptr(), rays_n, 15, z.data_ptr(), S, chunk, ctypes.byref(s),
                                           0.0, 1e-5, ws.data_ptr(), ws.numel(), p.data_ptr(), st)
             assert rc == 0, L.pcnerf_last_error()
+            e1.record()
             if rnd == 0:
                 outs[name] = p.clone()   # train-mode query output of this variant (checked against 'base')
             if bwd:
@@ -82,6 +86,7 @@ def main():
             torch.cuda.synchronize()
             if rnd == 0:
                 continue  # warm-up round
+            qt.setdefault(name, []).append(e0.elapsed_time(e1) * 1e3)   # whole train query (us)
             for t in TAGS:
                 tm, n, f = read(L, t)
                 if n:
@@ -101,6 +106,8 @@ def main():
     for name in Ls:
         out[name] = {TAGS[t]: {"us": round(sorted(v)[len(v) // 2][0], 1), "TF": round(sorted(v)[len(v) // 2][1], 1)}
                      for t, v in res[name].items() if v}
+        if name in qt:
+            out[name]["query_train_us"] = round(sorted(qt[name])[len(qt[name]) // 2], 1)
     ref = outs.get("base")
     if ref is not None:
         for name in Ls:
