@@ -31,6 +31,9 @@ namespace pcn {
 #ifndef PCN_WS_XD
 #define PCN_WS_XD 4  // k_train_ws / k_dgrad_ws: LDS read ring depth in k-groups
 #endif
+#ifndef PCN_S12_COPIES
+#define PCN_S12_COPIES 8  // k_wgrad_reduce: copies of the BatchNorm-backward sums (block m adds to copy m % COPIES)
+#endif
 
 #ifndef PCN_CLOCK_STAMP
 #define PCN_CLOCK_STAMP 0  // diagnostic builds only: phase stamps of 1 k_train_ws, 2 k_wgrad (pcnerf_debug_clock)
@@ -959,8 +962,9 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__
     const size_t wi = (size_t)m * in_f + wcol_h + nn;
     dW[wi] += (double)coefp[512 + nn] * G + (double)coefp[768 + nn] * dbm;
     const double w = (double)W[wi];
-    atomicAdd(&s12[2 * nn], w * dbm);
-    atomicAdd(&s12[2 * nn + 1], w * G);
+    double* s12c = s12 + (m % PCN_S12_COPIES) * 512;   // 256 / COPIES blocks per address instead of 256
+    atomicAdd(&s12c[2 * nn], w * dbm);
+    atomicAdd(&s12c[2 * nn + 1], w * G);
   }
   if (t == 0) db[m] += dbm;
 }
@@ -985,7 +989,12 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_ws(
   const int t = threadIdx.x;
   if (t < 256) {
     const int k = t;
-    const double S1 = s12[2 * k], dotp = s12[2 * k + 1];
+    double S1 = 0.0, dotp = 0.0;
+#pragma unroll
+    for (int c = 0; c < PCN_S12_COPIES; ++c) {
+      S1 += s12[512 * c + 2 * k];
+      dotp += s12[512 * c + 2 * k + 1];
+    }
     const float invstd = coefp[256 + k];
     cgm[k] = (float)(S1 / (double)n);
     ckk[k] = (((float)dotp * invstd) * invstd) / (float)n;
@@ -1137,6 +1146,8 @@ static GaccLayout gacc_layout() {
   return G;
 }
 
+constexpr int S12_LAYER = PCN_S12_COPIES * 512;
+
 struct BwdWs {
   float* h[8];
   float* g[2];
@@ -1164,7 +1175,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   for (int i = 0; i < 2; ++i) og[i] = take(tiles * TILE_FLOATS * 4);
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
-  const size_t os = take((8 * 512 + 257) * 8), oa = take((size_t)gacc_layout().total * 8);
+  const size_t os = take((8 * S12_LAYER + 257) * 8), oa = take((size_t)gacc_layout().total * 8);
   char* b = (char*)base;
   BwdWs w;
   for (int L = 0; L < 8; ++L) w.h[L] = (float*)(b + oh[L]);
@@ -1175,7 +1186,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.coef = (float*)(b + oc);
   w.part = (float*)(b + op);
   w.s12 = (double*)(b + os);
-  w.ostat = w.s12 + 8 * 512;   // s12 per layer [8][512], then the output layer's statistics: one memset per chunk
+  w.ostat = w.s12 + 8 * S12_LAYER;   // s12 per layer [8][COPIES][512], then the output layer's statistics
   w.gacc = (double*)(b + oa);
   w.bytes = off;
   return w;
@@ -1254,7 +1265,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
       hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
       // 2. occ_out + BatchNorm 8
-      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * 512 + 257) * sizeof(double), s));
+      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + 257) * sizeof(double), s));   // one memset per chunk
       hipLaunchKernelGGL(k_out_bwd_stats, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, ws.ostat);
       hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
@@ -1277,15 +1288,15 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
         ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<0>::PART * 4.0);
         if (L == 4)
           hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::RT), 0, s, ws.part, (int)wblocks,
-                             P.lin_w[4], coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + 512 * L);
+                             P.lin_w[4], coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + S12_LAYER * L);
         else
           hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::RT), 0, s, ws.part, (int)wblocks,
-                             P.lin_w[L], coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12 + 512 * L);
+                             P.lin_w[L], coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12 + S12_LAYER * L);
       }
       {
         ProfScope ps(s, PT_BWD_DGRAD, 2.0 * 256 * 256 * dn, 3072.0 * dn);
         hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
-                           hh[L - 1], n, ws.s12 + 512 * L, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1],
+                           hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1],
                            ws.g[cur ^ 1]);
       }
       cur ^= 1;
