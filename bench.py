@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=None,
                     help="bounded CPU-baseline sample (rays; default 4096, 1024 for train_step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fold", action="store_true",
+                    help="val/view only: the opt-in exact affine fold of the eval network (SURVEY fact 1), reported "
+                         "as its own line, never the headline")
     ap.add_argument("--gather", action="store_true",
                     help="gather every rank's depth_fine to rank 0 inside each step (eval-driver output path)")
     return ap.parse_args()
@@ -89,7 +92,7 @@ def main():
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from nof import _hip, synthetic as syn
+    from nof import _hip, _ops, synthetic as syn
     from nof.blocks import blocks_of_rank, gather_rows, max_over_ranks
     from nof.criteria import nof_loss
     from nof.networks import Embedding, NOF_coarse, NOF_fine
@@ -109,6 +112,10 @@ def main():
         rays = torch.from_numpy(syn.make_rays(a.rays, n_children=32, seed=1000 * block)).to(dev)
     train = a.mode in ("train_fwd", "train_step")
     grad = a.mode == "train_step"
+    if a.fold:
+        if train:
+            raise SystemExit("--fold applies to the eval modes (val, view) only")
+        _ops.set_eval_fold(True)
     mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234 + block)).to(dev).train(train)
     mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678 + block)).to(dev).train(train)
     emb = Embedding(3, 10)
@@ -177,14 +184,14 @@ def main():
     # dominant kernel: the MFMA kernel with the most time per step -- the 256 -> 256 pre-BN Linear of train mode
     # (k_train_ws<0,true>: 6 of 9 GEMMs per chunk), or the fused eval query
     knames = {0: "k_nof_eval", 1: "k_train_ws<0,true>", 2: "k_train_ws<8,false>",
-              3: "k_train_ws<8,true>", 10: "k_wgrad", 11: "k_dgrad_ws"}
+              3: "k_train_ws<8,true>", 10: "k_wgrad", 11: "k_dgrad_ws", 13: "k_nof_eval_fold"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
     ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)
     kernels = {}
     for t, nm in ((0, "eval_query"), (1, "train_hidden"), (2, "train_first"), (3, "train_skip"), (4, "train_out"),
                   (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
-                  (10, "wgrad"), (11, "dgrad"), (12, "bwd_other")):
+                  (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold")):
         tm, n, f, b = prof_read(L, t)
         if n:
             kernels[nm] = {"ms_per_step": round(tm, 3), "launches_per_step": n,
@@ -195,6 +202,16 @@ def main():
     avg_s = ktime_ms * 1e-3 / max(klaunch, 1)
     achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
     traffic = pmc_traffic(kname)
+    if a.fold:   # no MLP left: the query moves 8 B per sample (+ ray rows) and is bound by its sincos (VALU)
+        roof = {"kernel": kname, "bound": "hbm", "achieved": round(kbytes / max(klaunch, 1) / avg_s / 1e9, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(kbytes / max(klaunch, 1) / avg_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": kbytes / max(klaunch, 1),
+                "note": "VALU-bound (60 sincosf per sample); HBM fraction reported as the contract asks"}
+    else:
+        roof = {"kernel": kname, "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1)}
 
     cpu = cdref = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline belongs to the N=1 line only
@@ -228,17 +245,15 @@ def main():
                                 "train_step": "render_rays_train fwd + losses + backward + Adam step",
                                 "val": "render_rays_val fwd",
                                 "view": "render_rays_view_0525_2_2 two-step inference (method 2) + effective points"
-                                }[a.mode],
+                                }[a.mode] + (" -- exact affine fold of the eval network (opt-in)" if a.fold else ""),
                    "rays_per_gpu": a.rays, "N_samples": a.samples, "N_importance": a.importance,
                    "rows_per_gpu": int(rays.shape[0]),
                    "mlp_samples_per_ray": a.samples + a.samples + a.importance, "chunk": a.chunk,
                    "batchnorm": "train (batch stats per chunk)" if train else "eval (folded)",
+                   "network": "affine fold (sigmoid(a.e + c))" if a.fold else "9 Linear layers as written",
                    "segmented_ratio": 0.1 if train else None, "perturb": 1 if train else 0,
                    "parallelism": f"blocks{world}", "gather": bool(a.gather)},
-        "roofline": {"kernel": kname, "bound": "mfma", "achieved": round(achieved, 2),
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                     "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 2),
-                     "algorithmic_flop_per_launch": kflops / max(klaunch, 1)},
+        "roofline": roof,
         "cpu_baseline": cpu,
         "cd_vs_ref": cdref,
         "loss": loss_val,

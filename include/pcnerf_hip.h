@@ -59,6 +59,19 @@ int pcnerf_nof_query_eval(const float* rays, int64_t n_rays, int ray_stride, con
 /* NOF.forward on an already embedded batch: p_out[i] = NOF(emb[i, 0:63]) (eval mode, packed image). */
 int pcnerf_nof_forward_eval(const float* emb, int64_t n, const float* packed, float* p_out, void* stream);
 
+/* Exact affine fold of the eval network (opt-in fast path): LeakyReLU(True) is the identity
+ * (models.py:72,152,232) and eval BatchNorm is affine, so NOF(e) = sigmoid(a . e + c).  Writes fold[0..62] = a,
+ * fold[63] = c (64 doubles), composed in float64 from the module's parameters (models.py:44-123, :183-203). */
+int pcnerf_nof_fold_eval(const pcnerf_nof_params* params, double* fold, void* stream);
+
+/* pcnerf_nof_query_eval through the fold: p_out[g] = sigmoid(fl32(a . Embedding(o + d*z[g]) + c)).  Replaces the
+ * same eval chunk loop (render.py:18-25); rounding differs from the layer-by-layer network (~1e-7 rel logit). */
+int pcnerf_nof_query_eval_fold(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
+                               const double* fold, float* p_out, void* stream);
+
+/* pcnerf_nof_forward_eval through the fold: p_out[i] = sigmoid(fl32(a . emb[i, 0:63] + c)). */
+int pcnerf_nof_forward_eval_fold(const float* emb, int64_t n, const double* fold, float* p_out, void* stream);
+
 /* Embedding(3, 10).forward (models.py:27-41): out[i, 0:63] = [x, sin(2^k x), cos(2^k x)]_k for x = pts[i, 0:3]. */
 int pcnerf_embed(const float* pts, int64_t n, float* out, void* stream);
 

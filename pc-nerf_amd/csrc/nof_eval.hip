@@ -191,9 +191,131 @@ __global__ void k_embed(const float* __restrict__ pts, int64_t n, float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------- exact affine fold
+// Optional eval fast path: every LeakyReLU(True) of NOF is the identity (negative_slope = True
+// = 1.0, models.py:72,152,232) and eval-mode BatchNorm is affine per feature, so the whole eval network is
+// sigmoid(a . e + c) with a in R^63 (models.py:44-123, 183-203).  k_fold_eval composes it backwards from occ_out
+// in float64: with v the coefficients of h_L, h_L = alpha (W_L x + b_L) + beta gives c += v.(alpha b_L + beta),
+// v <- (v alpha) W_L (the skip layer 4 splits into its encoding and h_3 columns).  fold[0..62] = a, fold[63] = c.
+// The per-sample query is then the encoding, 63 float64 FMAs and the sigmoid (no MLP).  Rounding differs from
+// the layer-by-layer fp32 network (folded vs unfolded: ~1e-7 relative logit), so this path is
+// opt-in and reported separately.
+__device__ __forceinline__ double block_sum_256(double x, double* red) {   // 256 threads, fixed order
+  x = wave_sum_d(x);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = x;
+  __syncthreads();
+  return ((red[0] + red[1]) + (red[2] + red[3]));
+}
+
+__global__ __launch_bounds__(256) void k_fold_eval(NofParamsDev P, double* __restrict__ fold) {
+  __shared__ double va[256];
+  __shared__ double red[4];
+  const int t = threadIdx.x;
+  double v = (double)P.out_w[t];
+  double ae = 0.0;   // thread t < 63: coefficient of encoding feature t
+  double c = (double)P.out_b[0];
+  for (int L = 7; L >= 0; --L) {
+    const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
+    const double alpha = (double)P.bn_w[L][t] / sqrt((double)P.bn_rv[L][t] + (double)P.eps);
+    const double beta = (double)P.bn_b[L][t] - (double)P.bn_rm[L][t] * alpha;
+    c += block_sum_256(v * (alpha * (double)P.lin_b[L][t] + beta), red);
+    va[t] = v * alpha;
+    __syncthreads();
+    const float* __restrict__ W = P.lin_w[L];
+    if ((L == 0 || L == 4) && t < 63) {
+      double a = 0.0;
+      for (int n = 0; n < 256; ++n) a += va[n] * (double)W[(size_t)n * in_f + t];
+      ae += a;
+    }
+    if (L != 0) {
+      const int off = L == 4 ? 63 : 0;
+      double a = 0.0;
+      for (int n = 0; n < 256; ++n) a += va[n] * (double)W[(size_t)n * in_f + off + t];
+      v = a;
+    }
+    __syncthreads();
+  }
+  if (t < 63) fold[t] = ae;
+  if (t == 63) fold[63] = c;
+}
+
+// one thread per sample: p = sigmoid(fl32(a . e + c)); ein != NULL reads the (total, 63) embedding instead
+__global__ __launch_bounds__(256) void k_nof_eval_fold(const float* __restrict__ rays, int stride,
+                                                       const float* __restrict__ z, int64_t total, int S,
+                                                       const float* __restrict__ ein, const double* __restrict__ fold,
+                                                       float* __restrict__ p_out) {
+  __shared__ double a[64];
+  if (threadIdx.x < 64) a[threadIdx.x] = fold[threadIdx.x];
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  double acc = a[63];
+  if (ein) {
+    const float* e = ein + g * 63;
+#pragma unroll
+    for (int f = 0; f < 63; ++f) acc += a[f] * (double)e[f];
+  } else {
+    float p[3], e0[32], e1[32];
+    sample_point(rays + (g / S) * stride, z[g], p);
+    encode_half(p, 0, e0);   // features 2t
+    encode_half(p, 1, e1);   // features 2t + 1
+#pragma unroll
+    for (int t = 0; t < 32; ++t) {
+      acc += a[2 * t] * (double)e0[t];
+      if (2 * t + 1 < 63) acc += a[2 * t + 1] * (double)e1[t];
+    }
+  }
+  p_out[g] = sigmoid_ref((float)acc);
+}
+
 }  // namespace pcn
 
 using namespace pcn;
+
+extern "C" int pcnerf_nof_fold_eval(const pcnerf_nof_params* params, double* fold, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(params && fold, "pcnerf_nof_fold_eval: null argument");
+  NofParamsDev P;
+  PCN_CHECK(to_dev_params(params, 1e-5f, &P), "pcnerf_nof_fold_eval: null parameter pointer");
+  hipLaunchKernelGGL(k_fold_eval, dim3(1), dim3(256), 0, (hipStream_t)stream, P, fold);
+  PCN_LAUNCH_CHECK("pcnerf_nof_fold_eval");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_query_eval_fold(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                          int n_samples, const double* fold, float* p_out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && fold && p_out, "pcnerf_nof_query_eval_fold: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_nof_query_eval_fold: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_eval_fold: ray_stride < 6");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  const int64_t blocks = (total + 255) / 256;
+  PCN_CHECK(blocks < (int64_t)1 << 31, "pcnerf_nof_query_eval_fold: too many samples for one launch");
+  {
+    // algorithmic work per sample: 63 FMA + the encoding; bytes: z in, p out, ray rows
+    ProfScope ps((hipStream_t)stream, PT_EVAL_FOLD, 126.0 * (double)total,
+                 8.0 * (double)total + 4.0 * ray_stride * (double)n_rays);
+    hipLaunchKernelGGL(k_nof_eval_fold, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rays,
+                       ray_stride, z, total, n_samples, (const float*)nullptr, fold, p_out);
+  }
+  PCN_LAUNCH_CHECK("pcnerf_nof_query_eval_fold");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_forward_eval_fold(const float* emb, int64_t n, const double* fold, float* p_out,
+                                            void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(emb && fold && p_out, "pcnerf_nof_forward_eval_fold: null argument");
+  PCN_CHECK(n > 0, "pcnerf_nof_forward_eval_fold: empty input");
+  const int64_t blocks = (n + 255) / 256;
+  PCN_CHECK(blocks < (int64_t)1 << 31, "pcnerf_nof_forward_eval_fold: too many samples for one launch");
+  hipLaunchKernelGGL(k_nof_eval_fold, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)nullptr, 0, (const float*)nullptr, n, 1, emb, fold, p_out);
+  PCN_LAUNCH_CHECK("pcnerf_nof_forward_eval_fold");
+  PCN_API_END
+}
 
 extern "C" int pcnerf_embed(const float* pts, int64_t n, float* out, void* stream) {
   PCN_API_BEGIN

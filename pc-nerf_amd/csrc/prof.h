@@ -18,6 +18,7 @@ enum ProfTag {
   PT_BWD_WGRAD = 10,   // k_wgrad: weight-gradient GEMM partials (sum over samples on MFMA)
   PT_BWD_DGRAD = 11,   // k_dgrad_ws: data-gradient GEMM + BatchNorm backward
   PT_BWD_MISC = 12,    // output-layer backward, partial reduction, BN statistics
+  PT_EVAL_FOLD = 13,   // k_nof_eval_fold: exact affine fold of the eval network (opt-in)
 };
 extern bool g_prof_on;
 class ProfScope {

@@ -72,6 +72,9 @@ _SIGS = {
     "pcnerf_prof_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "pcnerf_nof_forward_eval": (c_int, [vp, i64, vp, vp, vp]),
+    "pcnerf_nof_fold_eval": (c_int, [ctypes.POINTER(NofParams), vp, vp]),
+    "pcnerf_nof_query_eval_fold": (c_int, [vp, i64, c_int, vp, c_int, vp, vp, vp]),
+    "pcnerf_nof_forward_eval_fold": (c_int, [vp, i64, vp, vp, vp]),
     "pcnerf_nof_forward_train": (c_int, [vp, i64, ctypes.POINTER(NofParams), c_float, c_float, vp, c_size, vp, vp]),
     "pcnerf_nof_backward_workspace_bytes": (c_size, [i64]),
     "pcnerf_nof_query_train_backward": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams), c_float,

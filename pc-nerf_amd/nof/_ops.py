@@ -6,6 +6,7 @@ kernels on the current stream.  Nothing here computes on the host.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -83,6 +84,33 @@ def pack_eval(model, device) -> torch.Tensor:
     return out
 
 
+# Exact affine fold of the eval network (opt-in; SURVEY fact 1: every LeakyReLU(True) is the identity, so the
+# eval-mode NOF is sigmoid(a . emb + c)).  Off by default: the drop-in evaluates the module as written.
+_EVAL_FOLD = os.environ.get("PCNERF_EVAL_FOLD", "0") == "1"
+
+
+def set_eval_fold(enabled: bool) -> bool:
+    """Route eval-mode NOF queries through the exact affine fold (True) or the full network (False, default).
+    Returns the previous setting."""
+    global _EVAL_FOLD
+    prev, _EVAL_FOLD = _EVAL_FOLD, bool(enabled)
+    return prev
+
+
+def eval_fold_enabled() -> bool:
+    return _EVAL_FOLD
+
+
+def fold_eval(model, device) -> torch.Tensor:
+    """(a, c) of the eval network as 64 float64 (a = fold[:63], c = fold[63]); rebuilt per call."""
+    L = H.lib()
+    out = torch.empty(64, dtype=torch.float64, device=device)
+    s, keep = _params(model)
+    _bn_config(model)
+    H.check(L.pcnerf_nof_fold_eval(ctypes.byref(s), out.data_ptr(), _stream(out)))
+    return out
+
+
 def _track_batches(model, n_chunks: int) -> None:
     for bn in model.norms():
         if bn.num_batches_tracked is not None:
@@ -110,6 +138,10 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None) ->
             H.check(L.pcnerf_nof_query_train(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
                                              ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(), p.data_ptr(), st))
         _track_batches(model, -(-R * S // int(chunk)))
+    elif _EVAL_FOLD:
+        fold = fold_eval(model, z.device)
+        H.check(L.pcnerf_nof_query_eval_fold(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, fold.data_ptr(),
+                                             p.data_ptr(), st))
     else:
         packed = pack_eval(model, z.device)
         H.check(L.pcnerf_nof_query_eval(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, packed.data_ptr(),
@@ -135,6 +167,9 @@ def nof_forward_embedded(model, x: torch.Tensor) -> torch.Tensor:
         H.check(L.pcnerf_nof_forward_train(x.data_ptr(), B, ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(),
                                            out.data_ptr(), st))
         _track_batches(model, 1)
+    elif _EVAL_FOLD:
+        fold = fold_eval(model, x.device)
+        H.check(L.pcnerf_nof_forward_eval_fold(x.data_ptr(), B, fold.data_ptr(), out.data_ptr(), st))
     else:
         packed = pack_eval(model, x.device)
         H.check(L.pcnerf_nof_forward_eval(x.data_ptr(), B, packed.data_ptr(), out.data_ptr(), st))
