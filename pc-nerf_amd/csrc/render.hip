@@ -382,6 +382,37 @@ __global__ __launch_bounds__(256) void k_resample(const float* __restrict__ Z, c
   for (int i = lane; i < S; i += 64) sb[i] = zs[i];
   for (int i = S + I + lane; i < P2; i += 64) sb[i] = __builtin_inff();
   __syncthreads();
+  // sort(cat(z, z_samples)) (render.py:463-467): both lists are (almost always) non-decreasing already, so the
+  // merged position of a coarse value is its index plus the fine values strictly below it, of a fine value its
+  // index plus the coarse values <= it (binary searches in LDS).  Any unsorted list in the block sends the whole
+  // block through the bitonic sort below (its barriers need every wave); the sorted values are the same.
+  bool mono = true;
+  for (int i = lane; i + 1 < S; i += 64) mono = mono && !(sb[i] > sb[i + 1]);
+  for (int i = lane; i + 1 < I; i += 64) mono = mono && !(sb[S + i] > sb[S + i + 1]);
+  if (!__syncthreads_or(mono ? 0 : 1)) {
+    if (active) {
+      float* out = ZF + ray * (S + I);
+      for (int i = lane; i < S; i += 64) {
+        const float v = sb[i];
+        int lo = 0, hi = I;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sb[S + mid] < v) lo = mid + 1; else hi = mid;
+        }
+        out[i + lo] = v;
+      }
+      for (int i = lane; i < I; i += 64) {
+        const float v = sb[S + i];
+        int lo = 0, hi = S;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sb[mid] <= v) lo = mid + 1; else hi = mid;
+        }
+        out[i + lo] = v;
+      }
+    }
+    return;
+  }
   // bitonic sort of P2 values (ascending); every wave of the block runs the same trip counts
   for (int k = 2; k <= P2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {

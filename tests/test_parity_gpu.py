@@ -210,6 +210,43 @@ def test_view_walk_fallback_matches_parallel():
     assert flags[:, 0].nonzero().flatten().tolist() == [2, 3, 6, 8, 9, 10, 11]
 
 
+@pytest.mark.parametrize("ratio", [0.1, 0.5])
+def test_segmented_coarse_z_bitexact(ratio):
+    """k_sample_coarse (render.py:429-442) against the oracle's sort of the two linspaces, bit for bit: the
+    binary-search merge (both lists non-decreasing) and, with every other ray's child interval reversed
+    (child_near > child_far: a decreasing list), the all-pairs rank fallback."""
+    from nof import _ops
+    rays = torch.from_numpy(syn.make_rays(512, seed=21))
+    rev = rays.clone()
+    rev[::2, 10], rev[::2, 11] = rays[::2, 11], rays[::2, 10]
+    for S in (64, 128, 200):
+        sp = int(S * (1 - ratio))
+        for r in (rays, rev):
+            got = _ops.sample_coarse(r.to(DEV), S, sp, 6, 7, 10, 11).cpu()
+            want = O.coarse_z(r, S, True, ratio)
+            assert torch.equal(got, want), (S, ratio)
+
+
+def test_resample_merge_exact():
+    """k_resample's sort(cat(z, z_samples)) (render.py:463-467): bit for bit the sort of the coarse z and the
+    fine samples the same pdf code draws (pcnerf_sample_pdf), for sorted coarse rows (binary-search merge) and with
+    every third row unsorted (the block falls back to the bitonic sort); and the fine samples against the oracle."""
+    from nof import _ops
+    gen = torch.Generator().manual_seed(7)
+    R, S, I = 256, 128, 256
+    z = torch.sort(torch.rand(R, S, generator=gen) * 30, -1)[0]
+    w = torch.rand(R, S, generator=gen)
+    u = torch.sort(torch.rand(R, I, generator=gen), -1)[0]
+    zr = z.clone()
+    zr[::3, 40], zr[::3, 41] = z[::3, 41], z[::3, 40]
+    for zz in (z, zr):
+        got = _ops.resample(zz.to(DEV), w.to(DEV), I, u.to(DEV)).cpu()
+        mid = 0.5 * (zz[:, 1:] + zz[:, :-1])
+        fine = _ops.sample_pdf_standalone(mid.to(DEV), w[:, 1:-1].to(DEV), I, False, u.to(DEV)).cpu()
+        assert torch.equal(got, torch.sort(torch.cat([zz, fine], -1), -1)[0])
+        close(fine, O.sample_pdf(mid, w[:, 1:-1], I, False, u).numpy(), 1e-5, 1e-6, "fine samples")
+
+
 def test_render_train_vs_oracle_config2_subset():
     """Config-2 rays at S=128/I=256 with several BatchNorm chunks, against the CPU oracle."""
     rays = syn.make_rays(192, seed=3)
