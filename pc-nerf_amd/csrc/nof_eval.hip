@@ -257,15 +257,27 @@ __global__ __launch_bounds__(256) void k_nof_eval_fold(const float* __restrict__
 #pragma unroll
     for (int f = 0; f < 63; ++f) acc += a[f] * (double)e[f];
   } else {
-    float p[3], e0[32], e1[32];
+    // the Embedding's 63 features (encode_half's arithmetic, each sincosf once) straight into the dot product
+    float p[3];
     sample_point(rays + (g / S) * stride, z[g], p);
-    encode_half(p, 0, e0);   // features 2t
-    encode_half(p, 1, e1);   // features 2t + 1
+    double part[6];   // six independent chains (sin / cos per coordinate), summed at the end
 #pragma unroll
-    for (int t = 0; t < 32; ++t) {
-      acc += a[2 * t] * (double)e0[t];
-      if (2 * t + 1 < 63) acc += a[2 * t + 1] * (double)e1[t];
+    for (int m = 0; m < 3; ++m) {
+      part[m] = a[m] * (double)p[m];
+      part[3 + m] = 0.0;
     }
+#pragma unroll 2
+    for (int k = 0; k < 10; ++k) {   // partly rolled: the 63 coefficients stay in LDS, not in 126 registers
+      const float sc = (float)(1 << k);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        float sv, cv;
+        sincosf(sc * p[m], &sv, &cv);
+        part[m] += a[3 + 6 * k + m] * (double)sv;
+        part[3 + m] += a[6 + 6 * k + m] * (double)cv;
+      }
+    }
+    acc += ((part[0] + part[1]) + (part[2] + part[3])) + (part[4] + part[5]);
   }
   p_out[g] = sigmoid_ref((float)acc);
 }
