@@ -247,6 +247,23 @@ def test_resample_merge_exact():
         close(fine, O.sample_pdf(mid, w[:, 1:-1], I, False, u).numpy(), 1e-5, 1e-6, "fine samples")
 
 
+def test_empty_rays_raise_like_the_reference():
+    """Zero rays: the reference's chunk loop collects nothing and torch.cat([]) raises (render.py:18-25, 44-51);
+    the HIP path refuses the empty input with an exception too, never a silent empty result."""
+    emb, mc, mf = models(False)
+    rays = torch.zeros((0, 15), device=DEV)
+    with torch.no_grad(), pytest.raises((RuntimeError, ValueError)):
+        R.render_rays_val(mc, mf, emb, rays, N_samples=64, N_importance=128, perturb=0, noise_std=0, chunk=4096)
+    with pytest.raises((RuntimeError, ValueError)):
+        O.render_rays_val(O.params_from_numpy(syn.init_nof_params(SEED_C)),
+                          O.params_from_numpy(syn.init_nof_params(SEED_F)), rays.cpu(), N_samples=64,
+                          N_importance=128, perturb=0, noise_std=0, chunk=4096)
+    emb, mc, mf = models(True)
+    with torch.no_grad(), pytest.raises((RuntimeError, ValueError)):
+        R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=4, N_samples=64, N_importance=128, perturb=0,
+                            noise_std=0, chunk=4096, issegmentated=1, childnerf_ratio=0.1, use_child_nerf_loss=1)
+
+
 def test_render_train_vs_oracle_config2_subset():
     """Config-2 rays at S=128/I=256 with several BatchNorm chunks, against the CPU oracle."""
     rays = syn.make_rays(192, seed=3)
