@@ -200,45 +200,65 @@ __global__ void k_embed(const float* __restrict__ pts, int64_t n, float* __restr
 // The per-sample query is then the encoding, 63 float64 FMAs and the sigmoid (no MLP).  Rounding differs from
 // the layer-by-layer fp32 network (folded vs unfolded: ~1e-7 relative logit), so this path is
 // opt-in and reported separately.
-__device__ __forceinline__ double block_sum_256(double x, double* red) {   // 256 threads, fixed order
-  x = wave_sum_d(x);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[w] = x;
-  __syncthreads();
-  return ((red[0] + red[1]) + (red[2] + red[3]));
+// sum_{n < 64} va[n] * w[n * ld] in float64, the 64 loads issued in two batches of 32 before any use (one
+// workgroup runs the whole fold, so load latency, not bandwidth, sets its time)
+__device__ __forceinline__ double gemv_slice(const float* __restrict__ w, int ld, const double* __restrict__ va) {
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int b = 0; b < 64; b += 32) {
+    float x[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) x[j] = w[(size_t)(b + j) * ld];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) acc[j & 3] += va[b + j] * (double)x[j];
+  }
+  return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
-__global__ __launch_bounds__(256) void k_fold_eval(NofParamsDev P, double* __restrict__ fold) {
+__global__ __launch_bounds__(1024) void k_fold_eval(NofParamsDev P, double* __restrict__ fold) {
+  // thread (t, sl): output column t, input rows n in [64 sl, 64 sl + 64) of each GEMV (16 loads in flight),
+  // the four slices summed in a fixed order through LDS
   __shared__ double va[256];
   __shared__ double red[4];
-  const int t = threadIdx.x;
-  double v = (double)P.out_w[t];
-  double ae = 0.0;   // thread t < 63: coefficient of encoding feature t
+  __shared__ double ps[2][4][256];
+  const int tid = threadIdx.x, t = tid & 255, sl = tid >> 8;
+  double v = (double)P.out_w[t];   // meaningful in slice 0
+  double ae = 0.0;                 // slice 0, t < 63: coefficient of encoding feature t
   double c = (double)P.out_b[0];
   for (int L = 7; L >= 0; --L) {
     const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
-    const double alpha = (double)P.bn_w[L][t] / sqrt((double)P.bn_rv[L][t] + (double)P.eps);
-    const double beta = (double)P.bn_b[L][t] - (double)P.bn_rm[L][t] * alpha;
-    c += block_sum_256(v * (alpha * (double)P.lin_b[L][t] + beta), red);
-    va[t] = v * alpha;
+    double cb = 0.0;
+    if (sl == 0) {
+      const double alpha = (double)P.bn_w[L][t] / sqrt((double)P.bn_rv[L][t] + (double)P.eps);
+      const double beta = (double)P.bn_b[L][t] - (double)P.bn_rm[L][t] * alpha;
+      cb = v * (alpha * (double)P.lin_b[L][t] + beta);
+      va[t] = v * alpha;
+      const double w = wave_sum_d(cb);
+      if ((t & 63) == 0) red[t >> 6] = w;
+    }
     __syncthreads();
+    c += (red[0] + red[1]) + (red[2] + red[3]);
     const float* __restrict__ W = P.lin_w[L];
+    const int n0 = 64 * sl;
+    double ea = 0.0, ha = 0.0;
     if ((L == 0 || L == 4) && t < 63) {
-      double a = 0.0;
-      for (int n = 0; n < 256; ++n) a += va[n] * (double)W[(size_t)n * in_f + t];
-      ae += a;
+      ea = gemv_slice(W + (size_t)n0 * in_f + t, in_f, va + n0);
     }
     if (L != 0) {
       const int off = L == 4 ? 63 : 0;
-      double a = 0.0;
-      for (int n = 0; n < 256; ++n) a += va[n] * (double)W[(size_t)n * in_f + off + t];
-      v = a;
+      ha = gemv_slice(W + (size_t)n0 * in_f + off + t, in_f, va + n0);
+    }
+    ps[0][sl][t] = ea;
+    ps[1][sl][t] = ha;
+    __syncthreads();
+    if (sl == 0) {
+      ae += (ps[0][0][t] + ps[0][1][t]) + (ps[0][2][t] + ps[0][3][t]);
+      if (L != 0) v = (ps[1][0][t] + ps[1][1][t]) + (ps[1][2][t] + ps[1][3][t]);
     }
     __syncthreads();
   }
-  if (t < 63) fold[t] = ae;
-  if (t == 63) fold[63] = c;
+  if (sl == 0 && t < 63) fold[t] = ae;
+  if (sl == 0 && t == 63) fold[63] = c;
 }
 
 // one thread per sample: p = sigmoid(fl32(a . e + c)); ein != NULL reads the (total, 63) embedding instead
@@ -291,7 +311,7 @@ extern "C" int pcnerf_nof_fold_eval(const pcnerf_nof_params* params, double* fol
   PCN_CHECK(params && fold, "pcnerf_nof_fold_eval: null argument");
   NofParamsDev P;
   PCN_CHECK(to_dev_params(params, 1e-5f, &P), "pcnerf_nof_fold_eval: null parameter pointer");
-  hipLaunchKernelGGL(k_fold_eval, dim3(1), dim3(256), 0, (hipStream_t)stream, P, fold);
+  hipLaunchKernelGGL(k_fold_eval, dim3(1), dim3(1024), 0, (hipStream_t)stream, P, fold);
   PCN_LAUNCH_CHECK("pcnerf_nof_fold_eval");
   PCN_API_END
 }
