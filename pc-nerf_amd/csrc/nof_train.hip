@@ -194,7 +194,12 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
                                                      int64_t n, const float* __restrict__ Wp,
                                                      const float* __restrict__ bias, BnPrev prev, float momentum,
                                                      float eps, float* __restrict__ hout,
-                                                     double* __restrict__ stats) {
+                                                     double* __restrict__ stats,
+                                                     const f32x4* __restrict__ etin, f32x4* __restrict__ etout) {
+  // etout (first layer): every tile's encoding float4s, [tile][g 0..7][lane] (8 KiB per tile), as staged;
+  // etin (skip layer): the same tiles read back instead of recomputing the sincosf from the ray rows (every
+  // caller runs the first layer of the chunk before its skip layer with the same buffer)
+  constexpr bool ETIN = KE && HP, ETOUT = KE && !HP;
   constexpr int KGT = KE + (HP ? KG_H : 0);
   constexpr int XD = (KE && HP) ? PCN_WS_XD_SKIP : WS_XD;   // the skip layer's 160 weight registers leave less
   __shared__ __attribute__((aligned(16))) float al[256];
@@ -258,13 +263,18 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
     }
     if (KE) {
       const int64_t gs = sample_of(tl);
-      if (ein) {
-        xs[0][t] = enc_feats_row(ein + gs * 63, h, t >> 6);
+      f32x4 e;
+      if (ETIN) {
+        e = etin[(size_t)tl * 512 + t];
+      } else if (ein) {
+        e = enc_feats_row(ein + gs * 63, h, t >> 6);
       } else {
         float p[3];
         sample_point(rays + (gs / S) * stride, z[gs], p);
-        xs[0][t] = enc_feats(p, h, t >> 6);
+        e = enc_feats(p, h, t >> 6);
       }
+      xs[0][t] = e;
+      if (ETOUT) etout[(size_t)tl * 512 + t] = e;
     }
   }
   __syncthreads();
@@ -294,6 +304,7 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
     f32x4 xr[XD];
     f32x4 v[4];    // HP: the next tile's raw activations, k-groups 3 to KGT-9 only
     float rr[7];   // KE: the next tile's ray origin/direction and z for this lane's sample (last 8 k-groups)
+    f32x4 ev;      // ETIN: the next tile's stored encoding float4
 #pragma unroll
     for (int d = 0; d < XD - 1; ++d) xr[d] = xb[d * 64];
 #pragma unroll
@@ -304,7 +315,8 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
         const f32x16 c = (kg == 0 && q == 0) ? f32x16{} : acc;
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[kg][q], xr[kg % XD][q], c, 0, 0, 0);
       }
-      if (KE && kg == (HP ? KGT - 8 : 0) && more && !ein) {   // after the activations' registers are free
+      if (ETIN && kg == KGT - 8 && more) ev = etin[(size_t)nxt * 512 + t];
+      if (ETOUT && kg == 0 && more && !ein) {   // after the activations' registers are free
         const int64_t gs = sample_of(nxt);
         const float* r = rays + (gs / S) * stride;
 #pragma unroll
@@ -334,7 +346,9 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
       }
       if (KE && kg == KGT - 1 && more) {
         f32x4 e;
-        if (ein) {
+        if (ETIN) {
+          e = ev;
+        } else if (ein) {
           e = enc_feats_row(ein + sample_of(nxt) * 63, h, t >> 6);
         } else {   // sample_point on the prefetched ray row
           float p[3];
@@ -343,6 +357,7 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
           e = enc_feats(p, h, t >> 6);
         }
         xs[buf ^ 1][t] = e;
+        if (ETOUT) etout[(size_t)nxt * 512 + t] = e;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -418,6 +433,7 @@ __global__ __launch_bounds__(256) void k_train_out(const float* __restrict__ hin
 struct TrainWs {
   float* bufA;
   float* bufB;
+  f32x4* enc;   // the chunk's encoding tiles: written by the first layer, read by the skip layer
   float* wp;
   double* stats;
   size_t bytes;
@@ -432,11 +448,13 @@ static TrainWs carve(void* base, int64_t chunk) {
     return o;
   };
   const size_t oA = take(tiles * TILE_FLOATS * 4), oB = take(tiles * TILE_FLOATS * 4);
+  const size_t oE = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
   char* b = (char*)base;
   TrainWs w;
   w.bufA = (float*)(b + oA);
   w.bufB = (float*)(b + oB);
+  w.enc = (f32x4*)(b + oE);
   w.wp = (float*)(b + ow);
   w.stats = (double*)(b + ost);
   w.bytes = off;
@@ -531,7 +549,7 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
       hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
                          ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps, hin,
-                         stats);
+                         stats, (const f32x4*)nullptr, ws.enc);
     }
     for (int L = 1; L < 8; ++L) {
       if (keep) {
@@ -544,13 +562,13 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
         hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
                            c0, ein, hin, n, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
-                           stats + 512 * L);
+                           stats + 512 * L, (const f32x4*)ws.enc, (f32x4*)nullptr);
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
         hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
                            ein, hin, n, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps, hout,
-                           stats + 512 * L);
+                           stats + 512 * L, (const f32x4*)nullptr, (f32x4*)nullptr);
       }
       float* t = hin;
       hin = hout;
@@ -1159,6 +1177,7 @@ struct BwdWs {
   double* s12;
   double* ostat;
   double* gacc;
+  f32x4* enc;   // encoding tiles of a recomputed chunk (first layer -> skip layer)
   size_t bytes;
 };
 
@@ -1173,6 +1192,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   size_t oh[8], og[2];
   for (int L = 0; L < 8; ++L) oh[L] = take(tiles * TILE_FLOATS * 4);
   for (int i = 0; i < 2; ++i) og[i] = take(tiles * TILE_FLOATS * 4);
+  const size_t oenc = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
   const size_t os = take((8 * S12_LAYER + 257) * 8), oa = take((size_t)gacc_layout().total * 8);
@@ -1188,6 +1208,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.s12 = (double*)(b + os);
   w.ostat = w.s12 + 8 * S12_LAYER;   // s12 per layer [8][COPIES][512], then the output layer's statistics
   w.gacc = (double*)(b + oa);
+  w.enc = (f32x4*)(b + oenc);
   w.bytes = off;
   return w;
 }
@@ -1245,7 +1266,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
       hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
                          ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps, ws.h[0],
-                         ws.stats);
+                         ws.stats, (const f32x4*)nullptr, ws.enc);
     }
     for (int L = 1; L < 8 && !kept; ++L) {
       const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], nullptr, nullptr, P.lin_b[L - 1], ws.stats + 512 * (L - 1)};
@@ -1253,12 +1274,12 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
         hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
                            c0, ein, ws.h[3], n, ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps, ws.h[4],
-                           ws.stats + 512 * 4);
+                           ws.stats + 512 * 4, (const f32x4*)ws.enc, (f32x4*)nullptr);
       } else {
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
         hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
                            ein, ws.h[L - 1], n, ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps, ws.h[L],
-                           ws.stats + 512 * L);
+                           ws.stats + 512 * L, (const f32x4*)nullptr, (f32x4*)nullptr);
       }
     }
     {
