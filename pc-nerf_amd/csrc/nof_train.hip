@@ -31,6 +31,9 @@ namespace pcn {
 #ifndef PCN_WS_XD
 #define PCN_WS_XD 4  // k_train_ws / k_dgrad_ws: LDS read ring depth in k-groups
 #endif
+#ifndef PCN_OSTAT1
+#define PCN_OSTAT1 1  // output-layer backward statistics in one pass (k_out_bwd_stats1) instead of four
+#endif
 #ifndef PCN_S12_COPIES
 #define PCN_S12_COPIES 8  // k_wgrad_reduce: copies of the BatchNorm-backward sums (block m adds to copy m % COPIES)
 #endif
@@ -731,6 +734,64 @@ __global__ __launch_bounds__(256) void k_out_bwd_stats(const float* __restrict__
   if (lane == 0) atomicAdd(&acc[256], (double)gs);
 }
 
+// One-pass form of k_out_bwd_stats: each lane keeps all 128 of its half's feature sums over its tiles (two
+// 16-load batches per tile in flight), reduces them across its 32 lanes with shuffles once at the end, and the
+// block adds its totals to copy (block % OSTAT_COPIES) of acc (fewer blocks per address); k_out_bwd_grad sums the
+// copies.
+constexpr int OSTAT_COPIES = PCN_OSTAT1 ? 8 : 1;
+__global__ __launch_bounds__(256) void k_out_bwd_stats1(const float* __restrict__ g, const float* __restrict__ pin,
+                                                        const float* __restrict__ h7, int64_t n,
+                                                        const float* __restrict__ coef7, double* __restrict__ acc) {
+  __shared__ __attribute__((aligned(16))) float mu[256];
+  __shared__ float wsum[4][257];
+  const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31, wv = t >> 6;
+  mu[t] = coef7[t];
+  __syncthreads();
+  const int64_t ntiles = (n + 31) / 32;
+  float a[128];
+#pragma unroll
+  for (int i = 0; i < 128; ++i) a[i] = 0.0f;
+  float gs = 0.0f;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wv; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t s = tile * 32 + li;
+    const float gv = s < n ? logit_grad(g, pin, s) : 0.0f;
+    if (h == 0) gs += gv;
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(h7 + tile * TILE_FLOATS) + lane;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      f32x4 x[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = x4[(16 * hb + j) * 64];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int gq = 16 * hb + j;
+        const f32x4 m = *reinterpret_cast<const f32x4*>(mu + 8 * gq + 4 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[4 * gq + q] += gv * (x[j][q] - m[q]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 128; ++i) {
+    float v = a[i];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);   // over the 32 lanes of this half
+    a[i] = v;
+  }
+  if (li == 0) {
+#pragma unroll
+    for (int i = 0; i < 128; ++i) wsum[wv][8 * (i >> 2) + 4 * h + (i & 3)] = a[i];
+  }
+  gs = wave_sum_f(gs);
+  if (lane == 0) wsum[wv][256] = gs;
+  __syncthreads();
+  double* ac = acc + (size_t)(blockIdx.x % OSTAT_COPIES) * 257;
+  const double tot = (((double)wsum[0][t] + (double)wsum[1][t]) + ((double)wsum[2][t] + (double)wsum[3][t]));
+  atomicAdd(&ac[t], tot);
+  if (t == 0)
+    atomicAdd(&ac[256], ((double)wsum[0][256] + (double)wsum[1][256]) + ((double)wsum[2][256] + (double)wsum[3][256]));
+}
+
 // dL/dh_7 = BN8_back(g_s * w_out); block 0 also accumulates d gamma_8, d beta_8, d w_out, d b_out.
 __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ g, const float* __restrict__ pin,
                                                       const float* __restrict__ h7, int64_t n,
@@ -747,7 +808,12 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
   __shared__ __attribute__((aligned(16))) float cwo[256];
   {
     const int k = threadIdx.x;
-    const double A = acc[k], G0 = acc[256];
+    double A = 0.0, G0 = 0.0;
+#pragma unroll
+    for (int c = 0; c < OSTAT_COPIES; ++c) {   // k_out_bwd_stats1's copies
+      A += acc[257 * c + k];
+      G0 += acc[257 * c + 256];
+    }
     const float wo = wout[k], invstd = coef7[256 + k];
     const double S1 = (double)wo * G0, dotp = (double)wo * A;
     cgm[k] = (float)(S1 / (double)n);
@@ -1195,7 +1261,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t oenc = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
-  const size_t os = take((8 * S12_LAYER + 257) * 8), oa = take((size_t)gacc_layout().total * 8);
+  const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257) * 8), oa = take((size_t)gacc_layout().total * 8);
   char* b = (char*)base;
   BwdWs w;
   for (int L = 0; L < 8; ++L) w.h[L] = (float*)(b + oh[L]);
@@ -1286,9 +1352,15 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
       hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
       // 2. occ_out + BatchNorm 8
-      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + 257) * sizeof(double), s));   // one memset per chunk
-      hipLaunchKernelGGL(k_out_bwd_stats, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
-                         ws.coef + 7 * 1024, ws.ostat);
+      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257) * sizeof(double), s));  // per chunk
+      if (PCN_OSTAT1) {
+        const unsigned sg = (unsigned)((ntiles + 3) / 4 < 256 ? (ntiles + 3) / 4 : 256);
+        hipLaunchKernelGGL(k_out_bwd_stats1, dim3(sg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
+                           ws.coef + 7 * 1024, ws.ostat);
+      } else {
+        hipLaunchKernelGGL(k_out_bwd_stats, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
+                           ws.coef + 7 * 1024, ws.ostat);
+      }
       hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, P.bn_w[7], P.out_w, ws.ostat, ws.gacc + G.g[7], ws.gacc + G.be[7],
                          ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0]);
