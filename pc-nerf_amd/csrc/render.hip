@@ -70,10 +70,14 @@ __global__ __launch_bounds__(256) void k_sample_coarse(const float* __restrict__
   // is its index plus the child values strictly below it (equal child values have higher indices), and the rank
   // of a child value its index plus the parent values <= it -- two binary searches instead of S comparisons.
   // The wave checks monotonicity first and falls back to the all-pairs rank otherwise (identical output).
+  // A NaN bound (NaN values compare false) makes the list non-monotone, so such rays take the rank path, which
+  // orders NaNs last like torch.sort.
   bool mono = true;
-  for (int a = lane; a + 1 < S; a += 64)
-    if (a + 1 != sp && seg_value(a, sp, sc, near, far, cn, cf) > seg_value(a + 1, sp, sc, near, far, cn, cf))
+  for (int a = lane; a < S; a += 64) {
+    const float va = seg_value(a, sp, sc, near, far, cn, cf);
+    if (!(va == va) || (a + 1 < S && a + 1 != sp && !(va <= seg_value(a + 1, sp, sc, near, far, cn, cf))))
       mono = false;
+  }
   if (__all(mono)) {
     for (int a = lane; a < S; a += 64) {
       const float va = seg_value(a, sp, sc, near, far, cn, cf);
@@ -99,9 +103,11 @@ __global__ __launch_bounds__(256) void k_sample_coarse(const float* __restrict__
   for (int a = lane; a < S; a += 64) {
     const float va = seg_value(a, sp, sc, near, far, cn, cf);
     int rank = 0;
+    const bool na = !(va == va);
     for (int b = 0; b < S; ++b) {
       const float vb = seg_value(b, sp, sc, near, far, cn, cf);
-      rank += (vb < va) || (vb == va && b < a);
+      const bool nb = !(vb == vb);
+      rank += (vb < va) || (na && !nb) || ((vb == va || (na && nb)) && b < a);   // NaNs after every number
     }
     zr[rank] = va;
   }
@@ -380,15 +386,17 @@ __global__ __launch_bounds__(256) void k_resample(const float* __restrict__ Z, c
   for (int i = lane; i < nbin; i += 64) bins[i] = 0.5f * (zs[i + 1] + zs[i]);
   pdf_samples(bins, ws + 1, nbin, cdf, I, U ? U + ray * I : nullptr, sb + S, lane);
   for (int i = lane; i < S; i += 64) sb[i] = zs[i];
-  for (int i = S + I + lane; i < P2; i += 64) sb[i] = __builtin_inff();
+  for (int i = S + I + lane; i < P2; i += 64) sb[i] = __builtin_nanf("");   // pads sort last, with any NaN
   __syncthreads();
   // sort(cat(z, z_samples)) (render.py:463-467): both lists are (almost always) non-decreasing already, so the
   // merged position of a coarse value is its index plus the fine values strictly below it, of a fine value its
   // index plus the coarse values <= it (binary searches in LDS).  Any unsorted list in the block sends the whole
   // block through the bitonic sort below (its barriers need every wave); the sorted values are the same.
+  // (a NaN compares false, so a list holding one is "unsorted" and goes to the NaN-aware bitonic sort)
   bool mono = true;
-  for (int i = lane; i + 1 < S; i += 64) mono = mono && !(sb[i] > sb[i + 1]);
-  for (int i = lane; i + 1 < I; i += 64) mono = mono && !(sb[S + i] > sb[S + i + 1]);
+  for (int i = lane; i < S; i += 64) mono = mono && (sb[i] == sb[i]) && (i + 1 >= S || sb[i] <= sb[i + 1]);
+  for (int i = lane; i < I; i += 64)
+    mono = mono && (sb[S + i] == sb[S + i]) && (i + 1 >= I || sb[S + i] <= sb[S + i + 1]);
   if (!__syncthreads_or(mono ? 0 : 1)) {
     if (active) {
       float* out = ZF + ray * (S + I);
@@ -421,7 +429,8 @@ __global__ __launch_bounds__(256) void k_resample(const float* __restrict__ Z, c
         if (ixj > i) {
           const float a = sb[i], b = sb[ixj];
           const bool up = (i & k) == 0;
-          if ((a > b) == up) {
+          const bool gt = (a == a) ? (a > b) : (b == b);   // NaN greater than every number (torch.sort order)
+          if (gt == up) {
             sb[i] = b;
             sb[ixj] = a;
           }

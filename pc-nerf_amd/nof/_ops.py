@@ -385,7 +385,10 @@ def child_range_loss(pred, target, rays, sub_nerf_test_num: int, kind: str, pre:
         raise RuntimeError("child range loss: pred and target differ in size")
     cid, stride = _child_ids(rays, n)
     L = H.lib()
-    ws = _workspace(pred.device, L.pcnerf_child_range_loss_workspace_bytes(int(sub_nerf_test_num)))
+    # its own buffer, not the shared scratch: the backward reads the per-child sums/counts from it, and any HIP op
+    # running between this forward and backward() (another micro-batch, a logging render) reuses the scratch
+    ws = torch.empty(max(1, int(L.pcnerf_child_range_loss_workspace_bytes(int(sub_nerf_test_num)))),
+                     dtype=torch.uint8, device=pred.device)
     out = torch.empty((1,), dtype=torch.float32, device=pred.device)
     H.check(L.pcnerf_child_range_loss(pred.data_ptr(), target.data_ptr(), n, cid, stride, int(sub_nerf_test_num),
                                       _KIND[kind], float(pre), float(post), ws.data_ptr(), out.data_ptr(),
@@ -452,11 +455,29 @@ def composite_backward(p, z, noise, noise_std, eps, rays, sub_nerf_test_num, g_d
     return out
 
 
+# Activation-store budget (bytes) of one train-mode pass; None = the default policy below.
+_STORE_BUDGET = None
+
+
+def set_activation_store_budget(nbytes):
+    """Explicit cap for the training forward's activation store (bytes per TrainPass; 0 disables it; None restores
+    the default).  Returns the previous setting.  The store lives from a pass's forward to its backward, so a
+    caller that allocates a lot in between should cap it; the bench opts into ``free HBM - 4 GiB``."""
+    global _STORE_BUDGET
+    prev, _STORE_BUDGET = _STORE_BUDGET, (None if nbytes is None else max(0, int(nbytes)))
+    return prev
+
+
 class ActivationStore:
     """Device buffer for the first ``n_chunks`` chunks' layer outputs + BatchNorm statistics of one train-mode
-    query (pcnerf_nof_store_bytes per chunk), so its backward skips their recomputation.  Sized to the HBM that is
-    free (driver-free + torch's cached-but-unused) after ``reserve`` bytes; ``PCNERF_ACT_STORE=0`` disables it,
-    ``PCNERF_ACT_STORE_GB`` caps it."""
+    query (pcnerf_nof_store_bytes per chunk), so its backward skips their recomputation.
+
+    Budget, in order: ``PCNERF_ACT_STORE=0`` disables it; ``set_activation_store_budget(n)`` or
+    ``PCNERF_ACT_STORE_GB`` set an explicit cap; otherwise the DEFAULT is half of the HBM free at the forward
+    (driver-free + torch's cached-but-unused) after ``reserve`` bytes -- the other half stays free for whatever
+    the caller allocates between forward and backward (a drop-in under Lightning: logging, other modules).  The
+    store never takes more than free HBM minus ``reserve``; chunks beyond the budget are recomputed in the
+    backward (same gradients)."""
 
     def __init__(self, device, total_samples: int, chunk: int, reserve: int):
         import os
@@ -467,10 +488,14 @@ class ActivationStore:
         if os.environ.get("PCNERF_ACT_STORE", "1") != "0" and n_chunks > 0:
             free, _ = torch.cuda.mem_get_info(device)
             free += torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
-            budget = max(0, free - int(reserve))
+            avail = max(0, free - int(reserve))
             cap = os.environ.get("PCNERF_ACT_STORE_GB")
-            if cap is not None:
-                budget = min(budget, int(float(cap) * (1 << 30)))
+            if _STORE_BUDGET is not None:
+                budget = min(avail, _STORE_BUDGET)
+            elif cap is not None:
+                budget = min(avail, int(float(cap) * (1 << 30)))
+            else:
+                budget = avail // 2
         self.n_chunks = min(n_chunks, budget // self.per_chunk)
         self.buf = None
         while self.n_chunks > 0:

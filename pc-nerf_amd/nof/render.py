@@ -77,9 +77,20 @@ def _noise(rng, key, z, noise_std):
 
 def sample_pdf(bins, weights, N_samples, det=False, pytest=False, *, u=None):
     """render.py:371-412: inverse-CDF samples, unsorted, ``bins`` (R, B), ``weights`` (R, B-1) -> (R, N).
-    ``u`` (keyword-only) injects the uniform draws when ``det`` is False."""
+    ``u`` (keyword-only) injects the uniform draws when ``det`` is False.
+
+    ``pytest=True`` is the reference's test hook (render.py:386-394): ``np.random.seed(0)`` (numpy's global
+    generator, as the reference seeds it), then ``u`` = float32 of ``np.linspace(0, 1, N)`` (det) or of
+    ``np.random.rand(R, N)``; the draws are made on the host and uploaded, the sampling itself runs on the device."""
     if pytest:
-        raise NotImplementedError("sample_pdf(pytest=True) (numpy-seeded draws) is not supported on the device")
+        R = bins.shape[0]
+        np.random.seed(0)
+        if det:
+            hu = np.broadcast_to(np.linspace(0., 1., N_samples), (R, N_samples))
+        else:
+            hu = np.random.rand(R, N_samples)
+        u = torch.from_numpy(np.ascontiguousarray(hu, dtype=np.float32)).to(bins.device)
+        det = False   # the uploaded draws are used as given (the linspace is numpy's, float64 rounded to float32)
     return _ops.sample_pdf_standalone(bins, weights, N_samples, det, u)
 
 

@@ -42,37 +42,52 @@ def _slab(o, d, lo, hi):
     return tmin.max(axis=-1), tmax.min(axis=-1)
 
 
-def make_children(n_children=32, seed=0, lo=PARENT_LO, hi=PARENT_HI, min_center_dist=3.0):
+def make_children(n_children=32, seed=0, lo=PARENT_LO, hi=PARENT_HI, min_center_dist=3.0, origin=(0.0, 0.0, 0.0)):
     """Child AABBs (n,2,3) fully inside the parent block, centres at least ``min_center_dist`` from the origin."""
     rng = np.random.default_rng(seed)
+    lo, hi, origin = np.asarray(lo, np.float64), np.asarray(hi, np.float64), np.asarray(origin, np.float64)
     boxes = []
     while len(boxes) < n_children:
         half = rng.uniform(0.5, 1.5, size=3) / 2
         c = rng.uniform(lo + half, hi - half)
-        if np.linalg.norm(c) < min_center_dist:
+        if np.linalg.norm(c - origin) < min_center_dist:
             continue
         boxes.append(np.stack([c - half, c + half]))
     return np.asarray(boxes)
 
 
-def make_rays(n_rays, n_children=32, seed=0, layout="train"):
-    """Config-2 synthetic rays.
+# MaiCity-00's parent box (shells/pretraining/MaiCity00_pcnerf_train.bash) split in x into parent blocks (config 4)
+MAICITY_LO = np.array([-12.0, -12.0, -2.0])
+MAICITY_HI = np.array([61.0, 12.0, 0.5])
+
+
+def block_bounds(b, n_blocks, lo=MAICITY_LO, hi=MAICITY_HI):
+    """Parent block b of ``n_blocks`` equal x-slices of [lo, hi], and a LiDAR origin at its centre (z = 0)."""
+    xs = np.linspace(lo[0], hi[0], n_blocks + 1)
+    blo, bhi = np.array([xs[b], lo[1], lo[2]]), np.array([xs[b + 1], hi[1], hi[2]])
+    return blo, bhi, np.array([0.5 * (xs[b] + xs[b + 1]), 0.5 * (lo[1] + hi[1]), 0.0])
+
+
+def make_rays(n_rays, n_children=32, seed=0, layout="train", lo=PARENT_LO, hi=PARENT_HI, origin=(0.0, 0.0, 0.0)):
+    """Config-2 synthetic rays (default parent block and origin), or those of another parent block ``[lo, hi]``
+    seen from ``origin`` (config 4's blocks).
 
     Returns ``rays`` float32 ``(n_rays, 15)`` for ``layout='train'``.  Every ray starts at the origin and ends at
     a uniformly drawn point of a uniformly drawn child box (its LiDAR return)."""
     assert layout == "train"
-    boxes = make_children(n_children, seed)
+    origin = np.asarray(origin, np.float64)
+    boxes = make_children(n_children, seed, lo, hi, origin=origin)
     rng = np.random.default_rng(seed + 1)
     cid = rng.integers(0, n_children, size=n_rays)
-    lo, hi = boxes[cid, 0], boxes[cid, 1]
-    t = rng.uniform(lo, hi)
+    blo, bhi = boxes[cid, 0], boxes[cid, 1]
+    t = rng.uniform(blo, bhi) - origin
     rng_ = np.linalg.norm(t, axis=1)
     d = t / rng_[:, None]
-    o = np.zeros_like(d)
-    cn, cf = _slab(o, d, lo - AABB_GROW, hi + AABB_GROW)
+    o = np.broadcast_to(origin, d.shape).copy()
+    cn, cf = _slab(o, d, blo - AABB_GROW, bhi + AABB_GROW)
     cn = np.maximum(cn, 0.0) - SURFACE_EXPAND
     cf = cf + SURFACE_EXPAND
-    _, pf = _slab(o, d, PARENT_LO, PARENT_HI)
+    _, pf = _slab(o, d, np.asarray(lo, np.float64), np.asarray(hi, np.float64))
     pf = np.maximum(pf, cf)
     rays = np.zeros((n_rays, 15), dtype=np.float64)
     rays[:, 0:3] = o

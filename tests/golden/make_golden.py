@@ -391,15 +391,100 @@ def gen_maicity_frames(step=40):
     save("maicity_frames", poses=poses, **frames)
 
 
+def gen_pdf_pytest():
+    """sample_pdf(..., pytest=True) (render.py:386-394): numpy-seeded u, det and random, on gen_pdf's inputs."""
+    rng = np.random.default_rng(31)
+    nr, nb = 64, 33
+    bins = np.sort(rng.uniform(0, 30, size=(nr, nb)), axis=1).astype(np.float32)
+    w = rng.uniform(0, 1, size=(nr, nb - 1)).astype(np.float32) ** 8
+    w = (w / (w.sum(1, keepdims=True) + 1e-10)).astype(np.float32)
+    with torch.no_grad():
+        det = R.sample_pdf(torch.from_numpy(bins), torch.from_numpy(w), 96, det=True, pytest=True)
+        rnd = R.sample_pdf(torch.from_numpy(bins), torch.from_numpy(w), 96, det=False, pytest=True)
+    save("sample_pdf_pytest", bins=bins, weights=w, samples_det=t(det), samples_rand=t(rnd))
+
+
+PCNERF_TRAIN = dict(use_child_nerf_loss=1, issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0, perturb=0,
+                    noise_std=0, chunk=262144)   # shells/pretraining/*_pcnerf_train.bash (perturb 0: deterministic)
+
+
+def train_outputs(res, rays, mc, mf):
+    gt = torch.from_numpy(rays[:, 14])
+    lr, lrf = range_losses(res["depth"], res["depth_fine"], gt, torch.from_numpy(rays), 0, 0)
+    total = lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"] + \
+        1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"]
+    return dict(depth=t(res["depth"]), depth_fine=t(res["depth_fine"]), child_free_loss=t(res["child_free_loss"]),
+                child_depth_loss=t(res["child_depth_loss"]), child_free_loss_fine=t(res["child_free_loss_fine"]),
+                child_depth_loss_fine=t(res["child_depth_loss_fine"]), loss_range=t(lr), loss_range_fine=t(lrf),
+                loss_total=t(total), running_c=running_stats(mc), running_f=running_stats(mf))
+
+
+def gen_config2_full():
+    """BASELINE config 2 at its full size: 65,536 rays of nof.synthetic.make_rays(65536, seed=0) (regenerated from the
+    seed by the test; only outputs are stored), 128/256 samples, train-mode BatchNorm over 262,144-sample chunks
+    (32 coarse + 96 fine chunks), child losses, segmented sampling 0.1, perturb 0."""
+    import time
+    torch.set_num_threads(os.cpu_count() or 1)
+    rays = syn.make_rays(65536, seed=0)
+    emb, mc, mf = models(train=True)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=32, N_samples=128,
+                                  N_importance=256, **PCNERF_TRAIN)
+    print("config2 full:", time.perf_counter() - t0, "s")
+    torch.set_num_threads(1)
+    save("config2_full", n_rays=65536, seed=0, N_samples=128, N_importance=256, **train_outputs(res, rays, mc, mf))
+
+
+def scene_rays():
+    return dict(np.load(os.path.join(HERE, "scene_rays.npz"), allow_pickle=False))
+
+
+def gen_config1_kitti():
+    """BASELINE config 1: a 4,096-ray batch of KITTI-00 rays (scene_rays.npz, made by make_scene_rays.py from the
+    fixture frames) through render_rays_train at 64/128 samples with the PC-NeRF KITTI shell's settings (one
+    262,144-sample coarse chunk, three fine chunks), and the val split through render_rays_val (eval mode)."""
+    sc = scene_rays()
+    rays = sc["kitti_train"]
+    n_child = int(sc["kitti_children"])
+    emb, mc, mf = models(train=True)
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=n_child, N_samples=64,
+                                  N_importance=128, **PCNERF_TRAIN)
+    out = train_outputs(res, rays, mc, mf)
+    emb, mc, mf = models(train=False)
+    val = sc["kitti_val"]
+    with torch.no_grad():
+        rv = R.render_rays_val(mc, mf, emb, torch.from_numpy(val), N_samples=64, N_importance=128, perturb=0,
+                               noise_std=0, chunk=262144)
+    save("config1_kitti", N_samples=64, N_importance=128, sub_nerf_test_num=n_child, **out,
+         val_depth=t(rv["depth"]), val_depth_fine=t(rv["depth_fine"]))
+
+
+def gen_config4_maicity():
+    """BASELINE config 4: MaiCity-00 split into 4 parent blocks, each with its own coarse/fine NOF (seeds
+    1234+b / 5678+b), up to 1,024 rows per block through render_rays_train at 128/256 samples."""
+    sc = scene_rays()
+    out = {}
+    for b in range(4):
+        rays = sc[f"maicity_b{b}"]
+        emb = Embedding(3, 10)
+        mc = syn.load_into(NOF_coarse(), syn.init_nof_params(SEED_C + b)).train()
+        mf = syn.load_into(NOF_fine(), syn.init_nof_params(SEED_F + b)).train()
+        with torch.no_grad():
+            res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=int(sc[f"maicity_b{b}_children"]),
+                                      N_samples=128, N_importance=256, **PCNERF_TRAIN)
+        out.update({f"b{b}_{k}": v for k, v in train_outputs(res, rays, mc, mf).items()})
+    save("config4_maicity", N_samples=128, N_importance=256, **out)
+
+
+GENERATORS = [gen_maicity_frames, gen_kitti_frames, gen_metrics, gen_grads, gen_aabb, gen_render_rays, gen_nof,
+              gen_pdf, gen_val, gen_train, gen_view, gen_pdf_pytest, gen_config1_kitti, gen_config4_maicity,
+              gen_config2_full]
+
 if __name__ == "__main__":
-    gen_maicity_frames()
-    gen_kitti_frames()
-    gen_metrics()
-    gen_grads()
-    gen_aabb()
-    gen_render_rays()
-    gen_nof()
-    gen_pdf()
-    gen_val()
-    gen_train()
-    gen_view()
+    # python make_golden.py [name ...]  (names without the gen_ prefix; default: all)
+    want = set(sys.argv[1:])
+    for fn in GENERATORS:
+        if not want or fn.__name__[4:] in want:
+            fn()

@@ -185,3 +185,51 @@ def test_grad_accumulates_and_running_stats_once():
             first = mc.layer2[6].weight.grad.clone()
     np.testing.assert_allclose(mc.layer2[6].weight.grad.cpu().numpy(), 2 * first.cpu().numpy(), rtol=1e-5,
                                atol=1e-6 * float(first.abs().max()))
+
+
+def test_child_range_loss_backward_after_interleaved_ops():
+    """The per-child range loss keeps its per-child sums/counts in a buffer of its own: other HIP work between its
+    forward and backward() (a second micro-batch's render, here) must not change its gradient."""
+    from nof.criteria import child_range_loss
+    g = torch.Generator().manual_seed(12)
+    n, N = 3000, 40
+    rays = torch.zeros((n, 15))
+    rays[:, 9] = torch.randint(1, N + 1, (n,), generator=g).float()
+    gt = 5 + 20 * torch.rand(n, generator=g)
+    pred = (gt + 0.3 * torch.randn(n, generator=g)).to(DEV)
+    rd, gd = rays.to(DEV), gt.to(DEV)
+    p1 = pred.clone().requires_grad_(True)
+    child_range_loss(p1, gd, rd, N, 1.0).sum().backward()
+    p2 = pred.clone().requires_grad_(True)
+    loss = child_range_loss(p2, gd, rd, N, 1.0)
+    emb, mc, mf = models()
+    with torch.no_grad():   # another render + child losses between the loss's forward and its backward
+        R.render_rays_train(mc, mf, emb, torch.from_numpy(syn.make_rays(256, seed=2)).to(DEV), sub_nerf_test_num=32,
+                            N_samples=64, N_importance=128, perturb=0, noise_std=0, chunk=8192, issegmentated=1,
+                            childnerf_ratio=0.1, use_child_nerf_divide=1, use_child_nerf_loss=1)
+        child_range_loss(pred, gd, rd, 7, 1.0)
+    loss.sum().backward()
+    assert torch.equal(p1.grad, p2.grad)
+
+
+def test_train_grads_vs_oracle_large_chunks():
+    """Chunks of 65,536 samples (2,048 tiles: the backward's multi-tile statistics pass, k_out_bwd_stats1,
+    accumulates several tiles per wave) -- 2,048 rays x (64 + 192) samples = 2 coarse + 6 fine chunks."""
+    R_, S, I = 2048, 64, 128
+    rays_np = syn.make_rays(R_, seed=29)
+    kw = dict(sub_nerf_test_num=32, N_samples=S, N_importance=I, perturb=0, noise_std=0, chunk=65536,
+              issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0, use_child_nerf_loss=1)
+    Pc, Pf = oracle_params(SEED_C), oracle_params(SEED_F)
+    rays_c = torch.from_numpy(rays_np)
+    ro = O.render_rays_train(Pc, Pf, rays_c, **kw)
+    lr, lrf = O.range_losses(ro["depth"], ro["depth_fine"], rays_c[:, 14])
+    O.total_loss(ro, lr, lrf).sum().backward()
+    gc, gf = oracle_summary(Pc, 5), oracle_summary(Pf, 6)
+    emb, mc, mf = models()
+    rays = torch.from_numpy(rays_np).to(DEV)
+    res = R.render_rays_train(mc, mf, emb, rays, **kw)
+    lr, lrf = range_losses(res["depth"], res["depth_fine"], rays[:, 14], rays, 0, 32)
+    total(res, lr, lrf).sum().backward()
+    pc, pf = named(mc), named(mf)
+    check_grads(lambda k: pc[k].grad.cpu().numpy(), list(pc), gc, "", GRTOL, NOISE)
+    check_grads(lambda k: pf[k].grad.cpu().numpy(), list(pf), gf, "", GRTOL, NOISE)

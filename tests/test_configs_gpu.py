@@ -1,0 +1,310 @@
+"""BASELINE.json's configurations on the GPU, against the reference.
+
+  config 1  KITTI-00 rays, 4,096-ray batch, 64/128 samples (train and val) -- rows rebuilt on the GPU by
+            nof.dataset from the fixture frames, checked bit for bit against the fixture's rows, then rendered and
+            compared with the reference's outputs on those rows (tests/golden/config1_kitti.npz);
+  config 2  the headline workload at FULL size: 65,536 rays, 128/256 samples, chunk 262,144 (32 coarse + 96 fine
+            BatchNorm chunks), child losses, against the reference run on the same rays (config2_full.npz);
+  config 3  the KITTI training loop at 262,144 rays/iter (64/128 samples): a full-size training step (forward,
+            losses, backward, Adam), property-checked (no CPU run of this size exists);
+  config 4  MaiCity-00 in 4 parent blocks, each with its own weights (config4_maicity.npz);
+  the training driver: k steps of Adam + MultiStepLR through train_kitti.fit() against the oracle's autograd +
+            torch.optim.Adam (parameters and per-step losses), once with BatchNorm inputs whose |mean|/std >> 1.
+
+Tolerances: depths, losses, BatchNorm running stats rtol 1e-4 (the north star's bound), atol 1e-6 for values
+near zero; the worst relative depth error over each config is reported (PCNERF_PARITY_REPORT=<path> appends it
+as a JSON line).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from nof import synthetic as syn
+from nof.criteria import nof_loss
+from nof.networks import Embedding, NOF_coarse, NOF_fine
+from nof import render as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SEED_C, SEED_F = 1234, 5678
+RTOL = 1e-4
+PCNERF_TRAIN = dict(use_child_nerf_loss=1, issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0, perturb=0,
+                    noise_std=0, chunk=262144)
+
+
+def models(train, sc=SEED_C, sf=SEED_F):
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(sc)).to(DEV).train(train)
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(sf)).to(DEV).train(train)
+    return Embedding(3, 10), mc, mf
+
+
+def running(m):
+    return np.stack([np.stack([bn.running_mean.cpu().numpy(), bn.running_var.cpu().numpy()]) for bn in m.norms()])
+
+
+def report(name, **vals):
+    path = os.environ.get("PCNERF_PARITY_REPORT")
+    if path:
+        with open(path, "a") as fh:
+            fh.write(json.dumps({"case": name, **{k: float(v) for k, v in vals.items()}}) + "\n")
+
+
+def max_rel(a, b):
+    a = a.detach().cpu().numpy().astype(np.float64) if torch.is_tensor(a) else np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-6)))
+
+
+def close(a, b, rtol=RTOL, atol=1e-6, what=""):
+    a = a.detach().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    np.testing.assert_allclose(a.astype(np.float64), b.astype(np.float64), rtol=rtol, atol=atol, err_msg=what)
+
+
+def check_train(res, g, rays, mc, mf, pre="", name=""):
+    """Depths, the four child losses, the range losses of train_kitti.py:144-146, the total, running stats."""
+    for k in ("depth", "depth_fine"):
+        close(res[k], g[pre + k], what=k)
+    for k in ("child_free_loss", "child_depth_loss", "child_free_loss_fine", "child_depth_loss_fine"):
+        close(res[k], g[pre + k], RTOL, 1e-9, k)
+    loss = nof_loss["smoothl1"]()
+    gt = rays[:, 14]
+    lr = 1e-1 * loss(1e1 * res["depth"], 1e1 * gt)
+    lrf = 1e-1 * loss(1e1 * res["depth_fine"], 1e1 * gt)
+    close(lr, g[pre + "loss_range"], what="loss_range")
+    close(lrf, g[pre + "loss_range_fine"], what="loss_range_fine")
+    tot = lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"] + \
+        1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"]
+    close(tot, g[pre + "loss_total"], what="loss_total")
+    close(running(mc), g[pre + "running_c"], RTOL, 1e-6, "running coarse")
+    close(running(mf), g[pre + "running_f"], RTOL, 1e-6, "running fine")
+    report(name, max_rel_depth=max_rel(res["depth"], g[pre + "depth"]),
+           max_rel_depth_fine=max_rel(res["depth_fine"], g[pre + "depth_fine"]),
+           rel_loss_total=max_rel(tot, g[pre + "loss_total"]), rays=rays.shape[0])
+
+
+# ----------------------------------------------------------------------------------------------- config 2
+def test_config2_full_size_vs_reference():
+    """65,536 rays x (128 + 384) MLP samples in train-mode BatchNorm chunks of 262,144, vs the reference."""
+    g = golden("config2_full")
+    rays = torch.from_numpy(syn.make_rays(int(g["n_rays"]), n_children=32, seed=int(g["seed"]))).to(DEV)
+    emb, mc, mf = models(True)
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=32, N_samples=128, N_importance=256,
+                                  **PCNERF_TRAIN)
+    check_train(res, g, rays, mc, mf, name="config2_full")
+    assert int(mc.norms()[0].num_batches_tracked) == 32 and int(mf.norms()[0].num_batches_tracked) == 96
+
+
+# ----------------------------------------------------------------------------------------------- config 1
+def kitti_scene(tmp_path):
+    from test_dataset import DS, DE, INTEREST, write_scene
+    from nof import dataset as D
+    root, pose_path, _ = write_scene(str(tmp_path))
+    kw = dict(data_start=DS, data_end=DE, cloud_size_val=64, range_delete_x=3, range_delete_y=2,
+              range_delete_z=1.25, sub_nerf_test_num=0, surface_expand=0.05, over_height=0.168, over_low=-2.0,
+              interest_x=INTEREST, interest_y=INTEREST, pose_path=pose_path, re_loaddata=1,
+              result_path=str(tmp_path / "out"), device=DEV)
+    return D.kitti_dataload(root, split="train", **kw), D.kitti_dataload(root, split="val", **kw)
+
+
+def test_config1_kitti_rays_train_and_val(tmp_path):
+    """KITTI-00 rows built on the GPU (nof.dataset) == the fixture's rows; a 4,096-ray batch through
+    render_rays_train (64/128, PC-NeRF KITTI settings) and the val split through render_rays_val."""
+    sc, g = golden("scene_rays"), golden("config1_kitti")
+    tr, va = kitti_scene(tmp_path)
+    assert tr.rays.shape[0] == int(sc["kitti_train_total"])
+    batch = tr.rays[torch.from_numpy(sc["kitti_train_idx"]).to(DEV)]
+    np.testing.assert_array_equal(batch.cpu().numpy(), sc["kitti_train"])
+    np.testing.assert_array_equal(va.rays.cpu().numpy(), sc["kitti_val"])
+    emb, mc, mf = models(True)
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, batch, sub_nerf_test_num=int(g["sub_nerf_test_num"]), N_samples=64,
+                                  N_importance=128, **PCNERF_TRAIN)
+    check_train(res, g, batch, mc, mf, name="config1_kitti_train")
+    emb, mc, mf = models(False)
+    with torch.no_grad():
+        rv = R.render_rays_val(mc, mf, emb, va.rays, N_samples=64, N_importance=128, perturb=0, noise_std=0,
+                               chunk=262144)
+    close(rv["depth"], g["val_depth"], what="val depth")
+    close(rv["depth_fine"], g["val_depth_fine"], what="val depth_fine")
+    report("config1_kitti_val", max_rel_depth_fine=max_rel(rv["depth_fine"], g["val_depth_fine"]),
+           rays=va.rays.shape[0])
+
+
+# ----------------------------------------------------------------------------------------------- config 4
+def test_config4_maicity_blocks(tmp_path):
+    """MaiCity-00 in 4 parent blocks (x split of [-12, 61]): each block's rows built on the GPU (maicity_dataload,
+    0406 face rule) == the fixture's; each block rendered with its own coarse/fine weights (128/256)."""
+    from test_dataset import M_RD, write_maicity
+    from nof import dataset as D
+    sc, g = golden("scene_rays"), golden("config4_maicity")
+    root, pose_path, _ = write_maicity(str(tmp_path))
+    for b in range(4):
+        lo, hi = sc[f"maicity_b{b}_lo"], sc[f"maicity_b{b}_hi"]
+        ds = D.maicity_dataload(root, split="train", data_start=0, data_end=6, cloud_size_val=16,
+                                range_delete_x=M_RD[0], range_delete_y=M_RD[1], range_delete_z=M_RD[2],
+                                sub_nerf_test_num=0, surface_expand=0.05, nerf_length_min=float(lo[0]),
+                                nerf_length_max=float(hi[0]), nerf_width_min=float(lo[1]), nerf_width_max=float(hi[1]),
+                                nerf_height_min=float(lo[2]), nerf_height_max=float(hi[2]), pose_path=pose_path,
+                                re_loaddata=1, result_path=str(tmp_path / f"out{b}"), device=DEV)
+        assert ds.rays.shape[0] == int(sc[f"maicity_b{b}_total"]), b
+        want = sc[f"maicity_b{b}"]
+        rays = ds.rays[:want.shape[0]].contiguous()
+        np.testing.assert_array_equal(rays.cpu().numpy(), want)
+        emb, mc, mf = models(True, SEED_C + b, SEED_F + b)
+        with torch.no_grad():
+            res = R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=int(sc[f"maicity_b{b}_children"]),
+                                      N_samples=128, N_importance=256, **PCNERF_TRAIN)
+        check_train(res, g, rays, mc, mf, pre=f"b{b}_", name=f"config4_maicity_b{b}")
+
+
+# ----------------------------------------------------------------------------------------------- config 3
+def test_config3_training_step_262144_rays(tmp_path):
+    """The KITTI training loop's step at 262,144 rays/iter (64/128 samples, chunk 262,144: 64 coarse + 192 fine
+    BatchNorm chunks, more than the activation store holds, so the backward recomputes part of the forward):
+    a batch drawn (with replacement) from the KITTI fixture scene's train rays; three steps of forward, range +
+    child losses, backward, Adam.  Properties: finite losses that decrease on the repeated batch, finite non-zero
+    gradients on both networks, running statistics and parameters updated."""
+    tr, _ = kitti_scene(tmp_path)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    idx = torch.randint(0, tr.rays.shape[0], (262144,), device=DEV, generator=gen)
+    rays = tr.rays[idx].contiguous()
+    emb, mc, mf = models(True)
+    params = list(mc.parameters()) + list(mf.parameters())
+    opt = torch.optim.Adam(params, lr=5e-4, eps=1e-8, weight_decay=1e-3)
+    w0 = mc.layer2[6].weight.detach().clone()
+    loss_fn = nof_loss["smoothl1"]()
+    losses = []
+    for _ in range(3):
+        opt.zero_grad(set_to_none=True)
+        res = R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=1171, N_samples=64, N_importance=128,
+                                  **PCNERF_TRAIN)
+        for k in ("depth", "depth_fine"):
+            assert torch.isfinite(res[k]).all()
+        gt = rays[:, 14]
+        loss = (1e-1 * loss_fn(1e1 * res["depth"], 1e1 * gt) + 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
+                + 1e6 * (res["child_free_loss"] + res["child_free_loss_fine"])
+                + 1e5 * (res["child_depth_loss"] + res["child_depth_loss_fine"]))
+        loss.backward()
+        for m in (mc, mf):
+            g = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+            assert torch.isfinite(g).all() and float(g.abs().max()) > 0
+        opt.step()
+        losses.append(float(loss))
+    assert all(np.isfinite(losses)) and losses[2] < losses[0], losses
+    assert int(mc.norms()[0].num_batches_tracked) == 3 * 64 and int(mf.norms()[0].num_batches_tracked) == 3 * 192
+    assert not torch.equal(w0, mc.layer2[6].weight.detach())
+    report("config3_train_step", loss0=losses[0], loss2=losses[2], rays=rays.shape[0])
+
+
+# ----------------------------------------------------------------------------------------------- driver trajectory
+class RayTable(torch.utils.data.Dataset):
+    def __init__(self, rays):
+        self.rays, self.ranges = rays, rays[:, 14].clone()
+
+    def __len__(self):
+        return self.rays.shape[0]
+
+    def __getitem__(self, index):
+        return {'rays': self.rays[index], 'ranges': self.ranges[index]}
+
+
+def _stress_bn(params: dict, scale: float) -> dict:
+    """Shift every BatchNorm's input mean far from zero relative to its spread: the BN shifts (and the Linear
+    biases) scaled by ``scale`` make each next layer's pre-BN activations |mean|/std >> 1."""
+    out = dict(params)
+    for k in out:
+        if k.endswith(".bias") and not k.startswith("occ_out"):
+            out[k] = (out[k] * scale).astype(np.float32)
+    return out
+
+
+@pytest.mark.parametrize("stress", [1.0, 30.0])
+def test_fit_trajectory_vs_oracle(tmp_path, stress):
+    """train_kitti.fit(): 6 epochs of one 256-ray batch (64/128 samples, chunk 8192: 2 coarse + 6 fine BatchNorm
+    chunks, perturb 0), Adam(lr 5e-4, eps 1e-8, wd 1e-3) + MultiStepLR([5, 120, 256], 0.2) (nof_utils.py:158-173,
+    train_kitti.py:108-115) -- the LR drops after epoch 5 -- against the oracle: same batches in the same
+    (device randperm) order through oracle autograd + torch.optim.Adam + MultiStepLR.  Losses every step and
+    the final parameters at rtol 1e-4 (parameters whose gradient is mathematically zero -- Linear biases before
+    BatchNorm, BN shifts before Linear->BN -- move by Adam steps on rounding noise / weight decay only: checked at
+    |delta| <= epochs * lr)."""
+    import train_kitti as T
+    from gradcheck import noise_level_grads
+    from nof.nof_utils import get_opts
+    from oracle import ref_cpu as O
+    n, epochs = 256, 6
+    rays_np = syn.make_rays(n, seed=77)
+    args = f"""--N_samples 64 --N_importance 128 --perturb 0 --noise_std 0 --chunk 8192 --batch_size {n}
+     --num_epochs {epochs} --optimizer adam --lr 5e-4 --weight_decay 1e-3 --decay_gamma 0.2 --use_child_nerf_divide 0
+     --use_child_nerf_loss 1 --use_segmentated_sample 1 --segmentated_child_nerf_ratio 0.1 --lambda_loss 1
+     --lambda_loss_fine 1 --lambda_child_free_loss 1000000 --lambda_child_depth_loss 100000 --sub_nerf_test_num 32
+     --seed 3 --visualize 0 --device cuda"""
+    h = get_opts(args.split())
+    pc_np = _stress_bn(syn.init_nof_params(SEED_C), stress)
+    pf_np = _stress_bn(syn.init_nof_params(SEED_F), stress)
+    system = T.NOFSystem(h, train_dataset=RayTable(torch.from_numpy(rays_np).to(DEV)),
+                         val_dataset=RayTable(torch.zeros((0, 15), device=DEV)))
+    syn.load_into(system.nof_coarse, pc_np)
+    syn.load_into(system.nof_fine, pf_np)
+    log = str(tmp_path / "log.jsonl")
+    T.fit(system, log_path=log)
+    hip_losses = [r["train/loss"] for r in map(json.loads, open(log)) if "train/loss" in r]
+    assert len(hip_losses) == epochs
+
+    # the oracle, fed the same batches in fit()'s order
+    gen = torch.Generator(device=DEV).manual_seed(int(h.seed))
+    Pc, Pf = O.params_from_numpy(pc_np), O.params_from_numpy(pf_np)
+    leaves = [P[k].requires_grad_(True) for P in (Pc, Pf) for k in P if k.endswith((".weight", ".bias"))]
+    opt = torch.optim.Adam(leaves, lr=5e-4, eps=1e-8, weight_decay=1e-3)
+    sched = torch.optim.lr_scheduler.MultiStepLR(opt, milestones=[5, 120, 256], gamma=0.2)
+    rays_c = torch.from_numpy(rays_np)
+    ref_losses = []
+    for _ in range(epochs):
+        perm = torch.randperm(n, device=DEV, generator=gen).cpu()
+        r = rays_c[perm]
+        opt.zero_grad()
+        res = O.render_rays_train(Pc, Pf, r, sub_nerf_test_num=32, N_samples=64, N_importance=128, perturb=0,
+                                  noise_std=0, chunk=8192, issegmentated=1, childnerf_ratio=0.1,
+                                  use_child_nerf_divide=0, use_child_nerf_loss=1)
+        lr, lrf = O.range_losses(res["depth"], res["depth_fine"], r[:, 14])
+        loss = O.total_loss(res, lr, lrf)
+        loss.backward()
+        opt.step()
+        sched.step()
+        ref_losses.append(float(loss))
+    np.testing.assert_allclose(hip_losses, ref_losses, rtol=RTOL)
+    # Parameters with mathematically zero gradients (noise_level_grads) take Adam steps on rounding noise plus
+    # weight decay: each may move by up to lr per step in either implementation.  A BatchNorm's running mean
+    # follows the Linear bias / previous BN shift in front of it, so running means get that drift as their
+    # tolerance; running variances are shift-invariant and held to rtol 1e-4.
+    nz = noise_level_grads()
+    drift = epochs * 5e-4 * 1.01
+    worst, worst_nz, worst_rm = 0.0, 0.0, 0.0
+    for tag, m, P in (("c", system.nof_coarse, Pc), ("f", system.nof_fine, Pf)):
+        sd = m.state_dict()
+        for k, v in sd.items():
+            if k.endswith("num_batches_tracked"):
+                continue
+            got, want = v.cpu().numpy().astype(np.float64), P[k].detach().numpy().astype(np.float64)
+            scale = np.abs(want).max()
+            err = float(np.max(np.abs(got - want)))
+            if k in nz:
+                np.testing.assert_allclose(got, want, rtol=0, atol=drift, err_msg=tag + k)
+                worst_nz = max(worst_nz, err)
+            elif k.endswith("running_mean"):
+                # the Linear feeding this BN: its bias and (after the first) the previous BN's shift through W
+                lin = O.LIN[O.BN.index(k[:-len(".running_mean")])]
+                w = sd[lin + ".weight"].abs().sum(1).cpu().numpy().astype(np.float64)
+                np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-6 * scale + drift * (1 + w), err_msg=tag + k)
+                worst_rm = max(worst_rm, err)
+            else:
+                np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-5 * scale, err_msg=tag + k)
+                worst = max(worst, err / scale)
+    report(f"fit_trajectory_stress{stress:g}", max_param_err_rel_scale=worst, max_noise_param_drift=worst_nz,
+           max_running_mean_err=worst_rm, loss_rel=max_rel(np.array(hip_losses), np.array(ref_losses)))

@@ -133,3 +133,57 @@ def test_train_grads(name):
     tot.sum().backward()
     check_grads(lambda k: Pc[k].grad.numpy(), kc, g, "c:", 1e-5)
     check_grads(lambda k: Pf[k].grad.numpy(), kf, g, "f:", 1e-5)
+
+
+def test_sample_pdf_pytest_hook():
+    """render.py:386-394 (pytest=True): np.random.seed(0) draws, det (numpy linspace) and random."""
+    g = golden("sample_pdf_pytest")
+    b, w = torch.from_numpy(g["bins"]), torch.from_numpy(g["weights"])
+    R, n = b.shape[0], 96
+    np.random.seed(0)
+    u_det = torch.from_numpy(np.broadcast_to(np.linspace(0., 1., n), (R, n)).astype(np.float32))
+    close(O.sample_pdf(b, w, n, det=False, u=u_det), g["samples_det"], 0, 0)
+    np.random.seed(0)
+    u_rnd = torch.from_numpy(np.random.rand(R, n).astype(np.float32))
+    close(O.sample_pdf(b, w, n, det=False, u=u_rnd), g["samples_rand"], 0, 0)
+
+
+PCNERF_TRAIN = dict(use_child_nerf_loss=1, issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0, perturb=0,
+                    noise_std=0, chunk=262144)
+
+
+def check_train(res, g, rays, Pc, Pf, pre=""):
+    for k in ("depth", "depth_fine", "child_free_loss", "child_depth_loss", "child_free_loss_fine",
+              "child_depth_loss_fine"):
+        close(res[k], g[pre + k], 1e-5, 1e-9)
+    lr, lrf = O.range_losses(res["depth"], res["depth_fine"], rays[:, 14])
+    close(lr, g[pre + "loss_range"], 1e-5)
+    close(lrf, g[pre + "loss_range_fine"], 1e-5)
+    close(O.total_loss(res, lr, lrf), g[pre + "loss_total"], 1e-5)
+    close(running(Pc), g[pre + "running_c"], 1e-5)
+    close(running(Pf), g[pre + "running_f"], 1e-5)
+
+
+def test_config1_kitti():
+    """Config 1: KITTI-00 4,096-ray batch (64/128, one 262,144-sample coarse chunk) and the val split (eval)."""
+    sc, g = golden("scene_rays"), golden("config1_kitti")
+    rays = torch.from_numpy(sc["kitti_train"])
+    Pc, Pf = P(SEED_C), P(SEED_F)
+    res = O.render_rays_train(Pc, Pf, rays, sub_nerf_test_num=int(g["sub_nerf_test_num"]), N_samples=64,
+                              N_importance=128, **PCNERF_TRAIN)
+    check_train(res, g, rays, Pc, Pf)
+    rv = O.render_rays_val(P(SEED_C), P(SEED_F), torch.from_numpy(sc["kitti_val"]), N_samples=64, N_importance=128,
+                           perturb=0, noise_std=0, chunk=262144)
+    close(rv["depth"], g["val_depth"], 1e-5, 1e-9)
+    close(rv["depth_fine"], g["val_depth_fine"], 1e-5, 1e-9)
+
+
+@pytest.mark.parametrize("b", [0, 1, 2, 3])
+def test_config4_maicity_block(b):
+    """Config 4: MaiCity-00 parent block b with its own coarse/fine weights (128/256 samples)."""
+    sc, g = golden("scene_rays"), golden("config4_maicity")
+    rays = torch.from_numpy(sc[f"maicity_b{b}"])
+    Pc, Pf = P(SEED_C + b), P(SEED_F + b)
+    res = O.render_rays_train(Pc, Pf, rays, sub_nerf_test_num=int(sc[f"maicity_b{b}_children"]), N_samples=128,
+                              N_importance=256, **PCNERF_TRAIN)
+    check_train(res, g, rays, Pc, Pf, pre=f"b{b}_")

@@ -365,3 +365,36 @@ def test_build_view_rows_vs_oracle(method):
     np.testing.assert_array_equal(g2.cpu().numpy(), rng)
     np.testing.assert_array_equal(o2.cpu().numpy(), other)
     np.testing.assert_array_equal(t2.cpu().numpy(), tin)
+
+
+def test_sample_pdf_pytest_hook():
+    """sample_pdf(pytest=True) (render.py:386-394): numpy-seeded draws, det and random, vs the reference."""
+    g = golden("sample_pdf_pytest")
+    b, w = torch.from_numpy(g["bins"]).to(DEV), torch.from_numpy(g["weights"]).to(DEV)
+    for det, key in ((True, "samples_det"), (False, "samples_rand")):
+        got = R.sample_pdf(b, w, 96, det=det, pytest=True)
+        close(got, g[key], RTOL, 1e-5, key)
+
+
+def test_nan_bounds_sort_like_torch():
+    """Rays with NaN child bounds / NaN coarse weights: the segmented coarse z and the fine merge hold every value
+    once with the NaNs last (torch.sort's order), never an unwritten slot (both kernels take their rank / bitonic
+    path when a list holds a NaN)."""
+    from nof import _ops
+    rays = torch.from_numpy(syn.make_rays(64, seed=23))
+    rays[::4, 10] = float("nan")
+    rays[1::4, 11] = float("nan")
+    got = _ops.sample_coarse(rays.to(DEV), 64, 57, 6, 7, 10, 11).cpu()
+    want = O.coarse_z(rays, 64, True, 0.1)
+    np.testing.assert_array_equal(got.numpy(), want.numpy())
+    gen = torch.Generator().manual_seed(4)
+    R_, S, I = 64, 64, 128
+    z = torch.sort(torch.rand(R_, S, generator=gen) * 30, -1)[0]
+    w = torch.rand(R_, S, generator=gen)
+    w[::5, 7] = float("nan")
+    z[2::5, 30] = float("nan")     # a NaN coarse depth: NaN bins and fine samples, NaNs in both merged lists
+    u = torch.sort(torch.rand(R_, I, generator=gen), -1)[0]
+    zf = _ops.resample(z.to(DEV), w.to(DEV), I, u.to(DEV)).cpu()
+    mid = 0.5 * (z[:, 1:] + z[:, :-1])
+    fine = _ops.sample_pdf_standalone(mid.to(DEV), w[:, 1:-1].contiguous().to(DEV), I, False, u.to(DEV)).cpu()
+    np.testing.assert_array_equal(zf.numpy(), torch.sort(torch.cat([z, fine], -1), -1)[0].numpy())
