@@ -1,23 +1,31 @@
-"""Benchmark: LiDAR rays/s (render + loss) at 128 samples/ray on MI355X -- BASELINE.json config 2.
+"""Benchmark: LiDAR rays/s (render + loss) at 128 samples/ray on MI355X -- BASELINE.json config 2 by default.
 
-Default (--mode train_fwd): one step = the reference training step's forward on one batch
-(train_kitti.py:117-155 without backward):
-``render_rays_train`` (train-mode BatchNorm over 262,144-sample chunks, segmented sampling ratio 0.1, child
-free/depth losses, perturb 1, noise_std 0) over 65,536 synthetic rays of one parent block with 32 child AABBs at
-N_samples=128 / N_importance=256 (512 MLP samples per ray), plus the SmoothL1 range losses and the weighted total
-loss.  Inputs are resident in HBM before timing starts.
+Default (--config 2, --mode train_fwd): one step = the reference training step's forward on one batch
+(train_kitti.py:117-155 without backward): ``render_rays_train`` (train-mode BatchNorm over 262,144-sample chunks,
+segmented sampling ratio 0.1, child free/depth losses, perturb 1, noise_std 0) over 65,536 synthetic rays of one
+parent block with 32 child AABBs at N_samples=128 / N_importance=256 (512 MLP samples per ray), plus the SmoothL1
+range losses and the weighted total loss.  Inputs are resident in HBM before timing starts.
 --mode train_step adds what Lightning does with that loss: loss.backward() through the HIP backward kernels and
-the reference's optimizer step (Adam lr 5e-4, eps 1e-8, weight_decay 1e-3 over both networks, nof_utils.py:162-173)
--- the end-to-end training iteration of config 3 on config 2's batch.  --mode val: render_rays_val (eval BN).
---mode view: config 5's two-step coarse-to-fine inference (render_rays_view_0525_2_2, method 2) on 13-column rows
-grouped per LiDAR ray; value counts LiDAR rays (groups), rows_per_gpu the rendered rows.
+the reference's optimizer step (Adam lr 5e-4, eps 1e-8, weight_decay 1e-3 over both networks, nof_utils.py:162-173).
+--mode val: render_rays_val (eval BN).  --mode view: two-step inference (render_rays_view_0525_2_2, method 2) on
+13-column rows grouped per LiDAR ray; value counts LiDAR rays (groups).
 
-Multi-GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``): one process per GPU, each
-rank renders its own parent block (own rays, own NOF weights) -- weak scaling with no collective
-inside the timed region; the only collectives are the barrier around it and the max-over-ranks of the time.
+The other BASELINE configs (--config):
+  3  KITTI-00 training loop: train_step at 262,144 rays/iter and 64/128 samples on the KITTI-00 fixture scene's
+     rays (nof.dataset on tests/golden/kitti_frames.npz, batch drawn with replacement); with N GPUs each rank takes
+     262,144 rays of a data-parallel step and the gradients are averaged over RCCL (nof.blocks.allreduce_grads);
+  4  MaiCity-00 bounds split into 4 parent blocks (own weights, 262,144 rays each, 128/256 samples), train_fwd,
+     blocks dealt over the ranks, every block's depths gathered to rank 0 over RCCL (strong scaling: 1M rays/iter);
+  5  8 parent blocks of two-step rows (view mode, 16,384 ray groups each), gathered to rank 0 (strong scaling).
+
+Multi-GPU: ``python bench.py --gpus N`` (no WORLD_SIZE in the environment) starts
+``python -m torch.distributed.run --nproc-per-node N`` on this same command line before anything touches the GPU
+and relays rank 0's line; under an external torchrun ``--gpus`` must equal WORLD_SIZE.  One process per GPU over
+RCCL; the timed region is bracketed by barriers and the time is the max over ranks.  ``--dry-run`` exercises the
+launcher and the distributed timing on CPU (gloo), with no GPU.
 
 Prints ONE JSON line (rank 0) with the throughput, the dominant kernel's roofline (HIP events over the timed
-region, on the kernels' own stream) and a CPU baseline (the CPU oracle on a bounded sample, rank 0 only).
+region, on the kernels' own stream) and a CPU baseline (the CPU oracle on a bounded sample, rank 0 at N=1 only).
 """
 from __future__ import annotations
 
@@ -25,6 +33,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,30 +47,100 @@ sys.path.insert(0, HERE)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # /opt/skills/guides/MI355X_MICROARCH.md (F32 MFMA = vector peak, no xf32)
 HBM_PEAK_GBS = 8000.0          # same guide (spec)
+MODE_OF_CONFIG = {2: "train_fwd", 3: "train_step", 4: "train_fwd", 5: "view"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2)
+    ap.add_argument("--mode", choices=["train_fwd", "train_step", "val", "view"], default=None,
+                    help="default: the config's workload (2: train_fwd, 3: train_step, 4: train_fwd, 5: view)")
     ap.add_argument("--rays", type=int, default=None,
-                    help="LiDAR rays per GPU (default 65,536; 16,384 ray groups = ~52k two-step rows for --mode view)")
-    ap.add_argument("--samples", type=int, default=128)
-    ap.add_argument("--importance", type=int, default=256)
+                    help="LiDAR rays per block (default 65,536; config 3: 262,144 per GPU; config 4: 262,144; "
+                         "view: 16,384 ray groups = ~52k two-step rows)")
+    ap.add_argument("--samples", type=int, default=None, help="N_samples (default 128; config 3: 64)")
+    ap.add_argument("--importance", type=int, default=None, help="N_importance (default 2 x N_samples)")
     ap.add_argument("--chunk", type=int, default=262144)
-    ap.add_argument("--mode", choices=["train_fwd", "train_step", "val", "view"], default="train_fwd")
     ap.add_argument("--cpu-rays", type=int, default=None,
-                    help="bounded CPU-baseline sample (rays; default 4096, 1024 for train_step)")
+                    help="bounded CPU-baseline sample (rays; default 4096, 1024 for train_step, 512 groups for view)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fold", action="store_true",
                     help="val/view only: the opt-in exact affine fold of the eval network (SURVEY fact 1), reported "
                          "as its own line, never the headline")
     ap.add_argument("--gather", action="store_true",
-                    help="gather every rank's depth_fine to rank 0 inside each step (eval-driver output path)")
-    return ap.parse_args()
+                    help="gather every block's depth_fine to rank 0 inside each step (eval-driver output path; on "
+                         "by default for configs 4 and 5)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / distributed-timing check on CPU (gloo): no GPU, no render")
+    a = ap.parse_args(argv)
+    a.mode = a.mode or MODE_OF_CONFIG[a.config]
+    if a.samples is None:
+        a.samples = 64 if a.config == 3 else 128
+    if a.importance is None:
+        a.importance = 2 * a.samples
+    if a.rays is None:
+        a.rays = 16384 if a.mode == "view" else 262144 if a.config in (3, 4) else 65536
+    if a.config in (4, 5):
+        a.gather = True
+    return a
 
 
+# ----------------------------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int, argv: list) -> int:
+    """One process per GPU: torch.distributed.run as a CHILD process (this process has not touched the GPU and
+    is not replaced); rank 0's JSON line reaches our stdout through the inherited descriptor."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(a, world, rank):
+    """The distributed skeleton of main() on CPU: gloo group, warmup, barrier-bracketed timed steps, max over
+    ranks, rank 0's line -- what the launcher test checks without a GPU."""
+    import torch.distributed as tdist
+    from nof.blocks import blocks_of_rank, max_over_ranks
+    dist = world > 1
+    if dist:
+        tdist.init_process_group("gloo")
+    blocks = blocks_of_rank(rank, world, world if a.config in (2, 3) else {4: 4, 5: 8}[a.config])
+    x = torch.randn(256, 256)
+
+    def step():
+        return (x @ x).sum()
+
+    for _ in range(a.warmup):
+        step()
+    if dist:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tdist.barrier()
+    elapsed = max_over_ranks(elapsed)
+    if rank == 0:
+        print(json.dumps({"metric": "launcher dry run", "value": a.steps / elapsed, "unit": "steps/s",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "dry_run": True,
+                          "rank0_blocks": blocks, "config": {"workload": f"config {a.config} dry run"}}), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------------- profiling
 def prof_read(L, tag):
     t, n, f, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
     rc = L.pcnerf_prof_read(tag, ctypes.byref(t), ctypes.byref(n), ctypes.byref(f), ctypes.byref(b))
@@ -70,21 +150,90 @@ def prof_read(L, tag):
 
 
 def pmc_traffic(kernel_name: str):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary (profiles/), or None."""
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json) and
+    where they come from (profile file + the commit it was measured at), or (None, None)."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d.get(kernel_name, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        return None
+        return None, None
+    v = d.get("kernels", d).get(kernel_name, {})
+    meta = d.get("_meta", {})
+    return v.get("hbm_bytes_per_launch"), ({"file": "profiles/pmc_traffic.json", "head": meta.get("head"),
+                                            "profile": meta.get("profile")} if v else None)
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+# ----------------------------------------------------------------------------------------------- workloads
+def kitti_fixture_rays(dev):
+    """The KITTI-00 fixture scene's train rays (tests/golden/kitti_frames.npz: scans 1151..1156, every 40th point),
+    built on the GPU by nof.dataset exactly as the parity tests build them."""
+    import tempfile
+    from nof import dataset as D
+    from nof import io as nio
+    g = dict(np.load(os.path.join(HERE, "tests", "golden", "kitti_frames.npz"), allow_pickle=False))
+    with tempfile.TemporaryDirectory() as tmp:
+        os.makedirs(os.path.join(tmp, "pcd"))
+        for k, v in g.items():
+            if k.startswith("f"):
+                nio.write_pcd(os.path.join(tmp, "pcd", f"{k[1:]}.pcd"), v)
+        with open(os.path.join(tmp, "poses.txt"), "w") as fh:
+            for _ in range(int(g["pose_first"])):
+                fh.write("1 0 0 0 0 1 0 0 0 0 1 0\n")
+            for row in g["poses"]:
+                fh.write(" ".join(repr(float(v)) for v in row) + "\n")
+        ds = D.kitti_dataload(os.path.join(tmp, "pcd"), split="train", data_start=1150, data_end=1155,
+                              cloud_size_val=64, range_delete_x=3, range_delete_y=2, range_delete_z=1.25,
+                              sub_nerf_test_num=0, surface_expand=0.05, over_height=0.168, over_low=-2.0,
+                              interest_x=20.0, interest_y=20.0, pose_path=os.path.join(tmp, "poses.txt"),
+                              re_loaddata=1, result_path=os.path.join(tmp, "out"), device=dev)
+    return ds.rays
+
+
+def make_blocks(a, rank, world, dev, syn):
+    """This rank's work: a list of parent blocks, each {rays, other, gt, seeds, sub_num}."""
+    from nof.blocks import blocks_of_rank
+    out = []
+    if a.config == 3:
+        scene = kitti_fixture_rays(dev)
+        gen = torch.Generator(device=dev).manual_seed(rank)
+        idx = torch.randint(0, scene.shape[0], (a.rays,), device=dev, generator=gen)
+        rays = scene[idx].contiguous()
+        return [dict(block=0, rays=rays, other=None, gt=rays[:, 14].contiguous(), seeds=(1234, 5678),
+                     sub_num=1171, scene=scene)]
+    n_blocks = {2: world, 4: 4, 5: 8}[a.config]
+    for b in blocks_of_rank(rank, world, n_blocks):
+        seeds = (1234 + b, 5678 + b)
+        if a.mode == "view":
+            vr, vo, vg = syn.make_view_rows(a.rays, n_children=32, seed=1000 * b)
+            out.append(dict(block=b, rays=torch.from_numpy(vr).to(dev), other=torch.from_numpy(vo).to(dev),
+                            gt=torch.from_numpy(vg).to(dev), seeds=seeds, sub_num=32))
+            continue
+        if a.config == 4:
+            lo, hi, origin = syn.block_bounds(b, 4)
+            r = syn.make_rays(a.rays, n_children=256, seed=1000 * b, lo=lo, hi=hi, origin=origin)
+            sub = 256
+        else:
+            r = syn.make_rays(a.rays, n_children=32, seed=1000 * b)
+            sub = 32
+        rays = torch.from_numpy(r).to(dev)
+        out.append(dict(block=b, rays=rays, other=None, gt=rays[:, 14].contiguous(), seeds=seeds, sub_num=sub))
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and a.gpus > 1:
+        sys.exit(launch(a.gpus, argv))
+    world = int(world_env or "1")
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} does not match WORLD_SIZE={world} of the launcher")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_run:
+        return dry_run(a, world, rank)
     dist = world > 1
     if dist:
         import torch.distributed as tdist
@@ -93,45 +242,36 @@ def main():
     dev = torch.device("cuda", local)
 
     from nof import _hip, _ops, synthetic as syn
-    from nof.blocks import blocks_of_rank, gather_rows, max_over_ranks
+    from nof.blocks import allreduce_grads, gather_rows, max_over_ranks
     from nof.criteria import nof_loss
     from nof.networks import Embedding, NOF_coarse, NOF_fine
     from nof.render import render_rays_train, render_rays_val, render_rays_view_0525_2_2
 
-    # this rank's parent block (one per GPU): its own child layout, rays and coarse/fine weights
-    (block,) = blocks_of_rank(rank, world, world)
     view = a.mode == "view"
-    if a.rays is None:
-        a.rays = 16384 if view else 65536
-    if view:   # config 5: two-step rows grouped per ray (group sizes of the reference's KITTI test frames)
-        vr, vo, vg = syn.make_view_rows(a.rays, n_children=32, seed=1000 * block)
-        rays = torch.from_numpy(vr).to(dev)
-        other = torch.from_numpy(vo).to(dev)
-        gt = torch.from_numpy(vg).to(dev)
-    else:
-        rays = torch.from_numpy(syn.make_rays(a.rays, n_children=32, seed=1000 * block)).to(dev)
     train = a.mode in ("train_fwd", "train_step")
     grad = a.mode == "train_step"
     if a.fold:
         if train:
             raise SystemExit("--fold applies to the eval modes (val, view) only")
         _ops.set_eval_fold(True)
-    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234 + block)).to(dev).train(train)
-    mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678 + block)).to(dev).train(train)
+    if grad:   # this caller allocates nothing between forward and backward: let the store take the free HBM
+        _ops.set_activation_store_budget(1 << 62)
+    blocks = make_blocks(a, rank, world, dev, syn)
+    for blk in blocks:
+        blk["mc"] = syn.load_into(NOF_coarse(), syn.init_nof_params(blk["seeds"][0])).to(dev).train(train)
+        blk["mf"] = syn.load_into(NOF_fine(), syn.init_nof_params(blk["seeds"][1])).to(dev).train(train)
     emb = Embedding(3, 10)
     loss_fn = nof_loss["smoothl1"]()
-    if not view:
-        gt = rays[:, 14].contiguous()
     opt = None
     if grad:
-        params = list(mc.parameters()) + list(mf.parameters())
+        params = [p for blk in blocks for m in (blk["mc"], blk["mf"]) for p in m.parameters()]
         opt = torch.optim.Adam(params, lr=5e-4, eps=1e-8, weight_decay=1e-3)   # nof_utils.py:167-169
+    dp = grad and dist and a.config == 3   # one block trained data-parallel: average gradients over ranks
 
-    def step():
-        if grad:
-            opt.zero_grad(set_to_none=True)
+    def block_step(blk):
+        mc, mf, rays, gt = blk["mc"], blk["mf"], blk["rays"], blk["gt"]
         if train:
-            res = render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=32, N_samples=a.samples,
+            res = render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=blk["sub_num"], N_samples=a.samples,
                                     N_importance=a.importance, perturb=1, noise_std=0, chunk=a.chunk,
                                     issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0,
                                     use_child_nerf_loss=1)
@@ -140,22 +280,34 @@ def main():
             loss = (lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"]
                     + 1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"])
         elif view:   # eval_kitti_render.py:1147-1161: two-step inference, effective rows' points kept
-            res = render_rays_view_0525_2_2(mc, mf, emb, rays, other, N_samples=a.samples,
+            res = render_rays_view_0525_2_2(mc, mf, emb, rays, blk["other"], N_samples=a.samples,
                                             N_importance=a.importance, perturb=0, noise_std=0, chunk=a.chunk,
                                             depth_inference_method=2)
             keep = res["rays_effective_flag_fine"].reshape(-1)
-            pts = res["points_inference_fine"][keep]
-            loss = pts.abs().mean()
+            loss = res["points_inference_fine"][keep].abs().mean()
         else:
             res = render_rays_val(mc, mf, emb, rays, N_samples=a.samples, N_importance=a.importance, perturb=0,
                                   noise_std=0, chunk=a.chunk)
             loss = 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
-        if a.gather:
-            gather_rows(res["depth_fine"][:, None], dst=0)
+        return loss, res["depth_fine"]
+
+    def step():
         if grad:
-            loss.backward()
+            opt.zero_grad(set_to_none=True)
+        losses, depths = [], []
+        for blk in blocks:
+            loss, d = block_step(blk)
+            if grad:
+                loss.backward()
+            losses.append(loss.detach().reshape(()))
+            depths.append(d.detach().reshape(-1, 1))
+        if a.gather:   # every block's per-ray depth to rank 0 (RCCL all_gather over xGMI)
+            gather_rows(torch.cat(depths) if depths else torch.zeros((0, 1), device=dev), dst=0)
+        if grad:
+            if dp:
+                allreduce_grads(opt.param_groups[0]["params"])
             opt.step()
-        return loss.detach()
+        return torch.stack(losses).sum() if losses else torch.zeros((), device=dev)
 
     L = _hip.lib()
     with (torch.enable_grad() if grad else torch.no_grad()):
@@ -194,14 +346,16 @@ def main():
                   (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold")):
         tm, n, f, b = prof_read(L, t)
         if n:
+            tr, src = pmc_traffic(knames.get(t, ""))
             kernels[nm] = {"ms_per_step": round(tm, 3), "launches_per_step": n,
                            "avg_us": round(1e3 * tm / n, 2),
                            "TFLOP/s": round(f / (tm * 1e-3) / 1e12, 2) if f else None,
-                           "GB/s": round(b / (tm * 1e-3) / 1e9, 1) if b else None}
+                           "GB/s": round(b / (tm * 1e-3) / 1e9, 1) if b else None,
+                           "hbm_bytes_per_launch_pmc": tr}
     L.pcnerf_prof_enable(0)
     avg_s = ktime_ms * 1e-3 / max(klaunch, 1)
     achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
-    traffic = pmc_traffic(kname)
+    traffic, traffic_src = pmc_traffic(kname)
     if a.fold:   # no MLP left: the query moves 8 B per sample (+ ray rows) and is bound by its sincos (VALU)
         roof = {"kernel": kname, "bound": "hbm", "achieved": round(kbytes / max(klaunch, 1) / avg_s / 1e9, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -212,20 +366,29 @@ def main():
         roof = {"kernel": kname, "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                 "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1)}
+    roof["traffic_source"] = traffic_src
 
     cpu = cdref = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline belongs to the N=1 line only
         if a.cpu_rays is None:
-            a.cpu_rays = 1024 if grad else 512 if view else 4096
-        cpu, ext = cpu_baseline(a, syn)
-        cdref = (cd_vs_ref_view if view else cd_vs_ref)(a, syn, ext, dev)
+            a.cpu_rays = 512 if view else 256 if a.config == 3 else 1024 if grad else 4096
+        sample = blocks[0]
+        cpu, ext = cpu_baseline(a, syn, sample)
+        cdref = (cd_vs_ref_view if view else cd_vs_ref)(a, syn, ext, dev, sample)
 
+    # rays processed per step by the whole job (weak scaling: every rank its own blocks / batch)
+    # (view: LiDAR rays = ray groups, a.rays per block; otherwise the rays of the block's batch)
+    n_local = a.rays * len(blocks) if view else sum(blk["rays"].shape[0] for blk in blocks)
+    n_tot = torch.tensor([float(n_local)], dtype=torch.float64, device=dev)
+    if dist:
+        tdist.all_reduce(n_tot)
+    rays_per_step = float(n_tot)
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
         return
-    rays_total = a.rays * world * a.steps
-    value = rays_total / elapsed
+    value = rays_per_step * a.steps / elapsed
+    scaling = "strong" if a.config in (4, 5) else "weak"
     out = {
         "metric": "LiDAR rays/s (render+loss) at 128 samples/ray; CD vs ref depth",
         "value": round(value, 1),
@@ -235,24 +398,32 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(1e3 * elapsed / a.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": ("synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)"
-                 + ("; ray groups with the group-size histogram of the reference's KITTI test frames" if view
-                    else "")),
+        "data": {2: "synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)",
+                 3: "KITTI-00 fixture scene (scans 1151-1156, every 40th point) rays built by nof.dataset, "
+                    "262,144-ray batches drawn with replacement; seeded NOF weights",
+                 4: "synthetic MaiCity-00 parent blocks (x-split of [-12,61]x[-12,12]x[-2,0.5], 256 child AABBs "
+                    "each); seeded per-block NOF weights",
+                 5: "synthetic two-step rows (group-size histogram of the reference's KITTI test frames), 8 "
+                    "parent blocks; seeded per-block NOF weights"}[a.config]
+                + ("; ray groups with the group-size histogram of the reference's KITTI test frames"
+                   if view and a.config == 2 else ""),
         "config": {"workload": {"train_fwd": "render_rays_train fwd + range/child losses",
                                 "train_step": "render_rays_train fwd + losses + backward + Adam step",
                                 "val": "render_rays_val fwd",
                                 "view": "render_rays_view_0525_2_2 two-step inference (method 2) + effective points"
                                 }[a.mode] + (" -- exact affine fold of the eval network (opt-in)" if a.fold else ""),
-                   "rays_per_gpu": a.rays, "N_samples": a.samples, "N_importance": a.importance,
-                   "rows_per_gpu": int(rays.shape[0]),
+                   "baseline_config": a.config,
+                   "rays_per_step": int(rays_per_step), "rays_per_block": a.rays,
+                   "blocks_rank0": [blk["block"] for blk in blocks],
+                   "N_samples": a.samples, "N_importance": a.importance,
                    "mlp_samples_per_ray": a.samples + a.samples + a.importance, "chunk": a.chunk,
                    "batchnorm": "train (batch stats per chunk)" if train else "eval (folded)",
                    "network": "affine fold (sigmoid(a.e + c))" if a.fold else "9 Linear layers as written",
                    "segmented_ratio": 0.1 if train else None, "perturb": 1 if train else 0,
-                   "parallelism": f"blocks{world}", "gather": bool(a.gather)},
+                   "parallelism": (f"dp{world}" if a.config == 3 else f"blocks{world}"), "gather": bool(a.gather)},
         "roofline": roof,
         "cpu_baseline": cpu,
         "cd_vs_ref": cdref,
@@ -264,19 +435,44 @@ def main():
         tdist.destroy_process_group()
 
 
-def cpu_baseline(a, syn):
+# ----------------------------------------------------------------------------------------------- CPU baseline
+def available_cores() -> int:
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU quota when one is set (a GPU box's
+    share of the host)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _best_of(fn, reps=3):
+    """Warm-up is done by the caller; best wall time of ``reps`` runs (warm-up 1, best of 3)."""
+    best, out = float("inf"), None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = fn()
+        best = min(best, time.perf_counter() - t0)
+    return best, out
+
+
+def cpu_baseline(a, syn, blk):
     """The CPU oracle (oracle/ref_cpu.py, the reference's arithmetic on torch CPU) on a bounded sample of the
-    same workload: ``--cpu-rays`` rays of the same block, same settings, forward + losses (+ backward + Adam in
-    train_step mode).  The RNG draws are generated here and returned with the oracle's depths, so the HIP path can
-    be run on the identical inputs for the "CD vs ref depth" half of the metric."""
+    same workload: ``--cpu-rays`` rays of rank 0's first block, same settings, forward + losses (+ backward + Adam
+    in train_step mode), warm-up + best of 3.  The RNG draws are generated here and returned with the oracle's
+    depths, so the HIP path can be run on the identical inputs for the "CD vs ref depth" half of the metric."""
     from oracle import ref_cpu as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = available_cores()
     torch.set_num_threads(threads)
     if a.mode == "view":
-        return cpu_baseline_view(a, syn, O, threads)
-    rays = torch.from_numpy(syn.make_rays(a.cpu_rays, n_children=32, seed=0))
-    Pc = O.params_from_numpy(syn.init_nof_params(1234))
-    Pf = O.params_from_numpy(syn.init_nof_params(5678))
+        return cpu_baseline_view(a, syn, O, threads, blk)
+    rays = blk["rays"][:a.cpu_rays].cpu()
+    Pc = O.params_from_numpy(syn.init_nof_params(blk["seeds"][0]))
+    Pf = O.params_from_numpy(syn.init_nof_params(blk["seeds"][1]))
     train = a.mode in ("train_fwd", "train_step")
     grad = a.mode == "train_step"
     gen = torch.Generator().manual_seed(7)
@@ -284,6 +480,7 @@ def cpu_baseline(a, syn):
     draws = {"perturb_rand": torch.rand(R, a.samples, generator=gen),
              "u": torch.rand(R, a.importance, generator=gen)} if train else {}
     leaves = []
+    init = {k: v.clone() for P in (Pc, Pf) for k, v in P.items()}
     if grad:
         for P in (Pc, Pf):
             for k in P:
@@ -293,9 +490,10 @@ def cpu_baseline(a, syn):
 
     def run(r, dr, step):
         if train:
-            res = O.render_rays_train(Pc, Pf, r, sub_nerf_test_num=32, N_samples=a.samples, N_importance=a.importance,
-                                      perturb=1, noise_std=0, chunk=a.chunk, issegmentated=1, childnerf_ratio=0.1,
-                                      use_child_nerf_loss=1, training=True, draws=dr)
+            res = O.render_rays_train(Pc, Pf, r, sub_nerf_test_num=blk["sub_num"], N_samples=a.samples,
+                                      N_importance=a.importance, perturb=1, noise_std=0, chunk=a.chunk,
+                                      issegmentated=1, childnerf_ratio=0.1, use_child_nerf_loss=1, training=True,
+                                      draws=dr)
             lr, lrf = O.range_losses(res["depth"], res["depth_fine"], r[:, 14])
             loss = O.total_loss(res, lr, lrf)
             if grad and step:
@@ -308,41 +506,47 @@ def cpu_baseline(a, syn):
 
     with (torch.enable_grad() if grad else torch.no_grad()):
         run(rays[:64], {k: v[:64] for k, v in draws.items()}, False)  # warm-up (no parameter update)
-        t0 = time.perf_counter()
-        res = run(rays, draws, True)
-        dt = time.perf_counter() - t0
+        dt, _ = _best_of(lambda: run(rays, draws, True))
+        # the depths the HIP path is compared with: the oracle's forward from the INITIAL weights
+        for P in (Pc, Pf):
+            for k in P:
+                P[k] = init[k].clone()
+        with torch.no_grad():
+            res = run(rays, draws, False)
     base = {"value": round(a.cpu_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{a.cpu_rays} rays of the same workload ({a.mode}, {a.samples}/{a.importance} samples, "
-                      f"chunk {a.chunk}) through oracle/ref_cpu.py on torch CPU, {dt:.1f} s"}
+            "sample": f"{a.cpu_rays} rays of the same workload (config {a.config} {a.mode}, {a.samples}/"
+                      f"{a.importance} samples, chunk {a.chunk}) through oracle/ref_cpu.py on torch CPU with "
+                      f"{threads} threads (affinity {len(os.sched_getaffinity(0))} CPUs, cgroup quota applied); "
+                      f"warm-up + best of 3 = {dt:.1f} s"}
     return base, {"rays": rays, "draws": draws, "depth_fine": res["depth_fine"].detach()}
 
 
-def cpu_baseline_view(a, syn, O, threads):
+def cpu_baseline_view(a, syn, O, threads, blk):
     """Two-step inference (render.py:614-699 restated in oracle/ref_cpu.py) on ``--cpu-rays`` ray groups."""
-    vr, vo, _ = syn.make_view_rows(a.cpu_rays, n_children=32, seed=0)
+    vr, vo, _ = syn.make_view_rows(a.cpu_rays, n_children=32, seed=1000 * blk["block"])
     rows, other = torch.from_numpy(vr), torch.from_numpy(vo)
-    Pc = O.params_from_numpy(syn.init_nof_params(1234))
-    Pf = O.params_from_numpy(syn.init_nof_params(5678))
+    Pc = O.params_from_numpy(syn.init_nof_params(blk["seeds"][0]))
+    Pf = O.params_from_numpy(syn.init_nof_params(blk["seeds"][1]))
     with torch.no_grad():
         O.render_rays_view(Pc, Pf, rows[:16], torch.zeros(16, dtype=torch.int64), a.samples, a.importance, a.chunk,
                            method=2)   # warm-up
-        t0 = time.perf_counter()
-        res = O.render_rays_view(Pc, Pf, rows, other, a.samples, a.importance, a.chunk, method=2)
-        dt = time.perf_counter() - t0
+        dt, res = _best_of(lambda: O.render_rays_view(Pc, Pf, rows, other, a.samples, a.importance, a.chunk,
+                                                      method=2))
     base = {"value": round(a.cpu_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
             "sample": f"{a.cpu_rays} ray groups ({rows.shape[0]} two-step rows, {a.samples}/{a.importance} samples, "
-                      f"method 2) through oracle/ref_cpu.py on torch CPU, {dt:.1f} s"}
+                      f"method 2) through oracle/ref_cpu.py on torch CPU with {threads} threads; warm-up + best of 3 "
+                      f"= {dt:.1f} s"}
     return base, {"rows": rows, "other": other, "res": res}
 
 
-def cd_vs_ref_view(a, syn, ext, dev):
+def cd_vs_ref_view(a, syn, ext, dev, blk):
     """HIP two-step inference on the CPU sample's rows vs the oracle: effective-row flags must agree; CD / F-score
     of the effective rows' fine points (what eval_kitti_render.py writes to the PCD)."""
     from nof import metrics as NM
     from nof.networks import Embedding, NOF_coarse, NOF_fine
     from nof.render import render_rays_view_0525_2_2
-    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234)).to(dev).eval()
-    mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678)).to(dev).eval()
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(blk["seeds"][0])).to(dev).eval()
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(blk["seeds"][1])).to(dev).eval()
     rows, other, ref = ext["rows"].to(dev), ext["other"].to(dev), ext["res"]
     with torch.no_grad():
         res = render_rays_view_0525_2_2(mc, mf, Embedding(3, 10), rows, other, N_samples=a.samples,
@@ -359,7 +563,7 @@ def cd_vs_ref_view(a, syn, ext, dev):
             "rays": int(rows.shape[0]), "vs": "oracle two-step points of the effective rows (same rows and weights)"}
 
 
-def cd_vs_ref(a, syn, ext, dev):
+def cd_vs_ref(a, syn, ext, dev, blk):
     """The HIP path on the CPU sample's rays and draws (fresh weights of the same seeds) vs the oracle's depths:
     Chamfer distance / F-score (0.2 m) of the rendered points o + d * depth_fine (nof.metrics on the GPU) and the
     largest relative depth error."""
@@ -367,14 +571,14 @@ def cd_vs_ref(a, syn, ext, dev):
     from nof.networks import Embedding, NOF_coarse, NOF_fine
     from nof.render import render_rays_train, render_rays_val
     train = a.mode in ("train_fwd", "train_step")
-    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(1234)).to(dev).train(train)
-    mf = syn.load_into(NOF_fine(), syn.init_nof_params(5678)).to(dev).train(train)
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(blk["seeds"][0])).to(dev).train(train)
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(blk["seeds"][1])).to(dev).train(train)
     rays = ext["rays"].to(dev)
     with torch.no_grad():
         if train:
-            res = render_rays_train(mc, mf, Embedding(3, 10), rays, sub_nerf_test_num=32, N_samples=a.samples,
-                                    N_importance=a.importance, perturb=1, noise_std=0, chunk=a.chunk,
-                                    issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0,
+            res = render_rays_train(mc, mf, Embedding(3, 10), rays, sub_nerf_test_num=blk["sub_num"],
+                                    N_samples=a.samples, N_importance=a.importance, perturb=1, noise_std=0,
+                                    chunk=a.chunk, issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0,
                                     use_child_nerf_loss=1, rng={k: v.to(dev) for k, v in ext["draws"].items()})
         else:
             res = render_rays_val(mc, mf, Embedding(3, 10), rays, N_samples=a.samples, N_importance=a.importance,
@@ -383,8 +587,9 @@ def cd_vs_ref(a, syn, ext, dev):
     p_hip = rays[:, 0:3] + rays[:, 3:6] * d_hip[:, None]
     p_ref = rays[:, 0:3] + rays[:, 3:6] * d_ref[:, None]
     cd, f = NM.eval_pts(p_hip, p_ref, 0.2)
-    rel = float(((d_hip - d_ref).abs() / d_ref.abs().clamp_min(1e-6)).max())
-    return {"cd_m": cd, "fscore": f, "max_rel_depth_err": rel, "rays": int(rays.shape[0]),
+    rel = ((d_hip - d_ref).abs() / d_ref.abs().clamp_min(1e-6)).double()
+    return {"cd_m": cd, "fscore": f, "max_rel_depth_err": float(rel.max()),
+            "frac_rel_err_gt_1e-4": float((rel > 1e-4).double().mean()), "rays": int(rays.shape[0]),
             "vs": "oracle depth_fine on the cpu_baseline sample (same rays, draws and initial weights)"}
 
 

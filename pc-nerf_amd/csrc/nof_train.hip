@@ -547,12 +547,15 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));
     float* hin = keep ? sc.h[0] : ws.bufA;
     float* hout = keep ? sc.h[1] : ws.bufB;
+    // the encoding tiles the skip layer reads back: written by THIS chunk's first-layer launch just below
+    const f32x4* enc_of_chunk = nullptr;
     {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
       hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
                          ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps, hin,
                          stats, (const f32x4*)nullptr, ws.enc);
+      enc_of_chunk = ws.enc;
     }
     for (int L = 1; L < 8; ++L) {
       if (keep) {
@@ -562,10 +565,11 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
       const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], P.bn_rm[L - 1], P.bn_rv[L - 1], P.lin_b[L - 1],
                         stats + 512 * (L - 1)};
       if (L == 4) {
+        PCN_CHECK(enc_of_chunk, "skip layer launched without this chunk's first-layer encoding tiles");
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
         hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
                            c0, ein, hin, n, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
-                           stats + 512 * L, (const f32x4*)ws.enc, (f32x4*)nullptr);
+                           stats + 512 * L, enc_of_chunk, (f32x4*)nullptr);
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
@@ -1327,20 +1331,23 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     for (int L = 0; L < 8; ++L) hh[L] = kept ? sc.h[L] : ws.h[L];
     const double* stats = kept ? sc.stats : ws.stats;
     if (!kept) PCN_HIP(hipMemsetAsync(ws.stats, 0, 8 * 512 * sizeof(double), s));
+    const f32x4* enc_of_chunk = nullptr;   // written by this chunk's recomputed first layer, read by its skip layer
     if (!kept) {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
       hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
                          ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps, ws.h[0],
                          ws.stats, (const f32x4*)nullptr, ws.enc);
+      enc_of_chunk = ws.enc;
     }
     for (int L = 1; L < 8 && !kept; ++L) {
       const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], nullptr, nullptr, P.lin_b[L - 1], ws.stats + 512 * (L - 1)};
       if (L == 4) {
+        PCN_CHECK(enc_of_chunk, "skip layer launched without this chunk's first-layer encoding tiles");
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
         hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
                            c0, ein, ws.h[3], n, ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps, ws.h[4],
-                           ws.stats + 512 * 4, (const f32x4*)ws.enc, (f32x4*)nullptr);
+                           ws.stats + 512 * 4, enc_of_chunk, (f32x4*)nullptr);
       } else {
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
         hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,

@@ -160,26 +160,48 @@ __global__ __launch_bounds__(256) void k_view_rows(const float* __restrict__ P, 
 // pick the first row of the group i..i+other[i] whose smoothed peak lies in its child mask, else the row with
 // the largest child weight sum (strict >, starting from i), i += other[i] + 1; other[i] < 0 -> i += 1.
 // Well-formed batches (every group's inner rows have other == 0, groups disjoint and complete) are processed in
-// parallel -- the walk then visits exactly the rows no group covers; anything else falls back to the literal
-// sequential walk.  One block; also finishes the opacity mean.
-__global__ __launch_bounds__(1024) void k_view_walk(const int64_t* __restrict__ other, int64_t n,
-                                                    const uint8_t* __restrict__ at_peak,
-                                                    const float* __restrict__ wsum, uint8_t* __restrict__ flag,
-                                                    int* __restrict__ covered, const double* __restrict__ opac_row,
-                                                    double n_elems, float* __restrict__ opac_out) {
-  __shared__ int bad;
-  __shared__ double red[16];
-  if (threadIdx.x == 0) bad = 0;
-  __syncthreads();
+// parallel over the grid -- the walk then visits exactly the rows no group covers; anything else falls back to
+// the literal sequential walk.  Three launches (the kernel boundaries order the phases across workgroups):
+//   k_walk_cover  every group head marks its inner rows covered and flags a malformed list; per-block partial
+//                 sums of the opacity terms;
+//   k_walk_pick   (well-formed) every uncovered row: flag it (other == 0) or pick its group's row;
+//   k_walk_finish one thread: the opacity mean from the partials in block order (deterministic), and the
+//                 sequential walk when the list was malformed.
+__device__ __forceinline__ void pick_group(const uint8_t* __restrict__ at_peak, const float* __restrict__ wsum,
+                                           uint8_t* __restrict__ flag, int64_t i, int64_t o) {
+  int64_t pick = i;
+  if (!at_peak[i]) {
+    bool found = false;
+    for (int64_t j = 0; j < o; ++j)
+      if (at_peak[i + j + 1]) {
+        pick = i + j + 1;
+        found = true;
+        break;
+      }
+    if (!found)
+      for (int64_t j = 0; j < o; ++j)
+        if (wsum[i + j + 1] > wsum[pick]) pick = i + j + 1;
+  }
+  flag[pick] = 1;
+}
+
+constexpr int WALK_THREADS = 256;
+
+__global__ __launch_bounds__(WALK_THREADS) void k_walk_cover(const int64_t* __restrict__ other, int64_t n,
+                                                             int* __restrict__ covered, int* __restrict__ bad,
+                                                             const double* __restrict__ opac_row,
+                                                             double* __restrict__ partial) {
+  __shared__ double red[WALK_THREADS / 64];
+  const int64_t i = (int64_t)blockIdx.x * WALK_THREADS + threadIdx.x;
   double os = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    os += opac_row[i];
+  if (i < n) {
+    os = opac_row[i];
     const int64_t o = other[i];
     if (o > 0) {
-      if (i + o >= n) bad = 1;
+      if (i + o >= n) atomicOr(bad, 1);
       for (int64_t j = i + 1; j <= i + o && j < n; ++j) {
-        if (other[j] != 0) bad = 1;
-        if (atomicAdd(&covered[j], 1) != 0) bad = 1;
+        if (other[j] != 0) atomicOr(bad, 1);
+        if (atomicAdd(&covered[j], 1) != 0) atomicOr(bad, 1);
       }
     }
   }
@@ -188,48 +210,46 @@ __global__ __launch_bounds__(1024) void k_view_walk(const int64_t* __restrict__ 
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
-    opac_out[0] = (float)(t / n_elems);
+    for (int w = 0; w < WALK_THREADS / 64; ++w) t += red[w];
+    partial[blockIdx.x] = t;
   }
-  __threadfence_block();
-  __syncthreads();
-  auto pick_group = [&](int64_t i, int64_t o) {
-    int64_t pick = i;
-    if (!at_peak[i]) {
-      bool found = false;
-      for (int64_t j = 0; j < o; ++j)
-        if (at_peak[i + j + 1]) {
-          pick = i + j + 1;
-          found = true;
-          break;
-        }
-      if (!found)
-        for (int64_t j = 0; j < o; ++j)
-          if (wsum[i + j + 1] > wsum[pick]) pick = i + j + 1;
-    }
-    flag[pick] = 1;
-  };
-  if (!bad) {
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      if (covered[i]) continue;
-      const int64_t o = other[i];
-      if (o == 0) flag[i] = 1;
-      else if (o > 0) pick_group(i, o);
-    }
-  } else if (threadIdx.x == 0) {
-    int64_t i = 0;
-    while (i < n) {
-      const int64_t o = other[i];
-      if (o == 0) {
-        flag[i] = 1;
-        i += 1;
-      } else if (o > 0) {
-        if (i + o >= n) break;  // the reference would raise IndexError here
-        pick_group(i, o);
-        i += o + 1;
-      } else {
-        i += 1;
-      }
+}
+
+__global__ __launch_bounds__(WALK_THREADS) void k_walk_pick(const int64_t* __restrict__ other, int64_t n,
+                                                            const int* __restrict__ covered,
+                                                            const int* __restrict__ bad,
+                                                            const uint8_t* __restrict__ at_peak,
+                                                            const float* __restrict__ wsum,
+                                                            uint8_t* __restrict__ flag) {
+  if (*bad) return;
+  const int64_t i = (int64_t)blockIdx.x * WALK_THREADS + threadIdx.x;
+  if (i >= n || covered[i]) return;
+  const int64_t o = other[i];
+  if (o == 0) flag[i] = 1;
+  else if (o > 0) pick_group(at_peak, wsum, flag, i, o);
+}
+
+__global__ void k_walk_finish(const int64_t* __restrict__ other, int64_t n, const int* __restrict__ bad,
+                              const uint8_t* __restrict__ at_peak, const float* __restrict__ wsum,
+                              uint8_t* __restrict__ flag, const double* __restrict__ partial, int nblocks,
+                              double n_elems, float* __restrict__ opac_out) {
+  if (threadIdx.x != 0) return;
+  double t = 0.0;
+  for (int b = 0; b < nblocks; ++b) t += partial[b];
+  opac_out[0] = (float)(t / n_elems);
+  if (!*bad) return;
+  int64_t i = 0;
+  while (i < n) {
+    const int64_t o = other[i];
+    if (o == 0) {
+      flag[i] = 1;
+      i += 1;
+    } else if (o > 0) {
+      if (i + o >= n) break;  // the reference would raise IndexError here
+      pick_group(at_peak, wsum, flag, i, o);
+      i += o + 1;
+    } else {
+      i += 1;
     }
   }
 }
@@ -268,7 +288,13 @@ extern "C" int pcnerf_view_rows(const float* p, const float* z, int64_t n_rows, 
   PCN_API_END
 }
 
-extern "C" size_t pcnerf_view_walk_workspace_bytes(int64_t n_rows) { return (size_t)(n_rows > 0 ? n_rows : 1) * 4; }
+static int64_t walk_blocks(int64_t n) { return (n + WALK_THREADS - 1) / WALK_THREADS; }
+
+// covered[n] (int) | bad (int, padded to 16 B) | per-block opacity partials (double)
+extern "C" size_t pcnerf_view_walk_workspace_bytes(int64_t n_rows) {
+  const int64_t n = n_rows > 0 ? n_rows : 1;
+  return (((size_t)n * 4 + 15) & ~(size_t)15) + 16 + (size_t)walk_blocks(n) * 8;
+}
 
 extern "C" int pcnerf_view_walk(const int64_t* other, int64_t n_rows, const uint8_t* at_peak, const float* child_sum,
                                 const double* opac_row, int n_samples, void* workspace, uint8_t* flags,
@@ -278,10 +304,20 @@ extern "C" int pcnerf_view_walk(const int64_t* other, int64_t n_rows, const uint
             "pcnerf_view_walk: null argument");
   PCN_CHECK(n_rows > 0, "pcnerf_view_walk: empty input");
   hipStream_t s = (hipStream_t)stream;
-  PCN_HIP(hipMemsetAsync(workspace, 0, pcnerf_view_walk_workspace_bytes(n_rows), s));
+  const int64_t nb = walk_blocks(n_rows);
+  PCN_CHECK(nb < (int64_t)1 << 31, "pcnerf_view_walk: too many rows");
+  char* w = (char*)workspace;
+  int* covered = (int*)w;
+  int* bad = (int*)(w + (((size_t)n_rows * 4 + 15) & ~(size_t)15));
+  double* partial = (double*)((char*)bad + 16);
+  PCN_HIP(hipMemsetAsync(workspace, 0, (((size_t)n_rows * 4 + 15) & ~(size_t)15) + 16, s));
   PCN_HIP(hipMemsetAsync(flags, 0, (size_t)n_rows, s));
-  hipLaunchKernelGGL(k_view_walk, dim3(1), dim3(1024), 0, s, other, n_rows, at_peak, child_sum, flags,
-                     (int*)workspace, opac_row, (double)n_rows * n_samples, opacity);
+  hipLaunchKernelGGL(k_walk_cover, dim3((unsigned)nb), dim3(WALK_THREADS), 0, s, other, n_rows, covered, bad, opac_row,
+                     partial);
+  hipLaunchKernelGGL(k_walk_pick, dim3((unsigned)nb), dim3(WALK_THREADS), 0, s, other, n_rows, covered, bad, at_peak,
+                     child_sum, flags);
+  hipLaunchKernelGGL(k_walk_finish, dim3(1), dim3(64), 0, s, other, n_rows, bad, at_peak, child_sum, flags, partial,
+                     (int)nb, (double)n_rows * n_samples, opacity);
   PCN_LAUNCH_CHECK("pcnerf_view_walk");
   PCN_API_END
 }

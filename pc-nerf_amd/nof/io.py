@@ -13,7 +13,10 @@
 """
 from __future__ import annotations
 
+import argparse
+import collections
 import os
+import pickle
 
 import numpy as np
 import torch
@@ -133,9 +136,29 @@ def save_view_rows(dir_: str, rows, other, ranges=None, true_in=None) -> None:
         np.save(os.path.join(dir_, "true_in_all_child.npy"), np.asarray(true_in, dtype=np.float32).reshape(-1, 1))
 
 
+# Non-tensor globals a Lightning checkpoint of the reference can hold besides what torch allows by default:
+# save_hyperparameters(argparse.Namespace) (train_kitti.py:23) and Lightning's AttributeDict (a dict subclass)
+# under its module paths across Lightning versions -- rebuilt as a plain OrderedDict, nothing of Lightning
+# imported or executed.  Each is a data container whose reconstruction runs no code of the file.
+_CKPT_SAFE_GLOBALS = [argparse.Namespace] + [(collections.OrderedDict, n) for n in (
+    "pytorch_lightning.utilities.parsing.AttributeDict", "lightning_fabric.utilities.data.AttributeDict",
+    "lightning.fabric.utilities.data.AttributeDict", "lightning.pytorch.utilities.parsing.AttributeDict")]
+
+
+def load_checkpoint(ckpt_path: str) -> dict:
+    """torch.load(weights_only=True) -- the file never executes anything -- retried with the data-container
+    globals above allowed when the checkpoint carries them (a full Lightning checkpoint: hyper_parameters,
+    optimizer / lr-scheduler states, callbacks, loops)."""
+    try:
+        return torch.load(ckpt_path, map_location="cpu", weights_only=True)
+    except pickle.UnpicklingError:
+        with torch.serialization.safe_globals(_CKPT_SAFE_GLOBALS):
+            return torch.load(ckpt_path, map_location="cpu", weights_only=True)
+
+
 def extract_model_state_dict(ckpt_path: str, model_name: str = "model", prefixes_to_ignore=()):
     """nof_utils.py:176-191: the ``model_name.``-prefixed entries of a (Lightning) checkpoint, prefix removed."""
-    ck = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+    ck = load_checkpoint(ckpt_path)
     if "state_dict" in ck:
         ck = ck["state_dict"]
     out = {}

@@ -419,12 +419,12 @@ def train_outputs(res, rays, mc, mf):
                 loss_total=t(total), running_c=running_stats(mc), running_f=running_stats(mf))
 
 
-def gen_config2_full():
+def gen_config2_full(threads=None, name="config2_full"):
     """BASELINE config 2 at its full size: 65,536 rays of nof.synthetic.make_rays(65536, seed=0) (regenerated from the
     seed by the test; only outputs are stored), 128/256 samples, train-mode BatchNorm over 262,144-sample chunks
     (32 coarse + 96 fine chunks), child losses, segmented sampling 0.1, perturb 0."""
     import time
-    torch.set_num_threads(os.cpu_count() or 1)
+    torch.set_num_threads(threads or os.cpu_count() or 1)
     rays = syn.make_rays(65536, seed=0)
     emb, mc, mf = models(train=True)
     t0 = time.perf_counter()
@@ -432,21 +432,23 @@ def gen_config2_full():
         res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=32, N_samples=128,
                                   N_importance=256, **PCNERF_TRAIN)
     print("config2 full:", time.perf_counter() - t0, "s")
+    save(name, n_rays=65536, seed=0, N_samples=128, N_importance=256, threads=torch.get_num_threads(),
+         **train_outputs(res, rays, mc, mf))
     torch.set_num_threads(1)
-    save("config2_full", n_rays=65536, seed=0, N_samples=128, N_importance=256, **train_outputs(res, rays, mc, mf))
 
 
 def scene_rays():
     return dict(np.load(os.path.join(HERE, "scene_rays.npz"), allow_pickle=False))
 
 
-def gen_config1_kitti():
+def gen_config1_kitti(threads=1, name="config1_kitti"):
     """BASELINE config 1: a 4,096-ray batch of KITTI-00 rays (scene_rays.npz, made by make_scene_rays.py from the
     fixture frames) through render_rays_train at 64/128 samples with the PC-NeRF KITTI shell's settings (one
     262,144-sample coarse chunk, three fine chunks), and the val split through render_rays_val (eval mode)."""
     sc = scene_rays()
     rays = sc["kitti_train"]
     n_child = int(sc["kitti_children"])
+    torch.set_num_threads(threads)
     emb, mc, mf = models(train=True)
     with torch.no_grad():
         res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=n_child, N_samples=64,
@@ -457,15 +459,17 @@ def gen_config1_kitti():
     with torch.no_grad():
         rv = R.render_rays_val(mc, mf, emb, torch.from_numpy(val), N_samples=64, N_importance=128, perturb=0,
                                noise_std=0, chunk=262144)
-    save("config1_kitti", N_samples=64, N_importance=128, sub_nerf_test_num=n_child, **out,
+    save(name, N_samples=64, N_importance=128, sub_nerf_test_num=n_child, threads=threads, **out,
          val_depth=t(rv["depth"]), val_depth_fine=t(rv["depth_fine"]))
+    torch.set_num_threads(1)
 
 
-def gen_config4_maicity():
+def gen_config4_maicity(threads=1, name="config4_maicity"):
     """BASELINE config 4: MaiCity-00 split into 4 parent blocks, each with its own coarse/fine NOF (seeds
     1234+b / 5678+b), up to 1,024 rows per block through render_rays_train at 128/256 samples."""
     sc = scene_rays()
     out = {}
+    torch.set_num_threads(threads)
     for b in range(4):
         rays = sc[f"maicity_b{b}"]
         emb = Embedding(3, 10)
@@ -475,12 +479,24 @@ def gen_config4_maicity():
             res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=int(sc[f"maicity_b{b}_children"]),
                                       N_samples=128, N_importance=256, **PCNERF_TRAIN)
         out.update({f"b{b}_{k}": v for k, v in train_outputs(res, rays, mc, mf).items()})
-    save("config4_maicity", N_samples=128, N_importance=256, **out)
+    save(name, N_samples=128, N_importance=256, threads=threads, **out)
+    torch.set_num_threads(1)
+
+
+def gen_self_spread():
+    """The reference against ITSELF: configs 1, 4 and 2 rerun with another torch thread count (different BLAS
+    blocking, so different float32 rounding; same inputs and weights).  Its fine depths move by up to ~7e-4
+    relative at KITTI ranges (render.py's fine samples sit where the high-frequency encoding turns an ulp of
+    position into ~1e-4 of occupancy), which is the floor any float32 reimplementation's parity sits on; the GPU
+    tests hold the HIP path to that spread (tests/test_configs_gpu.py)."""
+    gen_config1_kitti(threads=8, name="config1_kitti_alt")
+    gen_config4_maicity(threads=8, name="config4_maicity_alt")
+    gen_config2_full(threads=3, name="config2_full_alt")
 
 
 GENERATORS = [gen_maicity_frames, gen_kitti_frames, gen_metrics, gen_grads, gen_aabb, gen_render_rays, gen_nof,
               gen_pdf, gen_val, gen_train, gen_view, gen_pdf_pytest, gen_config1_kitti, gen_config4_maicity,
-              gen_config2_full]
+              gen_config2_full, gen_self_spread]
 
 if __name__ == "__main__":
     # python make_golden.py [name ...]  (names without the gen_ prefix; default: all)

@@ -124,3 +124,24 @@ def test_data_parallel_gradients_world2():
     full = torch.cat([p.grad.reshape(-1) for p in net.parameters()] + [torch.zeros(3)])
     torch.testing.assert_close(res[0][0], full, rtol=1e-5, atol=1e-7)
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.timeout(300)
+def test_bench_launcher_spawns_ranks():
+    """bench.py --gpus 2 with no WORLD_SIZE starts torch.distributed.run itself (child process, nothing touched the
+    GPU) and relays rank 0's line; --dry-run runs the distributed skeleton (gloo barrier, timed steps, max over
+    ranks) without a GPU.  Under an external launcher --gpus must equal WORLD_SIZE."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
+                          "--warmup", "1", "--config", "5"], capture_output=True, text=True, env=env, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout          # rank 0 only
+    assert lines[0]["n_gpus"] == 2 and lines[0]["dry_run"] and lines[0]["rank0_blocks"] == [0, 1, 2, 3]
+    bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--dry-run"],
+                         capture_output=True, text=True, env={**env, "WORLD_SIZE": "2"}, timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

@@ -1,0 +1,113 @@
+"""The distributed path on the GPU box (one MI355X): RCCL initialised for real, and data-parallel HIP gradients.
+
+* ``backend="nccl"`` (RCCL on ROCm) with a single rank: gather_rows / max_over_ranks / allreduce_grads run their
+  collectives on device tensors -- the code path bench.py --gpus N and train_kitti.py take on a node.
+* data parallel over 2 processes sharing the GPU (gloo carries the CUDA tensors: RCCL needs one GPU per rank):
+  each rank renders its shard of one global batch through the HIP kernels (train-mode BatchNorm over its own
+  chunks), backward, nof.blocks.allreduce_grads -- the averaged gradients must equal the mean of the two shards'
+  gradients computed one after the other in a single process (DESIGN (e): per-rank BatchNorm chunks, one
+  all_reduce of a flat bucket).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_rccl_single_rank_collectives():
+    from nof.blocks import allreduce_grads, gather_rows, max_over_ranks
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rows = torch.arange(12, dtype=torch.float32, device="cuda").reshape(6, 2)
+        assert torch.equal(gather_rows(rows, dst=0), rows)
+        assert max_over_ranks(3.5, device=torch.device("cuda", 0)) == 3.5
+        p = torch.nn.Parameter(torch.ones(5, device="cuda"))
+        p.grad = torch.full((5,), 2.0, device="cuda")
+        q = torch.nn.Parameter(torch.ones(3, device="cuda"))   # no gradient: contributes zeros
+        allreduce_grads([p, q])
+        assert torch.equal(p.grad, torch.full((5,), 2.0, device="cuda")) and torch.equal(q.grad, torch.zeros(3,
+                                                                                                         device="cuda"))
+    finally:
+        dist.destroy_process_group()
+
+
+KW = dict(sub_nerf_test_num=32, N_samples=32, N_importance=64, perturb=0, noise_std=0, chunk=4096, issegmentated=1,
+          childnerf_ratio=0.1, use_child_nerf_divide=0, use_child_nerf_loss=1)
+
+
+def _shard_grads(rays, seed_c=1234, seed_f=5678):
+    """Gradients of the train_kitti.py:117-155 loss on one shard, single process."""
+    from nof import synthetic as syn
+    from nof.criteria import nof_loss
+    from nof.networks import Embedding, NOF_coarse, NOF_fine
+    from nof.render import render_rays_train
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(seed_c)).cuda().train()
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(seed_f)).cuda().train()
+    res = render_rays_train(mc, mf, Embedding(3, 10), rays, **KW)
+    sl1 = nof_loss["smoothl1"]()
+    gt = rays[:, 14]
+    loss = (1e-1 * sl1(1e1 * res["depth"], 1e1 * gt) + 1e-1 * sl1(1e1 * res["depth_fine"], 1e1 * gt)
+            + 1e6 * (res["child_free_loss"] + res["child_free_loss_fine"])
+            + 1e5 * (res["child_depth_loss"] + res["child_depth_loss_fine"]))
+    loss.backward()
+    return list(mc.parameters()) + list(mf.parameters())
+
+
+def _dp_rank(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "pc-nerf_amd"), here):
+        sys.path.insert(0, p)
+    from nof import synthetic as syn
+    from nof.blocks import allreduce_grads, shard_batch
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        rays = torch.from_numpy(syn.make_rays(384, seed=41)).cuda()
+        idx = shard_batch(torch.arange(384, device="cuda"), rank, world)
+        params = _shard_grads(rays[idx].contiguous())
+        allreduce_grads(params)
+        q.put((rank, [p.grad.cpu().numpy() for p in params]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_data_parallel_hip_gradients_two_ranks():
+    from nof import synthetic as syn
+    from nof.blocks import shard_batch
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_dp_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, g = q.get(timeout=200)
+        got[r] = g
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    rays = torch.from_numpy(syn.make_rays(384, seed=41)).cuda()
+    shards = [shard_batch(torch.arange(384, device="cuda"), r, 2) for r in range(2)]
+    g0 = [p.grad.cpu().numpy() for p in _shard_grads(rays[shards[0]].contiguous())]
+    g1 = [p.grad.cpu().numpy() for p in _shard_grads(rays[shards[1]].contiguous())]
+    for a, b, x, y in zip(got[0], got[1], g0, g1):
+        np.testing.assert_array_equal(a, b)                       # every rank ends with the same gradients
+        want = (x + y) / 2
+        np.testing.assert_allclose(a, want, rtol=1e-6, atol=1e-6 * max(np.abs(want).max(), 1e-30))

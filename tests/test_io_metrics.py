@@ -109,3 +109,77 @@ def test_lightning_ckpt_roundtrip(tmp_path):
             assert k == k2 and torch.equal(v, v2)
     sd = nio.extract_model_state_dict(p, "nof_coarse", prefixes_to_ignore=["occ_out"])
     assert not any(k.startswith("occ_out") for k in sd) and "layer1.0.weight" in sd
+
+
+def _lightning_like_ckpt(path, mc, mf, hparams_kind):
+    """A checkpoint with the top-level keys and value types a Lightning (1.x/2.x) ModelCheckpoint writes for the
+    reference's NOFSystem (Lightning itself is not importable here): hyper_parameters from save_hyperparameters(
+    argparse.Namespace) -- a Namespace, or Lightning's AttributeDict (a dict subclass living in a Lightning module:
+    emulated by a class registered under that module path while saving) --, Adam + MultiStepLR states (a Counter
+    of milestones), ModelCheckpoint callback state, loops, version."""
+    import argparse
+    import collections
+    import sys
+    import types
+    hp = dict(N_samples=768, N_importance=1536, lr=5e-4, decay_step=[2], use_skip=True, ckpt_path=None,
+              exp_name="kitti00/1151_1200_view")
+    saved_mod = None
+    if hparams_kind == "namespace":
+        hyper = argparse.Namespace(**hp)
+    else:
+        names = ("pytorch_lightning", "pytorch_lightning.utilities", "pytorch_lightning.utilities.parsing")
+        saved_mod = {n: sys.modules.get(n) for n in names}
+        mods = [types.ModuleType(n) for n in names]
+        AttributeDict = type("AttributeDict", (dict,), {"__module__": names[-1]})
+        mods[-1].AttributeDict = AttributeDict
+        mods[0].utilities, mods[1].parsing = mods[1], mods[2]
+        for m in mods:
+            sys.modules[m.__name__] = m
+        hyper = AttributeDict(hp)
+    sd = {f"nof_coarse.{k}": v for k, v in mc.state_dict().items()}
+    sd.update({f"nof_fine.{k}": v for k, v in mf.state_dict().items()})
+    params = list(mc.parameters()) + list(mf.parameters())
+    opt = torch.optim.Adam(params, lr=5e-4, eps=1e-8, weight_decay=1e-3)
+    for p in params:
+        p.grad = torch.ones_like(p)
+    opt.step()
+    sched = torch.optim.lr_scheduler.MultiStepLR(opt, milestones=[5, 120, 256], gamma=0.2)
+    ck = {"epoch": 3, "global_step": 15759, "pytorch-lightning_version": "1.9.0", "state_dict": sd,
+          "loops": {"fit_loop": {"state_dict": {}, "epoch_progress": {"total": {"ready": 4, "completed": 3}}}},
+          "callbacks": {"ModelCheckpoint{'monitor': 'train/loss', 'mode': 'min'}": {
+              "monitor": "train/loss", "best_model_score": torch.tensor(0.42), "best_model_path": "/x/best.ckpt",
+              "best_k_models": {"/x/a.ckpt": torch.tensor(0.5)}, "last_model_path": "/x/last.ckpt"}},
+          "optimizer_states": [opt.state_dict()], "lr_schedulers": [sched.state_dict()],
+          "hparams_name": "hparams", "hyper_parameters": hyper}
+    assert isinstance(ck["lr_schedulers"][0]["milestones"], collections.Counter)
+    try:
+        torch.save(ck, path)
+    finally:
+        if hparams_kind != "namespace":
+            for n, m in saved_mod.items():
+                if m is None:
+                    del sys.modules[n]
+                else:
+                    sys.modules[n] = m
+
+
+@pytest.mark.parametrize("hparams_kind", ["namespace", "attributedict"])
+def test_lightning_full_checkpoint_loads_weights_only(tmp_path, hparams_kind):
+    """load_ckpt on a full Lightning-layout checkpoint: the plain weights_only load refuses the Namespace /
+    AttributeDict globals, the loader retries with those data containers allowed (still weights_only: nothing in
+    the file executes) and reads the nof_coarse. / nof_fine. weights."""
+    import pickle
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(3))
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(4))
+    p = str(tmp_path / "epoch=3.ckpt")
+    _lightning_like_ckpt(p, mc, mf, hparams_kind)
+    with pytest.raises(pickle.UnpicklingError):
+        torch.load(p, map_location="cpu", weights_only=True)
+    a, b = NOF_coarse(), NOF_fine()
+    nio.load_ckpt(a, p, model_name="nof_coarse")
+    nio.load_ckpt(b, p, model_name="nof_fine")
+    for x, y in ((a, mc), (b, mf)):
+        for (k, v), (k2, v2) in zip(x.state_dict().items(), y.state_dict().items()):
+            assert k == k2 and torch.equal(v, v2)
+    ck = nio.load_checkpoint(p)
+    assert ck["hyper_parameters"]["N_samples"] if hparams_kind != "namespace" else ck["hyper_parameters"].N_samples
