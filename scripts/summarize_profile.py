@@ -9,6 +9,7 @@ import csv
 import json
 import os
 import shutil
+import subprocess
 import sys
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
@@ -50,12 +51,23 @@ for r in stats:
     summary[k] = e
 with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as fh:
     json.dump(summary, fh, indent=1)
+# profiles/pmc_traffic.json: HBM bytes per launch of the CURRENT kernels, rebuilt from this round's profiles
+# (kernels of a profile measured at another commit are dropped; bench.py quotes the file and its commit)
 traffic_path = os.path.join(dst, "pmc_traffic.json")
 traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
+head = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip()
+meta = traffic.get("_meta", {})
+kernels = traffic.get("kernels", {}) if meta.get("head") == head else {}
 for k, e in summary.items():
     if "hbm_bytes_per_launch" in e:
-        traffic[k] = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "avg_us": e["avg_us"], "profile": tag}
+        kernels[k] = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "avg_us": e["avg_us"], "profile": tag}
+profs = sorted(set(meta.get("profile", "").split(",")) - {""} | {tag}) if meta.get("head") == head else [tag]
+cmd = open(os.path.join(src, "command.txt")).read().strip() if os.path.exists(os.path.join(src, "command.txt")) else ""
+out = {"_meta": {"head": head, "profile": ",".join(profs), "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                 "(scripts/profile.sh), bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction)",
+                 "commands": {**meta.get("commands", {}), tag: cmd} if meta.get("head") == head else {tag: cmd}},
+       "kernels": kernels}
 with open(traffic_path, "w") as fh:
-    json.dump(traffic, fh, indent=1)
+    json.dump(out, fh, indent=1)
 for k, e in list(summary.items())[:8]:
     print(k, e)
