@@ -480,7 +480,7 @@ def cpu_baseline(a, syn, blk):
     draws = {"perturb_rand": torch.rand(R, a.samples, generator=gen),
              "u": torch.rand(R, a.importance, generator=gen)} if train else {}
     leaves = []
-    init = {k: v.clone() for P in (Pc, Pf) for k, v in P.items()}
+    init = [{k: v.detach().clone() for k, v in P.items()} for P in (Pc, Pf)]
     if grad:
         for P in (Pc, Pf):
             for k in P:
@@ -508,9 +508,9 @@ def cpu_baseline(a, syn, blk):
         run(rays[:64], {k: v[:64] for k, v in draws.items()}, False)  # warm-up (no parameter update)
         dt, _ = _best_of(lambda: run(rays, draws, True))
         # the depths the HIP path is compared with: the oracle's forward from the INITIAL weights
-        for P in (Pc, Pf):
+        for P, P0 in zip((Pc, Pf), init):
             for k in P:
-                P[k] = init[k].clone()
+                P[k] = P0[k].clone()
         with torch.no_grad():
             res = run(rays, draws, False)
     base = {"value": round(a.cpu_rays / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",

@@ -5,7 +5,11 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${1:-r02}
 mkdir -p gpurun_out/bench
-run() { n=$1; shift; timeout -k 10 400 python bench.py "$@" > gpurun_out/bench/${TAG}_$n.json 2> gpurun_out/bench/${TAG}_$n.err; rc=$?;
+if [ -n "$LINES" ]; then   # a subset: LINES="train_fwd val ..."
+  for l in $LINES; do grep -q "^run $l " $0 || { echo "unknown line $l"; exit 2; }; done
+fi
+want() { [ -z "$LINES" ] || [[ " $LINES " == *" $1 "* ]]; }
+run() { n=$1; want $n || return 0; shift; timeout -k 10 400 python bench.py "$@" > gpurun_out/bench/${TAG}_$n.json 2> gpurun_out/bench/${TAG}_$n.err; rc=$?;
         echo "$n rc=$rc"; tail -c 300 gpurun_out/bench/${TAG}_$n.json; echo; return $rc; }
 run train_fwd --steps 20 --warmup 5 &&
 run val --mode val --steps 5 --warmup 2 &&

@@ -7,6 +7,10 @@ export TMPDIR=/tmp
 TAG=${1:-r02}; shift
 OUT=gpurun_out/prof/$TAG
 mkdir -p $OUT
+# heartbeat: PMC passes of a long workload print nothing for minutes
+( while sleep 50; do date +%s >> $OUT/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 echo "python3 bench.py --no-cpu-baseline $*" > $OUT/command.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
   python3 bench.py --no-cpu-baseline "$@" > $OUT/stats_bench.json 2> $OUT/stats.err
