@@ -336,7 +336,8 @@ def main(argv=None):
     # dominant kernel: the MFMA kernel with the most time per step -- the 256 -> 256 pre-BN Linear of train mode
     # (k_train_ws<0,true>: 6 of 9 GEMMs per chunk), or the fused eval query
     knames = {0: "k_nof_eval", 1: "k_train_ws<0,true>", 2: "k_train_ws<8,false>",
-              3: "k_train_ws<8,true>", 10: "k_wgrad", 11: "k_dgrad_ws", 13: "k_nof_eval_fold"}
+              3: "k_train_ws<8,true>", 10: "k_wgrad<0>", 11: "k_dgrad_ws", 13: "k_nof_eval_fold"}
+    pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
     ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)
@@ -346,7 +347,7 @@ def main(argv=None):
                   (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold")):
         tm, n, f, b = prof_read(L, t)
         if n:
-            tr, src = pmc_traffic(knames.get(t, ""))
+            tr, src = pmc_traffic(pmc_names.get(t, ""))
             kernels[nm] = {"ms_per_step": round(tm, 3), "launches_per_step": n,
                            "avg_us": round(1e3 * tm / n, 2),
                            "TFLOP/s": round(f / (tm * 1e-3) / 1e12, 2) if f else None,
