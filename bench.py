@@ -310,64 +310,47 @@ def main(argv=None):
         return torch.stack(losses).sum() if losses else torch.zeros((), device=dev)
 
     L = _hip.lib()
-    with (torch.enable_grad() if grad else torch.no_grad()):
-        for _ in range(a.warmup):
-            loss = step()
-        torch.cuda.synchronize(dev)
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for i in range(a.steps):
-            # per-kernel HIP events (kernel breakdown + roofline) around every launch of the LAST timed step
-            # only: their own cost (two hipEventRecord per launch) then weighs 1/steps on the timed region
-            if i == a.steps - 1:
-                L.pcnerf_prof_enable(1)
-            loss = step()
-        torch.cuda.synchronize(dev)
-        elapsed = time.perf_counter() - t0
-        if dist:
-            tdist.barrier()
-        loss_val = float(loss)
-    if not np.isfinite(loss_val):
-        raise RuntimeError(f"non-finite loss {loss_val}")
-    elapsed = max_over_ranks(elapsed, device=dev)
 
-    # dominant kernel: the MFMA kernel with the most time per step -- the 256 -> 256 pre-BN Linear of train mode
-    # (k_train_ws<0,true>: 6 of 9 GEMMs per chunk), or the fused eval query
-    knames = {0: "k_nof_eval", 1: "k_train_ws<0,true>", 2: "k_train_ws<8,false>",
-              3: "k_train_ws<8,true>", 10: "k_wgrad<0>", 11: "k_dgrad_ws", 13: "k_nof_eval_fold"}
-    pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
-    tag = max(knames, key=lambda t: prof_read(L, t)[0])
-    kname = knames[tag]
-    ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)
-    kernels = {}
-    for t, nm in ((0, "eval_query"), (1, "train_hidden"), (2, "train_first"), (3, "train_skip"), (4, "train_out"),
-                  (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
-                  (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold")):
-        tm, n, f, b = prof_read(L, t)
-        if n:
-            tr, src = pmc_traffic(pmc_names.get(t, ""))
-            kernels[nm] = {"ms_per_step": round(tm, 3), "launches_per_step": n,
-                           "avg_us": round(1e3 * tm / n, 2),
-                           "TFLOP/s": round(f / (tm * 1e-3) / 1e12, 2) if f else None,
-                           "GB/s": round(b / (tm * 1e-3) / 1e9, 1) if b else None,
-                           "hbm_bytes_per_launch_pmc": tr}
-    L.pcnerf_prof_enable(0)
-    avg_s = ktime_ms * 1e-3 / max(klaunch, 1)
-    achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
-    traffic, traffic_src = pmc_traffic(kname)
-    if a.fold:   # no MLP left: the query moves 8 B per sample (+ ray rows) and is bound by its sincos (VALU)
-        roof = {"kernel": kname, "bound": "hbm", "achieved": round(kbytes / max(klaunch, 1) / avg_s / 1e9, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(kbytes / max(klaunch, 1) / avg_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": kbytes / max(klaunch, 1),
-                "note": "VALU-bound (60 sincosf per sample); HBM fraction reported as the contract asks"}
-    else:
-        roof = {"kernel": kname, "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1)}
-    roof["traffic_source"] = traffic_src
+    def timed(steps, warmup):
+        """warmup, barrier, ``steps`` timed steps (HIP events on the last), barrier; max over ranks."""
+        with (torch.enable_grad() if grad else torch.no_grad()):
+            for _ in range(warmup):
+                loss = step()
+            torch.cuda.synchronize(dev)
+            if dist:
+                tdist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for i in range(steps):
+                # per-kernel HIP events (kernel breakdown + roofline) around every launch of the LAST timed step
+                # only: their own cost (two hipEventRecord per launch) then weighs 1/steps on the timed region
+                if i == steps - 1:
+                    L.pcnerf_prof_enable(1)
+                loss = step()
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - t0
+            if dist:
+                tdist.barrier()
+            lv = float(loss)
+        if not np.isfinite(lv):
+            raise RuntimeError(f"non-finite loss {lv}")
+        return max_over_ranks(el, device=dev), lv
+
+    train_math = _ops.get_train_math() if train else None
+    elapsed, loss_val = timed(a.steps, a.warmup)
+    roof, kernels = kernel_report(L, a, train_math)
+
+    # the same workload with the train-mode layers on the fp32 MFMA pipe (train_math "fp32"), for comparison
+    fp32_line = None
+    if train and train_math != "fp32":
+        _ops.set_train_math("fp32")
+        el32, _ = timed(a.steps, 1)
+        roof32, k32 = kernel_report(L, a, "fp32")
+        _ops.set_train_math(train_math)
+        fp32_line = {"value": None, "ms_per_step": round(1e3 * el32 / a.steps, 3), "roofline": roof32,
+                     "kernels": {k: v for k, v in k32.items() if k.startswith("train")},
+                     "note": "the same timed steps with the train-mode Linear layers as fp32 MFMA (v_mfma_f32_32x32x2_f32)"}
+        fp32_elapsed = el32
 
     cpu = cdref = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline belongs to the N=1 line only
@@ -389,6 +372,8 @@ def main(argv=None):
             tdist.destroy_process_group()
         return
     value = rays_per_step * a.steps / elapsed
+    if fp32_line is not None:
+        fp32_line["value"] = round(rays_per_step * a.steps / fp32_elapsed, 1)
     scaling = "strong" if a.config in (4, 5) else "weak"
     out = {
         "metric": "LiDAR rays/s (render+loss) at 128 samples/ray; CD vs ref depth",
@@ -401,7 +386,7 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32",   # every tensor and every accumulation; see train_math for the Linear layers' products
         "data": {2: "synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)",
                  3: "KITTI-00 fixture scene (scans 1151-1156, every 40th point) rays built by nof.dataset, "
                     "262,144-ray batches drawn with replacement; seeded NOF weights",
@@ -426,6 +411,8 @@ def main(argv=None):
                    "segmented_ratio": 0.1 if train else None, "perturb": 1 if train else 0,
                    "parallelism": (f"dp{world}" if a.config == 3 else f"blocks{world}"), "gather": bool(a.gather)},
         "roofline": roof,
+        "train_math": train_math,
+        "fp32_mfma": fp32_line,
         "cpu_baseline": cpu,
         "cd_vs_ref": cdref,
         "loss": loss_val,
@@ -434,6 +421,62 @@ def main(argv=None):
     print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------------- roofline
+FP16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense BF16/FP16 MFMA
+
+
+def kernel_report(L, a, train_math):
+    """Kernel breakdown of the last timed step (library HIP events) and the dominant kernel's roofline."""
+    split = train_math in ("f16x2_3", "f16x2_4")
+    nterm = 3 if train_math == "f16x2_3" else 4
+    hid = f"k_train_h<0,true,{nterm}>" if split else "k_train_ws<0,true>"
+    knames = {0: "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
+              3: f"k_train_h<8,true,{nterm}>" if split else "k_train_ws<8,true>", 10: "k_wgrad<0>",
+              11: "k_dgrad_ws", 13: "k_nof_eval_fold"}
+    pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
+    tag = max(knames, key=lambda t: prof_read(L, t)[0])
+    kname = knames[tag]
+    ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)
+    kernels = {}
+    for t, nm in ((0, "eval_query"), (1, "train_hidden"), (2, "train_first"), (3, "train_skip"), (4, "train_out"),
+                  (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
+                  (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold")):
+        tm, n, f, b = prof_read(L, t)
+        if n:
+            tr, src = pmc_traffic(pmc_names.get(t, ""))
+            kernels[nm] = {"kernel": pmc_names.get(t), "ms_per_step": round(tm, 3), "launches_per_step": n,
+                           "avg_us": round(1e3 * tm / n, 2),
+                           "TFLOP/s": round(f / (tm * 1e-3) / 1e12, 2) if f else None,
+                           "GB/s": round(b / (tm * 1e-3) / 1e9, 1) if b else None,
+                           "hbm_bytes_per_launch_pmc": tr}
+    L.pcnerf_prof_enable(0)
+    avg_s = ktime_ms * 1e-3 / max(klaunch, 1)
+    achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
+    gbs = kbytes / max(klaunch, 1) / avg_s / 1e9
+    traffic, traffic_src = pmc_traffic(kname)
+    if a.fold:   # no MLP left: the query moves 8 B per sample (+ ray rows) and is bound by its sincos (VALU)
+        roof = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": kbytes / max(klaunch, 1),
+                "note": "VALU-bound (60 sincosf per sample); HBM fraction reported as the contract asks"}
+    elif split and tag in (1, 2, 3):
+        # split-fp16 layer: nterm fp16 MFMA products per fp32 product; 1 KiB in + 1 KiB out per sample: the
+        # HBM stream (2 KiB/sample) is the tighter of its two roofs
+        roof = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 2),
+                "algorithmic_bytes_per_launch": kbytes / max(klaunch, 1),
+                "algorithmic_flop_per_launch": kflops / max(klaunch, 1),
+                "mfma_fp16": {"achieved_TFLOPs": round(nterm * achieved, 1), "peak_TFLOPs": FP16_MFMA_PEAK_TFLOPS,
+                              "frac": round(nterm * achieved / FP16_MFMA_PEAK_TFLOPS, 4),
+                              "fp32_equivalent_TFLOPs": round(achieved, 2)}}
+    else:
+        roof = {"kernel": kname, "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1)}
+    roof["traffic_source"] = traffic_src
+    return roof, kernels
 
 
 # ----------------------------------------------------------------------------------------------- CPU baseline

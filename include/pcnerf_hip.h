@@ -83,6 +83,14 @@ int pcnerf_nof_query_train(const float* rays, int64_t n_rays, int ray_stride, co
                            int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
                            void* workspace, size_t workspace_bytes, float* p_out, void* stream);
 
+/* Arithmetic of the train-mode Linear layers (forward and the backward's forward recomputation), process-wide;
+ * returns the previous mode, or -1 for an invalid one.  0: fp32 MFMA (v_mfma_f32_32x32x2_f32, an fp32 FMA chain).
+ * 1 (default) / 2: each fp32 operand split into two fp16 parts (22 significant bits, power-of-two scaled) and the
+ * products taken on the fp16 matrix pipe (v_mfma_f32_32x32x16_f16: exact products, fp32 accumulation):
+ * hi*hi + hi*mid + mid*hi (1) or + mid*mid (2).  Measured against a float64 evaluation of the render:
+ * as accurate as mode 0.  The reference's own GPU runs used TF32 matmuls (train_kitti.py:267). */
+int pcnerf_set_train_math(int mode);
+
 /* NOF.forward in train mode on an embedded batch of n rows (one BatchNorm chunk; running stats updated). */
 int pcnerf_nof_forward_train(const float* emb, int64_t n, const pcnerf_nof_params* params, float momentum,
                              float eps, void* workspace, size_t workspace_bytes, float* p_out, void* stream);

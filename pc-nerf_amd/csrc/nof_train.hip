@@ -404,6 +404,334 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
   CLK_EXIT(1)
 }
 
+// ---- k_train_h<KE, HP>: k_train_ws with the fp32 products taken on the fp16 matrix pipe (opt-in,
+// pcnerf_set_train_math(1)).  Each fp32 operand is split into two fp16 parts, v = hi + mid (hi = fp16(v),
+// mid = fp16(v - hi): 22 significant bits, relative representation error <= 2^-23), and
+// W x = Wh xh + Wh xm + Wm xh (+ Wm xm when NT == 4) on v_mfma_f32_32x32x16_f16: every fp16 x fp16 product is
+// exact in the fp32 accumulator, so the only departures from an fp32 FMA chain are the operands' 2^-23
+// representation error and the dropped term(s) (Wm xm ~ 2^-22 relative, NT == 3).  Power-of-two scales keep
+// the mid parts out of the fp16 subnormal range and the operands below 2^15: the packed weights of layer L carry
+// 2^sw[L] (max |W| 2^sw in [2^14, 2^15)), the staged activations 2^sx with sx chosen per launch from the
+// BatchNorm's own bound |x| <= sqrt(n) |gamma| + |beta| (Samuelson: no sample lies more than sqrt(n-1) standard
+// deviations from its chunk mean); the epilogue multiplies by 2^-(sw+sx) (exact).
+// Same tiles, layouts, statistics and pipeline as k_train_ws; the B operand (the staged tile) lives in LDS as
+// [k-step s][part][lane][8 halves], lane = sample + 32 (G & 1) holding features 16 s + 8 (G & 1) + 0..7 of 16-byte
+// feature group G = 2 s + (G & 1).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int KS_E = 4, KS_H = 16;   // k-steps of 16 features: encoding (64 incl. pad), hidden (256)
+constexpr size_t HW_E = (size_t)KS_E * 8 * 2 * 64;   // f16x8 per encoding part of a layer's image
+constexpr size_t HW_H = (size_t)KS_H * 8 * 2 * 64;
+// layer images in f16x8 units: [k-step][out-block 8][part 2][lane 64]
+__host__ __device__ constexpr size_t off_h(int layer, bool epart) {
+  return layer == 0 ? 0
+       : layer <= 3 ? HW_E + (size_t)(layer - 1) * HW_H
+       : layer == 4 ? (epart ? HW_E + 3 * HW_H : 2 * HW_E + 3 * HW_H)
+                    : 2 * HW_E + (size_t)(layer - 1) * HW_H;
+}
+constexpr size_t TRAIN_H_VECS = 2 * HW_E + 7 * HW_H;
+
+// per-layer weight scale exponents: sw[L] with max|W_L| 2^sw in [2^14, 2^15)
+__global__ __launch_bounds__(256) void k_wscale(NofParamsDev P, int* __restrict__ sw) {
+  const int L = blockIdx.x;
+  const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
+  const float* w = P.lin_w[L];
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < 256 * in_f; i += 256) m = fmaxf(m, fabsf(w[i]));
+  m = wave_max_f(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    sw[L] = m > 0.0f && m == m && m < 3.0e38f ? 14 - ilogbf(m) : 0;
+  }
+}
+
+__global__ void k_pack_train_h(NofParamsDev P, const int* __restrict__ sw, f16x8* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= TRAIN_H_VECS) return;
+  int layer;
+  bool epart;
+  size_t base;
+  if (idx < HW_E) { layer = 0; epart = true; base = 0; }
+  else if (idx < HW_E + 3 * HW_H) { layer = 1 + (int)((idx - HW_E) / HW_H); epart = false; base = off_h(layer, false); }
+  else if (idx < 2 * HW_E + 3 * HW_H) { layer = 4; epart = true; base = off_h(4, true); }
+  else if (idx < 2 * HW_E + 4 * HW_H) { layer = 4; epart = false; base = off_h(4, false); }
+  else { layer = 5 + (int)((idx - (2 * HW_E + 4 * HW_H)) / HW_H); epart = false; base = off_h(layer, false); }
+  const size_t j = idx - base;
+  const int lane = (int)(j & 63), part = (int)((j >> 6) & 1), ob = (int)((j >> 7) & 7), ks = (int)(j >> 10);
+  const int nn = 32 * ob + (lane & 31);
+  const int in_f = layer == 0 ? 63 : layer == 4 ? 319 : 256;
+  const float sc = ldexpf(1.0f, sw[layer]);
+  f16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int f = 16 * ks + 8 * (lane >> 5) + e;
+    int col;
+    if (epart) col = f < 63 ? f : -1;
+    else col = (layer == 4 ? 63 : 0) + f;
+    const float w = col < 0 ? 0.0f : P.lin_w[layer][(size_t)nn * in_f + col] * sc;
+    const _Float16 hi = (_Float16)w;
+    v[e] = part == 0 ? hi : (_Float16)(w - (float)hi);
+  }
+  out[idx] = v;
+}
+
+// hi / mid halves of 4 scaled fp32 values
+__device__ __forceinline__ void split4(const f32x4& x, f16x4& hi, f16x4& mid) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const _Float16 a = (_Float16)x[q];
+    hi[q] = a;
+    mid[q] = (_Float16)(x[q] - (float)a);
+  }
+}
+
+template <int KE, bool HP, int NT>
+__global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ rays, int stride,
+                                                    const float* __restrict__ z, int S, int64_t c0,
+                                                    const float* __restrict__ ein, const float* __restrict__ hin,
+                                                    int64_t n, const f16x8* __restrict__ Wp, const int* __restrict__ swp,
+                                                    int layer, const float* __restrict__ bias, BnPrev prev,
+                                                    float momentum, float eps, float* __restrict__ hout,
+                                                    double* __restrict__ stats, const f32x4* __restrict__ etin,
+                                                    f32x4* __restrict__ etout) {
+  constexpr bool ETIN = KE && HP, ETOUT = KE && !HP;
+  constexpr int KSE = KE ? KS_E : 0;               // encoding k-steps
+  constexpr int KS = KSE + (HP ? KS_H : 0);        // k-steps of 16 features
+  constexpr int XD = 3;                            // LDS read ring depth in k-steps
+  constexpr int S_LOAD = 2, S_STAGE0 = KS - 4, S_STAGE1 = KS - 3;   // HP: next tile's loads / staging
+  __shared__ __attribute__((aligned(16))) float al[256];
+  __shared__ __attribute__((aligned(16))) float be[256];
+  __shared__ __attribute__((aligned(16))) float bs[256];
+  __shared__ float smax[8];
+  __shared__ f16x8 xs[2][KS][2][64];
+  __shared__ f32x4 sred[8 * 64 * 8];   // per-lane running statistics, as k_train_ws
+  const int t = threadIdx.x;
+  if (t < 256) {
+    if (HP) bn_coeffs(prev, n, momentum, eps, al, be);
+    bs[t] = bias[t];
+  }
+  // activation scale 2^sx: the largest power of two keeping sqrt(n) |gamma| + |beta| below 2^15 (never above
+  // 2^0 for the skip layer, whose encoding part is not scaled)
+  int sx = 0;
+  if (HP) {
+    float bnd = 0.0f;
+    if (t < 256) bnd = sqrtf((float)n) * fabsf(prev.gamma[t]) + fabsf(prev.beta[t]);
+    bnd = wave_max_f(bnd);
+    if ((t & 63) == 0) smax[t >> 6] = bnd;
+    __syncthreads();
+    float m = smax[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) m = fmaxf(m, smax[i]);
+    sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
+    if (KE && sx > 0) sx = 0;
+    sx = sx > 24 ? 24 : sx;
+  }
+  const float xscale = ldexpf(1.0f, sx);
+  const float unscale = ldexpf(1.0f, -(swp[layer] + sx));
+  const int nt = (int)((n + 31) / 32);
+  const int gstride = (int)gridDim.x;
+  const int lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
+  f16x8 wr[KS][2];
+  {
+    const f16x8* __restrict__ w8 = Wp + lane;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 8 + blk) * 2 + p) * 64];
+  }
+  f32x4* const my_st = sred + (blk * 64 + lane) * 8;
+  const int st_sw = (lane >> 1) & 7;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) my_st[c] = f32x4{};
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);
+  int buf = 0;
+  // staging: thread t owns the activation float4s t + 512 m (m = 0..3) of a tile: feature group G = KE + (t >> 6)
+  // + 8 m, lane t & 63 (sample li, half h) -> LDS [s = G >> 1][part][li + 32 (G & 1)][4 h .. 4 h + 3]
+  auto put = [&](int b, int G, const f32x4& x) {
+    f16x4 hi, mid;
+    split4(x, hi, mid);
+    const int s = G >> 1, ln = li + 32 * (G & 1);
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][s][0][ln]) + 4 * h) = hi;
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][s][1][ln]) + 4 * h) = mid;
+  };
+  auto stage = [&](int b, const f32x4 (&v)[4], int m) {
+    const int g = (t >> 6) + 8 * m;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
+    const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
+    f32x4 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = (v[m][q] * a[q] + c[q]) * xscale;
+    put(b, KE + g, x);
+  };
+  auto put_enc = [&](int b, const f32x4& e) {   // encoding group t >> 6 (not scaled: sx <= 0 -> x 2^sx only if < 1)
+    f32x4 x = e;
+    if (sx != 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] *= xscale;
+    }
+    put(b, t >> 6, x);
+  };
+  auto sample_of = [&](int tile) {
+    int64_t sl = (int64_t)tile * 32 + li;
+    if (sl >= n) sl = n - 1;
+    return c0 + sl;
+  };
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  if (tl < nt) {
+    if (HP) {
+      f32x4 v[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)tl * TILE_FLOATS + (size_t)m * 2048)[t];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) stage(0, v, m);
+    }
+    if (KE) {
+      const int64_t gs = sample_of(tl);
+      f32x4 e;
+      if (ETIN) {
+        e = etin[(size_t)tl * 512 + t];
+      } else if (ein) {
+        e = enc_feats_row(ein + gs * 63, h, t >> 6);
+      } else {
+        float p[3];
+        sample_point(rays + (gs / S) * stride, z[gs], p);
+        e = enc_feats(p, h, t >> 6);
+      }
+      put_enc(0, e);
+      if (ETOUT) etout[(size_t)tl * 512 + t] = e;
+    }
+  }
+  __syncthreads();
+  auto epi = [&](const f32x16& pacc, int ptile, int j) {
+    const bool valid = (int64_t)ptile * 32 + li < n;
+    const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
+    f32x4 s1 = my_st[(2 * j) ^ st_sw], s2 = my_st[(2 * j + 1) ^ st_sw];
+    f32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float d = pacc[4 * j + q] * unscale;
+      o[q] = d + bj[q];
+      const float dv = valid ? d : 0.0f;
+      s1[q] += dv;
+      s2[q] += dv * dv;
+    }
+    my_st[(2 * j) ^ st_sw] = s1;
+    my_st[(2 * j + 1) ^ st_sw] = s2;
+    float* base = hout + (size_t)ptile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
+    reinterpret_cast<f32x4*>(base)[lane] = o;
+  };
+  auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tile + gstride);
+    const bool more = nxt < nt;
+    f16x8 xr[XD][2];
+    f32x4 v[4];
+    float rr[7];
+    f32x4 ev;
+#pragma unroll
+    for (int d = 0; d < XD - 1; ++d) {
+      xr[d][0] = xs[buf][d][0][lane];
+      xr[d][1] = xs[buf][d][1][lane];
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + XD - 1 < KS) {
+        xr[(ks + XD - 1) % XD][0] = xs[buf][ks + XD - 1][0][lane];
+        xr[(ks + XD - 1) % XD][1] = xs[buf][ks + XD - 1][1][lane];
+      }
+      const f16x8 xh = xr[ks % XD][0], xm = xr[ks % XD][1];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xh, ks == 0 ? f32x16{} : acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
+      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
+      if (ETIN && ks == KS - 4 && more) ev = etin[(size_t)nxt * 512 + t];
+      if (ETOUT && ks == 0 && more && !ein) {
+        const int64_t gs = sample_of(nxt);
+        const float* r = rays + (gs / S) * stride;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) rr[c] = r[c];
+        rr[6] = z[gs];
+      }
+      if (ks == 1 && ptile >= 0) {
+        epi(pacc, ptile, 0);
+        epi(pacc, ptile, 1);
+      }
+      if (ks == 2 && ptile >= 0) {
+        epi(pacc, ptile, 2);
+        epi(pacc, ptile, 3);
+      }
+      if (HP && ks == S_LOAD && more) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)nxt * TILE_FLOATS + (size_t)m * 2048)[t];
+      }
+      if (HP && ks == S_STAGE0 && more) {
+        stage(buf ^ 1, v, 0);
+        stage(buf ^ 1, v, 1);
+      }
+      if (HP && ks == S_STAGE1 && more) {
+        stage(buf ^ 1, v, 2);
+        stage(buf ^ 1, v, 3);
+      }
+      if (KE && ks == KS - 1 && more) {
+        f32x4 e;
+        if (ETIN) {
+          e = ev;
+        } else if (ein) {
+          e = enc_feats_row(ein + sample_of(nxt) * 63, h, t >> 6);
+        } else {
+          float p[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) p[c] = rr[c] + rr[3 + c] * rr[6];
+          e = enc_feats(p, h, t >> 6);
+        }
+        put_enc(buf ^ 1, e);
+        if (ETOUT) etout[(size_t)nxt * 512 + t] = e;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    buf ^= 1;
+  };
+  f32x16 accA, accB;
+  int ptile = -1;
+  while (tl < nt) {
+    body(accA, accB, tl, ptile);
+    ptile = tl;
+    tl = __builtin_amdgcn_readfirstlane(tl + gstride);
+    if (tl >= nt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epi(accA, ptile, j);
+      break;
+    }
+    body(accB, accA, tl, ptile);
+    ptile = tl;
+    tl = __builtin_amdgcn_readfirstlane(tl + gstride);
+    if (tl >= nt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epi(accB, ptile, j);
+    }
+  }
+  __syncthreads();
+  {
+    const int nn = t >> 1, mo = t & 1, ib = nn & 31, wb = nn >> 5;
+    const int hh = (ib >> 2) & 1, jj = ib >> 3, qq = ib & 3;
+    double a = 0.0;
+#pragma unroll 8
+    for (int l = 0; l < 32; ++l) {
+      const int ln = 32 * hh + l;
+      a += (double)sred[(wb * 64 + ln) * 8 + ((2 * jj + mo) ^ ((ln >> 1) & 7))][qq];
+    }
+    atomicAdd(&stats[t], a);
+  }
+}
+
 // occ_out on BatchNorm 8 (applied on load) + sigmoid; one wave per 32-sample tile.
 __global__ __launch_bounds__(256) void k_train_out(const float* __restrict__ hin, int64_t n, BnPrev prev,
                                                    float momentum, float eps, const float* __restrict__ wout,
@@ -438,9 +766,16 @@ struct TrainWs {
   float* bufB;
   f32x4* enc;   // the chunk's encoding tiles: written by the first layer, read by the skip layer
   float* wp;
+  f16x8* wh;    // split-fp16 weight image (train math 1/2)
+  int* sw;      // its per-layer scale exponents
   double* stats;
   size_t bytes;
 };
+
+// Train-mode MLP arithmetic: 0 = fp32 MFMA, 1 = split fp16 with 3 products (default), 2 = split fp16 with 4
+// products (k_train_h).  Process-wide; pcnerf_set_train_math.  Mode 1 renders config 2 within 1.9e-5 of a float64
+// evaluation of the same rays (fp32 MFMA: 2.2e-5; the reference itself: 1.1e-4) at 1.9x the speed.
+static int g_train_math = 1;
 
 static TrainWs carve(void* base, int64_t chunk) {
   const size_t tiles = (size_t)((chunk + 31) / 32);
@@ -453,12 +788,15 @@ static TrainWs carve(void* base, int64_t chunk) {
   const size_t oA = take(tiles * TILE_FLOATS * 4), oB = take(tiles * TILE_FLOATS * 4);
   const size_t oE = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
+  const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
   char* b = (char*)base;
   TrainWs w;
   w.bufA = (float*)(b + oA);
   w.bufB = (float*)(b + oB);
   w.enc = (f32x4*)(b + oE);
   w.wp = (float*)(b + ow);
+  w.wh = (f16x8*)(b + owh);
+  w.sw = (int*)(b + osw);
   w.stats = (double*)(b + ost);
   w.bytes = off;
   return w;
@@ -469,6 +807,60 @@ static TrainWs carve(void* base, int64_t chunk) {
 using namespace pcn;
 
 extern "C" size_t pcnerf_nof_train_workspace_bytes(int64_t chunk) { return carve(nullptr, chunk).bytes; }
+
+extern "C" int pcnerf_set_train_math(int mode) {
+  if (mode < 0 || mode > 2) {
+    pcn::set_error("pcnerf_set_train_math: mode must be 0 (fp32 MFMA), 1 or 2 (split fp16, 3 / 4 products)");
+    return -1;
+  }
+  const int prev = pcn::g_train_math;
+  pcn::g_train_math = mode;
+  return prev;
+}
+
+// The train-mode layer launches of one chunk under the selected arithmetic (layer 0: KE_FIRST, hidden, skip).
+namespace pcn {
+struct TrainLayerLaunch {
+  const float* rays;
+  int stride;
+  const float* z;
+  int S;
+  int64_t c0;
+  const float* ein;
+  int64_t n;
+  unsigned gws;
+  float mom, eps;
+  hipStream_t s;
+};
+
+template <int KE, bool HP>
+static void launch_layer(const TrainLayerLaunch& q, const NofParamsDev& P, const float* wp, const f16x8* wh,
+                         const int* sw, int L, const float* hin, const BnPrev& prev, float* hout, double* stats,
+                         const f32x4* etin, f32x4* etout) {
+  const int m = g_train_math;
+  if (m == 0) {
+    hipLaunchKernelGGL((k_train_ws<KE, HP>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0, q.ein,
+                       hin, q.n, wp + off_w(L, KE != 0), P.lin_b[L], prev, q.mom, q.eps, hout, stats, etin, etout);
+  } else if (m == 1) {
+    hipLaunchKernelGGL((k_train_h<KE, HP, 3>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0,
+                       q.ein, hin, q.n, wh + off_h(L, KE != 0), sw, L, P.lin_b[L], prev, q.mom, q.eps, hout, stats,
+                       etin, etout);
+  } else {
+    hipLaunchKernelGGL((k_train_h<KE, HP, 4>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0,
+                       q.ein, hin, q.n, wh + off_h(L, KE != 0), sw, L, P.lin_b[L], prev, q.mom, q.eps, hout, stats,
+                       etin, etout);
+  }
+}
+
+static void pack_weights(const NofParamsDev& P, float* wp, f16x8* wh, int* sw, hipStream_t s) {
+  if (g_train_math == 0) {
+    hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, wp);
+  } else {
+    hipLaunchKernelGGL(k_wscale, dim3(8), dim3(256), 0, s, P, sw);
+    hipLaunchKernelGGL(k_pack_train_h, dim3((unsigned)((TRAIN_H_VECS + 255) / 256)), dim3(256), 0, s, P, sw, wh);
+  }
+}
+}  // namespace pcn
 
 #if PCN_CLOCK_STAMP
 // diagnostic builds: median over workgroups of the last hidden-layer launch's in-kernel clock (MHz) and cycles
@@ -533,7 +925,7 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
   // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wp);
+  pack_weights(P, ws.wp, ws.wh, ws.sw, s);
   for (int64_t c0 = 0; c0 < total; c0 += chunk) {
     const int64_t n = total - c0 < chunk ? total - c0 : chunk;
     const int64_t ntiles = (n + 31) / 32;
@@ -552,9 +944,8 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
-      hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
-                         ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, momentum, eps, hin,
-                         stats, (const f32x4*)nullptr, ws.enc);
+      const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};
+      launch_layer<KG_E, false>(q, P, ws.wp, ws.wh, ws.sw, 0, nullptr, none, hin, stats, nullptr, ws.enc);
       enc_of_chunk = ws.enc;
     }
     for (int L = 1; L < 8; ++L) {
@@ -567,15 +958,14 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
       if (L == 4) {
         PCN_CHECK(enc_of_chunk, "skip layer launched without this chunk's first-layer encoding tiles");
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
-        hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
-                           c0, ein, hin, n, ws.wp + off_w(4, true), P.lin_b[L], prev, momentum, eps, hout,
-                           stats + 512 * L, enc_of_chunk, (f32x4*)nullptr);
+        const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};
+        launch_layer<KG_E, true>(q, P, ws.wp, ws.wh, ws.sw, 4, hin, prev, hout, stats + 512 * L, enc_of_chunk,
+                                 nullptr);
       } else {
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
-                           ein, hin, n, ws.wp + off_w(L, false), P.lin_b[L], prev, momentum, eps, hout,
-                           stats + 512 * L, (const f32x4*)nullptr, (f32x4*)nullptr);
+        const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};
+        launch_layer<0, true>(q, P, ws.wp, ws.wh, ws.sw, L, hin, prev, hout, stats + 512 * L, nullptr, nullptr);
       }
       float* t = hin;
       hin = hout;
@@ -1248,6 +1638,8 @@ struct BwdWs {
   double* ostat;
   double* gacc;
   f32x4* enc;   // encoding tiles of a recomputed chunk (first layer -> skip layer)
+  f16x8* wh;    // split-fp16 weight image for recomputation under train math 1/2
+  int* sw;
   size_t bytes;
 };
 
@@ -1266,8 +1658,11 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
   const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257) * 8), oa = take((size_t)gacc_layout().total * 8);
+  const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
   char* b = (char*)base;
   BwdWs w;
+  w.wh = (f16x8*)(b + owh);
+  w.sw = (int*)(b + osw);
   for (int L = 0; L < 8; ++L) w.h[L] = (float*)(b + oh[L]);
   for (int i = 0; i < 2; ++i) w.g[i] = (float*)(b + og[i]);
   w.wp = (float*)(b + ow);
@@ -1313,6 +1708,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   const GaccLayout G = gacc_layout();
   hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wp);
+  if (g_train_math != 0) pack_weights(P, nullptr, ws.wh, ws.sw, s);   // the forward's arithmetic for recomputation
   hipLaunchKernelGGL(k_pack_dgrad, dim3((unsigned)((DGRAD_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wt);
   PCN_HIP(hipMemsetAsync(ws.gacc, 0, (size_t)G.total * 8, s));
   const float mom = 0.0f;  // unused: the recomputation passes no running stats
@@ -1335,9 +1731,8 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     if (!kept) {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
-      hipLaunchKernelGGL((k_train_ws<KG_E, false>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
-                         ein, (const float*)nullptr, n, ws.wp + off_w(0, true), P.lin_b[0], none, mom, eps, ws.h[0],
-                         ws.stats, (const f32x4*)nullptr, ws.enc);
+      const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, mom, eps, s};
+      launch_layer<KG_E, false>(q, P, ws.wp, ws.wh, ws.sw, 0, nullptr, none, ws.h[0], ws.stats, nullptr, ws.enc);
       enc_of_chunk = ws.enc;
     }
     for (int L = 1; L < 8 && !kept; ++L) {
@@ -1345,14 +1740,14 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       if (L == 4) {
         PCN_CHECK(enc_of_chunk, "skip layer launched without this chunk's first-layer encoding tiles");
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
-        hipLaunchKernelGGL((k_train_ws<KG_E, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples,
-                           c0, ein, ws.h[3], n, ws.wp + off_w(4, true), P.lin_b[4], prev, mom, eps, ws.h[4],
-                           ws.stats + 512 * 4, enc_of_chunk, (f32x4*)nullptr);
+        const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, mom, eps, s};
+        launch_layer<KG_E, true>(q, P, ws.wp, ws.wh, ws.sw, 4, ws.h[3], prev, ws.h[4], ws.stats + 512 * 4,
+                                 enc_of_chunk, nullptr);
       } else {
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
-        hipLaunchKernelGGL((k_train_ws<0, true>), dim3(gws), dim3(512), 0, s, rays, ray_stride, z, n_samples, c0,
-                           ein, ws.h[L - 1], n, ws.wp + off_w(L, false), P.lin_b[L], prev, mom, eps, ws.h[L],
-                           ws.stats + 512 * L, (const f32x4*)nullptr, (f32x4*)nullptr);
+        const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, mom, eps, s};
+        launch_layer<0, true>(q, P, ws.wp, ws.wh, ws.sw, L, ws.h[L - 1], prev, ws.h[L], ws.stats + 512 * L, nullptr,
+                              nullptr);
       }
     }
     {

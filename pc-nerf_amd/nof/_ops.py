@@ -111,6 +111,32 @@ def fold_eval(model, device) -> torch.Tensor:
     return out
 
 
+# Arithmetic of the train-mode Linear layers (pcnerf_set_train_math): fp32 operands split into two fp16 parts
+# (22 significant bits) with exact products on the fp16 matrix pipe and fp32 accumulation, "f16x2_3" (default:
+# hi*hi + hi*mid + mid*hi) or "f16x2_4" (+ mid*mid), or "fp32" (fp32 MFMA).
+TRAIN_MATH = {"fp32": 0, "f16x2_3": 1, "f16x2_4": 2}
+
+
+def set_train_math(mode: str) -> str:
+    """Select the train-mode layer arithmetic; returns the previous mode's name."""
+    if mode not in TRAIN_MATH:
+        raise ValueError(f"train math must be one of {sorted(TRAIN_MATH)}")
+    prev = H.lib().pcnerf_set_train_math(TRAIN_MATH[mode])
+    if prev < 0:
+        raise RuntimeError(H.lib().pcnerf_last_error().decode())
+    return {v: k for k, v in TRAIN_MATH.items()}[prev]
+
+
+def get_train_math() -> str:
+    prev = set_train_math("fp32")
+    set_train_math(prev)
+    return prev
+
+
+if os.environ.get("PCNERF_TRAIN_MATH"):
+    set_train_math(os.environ["PCNERF_TRAIN_MATH"])
+
+
 def _track_batches(model, n_chunks: int) -> None:
     for bn in model.norms():
         if bn.num_batches_tracked is not None:

@@ -58,8 +58,16 @@ def named(m):
     return dict(m.named_parameters())
 
 
+@pytest.fixture(params=["f16x2_3", "fp32"])
+def train_math(request):
+    from nof import _ops
+    prev = _ops.set_train_math(request.param)
+    yield request.param
+    _ops.set_train_math(prev)
+
+
 @pytest.mark.parametrize("name", ["pcnerf", "divide", "original"])
-def test_train_grads_vs_reference(name):
+def test_train_grads_vs_reference(name, train_math):
     g = golden(f"grads_{name}")
     emb, mc, mf = models()
     rays = torch.from_numpy(g["rays"]).to(DEV)
@@ -103,7 +111,7 @@ def oracle_summary(P, seed):
 
 @pytest.mark.parametrize("divide,noise_std,store", [(0, 0.0, "all"), (1, 1e-3, "all"), (0, 0.0, "part"),
                                                      (1, 1e-3, "none")])
-def test_train_grads_vs_oracle_ragged_chunks_with_draws(divide, noise_std, store, monkeypatch):
+def test_train_grads_vs_oracle_ragged_chunks_with_draws(divide, noise_std, store, monkeypatch, train_math):
     """512 rays, 64 + 128 samples, chunk 30000 (the fine pass's last chunk is 8304 samples: a padded tail tile),
     stratified perturbation and importance draws (the reference's training runs perturb=1, noise_std=0,
     logs/*/hparams.yaml) plus a small weight noise, injected identically into both paths.  (Noise of the order

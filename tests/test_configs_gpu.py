@@ -137,7 +137,16 @@ def check_train(res, g, rays, mc, mf, pre="", name="", f64=None, alt=None):
 
 
 # ----------------------------------------------------------------------------------------------- config 2
-def test_config2_full_size_vs_reference():
+@pytest.fixture(params=["f16x2_3", "fp32"])
+def train_math(request):
+    """The train-mode layer arithmetic (nof._ops.set_train_math): the default split-fp16 products and fp32 MFMA."""
+    from nof import _ops
+    prev = _ops.set_train_math(request.param)
+    yield request.param
+    _ops.set_train_math(prev)
+
+
+def test_config2_full_size_vs_reference(train_math):
     """65,536 rays x (128 + 384) MLP samples in train-mode BatchNorm chunks of 262,144, vs the reference."""
     g = golden("config2_full")
     rays = torch.from_numpy(syn.make_rays(int(g["n_rays"]), n_children=32, seed=int(g["seed"]))).to(DEV)
@@ -148,7 +157,7 @@ def test_config2_full_size_vs_reference():
     dump = os.environ.get("PCNERF_PARITY_DUMP")
     if dump:   # the HIP depths, for offline analysis against the reference / a float64 evaluation
         np.savez_compressed(dump, depth=res["depth"].cpu().numpy(), depth_fine=res["depth_fine"].cpu().numpy())
-    check_train(res, g, rays, mc, mf, name="config2_full", f64=golden("config2_full_f64"),
+    check_train(res, g, rays, mc, mf, name=f"config2_full_{train_math}", f64=golden("config2_full_f64"),
                 alt=golden("config2_full_alt"))
     assert int(mc.norms()[0].num_batches_tracked) == 32 and int(mf.norms()[0].num_batches_tracked) == 96
 
@@ -165,7 +174,7 @@ def kitti_scene(tmp_path):
     return D.kitti_dataload(root, split="train", **kw), D.kitti_dataload(root, split="val", **kw)
 
 
-def test_config1_kitti_rays_train_and_val(tmp_path):
+def test_config1_kitti_rays_train_and_val(tmp_path, train_math):
     """KITTI-00 rows built on the GPU (nof.dataset) == the fixture's rows; a 4,096-ray batch through
     render_rays_train (64/128, PC-NeRF KITTI settings) and the val split through render_rays_val."""
     sc, g = golden("scene_rays"), golden("config1_kitti")
@@ -178,7 +187,7 @@ def test_config1_kitti_rays_train_and_val(tmp_path):
     with torch.no_grad():
         res = R.render_rays_train(mc, mf, emb, batch, sub_nerf_test_num=int(g["sub_nerf_test_num"]), N_samples=64,
                                   N_importance=128, **PCNERF_TRAIN)
-    check_train(res, g, batch, mc, mf, name="config1_kitti_train", f64=golden("config1_kitti_f64"),
+    check_train(res, g, batch, mc, mf, name=f"config1_kitti_train_{train_math}", f64=golden("config1_kitti_f64"),
                 alt=golden("config1_kitti_alt"))
     emb, mc, mf = models(False)
     with torch.no_grad():

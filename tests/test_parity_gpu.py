@@ -52,7 +52,7 @@ def test_nof_eval_forward():
     close(p, g["p"], 2e-5, 1e-7, "p eval")
 
 
-def test_nof_train_forward_chunks_and_running_stats():
+def test_nof_train_forward_chunks_and_running_stats(train_math):
     g = golden("nof_train")
     _, mc, _ = models(True)
     emb = Embedding(3, 10)
@@ -107,8 +107,17 @@ def test_render_val(S):
 TRAIN = ["pcnerf", "pcnerf_noseg", "pcnerf_divide", "original", "pcnerf_perturb", "pcnerf_s128"]
 
 
+@pytest.fixture(params=["f16x2_3", "fp32"])
+def train_math(request):
+    """The train-mode layer arithmetic (nof._ops.set_train_math): the default split-fp16 products and fp32 MFMA."""
+    from nof import _ops
+    prev = _ops.set_train_math(request.param)
+    yield request.param
+    _ops.set_train_math(prev)
+
+
 @pytest.mark.parametrize("name", TRAIN)
-def test_render_train(name):
+def test_render_train(name, train_math):
     g = golden(f"render_train_{name}")
     emb, mc, mf = models(True)
     rng = {k: torch.from_numpy(g[k]).to(DEV) for k in ("perturb_rand", "u") if k in g}
@@ -264,7 +273,7 @@ def test_empty_rays_raise_like_the_reference():
                             noise_std=0, chunk=4096, issegmentated=1, childnerf_ratio=0.1, use_child_nerf_loss=1)
 
 
-def test_render_train_vs_oracle_config2_subset():
+def test_render_train_vs_oracle_config2_subset(train_math):
     """Config-2 rays at S=128/I=256 with several BatchNorm chunks, against the CPU oracle."""
     rays = syn.make_rays(192, seed=3)
     emb, mc, mf = models(True)
@@ -280,7 +289,7 @@ def test_render_train_vs_oracle_config2_subset():
 
 
 @pytest.mark.parametrize("chunk", [50, 1000, 262144])
-def test_render_train_tiny_and_odd_chunks(chunk):
+def test_render_train_tiny_and_odd_chunks(chunk, train_math):
     """BatchNorm chunks of 50 samples (two 32-sample tiles, the second partial: a 2-workgroup grid), 1000 and one
     chunk covering everything, against the CPU oracle -- the train kernels' grid, tail-tile and statistics paths.
     Checked on the coarse pass and its running statistics: with 16 coarse samples the fine pass's resampling is
