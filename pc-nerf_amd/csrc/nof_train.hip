@@ -38,6 +38,36 @@ namespace pcn {
 #define PCN_S12_COPIES 8  // k_wgrad_reduce: copies of the BatchNorm-backward sums (block m adds to copy m % COPIES)
 #endif
 
+// k_train_h schedule (A/B knobs): ring depth of B-operand reads, k-step of the next tile's raw loads, staging
+// k-steps counted from the end, k-step of the previous tile's epilogue, static priority for waves 4-7
+#ifndef PCN_H_XD
+#define PCN_H_XD 3
+#endif
+#ifndef PCN_H_XD_SKIP
+#define PCN_H_XD_SKIP 2
+#endif
+#ifndef PCN_H_LOAD
+#define PCN_H_LOAD 2
+#endif
+#ifndef PCN_H_STAGE
+#define PCN_H_STAGE 4
+#endif
+#ifndef PCN_H_EPI
+#define PCN_H_EPI 1
+#endif
+#ifndef PCN_H_PRIO
+#define PCN_H_PRIO 1
+#endif
+#ifndef PCN_H_LMAP
+#define PCN_H_LMAP 0   // staging lane map (conflict-free 8-byte LDS writes)
+#endif
+#ifndef PCN_H_REGSTAT
+#define PCN_H_REGSTAT 1  // hidden layers: running statistics in registers, epilogue after each tile's MFMAs
+#endif
+#ifndef PCN_H_AHEAD
+#define PCN_H_AHEAD 1  // raw activation loads 1 or 2 tiles ahead
+#endif
+
 #ifndef PCN_CLOCK_STAMP
 #define PCN_CLOCK_STAMP 0  // diagnostic builds only: phase stamps of 1 k_train_ws, 2 k_wgrad (pcnerf_debug_clock)
 #endif
@@ -501,14 +531,22 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   constexpr bool ETIN = KE && HP, ETOUT = KE && !HP;
   constexpr int KSE = KE ? KS_E : 0;               // encoding k-steps
   constexpr int KS = KSE + (HP ? KS_H : 0);        // k-steps of 16 features
-  constexpr int XD = 3;                            // LDS read ring depth in k-steps
-  constexpr int S_LOAD = 2, S_STAGE0 = KS - 4, S_STAGE1 = KS - 3;   // HP: next tile's loads / staging
+  constexpr int XD = (KE && HP) ? PCN_H_XD_SKIP : PCN_H_XD;   // LDS read ring depth in k-steps
+  // HP: the next tile's raw loads, their staging (BatchNorm + split + LDS), the previous tile's epilogue
+  constexpr int S_LOAD = PCN_H_LOAD, S_STAGE0 = KS - PCN_H_STAGE, S_STAGE1 = S_STAGE0 + 1;
+  constexpr int S_EPI = PCN_H_EPI;
+  constexpr int AHEAD = (KE && HP) ? 1 : PCN_H_AHEAD;   // the skip layer's 160 weight registers leave no room
+  // REGSTAT: each tile's epilogue right after its MFMAs, the per-lane running statistics in registers (no LDS
+  // read-modify-write per tile, one accumulator set); the B buffers double as the final reduction area
+  constexpr bool REGSTAT = HP && !KE && PCN_H_REGSTAT;   // (the skip layer would spill)
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
   __shared__ float smax[8];
   __shared__ f16x8 xs[2][KS][2][64];
-  __shared__ f32x4 sred[8 * 64 * 8];   // per-lane running statistics, as k_train_ws
+  __shared__ f32x4 sred_[REGSTAT ? 1 : 8 * 64 * 8];   // per-lane running statistics, as k_train_ws
+  static_assert(!REGSTAT || sizeof(xs) >= 8 * 64 * 8 * sizeof(f32x4), "reduction area");
+  f32x4* const sred = REGSTAT ? reinterpret_cast<f32x4*>(&xs[0][0][0][0]) : sred_;
   const int t = threadIdx.x;
   if (t < 256) {
     if (HP) bn_coeffs(prev, n, momentum, eps, al, be);
@@ -535,7 +573,11 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
+  // staging identity: the HBM lane (sample ls + 32 hs) whose float4s this thread stages; PCN_H_LMAP interleaves
+  // the halves across neighbouring lanes so each 16-lane group's 8-byte LDS writes cover 128 contiguous bytes
+  const int sln = PCN_H_LMAP ? ((lane >> 1) + 32 * (lane & 1)) : lane, ls = sln & 31, hs = sln >> 5;
   const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH two-waves item 4
   f16x8 wr[KS][2];
   {
     const f16x8* __restrict__ w8 = Wp + lane;
@@ -546,8 +588,12 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   }
   f32x4* const my_st = sred + (blk * 64 + lane) * 8;
   const int st_sw = (lane >> 1) & 7;
+  f32x4 rs[8];   // REGSTAT: chunk 2j = sum d, 2j+1 = sum d^2 of accumulator registers 4j..4j+3
 #pragma unroll
-  for (int c = 0; c < 8; ++c) my_st[c] = f32x4{};
+  for (int c = 0; c < 8; ++c) {
+    rs[c] = f32x4{};
+    if (!REGSTAT) my_st[c] = f32x4{};
+  }
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0);
   int buf = 0;
@@ -556,14 +602,14 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   auto put = [&](int b, int G, const f32x4& x) {
     f16x4 hi, mid;
     split4(x, hi, mid);
-    const int s = G >> 1, ln = li + 32 * (G & 1);
-    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][s][0][ln]) + 4 * h) = hi;
-    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][s][1][ln]) + 4 * h) = mid;
+    const int s = G >> 1, ln = ls + 32 * (G & 1);
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][s][0][ln]) + 4 * hs) = hi;
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][s][1][ln]) + 4 * hs) = mid;
   };
   auto stage = [&](int b, const f32x4 (&v)[4], int m) {
     const int g = (t >> 6) + 8 * m;
-    const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
-    const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
+    const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * hs);
+    const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * hs);
     f32x4 x;
 #pragma unroll
     for (int q = 0; q < 4; ++q) x[q] = (v[m][q] * a[q] + c[q]) * xscale;
@@ -577,8 +623,15 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     }
     put(b, t >> 6, x);
   };
+  // the raw activation float4s of a tile this thread stages ([g][HBM lane][4], g = (t >> 6) + 8 m)
+  auto load_tile = [&](f32x4 (&v)[4], int tile) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)tile * TILE_FLOATS)[(t & ~63) + sln + 512 * m];
+  };
+  const int etix = (t & ~63) + sln;   // this thread's encoding float4 in a stored tile [g][HBM lane]
   auto sample_of = [&](int tile) {
-    int64_t sl = (int64_t)tile * 32 + li;
+    int64_t sl = (int64_t)tile * 32 + ls;
     if (sl >= n) sl = n - 1;
     return c0 + sl;
   };
@@ -586,9 +639,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   if (tl < nt) {
     if (HP) {
       f32x4 v[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)tl * TILE_FLOATS + (size_t)m * 2048)[t];
+      load_tile(v, tl);
 #pragma unroll
       for (int m = 0; m < 4; ++m) stage(0, v, m);
     }
@@ -596,16 +647,16 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       const int64_t gs = sample_of(tl);
       f32x4 e;
       if (ETIN) {
-        e = etin[(size_t)tl * 512 + t];
+        e = etin[(size_t)tl * 512 + etix];
       } else if (ein) {
-        e = enc_feats_row(ein + gs * 63, h, t >> 6);
+        e = enc_feats_row(ein + gs * 63, hs, t >> 6);
       } else {
         float p[3];
         sample_point(rays + (gs / S) * stride, z[gs], p);
-        e = enc_feats(p, h, t >> 6);
+        e = enc_feats(p, hs, t >> 6);
       }
       put_enc(0, e);
-      if (ETOUT) etout[(size_t)tl * 512 + t] = e;
+      if (ETOUT) etout[(size_t)tl * 512 + etix] = e;
     }
   }
   __syncthreads();
@@ -627,11 +678,29 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     float* base = hout + (size_t)ptile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
     reinterpret_cast<f32x4*>(base)[lane] = o;
   };
-  auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile) {
+  // AHEAD == 2: the raw loads run two tiles ahead (vload gets tile + 2 gstride while vstage, loaded one
+  // tile earlier, is staged for tile + gstride); == 1: loaded and staged within the same tile
+  auto epir = [&](const f32x16& acc, int tile, int j) {   // REGSTAT epilogue
+    const bool valid = (int64_t)tile * 32 + li < n;
+    const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
+    f32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float d = acc[4 * j + q] * unscale;
+      o[q] = d + bj[q];
+      const float dv = valid ? d : 0.0f;
+      rs[2 * j][q] += dv;
+      rs[2 * j + 1][q] += dv * dv;
+    }
+    float* base = hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
+    reinterpret_cast<f32x4*>(base)[lane] = o;
+  };
+  auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile, f32x4 (&vstage)[4], f32x4 (&vload)[4]) {
     const int nxt = __builtin_amdgcn_readfirstlane(tile + gstride);
     const bool more = nxt < nt;
+    const int nxt2 = __builtin_amdgcn_readfirstlane(tile + 2 * gstride);
     f16x8 xr[XD][2];
-    f32x4 v[4];
+    f32x4 vloc[4];   // AHEAD == 1: this tile's loads of the next tile
     float rr[7];
     f32x4 ev;
 #pragma unroll
@@ -650,7 +719,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
       if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
-      if (ETIN && ks == KS - 4 && more) ev = etin[(size_t)nxt * 512 + t];
+      if (ETIN && ks == KS - 4 && more) ev = etin[(size_t)nxt * 512 + etix];
       if (ETOUT && ks == 0 && more && !ein) {
         const int64_t gs = sample_of(nxt);
         const float* r = rays + (gs / S) * stride;
@@ -658,51 +727,80 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
         for (int c = 0; c < 6; ++c) rr[c] = r[c];
         rr[6] = z[gs];
       }
-      if (ks == 1 && ptile >= 0) {
+      if (!REGSTAT && ks == S_EPI && ptile >= 0) {
         epi(pacc, ptile, 0);
         epi(pacc, ptile, 1);
       }
-      if (ks == 2 && ptile >= 0) {
+      if (!REGSTAT && ks == S_EPI + 1 && ptile >= 0) {
         epi(pacc, ptile, 2);
         epi(pacc, ptile, 3);
       }
-      if (HP && ks == S_LOAD && more) {
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-          v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)nxt * TILE_FLOATS + (size_t)m * 2048)[t];
-      }
-      if (HP && ks == S_STAGE0 && more) {
-        stage(buf ^ 1, v, 0);
-        stage(buf ^ 1, v, 1);
-      }
-      if (HP && ks == S_STAGE1 && more) {
-        stage(buf ^ 1, v, 2);
-        stage(buf ^ 1, v, 3);
+      if constexpr (HP && AHEAD == 2) {
+        if (ks == S_LOAD && nxt2 < nt) load_tile(vload, nxt2);
+        if (ks == S_STAGE0 && more) {
+          stage(buf ^ 1, vstage, 0);
+          stage(buf ^ 1, vstage, 1);
+        }
+        if (ks == S_STAGE1 && more) {
+          stage(buf ^ 1, vstage, 2);
+          stage(buf ^ 1, vstage, 3);
+        }
+      } else if constexpr (HP) {
+        if (ks == S_LOAD && more) load_tile(vloc, nxt);
+        if (ks == S_STAGE0 && more) {
+          stage(buf ^ 1, vloc, 0);
+          stage(buf ^ 1, vloc, 1);
+        }
+        if (ks == S_STAGE1 && more) {
+          stage(buf ^ 1, vloc, 2);
+          stage(buf ^ 1, vloc, 3);
+        }
       }
       if (KE && ks == KS - 1 && more) {
         f32x4 e;
         if (ETIN) {
           e = ev;
         } else if (ein) {
-          e = enc_feats_row(ein + sample_of(nxt) * 63, h, t >> 6);
+          e = enc_feats_row(ein + sample_of(nxt) * 63, hs, t >> 6);
         } else {
           float p[3];
 #pragma unroll
           for (int c = 0; c < 3; ++c) p[c] = rr[c] + rr[3 + c] * rr[6];
-          e = enc_feats(p, h, t >> 6);
+          e = enc_feats(p, hs, t >> 6);
         }
         put_enc(buf ^ 1, e);
-        if (ETOUT) etout[(size_t)nxt * 512 + t] = e;
+        if (ETOUT) etout[(size_t)nxt * 512 + etix] = e;
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if (REGSTAT) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epir(acc, tile, j);
     }
     __syncthreads();
     buf ^= 1;
   };
   f32x16 accA, accB;
+  f32x4 vA[4], vB[4];
+  if (HP && AHEAD == 2) {
+    const int t1 = __builtin_amdgcn_readfirstlane(tl + gstride);
+    if (t1 < nt) load_tile(vA, t1);
+  }
   int ptile = -1;
+  if (REGSTAT) {
+    while (tl < nt) {
+      body(accA, accA, tl, -1, vA, vB);
+      tl = __builtin_amdgcn_readfirstlane(tl + gstride);
+      if (tl >= nt) break;
+      body(accA, accA, tl, -1, vB, vA);
+      tl = __builtin_amdgcn_readfirstlane(tl + gstride);
+    }
+    tl = nt;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) my_st[c ^ st_sw] = rs[c];
+  }
   while (tl < nt) {
-    body(accA, accB, tl, ptile);
+    body(accA, accB, tl, ptile, vA, vB);
     ptile = tl;
     tl = __builtin_amdgcn_readfirstlane(tl + gstride);
     if (tl >= nt) {
@@ -710,7 +808,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       for (int j = 0; j < 4; ++j) epi(accA, ptile, j);
       break;
     }
-    body(accB, accA, tl, ptile);
+    body(accB, accA, tl, ptile, vB, vA);
     ptile = tl;
     tl = __builtin_amdgcn_readfirstlane(tl + gstride);
     if (tl >= nt) {
