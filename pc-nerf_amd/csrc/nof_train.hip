@@ -64,6 +64,9 @@ namespace pcn {
 #ifndef PCN_H_REGSTAT
 #define PCN_H_REGSTAT 1  // hidden layers: running statistics in registers, epilogue after each tile's MFMAs
 #endif
+#ifndef PCN_H_DMA
+#define PCN_H_DMA 0  // hidden layers: k_train_hd (raw tiles by LDS-DMA two tiles ahead)
+#endif
 #ifndef PCN_H_AHEAD
 #define PCN_H_AHEAD 1  // raw activation loads 1 or 2 tiles ahead
 #endif
@@ -830,6 +833,191 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   }
 }
 
+// ---- k_train_hd<NT>: the hidden-layer k_train_h (REGSTAT form) with the raw activation tiles brought in by LDS-DMA
+// (global_load_lds_dwordx4) two tiles ahead into a 2-slot ring, so 64 KiB per CU stay in flight without registers.
+// Iteration i (tile t_i = blockIdx + i G): its start issues tile t_{i+2}'s DMA into slot i & 1 (which held t_i, staged
+// during iteration i-1); its staging point waits (counted vmcnt) for the thread's own DMA of t_{i+1} in slot (i+1) & 1
+// -- every thread reads back exactly the 16-byte pieces it DMA'd (slot layout = the HBM tile's [g][lane][4]), so no
+// barrier is needed for the raw data.  All LDS lives in one __shared__ array and the tile barrier is a raw
+// s_barrier after lgkmcnt(0) (a __syncthreads() would drain the DMA in flight: cdna_hip_programming.md glds rules).
+// Two 16-byte LDS reads (p[0], p[stride]) in inline asm, completed before return: invisible to hipcc's waitcnt
+// pass, which would otherwise wait vmcnt(0) -- every DMA and store in flight -- before reading a DMA-written slot.
+__device__ __forceinline__ void lds_read2_asm(const f32x4* p, int stride, f32x4& a, f32x4& b) {
+  const unsigned ad = (unsigned)(size_t)(const __attribute__((address_space(3))) f32x4*)p;
+  const unsigned bd = ad + (unsigned)stride * 16u;
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(a), "=&v"(b) : "v"(ad), "v"(bd) : "memory");
+}
+
+template <int NT>
+__global__ __launch_bounds__(512, 1) void k_train_hd(const float* __restrict__ hin, int64_t n,
+                                                     const f16x8* __restrict__ Wp, const int* __restrict__ swp,
+                                                     int layer, const float* __restrict__ bias, BnPrev prev,
+                                                     float momentum, float eps, float* __restrict__ hout,
+                                                     double* __restrict__ stats) {
+  constexpr int KS = KS_H, XD = PCN_H_XD;
+  constexpr int S_STAGE0 = KS - PCN_H_STAGE, S_STAGE1 = S_STAGE0 + 1;
+  constexpr int OFF_AL = 0, OFF_BE = 1024, OFF_BS = 2048, OFF_MAX = 3072, OFF_XS = 4096;
+  constexpr int XS_BYTES = 2 * KS * 2 * 64 * 16, OFF_RAW = OFF_XS + XS_BYTES, RAW_SLOT = 32768;
+  __shared__ __attribute__((aligned(16))) char smem[OFF_RAW + 2 * RAW_SLOT];
+  float* const al = reinterpret_cast<float*>(smem + OFF_AL);
+  float* const be = reinterpret_cast<float*>(smem + OFF_BE);
+  float* const bs = reinterpret_cast<float*>(smem + OFF_BS);
+  float* const smax = reinterpret_cast<float*>(smem + OFF_MAX);
+  f16x8* const xs = reinterpret_cast<f16x8*>(smem + OFF_XS);   // [buf][s][part][lane]
+  f32x4* const raw = reinterpret_cast<f32x4*>(smem + OFF_RAW);  // [slot][2048]
+  auto XS = [&](int b, int s, int p, int l) -> f16x8& { return xs[((b * KS + s) * 2 + p) * 64 + l]; };
+  const int t = threadIdx.x;
+  if (t < 256) {
+    bn_coeffs(prev, n, momentum, eps, al, be);
+    bs[t] = bias[t];
+  }
+  float bnd = t < 256 ? sqrtf((float)n) * fabsf(prev.gamma[t]) + fabsf(prev.beta[t]) : 0.0f;
+  bnd = wave_max_f(bnd);
+  if ((t & 63) == 0) smax[t >> 6] = bnd;
+  __syncthreads();
+  float mb = smax[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) mb = fmaxf(mb, smax[i]);
+  int sx = (mb > 0.0f && mb < 3.0e38f) ? 14 - ilogbf(mb) : 0;
+  sx = sx > 24 ? 24 : sx;
+  const float xscale = ldexpf(1.0f, sx);
+  const float unscale = ldexpf(1.0f, -(swp[layer] + sx));
+  const int nt = (int)((n + 31) / 32);
+  const int G = (int)gridDim.x;
+  const int lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);
+  f16x8 wr[KS][2];
+  {
+    const f16x8* __restrict__ w8 = Wp + lane;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 8 + blk) * 2 + p) * 64];
+  }
+  f32x4 rs[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) rs[c] = f32x4{};
+  // raw tile pieces: this thread's 4 float4 of a tile are [g = (t >> 6) + 8 m][lane] = float4 t + 512 m
+  auto dma = [&](int slot, int tile) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const f32x4*>(hin + (size_t)tile * TILE_FLOATS) +
+                                                          t + 512 * m),
+          (__attribute__((address_space(3))) void*)(raw + slot * 2048 + (t & ~63) + 512 * m), 16, 0, 0);
+  };
+  auto stage = [&](int b, const f32x4& v, int m) {
+    const int g = (t >> 6) + 8 * m;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
+    const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
+    f32x4 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = (v[q] * a[q] + c[q]) * xscale;
+    f16x4 hi, mid;
+    split4(x, hi, mid);
+    const int s = g >> 1, ln = li + 32 * (g & 1);
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&XS(b, s, 0, ln)) + 4 * h) = hi;
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&XS(b, s, 1, ln)) + 4 * h) = mid;
+  };
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  // prologue: tile t_0 through registers into xs[0]; t_1's DMA into slot 1
+  if (tl < nt) {
+    f32x4 v[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)tl * TILE_FLOATS)[t + 512 * m];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) stage(0, v[m], m);
+  }
+  __builtin_amdgcn_s_waitcnt(0);   // weights and t_0 in registers before any DMA is outstanding
+  if (tl + G < nt) dma(1, tl + G);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int buf = 0;
+  for (int i = 0; tl < nt; ++i) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tl + G), nxt2 = __builtin_amdgcn_readfirstlane(tl + 2 * G);
+    const bool more = nxt < nt, more2 = nxt2 < nt;
+    if (more2) dma(i & 1, nxt2);
+    f32x16 acc;
+    f16x8 xr[XD][2];
+#pragma unroll
+    for (int d = 0; d < XD - 1; ++d) {
+      xr[d][0] = XS(buf, d, 0, lane);
+      xr[d][1] = XS(buf, d, 1, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + XD - 1 < KS) {
+        xr[(ks + XD - 1) % XD][0] = XS(buf, ks + XD - 1, 0, lane);
+        xr[(ks + XD - 1) % XD][1] = XS(buf, ks + XD - 1, 1, lane);
+      }
+      const f16x8 xh = xr[ks % XD][0], xm = xr[ks % XD][1];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xh, ks == 0 ? f32x16{} : acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
+      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
+      if (ks == S_STAGE0 && more) {
+        // own DMA of t_{i+1}: younger VMEM ops are iteration i-1's 4 epilogue stores (i > 0) and this
+        // iteration's DMA of t_{i+2} (4, when issued)
+        if (i > 0 && more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (i > 0 || more2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        f32x4 r0, r1;
+        lds_read2_asm(raw + ((i + 1) & 1) * 2048 + t, 512, r0, r1);
+        stage(buf ^ 1, r0, 0);
+        stage(buf ^ 1, r1, 1);
+      }
+      if (ks == S_STAGE1 && more) {
+        f32x4 r2, r3;
+        lds_read2_asm(raw + ((i + 1) & 1) * 2048 + t + 1024, 512, r2, r3);
+        stage(buf ^ 1, r2, 2);
+        stage(buf ^ 1, r3, 3);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue of this tile: raw h (+ bias) to HBM, running statistics of (h - bias) in registers
+    const bool valid = (int64_t)tl * 32 + li < n;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
+      f32x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float d = acc[4 * j + q] * unscale;
+        o[q] = d + bj[q];
+        const float dv = valid ? d : 0.0f;
+        rs[2 * j][q] += dv;
+        rs[2 * j + 1][q] += dv * dv;
+      }
+      reinterpret_cast<f32x4*>(hout + (size_t)tl * TILE_FLOATS + (size_t)(4 * blk + j) * 256)[lane] = o;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    buf ^= 1;
+    tl = nxt;
+  }
+  // per-neuron sums: the per-lane statistics through LDS (the B buffers), one float64 atomic per (neuron, moment)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  f32x4* const sred = reinterpret_cast<f32x4*>(smem + OFF_XS);
+  const int st_sw = (lane >> 1) & 7;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) sred[(blk * 64 + lane) * 8 + (c ^ st_sw)] = rs[c];
+  __syncthreads();
+  {
+    const int nn = t >> 1, mo = t & 1, ib = nn & 31, wb = nn >> 5;
+    const int hh = (ib >> 2) & 1, jj = ib >> 3, qq = ib & 3;
+    double a = 0.0;
+#pragma unroll 8
+    for (int l = 0; l < 32; ++l) {
+      const int ln = 32 * hh + l;
+      a += (double)sred[(wb * 64 + ln) * 8 + ((2 * jj + mo) ^ ((ln >> 1) & 7))][qq];
+    }
+    atomicAdd(&stats[t], a);
+  }
+}
+
 // occ_out on BatchNorm 8 (applied on load) + sigmoid; one wave per 32-sample tile.
 __global__ __launch_bounds__(256) void k_train_out(const float* __restrict__ hin, int64_t n, BnPrev prev,
                                                    float momentum, float eps, const float* __restrict__ wout,
@@ -939,6 +1127,13 @@ static void launch_layer(const TrainLayerLaunch& q, const NofParamsDev& P, const
   if (m == 0) {
     hipLaunchKernelGGL((k_train_ws<KE, HP>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0, q.ein,
                        hin, q.n, wp + off_w(L, KE != 0), P.lin_b[L], prev, q.mom, q.eps, hout, stats, etin, etout);
+  } else if (PCN_H_DMA && KE == 0 && HP) {
+    if (m == 1)
+      hipLaunchKernelGGL(k_train_hd<3>, dim3(q.gws), dim3(512), 0, q.s, hin, q.n, wh + off_h(L, false), sw, L,
+                         P.lin_b[L], prev, q.mom, q.eps, hout, stats);
+    else
+      hipLaunchKernelGGL(k_train_hd<4>, dim3(q.gws), dim3(512), 0, q.s, hin, q.n, wh + off_h(L, false), sw, L,
+                         P.lin_b[L], prev, q.mom, q.eps, hout, stats);
   } else if (m == 1) {
     hipLaunchKernelGGL((k_train_h<KE, HP, 3>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0,
                        q.ein, hin, q.n, wh + off_h(L, KE != 0), sw, L, P.lin_b[L], prev, q.mom, q.eps, hout, stats,
