@@ -346,7 +346,7 @@ def test_fit_trajectory_vs_oracle(tmp_path, stress):
     # within Adam's largest possible movement; each tensor's update (final - initial) matching the reference's
     # to 1 % in norm (the trajectory); a running mean follows the
     # bias / previous BN shift feeding its Linear, so it gets that drift through the Linear as tolerance; running
-    # variances of the drifted network within 2e-3.
+    # variances of the drifted network within 5e-3.
     nz = noise_level_grads()
     adam_max = 2 * 3.2 * 5e-4 * epochs
     init = {("c", k): v for k, v in pc_np.items()}
@@ -360,8 +360,10 @@ def test_fit_trajectory_vs_oracle(tmp_path, stress):
             got, want = v.cpu().numpy().astype(np.float64), P[k].detach().numpy().astype(np.float64)
             err = got - want
             if k.endswith("running_var"):
-                # the statistics of the updated network: its parameters carry the Adam drift described above
-                np.testing.assert_allclose(got, want, rtol=2e-3, atol=1e-7, err_msg=tag + k)
+                # the statistics of the updated network: its parameters carry the Adam drift described above, and
+                # the fine network's statistics the fine-sample spread the reference shows against itself
+                # (running stats of the config fixtures move by ~2e-3 between its own thread counts)
+                np.testing.assert_allclose(got, want, rtol=5e-3, atol=1e-7, err_msg=tag + k)
                 worst_rv = max(worst_rv, float(np.max(np.abs(err) / np.abs(want))))
             elif k.endswith("running_mean"):
                 lin = O.LIN[O.BN.index(k[:-len(".running_mean")])]
