@@ -1486,7 +1486,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
                                                       const float* __restrict__ wout, const double* __restrict__ acc,
                                                       double* __restrict__ d_gamma, double* __restrict__ d_beta,
                                                       double* __restrict__ d_wout, double* __restrict__ d_bout,
-                                                      float* __restrict__ gout) {
+                                                      float* __restrict__ gout, float* __restrict__ tmax) {
   __shared__ __attribute__((aligned(16))) float cgm[256];
   __shared__ __attribute__((aligned(16))) float ckk[256];
   __shared__ __attribute__((aligned(16))) float cmu[256];
@@ -1525,6 +1525,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
     const float gv = valid ? logit_grad(g, pin, s) : 0.0f;
     const f32x4* x4 = reinterpret_cast<const f32x4*>(h7 + tile * TILE_FLOATS) + lane;
     f32x4* o4 = reinterpret_cast<f32x4*>(gout + tile * TILE_FLOATS) + lane;
+    float mx = 0.0f;
 #pragma unroll 8
     for (int gq = 0; gq < 32; ++gq) {
       const f32x4 x = x4[gq * 64];
@@ -1534,8 +1535,13 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
       for (int q = 0; q < 4; ++q) {
         const int f = f0 + q;
         o[q] = valid ? ((gv * cwo[f] - cgm[f]) - (x[q] - cmu[f]) * ckk[f]) * cis[f] * cga[f] : 0.0f;
+        mx = fmaxf(mx, fabsf(o[q]));
       }
       o4[gq * 64] = o;
+    }
+    if (tmax) {   // the tile's largest |dL/dh_7| (k_dgrad_h's operand scale), one wave per tile
+      mx = wave_max_f(mx);
+      if (lane < 8) tmax[tile * 8 + lane] = mx;
     }
   }
 }
@@ -1880,6 +1886,349 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_ws(
   }
 }
 
+// ---- Backward under the split train math (pcnerf_set_train_math 1/2).
+//
+// k_dgrad_h<NT>: k_dgrad_ws's product dL/dy = W^T dL/dh on the fp16 matrix pipe, in k_train_h's form (W^T resident
+// as hi/mid fp16 parts x 2^sw, the dL/dh tile staged split into LDS, NT products per k-step).  dL/dh has no bound
+// known before it exists, so its producer (k_out_bwd_grad, or the previous k_dgrad_h) records every tile's largest
+// |value| (tmax[tile][8], one entry per wave) and the staging scales the tile by 2^sg with that max x 2^sg in
+// [2^14, 2^15): a per-tile scale factors out of the tile's own product (the accumulator is per tile) and is undone
+// in its epilogue.  The epilogue is k_dgrad_ws's BatchNorm backward; it records the output tile's max for the next
+// layer.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int tile_scale_exp(float m) {
+  if (!(m > 0.0f) || !(m < 3.0e38f)) return 0;   // zero, NaN or inf tiles: unscaled
+  int e = 14 - ilogbf(m);
+  return e < -100 ? -100 : e > 100 ? 100 : e;
+}
+
+// W^T image for k_dgrad_h: layer L (1..7) at (L-1) HW_H, [ks][out-block 8][part 2][lane 64] f16x8, row i = input
+// feature 32 ob + (lane & 31) of layer L, k = neuron 16 ks + 8 (lane >> 5) + e; scaled by 2^sw[L] like the forward
+__global__ void k_pack_dgrad_h(NofParamsDev P, const int* __restrict__ sw, f16x8* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 7 * HW_H) return;
+  const int L = 1 + (int)(idx / HW_H);
+  const size_t j = idx % HW_H;
+  const int lane = (int)(j & 63), part = (int)((j >> 6) & 1), ob = (int)((j >> 7) & 7), ks = (int)(j >> 10);
+  const int i = 32 * ob + (lane & 31), in_f = in_features(L), col = (L == 4 ? 63 : 0) + i;
+  const float sc = ldexpf(1.0f, sw[L]);
+  f16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 16 * ks + 8 * (lane >> 5) + e;
+    const float w = P.lin_w[L][(size_t)k * in_f + col] * sc;
+    const _Float16 hi = (_Float16)w;
+    v[e] = part == 0 ? hi : (_Float16)(w - (float)hi);
+  }
+  out[idx] = v;
+}
+
+template <int NT>
+__global__ __launch_bounds__(512, 1) void k_dgrad_h(
+    const float* __restrict__ gin, const float* __restrict__ tmax_in, const f16x8* __restrict__ Wt,
+    const int* __restrict__ swp, int layer, const float* __restrict__ hprev, int64_t n,
+    const double* __restrict__ s12, const float* __restrict__ coefp, const float* __restrict__ gamma,
+    double* __restrict__ d_gamma, double* __restrict__ d_beta, float* __restrict__ gout,
+    float* __restrict__ tmax_out) {
+  constexpr int KS = KS_H, XD = PCN_H_XD;
+  constexpr int S_LOAD = PCN_H_LOAD, S_STAGE0 = KS - PCN_H_STAGE, S_STAGE1 = S_STAGE0 + 1, S_HX = 8;
+  __shared__ __attribute__((aligned(16))) float cgm[256];
+  __shared__ __attribute__((aligned(16))) float ckk[256];
+  __shared__ __attribute__((aligned(16))) float cmu[256];
+  __shared__ __attribute__((aligned(16))) float cis[256];
+  __shared__ __attribute__((aligned(16))) float cga[256];
+  __shared__ f16x8 xs[2][KS][2][64];
+  const int t = threadIdx.x;
+  if (t < 256) {
+    const int k = t;
+    double S1 = 0.0, dotp = 0.0;
+#pragma unroll
+    for (int c = 0; c < PCN_S12_COPIES; ++c) {
+      S1 += s12[512 * c + 2 * k];
+      dotp += s12[512 * c + 2 * k + 1];
+    }
+    const float invstd = coefp[256 + k];
+    cgm[k] = (float)(S1 / (double)n);
+    ckk[k] = (((float)dotp * invstd) * invstd) / (float)n;
+    cmu[k] = coefp[k];
+    cis[k] = invstd;
+    cga[k] = gamma[k];
+    if (blockIdx.x == 0) {
+      d_gamma[k] += dotp * (double)invstd;
+      d_beta[k] += S1;
+    }
+  }
+  const float wunscale = ldexpf(1.0f, -swp[layer]);
+  const int nt = (int)((n + 31) / 32);
+  const int gstride = (int)gridDim.x;
+  const int lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);
+  f16x8 wr[KS][2];
+  {
+    const f16x8* __restrict__ w8 = Wt + lane;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 8 + blk) * 2 + p) * 64];
+  }
+  auto tile_exp = [&](int tile) {
+    const f32x4* tm = reinterpret_cast<const f32x4*>(tmax_in + (size_t)tile * 8);
+    const f32x4 a = tm[0], b = tm[1];
+    const float m = fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3])));
+    return __builtin_amdgcn_readfirstlane(tile_scale_exp(m));
+  };
+  // staging: thread t's float4s t + 512 m of the tile (feature group g = (t >> 6) + 8 m, lane t & 63), scaled by
+  // 2^sg and split -> LDS [s = g >> 1][part][li + 32 (g & 1)][4 h ..], as k_train_h's put
+  auto stage = [&](int b, const f32x4 (&v)[4], int m, float xscale) {
+    const int g = (t >> 6) + 8 * m;
+    f32x4 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = v[m][q] * xscale;
+    f16x4 hi, mid;
+    split4(x, hi, mid);
+    const int s = g >> 1, ln = li + 32 * (g & 1);
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][s][0][ln]) + 4 * h) = hi;
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][s][1][ln]) + 4 * h) = mid;
+  };
+  auto load_tile = [&](f32x4 (&v)[4], int tile) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) v[m] = reinterpret_cast<const f32x4*>(gin + (size_t)tile * TILE_FLOATS)[t + 512 * m];
+  };
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  int sg = 0;
+  if (tl < nt) {
+    sg = tile_exp(tl);
+    f32x4 v[4];
+    load_tile(v, tl);
+    const float xscale = ldexpf(1.0f, sg);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) stage(0, v, m, xscale);
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);
+  int buf = 0;
+  auto epi = [&](const f32x16& acc, const f32x4 (&hx)[4], int tile, float unscale) {
+    const bool valid = (int64_t)tile * 32 + li < n;
+    float mx = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f0 = 8 * (4 * blk + j) + 4 * h;
+      const f32x4 gm = *reinterpret_cast<const f32x4*>(cgm + f0), kk = *reinterpret_cast<const f32x4*>(ckk + f0);
+      const f32x4 mu = *reinterpret_cast<const f32x4*>(cmu + f0), is = *reinterpret_cast<const f32x4*>(cis + f0);
+      const f32x4 ga = *reinterpret_cast<const f32x4*>(cga + f0);
+      f32x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float d = (acc[4 * j + q] * wunscale) * unscale;
+        o[q] = valid ? ((d - gm[q]) - (hx[j][q] - mu[q]) * kk[q]) * is[q] * ga[q] : 0.0f;
+        mx = fmaxf(mx, fabsf(o[q]));
+      }
+      reinterpret_cast<f32x4*>(gout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256)[lane] = o;
+    }
+    mx = wave_max_f(mx);
+    if (lane == 0) tmax_out[(size_t)tile * 8 + blk] = mx;
+  };
+  while (tl < nt) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
+    const bool more = nxt < nt;
+    const float unscale = ldexpf(1.0f, -sg);
+    int sgn = 0;
+    f32x16 acc;
+    f16x8 xr[XD][2];
+    f32x4 vloc[4], hx[4];
+#pragma unroll
+    for (int d = 0; d < XD - 1; ++d) {
+      xr[d][0] = xs[buf][d][0][lane];
+      xr[d][1] = xs[buf][d][1][lane];
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + XD - 1 < KS) {
+        xr[(ks + XD - 1) % XD][0] = xs[buf][ks + XD - 1][0][lane];
+        xr[(ks + XD - 1) % XD][1] = xs[buf][ks + XD - 1][1][lane];
+      }
+      const f16x8 xh = xr[ks % XD][0], xm = xr[ks % XD][1];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xh, ks == 0 ? f32x16{} : acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
+      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
+      if (ks == S_LOAD && more) {
+        load_tile(vloc, nxt);
+        sgn = tile_exp(nxt);
+      }
+      if (ks == S_HX) {   // this tile's h_{L-1} operand of the BatchNorm backward
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          hx[j] = reinterpret_cast<const f32x4*>(hprev + (size_t)tl * TILE_FLOATS + (size_t)(4 * blk + j) * 256)[lane];
+      }
+      if (ks == S_STAGE0 && more) {
+        const float xscale = ldexpf(1.0f, sgn);
+        stage(buf ^ 1, vloc, 0, xscale);
+        stage(buf ^ 1, vloc, 1, xscale);
+      }
+      if (ks == S_STAGE1 && more) {
+        const float xscale = ldexpf(1.0f, sgn);
+        stage(buf ^ 1, vloc, 2, xscale);
+        stage(buf ^ 1, vloc, 3, xscale);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    epi(acc, hx, tl, unscale);
+    __syncthreads();
+    buf ^= 1;
+    sg = sgn;
+    tl = nxt;
+  }
+}
+
+// k_wgrad_b3: k_wgrad<0>'s G = sum_s dL/dh (x) (h_{L-1} - mean) with each fp32 operand split into three bf16 parts
+// (v = hi + mid + lo: all 24 bits of the fp32 value, bf16 keeps fp32's exponent range, so no scaling) and the six
+// products down to 2^-16 (hh, hm, mh, hl, lh, mm) on v_mfma_f32_32x32x16_bf16: the dropped ml, lm, ll are
+// <= 2^-23 relative, like fp32 rounding.  The contraction runs over samples, 16 per k-step, so an operand lane
+// needs 8 consecutive samples of one feature:
+//   x (B operand, read by all 8 waves): waves 4-7 stage it transposed and split, one thread per 4 features x 8
+//     samples (128 contiguous bytes of the tile), into [k-step 2][part 3][block 8][lane 64] bf16x8 with lane
+//     swizzle l ^ ((l >> 3) & 3) (conflict-free 16-byte writes and reads);
+//   dL/dh (A operand, read by its wave only): waves 0-3 copy the raw tile into LDS ([g][half][sample ^ c][4],
+//     c = 2 (g & 3) + half: conflict-free 4-byte reads) and each wave splits its 8 values per k-step itself.
+// Two buffers of 80 KiB (all 160 KiB of the CU's LDS); one barrier per tile; the next tile's loads are in flight
+// during the MFMAs.  Partials and db as k_wgrad<0> (k_wgrad_reduce<0> sums them).
+constexpr int WB3_GF = 8192;                                   // raw dL/dh floats per buffer
+constexpr int WB3_XV = 2 * 3 * 8 * 64;                         // split x bf16x8 per buffer
+constexpr size_t WB3_BUF = (size_t)WB3_GF * 4 + (size_t)WB3_XV * 16;   // 80 KiB
+constexpr size_t WB3_LDS = 2 * WB3_BUF;
+
+__device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 a = (__bf16)v[j];
+    const float r = v[j] - (float)a;   // exact (Sterbenz)
+    const __bf16 b = (__bf16)r;
+    hi[j] = a;
+    mid[j] = b;
+    lo[j] = (__bf16)(r - (float)b);
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void k_wgrad_b3(const float* __restrict__ gin, const float* __restrict__ hprev,
+                                                     const float* __restrict__ mu, int64_t n,
+                                                     float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float wb3[];
+  const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool xrole = wv >= 4;
+  const int nt = (int)((n + 31) / 32);
+  const int gstride = (int)gridDim.x;
+  // x role: u = t - 256 -> half th, group-in-block tg3, sample octet to, block blk; features 32 blk + 8 tg3 + 4 th + q
+  const int u = t & 255, th = u & 1, tg3 = (u >> 1) & 3, to = (u >> 3) & 3, xblk = u >> 5;
+  const int xg = 4 * xblk + tg3;
+  f32x4 mu4 = {};
+  if (xrole) mu4 = *reinterpret_cast<const f32x4*>(mu + 8 * xg + 4 * th);
+  // x role: 8 float4 at [xg][th 32 + 8 to + i]; g role: float4s u + 256 i of the tile ([g][lane])
+  auto load_tile = [&](f32x4 (&r)[8], int tile) {
+    if (xrole) {
+      const f32x4* p = reinterpret_cast<const f32x4*>(hprev + (size_t)tile * TILE_FLOATS) + xg * 64 + th * 32 + 8 * to;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = p[i];
+    } else {
+      const f32x4* p = reinterpret_cast<const f32x4*>(gin + (size_t)tile * TILE_FLOATS) + u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = p[256 * i];
+    }
+  };
+  auto stage = [&](int b, const f32x4 (&r)[8], int tile) {
+    float* gb = wb3 + (size_t)b * (WB3_BUF / 4);
+    if (xrole) {
+      bf16x8* xb = reinterpret_cast<bf16x8*>(gb + WB3_GF);
+      const int s0 = tile * 32 + 8 * to;
+      const int ks = to >> 1, hh = to & 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (int64_t)s0 + i < n ? r[i][q] - mu4[q] : 0.0f;
+        bf16x8 p0, p1, p2;
+        split3_bf16(v, p0, p1, p2);
+        const int lp = 8 * tg3 + 4 * th + (q ^ tg3) + 32 * hh;   // swizzled lane of feature (f & 31), half hh
+        xb[((ks * 3 + 0) * 8 + xblk) * 64 + lp] = p0;
+        xb[((ks * 3 + 1) * 8 + xblk) * 64 + lp] = p1;
+        xb[((ks * 3 + 2) * 8 + xblk) * 64 + lp] = p2;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int idx = u + 256 * i, g = idx >> 6, ln = idx & 63, s = ln & 31, hh = ln >> 5;
+        const int c = 2 * (g & 3) + hh;
+        *reinterpret_cast<f32x4*>(gb + g * 256 + hh * 128 + (s ^ c) * 4) = r[i];
+      }
+    }
+  };
+  f32x16 acc[8];
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) acc[nb] = f32x16{};
+  float dbacc = 0.0f;
+  // A read: feature m = 32 wv + li -> g = 4 wv + (li >> 3), half (li >> 2) & 1, q = li & 3; sample 16 ks + 8 h + j
+  const int ag = 4 * wv + (li >> 3), ahh = (li >> 2) & 1, aq = li & 3, ac = 2 * (ag & 3) + ahh;
+  const int abase = ag * 256 + ahh * 128 + aq;
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  f32x4 r[8];
+  if (tl < nt) {
+    load_tile(r, tl);
+    stage(0, r, tl);
+  }
+  __syncthreads();
+  int buf = 0;
+  while (tl < nt) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
+    if (nxt < nt) load_tile(r, nxt);
+    const float* gb = wb3 + (size_t)buf * (WB3_BUF / 4);
+    const bf16x8* xb = reinterpret_cast<const bf16x8*>(gb + WB3_GF);
+    const int xl = lane ^ ((lane >> 3) & 3);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      float av[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int s = 16 * ks + 8 * h + j;
+        av[j] = gb[abase + (s ^ ac) * 4];
+        dbacc += av[j];
+      }
+      bf16x8 a0, a1, a2;
+      split3_bf16(av, a0, a1, a2);
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) {
+        const bf16x8 b0 = xb[((ks * 3 + 0) * 8 + nb) * 64 + xl];
+        const bf16x8 b1 = xb[((ks * 3 + 1) * 8 + nb) * 64 + xl];
+        const bf16x8 b2 = xb[((ks * 3 + 2) * 8 + nb) * 64 + xl];
+        f32x16 c = acc[nb];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c, 0, 0, 0);
+        acc[nb] = c;
+      }
+    }
+    if (nxt < nt) stage(buf ^ 1, r, nxt);
+    __syncthreads();
+    buf ^= 1;
+    tl = nxt;
+  }
+  constexpr int C = 256;
+  float* pb = part + (size_t)blockIdx.x * WgradCfg<0>::PART;
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) {
+    const int m = 32 * wv + (rr & 3) + 8 * (rr >> 2) + 4 * h;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) pb[(size_t)m * C + 32 * nb + li] = acc[nb][rr];
+  }
+  dbacc += __shfl_xor(dbacc, 32, 64);
+  if (h == 0) pb[(size_t)256 * C + 32 * wv + li] = dbacc;
+}
+
 struct GradTable {
   float* dst[34];
   int64_t off[34];
@@ -1933,6 +2282,8 @@ struct BwdWs {
   f32x4* enc;   // encoding tiles of a recomputed chunk (first layer -> skip layer)
   f16x8* wh;    // split-fp16 weight image for recomputation under train math 1/2
   int* sw;
+  f16x8* wth;   // split-fp16 W^T image of k_dgrad_h (train math 1/2)
+  float* tmax[2];   // per-tile max |dL/dh| of g[0] / g[1] ([tile][8])
   size_t bytes;
 };
 
@@ -1952,8 +2303,13 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
   const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257) * 8), oa = take((size_t)gacc_layout().total * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
+  const size_t owt = take(7 * HW_H * sizeof(f16x8));
+  const size_t otm0 = take(tiles * 8 * sizeof(float)), otm1 = take(tiles * 8 * sizeof(float));
   char* b = (char*)base;
   BwdWs w;
+  w.wth = (f16x8*)(b + owt);
+  w.tmax[0] = (float*)(b + otm0);
+  w.tmax[1] = (float*)(b + otm1);
   w.wh = (f16x8*)(b + owh);
   w.sw = (int*)(b + osw);
   for (int L = 0; L < 8; ++L) w.h[L] = (float*)(b + oh[L]);
@@ -1985,6 +2341,16 @@ static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int 
                      mu, part);
 }
 
+static void launch_wgrad_b3(unsigned blocks, hipStream_t s, int64_t n, const float* gin, const float* hprev,
+                            const float* mu, float* part) {
+  static bool attr = false;
+  if (!attr) {
+    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_b3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WB3_LDS));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_wgrad_b3, dim3(blocks), dim3(512), WB3_LDS, s, gin, hprev, mu, n, part);
+}
+
 }  // namespace pcn
 
 extern "C" size_t pcnerf_nof_backward_workspace_bytes(int64_t chunk) { return carve_bwd(nullptr, chunk).bytes; }
@@ -2001,7 +2367,11 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   const GaccLayout G = gacc_layout();
   hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wp);
-  if (g_train_math != 0) pack_weights(P, nullptr, ws.wh, ws.sw, s);   // the forward's arithmetic for recomputation
+  const bool split = g_train_math != 0;
+  if (split) {   // the forward's arithmetic for recomputation, and k_dgrad_h's W^T image
+    pack_weights(P, nullptr, ws.wh, ws.sw, s);
+    hipLaunchKernelGGL(k_pack_dgrad_h, dim3((unsigned)((7 * HW_H + 255) / 256)), dim3(256), 0, s, P, ws.sw, ws.wth);
+  }
   hipLaunchKernelGGL(k_pack_dgrad, dim3((unsigned)((DGRAD_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wt);
   PCN_HIP(hipMemsetAsync(ws.gacc, 0, (size_t)G.total * 8, s));
   const float mom = 0.0f;  // unused: the recomputation passes no running stats
@@ -2058,7 +2428,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       }
       hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, P.bn_w[7], P.out_w, ws.ostat, ws.gacc + G.g[7], ws.gacc + G.be[7],
-                         ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0]);
+                         ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0], split ? ws.tmax[0] : nullptr);
     }
     // 3. layers 7..1
     int cur = 0;
@@ -2068,6 +2438,8 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
         ProfScope ps(s, PT_BWD_WGRAD, 2.0 * 256.0 * (L == 4 ? 320 : 256) * dn, (L == 4 ? 2048.0 : 2048.0) * dn);
         if (L == 4)
           launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
+        else if (split)
+          launch_wgrad_b3(wblocks, s, n, ws.g[cur], hh[L - 1], coefp, ws.part);
         else
           launch_wgrad<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
                           ws.part);
@@ -2083,9 +2455,20 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       }
       {
         ProfScope ps(s, PT_BWD_DGRAD, 2.0 * 256 * 256 * dn, 3072.0 * dn);
-        hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
-                           hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1],
-                           ws.g[cur ^ 1]);
+        if (split && g_train_math == 1)
+          hipLaunchKernelGGL(k_dgrad_h<3>, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.tmax[cur],
+                             ws.wth + (size_t)(L - 1) * HW_H, ws.sw, L, hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp,
+                             P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1], ws.g[cur ^ 1],
+                             ws.tmax[cur ^ 1]);
+        else if (split)
+          hipLaunchKernelGGL(k_dgrad_h<4>, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.tmax[cur],
+                             ws.wth + (size_t)(L - 1) * HW_H, ws.sw, L, hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp,
+                             P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1], ws.g[cur ^ 1],
+                             ws.tmax[cur ^ 1]);
+        else
+          hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
+                             hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
+                             ws.gacc + G.be[L - 1], ws.g[cur ^ 1]);
       }
       cur ^= 1;
     }
