@@ -70,6 +70,22 @@ namespace pcn {
 #ifndef PCN_H_AHEAD
 #define PCN_H_AHEAD 1  // raw activation loads 1 or 2 tiles ahead
 #endif
+// k_wgrad_b3 schedule (column blocks of a half tile)
+#ifndef PCN_WB3_AREAD
+#define PCN_WB3_AREAD 3   // column block that reads the next half tile's A values (split two blocks later)
+#endif
+#ifndef PCN_WB3_STAGE
+#define PCN_WB3_STAGE 0   // column block of the first staging piece
+#endif
+#ifndef PCN_WB3_RB
+#define PCN_WB3_RB 1      // row blocks of 32 per wave (8 / RB waves per workgroup)
+#endif
+#ifndef PCN_WB3_SGB
+#define PCN_WB3_SGB 0     // > 0: sched_group_barrier interleave with this many VALU per MFMA
+#endif
+#ifndef PCN_WB3_SPACE
+#define PCN_WB3_SPACE 2   // column blocks between staging pieces
+#endif
 
 #ifndef PCN_CLOCK_STAMP
 #define PCN_CLOCK_STAMP 0  // diagnostic builds only: phase stamps of 1 k_train_ws, 2 k_wgrad (pcnerf_debug_clock)
@@ -2086,19 +2102,24 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
 // k_wgrad_b3: k_wgrad<0>'s G = sum_s dL/dh (x) (h_{L-1} - mean) with each fp32 operand split into three bf16 parts
 // (v = hi + mid + lo: all 24 bits of the fp32 value, bf16 keeps fp32's exponent range, so no scaling) and the six
 // products down to 2^-16 (hh, hm, mh, hl, lh, mm) on v_mfma_f32_32x32x16_bf16: the dropped ml, lm, ll are
-// <= 2^-23 relative, like fp32 rounding.  The contraction runs over samples, 16 per k-step, so an operand lane
-// needs 8 consecutive samples of one feature:
-//   x (B operand, read by all 8 waves): waves 4-7 stage it transposed and split, one thread per 4 features x 8
-//     samples (128 contiguous bytes of the tile), into [k-step 2][part 3][block 8][lane 64] bf16x8 with lane
-//     swizzle l ^ ((l >> 3) & 3) (conflict-free 16-byte writes and reads);
-//   dL/dh (A operand, read by its wave only): waves 0-3 copy the raw tile into LDS ([g][half][sample ^ c][4],
-//     c = 2 (g & 3) + half: conflict-free 4-byte reads) and each wave splits its 8 values per k-step itself.
-// Two buffers of 80 KiB (all 160 KiB of the CU's LDS); one barrier per tile; the next tile's loads are in flight
-// during the MFMAs.  Partials and db as k_wgrad<0> (k_wgrad_reduce<0> sums them).
-constexpr int WB3_GF = 8192;                                   // raw dL/dh floats per buffer
-constexpr int WB3_XV = 2 * 3 * 8 * 64;                         // split x bf16x8 per buffer
-constexpr size_t WB3_BUF = (size_t)WB3_GF * 4 + (size_t)WB3_XV * 16;   // 80 KiB
-constexpr size_t WB3_LDS = 2 * WB3_BUF;
+// <= 2^-23 relative, like fp32 rounding.  The contraction runs over samples, 16 per k-step, so the unit of work
+// is a half tile (16 samples, one k-step), and an operand lane needs 8 consecutive samples of one feature.  Every
+// thread loads 2 float4 of each operand per half tile (256-byte coalesced runs of the tile's [g][lane][4] order)
+// and stages them into a ring of three LDS buffers (44 KiB each), two half tiles ahead:
+//   x (B operand, read by all 8 waves): split, each part stored as [sample 16][feature 256] bf16 rows of 576 B;
+//     16-byte chunk c of row r at (c ^ ((r >> 1) & 3)) and its 8-byte halves swapped when r & 8: conflict-free
+//     8-byte writes, and ds_read_b64_tr_b16 reads (4 consecutive samples of the lane's feature, two per part)
+//     that are conflict-free and affine in the column block (one base VGPR, immediate offsets);
+//   dL/dh (A operand, read by its wave only): copied raw ([g][half][sample ^ c][4], c = 2 (g & 3) + half:
+//     conflict-free 4-byte reads), each wave splitting its 8 values per half tile itself.
+// One barrier per half tile.  Partials and db as k_wgrad<0> (k_wgrad_reduce<0> sums them).
+constexpr int WB3_PITCH = 576;                                  // x row bytes (512 + 64: conflict-free tr reads)
+constexpr int WB3_XPART = 16 * WB3_PITCH;                       // bytes per part of one half tile
+constexpr int WB3_GB = 16 * 256 * 4;                            // raw dL/dh bytes per half tile
+constexpr size_t WB3_BUF = (size_t)WB3_GB + 3 * WB3_XPART;      // 44 KiB
+constexpr size_t WB3_LDS = 3 * WB3_BUF;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
 #pragma unroll
@@ -2112,121 +2133,202 @@ __device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& hi, bf1
   }
 }
 
-__global__ __launch_bounds__(512, 1) void k_wgrad_b3(const float* __restrict__ gin, const float* __restrict__ hprev,
-                                                     const float* __restrict__ mu, int64_t n,
-                                                     float* __restrict__ part) {
+// byte offset of features f .. f+3 (f % 4 == 0) of row r (sample within the half tile) in one x part
+__device__ __forceinline__ int wb3_xoff(int r, int f) {
+  const int c = (f >> 3) ^ ((r >> 1) & 3);
+  const int half = ((f >> 2) & 1) ^ ((r >> 3) & 1);
+  return r * WB3_PITCH + 16 * c + 8 * half;
+}
+
+// RB: row blocks (32 features of dL/dh) per wave; 8 / RB waves per workgroup
+template <int RB>
+__global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restrict__ gin,
+                                                          const float* __restrict__ hprev,
+                                                          const float* __restrict__ mu, int64_t n,
+                                                          float* __restrict__ part) {
+  constexpr int NT = 512 / RB, NI = 2 * RB;   // threads; float4 per thread per operand and half tile
   extern __shared__ __attribute__((aligned(16))) float wb3[];
   const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  const bool xrole = wv >= 4;
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
-  // x role: u = t - 256 -> half th, group-in-block tg3, sample octet to, block blk; features 32 blk + 8 tg3 + 4 th + q
-  const int u = t & 255, th = u & 1, tg3 = (u >> 1) & 3, to = (u >> 3) & 3, xblk = u >> 5;
-  const int xg = 4 * xblk + tg3;
-  f32x4 mu4 = {};
-  if (xrole) mu4 = *reinterpret_cast<const f32x4*>(mu + 8 * xg + 4 * th);
-  // x role: 8 float4 at [xg][th 32 + 8 to + i]; g role: float4s u + 256 i of the tile ([g][lane])
-  auto load_tile = [&](f32x4 (&r)[8], int tile) {
-    if (xrole) {
-      const f32x4* p = reinterpret_cast<const f32x4*>(hprev + (size_t)tile * TILE_FLOATS) + xg * 64 + th * 32 + 8 * to;
+  const int tb = (int)(TILE_FLOATS * 4);
+  // staging map: float4 idx = t + NT i (i < NI) of a half tile hs: feature group sg = idx >> 5, HBM lane
+  // 32 shh + 16 hs + sl (shh = (idx >> 4) & 1, sl = idx & 15); buffer loads, offsets in SGPRs + one VGPR
+  const int sl = t & 15, shh = (t >> 4) & 1, sg0 = t >> 5;   // sg = sg0 + (NT / 32) i
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)gin, (short)0, nt * tb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)hprev, (short)0, nt * tb, 0x00020000);
+  const int voff = (sg0 * 64 + 32 * shh + sl) * 16;
+  auto load_half = [&](f32x4 (&rv)[2 * NI], int tile, int hs) {
+    const int so = tile * tb + hs * 256;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) r[i] = p[i];
-    } else {
-      const f32x4* p = reinterpret_cast<const f32x4*>(gin + (size_t)tile * TILE_FLOATS) + u;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) r[i] = p[256 * i];
+    for (int i = 0; i < NI; ++i) {
+      rv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, voff, so + NT * 32 * i, 0));
+      rv[NI + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, so + NT * 32 * i, 0));
     }
   };
-  auto stage = [&](int b, const f32x4 (&r)[8], int tile) {
-    float* gb = wb3 + (size_t)b * (WB3_BUF / 4);
-    if (xrole) {
-      bf16x8* xb = reinterpret_cast<bf16x8*>(gb + WB3_GF);
-      const int s0 = tile * 32 + 8 * to;
-      const int ks = to >> 1, hh = to & 1;
+  f32x4 mu2[NI];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float v[8];
+  for (int i = 0; i < NI; ++i) mu2[i] = *reinterpret_cast<const f32x4*>(mu + 8 * (sg0 + (NT / 32) * i) + 4 * shh);
+  // staging piece k of a half tile into buffer b: k even the dL/dh float4 i = k / 2, k odd the x float4 i
+  auto stage_piece = [&](int b, const f32x4 (&rv)[2 * NI], int tile, int hs, int k) {
+    char* base = reinterpret_cast<char*>(wb3) + (size_t)b * WB3_BUF;
+    const int i = k >> 1, g = sg0 + (NT / 32) * i;
+    if ((k & 1) == 0) {
+      const int c = 2 * (g & 3) + shh;
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + g * 128 + shh * 64 + (sl ^ c) * 4) = rv[i];
+      return;
+    }
+    char* xb = base + WB3_GB;
+    const bool valid = (int64_t)tile * 32 + 16 * hs + sl < n;
+    s16x4 p0, p1, p2;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (int64_t)s0 + i < n ? r[i][q] - mu4[q] : 0.0f;
-        bf16x8 p0, p1, p2;
-        split3_bf16(v, p0, p1, p2);
-        const int lp = 8 * tg3 + 4 * th + (q ^ tg3) + 32 * hh;   // swizzled lane of feature (f & 31), half hh
-        xb[((ks * 3 + 0) * 8 + xblk) * 64 + lp] = p0;
-        xb[((ks * 3 + 1) * 8 + xblk) * 64 + lp] = p1;
-        xb[((ks * 3 + 2) * 8 + xblk) * 64 + lp] = p2;
-      }
-    } else {
+    for (int q = 0; q < 4; ++q) {
+      const float v = valid ? rv[NI + i][q] - mu2[i][q] : 0.0f;
+      const __bf16 a = (__bf16)v;
+      const float r = v - (float)a;
+      const __bf16 bb = (__bf16)r;
+      p0[q] = __builtin_bit_cast(short, a);
+      p1[q] = __builtin_bit_cast(short, bb);
+      p2[q] = __builtin_bit_cast(short, (__bf16)(r - (float)bb));
+    }
+    const int off = wb3_xoff(sl, 8 * g + 4 * shh);
+    *reinterpret_cast<s16x4*>(xb + off) = p0;
+    *reinterpret_cast<s16x4*>(xb + WB3_XPART + off) = p1;
+    *reinterpret_cast<s16x4*>(xb + 2 * WB3_XPART + off) = p2;
+  };
+  f32x16 acc[RB][8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int idx = u + 256 * i, g = idx >> 6, ln = idx & 63, s = ln & 31, hh = ln >> 5;
-        const int c = 2 * (g & 3) + hh;
-        *reinterpret_cast<f32x4*>(gb + g * 256 + hh * 128 + (s ^ c) * 4) = r[i];
-      }
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) acc[rb][nb] = f32x16{};
+  float dbacc[RB] = {};
+  // A read: feature m = 32 (RB wv + rb) + li -> g = 4 (RB wv + rb) + (li >> 3), half (li >> 2) & 1, q = li & 3;
+  // row 8 h + j (the swizzle c = 2 (g & 3) + half does not depend on rb)
+  const int ag = 4 * RB * wv + (li >> 3), ahh = (li >> 2) & 1, aq = li & 3, ac = 2 * (ag & 3) + ahh;
+  const int abase = ag * 128 + ahh * 64 + aq;
+  // B transposed reads: 16-lane group (h, column half ch); lane 4 q + pp supplies row 8 h + 4 r + q, features
+  // 32 nb + 16 ch + 4 pp, and receives column (lane & 15) of the 4 rows
+  const int trq = (lane >> 2) & 3, trp = lane & 3, trch = (lane >> 4) & 1;
+  const int trow0 = 8 * h + trq;   // + 4 r
+  const int troff0 = wb3_xoff(trow0, 16 * trch + 4 * trp), troff1 = wb3_xoff(trow0 + 4, 16 * trch + 4 * trp);
+  // half tiles of this workgroup: u = 0, 1, ... -> tile blockIdx + (u >> 1) gridDim, half u & 1
+  const int tl0 = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  const int nh = tl0 < nt ? 2 * ((nt - 1 - tl0) / gstride + 1) : 0;
+  auto tile_of = [&](int u) { return tl0 + (u >> 1) * gstride; };
+  auto bufp = [&](int b) { return reinterpret_cast<const char*>(wb3) + (size_t)b * WB3_BUF; };
+  auto readA = [&](float (&av)[RB][8], int b) {
+    const float* gbuf = reinterpret_cast<const float*>(bufp(b));
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) av[rb][j] = gbuf[abase + 512 * rb + ((8 * h + j) ^ ac) * 4];
+  };
+  auto splitA = [&](float (&av)[RB][8], bf16x8 (&a)[RB][3], bool count) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dbacc[rb] += count ? av[rb][j] : 0.0f;
+      split3_bf16(av[rb], a[rb][0], a[rb][1], a[rb][2]);
     }
   };
-  f32x16 acc[8];
+  auto readB = [&](bf16x8 (&bv)[3], int b, int nb) {
+    const char* xb = bufp(b) + WB3_GB;
 #pragma unroll
-  for (int nb = 0; nb < 8; ++nb) acc[nb] = f32x16{};
-  float dbacc = 0.0f;
-  // A read: feature m = 32 wv + li -> g = 4 wv + (li >> 3), half (li >> 2) & 1, q = li & 3; sample 16 ks + 8 h + j
-  const int ag = 4 * wv + (li >> 3), ahh = (li >> 2) & 1, aq = li & 3, ac = 2 * (ag & 3) + ahh;
-  const int abase = ag * 256 + ahh * 128 + aq;
-  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
-  f32x4 r[8];
-  if (tl < nt) {
-    load_tile(r, tl);
-    stage(0, r, tl);
-  }
+    for (int p = 0; p < 3; ++p) {
+      const char* pb = xb + p * WB3_XPART + 64 * nb;
+      const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(__attribute__((address_space(3))) void*)(pb + troff0));
+      const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(__attribute__((address_space(3))) void*)(pb + troff1));
+      bv[p] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+  };
+  // Pipeline: half tile u computes from buffer u % 3 while half tile u + 2 is staged into buffer (u + 2) % 3 from
+  // registers loaded during u - 1 (pieces at column blocks S_P0 + k S_PD), the loads of u + 3 go out after the last
+  // piece, and u + 1's A operand and first B block are read (already staged and fenced) before the barrier.
+  f32x4 rv[2 * NI];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (u < nh) {
+      load_half(rv, tile_of(u), u & 1);
+#pragma unroll
+      for (int k = 0; k < 2 * NI; ++k) stage_piece(u, rv, tile_of(u), u & 1, k);
+    }
+  if (2 < nh) load_half(rv, tile_of(2), 0);
   __syncthreads();
-  int buf = 0;
-  while (tl < nt) {
-    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
-    if (nxt < nt) load_tile(r, nxt);
-    const float* gb = wb3 + (size_t)buf * (WB3_BUF / 4);
-    const bf16x8* xb = reinterpret_cast<const bf16x8*>(gb + WB3_GF);
-    const int xl = lane ^ ((lane >> 3) & 3);
+  constexpr int S_P0 = PCN_WB3_STAGE, S_PD = PCN_WB3_SPACE, S_APF = PCN_WB3_AREAD;
+  static_assert(S_P0 + (2 * NI - 1) * S_PD < 8, "staging pieces within the half tile");
+  bf16x8 Acur[RB][3], Anext[RB][3], B[2][3];
+  if (nh > 0) {
+    float av[RB][8];
+    readA(av, 0);
+    splitA(av, Acur, true);
+    readB(B[0], 0, 0);
+  }
+  int bcur = 0;
+  // the loop body is branch-free (a branch would split the scheduling regions the MFMA chains are interleaved in):
+  // past the end, the reads of half tile u + 1 and the staging of u + 2 touch buffers nobody reads afterwards, and
+  // the loads of u + 3 re-read the last half tile
+  for (int u = 0; u < nh; ++u) {
+    const int bn1 = bcur == 2 ? 0 : bcur + 1, bn2 = bcur == 0 ? 2 : bcur - 1;
+    const int u2 = u + 2 < nh ? u + 2 : nh - 1, u3 = u + 3 < nh ? u + 3 : nh - 1;
+    float av[RB][8];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      float av[8];
+    for (int nb = 0; nb < 8; ++nb) {
+      if (nb + 1 < 8) readB(B[(nb + 1) & 1], bcur, nb + 1);
+      else readB(B[0], bn1, 0);
+      if (nb == S_APF) readA(av, bn1);
+      if (nb == S_APF + 2) splitA(av, Anext, u + 1 < nh);
+      const bf16x8* bo = B[nb & 1];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int s = 16 * ks + 8 * h + j;
-        av[j] = gb[abase + (s ^ ac) * 4];
-        dbacc += av[j];
+      for (int rb = 0; rb < RB; ++rb) {
+        const bf16x8* a = Acur[rb];
+        f32x16 c = acc[rb][nb];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bo[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bo[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bo[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[0], c, 0, 0, 0);
+        acc[rb][nb] = c;
       }
-      bf16x8 a0, a1, a2;
-      split3_bf16(av, a0, a1, a2);
 #pragma unroll
-      for (int nb = 0; nb < 8; ++nb) {
-        const bf16x8 b0 = xb[((ks * 3 + 0) * 8 + nb) * 64 + xl];
-        const bf16x8 b1 = xb[((ks * 3 + 1) * 8 + nb) * 64 + xl];
-        const bf16x8 b2 = xb[((ks * 3 + 2) * 8 + nb) * 64 + xl];
-        f32x16 c = acc[nb];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c, 0, 0, 0);
-        acc[nb] = c;
+      for (int k = 0; k < 2 * NI; ++k)
+        if (nb == S_P0 + k * S_PD) stage_piece(bn2, rv, tile_of(u2), u2 & 1, k);
+      if (nb == S_P0 + (2 * NI - 1) * S_PD) load_half(rv, tile_of(u3), u3 & 1);
+      if (PCN_WB3_SGB) {   // interleave: each MFMA followed by an LDS read, some VALU, an LDS write
+#pragma unroll
+        for (int i = 0; i < 6 * RB; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, PCN_WB3_SGB, 0);
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        }
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (nxt < nt) stage(buf ^ 1, r, nxt);
     __syncthreads();
-    buf ^= 1;
-    tl = nxt;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) Acur[rb][p] = Anext[rb][p];
+    bcur = bn1;
   }
   constexpr int C = 256;
   float* pb = part + (size_t)blockIdx.x * WgradCfg<0>::PART;
 #pragma unroll
-  for (int rr = 0; rr < 16; ++rr) {
-    const int m = 32 * wv + (rr & 3) + 8 * (rr >> 2) + 4 * h;
+  for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb) pb[(size_t)m * C + 32 * nb + li] = acc[nb][rr];
+    for (int rr = 0; rr < 16; ++rr) {
+      const int m = 32 * (RB * wv + rb) + (rr & 3) + 8 * (rr >> 2) + 4 * h;
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) pb[(size_t)m * C + 32 * nb + li] = acc[rb][nb][rr];
+    }
+    float d = dbacc[rb] + __shfl_xor(dbacc[rb], 32, 64);
+    if (h == 0) pb[(size_t)256 * C + 32 * (RB * wv + rb) + li] = d;
   }
-  dbacc += __shfl_xor(dbacc, 32, 64);
-  if (h == 0) pb[(size_t)256 * C + 32 * wv + li] = dbacc;
 }
 
 struct GradTable {
@@ -2343,12 +2445,14 @@ static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int 
 
 static void launch_wgrad_b3(unsigned blocks, hipStream_t s, int64_t n, const float* gin, const float* hprev,
                             const float* mu, float* part) {
+  constexpr int RB = PCN_WB3_RB;
   static bool attr = false;
   if (!attr) {
-    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_b3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WB3_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_b3<RB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)WB3_LDS));
     attr = true;
   }
-  hipLaunchKernelGGL(k_wgrad_b3, dim3(blocks), dim3(512), WB3_LDS, s, gin, hprev, mu, n, part);
+  hipLaunchKernelGGL(k_wgrad_b3<RB>, dim3(blocks), dim3(512 / RB), WB3_LDS, s, gin, hprev, mu, n, part);
 }
 
 }  // namespace pcn
@@ -2435,7 +2539,8 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     for (int L = 7; L >= 1; --L) {
       const float* coefp = ws.coef + 1024 * (L - 1);
       {
-        ProfScope ps(s, PT_BWD_WGRAD, 2.0 * 256.0 * (L == 4 ? 320 : 256) * dn, (L == 4 ? 2048.0 : 2048.0) * dn);
+        ProfScope ps(s, split && L != 4 ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * (L == 4 ? 320 : 256) * dn,
+                     2048.0 * dn);
         if (L == 4)
           launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
         else if (split)

@@ -16,9 +16,10 @@ enum ProfTag {
   PT_SAMPLE = 8,       // k_sample_coarse / k_perturb
   PT_COMPOSITE_BWD = 9,// k_composite_bwd
   PT_BWD_WGRAD = 10,   // k_wgrad: weight-gradient GEMM partials (sum over samples on MFMA)
-  PT_BWD_DGRAD = 11,   // k_dgrad_ws: data-gradient GEMM + BatchNorm backward
+  PT_BWD_DGRAD = 11,   // k_dgrad_ws / k_dgrad_h: data-gradient GEMM + BatchNorm backward
   PT_BWD_MISC = 12,    // output-layer backward, partial reduction, BN statistics
   PT_EVAL_FOLD = 13,   // k_nof_eval_fold: exact affine fold of the eval network (opt-in)
+  PT_BWD_WGRAD_H = 14, // k_wgrad_b3: hidden-layer weight gradient under the split train math
 };
 extern bool g_prof_on;
 class ProfScope {

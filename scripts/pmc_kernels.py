@@ -20,3 +20,7 @@ for k, c in rows.items():
             if n in a:
                 out.append(f"{n[3:]}={100 * a[n] / a['SQ_WAVE_CYCLES']:.1f}%")
     print(" ".join(out))
+if len(sys.argv) > 2:   # raw per-launch averages of every counter for kernels whose name contains argv[2]
+    for k, c in rows.items():
+        if sys.argv[2] in k:
+            print(k[:60], {n: round(sum(v) / len(v)) for n, v in sorted(c.items())})
