@@ -2099,25 +2099,32 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
   }
 }
 
-// k_wgrad_b3: k_wgrad<0>'s G = sum_s dL/dh (x) (h_{L-1} - mean) with each fp32 operand split into three bf16 parts
+// k_wgrad_b3<RB, MODE>: k_wgrad<MODE>'s G = sum_s dL/dh (x) x with each fp32 operand split into three bf16 parts
 // (v = hi + mid + lo: all 24 bits of the fp32 value, bf16 keeps fp32's exponent range, so no scaling) and the six
 // products down to 2^-16 (hh, hm, mh, hl, lh, mm) on v_mfma_f32_32x32x16_bf16: the dropped ml, lm, ll are
-// <= 2^-23 relative, like fp32 rounding.  The contraction runs over samples, 16 per k-step, so the unit of work
-// is a half tile (16 samples, one k-step), and an operand lane needs 8 consecutive samples of one feature.  Every
-// thread loads 2 float4 of each operand per half tile (256-byte coalesced runs of the tile's [g][lane][4] order)
-// and stages them into a ring of three LDS buffers (44 KiB each), two half tiles ahead:
-//   x (B operand, read by all 8 waves): split, each part stored as [sample 16][feature 256] bf16 rows of 576 B;
-//     16-byte chunk c of row r at (c ^ ((r >> 1) & 3)) and its 8-byte halves swapped when r & 8: conflict-free
-//     8-byte writes, and ds_read_b64_tr_b16 reads (4 consecutive samples of the lane's feature, two per part)
-//     that are conflict-free and affine in the column block (one base VGPR, immediate offsets);
+// <= 2^-23 relative, like fp32 rounding.  x = h_{L-1} - mean (MODE 0, hidden layers), the encoding (MODE 1, layer
+// 0) or both (MODE 2, the skip layer: encoding columns first, as k_wgrad).  The contraction runs over samples, 16
+// per k-step, so the unit of work is a half tile (16 samples, one k-step), and an operand lane needs 8 consecutive
+// samples of one feature.  Every thread loads 2 float4 of each operand per half tile (256-byte coalesced runs of
+// the tile's [g][lane][4] order) and stages them into a ring of three LDS buffers, two half tiles ahead:
+//   x (B operand, read by all 8 waves): split, each part stored as [sample 16][feature] bf16 rows (pitch 2 x the
+//     feature count + 64 B); 16-byte chunk c of row r at (c ^ ((r >> 1) & 3)) and its 8-byte halves swapped when
+//     r & 8: conflict-free 8-byte writes, and ds_read_b64_tr_b16 reads (4 consecutive samples of the lane's
+//     feature, two per part) that are conflict-free and affine in the column block (immediate offsets); the
+//     encoding columns are computed while staging (enc_feats from the ray row, or the stored embedding row);
 //   dL/dh (A operand, read by its wave only): copied raw ([g][half][sample ^ c][4], c = 2 (g & 3) + half:
 //     conflict-free 4-byte reads), each wave splitting its 8 values per half tile itself.
-// One barrier per half tile.  Partials and db as k_wgrad<0> (k_wgrad_reduce<0> sums them).
-constexpr int WB3_PITCH = 576;                                  // x row bytes (512 + 64: conflict-free tr reads)
-constexpr int WB3_XPART = 16 * WB3_PITCH;                       // bytes per part of one half tile
-constexpr int WB3_GB = 16 * 256 * 4;                            // raw dL/dh bytes per half tile
-constexpr size_t WB3_BUF = (size_t)WB3_GB + 3 * WB3_XPART;      // 44 KiB
-constexpr size_t WB3_LDS = 3 * WB3_BUF;
+// One barrier per half tile.  Partials and db in k_wgrad<MODE>'s layout (k_wgrad_reduce<MODE> sums them).
+template <int MODE>
+struct Wb3Cfg {
+  static constexpr bool HX = MODE != 1, EX = MODE != 0;
+  static constexpr int NBLK = (EX ? 2 : 0) + (HX ? 8 : 0);        // 32-column blocks of G
+  static constexpr int PITCH = 64 * NBLK + 64;                     // x row bytes: 576, 192, 704
+  static constexpr int XPART = 16 * PITCH;
+  static constexpr int GB = 16 * 256 * 4;                          // raw dL/dh bytes per half tile
+  static constexpr size_t BUF = (size_t)GB + 3 * XPART;
+  static constexpr size_t LDS = 3 * BUF;
+};
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
@@ -2133,20 +2140,42 @@ __device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& hi, bf1
   }
 }
 
+__device__ __forceinline__ void split3_x4(const f32x4& v, s16x4& p0, s16x4& p1, s16x4& p2) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const __bf16 a = (__bf16)v[q];
+    const float r = v[q] - (float)a;
+    const __bf16 bb = (__bf16)r;
+    p0[q] = __builtin_bit_cast(short, a);
+    p1[q] = __builtin_bit_cast(short, bb);
+    p2[q] = __builtin_bit_cast(short, (__bf16)(r - (float)bb));
+  }
+}
+
 // byte offset of features f .. f+3 (f % 4 == 0) of row r (sample within the half tile) in one x part
+template <int PITCH>
 __device__ __forceinline__ int wb3_xoff(int r, int f) {
   const int c = (f >> 3) ^ ((r >> 1) & 3);
   const int half = ((f >> 2) & 1) ^ ((r >> 3) & 1);
-  return r * WB3_PITCH + 16 * c + 8 * half;
+  return r * PITCH + 16 * c + 8 * half;
 }
 
-// RB: row blocks (32 features of dL/dh) per wave; 8 / RB waves per workgroup
-template <int RB>
-__global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restrict__ gin,
+// RB: row blocks (32 features of dL/dh) per wave; 8 / RB waves per workgroup.  LAY: the k_wgrad mode whose partial
+// layout is written -- the skip layer (LAY 2) runs MODE 0 (its h columns, at column 64, and db) and MODE 1 (its
+// encoding columns): its 10 column blocks would not fit the accumulator registers of one launch
+template <int RB, int MODE, int LAY>
+__global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restrict__ rays, int stride,
+                                                          const float* __restrict__ z, int S, int64_t c0,
+                                                          const float* __restrict__ ein,
+                                                          const float* __restrict__ gin,
                                                           const float* __restrict__ hprev,
                                                           const float* __restrict__ mu, int64_t n,
                                                           float* __restrict__ part) {
+  using Cfg = Wb3Cfg<MODE>;
+  constexpr bool HX = Cfg::HX, EX = Cfg::EX;
+  constexpr int NBLK = Cfg::NBLK, PITCH = Cfg::PITCH, XPART = Cfg::XPART, GB = Cfg::GB;
   constexpr int NT = 512 / RB, NI = 2 * RB;   // threads; float4 per thread per operand and half tile
+  constexpr int HOFF = EX ? 64 : 0;           // first h feature column in the x image
   extern __shared__ __attribute__((aligned(16))) float wb3[];
   const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2156,52 +2185,85 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   // staging map: float4 idx = t + NT i (i < NI) of a half tile hs: feature group sg = idx >> 5, HBM lane
   // 32 shh + 16 hs + sl (shh = (idx >> 4) & 1, sl = idx & 15); buffer loads, offsets in SGPRs + one VGPR
   const int sl = t & 15, shh = (t >> 4) & 1, sg0 = t >> 5;   // sg = sg0 + (NT / 32) i
+  // encoding staging (EX): row er = t & 15, features 4 eq .. 4 eq + 3 (eq = (t >> 4) & 15; threads t and t + 256
+  // compute and store the same values)
+  const int er = t & 15, eq = (t >> 4) & 15;
   const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)gin, (short)0, nt * tb, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)hprev, (short)0, nt * tb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(HX ? hprev : gin), (short)0, nt * tb, 0x00020000);
   const int voff = (sg0 * 64 + 32 * shh + sl) * 16;
-  auto load_half = [&](f32x4 (&rv)[2 * NI], int tile, int hs) {
+  constexpr int NR = 2 * NI + (EX ? 2 : 0);   // staging registers (float4): dL/dh, x, ray row + z
+  auto sample_of = [&](int tile, int hs) {
+    int64_t s = (int64_t)tile * 32 + 16 * hs + er;
+    if (s >= n) s = n - 1;
+    return c0 + s;
+  };
+  auto load_half = [&](f32x4 (&rv)[NR], int tile, int hs) {
     const int so = tile * tb + hs * 256;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       rv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, voff, so + NT * 32 * i, 0));
-      rv[NI + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, so + NT * 32 * i, 0));
+      if (HX)
+        rv[NI + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, so + NT * 32 * i, 0));
+    }
+    if constexpr (EX) {   // the sample's ray origin, direction and z
+      if (ein) return;
+      const int64_t gs = sample_of(tile, hs);
+      const float* r = rays + (gs / S) * stride;
+      rv[2 * NI] = f32x4{r[0], r[1], r[2], r[3]};
+      rv[2 * NI + 1] = f32x4{r[4], r[5], z[gs], 0.0f};
     }
   };
   f32x4 mu2[NI];
 #pragma unroll
-  for (int i = 0; i < NI; ++i) mu2[i] = *reinterpret_cast<const f32x4*>(mu + 8 * (sg0 + (NT / 32) * i) + 4 * shh);
-  // staging piece k of a half tile into buffer b: k even the dL/dh float4 i = k / 2, k odd the x float4 i
-  auto stage_piece = [&](int b, const f32x4 (&rv)[2 * NI], int tile, int hs, int k) {
-    char* base = reinterpret_cast<char*>(wb3) + (size_t)b * WB3_BUF;
-    const int i = k >> 1, g = sg0 + (NT / 32) * i;
-    if ((k & 1) == 0) {
-      const int c = 2 * (g & 3) + shh;
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + g * 128 + shh * 64 + (sl ^ c) * 4) = rv[i];
+  for (int i = 0; i < NI; ++i)
+    mu2[i] = HX ? *reinterpret_cast<const f32x4*>(mu + 8 * (sg0 + (NT / 32) * i) + 4 * shh) : f32x4{};
+  // staging pieces of a half tile: k < NI the dL/dh float4 k; NI <= k < 2 NI the x float4 k - NI (HX); the
+  // encoding piece last (EX)
+  constexpr int NP = NI * (HX ? 2 : 1) + (EX ? 1 : 0);
+  auto stage_piece = [&](int b, const f32x4 (&rv)[NR], int tile, int hs, int k) {
+    char* base = reinterpret_cast<char*>(wb3) + (size_t)b * Cfg::BUF;
+    char* xb = base + GB;
+    if (k < NI) {
+      const int g = sg0 + (NT / 32) * k, c = 2 * (g & 3) + shh;
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + g * 128 + shh * 64 + (sl ^ c) * 4) = rv[k];
       return;
     }
-    char* xb = base + WB3_GB;
-    const bool valid = (int64_t)tile * 32 + 16 * hs + sl < n;
-    s16x4 p0, p1, p2;
+    s16x4 p0 = {}, p1 = {}, p2 = {};
+    int off = 0;
+    if (HX && k < 2 * NI) {
+      const int i = (k - NI) & (NI - 1), g = sg0 + (NT / 32) * i;
+      const bool valid = (int64_t)tile * 32 + 16 * hs + sl < n;
+      f32x4 v;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float v = valid ? rv[NI + i][q] - mu2[i][q] : 0.0f;
-      const __bf16 a = (__bf16)v;
-      const float r = v - (float)a;
-      const __bf16 bb = (__bf16)r;
-      p0[q] = __builtin_bit_cast(short, a);
-      p1[q] = __builtin_bit_cast(short, bb);
-      p2[q] = __builtin_bit_cast(short, (__bf16)(r - (float)bb));
+      for (int q = 0; q < 4; ++q) v[q] = valid ? rv[(NI + i) % NR][q] - mu2[i][q] : 0.0f;
+      split3_x4(v, p0, p1, p2);
+      off = wb3_xoff<PITCH>(sl, HOFF + 8 * g + 4 * shh);
+    } else if constexpr (EX) {
+      const bool valid = (int64_t)tile * 32 + 16 * hs + er < n;
+      f32x4 e;
+      if (ein) {
+        e = enc_feats_row(ein + sample_of(tile, hs) * 63, eq & 1, eq >> 1);
+      } else {
+        const f32x4 ra = rv[2 * NI], rb2 = rv[2 * NI + 1];   // {o0, o1, o2, d0}, {d1, d2, z, -}
+        const float zz = rb2[2];
+        float pp[3] = {ra[0] + ra[3] * zz, ra[1] + rb2[0] * zz, ra[2] + rb2[1] * zz};   // sample_point
+        e = enc_feats(pp, eq & 1, eq >> 1);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) e[q] = valid ? e[q] : 0.0f;
+      split3_x4(e, p0, p1, p2);
+      off = wb3_xoff<PITCH>(er, 4 * eq);
     }
-    const int off = wb3_xoff(sl, 8 * g + 4 * shh);
     *reinterpret_cast<s16x4*>(xb + off) = p0;
-    *reinterpret_cast<s16x4*>(xb + WB3_XPART + off) = p1;
-    *reinterpret_cast<s16x4*>(xb + 2 * WB3_XPART + off) = p2;
+    *reinterpret_cast<s16x4*>(xb + XPART + off) = p1;
+    *reinterpret_cast<s16x4*>(xb + 2 * XPART + off) = p2;
   };
-  f32x16 acc[RB][8];
+  f32x16 acc[RB][NBLK];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb) acc[rb][nb] = f32x16{};
+    for (int nb = 0; nb < NBLK; ++nb) acc[rb][nb] = f32x16{};
   float dbacc[RB] = {};
   // A read: feature m = 32 (RB wv + rb) + li -> g = 4 (RB wv + rb) + (li >> 3), half (li >> 2) & 1, q = li & 3;
   // row 8 h + j (the swizzle c = 2 (g & 3) + half does not depend on rb)
@@ -2211,12 +2273,13 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   // 32 nb + 16 ch + 4 pp, and receives column (lane & 15) of the 4 rows
   const int trq = (lane >> 2) & 3, trp = lane & 3, trch = (lane >> 4) & 1;
   const int trow0 = 8 * h + trq;   // + 4 r
-  const int troff0 = wb3_xoff(trow0, 16 * trch + 4 * trp), troff1 = wb3_xoff(trow0 + 4, 16 * trch + 4 * trp);
+  const int troff0 = wb3_xoff<PITCH>(trow0, 16 * trch + 4 * trp);
+  const int troff1 = wb3_xoff<PITCH>(trow0 + 4, 16 * trch + 4 * trp);
   // half tiles of this workgroup: u = 0, 1, ... -> tile blockIdx + (u >> 1) gridDim, half u & 1
   const int tl0 = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
   const int nh = tl0 < nt ? 2 * ((nt - 1 - tl0) / gstride + 1) : 0;
   auto tile_of = [&](int u) { return tl0 + (u >> 1) * gstride; };
-  auto bufp = [&](int b) { return reinterpret_cast<const char*>(wb3) + (size_t)b * WB3_BUF; };
+  auto bufp = [&](int b) { return reinterpret_cast<const char*>(wb3) + (size_t)b * Cfg::BUF; };
   auto readA = [&](float (&av)[RB][8], int b) {
     const float* gbuf = reinterpret_cast<const float*>(bufp(b));
 #pragma unroll
@@ -2233,10 +2296,10 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     }
   };
   auto readB = [&](bf16x8 (&bv)[3], int b, int nb) {
-    const char* xb = bufp(b) + WB3_GB;
+    const char* xb = bufp(b) + GB;
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
-      const char* pb = xb + p * WB3_XPART + 64 * nb;
+      const char* pb = xb + p * XPART + 64 * nb;
       const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) s16x4*)(__attribute__((address_space(3))) void*)(pb + troff0));
       const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -2247,18 +2310,20 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   // Pipeline: half tile u computes from buffer u % 3 while half tile u + 2 is staged into buffer (u + 2) % 3 from
   // registers loaded during u - 1 (pieces at column blocks S_P0 + k S_PD), the loads of u + 3 go out after the last
   // piece, and u + 1's A operand and first B block are read (already staged and fenced) before the barrier.
-  f32x4 rv[2 * NI];
+  f32x4 rv[NR];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
     if (u < nh) {
       load_half(rv, tile_of(u), u & 1);
 #pragma unroll
-      for (int k = 0; k < 2 * NI; ++k) stage_piece(u, rv, tile_of(u), u & 1, k);
+      for (int k = 0; k < NP; ++k) stage_piece(u, rv, tile_of(u), u & 1, k);
     }
   if (2 < nh) load_half(rv, tile_of(2), 0);
   __syncthreads();
-  constexpr int S_P0 = PCN_WB3_STAGE, S_PD = PCN_WB3_SPACE, S_APF = PCN_WB3_AREAD;
-  static_assert(S_P0 + (2 * NI - 1) * S_PD < 8, "staging pieces within the half tile");
+  constexpr int S_PD = NBLK / NP < PCN_WB3_SPACE ? NBLK / NP : PCN_WB3_SPACE;
+  constexpr int S_P0 = PCN_WB3_STAGE + (NP - 1) * S_PD < NBLK ? PCN_WB3_STAGE : 0;
+  constexpr int S_APF = PCN_WB3_AREAD < NBLK ? PCN_WB3_AREAD : NBLK - 1;
+  constexpr int S_ASP = S_APF + 2 < NBLK ? S_APF + 2 : NBLK - 1;
   bf16x8 Acur[RB][3], Anext[RB][3], B[2][3];
   if (nh > 0) {
     float av[RB][8];
@@ -2275,11 +2340,11 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     const int u2 = u + 2 < nh ? u + 2 : nh - 1, u3 = u + 3 < nh ? u + 3 : nh - 1;
     float av[RB][8];
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb) {
-      if (nb + 1 < 8) readB(B[(nb + 1) & 1], bcur, nb + 1);
+    for (int nb = 0; nb < NBLK; ++nb) {
+      if (nb + 1 < NBLK) readB(B[(nb + 1) & 1], bcur, nb + 1);
       else readB(B[0], bn1, 0);
       if (nb == S_APF) readA(av, bn1);
-      if (nb == S_APF + 2) splitA(av, Anext, u + 1 < nh);
+      if (nb == S_ASP) splitA(av, Anext, u + 1 < nh);
       const bf16x8* bo = B[nb & 1];
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
@@ -2294,19 +2359,9 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
         acc[rb][nb] = c;
       }
 #pragma unroll
-      for (int k = 0; k < 2 * NI; ++k)
+      for (int k = 0; k < NP; ++k)
         if (nb == S_P0 + k * S_PD) stage_piece(bn2, rv, tile_of(u2), u2 & 1, k);
-      if (nb == S_P0 + (2 * NI - 1) * S_PD) load_half(rv, tile_of(u3), u3 & 1);
-      if (PCN_WB3_SGB) {   // interleave: each MFMA followed by an LDS read, some VALU, an LDS write
-#pragma unroll
-        for (int i = 0; i < 6 * RB; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, PCN_WB3_SGB, 0);
-          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-        }
-      }
+      if (nb == S_P0 + (NP - 1) * S_PD) load_half(rv, tile_of(u3), u3 & 1);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
@@ -2316,18 +2371,20 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       for (int p = 0; p < 3; ++p) Acur[rb][p] = Anext[rb][p];
     bcur = bn1;
   }
-  constexpr int C = 256;
-  float* pb = part + (size_t)blockIdx.x * WgradCfg<0>::PART;
+  static_assert(MODE != 2 && (LAY == MODE || LAY == 2), "partial layouts");
+  constexpr int C = WgradCfg<LAY>::C, COL = (LAY == 2 && MODE == 0) ? 64 : 0;
+  constexpr bool DB = MODE == 0 || LAY == 1;
+  float* pb = part + (size_t)blockIdx.x * WgradCfg<LAY>::PART;
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
     for (int rr = 0; rr < 16; ++rr) {
       const int m = 32 * (RB * wv + rb) + (rr & 3) + 8 * (rr >> 2) + 4 * h;
 #pragma unroll
-      for (int nb = 0; nb < 8; ++nb) pb[(size_t)m * C + 32 * nb + li] = acc[rb][nb][rr];
+      for (int nb = 0; nb < NBLK; ++nb) pb[(size_t)m * C + COL + 32 * nb + li] = acc[rb][nb][rr];
     }
     float d = dbacc[rb] + __shfl_xor(dbacc[rb], 32, 64);
-    if (h == 0) pb[(size_t)256 * C + 32 * (RB * wv + rb) + li] = d;
+    if (DB && h == 0) pb[(size_t)256 * C + 32 * (RB * wv + rb) + li] = d;
   }
 }
 
@@ -2443,16 +2500,31 @@ static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int 
                      mu, part);
 }
 
-static void launch_wgrad_b3(unsigned blocks, hipStream_t s, int64_t n, const float* gin, const float* hprev,
-                            const float* mu, float* part) {
-  constexpr int RB = PCN_WB3_RB;
+template <int MODE, int LAY>
+static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
+                                int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
+                                const float* mu, float* part) {
+  constexpr int RB = MODE == 0 ? PCN_WB3_RB : 1;
+  constexpr size_t lds = Wb3Cfg<MODE>::LDS;
   static bool attr = false;
   if (!attr) {
-    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_b3<RB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)WB3_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_b3<RB, MODE, LAY>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL(k_wgrad_b3<RB>, dim3(blocks), dim3(512 / RB), WB3_LDS, s, gin, hprev, mu, n, part);
+  hipLaunchKernelGGL((k_wgrad_b3<RB, MODE, LAY>), dim3(blocks), dim3(512 / RB), lds, s, rays, stride, z, S, c0, ein,
+                     gin, hprev, mu, n, part);
+}
+
+// the weight-gradient partials of k_wgrad<MODE> under the split train math
+template <int MODE>
+static void launch_wgrad_b3(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
+                            int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
+                            const float* mu, float* part) {
+  if constexpr (MODE != 1)
+    launch_wgrad_b3_one<0, MODE>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, part);
+  if constexpr (MODE != 0)
+    launch_wgrad_b3_one<1, MODE>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, part);
 }
 
 }  // namespace pcn
@@ -2539,12 +2611,16 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     for (int L = 7; L >= 1; --L) {
       const float* coefp = ws.coef + 1024 * (L - 1);
       {
-        ProfScope ps(s, split && L != 4 ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * (L == 4 ? 320 : 256) * dn,
+        ProfScope ps(s, split ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * (L == 4 ? 320 : 256) * dn,
                      2048.0 * dn);
-        if (L == 4)
-          launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
+        if (split && L == 4)
+          launch_wgrad_b3<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp,
+                             ws.part);
         else if (split)
-          launch_wgrad_b3(wblocks, s, n, ws.g[cur], hh[L - 1], coefp, ws.part);
+          launch_wgrad_b3<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
+                             ws.part);
+        else if (L == 4)
+          launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
         else
           launch_wgrad<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
                           ws.part);
@@ -2579,8 +2655,13 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     }
     // 4. layer 0 on the encoding
     {
-      ProfScope ps(s, PT_BWD_WGRAD, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
-      launch_wgrad<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr, ws.part);
+      ProfScope ps(s, split ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
+      if (split)
+        launch_wgrad_b3<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
+                           ws.part);
+      else
+        launch_wgrad<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
+                        ws.part);
     }
     {
       ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<1>::PART * 4.0);
