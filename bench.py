@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-rays", type=int, default=None,
                     help="bounded CPU-baseline sample (rays; default 4096, 1024 for train_step, 512 groups for view)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32-line", action="store_true",
+                    help="skip the comparison run of the train lines under the fp32 MFMA train math (profiling)")
     ap.add_argument("--fold", action="store_true",
                     help="val/view only: the opt-in exact affine fold of the eval network (SURVEY fact 1), reported "
                          "as its own line, never the headline")
@@ -342,7 +344,7 @@ def main(argv=None):
 
     # the same workload with the train-mode layers on the fp32 MFMA pipe (train_math "fp32"), for comparison
     fp32_line = None
-    if train and train_math != "fp32":
+    if train and train_math != "fp32" and not a.no_fp32_line:
         _ops.set_train_math("fp32")
         el32, _ = timed(a.steps, 1)
         roof32, k32 = kernel_report(L, a, "fp32")

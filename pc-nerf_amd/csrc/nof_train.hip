@@ -2185,9 +2185,8 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   // staging map: float4 idx = t + NT i (i < NI) of a half tile hs: feature group sg = idx >> 5, HBM lane
   // 32 shh + 16 hs + sl (shh = (idx >> 4) & 1, sl = idx & 15); buffer loads, offsets in SGPRs + one VGPR
   const int sl = t & 15, shh = (t >> 4) & 1, sg0 = t >> 5;   // sg = sg0 + (NT / 32) i
-  // encoding staging (EX): row er = t & 15, features 4 eq .. 4 eq + 3 (eq = (t >> 4) & 15; threads t and t + 256
-  // compute and store the same values)
-  const int er = t & 15, eq = (t >> 4) & 15;
+  // encoding staging (EX): row er = t & 15, sincos task ej = t >> 4
+  const int er = t & 15, ej = t >> 4;
   const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)gin, (short)0, nt * tb, 0x00020000);
   const __amdgpu_buffer_rsrc_t rx =
       __builtin_amdgcn_make_buffer_rsrc((void*)(HX ? hprev : gin), (short)0, nt * tb, 0x00020000);
@@ -2240,20 +2239,44 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       split3_x4(v, p0, p1, p2);
       off = wb3_xoff<PITCH>(sl, HOFF + 8 * g + 4 * shh);
     } else if constexpr (EX) {
+      // one sincos per thread: row er, task ej < 30 -> 2^k p[m] (k = ej / 3, m = ej % 3) feeding features
+      // 3 + 6 k + m (sin) and 6 + 6 k + m (cos); ej == 30: x, y, z and the zero pad 63; ej == 31 idle
       const bool valid = (int64_t)tile * 32 + 16 * hs + er < n;
-      f32x4 e;
-      if (ein) {
-        e = enc_feats_row(ein + sample_of(tile, hs) * 63, eq & 1, eq >> 1);
-      } else {
+      const int64_t gs = sample_of(tile, hs);
+      float pp[3];
+      if (!ein) {
         const f32x4 ra = rv[2 * NI], rb2 = rv[2 * NI + 1];   // {o0, o1, o2, d0}, {d1, d2, z, -}
         const float zz = rb2[2];
-        float pp[3] = {ra[0] + ra[3] * zz, ra[1] + rb2[0] * zz, ra[2] + rb2[1] * zz};   // sample_point
-        e = enc_feats(pp, eq & 1, eq >> 1);
+        pp[0] = ra[0] + ra[3] * zz;   // sample_point
+        pp[1] = ra[1] + rb2[0] * zz;
+        pp[2] = ra[2] + rb2[1] * zz;
       }
+      auto put1 = [&](int f, float v) {
+        s16x4 q0, q1, q2;
+        split3_x4(f32x4{valid ? v : 0.0f, 0.0f, 0.0f, 0.0f}, q0, q1, q2);
+        const int o = wb3_xoff<PITCH>(er, f & ~3) + 2 * (f & 3);
+        *reinterpret_cast<short*>(xb + o) = q0[0];
+        *reinterpret_cast<short*>(xb + XPART + o) = q1[0];
+        *reinterpret_cast<short*>(xb + 2 * XPART + o) = q2[0];
+      };
+      if (ej < 30) {
+        const int k = ej / 3, m = ej - 3 * k;
+        float sn, cs;
+        if (ein) {
+          sn = ein[gs * 63 + 3 + 6 * k + m];
+          cs = ein[gs * 63 + 6 + 6 * k + m];
+        } else {
+          const float pm = m == 0 ? pp[0] : m == 1 ? pp[1] : pp[2];
+          sincosf(__int_as_float((127 + k) << 23) * pm, &sn, &cs);   // encode_half's (float)(1 << k) * p[m]
+        }
+        put1(3 + 6 * k + m, sn);
+        put1(6 + 6 * k + m, cs);
+      } else if (ej == 30) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) e[q] = valid ? e[q] : 0.0f;
-      split3_x4(e, p0, p1, p2);
-      off = wb3_xoff<PITCH>(er, 4 * eq);
+        for (int c = 0; c < 3; ++c) put1(c, ein ? ein[gs * 63 + c] : pp[c]);
+        put1(63, 0.0f);
+      }
+      return;
     }
     *reinterpret_cast<s16x4*>(xb + off) = p0;
     *reinterpret_cast<s16x4*>(xb + XPART + off) = p1;
