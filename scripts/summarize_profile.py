@@ -8,6 +8,7 @@ import collections
 import csv
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -18,8 +19,23 @@ dst = "profiles"
 os.makedirs(dst, exist_ok=True)
 
 
+def demangle(name):
+    """rocprofv3 leaves names with fp16/bf16 vector parameters mangled (and c++filt here cannot read them): the
+    pcn:: kernel name and its integer / bool template arguments are all this needs."""
+    m = re.match(r"_ZN3pcn(\d+)", name)
+    if not m:
+        return name
+    i = m.end()
+    n = int(m.group(1))
+    ident, i = name[i:i + n], i + n
+    if i < len(name) and name[i] == "I":
+        args = re.findall(r"L([ib])(\d+)E", name[i + 1:name.find("EE", i) + 1])
+        ident += "<" + ",".join(("true" if v == "1" else "false") if t == "b" else v for t, v in args) + ">"
+    return "pcn::" + ident + "()"
+
+
 def short(name):
-    n = name.split("(")[0].replace("void ", "").replace("pcn::", "")
+    n = demangle(name).split("(")[0].replace("void ", "").replace("pcn::", "")
     return n.replace(" ", "")
 
 
