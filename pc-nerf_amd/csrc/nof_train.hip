@@ -67,6 +67,9 @@ namespace pcn {
 #ifndef PCN_H_DMA
 #define PCN_H_DMA 0  // hidden layers: k_train_hd (raw tiles by LDS-DMA two tiles ahead)
 #endif
+#ifndef PCN_H_REV
+#define PCN_H_REV 0xAA   // bit L: layer L traverses its chunk's tiles in reverse order
+#endif
 #ifndef PCN_H_AHEAD
 #define PCN_H_AHEAD 1  // raw activation loads 1 or 2 tiles ahead
 #endif
@@ -591,6 +594,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   const float unscale = ldexpf(1.0f, -(swp[layer] + sx));
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
+  // tile order: odd layers walk the chunk backwards, so a layer first reads the tiles its predecessor wrote last
+  // (still in the memory-side cache) -- P maps the loop's tile to the tile of the chunk
+  const bool rev = (PCN_H_REV >> layer) & 1;
+  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
   // staging identity: the HBM lane (sample ls + 32 hs) whose float4s this thread stages; PCN_H_LMAP interleaves
   // the halves across neighbouring lanes so each 16-lane group's 8-byte LDS writes cover 128 contiguous bytes
@@ -646,11 +653,11 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   auto load_tile = [&](f32x4 (&v)[4], int tile) {
 #pragma unroll
     for (int m = 0; m < 4; ++m)
-      v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)tile * TILE_FLOATS)[(t & ~63) + sln + 512 * m];
+      v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)P(tile) * TILE_FLOATS)[(t & ~63) + sln + 512 * m];
   };
   const int etix = (t & ~63) + sln;   // this thread's encoding float4 in a stored tile [g][HBM lane]
   auto sample_of = [&](int tile) {
-    int64_t sl = (int64_t)tile * 32 + ls;
+    int64_t sl = (int64_t)P(tile) * 32 + ls;
     if (sl >= n) sl = n - 1;
     return c0 + sl;
   };
@@ -666,7 +673,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       const int64_t gs = sample_of(tl);
       f32x4 e;
       if (ETIN) {
-        e = etin[(size_t)tl * 512 + etix];
+        e = etin[(size_t)P(tl) * 512 + etix];
       } else if (ein) {
         e = enc_feats_row(ein + gs * 63, hs, t >> 6);
       } else {
@@ -675,11 +682,12 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
         e = enc_feats(p, hs, t >> 6);
       }
       put_enc(0, e);
-      if (ETOUT) etout[(size_t)tl * 512 + etix] = e;
+      if (ETOUT) etout[(size_t)P(tl) * 512 + etix] = e;
     }
   }
   __syncthreads();
-  auto epi = [&](const f32x16& pacc, int ptile, int j) {
+  auto epi = [&](const f32x16& pacc, int ptile_l, int j) {
+    const int ptile = P(ptile_l);
     const bool valid = (int64_t)ptile * 32 + li < n;
     const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
     f32x4 s1 = my_st[(2 * j) ^ st_sw], s2 = my_st[(2 * j + 1) ^ st_sw];
@@ -699,7 +707,8 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   };
   // AHEAD == 2: the raw loads run two tiles ahead (vload gets tile + 2 gstride while vstage, loaded one
   // tile earlier, is staged for tile + gstride); == 1: loaded and staged within the same tile
-  auto epir = [&](const f32x16& acc, int tile, int j) {   // REGSTAT epilogue
+  auto epir = [&](const f32x16& acc, int tile_l, int j) {   // REGSTAT epilogue
+    const int tile = P(tile_l);
     const bool valid = (int64_t)tile * 32 + li < n;
     const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
     f32x4 o;
@@ -738,7 +747,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
       if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
-      if (ETIN && ks == KS - 4 && more) ev = etin[(size_t)nxt * 512 + etix];
+      if (ETIN && ks == KS - 4 && more) ev = etin[(size_t)P(nxt) * 512 + etix];
       if (ETOUT && ks == 0 && more && !ein) {
         const int64_t gs = sample_of(nxt);
         const float* r = rays + (gs / S) * stride;
@@ -788,7 +797,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
           e = enc_feats(p, hs, t >> 6);
         }
         put_enc(buf ^ 1, e);
-        if (ETOUT) etout[(size_t)nxt * 512 + etix] = e;
+        if (ETOUT) etout[(size_t)P(nxt) * 512 + etix] = e;
       }
       __builtin_amdgcn_sched_barrier(0);
     }

@@ -111,9 +111,10 @@ def fold_eval(model, device) -> torch.Tensor:
     return out
 
 
-# Arithmetic of the train-mode Linear layers (pcnerf_set_train_math): fp32 operands split into two fp16 parts
-# (22 significant bits) with exact products on the fp16 matrix pipe and fp32 accumulation, "f16x2_3" (default:
-# hi*hi + hi*mid + mid*hi) or "f16x2_4" (+ mid*mid), or "fp32" (fp32 MFMA).
+# Arithmetic of the train-mode MLP, forward and backward (pcnerf_set_train_math): fp32 operands split into two fp16
+# parts (22 significant bits) with exact products on the fp16 matrix pipe and fp32 accumulation, "f16x2_3"
+# (default: hi*hi + hi*mid + mid*hi) or "f16x2_4" (+ mid*mid) -- the weight gradients under either as three bf16
+# parts and six products -- or "fp32" (fp32 MFMA throughout).
 TRAIN_MATH = {"fp32": 0, "f16x2_3": 1, "f16x2_4": 2}
 
 
