@@ -61,14 +61,14 @@ namespace pcn {
 #ifndef PCN_H_LMAP
 #define PCN_H_LMAP 0   // staging lane map (conflict-free 8-byte LDS writes)
 #endif
+#ifndef PCN_H_WENC
+#define PCN_H_WENC 1  // skip layer: encoding weights in LDS, REGSTAT form
+#endif
 #ifndef PCN_H_REGSTAT
 #define PCN_H_REGSTAT 1  // hidden layers: running statistics in registers, epilogue after each tile's MFMAs
 #endif
 #ifndef PCN_H_DMA
 #define PCN_H_DMA 0  // hidden layers: k_train_hd (raw tiles by LDS-DMA two tiles ahead)
-#endif
-#ifndef PCN_H_REV
-#define PCN_H_REV 0xAA   // bit L: layer L traverses its chunk's tiles in reverse order
 #endif
 #ifndef PCN_H_AHEAD
 #define PCN_H_AHEAD 1  // raw activation loads 1 or 2 tiles ahead
@@ -560,13 +560,17 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   constexpr int AHEAD = (KE && HP) ? 1 : PCN_H_AHEAD;   // the skip layer's 160 weight registers leave no room
   // REGSTAT: each tile's epilogue right after its MFMAs, the per-lane running statistics in registers (no LDS
   // read-modify-write per tile, one accumulator set); the B buffers double as the final reduction area
-  constexpr bool REGSTAT = HP && !KE && PCN_H_REGSTAT;   // (the skip layer would spill)
+  // WENC (skip layer): the encoding k-steps' weights live in LDS, read two k-steps ahead, instead of 32 registers --
+  // which lets the skip layer take the REGSTAT form as well
+  constexpr bool WENC = KE && HP && PCN_H_WENC;
+  constexpr bool REGSTAT = HP && (!KE || WENC) && PCN_H_REGSTAT;
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
   __shared__ float smax[8];
   __shared__ f16x8 xs[2][KS][2][64];
   __shared__ f32x4 sred_[REGSTAT ? 1 : 8 * 64 * 8];   // per-lane running statistics, as k_train_ws
+  __shared__ f16x8 wenc_[WENC ? HW_E : 1];
   static_assert(!REGSTAT || sizeof(xs) >= 8 * 64 * 8 * sizeof(f32x4), "reduction area");
   f32x4* const sred = REGSTAT ? reinterpret_cast<f32x4*>(&xs[0][0][0][0]) : sred_;
   const int t = threadIdx.x;
@@ -591,12 +595,12 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     sx = sx > 24 ? 24 : sx;
   }
   const float xscale = ldexpf(1.0f, sx);
-  const float unscale = ldexpf(1.0f, -(swp[layer] + sx));
+  const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
   // tile order: odd layers walk the chunk backwards, so a layer first reads the tiles its predecessor wrote last
   // (still in the memory-side cache) -- P maps the loop's tile to the tile of the chunk
-  const bool rev = (PCN_H_REV >> layer) & 1;
+  const bool rev = !KE && ((layer >> 8) & 1);   // (the first and skip layers keep the forward walk: registers)
   auto P = [&](int x) { return rev ? nt - 1 - x : x; };
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
   // staging identity: the HBM lane (sample ls + 32 hs) whose float4s this thread stages; PCN_H_LMAP interleaves
@@ -608,10 +612,13 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   {
     const f16x8* __restrict__ w8 = Wp + lane;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+    for (int ks = WENC ? KSE : 0; ks < KS; ++ks)
 #pragma unroll
       for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 8 + blk) * 2 + p) * 64];
+    if (WENC)
+      for (int j = t; j < (int)HW_E; j += 512) wenc_[j] = Wp[j];
   }
+  auto wenc = [&](int ks, int p) { return wenc_[((ks * 8 + blk) * 2 + p) * 64 + lane]; };
   f32x4* const my_st = sred + (blk * 64 + lane) * 8;
   const int st_sw = (lane >> 1) & 7;
   f32x4 rs[8];   // REGSTAT: chunk 2j = sum d, 2j+1 = sum d^2 of accumulator registers 4j..4j+3
@@ -731,6 +738,13 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     f32x4 vloc[4];   // AHEAD == 1: this tile's loads of the next tile
     float rr[7];
     f32x4 ev;
+    f16x8 we[2][2];   // WENC: weights of encoding k-steps ks, ks + 1
+    if (WENC) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) we[d][p] = wenc(d, p);
+    }
 #pragma unroll
     for (int d = 0; d < XD - 1; ++d) {
       xr[d][0] = xs[buf][d][0][lane];
@@ -743,10 +757,16 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
         xr[(ks + XD - 1) % XD][1] = xs[buf][ks + XD - 1][1][lane];
       }
       const f16x8 xh = xr[ks % XD][0], xm = xr[ks % XD][1];
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xh, ks == 0 ? f32x16{} : acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
-      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
+      const bool wl = WENC && ks < KSE;
+      const f16x8 w0 = wl ? we[ks & 1][0] : wr[ks][0], w1 = wl ? we[ks & 1][1] : wr[ks][1];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0, xh, ks == 0 ? f32x16{} : acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0, xm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w1, xh, acc, 0, 0, 0);
+      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w1, xm, acc, 0, 0, 0);
+      if (WENC && ks + 2 < KSE) {
+        we[ks & 1][0] = wenc(ks + 2, 0);
+        we[ks & 1][1] = wenc(ks + 2, 1);
+      }
       if (ETIN && ks == KS - 4 && more) ev = etin[(size_t)P(nxt) * 512 + etix];
       if (ETOUT && ks == 0 && more && !ein) {
         const int64_t gs = sample_of(nxt);
@@ -1144,6 +1164,18 @@ struct TrainLayerLaunch {
   hipStream_t s;
 };
 
+// Tile order of the split train layers: bit L of the mask reverses layer L's walk over its chunk (default: the
+// odd hidden layers, so each hidden layer first reads the tiles its predecessor wrote last); PCNERF_TILE_REV
+// overrides it (A/B runs).
+static int tile_rev(int L) {
+  static int mask = -1;
+  if (mask < 0) {
+    const char* e = getenv("PCNERF_TILE_REV");
+    mask = e ? (int)strtol(e, nullptr, 0) : 0xAA;
+  }
+  return (mask >> L) & 1;
+}
+
 template <int KE, bool HP>
 static void launch_layer(const TrainLayerLaunch& q, const NofParamsDev& P, const float* wp, const f16x8* wh,
                          const int* sw, int L, const float* hin, const BnPrev& prev, float* hout, double* stats,
@@ -1161,12 +1193,12 @@ static void launch_layer(const TrainLayerLaunch& q, const NofParamsDev& P, const
                          P.lin_b[L], prev, q.mom, q.eps, hout, stats);
   } else if (m == 1) {
     hipLaunchKernelGGL((k_train_h<KE, HP, 3>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0,
-                       q.ein, hin, q.n, wh + off_h(L, KE != 0), sw, L, P.lin_b[L], prev, q.mom, q.eps, hout, stats,
-                       etin, etout);
+                       q.ein, hin, q.n, wh + off_h(L, KE != 0), sw, L | (tile_rev(L) << 8), P.lin_b[L], prev, q.mom,
+                       q.eps, hout, stats, etin, etout);
   } else {
     hipLaunchKernelGGL((k_train_h<KE, HP, 4>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0,
-                       q.ein, hin, q.n, wh + off_h(L, KE != 0), sw, L, P.lin_b[L], prev, q.mom, q.eps, hout, stats,
-                       etin, etout);
+                       q.ein, hin, q.n, wh + off_h(L, KE != 0), sw, L | (tile_rev(L) << 8), P.lin_b[L], prev, q.mom,
+                       q.eps, hout, stats, etin, etout);
   }
 }
 
