@@ -61,6 +61,15 @@ namespace pcn {
 #ifndef PCN_H_LMAP
 #define PCN_H_LMAP 0   // staging lane map (conflict-free 8-byte LDS writes)
 #endif
+#ifndef PCN_H_WLDS
+#define PCN_H_WLDS 0  // hidden layers: k-steps of weights read from LDS instead of registers
+#endif
+#ifndef PCN_H_ABL
+#define PCN_H_ABL 0   // timing-only ablations of the hidden layer: 1 no stores, 2 no loads, 4 no staging, 8 no barrier
+#endif
+#ifndef PCN_H1
+#define PCN_H1 1      // forward without activation store: layer 1 recomputes h0 from the encoding tiles
+#endif
 #ifndef PCN_H_WENC
 #define PCN_H_WENC 1  // skip layer: encoding weights in LDS, REGSTAT form
 #endif
@@ -557,20 +566,23 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   // HP: the next tile's raw loads, their staging (BatchNorm + split + LDS), the previous tile's epilogue
   constexpr int S_LOAD = PCN_H_LOAD, S_STAGE0 = KS - PCN_H_STAGE, S_STAGE1 = S_STAGE0 + 1;
   constexpr int S_EPI = PCN_H_EPI;
-  constexpr int AHEAD = (KE && HP) ? 1 : PCN_H_AHEAD;   // the skip layer's 160 weight registers leave no room
+  constexpr int AHEAD = (KE && HP) ? 1 : PCN_H_AHEAD;   // the skip layer's weight registers leave no room
   // REGSTAT: each tile's epilogue right after its MFMAs, the per-lane running statistics in registers (no LDS
   // read-modify-write per tile, one accumulator set); the B buffers double as the final reduction area
   // WENC (skip layer): the encoding k-steps' weights live in LDS, read two k-steps ahead, instead of 32 registers --
   // which lets the skip layer take the REGSTAT form as well
   constexpr bool WENC = KE && HP && PCN_H_WENC;
   constexpr bool REGSTAT = HP && (!KE || WENC) && PCN_H_REGSTAT;
+  // NWL: k-steps whose weights come from LDS (two k-steps ahead) -- the skip layer's encoding k-steps (WENC), or
+  // the hidden layer's first PCN_H_WLDS (registers for loads two tiles ahead)
+  constexpr int NWL = WENC ? KSE : (HP && !KE) ? PCN_H_WLDS : 0;
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
   __shared__ float smax[8];
   __shared__ f16x8 xs[2][KS][2][64];
   __shared__ f32x4 sred_[REGSTAT ? 1 : 8 * 64 * 8];   // per-lane running statistics, as k_train_ws
-  __shared__ f16x8 wenc_[WENC ? HW_E : 1];
+  __shared__ f16x8 wenc_[NWL ? NWL * 8 * 2 * 64 : 1];
   static_assert(!REGSTAT || sizeof(xs) >= 8 * 64 * 8 * sizeof(f32x4), "reduction area");
   f32x4* const sred = REGSTAT ? reinterpret_cast<f32x4*>(&xs[0][0][0][0]) : sred_;
   const int t = threadIdx.x;
@@ -612,11 +624,11 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   {
     const f16x8* __restrict__ w8 = Wp + lane;
 #pragma unroll
-    for (int ks = WENC ? KSE : 0; ks < KS; ++ks)
+    for (int ks = NWL; ks < KS; ++ks)
 #pragma unroll
       for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 8 + blk) * 2 + p) * 64];
-    if (WENC)
-      for (int j = t; j < (int)HW_E; j += 512) wenc_[j] = Wp[j];
+    if (NWL)
+      for (int j = t; j < NWL * 8 * 2 * 64; j += 512) wenc_[j] = Wp[j];
   }
   auto wenc = [&](int ks, int p) { return wenc_[((ks * 8 + blk) * 2 + p) * 64 + lane]; };
   f32x4* const my_st = sred + (blk * 64 + lane) * 8;
@@ -709,8 +721,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     }
     my_st[(2 * j) ^ st_sw] = s1;
     my_st[(2 * j + 1) ^ st_sw] = s2;
-    float* base = hout + (size_t)ptile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
-    reinterpret_cast<f32x4*>(base)[lane] = o;
+    if (hout) {   // (the first layer runs statistics-only when k_train_h1 recomputes its output)
+      float* base = hout + (size_t)ptile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
+      reinterpret_cast<f32x4*>(base)[lane] = o;
+    }
   };
   // AHEAD == 2: the raw loads run two tiles ahead (vload gets tile + 2 gstride while vstage, loaded one
   // tile earlier, is staged for tile + gstride); == 1: loaded and staged within the same tile
@@ -728,7 +742,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       rs[2 * j + 1][q] += dv * dv;
     }
     float* base = hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
-    reinterpret_cast<f32x4*>(base)[lane] = o;
+    if (!(PCN_H_ABL & 1)) reinterpret_cast<f32x4*>(base)[lane] = o;
   };
   auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile, f32x4 (&vstage)[4], f32x4 (&vload)[4]) {
     const int nxt = __builtin_amdgcn_readfirstlane(tile + gstride);
@@ -738,8 +752,8 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     f32x4 vloc[4];   // AHEAD == 1: this tile's loads of the next tile
     float rr[7];
     f32x4 ev;
-    f16x8 we[2][2];   // WENC: weights of encoding k-steps ks, ks + 1
-    if (WENC) {
+    f16x8 we[2][2];   // NWL: weights of LDS k-steps ks, ks + 1
+    if (NWL) {
 #pragma unroll
       for (int d = 0; d < 2; ++d)
 #pragma unroll
@@ -757,13 +771,13 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
         xr[(ks + XD - 1) % XD][1] = xs[buf][ks + XD - 1][1][lane];
       }
       const f16x8 xh = xr[ks % XD][0], xm = xr[ks % XD][1];
-      const bool wl = WENC && ks < KSE;
+      const bool wl = ks < NWL;
       const f16x8 w0 = wl ? we[ks & 1][0] : wr[ks][0], w1 = wl ? we[ks & 1][1] : wr[ks][1];
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0, xh, ks == 0 ? f32x16{} : acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0, xm, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w1, xh, acc, 0, 0, 0);
       if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w1, xm, acc, 0, 0, 0);
-      if (WENC && ks + 2 < KSE) {
+      if (ks + 2 < NWL) {
         we[ks & 1][0] = wenc(ks + 2, 0);
         we[ks & 1][1] = wenc(ks + 2, 1);
       }
@@ -794,14 +808,20 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
           stage(buf ^ 1, vstage, 3);
         }
       } else if constexpr (HP) {
-        if (ks == S_LOAD && more) load_tile(vloc, nxt);
-        if (ks == S_STAGE0 && more) {
-          stage(buf ^ 1, vloc, 0);
-          stage(buf ^ 1, vloc, 1);
+        if (ks == S_LOAD && more && !(PCN_H_ABL & 2)) load_tile(vloc, nxt);
+        if ((PCN_H_ABL & 2) && ks == S_LOAD) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) vloc[m] = f32x4{1.0f, 1.0f, 1.0f, 1.0f} * (float)(ks + m);
         }
-        if (ks == S_STAGE1 && more) {
-          stage(buf ^ 1, vloc, 2);
-          stage(buf ^ 1, vloc, 3);
+        if (!(PCN_H_ABL & 4)) {
+          if (ks == S_STAGE0 && more) {
+            stage(buf ^ 1, vloc, 0);
+            stage(buf ^ 1, vloc, 1);
+          }
+          if (ks == S_STAGE1 && more) {
+            stage(buf ^ 1, vloc, 2);
+            stage(buf ^ 1, vloc, 3);
+          }
         }
       }
       if (KE && ks == KS - 1 && more) {
@@ -825,7 +845,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
 #pragma unroll
       for (int j = 0; j < 4; ++j) epir(acc, tile, j);
     }
-    __syncthreads();
+    if (!(PCN_H_ABL & 8)) __syncthreads();
     buf ^= 1;
   };
   f32x16 accA, accB;
@@ -864,6 +884,207 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       for (int j = 0; j < 4; ++j) epi(accB, ptile, j);
     }
   }
+  __syncthreads();
+  {
+    const int nn = t >> 1, mo = t & 1, ib = nn & 31, wb = nn >> 5;
+    const int hh = (ib >> 2) & 1, jj = ib >> 3, qq = ib & 3;
+    double a = 0.0;
+#pragma unroll 8
+    for (int l = 0; l < 32; ++l) {
+      const int ln = 32 * hh + l;
+      a += (double)sred[(wb * 64 + ln) * 8 + ((2 * jj + mo) ^ ((ln >> 1) & 7))][qq];
+    }
+    atomicAdd(&stats[t], a);
+  }
+}
+
+// ---- k_train_h1<NT>: hidden layer 1 straight from the chunk's encoding tiles.  The first layer's output h0 is a
+// 268 MB round trip per chunk (written by layer 0, read back here) although it is W0 e + b0 of the 67 MB of
+// encoding tiles layer 0 also writes.  So layer 0 runs statistics-only (no h0 store), and this kernel recomputes
+// each tile's h0 with the first layer's own instruction sequence (the same split products in the same order on
+// the same split operands: bit-identical h0), applies BatchNorm 0 and stages it as the B operand of W1 -- 8 KiB
+// read per tile instead of 32 KiB.  Structure = k_train_h's hidden REGSTAT form; per tile: W1 products of tile T
+// (16 k-steps), its epilogue, then W0 products of tile T + 1 (4 k-steps, W0 in LDS, reusing the accumulator) and
+// their BatchNorm + split into the other B buffer; the encoding tile of T + 2 is loaded during T's k-loop and
+// staged (split) into a two-slot LDS ring.  One barrier per tile.
+template <int NT>
+__global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ etin, int64_t n,
+                                                     const f16x8* __restrict__ W1p, const f16x8* __restrict__ W0p,
+                                                     const int* __restrict__ swp, int layer,
+                                                     const float* __restrict__ bias, BnPrev prev, float momentum,
+                                                     float eps, float* __restrict__ hout,
+                                                     double* __restrict__ stats) {
+  constexpr int KS = KS_H, XD = PCN_H_XD;
+  constexpr int S_ELOAD = 2, S_EPUT = KS - 4;
+  __shared__ __attribute__((aligned(16))) float al[256];
+  __shared__ __attribute__((aligned(16))) float be[256];
+  __shared__ __attribute__((aligned(16))) float bs[256];
+  __shared__ __attribute__((aligned(16))) float b0s[256];
+  __shared__ float smax[8];
+  __shared__ f16x8 xs[2][KS][2][64];
+  __shared__ f16x8 eb[2][KS_E][2][64];   // split encoding tiles (B operand of W0), two slots
+  __shared__ f16x8 w0s[HW_E];            // W0's image [k-step][out-block][part][lane]
+  static_assert(sizeof(xs) >= 8 * 64 * 8 * sizeof(f32x4), "reduction area");
+  f32x4* const sred = reinterpret_cast<f32x4*>(&xs[0][0][0][0]);
+  const int t = threadIdx.x;
+  if (t < 256) {
+    bn_coeffs(prev, n, momentum, eps, al, be);   // BatchNorm 0
+    bs[t] = bias[t];
+    b0s[t] = prev.lin_bias[t];
+  }
+  int sx;
+  {
+    float bnd = 0.0f;
+    if (t < 256) bnd = sqrtf((float)n) * fabsf(prev.gamma[t]) + fabsf(prev.beta[t]);
+    bnd = wave_max_f(bnd);
+    if ((t & 63) == 0) smax[t >> 6] = bnd;
+    __syncthreads();
+    float m = smax[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) m = fmaxf(m, smax[i]);
+    sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
+    sx = sx > 24 ? 24 : sx;
+  }
+  const float xscale = ldexpf(1.0f, sx);
+  const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
+  const float unscale0 = ldexpf(1.0f, -swp[0]);   // layer 0: unscaled encoding operand (its sx is 0)
+  const int nt = (int)((n + 31) / 32);
+  const int gstride = (int)gridDim.x;
+  const bool rev = (layer >> 8) & 1;
+  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
+  const int lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);
+  f16x8 wr[KS][2];
+  {
+    const f16x8* __restrict__ w8 = W1p + lane;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 8 + blk) * 2 + p) * 64];
+    for (int j = t; j < (int)HW_E; j += 512) w0s[j] = W0p[j];
+  }
+  f32x4 rs[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) rs[c] = f32x4{};
+  // split 4 values into the B layout [k-step G >> 1][part][li + 32 (G & 1)][4 h ..] of feature group G
+  auto putb = [&](f16x8 (*dst)[2][64], int G, const f32x4& x) {
+    f16x4 hi, mid;
+    split4(x, hi, mid);
+    const int ln = li + 32 * (G & 1);
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&dst[G >> 1][0][ln]) + 4 * h) = hi;
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&dst[G >> 1][1][ln]) + 4 * h) = mid;
+  };
+  auto load_enc = [&](int tile) { return etin[(size_t)P(tile) * 512 + t]; };   // group t >> 6, lane
+  auto put_enc = [&](int slot, const f32x4& e) { putb(eb[slot], t >> 6, e); };
+  // h0 of the wave's 32 neurons for `tile` (W0 products exactly as k_train_h<8,false>), BatchNorm 0, split into
+  // B buffer b at groups 4 blk + j
+  // operands of W0 k-step ks for encoding slot `slot`: {w hi, w mid, x hi, x mid}
+  auto h0_ops = [&](f16x8 (&o)[4], int slot, int ks) {
+    o[0] = w0s[((ks * 8 + blk) * 2 + 0) * 64 + lane];
+    o[1] = w0s[((ks * 8 + blk) * 2 + 1) * 64 + lane];
+    o[2] = eb[slot][ks][0][lane];
+    o[3] = eb[slot][ks][1][lane];
+  };
+  // (ops0: k-step 0's operands, read ahead by the caller)
+  auto h0_stage = [&](f32x16& acc, int slot, int b, const f16x8 (&ops0)[4]) {
+    f16x8 op[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) op[0][i] = ops0[i];
+#pragma unroll
+    for (int ks = 0; ks < KS_E; ++ks) {
+      if (ks + 1 < KS_E) h0_ops(op[(ks + 1) & 1], slot, ks + 1);
+      const f16x8 *o = op[ks & 1];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[0], o[2], ks == 0 ? f32x16{} : acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[0], o[3], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[1], o[2], acc, 0, 0, 0);
+      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[1], o[3], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f0 = 32 * blk + 8 * j + 4 * h;
+      const f32x4 bj = *reinterpret_cast<const f32x4*>(b0s + f0);
+      const f32x4 a = *reinterpret_cast<const f32x4*>(al + f0), c = *reinterpret_cast<const f32x4*>(be + f0);
+      f32x4 x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float hv = acc[4 * j + q] * unscale0 + bj[q];   // k_train_h's epilogue: o = d + b
+        x[q] = (hv * a[q] + c[q]) * xscale;                   // its staging: (v alpha + beta') 2^sx
+      }
+      putb(xs[b], 4 * blk + j, x);
+    }
+  };
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  f32x16 acc;
+  if (tl < nt) {
+    put_enc(0, load_enc(tl));
+    const int t1 = tl + gstride;
+    if (t1 < nt) put_enc(1, load_enc(t1));
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);   // W1 resident
+  if (tl < nt) {
+    f16x8 o0[4];
+    h0_ops(o0, 0, 0);
+    h0_stage(acc, 0, 0, o0);
+  }
+  __syncthreads();
+  int buf = 0;
+  while (tl < nt) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
+    const int nxt2 = __builtin_amdgcn_readfirstlane(tl + 2 * gstride);
+    const bool more = nxt < nt, more2 = nxt2 < nt;
+    f16x8 xr[XD][2];
+    f32x4 ev;
+    f16x8 o0[4];   // W0 k-step 0 operands of tile + 1, read during the last W1 k-step
+#pragma unroll
+    for (int d = 0; d < XD - 1; ++d) {
+      xr[d][0] = xs[buf][d][0][lane];
+      xr[d][1] = xs[buf][d][1][lane];
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + XD - 1 < KS) {
+        xr[(ks + XD - 1) % XD][0] = xs[buf][ks + XD - 1][0][lane];
+        xr[(ks + XD - 1) % XD][1] = xs[buf][ks + XD - 1][1][lane];
+      }
+      const f16x8 xh = xr[ks % XD][0], xm = xr[ks % XD][1];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xh, ks == 0 ? f32x16{} : acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
+      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
+      if (ks == S_ELOAD && more2) ev = load_enc(nxt2);
+      if (ks == S_EPUT && more2) put_enc(buf, ev);   // slot of tile + 2 = this tile's slot (read one tile ago)
+      if (ks == KS - 1) h0_ops(o0, buf ^ 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    {   // epilogue of this tile (as k_train_h's REGSTAT epilogue)
+      const int tile = P(tl);
+      const bool valid = (int64_t)tile * 32 + li < n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
+        f32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float d = acc[4 * j + q] * unscale;
+          o[q] = d + bj[q];
+          const float dv = valid ? d : 0.0f;
+          rs[2 * j][q] += dv;
+          rs[2 * j + 1][q] += dv * dv;
+        }
+        reinterpret_cast<f32x4*>(hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256)[lane] = o;
+      }
+    }
+    if (more) h0_stage(acc, buf ^ 1, buf ^ 1, o0);   // tile + 1's encoding sits in the other slot
+    __syncthreads();
+    buf ^= 1;
+    tl = nxt;
+  }
+  f32x4* const my_st = sred + (blk * 64 + lane) * 8;
+  const int st_sw = (lane >> 1) & 7;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) my_st[c ^ st_sw] = rs[c];
   __syncthreads();
   {
     const int nn = t >> 1, mo = t & 1, ib = nn & 31, wb = nn >> 5;
@@ -1291,11 +1512,15 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     float* hout = keep ? sc.h[1] : ws.bufB;
     // the encoding tiles the skip layer reads back: written by THIS chunk's first-layer launch just below
     const f32x4* enc_of_chunk = nullptr;
+    // split math, nothing kept for a backward: layer 0 statistics-only, layer 1 recomputes h0 from the encoding
+    // tiles (k_train_h1)
+    const bool h1 = PCN_H1 && !keep && g_train_math != 0;
     {
       const BnPrev none{};
-      ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + 1024.0) * dn);
+      ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + (h1 ? 256.0 : 1024.0 + 256.0)) * dn);
       const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};
-      launch_layer<KG_E, false>(q, P, ws.wp, ws.wh, ws.sw, 0, nullptr, none, hin, stats, nullptr, ws.enc);
+      launch_layer<KG_E, false>(q, P, ws.wp, ws.wh, ws.sw, 0, nullptr, none, h1 ? nullptr : hin, stats, nullptr,
+                                ws.enc);
       enc_of_chunk = ws.enc;
     }
     for (int L = 1; L < 8; ++L) {
@@ -1305,7 +1530,17 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
       }
       const BnPrev prev{P.bn_w[L - 1], P.bn_b[L - 1], P.bn_rm[L - 1], P.bn_rv[L - 1], P.lin_b[L - 1],
                         stats + 512 * (L - 1)};
-      if (L == 4) {
+      if (L == 1 && h1) {
+        ProfScope ps(s, PT_TRAIN_H1, 2.0 * (63 + 256) * 256 * dn, (256.0 + 1024.0) * dn);
+        if (g_train_math == 1)
+          hipLaunchKernelGGL(k_train_h1<3>, dim3(gws), dim3(512), 0, s, enc_of_chunk, n, ws.wh + off_h(1, false),
+                             ws.wh + off_h(0, true), ws.sw, 1 | (tile_rev(1) << 8), P.lin_b[1], prev, momentum, eps,
+                             hout, stats + 512);
+        else
+          hipLaunchKernelGGL(k_train_h1<4>, dim3(gws), dim3(512), 0, s, enc_of_chunk, n, ws.wh + off_h(1, false),
+                             ws.wh + off_h(0, true), ws.sw, 1 | (tile_rev(1) << 8), P.lin_b[1], prev, momentum, eps,
+                             hout, stats + 512);
+      } else if (L == 4) {
         PCN_CHECK(enc_of_chunk, "skip layer launched without this chunk's first-layer encoding tiles");
         ProfScope ps(s, PT_TRAIN_SKIP, 2.0 * 319 * 256 * dn, (4.0 + 2048.0) * dn);
         const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};

@@ -19,7 +19,8 @@ enum ProfTag {
   PT_BWD_DGRAD = 11,   // k_dgrad_ws / k_dgrad_h: data-gradient GEMM + BatchNorm backward
   PT_BWD_MISC = 12,    // output-layer backward, partial reduction, BN statistics
   PT_EVAL_FOLD = 13,   // k_nof_eval_fold: exact affine fold of the eval network (opt-in)
-  PT_BWD_WGRAD_H = 14, // k_wgrad_b3: hidden-layer weight gradient under the split train math
+  PT_BWD_WGRAD_H = 14, // k_wgrad_b3: weight gradients under the split train math
+  PT_TRAIN_H1 = 15,    // k_train_h1: layer 1 from the encoding tiles (h0 recomputed)
 };
 extern bool g_prof_on;
 class ProfScope {

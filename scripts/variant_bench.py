@@ -16,7 +16,7 @@ from nof import _ops, synthetic as syn  # noqa: E402
 from nof.networks import NOF_coarse  # noqa: E402
 
 TAGS = {0: "eval", 1: "hidden", 2: "first", 3: "skip", 4: "out", 5: "fold", 10: "wgrad", 11: "dgrad",
-        12: "bwd_other", 14: "wgrad_b3"}
+        12: "bwd_other", 14: "wgrad_b3", 15: "h1"}
 
 
 def load(path):
