@@ -16,6 +16,7 @@
 // (the tile's float4 itself), D (reg r, lane l) = out[neuron 32b + (r&3) + 8(r>>2) + 4(l>>5)][sample l&31], so
 // registers 4j..4j+3 are the output tile's float4 at group 4b+j.  feature(t, h) = 8(t>>2) + 4h + (t&3).
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -61,6 +62,9 @@ namespace pcn {
 #ifndef PCN_H_LMAP
 #define PCN_H_LMAP 0   // staging lane map (conflict-free 8-byte LDS writes)
 #endif
+#ifndef PCN_H_RING4
+#define PCN_H_RING4 0   // hidden layers: four B buffers, staging two tiles ahead, a barrier every second tile (no gain)
+#endif
 #ifndef PCN_H_WLDS
 #define PCN_H_WLDS 0  // hidden layers: k-steps of weights read from LDS instead of registers
 #endif
@@ -88,6 +92,9 @@ namespace pcn {
 #endif
 #ifndef PCN_WB3_STAGE
 #define PCN_WB3_STAGE 0   // column block of the first staging piece
+#endif
+#ifndef PCN_WGRAD_H2
+#define PCN_WGRAD_H2 1    // split-math weight gradients as f16x2 (else three bf16 parts)
 #endif
 #ifndef PCN_WB3_RB
 #define PCN_WB3_RB 1      // row blocks of 32 per wave (8 / RB waves per workgroup)
@@ -576,11 +583,15 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   // NWL: k-steps whose weights come from LDS (two k-steps ahead) -- the skip layer's encoding k-steps (WENC), or
   // the hidden layer's first PCN_H_WLDS (registers for loads two tiles ahead)
   constexpr int NWL = WENC ? KSE : (HP && !KE) ? PCN_H_WLDS : 0;
+  // RING4 (hidden layers): a ring of four B buffers staged two tiles ahead, so a barrier every second tile suffices
+  // (a buffer is rewritten two tiles after its last read and read two tiles after its staging)
+  constexpr bool RING4 = REGSTAT && !KE && AHEAD == 1 && PCN_H_RING4;
+  constexpr int NBUF = RING4 ? 4 : 2;
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
   __shared__ float smax[8];
-  __shared__ f16x8 xs[2][KS][2][64];
+  __shared__ f16x8 xs[NBUF][KS][2][64];
   __shared__ f32x4 sred_[REGSTAT ? 1 : 8 * 64 * 8];   // per-lane running statistics, as k_train_ws
   __shared__ f16x8 wenc_[NWL ? NWL * 8 * 2 * 64 : 1];
   static_assert(!REGSTAT || sizeof(xs) >= 8 * 64 * 8 * sizeof(f32x4), "reduction area");
@@ -687,6 +698,11 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       load_tile(v, tl);
 #pragma unroll
       for (int m = 0; m < 4; ++m) stage(0, v, m);
+      if (RING4 && tl + gstride < nt) {
+        load_tile(v, tl + gstride);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) stage(1, v, m);
+      }
     }
     if (KE) {
       const int64_t gs = sample_of(tl);
@@ -744,10 +760,14 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     float* base = hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
     if (!(PCN_H_ABL & 1)) reinterpret_cast<f32x4*>(base)[lane] = o;
   };
-  auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile, f32x4 (&vstage)[4], f32x4 (&vload)[4]) {
+  auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile, f32x4 (&vstage)[4], f32x4 (&vload)[4],
+                  bool sync) {
     const int nxt = __builtin_amdgcn_readfirstlane(tile + gstride);
     const bool more = nxt < nt;
     const int nxt2 = __builtin_amdgcn_readfirstlane(tile + 2 * gstride);
+    const int bnext = RING4 ? ((buf + 2) & 3) : (buf ^ 1);   // the buffer this tile stages into
+    const int tst = RING4 ? nxt2 : nxt;                     // ... for this tile
+    const bool mst = tst < nt;
     f16x8 xr[XD][2];
     f32x4 vloc[4];   // AHEAD == 1: this tile's loads of the next tile
     float rr[7];
@@ -808,19 +828,19 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
           stage(buf ^ 1, vstage, 3);
         }
       } else if constexpr (HP) {
-        if (ks == S_LOAD && more && !(PCN_H_ABL & 2)) load_tile(vloc, nxt);
+        if (ks == S_LOAD && mst && !(PCN_H_ABL & 2)) load_tile(vloc, tst);
         if ((PCN_H_ABL & 2) && ks == S_LOAD) {
 #pragma unroll
           for (int m = 0; m < 4; ++m) vloc[m] = f32x4{1.0f, 1.0f, 1.0f, 1.0f} * (float)(ks + m);
         }
         if (!(PCN_H_ABL & 4)) {
-          if (ks == S_STAGE0 && more) {
-            stage(buf ^ 1, vloc, 0);
-            stage(buf ^ 1, vloc, 1);
+          if (ks == S_STAGE0 && mst) {
+            stage(bnext, vloc, 0);
+            stage(bnext, vloc, 1);
           }
-          if (ks == S_STAGE1 && more) {
-            stage(buf ^ 1, vloc, 2);
-            stage(buf ^ 1, vloc, 3);
+          if (ks == S_STAGE1 && mst) {
+            stage(bnext, vloc, 2);
+            stage(bnext, vloc, 3);
           }
         }
       }
@@ -845,8 +865,8 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
 #pragma unroll
       for (int j = 0; j < 4; ++j) epir(acc, tile, j);
     }
-    if (!(PCN_H_ABL & 8)) __syncthreads();
-    buf ^= 1;
+    if (!(PCN_H_ABL & 8) && sync) __syncthreads();
+    buf = RING4 ? ((buf + 1) & 3) : (buf ^ 1);
   };
   f32x16 accA, accB;
   f32x4 vA[4], vB[4];
@@ -857,10 +877,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   int ptile = -1;
   if (REGSTAT) {
     while (tl < nt) {
-      body(accA, accA, tl, -1, vA, vB);
+      body(accA, accA, tl, -1, vA, vB, !RING4);
       tl = __builtin_amdgcn_readfirstlane(tl + gstride);
       if (tl >= nt) break;
-      body(accA, accA, tl, -1, vB, vA);
+      body(accA, accA, tl, -1, vB, vA, true);
       tl = __builtin_amdgcn_readfirstlane(tl + gstride);
     }
     tl = nt;
@@ -868,7 +888,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     for (int c = 0; c < 8; ++c) my_st[c ^ st_sw] = rs[c];
   }
   while (tl < nt) {
-    body(accA, accB, tl, ptile, vA, vB);
+    body(accA, accB, tl, ptile, vA, vB, true);
     ptile = tl;
     tl = __builtin_amdgcn_readfirstlane(tl + gstride);
     if (tl >= nt) {
@@ -876,7 +896,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       for (int j = 0; j < 4; ++j) epi(accA, ptile, j);
       break;
     }
-    body(accB, accA, tl, ptile, vB, vA);
+    body(accB, accA, tl, ptile, vB, vA, true);
     ptile = tl;
     tl = __builtin_amdgcn_readfirstlane(tl + gstride);
     if (tl >= nt) {
@@ -1778,7 +1798,8 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
                                                       const float* __restrict__ wout, const double* __restrict__ acc,
                                                       double* __restrict__ d_gamma, double* __restrict__ d_beta,
                                                       double* __restrict__ d_wout, double* __restrict__ d_bout,
-                                                      float* __restrict__ gout, float* __restrict__ tmax) {
+                                                      float* __restrict__ gout, float* __restrict__ tmax,
+                                                      unsigned* __restrict__ gmax) {
   __shared__ __attribute__((aligned(16))) float cgm[256];
   __shared__ __attribute__((aligned(16))) float ckk[256];
   __shared__ __attribute__((aligned(16))) float cmu[256];
@@ -1811,6 +1832,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
   __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
   const int64_t ntiles = (n + 31) / 32;
+  float gm = 0.0f;   // the wave's largest |dL/dh_7| over its tiles
   for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles; tile += (int64_t)gridDim.x * 4) {
     const int64_t s = tile * 32 + li;
     const bool valid = s < n;
@@ -1834,8 +1856,10 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
     if (tmax) {   // the tile's largest |dL/dh_7| (k_dgrad_h's operand scale), one wave per tile
       mx = wave_max_f(mx);
       if (lane < 8) tmax[tile * 8 + lane] = mx;
+      gm = fmaxf(gm, mx);
     }
   }
+  if (gmax && lane == 0) atomicMax(gmax, __float_as_uint(gm));   // non-negative floats order as their bits
 }
 
 // ---- weight gradient: G[m][n] = sum_s dL/dh_L[s][m] * X[s][n] over one chunk, partials per block.
@@ -2222,8 +2246,9 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
     const int* __restrict__ swp, int layer, const float* __restrict__ hprev, int64_t n,
     const double* __restrict__ s12, const float* __restrict__ coefp, const float* __restrict__ gamma,
     double* __restrict__ d_gamma, double* __restrict__ d_beta, float* __restrict__ gout,
-    float* __restrict__ tmax_out) {
+    float* __restrict__ tmax_out, unsigned* __restrict__ gmax_out) {
   constexpr int KS = KS_H, XD = PCN_H_XD;
+  float gm = 0.0f;   // the wave's largest |dL/dh_{L-1}| over its tiles (k_wgrad_b3's chunk-wide scale)
   constexpr int S_LOAD = PCN_H_LOAD, S_STAGE0 = KS - PCN_H_STAGE, S_STAGE1 = S_STAGE0 + 1, S_HX = 8;
   __shared__ __attribute__((aligned(16))) float cgm[256];
   __shared__ __attribute__((aligned(16))) float ckk[256];
@@ -2321,6 +2346,7 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
     }
     mx = wave_max_f(mx);
     if (lane == 0) tmax_out[(size_t)tile * 8 + blk] = mx;
+    gm = fmaxf(gm, mx);
   };
   while (tl < nt) {
     const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
@@ -2373,6 +2399,7 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
     sg = sgn;
     tl = nxt;
   }
+  if (gmax_out && lane == 0) atomicMax(gmax_out, __float_as_uint(gm));
 }
 
 // k_wgrad_b3<RB, MODE>: k_wgrad<MODE>'s G = sum_s dL/dh (x) x with each fp32 operand split into three bf16 parts
@@ -2391,14 +2418,15 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
 //   dL/dh (A operand, read by its wave only): copied raw ([g][half][sample ^ c][4], c = 2 (g & 3) + half:
 //     conflict-free 4-byte reads), each wave splitting its 8 values per half tile itself.
 // One barrier per half tile.  Partials and db in k_wgrad<MODE>'s layout (k_wgrad_reduce<MODE> sums them).
-template <int MODE>
+template <int MODE, bool H2 = false>
 struct Wb3Cfg {
   static constexpr bool HX = MODE != 1, EX = MODE != 0;
+  static constexpr int NPART = H2 ? 2 : 3;                         // operand parts: f16 hi/mid or bf16 hi/mid/lo
   static constexpr int NBLK = (EX ? 2 : 0) + (HX ? 8 : 0);        // 32-column blocks of G
   static constexpr int PITCH = 64 * NBLK + 64;                     // x row bytes: 576, 192, 704
   static constexpr int XPART = 16 * PITCH;
   static constexpr int GB = 16 * 256 * 4;                          // raw dL/dh bytes per half tile
-  static constexpr size_t BUF = (size_t)GB + 3 * XPART;
+  static constexpr size_t BUF = (size_t)GB + NPART * XPART;
   static constexpr size_t LDS = 3 * BUF;
 };
 
@@ -2428,6 +2456,24 @@ __device__ __forceinline__ void split3_x4(const f32x4& v, s16x4& p0, s16x4& p1, 
   }
 }
 
+__device__ __forceinline__ void split2_x4(const f32x4& v, s16x4& p0, s16x4& p1) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const _Float16 a = (_Float16)v[q];
+    p0[q] = __builtin_bit_cast(short, a);
+    p1[q] = __builtin_bit_cast(short, (_Float16)(v[q] - (float)a));
+  }
+}
+
+__device__ __forceinline__ void split2_f16(const float (&v)[8], f16x8& hi, f16x8& mid) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 a = (_Float16)v[j];
+    hi[j] = a;
+    mid[j] = (_Float16)(v[j] - (float)a);
+  }
+}
+
 // byte offset of features f .. f+3 (f % 4 == 0) of row r (sample within the half tile) in one x part
 template <int PITCH>
 __device__ __forceinline__ int wb3_xoff(int r, int f) {
@@ -2439,21 +2485,50 @@ __device__ __forceinline__ int wb3_xoff(int r, int f) {
 // RB: row blocks (32 features of dL/dh) per wave; 8 / RB waves per workgroup.  LAY: the k_wgrad mode whose partial
 // layout is written -- the skip layer (LAY 2) runs MODE 0 (its h columns, at column 64, and db) and MODE 1 (its
 // encoding columns): its 10 column blocks would not fit the accumulator registers of one launch
-template <int RB, int MODE, int LAY>
+// H2: the f16x2 form (NT products of two fp16 parts, as the forward): dL/dh scaled by 2^sg from the chunk's
+// largest |dL/dh| (`gmax`, recorded by the producer), x per column by 2^sx from its own bound (the Samuelson bound
+// sqrt(n) / invstd of h - mean; 2^14 for the encoding's sin/cos, 1 for its xyz), both undone on the partials.
+template <int RB, int MODE, int LAY, bool H2, int NTP>
 __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restrict__ rays, int stride,
                                                           const float* __restrict__ z, int S, int64_t c0,
                                                           const float* __restrict__ ein,
                                                           const float* __restrict__ gin,
                                                           const float* __restrict__ hprev,
                                                           const float* __restrict__ mu, int64_t n,
+                                                          const unsigned* __restrict__ gmax,
                                                           float* __restrict__ part) {
-  using Cfg = Wb3Cfg<MODE>;
+  using Cfg = Wb3Cfg<MODE, H2>;
+  constexpr int NPART = Cfg::NPART;
   constexpr bool HX = Cfg::HX, EX = Cfg::EX;
   constexpr int NBLK = Cfg::NBLK, PITCH = Cfg::PITCH, XPART = Cfg::XPART, GB = Cfg::GB;
   constexpr int NT = 512 / RB, NI = 2 * RB;   // threads; float4 per thread per operand and half tile
   constexpr int HOFF = EX ? 64 : 0;           // first h feature column in the x image
+  using P8 = std::conditional_t<H2, f16x8, bf16x8>;   // operand part type
   extern __shared__ __attribute__((aligned(16))) float wb3[];
   const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31;
+  // H2: per-column scales of G (x operand) after the three buffers; dL/dh's chunk-wide scale
+  float* const csc = wb3 + 3 * Cfg::BUF / 4;
+  float* const cun = csc + NBLK * 32;
+  float gsc = 1.0f, gun = 1.0f;
+  if constexpr (H2) {
+    for (int c = t; c < NBLK * 32; c += 512 / RB) {
+      int e;
+      if (EX && c < 64) {
+        e = (c >= 3 && c < 63) ? 14 : 0;   // |sin|, |cos| <= 1; xyz unscaled
+      } else {
+        const float invstd = mu[256 + (c - HOFF)];
+        const float bnd = sqrtf((float)n) / invstd;   // Samuelson: |h - mean| <= sqrt(n) sigma
+        e = (bnd > 0.0f && bnd < 3.0e38f) ? 14 - ilogbf(bnd) : 0;
+        e = e < -60 ? -60 : e > 60 ? 60 : e;
+      }
+      csc[c] = ldexpf(1.0f, e);
+      cun[c] = ldexpf(1.0f, -e);
+    }
+    const int eg = tile_scale_exp(__uint_as_float(*gmax));
+    gsc = ldexpf(1.0f, eg);
+    gun = ldexpf(1.0f, -eg);
+    __syncthreads();
+  }
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
@@ -2512,7 +2587,14 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       f32x4 v;
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = valid ? rv[(NI + i) % NR][q] - mu2[i][q] : 0.0f;
-      split3_x4(v, p0, p1, p2);
+      if constexpr (H2) {
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(csc + HOFF + 8 * g + 4 * shh);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] *= sc[q];
+        split2_x4(v, p0, p1);
+      } else {
+        split3_x4(v, p0, p1, p2);
+      }
       off = wb3_xoff<PITCH>(sl, HOFF + 8 * g + 4 * shh);
     } else if constexpr (EX) {
       // one sincos per thread: row er, task ej < 30 -> 2^k p[m] (k = ej / 3, m = ej % 3) feeding features
@@ -2528,12 +2610,14 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
         pp[2] = ra[2] + rb2[1] * zz;
       }
       auto put1 = [&](int f, float v) {
-        s16x4 q0, q1, q2;
-        split3_x4(f32x4{valid ? v : 0.0f, 0.0f, 0.0f, 0.0f}, q0, q1, q2);
+        s16x4 q0, q1, q2 = {};
+        const f32x4 v4 = f32x4{valid ? (H2 ? v * csc[f] : v) : 0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (H2) split2_x4(v4, q0, q1);
+        else split3_x4(v4, q0, q1, q2);
         const int o = wb3_xoff<PITCH>(er, f & ~3) + 2 * (f & 3);
         *reinterpret_cast<short*>(xb + o) = q0[0];
         *reinterpret_cast<short*>(xb + XPART + o) = q1[0];
-        *reinterpret_cast<short*>(xb + 2 * XPART + o) = q2[0];
+        if (!H2) *reinterpret_cast<short*>(xb + 2 * XPART + o) = q2[0];
       };
       if (ej < 30) {
         const int k = ej / 3, m = ej - 3 * k;
@@ -2556,7 +2640,7 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     }
     *reinterpret_cast<s16x4*>(xb + off) = p0;
     *reinterpret_cast<s16x4*>(xb + XPART + off) = p1;
-    *reinterpret_cast<s16x4*>(xb + 2 * XPART + off) = p2;
+    if (!H2) *reinterpret_cast<s16x4*>(xb + 2 * XPART + off) = p2;
   };
   f32x16 acc[RB][NBLK];
 #pragma unroll
@@ -2586,24 +2670,31 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
 #pragma unroll
       for (int j = 0; j < 8; ++j) av[rb][j] = gbuf[abase + 512 * rb + ((8 * h + j) ^ ac) * 4];
   };
-  auto splitA = [&](float (&av)[RB][8], bf16x8 (&a)[RB][3], bool count) {
+  auto splitA = [&](float (&av)[RB][8], P8 (&a)[RB][NPART], bool count) {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) dbacc[rb] += count ? av[rb][j] : 0.0f;
-      split3_bf16(av[rb], a[rb][0], a[rb][1], a[rb][2]);
+      if constexpr (H2) {
+        float sv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sv[j] = av[rb][j] * gsc;
+        split2_f16(sv, a[rb][0], a[rb][1]);
+      } else {
+        split3_bf16(av[rb], a[rb][0], a[rb][1], a[rb][2]);
+      }
     }
   };
-  auto readB = [&](bf16x8 (&bv)[3], int b, int nb) {
+  auto readB = [&](P8 (&bv)[NPART], int b, int nb) {
     const char* xb = bufp(b) + GB;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < NPART; ++p) {
       const char* pb = xb + p * XPART + 64 * nb;
       const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) s16x4*)(__attribute__((address_space(3))) void*)(pb + troff0));
       const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) s16x4*)(__attribute__((address_space(3))) void*)(pb + troff1));
-      bv[p] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+      bv[p] = __builtin_bit_cast(P8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
     }
   };
   // Pipeline: half tile u computes from buffer u % 3 while half tile u + 2 is staged into buffer (u + 2) % 3 from
@@ -2623,7 +2714,7 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   constexpr int S_P0 = PCN_WB3_STAGE + (NP - 1) * S_PD < NBLK ? PCN_WB3_STAGE : 0;
   constexpr int S_APF = PCN_WB3_AREAD < NBLK ? PCN_WB3_AREAD : NBLK - 1;
   constexpr int S_ASP = S_APF + 2 < NBLK ? S_APF + 2 : NBLK - 1;
-  bf16x8 Acur[RB][3], Anext[RB][3], B[2][3];
+  P8 Acur[RB][NPART], Anext[RB][NPART], B[2][NPART];
   if (nh > 0) {
     float av[RB][8];
     readA(av, 0);
@@ -2644,17 +2735,24 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       else readB(B[0], bn1, 0);
       if (nb == S_APF) readA(av, bn1);
       if (nb == S_ASP) splitA(av, Anext, u + 1 < nh);
-      const bf16x8* bo = B[nb & 1];
+      const P8* bo = B[nb & 1];
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
-        const bf16x8* a = Acur[rb];
+        const P8* a = Acur[rb];
         f32x16 c = acc[rb][nb];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bo[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bo[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bo[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[0], c, 0, 0, 0);
+        if constexpr (H2) {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bo[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bo[1], c, 0, 0, 0);
+          if (NTP == 4) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bo[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bo[0], c, 0, 0, 0);
+        } else {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bo[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bo[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bo[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bo[0], c, 0, 0, 0);
+        }
         acc[rb][nb] = c;
       }
 #pragma unroll
@@ -2667,7 +2765,7 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) Acur[rb][p] = Anext[rb][p];
+      for (int p = 0; p < NPART; ++p) Acur[rb][p] = Anext[rb][p];
     bcur = bn1;
   }
   static_assert(MODE != 2 && (LAY == MODE || LAY == 2), "partial layouts");
@@ -2680,7 +2778,8 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     for (int rr = 0; rr < 16; ++rr) {
       const int m = 32 * (RB * wv + rb) + (rr & 3) + 8 * (rr >> 2) + 4 * h;
 #pragma unroll
-      for (int nb = 0; nb < NBLK; ++nb) pb[(size_t)m * C + COL + 32 * nb + li] = acc[rb][nb][rr];
+      for (int nb = 0; nb < NBLK; ++nb)
+        pb[(size_t)m * C + COL + 32 * nb + li] = H2 ? (acc[rb][nb][rr] * gun) * cun[32 * nb + li] : acc[rb][nb][rr];
     }
     float d = dbacc[rb] + __shfl_xor(dbacc[rb], 32, 64);
     if (DB && h == 0) pb[(size_t)256 * C + 32 * (RB * wv + rb) + li] = d;
@@ -2742,6 +2841,7 @@ struct BwdWs {
   int* sw;
   f16x8* wth;   // split-fp16 W^T image of k_dgrad_h (train math 1/2)
   float* tmax[2];   // per-tile max |dL/dh| of g[0] / g[1] ([tile][8])
+  unsigned* gmax;   // per layer L: the chunk's largest |dL/dh_L| (float bits; zeroed with s12 per chunk)
   size_t bytes;
 };
 
@@ -2759,7 +2859,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t oenc = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
-  const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257) * 8), oa = take((size_t)gacc_layout().total * 8);
+  const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257 + 8) * 8), oa = take((size_t)gacc_layout().total * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
   const size_t owt = take(7 * HW_H * sizeof(f16x8));
   const size_t otm0 = take(tiles * 8 * sizeof(float)), otm1 = take(tiles * 8 * sizeof(float));
@@ -2779,6 +2879,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.part = (float*)(b + op);
   w.s12 = (double*)(b + os);
   w.ostat = w.s12 + 8 * S12_LAYER;   // s12 per layer [8][COPIES][512], then the output layer's statistics
+  w.gmax = (unsigned*)(w.ostat + OSTAT_COPIES * 257);
   w.gacc = (double*)(b + oa);
   w.enc = (f32x4*)(b + oenc);
   w.bytes = off;
@@ -2799,31 +2900,41 @@ static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int 
                      mu, part);
 }
 
-template <int MODE, int LAY>
+template <int MODE, int LAY, bool H2, int NTP>
 static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                                 int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
-                                const float* mu, float* part) {
+                                const float* mu, const unsigned* gmax, float* part) {
   constexpr int RB = MODE == 0 ? PCN_WB3_RB : 1;
-  constexpr size_t lds = Wb3Cfg<MODE>::LDS;
+  using Cfg = Wb3Cfg<MODE, H2>;
+  constexpr size_t lds = 3 * Cfg::BUF + (H2 ? 2 * Cfg::NBLK * 32 * sizeof(float) : 0);
+  static_assert(lds <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_b3<RB, MODE, LAY>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_b3<RB, MODE, LAY, H2, NTP>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((k_wgrad_b3<RB, MODE, LAY>), dim3(blocks), dim3(512 / RB), lds, s, rays, stride, z, S, c0, ein,
-                     gin, hprev, mu, n, part);
+  hipLaunchKernelGGL((k_wgrad_b3<RB, MODE, LAY, H2, NTP>), dim3(blocks), dim3(512 / RB), lds, s, rays, stride, z, S,
+                     c0, ein, gin, hprev, mu, n, gmax, part);
 }
 
-// the weight-gradient partials of k_wgrad<MODE> under the split train math
+// the weight-gradient partials of k_wgrad<MODE> under the split train math: f16x2 (PCN_WGRAD_H2, with the
+// forward's product count) or three bf16 parts
 template <int MODE>
 static void launch_wgrad_b3(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                             int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
-                            const float* mu, float* part) {
-  if constexpr (MODE != 1)
-    launch_wgrad_b3_one<0, MODE>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, part);
-  if constexpr (MODE != 0)
-    launch_wgrad_b3_one<1, MODE>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, part);
+                            const float* mu, const unsigned* gmax, float* part) {
+  auto one = [&](auto mode, auto lay) {
+    constexpr int M = decltype(mode)::value, LY = decltype(lay)::value;
+    if (PCN_WGRAD_H2 && g_train_math == 1)
+      launch_wgrad_b3_one<M, LY, true, 3>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
+    else if (PCN_WGRAD_H2)
+      launch_wgrad_b3_one<M, LY, true, 4>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
+    else
+      launch_wgrad_b3_one<M, LY, false, 3>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
+  };
+  if constexpr (MODE != 1) one(std::integral_constant<int, 0>{}, std::integral_constant<int, MODE>{});
+  if constexpr (MODE != 0) one(std::integral_constant<int, 1>{}, std::integral_constant<int, MODE>{});
 }
 
 }  // namespace pcn
@@ -2892,7 +3003,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
       hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
       // 2. occ_out + BatchNorm 8
-      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257) * sizeof(double), s));  // per chunk
+      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257 + 8) * sizeof(double), s));  // per chunk
       if (PCN_OSTAT1) {
         const unsigned sg = (unsigned)((ntiles + 3) / 4 < 256 ? (ntiles + 3) / 4 : 256);
         hipLaunchKernelGGL(k_out_bwd_stats1, dim3(sg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
@@ -2903,7 +3014,8 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       }
       hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, P.bn_w[7], P.out_w, ws.ostat, ws.gacc + G.g[7], ws.gacc + G.be[7],
-                         ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0], split ? ws.tmax[0] : nullptr);
+                         ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0], split ? ws.tmax[0] : nullptr,
+                         split ? ws.gmax + 7 : nullptr);
     }
     // 3. layers 7..1
     int cur = 0;
@@ -2914,10 +3026,10 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
                      2048.0 * dn);
         if (split && L == 4)
           launch_wgrad_b3<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp,
-                             ws.part);
+                             ws.gmax + L, ws.part);
         else if (split)
           launch_wgrad_b3<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
-                             ws.part);
+                             ws.gmax + L, ws.part);
         else if (L == 4)
           launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
         else
@@ -2939,12 +3051,12 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
           hipLaunchKernelGGL(k_dgrad_h<3>, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.tmax[cur],
                              ws.wth + (size_t)(L - 1) * HW_H, ws.sw, L, hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp,
                              P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1], ws.g[cur ^ 1],
-                             ws.tmax[cur ^ 1]);
+                             ws.tmax[cur ^ 1], ws.gmax + (L - 1));
         else if (split)
           hipLaunchKernelGGL(k_dgrad_h<4>, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.tmax[cur],
                              ws.wth + (size_t)(L - 1) * HW_H, ws.sw, L, hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp,
                              P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1], ws.g[cur ^ 1],
-                             ws.tmax[cur ^ 1]);
+                             ws.tmax[cur ^ 1], ws.gmax + (L - 1));
         else
           hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
                              hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
@@ -2957,7 +3069,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, split ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
       if (split)
         launch_wgrad_b3<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
-                           ws.part);
+                           ws.gmax + 0, ws.part);
       else
         launch_wgrad<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
                         ws.part);
