@@ -1641,6 +1641,8 @@ extern "C" int pcnerf_nof_forward_train(const float* emb, int64_t n, const pcner
 namespace pcn {
 
 constexpr size_t DGRAD_W_FLOATS = 7 * SZ_H;
+constexpr int GMAX_SLOTS = 64;                     // per layer: atomicMax targets of the |dL/dh| maxima
+constexpr int GMAX_DBL = 8 * GMAX_SLOTS / 2;       // their doubles in the per-chunk s12 region
 constexpr int WG_BLOCKS = 256;  // weight-gradient partials per chunk (one 8-wave block per CU)
 
 __host__ __device__ constexpr int in_features(int L) { return L == 0 ? 63 : L == 4 ? 319 : 256; }
@@ -1839,7 +1841,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
     const float gv = valid ? logit_grad(g, pin, s) : 0.0f;
     const f32x4* x4 = reinterpret_cast<const f32x4*>(h7 + tile * TILE_FLOATS) + lane;
     f32x4* o4 = reinterpret_cast<f32x4*>(gout + tile * TILE_FLOATS) + lane;
-    float mx = 0.0f;
+    f32x4 mq = {};   // per-q running maxima (four short dependency chains, not one of 128)
 #pragma unroll 8
     for (int gq = 0; gq < 32; ++gq) {
       const f32x4 x = x4[gq * 64];
@@ -1849,17 +1851,20 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
       for (int q = 0; q < 4; ++q) {
         const int f = f0 + q;
         o[q] = valid ? ((gv * cwo[f] - cgm[f]) - (x[q] - cmu[f]) * ckk[f]) * cis[f] * cga[f] : 0.0f;
-        mx = fmaxf(mx, fabsf(o[q]));
+        mq[q] = fmaxf(mq[q], fabsf(o[q]));
       }
       o4[gq * 64] = o;
     }
     if (tmax) {   // the tile's largest |dL/dh_7| (k_dgrad_h's operand scale), one wave per tile
+      float mx = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
       mx = wave_max_f(mx);
       if (lane < 8) tmax[tile * 8 + lane] = mx;
       gm = fmaxf(gm, mx);
     }
   }
-  if (gmax && lane == 0) atomicMax(gmax, __float_as_uint(gm));   // non-negative floats order as their bits
+  // non-negative floats order as their bits; one of GMAX_SLOTS addresses per wave (a single address would
+  // serialise thousands of atomics), the consumer takes the max over the slots
+  if (gmax && lane == 0) atomicMax(gmax + ((blockIdx.x * 4 + (threadIdx.x >> 6)) & (GMAX_SLOTS - 1)), __float_as_uint(gm));
 }
 
 // ---- weight gradient: G[m][n] = sum_s dL/dh_L[s][m] * X[s][n] over one chunk, partials per block.
@@ -2399,7 +2404,7 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
     sg = sgn;
     tl = nxt;
   }
-  if (gmax_out && lane == 0) atomicMax(gmax_out, __float_as_uint(gm));
+  if (gmax_out && lane == 0) atomicMax(gmax_out + ((blockIdx.x * 8 + blk) & (GMAX_SLOTS - 1)), __float_as_uint(gm));
 }
 
 // k_wgrad_b3<RB, MODE>: k_wgrad<MODE>'s G = sum_s dL/dh (x) x with each fp32 operand split into three bf16 parts
@@ -2524,7 +2529,9 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       csc[c] = ldexpf(1.0f, e);
       cun[c] = ldexpf(1.0f, -e);
     }
-    const int eg = tile_scale_exp(__uint_as_float(*gmax));
+    unsigned gm = 0;
+    for (int i = 0; i < GMAX_SLOTS; ++i) gm = max(gm, gmax[i]);   // (uniform loads)
+    const int eg = tile_scale_exp(__uint_as_float(gm));
     gsc = ldexpf(1.0f, eg);
     gun = ldexpf(1.0f, -eg);
     __syncthreads();
@@ -2841,7 +2848,7 @@ struct BwdWs {
   int* sw;
   f16x8* wth;   // split-fp16 W^T image of k_dgrad_h (train math 1/2)
   float* tmax[2];   // per-tile max |dL/dh| of g[0] / g[1] ([tile][8])
-  unsigned* gmax;   // per layer L: the chunk's largest |dL/dh_L| (float bits; zeroed with s12 per chunk)
+  unsigned* gmax;   // per layer L: GMAX_SLOTS partial maxima of the chunk's |dL/dh_L| (float bits; zeroed per chunk)
   size_t bytes;
 };
 
@@ -2859,7 +2866,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t oenc = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
-  const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257 + 8) * 8), oa = take((size_t)gacc_layout().total * 8);
+  const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257 + GMAX_DBL) * 8), oa = take((size_t)gacc_layout().total * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
   const size_t owt = take(7 * HW_H * sizeof(f16x8));
   const size_t otm0 = take(tiles * 8 * sizeof(float)), otm1 = take(tiles * 8 * sizeof(float));
@@ -3003,7 +3010,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
       hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
       // 2. occ_out + BatchNorm 8
-      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257 + 8) * sizeof(double), s));  // per chunk
+      PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257 + GMAX_DBL) * sizeof(double), s));  // per chunk
       if (PCN_OSTAT1) {
         const unsigned sg = (unsigned)((ntiles + 3) / 4 < 256 ? (ntiles + 3) / 4 : 256);
         hipLaunchKernelGGL(k_out_bwd_stats1, dim3(sg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
@@ -3015,7 +3022,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, P.bn_w[7], P.out_w, ws.ostat, ws.gacc + G.g[7], ws.gacc + G.be[7],
                          ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0], split ? ws.tmax[0] : nullptr,
-                         split ? ws.gmax + 7 : nullptr);
+                         split ? ws.gmax + 7 * GMAX_SLOTS : nullptr);
     }
     // 3. layers 7..1
     int cur = 0;
@@ -3026,10 +3033,10 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
                      2048.0 * dn);
         if (split && L == 4)
           launch_wgrad_b3<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp,
-                             ws.gmax + L, ws.part);
+                             ws.gmax + L * GMAX_SLOTS, ws.part);
         else if (split)
           launch_wgrad_b3<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
-                             ws.gmax + L, ws.part);
+                             ws.gmax + L * GMAX_SLOTS, ws.part);
         else if (L == 4)
           launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
         else
@@ -3051,12 +3058,12 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
           hipLaunchKernelGGL(k_dgrad_h<3>, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.tmax[cur],
                              ws.wth + (size_t)(L - 1) * HW_H, ws.sw, L, hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp,
                              P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1], ws.g[cur ^ 1],
-                             ws.tmax[cur ^ 1], ws.gmax + (L - 1));
+                             ws.tmax[cur ^ 1], ws.gmax + (L - 1) * GMAX_SLOTS);
         else if (split)
           hipLaunchKernelGGL(k_dgrad_h<4>, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.tmax[cur],
                              ws.wth + (size_t)(L - 1) * HW_H, ws.sw, L, hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp,
                              P.bn_w[L - 1], ws.gacc + G.g[L - 1], ws.gacc + G.be[L - 1], ws.g[cur ^ 1],
-                             ws.tmax[cur ^ 1], ws.gmax + (L - 1));
+                             ws.tmax[cur ^ 1], ws.gmax + (L - 1) * GMAX_SLOTS);
         else
           hipLaunchKernelGGL(k_dgrad_ws, dim3(gws), dim3(512), 0, s, ws.g[cur], ws.wt + (size_t)(L - 1) * SZ_H,
                              hh[L - 1], n, ws.s12 + S12_LAYER * L, coefp, P.bn_w[L - 1], ws.gacc + G.g[L - 1],
@@ -3069,7 +3076,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, split ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
       if (split)
         launch_wgrad_b3<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
-                           ws.gmax + 0, ws.part);
+                           ws.gmax + 0 * GMAX_SLOTS, ws.part);
       else
         launch_wgrad<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
                         ws.part);
