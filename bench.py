@@ -437,7 +437,7 @@ def kernel_report(L, a, train_math):
     knames = {0: "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
               3: f"k_train_h<8,true,{nterm}>" if split else "k_train_ws<8,true>",
               10: "k_wgrad<2>+k_wgrad<1>" if split else "k_wgrad<0>", 11: f"k_dgrad_h<{nterm}>" if split else "k_dgrad_ws",
-              13: "k_nof_eval_fold", 14: "k_wgrad_b3<1,0,0>", 15: f"k_train_h1<{nterm}>"}
+              13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
