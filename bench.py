@@ -70,8 +70,9 @@ def parse(argv=None):
     ap.add_argument("--no-fp32-line", action="store_true",
                     help="skip the comparison run of the train lines under the fp32 MFMA train math (profiling)")
     ap.add_argument("--fold", action="store_true",
-                    help="val/view only: the opt-in exact affine fold of the eval network (SURVEY fact 1), reported "
-                         "as its own line, never the headline")
+                    help="the opt-in exact affine fold (SURVEY fact 1): eval modes fold the eval network, train modes "
+                         "the train-mode network per BatchNorm chunk (forward and backward); reported as its own "
+                         "line, never the headline")
     ap.add_argument("--gather", action="store_true",
                     help="gather every block's depth_fine to rank 0 inside each step (eval-driver output path; on "
                          "by default for configs 4 and 5)")
@@ -254,8 +255,9 @@ def main(argv=None):
     grad = a.mode == "train_step"
     if a.fold:
         if train:
-            raise SystemExit("--fold applies to the eval modes (val, view) only")
-        _ops.set_eval_fold(True)
+            _ops.set_train_fold(True)
+        else:
+            _ops.set_eval_fold(True)
     if grad:   # this caller allocates nothing between forward and backward: let the store take the free HBM
         _ops.set_activation_store_budget(1 << 62)
     blocks = make_blocks(a, rank, world, dev, syn)
@@ -338,13 +340,13 @@ def main(argv=None):
             raise RuntimeError(f"non-finite loss {lv}")
         return max_over_ranks(el, device=dev), lv
 
-    train_math = _ops.get_train_math() if train else None
+    train_math = (("fold" if a.fold else _ops.get_train_math()) if train else None)
     elapsed, loss_val = timed(a.steps, a.warmup)
     roof, kernels = kernel_report(L, a, train_math)
 
     # the same workload with the train-mode layers on the fp32 MFMA pipe (train_math "fp32"), for comparison
     fp32_line = None
-    if train and train_math != "fp32" and not a.no_fp32_line:
+    if train and train_math != "fp32" and not a.no_fp32_line and not a.fold:
         _ops.set_train_math("fp32")
         el32, _ = timed(a.steps, 1)
         roof32, k32 = kernel_report(L, a, "fp32")
@@ -402,7 +404,9 @@ def main(argv=None):
                                 "train_step": "render_rays_train fwd + losses + backward + Adam step",
                                 "val": "render_rays_val fwd",
                                 "view": "render_rays_view_0525_2_2 two-step inference (method 2) + effective points"
-                                }[a.mode] + (" -- exact affine fold of the eval network (opt-in)" if a.fold else ""),
+                                }[a.mode] + ((" -- exact affine fold of the train-mode network per BatchNorm chunk "
+                                              "(opt-in)" if train else " -- exact affine fold of the eval network "
+                                              "(opt-in)") if a.fold else ""),
                    "baseline_config": a.config,
                    "rays_per_step": int(rays_per_step), "rays_per_block": a.rays,
                    "blocks_rank0": [blk["block"] for blk in blocks],
@@ -437,7 +441,8 @@ def kernel_report(L, a, train_math):
     knames = {0: "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
               3: f"k_train_h<8,true,{nterm}>" if split else "k_train_ws<8,true>",
               10: "k_wgrad<2>+k_wgrad<1>" if split else "k_wgrad<0>", 11: f"k_dgrad_h<{nterm}>" if split else "k_dgrad_ws",
-              13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>"}
+              13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>",
+              16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
@@ -446,7 +451,7 @@ def kernel_report(L, a, train_math):
     for t, nm in ((0, "eval_query"), (1, "train_hidden"), (2, "train_first"), (3, "train_skip"), (4, "train_out"),
                   (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
                   (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold"), (14, "wgrad_b3"),
-                  (15, "train_h1")):
+                  (15, "train_h1"), (16, "fold_moments"), (17, "fold_algebra")):
         tm, n, f, b = prof_read(L, t)
         if n:
             tr, src = pmc_traffic(pmc_names.get(t, ""))

@@ -135,6 +135,30 @@ int pcnerf_nof_forward_train_backward(const float* emb, int64_t n, const pcnerf_
                                       const float* p, const float* grad_p, void* workspace, size_t workspace_bytes,
                                       const pcnerf_nof_grads* grads, void* stream);
 
+/* ---------------------------------------------------------------- opt-in train-mode affine fold
+ * Exact affine fold of the TRAIN-mode network (SURVEY fact 1 with BatchNorm batch statistics; not the default --
+ * the drop-in evaluates the module as written).  Every LeakyReLU(True) is the identity (models.py:72,152,232), so
+ * within one BatchNorm chunk (render.py:47-50) every layer's batch mean and variance follow exactly from the
+ * chunk's encoding mean and covariance, and NOF(e) = sigmoid(a_c . e + c_c) per chunk c (models.py:183-203).  The
+ * forward computes those per-chunk moments, the float64 layer algebra, p_out and the running-stat updates (chunk by
+ * chunk, as pcnerf_nof_query_train); `state` (pcnerf_nof_train_fold_bytes(total_samples, chunk) bytes) keeps what
+ * the backward needs and must stay unchanged until it runs.  The backward ADDS the parameter gradients (the
+ * Linear biases and the shifts of BatchNorms 0-6 are exactly zero there: the next BatchNorm removes the mean). */
+size_t pcnerf_nof_train_fold_bytes(int64_t total_samples, int64_t chunk);
+int pcnerf_nof_query_train_fold(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
+                                int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
+                                void* state, size_t state_bytes, float* p_out, void* stream);
+int pcnerf_nof_forward_train_fold(const float* emb, int64_t n, const pcnerf_nof_params* params, float momentum,
+                                  float eps, void* state, size_t state_bytes, float* p_out, void* stream);
+int pcnerf_nof_query_train_fold_backward(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                         int n_samples, int64_t chunk, const pcnerf_nof_params* params, float eps,
+                                         const float* grad_logit, void* state, size_t state_bytes,
+                                         const pcnerf_nof_grads* grads, void* stream);
+/* NOF.forward(emb) through the fold (one chunk of n rows); grad_p = dL/dp of its output p. */
+int pcnerf_nof_forward_train_fold_backward(const float* emb, int64_t n, const pcnerf_nof_params* params, float eps,
+                                           const float* p, const float* grad_p, void* state, size_t state_bytes,
+                                           const pcnerf_nof_grads* grads, void* stream);
+
 /* ---------------------------------------------------------------- sampling (render.py:429-454, :497-511)
  * z[ray, :] = linspace sampling of [rays[near_col], rays[far_col]] with n_samples points; if
  * n_parent < n_samples the segmented scheme is used: n_parent points over [near, far] and
@@ -279,7 +303,8 @@ int pcnerf_range_metrics(const float* pred, const float* gt, const float* origin
  * pcnerf_prof_enable(1) makes every subsequent launch record a HIP event pair on its stream; tags:
  * 0 eval query, 1 train hidden Linear, 2 train first Linear, 3 train skip Linear, 4 train occ_out,
  * 5 BN fold, 6 composite, 7 resample, 8 sampling, 9 composite backward, 10 weight-gradient GEMM,
- * 11 data-gradient GEMM, 12 other backward kernels.  pcnerf_prof_read synchronises the tag's events and returns
+ * 11 data-gradient GEMM, 12 other backward kernels, 13 eval/train fold per-sample query, 14 split-math weight
+ * gradients, 15 fused first layers, 16 train-fold moments, 17 train-fold layer algebra.  pcnerf_prof_read synchronises the tag's events and returns
  * the summed duration, launch count and algorithmic FLOPs / bytes of those launches. */
 int pcnerf_prof_enable(int on);
 int pcnerf_prof_read(int tag, double* total_ms, int64_t* launches, double* flops, double* bytes);

@@ -261,16 +261,29 @@ __global__ __launch_bounds__(1024) void k_fold_eval(NofParamsDev P, double* __re
   if (sl == 0 && t == 63) fold[63] = c;
 }
 
-// one thread per sample: p = sigmoid(fl32(a . e + c)); ein != NULL reads the (total, 63) embedding instead
+// one thread per sample: p = sigmoid(fl32(a . e + c)); ein != NULL reads the (total, 63) embedding instead.
+// MODE 0: one coefficient set (eval fold); the train fold has one set per BatchNorm chunk of `chunk` samples:
+// MODE 1 (chunk >= 256: a block spans at most two chunks) stages both in LDS, MODE 2 (small chunks) reads them
+// from global memory per sample.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_nof_eval_fold(const float* __restrict__ rays, int stride,
                                                        const float* __restrict__ z, int64_t total, int S,
                                                        const float* __restrict__ ein, const double* __restrict__ fold,
-                                                       float* __restrict__ p_out) {
-  __shared__ double a[64];
-  if (threadIdx.x < 64) a[threadIdx.x] = fold[threadIdx.x];
+                                                       int64_t chunk, int64_t nfold, float* __restrict__ p_out) {
+  __shared__ double a2[2][64];
+  const int64_t gb = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t cb = MODE == 1 ? gb / chunk : 0;
+  if (MODE != 2 && threadIdx.x < (MODE == 1 ? 128 : 64)) {
+    int64_t cc = cb + (threadIdx.x >> 6);
+    if (cc >= nfold) cc = nfold - 1;
+    a2[threadIdx.x >> 6][threadIdx.x & 63] = fold[cc * 64 + (threadIdx.x & 63)];
+  }
   __syncthreads();
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t g = gb + threadIdx.x;
   if (g >= total) return;
+  const double* __restrict__ a = a2[0];
+  if (MODE == 1) a = a2[g / chunk - cb];
+  if (MODE == 2) a = fold + 64 * (g / chunk);
   double acc = a[63];
   if (ein) {
     const float* e = ein + g * 63;
@@ -302,6 +315,22 @@ __global__ __launch_bounds__(256) void k_nof_eval_fold(const float* __restrict__
   p_out[g] = sigmoid_ref((float)acc);
 }
 
+void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
+                        const double* fold, int64_t chunk, float* p_out, hipStream_t s) {
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks >= (int64_t)1 << 31) throw std::runtime_error("fold query: too many samples for one launch");
+  const int64_t nfold = (total + chunk - 1) / chunk;
+  if (nfold <= 1)
+    hipLaunchKernelGGL(k_nof_eval_fold<0>, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein,
+                       fold, total, (int64_t)1, p_out);
+  else if (chunk >= 256)
+    hipLaunchKernelGGL(k_nof_eval_fold<1>, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein,
+                       fold, chunk, nfold, p_out);
+  else
+    hipLaunchKernelGGL(k_nof_eval_fold<2>, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein,
+                       fold, chunk, nfold, p_out);
+}
+
 }  // namespace pcn
 
 using namespace pcn;
@@ -329,8 +358,7 @@ extern "C" int pcnerf_nof_query_eval_fold(const float* rays, int64_t n_rays, int
     // algorithmic work per sample: 63 FMA + the encoding; bytes: z in, p out, ray rows
     ProfScope ps((hipStream_t)stream, PT_EVAL_FOLD, 126.0 * (double)total,
                  8.0 * (double)total + 4.0 * ray_stride * (double)n_rays);
-    hipLaunchKernelGGL(k_nof_eval_fold, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rays,
-                       ray_stride, z, total, n_samples, (const float*)nullptr, fold, p_out);
+    launch_fold_logits(rays, ray_stride, z, total, n_samples, nullptr, fold, total, p_out, (hipStream_t)stream);
   }
   PCN_LAUNCH_CHECK("pcnerf_nof_query_eval_fold");
   PCN_API_END
@@ -343,8 +371,7 @@ extern "C" int pcnerf_nof_forward_eval_fold(const float* emb, int64_t n, const d
   PCN_CHECK(n > 0, "pcnerf_nof_forward_eval_fold: empty input");
   const int64_t blocks = (n + 255) / 256;
   PCN_CHECK(blocks < (int64_t)1 << 31, "pcnerf_nof_forward_eval_fold: too many samples for one launch");
-  hipLaunchKernelGGL(k_nof_eval_fold, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                     (const float*)nullptr, 0, (const float*)nullptr, n, 1, emb, fold, p_out);
+  launch_fold_logits(nullptr, 0, nullptr, n, 1, emb, fold, n, p_out, (hipStream_t)stream);
   PCN_LAUNCH_CHECK("pcnerf_nof_forward_eval_fold");
   PCN_API_END
 }

@@ -1,0 +1,810 @@
+// Opt-in exact affine fold of the TRAIN-mode network, forward and backward (SURVEY fact 1, §7 "alternative exact
+// route").  Never the default: the drop-in evaluates the module as written (nof_train.hip).
+//
+// Every LeakyReLU(True) of NOF is the identity (negative_slope = 1, models.py:72,152,232), so within one BatchNorm
+// chunk (render.py:47-50) every layer output is an affine map of the sample's encoding e (models.py:27-41):
+//   x_L = P_L (e - ebar) + beta_L,   P_L = s_L (.) P'_L,   P'_L = W_L P_{L-1}   (skip layer: W_e + W_h P_3)
+// and BatchNorm's batch statistics follow exactly from the chunk's encoding mean ebar and covariance Sigma:
+//   mean(h_L) = W_L mean(x_{L-1}) + b_L,  var(h_L)_i = p'_i^T Sigma p'_i,  s_L = gamma / sqrt(var + eps)
+// (models.py:183-203; nn.BatchNorm1d train: biased variance for the normalisation, unbiased for running_var).
+// The chunk's network is then sigmoid(a_c . e + c_c) with a_c = w_out P_7, c_c = w_out . beta_7 + b_out - a_c . ebar.
+// Rounding differs from the layer-by-layer fp32 network (the algebra runs in float64), so the path is opt-in and
+// reported as its own bench line.
+//
+// Forward per query (all chunks of one render pass batched into each launch):
+//   k_tf_moments   per chunk: sum over samples of d d^T, d = [e - e0, 1] (e0 = the chunk's first encoding,
+//                  a shift against cancellation), fp16 hi/mid parts on the matrix pipe per 64-sample tile (three
+//                  exact products, fp32 accumulation), float64 across tiles
+//   k_tf_stats     ebar, Sigma per chunk (float64)
+//   k_tf_layer<L>  P'_L, Q_L = P'_L Sigma, var, s, the pre-BN mean (float64 GEMMs, 64-row tiles x chunks)
+//   k_tf_out       (a_c, c_c);  launch_fold_logits: p = sigmoid(a_c . e + c_c) per sample
+//   k_tf_running   running_mean / running_var, chunk by chunk in order (bn_coeffs' arithmetic)
+// Backward (dL/dlogit per sample):
+//   k_tf_gmoments  per chunk: abar = sum_s g_s (e_s - ebar), gbar = sum_s g_s
+//   k_tf_bwd_out   occ_out / beta_7 gradients, adjoint of P_7 -> through BatchNorm 7 to the adjoint A'_7 of P'_7
+//   per layer L = 7..0: k_tf_dw<L> (dW_L = sum_c A'_L P_{L-1}^T, chunk-group partials), k_tf_dw_reduce<L>,
+//                  k_tf_bwd_layer<L> (A_{L-1} = W_L^T A'_L, then BatchNorm L-1's backward:
+//                  ds = A.p', dgamma += ds / sqrt(var+eps), dvar = -ds gamma / (2 (var+eps)^1.5),
+//                  A'_{L-1} = s A + 2 dvar Q_{L-1})
+//   k_tf_vec_reduce gamma / out gradients summed over chunks.
+// The Linear biases and the shifts of every BatchNorm that feeds Linear->BatchNorm get exactly zero gradient (the
+// next BatchNorm removes the mean); the reference's autograd gives rounding noise there.
+#include <algorithm>
+
+#include "common.h"
+#include "pcnerf_internal.h"
+#include "prof.h"
+
+namespace pcn {
+
+constexpr int TF_WPC_MAX = 16;   // moment workgroups per chunk
+constexpr int TF_G_MAX = 16;     // chunk groups of the weight-gradient partials
+
+struct FoldDev {   // device views of the fold state (float64 throughout)
+  int64_t C;       // BatchNorm chunks of the query
+  int wpc, G;
+  double* mom;     // [C][wpc][64][64] moment partials (blocks 00, 01, 11 of d d^T)
+  double* sig;     // [C][64][64] Sigma (row / column 63 zero)
+  double* eb;      // [C][64] ebar (63 used)
+  double* e0;      // [C][64] the chunk's shift
+  double* pp;      // [8][C][256][64] P'_L (column 63: W_L mean(x_{L-1}))
+  double* q;       // [8][C][256][64] P'_L Sigma
+  double* sr;      // [8][C][4][256] s, 1/sqrt(var+eps), mean(h_L), var(h_L)
+  double* fold;    // [C][64] (a_c, c_c)
+  double* gm;      // [C][wpc][64] backward moment partials
+  double* ab;      // [2][C][256][64] A'_L ping-pong
+  double* dg;      // [8][C][256] dgamma per chunk
+  double* dw;      // [G][256][256] weight-gradient partials (h columns)
+  double* vec;     // [C][576] d out_w (256), d beta_7 (256), d out_b (1)
+};
+
+struct FoldLayout {
+  int64_t C;
+  int wpc, G;
+  size_t off[13];
+  size_t doubles;
+};
+
+static FoldLayout fold_layout(int64_t total, int64_t chunk) {
+  FoldLayout F{};
+  F.C = (total + chunk - 1) / chunk;
+  const int64_t tiles = (std::min(chunk, total) + 63) / 64;
+  F.wpc = (int)std::max<int64_t>(1, std::min<int64_t>(TF_WPC_MAX, tiles / 64));
+  F.G = (int)std::min<int64_t>(F.C, TF_G_MAX);
+  const size_t C = (size_t)F.C, wpc = (size_t)F.wpc, G = (size_t)F.G;
+  const size_t n[13] = {C * wpc * 4096, C * 4096, C * 64, C * 64, 8 * C * 256 * 64, 8 * C * 256 * 64,
+                        8 * C * 1024, C * 64, C * wpc * 64, 2 * C * 256 * 64, 8 * C * 256, G * 256 * 256, C * 576};
+  size_t o = 0;
+  for (int i = 0; i < 13; ++i) {
+    F.off[i] = o;
+    o += (n[i] + 31) & ~(size_t)31;   // 256-byte aligned pieces
+  }
+  F.doubles = o;
+  return F;
+}
+
+static FoldDev fold_dev(const FoldLayout& L, void* state) {
+  double* b = (double*)state;
+  FoldDev F;
+  F.C = L.C;
+  F.wpc = L.wpc;
+  F.G = L.G;
+  double** dst[13] = {&F.mom, &F.sig, &F.eb, &F.e0, &F.pp, &F.q, &F.sr, &F.fold, &F.gm, &F.ab, &F.dg, &F.dw, &F.vec};
+  for (int i = 0; i < 13; ++i) *dst[i] = b + L.off[i];
+  return F;
+}
+
+struct SampleSrc {   // the query's flattened ray-major samples (rays + z) or an embedded batch (ein)
+  const float* rays;
+  int stride;
+  const float* z;
+  int S;
+  const float* ein;
+  int64_t total, chunk;
+};
+
+__device__ __forceinline__ void sample_enc(const SampleSrc& q, int64_t g, float (&f)[64]) {
+  if (q.ein) {
+    const float* r = q.ein + g * 63;
+#pragma unroll
+    for (int k = 0; k < 63; ++k) f[k] = r[k];
+    f[63] = 0.0f;
+  } else {
+    float p[3];
+    sample_point(q.rays + (g / q.S) * q.stride, q.z[g], p);
+    encode_full(p, f);
+  }
+}
+
+__device__ __forceinline__ int64_t chunk_len(const SampleSrc& q, int64_t c) {
+  const int64_t r = q.total - c * q.chunk;
+  return r < q.chunk ? r : q.chunk;
+}
+
+// ------------------------------------------------------------------------------------------------- forward
+// grid (wpc, C), 256 threads.  Each wave stages 64 samples' d = [e - e0, 1] (zero past the chunk) as two fp16
+// parts (hi = fp16(d), mid = fp16(d - hi): 22 significant bits) in a [feature][sample] LDS tile, and accumulates
+// d d^T (blocks 00, 01, 11 of 64 x 64) on v_mfma_f32_32x32x16_f16 as hi.hi + hi.mid + mid.hi (exact products,
+// fp32 accumulation over the 64-sample tile, float64 across tiles).  The tile rows are 72 halves apart, so the
+// operand reads (16 bytes: 8 samples of one feature) of 16 lanes hit 16 disjoint bank groups.
+typedef _Float16 tf_f16x8 __attribute__((ext_vector_type(8)));
+constexpr int TM_P = 72;
+
+__global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
+  __shared__ __attribute__((aligned(16))) _Float16 th[4][2][64 * TM_P];
+  __shared__ float sh0[64];
+  const int c = blockIdx.y, w = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t c0 = (int64_t)c * q.chunk, n = chunk_len(q, c);
+  if (tid == 0) {
+    float f[64];
+    sample_enc(q, c0, f);
+#pragma unroll
+    for (int k = 0; k < 63; ++k) sh0[k] = f[k];
+    sh0[63] = 0.0f;
+  }
+  __syncthreads();
+  if (w == 0 && tid < 64) F.e0[(int64_t)c * 64 + tid] = (double)sh0[tid];
+  const int64_t ntile = (n + 63) / 64, per = (ntile + F.wpc - 1) / F.wpc;
+  const int64_t t0 = std::min(ntile, (int64_t)w * per), t1 = std::min(ntile, t0 + per);
+  f32x16 a00 = {}, a01 = {}, a11 = {};
+  double d00[16], d01[16], d11[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) d00[r] = d01[r] = d11[r] = 0.0;
+  _Float16* hi = th[wave][0];
+  _Float16* mi = th[wave][1];
+  for (int64_t base = t0; base < t1; base += 4) {   // same trip count in every wave (barriers below)
+    const int64_t t = base + wave, i = t * 64 + lane;
+    const bool ok = t < t1 && i < n;
+    auto put = [&](int f, float v) {
+      const float d = ok ? v - sh0[f] : 0.0f;
+      const _Float16 h = (_Float16)d;
+      hi[f * TM_P + lane] = h;
+      mi[f * TM_P + lane] = (_Float16)(d - (float)h);
+    };
+    if (q.ein) {
+      const float* r = q.ein + (c0 + (ok ? i : 0)) * 63;
+#pragma unroll 7
+      for (int f = 0; f < 63; ++f) put(f, r[f]);
+    } else {
+      float p[3] = {0.0f, 0.0f, 0.0f};
+      if (ok) sample_point(q.rays + ((c0 + i) / q.S) * q.stride, q.z[c0 + i], p);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) put(m, p[m]);
+#pragma unroll 2
+      for (int k = 0; k < 10; ++k) {
+        const float sc = (float)(1 << k);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          float sv, cv;
+          sincosf(sc * p[m], &sv, &cv);
+          put(3 + 6 * k + m, sv);
+          put(6 + 6 * k + m, cv);
+        }
+      }
+    }
+    hi[63 * TM_P + lane] = ok ? (_Float16)1.0f : (_Float16)0.0f;
+    mi[63 * TM_P + lane] = (_Float16)0.0f;
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int o = (lane & 31) * TM_P + 16 * ks + 8 * (lane >> 5);
+      const tf_f16x8 h0 = *reinterpret_cast<const tf_f16x8*>(hi + o);
+      const tf_f16x8 m0 = *reinterpret_cast<const tf_f16x8*>(mi + o);
+      const tf_f16x8 h1 = *reinterpret_cast<const tf_f16x8*>(hi + 32 * TM_P + o);
+      const tf_f16x8 m1 = *reinterpret_cast<const tf_f16x8*>(mi + 32 * TM_P + o);
+      a00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h0, h0, a00, 0, 0, 0);
+      a01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h0, h1, a01, 0, 0, 0);
+      a11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h1, h1, a11, 0, 0, 0);
+      a00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h0, m0, a00, 0, 0, 0);
+      a01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h0, m1, a01, 0, 0, 0);
+      a11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h1, m1, a11, 0, 0, 0);
+      a00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m0, h0, a00, 0, 0, 0);
+      a01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m0, h1, a01, 0, 0, 0);
+      a11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m1, h1, a11, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      d00[r] += (double)a00[r];
+      d01[r] += (double)a01[r];
+      d11[r] += (double)a11[r];
+      a00[r] = a01[r] = a11[r] = 0.0f;
+    }
+    __syncthreads();
+  }
+  // the four waves' blocks summed in a fixed order through LDS (aliasing the tiles), then one coalesced store
+  double* red = reinterpret_cast<double*>(&th[0][0][0]);
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j = lane & 31;
+        if (wv == 0) {
+          red[i * 64 + j] = d00[r];
+          red[i * 64 + 32 + j] = d01[r];
+          red[(32 + i) * 64 + 32 + j] = d11[r];
+          red[(32 + i) * 64 + j] = 0.0;
+        } else {
+          red[i * 64 + j] += d00[r];
+          red[i * 64 + 32 + j] += d01[r];
+          red[(32 + i) * 64 + 32 + j] += d11[r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  double* out = F.mom + ((int64_t)c * F.wpc + w) * 4096;
+  for (int k = tid; k < 4096; k += 256) out[k] = red[k];
+}
+
+// grid C, 256 threads: n = sum d_63^2, dbar = sum d / n, Sigma = sum d d^T / n - dbar dbar^T, ebar = e0 + dbar.
+__global__ __launch_bounds__(256) void k_tf_stats(FoldDev F) {
+  __shared__ double G[4096];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const double* m = F.mom + (int64_t)c * F.wpc * 4096;
+  for (int k = tid; k < 4096; k += 256) {
+    double s = 0.0;
+    for (int w = 0; w < F.wpc; ++w) s += m[(int64_t)w * 4096 + k];
+    G[k] = s;
+  }
+  __syncthreads();
+  const double n = G[63 * 64 + 63];
+  for (int k = tid; k < 4096; k += 256) {
+    const int i = k >> 6, j = k & 63;
+    double v = 0.0;
+    if (i < 63 && j < 63) {
+      const int lo = i < j ? i : j, hi = i < j ? j : i;   // blocks 00, 01, 11 hold the upper triangle
+      v = G[lo * 64 + hi] / n - (G[i * 64 + 63] / n) * (G[j * 64 + 63] / n);
+    }
+    F.sig[(int64_t)c * 4096 + k] = v;
+  }
+  if (tid < 64) F.eb[(int64_t)c * 64 + tid] = tid < 63 ? F.e0[(int64_t)c * 64 + tid] + G[tid * 64 + 63] / n : 0.0;
+}
+
+// grid (4, C), 256 threads: rows R0..R0+63 of P'_L = W_L B for chunk c, where B's rows are [unit_k | ebar_k] for
+// the encoding inputs and [s_{L-1,k} P'_{L-1}[k] | beta_{L-1,k}] for the previous layer's features; then
+// Q = P' Sigma, var_i = Q_i . p'_i, s = gamma / sqrt(var + eps), mean(h_L) = P'[:, 63] + b_L.
+// Thread (ty, tx) owns rows 16 i + ty and columns 16 j + tx of the tile.
+template <int L>
+__global__ __launch_bounds__(256) void k_tf_layer(NofParamsDev P, FoldDev F, double eps) {
+  constexpr int IN = L == 0 ? 63 : L == 4 ? 319 : 256;
+  constexpr int KE = (L == 0 || L == 4) ? 63 : 0;
+  __shared__ double As[64][33];
+  __shared__ double Bs[32][64];
+  __shared__ double Ps[64][65];
+  __shared__ double Sg[64][64];
+  const int64_t C = F.C;
+  const int c = blockIdx.y, R0 = blockIdx.x * 64, tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const float* __restrict__ W = P.lin_w[L];
+  const double* eb = F.eb + (int64_t)c * 64;
+  const double* pprev = F.pp + ((int64_t)(L > 0 ? L - 1 : 0) * C + c) * 256 * 64;
+  const double* sprev = F.sr + ((int64_t)(L > 0 ? L - 1 : 0) * C + c) * 1024;
+  const float* bprev = P.bn_b[L > 0 ? L - 1 : 0];
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int k0 = 0; k0 < IN; k0 += 32) {
+    for (int e = tid; e < 2048; e += 256) {
+      const int r = e >> 5, kk = e & 31, k = k0 + kk;
+      As[r][kk] = k < IN ? (double)W[(int64_t)(R0 + r) * IN + k] : 0.0;
+    }
+    for (int e = tid; e < 2048; e += 256) {
+      const int kk = e >> 6, col = e & 63, k = k0 + kk;
+      double v = 0.0;
+      if (k < KE) {
+        v = col < 63 ? (k == col ? 1.0 : 0.0) : eb[k];
+      } else if (k < IN) {
+        const int kh = k - KE;
+        v = col < 63 ? sprev[kh] * pprev[kh * 64 + col] : (double)bprev[kh];
+      }
+      Bs[kk][col] = v;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < 32; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[16 * i + ty][kk];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][16 * j + tx];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
+    }
+    __syncthreads();
+  }
+  const int64_t base = (((int64_t)L * C + c) * 256 + R0) * 64;
+  double* pp = F.pp + base;
+  double* qo = F.q + base;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pp[(16 * i + ty) * 64 + 16 * j + tx] = acc[i][j];
+      Ps[16 * i + ty][16 * j + tx] = acc[i][j];
+    }
+  const double* sg = F.sig + (int64_t)c * 4096;
+  for (int e = tid; e < 4096; e += 256) Sg[e >> 6][e & 63] = sg[e];
+  __syncthreads();
+  double qv[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qv[i][j] = 0.0;
+#pragma unroll 3
+  for (int k = 0; k < 63; ++k) {
+    double a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = Ps[16 * i + ty][k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = Sg[k][16 * j + tx];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qv[i][j] += a[i] * b[j];
+  }
+  double* sr = F.sr + ((int64_t)L * C + c) * 1024;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      qo[(16 * i + ty) * 64 + 16 * j + tx] = qv[i][j];
+      if (16 * j + tx < 63) v += qv[i][j] * acc[i][j];
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+    if (tx == 0) {
+      const int row = R0 + 16 * i + ty;
+      if (v < 0.0) v = 0.0;
+      const double rinv = 1.0 / sqrt(v + eps);
+      sr[row] = (double)P.bn_w[L][row] * rinv;
+      sr[256 + row] = rinv;
+      sr[512 + row] = Ps[16 * i + ty][63] + (double)P.lin_b[L][row];
+      sr[768 + row] = v;
+    }
+  }
+}
+
+// grid C, 256 threads: a_c = sum_i w_i s_7i P'_7[i][:63], c_c = w . beta_7 + b_out - a_c . ebar.
+__global__ __launch_bounds__(256) void k_tf_out(NofParamsDev P, FoldDev F) {
+  __shared__ double u[256];
+  __shared__ double part[4][64];
+  __shared__ double cw[4];
+  const int c = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t C = F.C;
+  const double* sr7 = F.sr + (7 * C + c) * 1024;
+  u[tid] = (double)P.out_w[tid] * sr7[tid];
+  const double cb = wave_sum_d((double)P.out_w[tid] * (double)P.bn_b[7][tid]);
+  if (lane == 0) cw[wave] = cb;
+  __syncthreads();
+  const double* pp7 = F.pp + (7 * C + c) * 256 * 64;
+  double s = 0.0;
+  for (int i = 64 * wave; i < 64 * wave + 64; ++i) s += u[i] * pp7[i * 64 + lane];
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0) {
+    const double a = lane < 63 ? (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]) : 0.0;
+    const double t = wave_sum_d(a * F.eb[(int64_t)c * 64 + lane]);
+    F.fold[(int64_t)c * 64 + lane] =
+        lane < 63 ? a : ((cw[0] + cw[1]) + (cw[2] + cw[3])) + (double)P.out_b[0] - t;
+  }
+}
+
+// grid 8, 256 threads: running stats chunk by chunk, bn_coeffs' arithmetic (float64 update, stored as float).
+__global__ void k_tf_running(NofParamsDev P, FoldDev F, SampleSrc q, double mom) {
+  const int L = blockIdx.x, k = threadIdx.x;
+  if (!P.bn_rm[L]) return;
+  float rm = P.bn_rm[L][k], rv = P.bn_rv[L][k];
+  for (int64_t c = 0; c < F.C; ++c) {
+    const double* sr = F.sr + ((int64_t)L * F.C + c) * 1024;
+    const int64_t n = chunk_len(q, c);
+    const double mean = sr[512 + k], var = sr[768 + k];
+    rm = (float)(mom * mean + (1.0 - mom) * (double)rm);
+    const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+    rv = (float)(mom * unb + (1.0 - mom) * (double)rv);
+  }
+  P.bn_rm[L][k] = rm;
+  P.bn_rv[L][k] = rv;
+}
+
+// ------------------------------------------------------------------------------------------------- backward
+__device__ __forceinline__ float fold_logit_grad(const float* __restrict__ g, const float* __restrict__ p,
+                                                 int64_t i) {
+  if (!p) return g[i];
+  const float pv = p[i];
+  return g[i] * (1.0f - pv) * pv;   // sigmoid backward (as nof_train.hip's logit_grad)
+}
+
+// grid (wpc, C), 256 threads: sum g_s d_s (d as in k_tf_moments, fp32 here; d_63 = 1).  Each wave stages 64
+// samples' d as a [sample][feature] fp32 tile (one lane per sample, its encoding written as computed) and g in
+// LDS; then lane f accumulates sum_s g_s d_s[f] over the tile in float64 (exact products, one register).
+__global__ __launch_bounds__(256) void k_tf_gmoments(SampleSrc q, FoldDev F, const float* __restrict__ g,
+                                                     const float* __restrict__ p) {
+  __shared__ float tile[4][64 * 65];
+  __shared__ float gs[4][64];
+  __shared__ float sh0[64];
+  __shared__ double red[4][64];
+  const int c = blockIdx.y, w = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t c0 = (int64_t)c * q.chunk, n = chunk_len(q, c);
+  if (tid < 64) sh0[tid] = (float)F.e0[(int64_t)c * 64 + tid];
+  __syncthreads();
+  const int64_t ntile = (n + 63) / 64, per = (ntile + F.wpc - 1) / F.wpc;
+  const int64_t t0 = std::min(ntile, (int64_t)w * per), t1 = std::min(ntile, t0 + per);
+  float* my = tile[wave];
+  double acc = 0.0;
+  for (int64_t base = t0; base < t1; base += 4) {   // same trip count in every wave (barriers below)
+    const int64_t t = base + wave, i = t * 64 + lane;
+    const bool ok = t < t1 && i < n;
+    auto put = [&](int f, float v) { my[lane * 65 + f] = ok ? v - sh0[f] : 0.0f; };
+    if (q.ein) {
+      const float* r = q.ein + (c0 + (ok ? i : 0)) * 63;
+#pragma unroll 7
+      for (int f = 0; f < 63; ++f) put(f, r[f]);
+    } else {
+      float pt[3] = {0.0f, 0.0f, 0.0f};
+      if (ok) sample_point(q.rays + ((c0 + i) / q.S) * q.stride, q.z[c0 + i], pt);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) put(m, pt[m]);
+#pragma unroll 2
+      for (int k = 0; k < 10; ++k) {
+        const float sc = (float)(1 << k);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          float sv, cv;
+          sincosf(sc * pt[m], &sv, &cv);
+          put(3 + 6 * k + m, sv);
+          put(6 + 6 * k + m, cv);
+        }
+      }
+    }
+    my[lane * 65 + 63] = ok ? 1.0f : 0.0f;
+    gs[wave][lane] = ok ? fold_logit_grad(g, p, c0 + i) : 0.0f;
+    __syncthreads();
+#pragma unroll 16
+    for (int s = 0; s < 64; ++s) acc += (double)gs[wave][s] * (double)my[s * 65 + lane];
+    __syncthreads();
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (tid < 64)
+    F.gm[((int64_t)c * F.wpc + w) * 64 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+}
+
+// grid C, 256 threads: abar = sum g (d - dbar), gbar = sum g; occ_out / beta_7 gradient partials; the adjoint of
+// P_7 is w_i abar_j, taken through BatchNorm 7 to A'_7 (ab[1]).
+__global__ __launch_bounds__(256) void k_tf_bwd_out(NofParamsDev P, FoldDev F) {
+  __shared__ double ab[64];
+  __shared__ double dot[256], coef[256], dvv[256];
+  __shared__ double gbar_s;
+  const int c = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t C = F.C;
+  if (wave == 0) {
+    double G = 0.0;
+    for (int w = 0; w < F.wpc; ++w) G += F.gm[((int64_t)c * F.wpc + w) * 64 + lane];
+    const double gb = __shfl(G, 63, 64);
+    ab[lane] = lane < 63 ? G - gb * (F.eb[(int64_t)c * 64 + lane] - F.e0[(int64_t)c * 64 + lane]) : 0.0;
+    if (lane == 0) gbar_s = gb;
+  }
+  __syncthreads();
+  const double* pp7 = F.pp + (7 * C + c) * 256 * 64;
+  const double* q7 = F.q + (7 * C + c) * 256 * 64;
+  for (int r = wave; r < 256; r += 4) {
+    const double d = wave_sum_d(ab[lane] * pp7[r * 64 + lane]);
+    if (lane == 0) dot[r] = d;
+  }
+  __syncthreads();
+  const double* sr7 = F.sr + (7 * C + c) * 1024;
+  {
+    const int i = tid;
+    const double gb = gbar_s, s7 = sr7[i], rinv = sr7[256 + i], gam = (double)P.bn_w[7][i];
+    const double w = (double)P.out_w[i], beta = (double)P.bn_b[7][i];
+    double* v = F.vec + (int64_t)c * 576;
+    v[i] = s7 * dot[i] + beta * gb;
+    v[256 + i] = w * gb;
+    if (i == 0) v[512] = gb;
+    const double ds = w * dot[i];
+    F.dg[(7 * C + c) * 256 + i] = ds * rinv;
+    dvv[i] = -0.5 * ds * gam * rinv * rinv * rinv;
+    coef[i] = s7 * w;
+  }
+  __syncthreads();
+  double* out = F.ab + (1 * C + c) * 256 * 64;
+  for (int r = wave; r < 256; r += 4)
+    out[r * 64 + lane] = lane < 63 ? coef[r] * ab[lane] + 2.0 * dvv[r] * q7[r * 64 + lane] : 0.0;
+}
+
+// grid (4, C), 256 threads: A_{L-1}[k][j] = sum_i W_L[i][OFF + k] A'_L[i][j] for rows k0..k0+63, then BatchNorm
+// L-1's backward to A'_{L-1} (ab[(L-1)&1]) and dgamma_{L-1} per chunk.
+template <int L>
+__global__ __launch_bounds__(256) void k_tf_bwd_layer(NofParamsDev P, FoldDev F) {
+  constexpr int IN = L == 4 ? 319 : 256, OFF = L == 4 ? 63 : 0;
+  __shared__ double As[64][33];
+  __shared__ double Bs[32][64];
+  const int64_t C = F.C;
+  const int c = blockIdx.y, K0 = blockIdx.x * 64, tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const float* __restrict__ W = P.lin_w[L];
+  const double* abin = F.ab + ((int64_t)(L & 1) * C + c) * 256 * 64;
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int i0 = 0; i0 < 256; i0 += 32) {
+    for (int e = tid; e < 2048; e += 256) {
+      const int ii = e >> 6, kk = e & 63;
+      As[kk][ii] = (double)W[(int64_t)(i0 + ii) * IN + OFF + K0 + kk];
+    }
+    for (int e = tid; e < 2048; e += 256) {
+      const int ii = e >> 6, j = e & 63;
+      Bs[ii][j] = abin[(i0 + ii) * 64 + j];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int ii = 0; ii < 32; ++ii) {
+      double a[4], b[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) a[x] = As[16 * x + ty][ii];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) b[y] = Bs[ii][16 * y + tx];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * b[y];
+    }
+    __syncthreads();
+  }
+  constexpr int LP = L - 1;
+  const double* ppp = F.pp + ((int64_t)LP * C + c) * 256 * 64;
+  const double* qq = F.q + ((int64_t)LP * C + c) * 256 * 64;
+  const double* srp = F.sr + ((int64_t)LP * C + c) * 1024;
+  double* out = F.ab + ((int64_t)(LP & 1) * C + c) * 256 * 64;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const int k = K0 + 16 * x + ty;
+    double ds = 0.0;
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+      if (16 * y + tx < 63) ds += acc[x][y] * ppp[k * 64 + 16 * y + tx];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) ds += __shfl_xor(ds, o, 64);
+    const double s = srp[k], rinv = srp[256 + k], gam = (double)P.bn_w[LP][k];
+    if (tx == 0) F.dg[((int64_t)LP * C + c) * 256 + k] = ds * rinv;
+    const double dv = -0.5 * ds * gam * rinv * rinv * rinv;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int col = 16 * y + tx;
+      out[k * 64 + col] = col < 63 ? s * acc[x][y] + 2.0 * dv * qq[k * 64 + col] : 0.0;
+    }
+  }
+}
+
+// grid (16, G), 256 threads: partial g of dW_L's h columns, sum over the group's chunks of
+// A'_L[i][j] * s_{L-1,k} P'_{L-1}[k][j] (j < 63), one 64 x 64 tile (rows I0, columns K0) per workgroup.
+template <int L>
+__global__ __launch_bounds__(256) void k_tf_dw(FoldDev F) {
+  __shared__ double As[64][65];
+  __shared__ double Bs[64][65];
+  const int64_t C = F.C;
+  const int I0 = (blockIdx.x >> 2) * 64, K0 = (blockIdx.x & 3) * 64, g = blockIdx.y;
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const int64_t cg0 = C * g / F.G, cg1 = C * (g + 1) / F.G;
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int64_t c = cg0; c < cg1; ++c) {
+    const double* abin = F.ab + ((int64_t)(L & 1) * C + c) * 256 * 64;
+    const double* pp = F.pp + ((int64_t)(L - 1) * C + c) * 256 * 64;
+    const double* s = F.sr + ((int64_t)(L - 1) * C + c) * 1024;
+    for (int e = tid; e < 4096; e += 256) {
+      const int r = e >> 6, j = e & 63;
+      As[r][j] = abin[(I0 + r) * 64 + j];
+      Bs[j][r] = j < 63 ? s[K0 + r] * pp[(K0 + r) * 64 + j] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 3
+    for (int j = 0; j < 63; ++j) {
+      double a[4], b[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) a[x] = As[16 * x + ty][j];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) b[y] = Bs[j][16 * y + tx];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * b[y];
+    }
+    __syncthreads();
+  }
+  double* out = F.dw + (int64_t)g * 65536;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) out[(I0 + 16 * x + ty) * 256 + K0 + 16 * y + tx] = acc[x][y];
+}
+
+// grid 256 (rows i), 320 threads (columns): dW_L[i][col] += encoding columns: sum_c A'_L[i][col]; h columns: the
+// chunk-group partials, in a fixed order.
+template <int L>
+__global__ __launch_bounds__(320) void k_tf_dw_reduce(FoldDev F, float* __restrict__ gw) {
+  constexpr int IN = L == 0 ? 63 : L == 4 ? 319 : 256;
+  constexpr int KE = (L == 0 || L == 4) ? 63 : 0;
+  const int i = blockIdx.x, col = threadIdx.x;
+  if (col >= IN) return;
+  double s = 0.0;
+  if (col < KE) {
+    for (int64_t c = 0; c < F.C; ++c) s += F.ab[((int64_t)(L & 1) * F.C + c) * 256 * 64 + i * 64 + col];
+  } else {
+    for (int g = 0; g < F.G; ++g) s += F.dw[(int64_t)g * 65536 + i * 256 + col - KE];
+  }
+  gw[(int64_t)i * IN + col] += (float)s;
+}
+
+// grid 10, 256 threads: blocks 0-7 dgamma_L, block 8 d out_w, block 9 d beta_7 and d out_b, summed over chunks.
+__global__ void k_tf_vec_reduce(FoldDev F, pcnerf_nof_grads G) {
+  const int b = blockIdx.x, k = threadIdx.x;
+  double s = 0.0;
+  if (b < 8) {
+    if (!G.bn_w[b]) return;
+    for (int64_t c = 0; c < F.C; ++c) s += F.dg[((int64_t)b * F.C + c) * 256 + k];
+    G.bn_w[b][k] += (float)s;
+  } else if (b == 8) {
+    if (!G.out_w) return;
+    for (int64_t c = 0; c < F.C; ++c) s += F.vec[c * 576 + k];
+    G.out_w[k] += (float)s;
+  } else {
+    if (G.bn_b[7]) {
+      for (int64_t c = 0; c < F.C; ++c) s += F.vec[c * 576 + 256 + k];
+      G.bn_b[7][k] += (float)s;
+    }
+    if (k == 0 && G.out_b) {
+      double t = 0.0;
+      for (int64_t c = 0; c < F.C; ++c) t += F.vec[c * 576 + 512];
+      G.out_b[0] += (float)t;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------- host
+template <int L>
+static void launch_layer(const NofParamsDev& P, const FoldDev& F, double eps, hipStream_t s) {
+  hipLaunchKernelGGL(k_tf_layer<L>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F, eps);
+}
+
+static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, float momentum, float eps,
+                         void* state, size_t state_bytes, float* p_out, hipStream_t s) {
+  PCN_CHECK(q.total > 0 && q.chunk > 0, "train fold: empty input");
+  const FoldLayout Lo = fold_layout(q.total, q.chunk);
+  PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train fold: state buffer too small");
+  PCN_CHECK(Lo.C < 65536, "train fold: too many chunks for one query");
+  NofParamsDev P;
+  PCN_CHECK(to_dev_params(params, eps, &P), "train fold: null parameter pointer");
+  const FoldDev F = fold_dev(Lo, state);
+  const double ep = (double)eps;
+  {
+    // algorithmic work per sample: the encoding + 3 x 32 x 32 x 2 flops per k-step pair; bytes: z in, ray rows
+    ProfScope ps(s, PT_FOLD_MOMENTS, 6144.0 * (double)q.total, 4.0 * (double)q.total);
+    hipLaunchKernelGGL(k_tf_moments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F);
+  }
+  {
+    ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
+    hipLaunchKernelGGL(k_tf_stats, dim3((unsigned)F.C), dim3(256), 0, s, F);
+    launch_layer<0>(P, F, ep, s);
+    launch_layer<1>(P, F, ep, s);
+    launch_layer<2>(P, F, ep, s);
+    launch_layer<3>(P, F, ep, s);
+    launch_layer<4>(P, F, ep, s);
+    launch_layer<5>(P, F, ep, s);
+    launch_layer<6>(P, F, ep, s);
+    launch_layer<7>(P, F, ep, s);
+    hipLaunchKernelGGL(k_tf_out, dim3((unsigned)F.C), dim3(256), 0, s, P, F);
+  }
+  {
+    ProfScope ps(s, PT_EVAL_FOLD, 126.0 * (double)q.total, 8.0 * (double)q.total);
+    launch_fold_logits(q.rays, q.stride, q.z, q.total, q.S, q.ein, F.fold, q.chunk, p_out, s);
+  }
+  hipLaunchKernelGGL(k_tf_running, dim3(8), dim3(256), 0, s, P, F, q, (double)momentum);
+}
+
+template <int L>
+static void backward_layer(const NofParamsDev& P, const FoldDev& F, const pcnerf_nof_grads* G, hipStream_t s) {
+  if constexpr (L > 0) hipLaunchKernelGGL(k_tf_dw<L>, dim3(16, F.G), dim3(256), 0, s, F);
+  if (G->lin_w[L]) hipLaunchKernelGGL(k_tf_dw_reduce<L>, dim3(256), dim3(320), 0, s, F, G->lin_w[L]);
+  if constexpr (L > 0) hipLaunchKernelGGL(k_tf_bwd_layer<L>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+}
+
+static void fold_backward(const SampleSrc& q, const pcnerf_nof_params* params, float eps, const float* g,
+                          const float* p, void* state, size_t state_bytes, const pcnerf_nof_grads* G,
+                          hipStream_t s) {
+  PCN_CHECK(q.total > 0 && q.chunk > 0, "train fold backward: empty input");
+  const FoldLayout Lo = fold_layout(q.total, q.chunk);
+  PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train fold backward: state buffer too small");
+  NofParamsDev P;
+  PCN_CHECK(to_dev_params(params, eps, &P), "train fold backward: null parameter pointer");
+  const FoldDev F = fold_dev(Lo, state);
+  {
+    ProfScope ps(s, PT_FOLD_MOMENTS, 126.0 * (double)q.total, 8.0 * (double)q.total);
+    hipLaunchKernelGGL(k_tf_gmoments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F, g, p);
+  }
+  ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
+  hipLaunchKernelGGL(k_tf_bwd_out, dim3((unsigned)F.C), dim3(256), 0, s, P, F);
+  backward_layer<7>(P, F, G, s);
+  backward_layer<6>(P, F, G, s);
+  backward_layer<5>(P, F, G, s);
+  backward_layer<4>(P, F, G, s);
+  backward_layer<3>(P, F, G, s);
+  backward_layer<2>(P, F, G, s);
+  backward_layer<1>(P, F, G, s);
+  backward_layer<0>(P, F, G, s);
+  hipLaunchKernelGGL(k_tf_vec_reduce, dim3(10), dim3(256), 0, s, F, *G);
+}
+
+}  // namespace pcn
+
+using namespace pcn;
+
+extern "C" size_t pcnerf_nof_train_fold_bytes(int64_t total_samples, int64_t chunk) {
+  if (total_samples <= 0 || chunk <= 0) return 0;
+  return fold_layout(total_samples, std::min(chunk, total_samples)).doubles * sizeof(double);
+}
+
+extern "C" int pcnerf_nof_query_train_fold(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                           int n_samples, int64_t chunk, const pcnerf_nof_params* params,
+                                           float momentum, float eps, void* state, size_t state_bytes, float* p_out,
+                                           void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && state && p_out, "pcnerf_nof_query_train_fold: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_fold: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_fold: ray_stride < 6");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  const SampleSrc q{rays, ray_stride, z, n_samples, nullptr, total, std::min(chunk, total)};
+  fold_forward(q, params, momentum, eps, state, state_bytes, p_out, (hipStream_t)stream);
+  PCN_LAUNCH_CHECK("pcnerf_nof_query_train_fold");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_forward_train_fold(const float* emb, int64_t n, const pcnerf_nof_params* params,
+                                             float momentum, float eps, void* state, size_t state_bytes,
+                                             float* p_out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(emb && params && state && p_out, "pcnerf_nof_forward_train_fold: null argument");
+  PCN_CHECK(n > 1, "pcnerf_nof_forward_train_fold: Expected more than 1 value per channel when training");
+  const SampleSrc q{nullptr, 0, nullptr, 1, emb, n, n};
+  fold_forward(q, params, momentum, eps, state, state_bytes, p_out, (hipStream_t)stream);
+  PCN_LAUNCH_CHECK("pcnerf_nof_forward_train_fold");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_query_train_fold_backward(const float* rays, int64_t n_rays, int ray_stride,
+                                                    const float* z, int n_samples, int64_t chunk,
+                                                    const pcnerf_nof_params* params, float eps,
+                                                    const float* grad_logit, void* state, size_t state_bytes,
+                                                    const pcnerf_nof_grads* grads, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && grad_logit && state && grads,
+            "pcnerf_nof_query_train_fold_backward: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_fold_backward: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_fold_backward: ray_stride < 6");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  const SampleSrc q{rays, ray_stride, z, n_samples, nullptr, total, std::min(chunk, total)};
+  fold_backward(q, params, eps, grad_logit, nullptr, state, state_bytes, grads, (hipStream_t)stream);
+  PCN_LAUNCH_CHECK("pcnerf_nof_query_train_fold_backward");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_forward_train_fold_backward(const float* emb, int64_t n, const pcnerf_nof_params* params,
+                                                      float eps, const float* p, const float* grad_p, void* state,
+                                                      size_t state_bytes, const pcnerf_nof_grads* grads,
+                                                      void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(emb && params && p && grad_p && state && grads, "pcnerf_nof_forward_train_fold_backward: null argument");
+  PCN_CHECK(n > 1, "pcnerf_nof_forward_train_fold_backward: empty input");
+  const SampleSrc q{nullptr, 0, nullptr, 1, emb, n, n};
+  fold_backward(q, params, eps, grad_p, p, state, state_bytes, grads, (hipStream_t)stream);
+  PCN_LAUNCH_CHECK("pcnerf_nof_forward_train_fold_backward");
+  PCN_API_END
+}

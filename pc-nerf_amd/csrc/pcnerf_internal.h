@@ -23,6 +23,10 @@ struct NofParamsDev {
 
 bool to_dev_params(const pcnerf_nof_params* p, float eps, NofParamsDev* d);
 void set_error(const std::string& msg);
+// p_out[g] = sigmoid(fl32(a_c . Embedding(sample g) + c_c)), (a_c, c_c) = fold[64 c .. 64 c + 63] for the
+// BatchNorm chunk c = g / chunk (nof_eval.hip: the eval fold with chunk >= total, the train fold per chunk)
+void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
+                        const double* fold, int64_t chunk, float* p_out, hipStream_t s);
 
 // p = o + d*z, one rounding per op (render.py:458; built with -ffp-contract=off).
 __device__ __forceinline__ void sample_point(const float* __restrict__ r, float z, float (&p)[3]) {
@@ -36,9 +40,7 @@ __device__ __forceinline__ void sample_point(const float* __restrict__ r, float 
 // and only sinf/cosf rounding remains (full-range ocml sincosf, never the __sinf fast path).
 // Lane half h receives, for k-step t = 0..31, feature 2t + h (MAP 0: eval chain) or 8(t>>2) + 4h + (t&3)
 // (MAP 1: train-mode layer kernels, whose memory-resident activations use 16-byte feature groups).
-template <int MAP = 0>
-__device__ __forceinline__ void encode_half(const float (&p)[3], int h, float (&e)[32]) {
-  float f[64];
+__device__ __forceinline__ void encode_full(const float (&p)[3], float (&f)[64]) {
   f[0] = p[0];
   f[1] = p[1];
   f[2] = p[2];
@@ -54,6 +56,12 @@ __device__ __forceinline__ void encode_half(const float (&p)[3], int h, float (&
     }
   }
   f[63] = 0.0f;
+}
+
+template <int MAP = 0>
+__device__ __forceinline__ void encode_half(const float (&p)[3], int h, float (&e)[32]) {
+  float f[64];
+  encode_full(p, f);
 #pragma unroll
   for (int t = 0; t < 32; ++t) {
     if (MAP == 0) e[t] = h ? f[2 * t + 1] : f[2 * t];

@@ -21,6 +21,8 @@ enum ProfTag {
   PT_EVAL_FOLD = 13,   // k_nof_eval_fold: exact affine fold of the eval network (opt-in)
   PT_BWD_WGRAD_H = 14, // k_wgrad_b3: weight gradients under the split train math
   PT_TRAIN_H1 = 15,    // k_train_h1: layer 1 from the encoding tiles (h0 recomputed)
+  PT_FOLD_MOMENTS = 16,// train fold: k_tf_moments / k_tf_gmoments (per-sample encoding moments)
+  PT_FOLD_ALGEBRA = 17,// train fold: the per-chunk float64 layer algebra (forward or backward)
 };
 extern bool g_prof_on;
 class ProfScope {

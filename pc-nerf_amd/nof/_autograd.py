@@ -22,12 +22,16 @@ class TrainPass(torch.autograd.Function):
     def forward(ctx, model, rays, z, noise, noise_std, eps, chunk, with_losses, sub_num, *params):
         # a chunk larger than the pass is the same single BatchNorm chunk: size workspaces and store by the pass
         chunk = max(1, min(int(chunk), z.numel()))
-        # keep the chunks' layer outputs for the backward in the HBM left after its workspace (+ 4 GiB margin)
-        L = _ops.H.lib()
-        reserve = int(L.pcnerf_nof_backward_workspace_bytes(int(chunk))) + (4 << 30)
-        store = _ops.ActivationStore(z.device, z.numel(), chunk, reserve)
-        p = _ops.query(model, rays, z, chunk, store)
-        ctx.store = store
+        ctx.store = ctx.fold = None
+        if _ops.train_fold_enabled():   # opt-in exact affine fold: per-chunk moments + layer maps, no activations
+            ctx.fold = _ops.fold_state(z.device, z.numel(), chunk)
+            p = _ops.query(model, rays, z, chunk, fold=ctx.fold)
+        else:
+            # keep the chunks' layer outputs for the backward in the HBM left after its workspace (+ 4 GiB margin)
+            L = _ops.H.lib()
+            reserve = int(L.pcnerf_nof_backward_workspace_bytes(int(chunk))) + (4 << 30)
+            ctx.store = _ops.ActivationStore(z.device, z.numel(), chunk, reserve)
+            p = _ops.query(model, rays, z, chunk, ctx.store)
         w, depth, fr, sl = _ops.composite(p, z, noise, noise_std, eps, rays if with_losses else None)
         if with_losses:
             free, dl = _ops.child_losses(fr, sl, rays, sub_num > 0, sub_num)
@@ -46,15 +50,19 @@ class TrainPass(torch.autograd.Function):
             g_free = g_dl = None
         g_logit = _ops.composite_backward(p, z, noise, ctx.noise_std, ctx.eps, rays if ctx.with_losses else None,
                                           ctx.sub_num, g_depth, g_free, g_dl)
-        grads = _ops.nof_query_backward(ctx.model, rays, z, ctx.chunk, g_logit, ctx.store)
-        ctx.store.release()
+        if ctx.fold is not None:
+            grads = _ops.nof_query_backward_fold(ctx.model, rays, z, ctx.chunk, g_logit, ctx.fold)
+            ctx.fold = None
+        else:
+            grads = _ops.nof_query_backward(ctx.model, rays, z, ctx.chunk, g_logit, ctx.store)
+            ctx.store.release()
         return (None,) * 9 + tuple(grads)
 
 
 class NofForward(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, x, *params):
-        p = _ops.nof_forward_embedded(model, x)
+        p, ctx.fold = _ops.nof_forward_embedded(model, x, with_fold_state=True)
         ctx.model = model
         ctx.save_for_backward(x, p)
         return p
@@ -62,7 +70,12 @@ class NofForward(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_p):
         x, p = ctx.saved_tensors
-        grads = _ops.nof_forward_backward(ctx.model, x, p.reshape(-1), g_p.contiguous().reshape(-1))
+        if ctx.fold is not None:
+            grads = _ops.nof_forward_backward_fold(ctx.model, x, p.reshape(-1), g_p.contiguous().reshape(-1),
+                                                   ctx.fold)
+            ctx.fold = None
+        else:
+            grads = _ops.nof_forward_backward(ctx.model, x, p.reshape(-1), g_p.contiguous().reshape(-1))
         return (None, None) + tuple(grads)
 
 

@@ -138,20 +138,56 @@ if os.environ.get("PCNERF_TRAIN_MATH"):
     set_train_math(os.environ["PCNERF_TRAIN_MATH"])
 
 
+# Exact affine fold of the TRAIN-mode network (opt-in): every layer's BatchNorm batch statistics
+# follow from the chunk's encoding mean and covariance, so each chunk's network is sigmoid(a_c . emb + c_c)
+# (csrc/nof_fold.hip).  Off by default: the drop-in evaluates the module as written.
+_TRAIN_FOLD = os.environ.get("PCNERF_TRAIN_FOLD", "0") == "1"
+
+
+def set_train_fold(enabled: bool) -> bool:
+    """Route train-mode NOF queries (forward and backward) through the exact affine fold (True) or the full
+    network (False, default).  Returns the previous setting."""
+    global _TRAIN_FOLD
+    prev, _TRAIN_FOLD = _TRAIN_FOLD, bool(enabled)
+    return prev
+
+
+def train_fold_enabled() -> bool:
+    return _TRAIN_FOLD
+
+
+def fold_state(device, total_samples: int, chunk: int) -> torch.Tensor:
+    """Device buffer of the train fold's per-chunk moments and layer maps (forward -> backward)."""
+    n = int(H.lib().pcnerf_nof_train_fold_bytes(int(total_samples), int(chunk)))
+    return torch.empty((max(n, 1),), dtype=torch.uint8, device=device)
+
+
 def _track_batches(model, n_chunks: int) -> None:
     for bn in model.norms():
         if bn.num_batches_tracked is not None:
             bn.num_batches_tracked.add_(n_chunks)
 
 
-def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None) -> torch.Tensor:
+def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fold=None) -> torch.Tensor:
     """Occupancy p (R, S) of the samples o + d*z through Embedding + NOF (render.py:18-25 / 44-51).
-    ``store`` (train mode): an ActivationStore whose chunks keep the layer outputs for the backward."""
+    ``store`` (train mode): an ActivationStore whose chunks keep the layer outputs for the backward.
+    ``fold`` (train mode): a fold_state buffer -- the query runs through the train fold and keeps its state there
+    (also taken, with a temporary buffer, when set_train_fold(True))."""
     L = H.lib()
     R, S = z.shape
     p = torch.empty((R, S), dtype=torch.float32, device=z.device)
     st = _stream(z)
-    if model.training:
+    if model.training and (fold is not None or _TRAIN_FOLD):
+        chunk = max(1, min(int(chunk), R * S))
+        mom, eps = _bn_config(model)
+        s, keep = _params(model)
+        if fold is None:
+            fold = fold_state(z.device, R * S, chunk)
+        H.check(L.pcnerf_nof_query_train_fold(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                              ctypes.byref(s), mom, eps, fold.data_ptr(), fold.numel(),
+                                              p.data_ptr(), st))
+        _track_batches(model, -(-R * S // int(chunk)))
+    elif model.training:
         chunk = max(1, min(int(chunk), R * S))   # a larger chunk is the same single BatchNorm chunk
         mom, eps = _bn_config(model)
         s, keep = _params(model)
@@ -176,8 +212,9 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None) ->
     return p
 
 
-def nof_forward_embedded(model, x: torch.Tensor) -> torch.Tensor:
-    """NOF.forward on a (B, 63) embedded batch (one BatchNorm batch in train mode)."""
+def nof_forward_embedded(model, x: torch.Tensor, with_fold_state: bool = False):
+    """NOF.forward on a (B, 63) embedded batch (one BatchNorm batch in train mode).  ``with_fold_state``: return
+    (p, fold state or None) -- the state the train fold's backward needs when set_train_fold(True)."""
     L = H.lib()
     x = _f32(x)
     if x.dim() != 2 or x.shape[1] != 63:
@@ -185,7 +222,17 @@ def nof_forward_embedded(model, x: torch.Tensor) -> torch.Tensor:
     B = x.shape[0]
     out = torch.empty((B, 1), dtype=torch.float32, device=x.device)
     st = _stream(x)
-    if model.training:
+    fold = None
+    if model.training and _TRAIN_FOLD:
+        if B <= 1:
+            raise ValueError("Expected more than 1 value per channel when training")
+        mom, eps = _bn_config(model)
+        s, keep = _params(model)
+        fold = fold_state(x.device, B, B)
+        H.check(L.pcnerf_nof_forward_train_fold(x.data_ptr(), B, ctypes.byref(s), mom, eps, fold.data_ptr(),
+                                                fold.numel(), out.data_ptr(), st))
+        _track_batches(model, 1)
+    elif model.training:
         if B <= 1:
             raise ValueError("Expected more than 1 value per channel when training")
         mom, eps = _bn_config(model)
@@ -200,7 +247,7 @@ def nof_forward_embedded(model, x: torch.Tensor) -> torch.Tensor:
     else:
         packed = pack_eval(model, x.device)
         H.check(L.pcnerf_nof_forward_eval(x.data_ptr(), B, packed.data_ptr(), out.data_ptr(), st))
-    return out
+    return (out, fold) if with_fold_state else out
 
 
 def embed(x: torch.Tensor) -> torch.Tensor:
@@ -555,6 +602,32 @@ def nof_query_backward(model, rays, z, chunk: int, g_logit, store=None) -> list:
         H.check(L.pcnerf_nof_query_train_backward(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
                                                   ctypes.byref(s), eps, _f32(g_logit).data_ptr(), ws.data_ptr(),
                                                   ws.numel(), ctypes.byref(gs), _stream(z)))
+    return out
+
+
+def nof_query_backward_fold(model, rays, z, chunk: int, g_logit, fold) -> list:
+    """Parameter gradients of the train fold's query (state from query(..., fold=...)) given dL/dlogit."""
+    L = H.lib()
+    R, S = z.shape
+    _, eps = _bn_config(model)
+    s, keep = _params(model)
+    gs, out = _grads_struct(model, z.device)
+    H.check(L.pcnerf_nof_query_train_fold_backward(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                                   ctypes.byref(s), eps, _f32(g_logit).data_ptr(), fold.data_ptr(),
+                                                   fold.numel(), ctypes.byref(gs), _stream(z)))
+    return out
+
+
+def nof_forward_backward_fold(model, x, p, g_p, fold) -> list:
+    """Parameter gradients of NOF.forward(x) through the train fold given dL/dp."""
+    L = H.lib()
+    B = x.shape[0]
+    _, eps = _bn_config(model)
+    s, keep = _params(model)
+    gs, out = _grads_struct(model, x.device)
+    H.check(L.pcnerf_nof_forward_train_fold_backward(x.data_ptr(), B, ctypes.byref(s), eps, _f32(p).data_ptr(),
+                                                     _f32(g_p).data_ptr(), fold.data_ptr(), fold.numel(),
+                                                     ctypes.byref(gs), _stream(x)))
     return out
 
 
