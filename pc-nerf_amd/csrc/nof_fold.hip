@@ -16,7 +16,8 @@
 //                  a shift against cancellation), fp16 hi/mid parts on the matrix pipe per 64-sample tile (three
 //                  exact products, fp32 accumulation), float64 across tiles
 //   k_tf_stats     ebar, Sigma per chunk (float64)
-//   k_tf_layer<L>  P'_L, Q_L = P'_L Sigma, var, s, the pre-BN mean (float64 GEMMs, 64-row tiles x chunks)
+//   k_tf_layer<L>  P'_L, Q_L = P'_L Sigma, var, s, the pre-BN mean (float64 GEMMs on v_mfma_f64_16x16x4_f64,
+//                  64-row tiles x chunks)
 //   k_tf_out       (a_c, c_c);  launch_fold_logits: p = sigmoid(a_c . e + c_c) per sample
 //   k_tf_running   running_mean / running_var, chunk by chunk in order (bn_coeffs' arithmetic)
 // Backward (dL/dlogit per sample):
@@ -128,6 +129,14 @@ __device__ __forceinline__ int64_t chunk_len(const SampleSrc& q, int64_t c) {
 // fp32 accumulation over the 64-sample tile, float64 across tiles).  The tile rows are 72 halves apart, so the
 // operand reads (16 bytes: 8 samples of one feature) of 16 lanes hit 16 disjoint bank groups.
 typedef _Float16 tf_f16x8 __attribute__((ext_vector_type(8)));
+
+// orders one wave's LDS writes before its reads of the same tile (and the reads before the next tile's writes):
+// the tiles are wave-private, so no workgroup barrier is needed and the four waves run out of phase
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 constexpr int TM_P = 72;
 
 __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
@@ -152,9 +161,9 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
   for (int r = 0; r < 16; ++r) d00[r] = d01[r] = d11[r] = 0.0;
   _Float16* hi = th[wave][0];
   _Float16* mi = th[wave][1];
-  for (int64_t base = t0; base < t1; base += 4) {   // same trip count in every wave (barriers below)
-    const int64_t t = base + wave, i = t * 64 + lane;
-    const bool ok = t < t1 && i < n;
+  for (int64_t t = t0 + wave; t < t1; t += 4) {   // waves independent: wave-local LDS tiles
+    const int64_t i = t * 64 + lane;
+    const bool ok = i < n;
     auto put = [&](int f, float v) {
       const float d = ok ? v - sh0[f] : 0.0f;
       const _Float16 h = (_Float16)d;
@@ -184,7 +193,7 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
     }
     hi[63 * TM_P + lane] = ok ? (_Float16)1.0f : (_Float16)0.0f;
     mi[63 * TM_P + lane] = (_Float16)0.0f;
-    __syncthreads();
+    wave_lds_sync();
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int o = (lane & 31) * TM_P + 16 * ks + 8 * (lane >> 5);
@@ -209,9 +218,11 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
       d11[r] += (double)a11[r];
       a00[r] = a01[r] = a11[r] = 0.0f;
     }
-    __syncthreads();
+    wave_lds_sync();
   }
-  // the four waves' blocks summed in a fixed order through LDS (aliasing the tiles), then one coalesced store
+  // the four waves' blocks summed in a fixed order through LDS (aliasing the tiles, once every wave is done with
+  // its own), then one coalesced store
+  __syncthreads();
   double* red = reinterpret_cast<double*>(&th[0][0][0]);
   for (int wv = 0; wv < 4; ++wv) {
     if (wave == wv) {
@@ -236,16 +247,21 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
   for (int k = tid; k < 4096; k += 256) out[k] = red[k];
 }
 
+// grid (16, C), 256 threads (wpc > 1): the moment partials of a chunk summed in a fixed order into partial 0.
+__global__ __launch_bounds__(256) void k_tf_msum(FoldDev F) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  double* m = F.mom + (int64_t)blockIdx.y * F.wpc * 4096 + k;
+  double s = m[0];
+  for (int w = 1; w < F.wpc; ++w) s += m[(int64_t)w * 4096];
+  m[0] = s;
+}
+
 // grid C, 256 threads: n = sum d_63^2, dbar = sum d / n, Sigma = sum d d^T / n - dbar dbar^T, ebar = e0 + dbar.
 __global__ __launch_bounds__(256) void k_tf_stats(FoldDev F) {
   __shared__ double G[4096];
   const int c = blockIdx.x, tid = threadIdx.x;
   const double* m = F.mom + (int64_t)c * F.wpc * 4096;
-  for (int k = tid; k < 4096; k += 256) {
-    double s = 0.0;
-    for (int w = 0; w < F.wpc; ++w) s += m[(int64_t)w * 4096 + k];
-    G[k] = s;
-  }
+  for (int k = tid; k < 4096; k += 256) G[k] = m[k];
   __syncthreads();
   const double n = G[63 * 64 + 63];
   for (int k = tid; k < 4096; k += 256) {
@@ -260,111 +276,139 @@ __global__ __launch_bounds__(256) void k_tf_stats(FoldDev F) {
   if (tid < 64) F.eb[(int64_t)c * 64 + tid] = tid < 63 ? F.e0[(int64_t)c * 64 + tid] + G[tid * 64 + 63] / n : 0.0;
 }
 
+// ---- float64 64 x 64 tiles on v_mfma_f64_16x16x4_f64 (A[l&15][k=l>>4], B[k=l>>4][l&15], D[(l>>4)+4r][l&15]).
+// Four waves per workgroup, wave w owns the 32 x 32 quadrant (rows 32(w>>1), columns 32(w&1)) as 2 x 2 blocks.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int TP = 65;   // LDS pitch (doubles) of a 64-wide tile: odd, so 16 lanes' 8-byte reads are conflict-free
+
+// acc += A B over k in [0, 64): A(r, k) = ATR ? As[k TP + r] : As[r TP + k], B(k, c) = BTR ? Bs[c TP + k] : Bs[k TP + c]
+template <bool ATR, bool BTR>
+__device__ __forceinline__ void mfma64_quad(const double* As, const double* Bs, int R, int Cc, int lane,
+                                            f64x4 (&acc)[2][2]) {
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < 64; k0 += 4) {
+    const int k = k0 + lk;
+    double a[2], b[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const int r = R + 16 * x + li, c = Cc + 16 * x + li;
+      a[x] = ATR ? As[k * TP + r] : As[r * TP + k];
+      b[x] = BTR ? Bs[c * TP + k] : Bs[k * TP + c];
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[y], acc[x][y], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ int q_row(int R, int x, int r, int lane) { return R + 16 * x + (lane >> 4) + 4 * r; }
+__device__ __forceinline__ int q_col(int Cc, int y, int lane) { return Cc + 16 * y + (lane & 15); }
+
+// sum over the tile's 64 columns of v[x][y][r] for each of the wave's rows (16 lanes x 2 blocks x 2 waves):
+// red[2][64] in LDS receives the two column halves (the caller syncs and adds them).
+__device__ __forceinline__ void row_sum_to_lds(double (&v)[2][4], int R, int wave, int lane, double* red) {
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double t = v[x][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+      if ((lane & 15) == 0) red[(wave & 1) * 64 + q_row(R, x, r, lane)] = t;
+    }
+}
+
 // grid (4, C), 256 threads: rows R0..R0+63 of P'_L = W_L B for chunk c, where B's rows are [unit_k | ebar_k] for
-// the encoding inputs and [s_{L-1,k} P'_{L-1}[k] | beta_{L-1,k}] for the previous layer's features; then
-// Q = P' Sigma, var_i = Q_i . p'_i, s = gamma / sqrt(var + eps), mean(h_L) = P'[:, 63] + b_L.
-// Thread (ty, tx) owns rows 16 i + ty and columns 16 j + tx of the tile.
+// the encoding inputs and [s_{L-1,k} P'_{L-1}[k] | beta_{L-1,k}] for the previous layer's features (64-deep k
+// slices staged in LDS); then Q = P' Sigma (P' and Sigma staged), var_i = Q_i . p'_i, s = gamma / sqrt(var + eps),
+// mean(h_L) = P'[:, 63] + b_L.
 template <int L>
 __global__ __launch_bounds__(256) void k_tf_layer(NofParamsDev P, FoldDev F, double eps) {
   constexpr int IN = L == 0 ? 63 : L == 4 ? 319 : 256;
   constexpr int KE = (L == 0 || L == 4) ? 63 : 0;
-  __shared__ double As[64][33];
-  __shared__ double Bs[32][64];
-  __shared__ double Ps[64][65];
-  __shared__ double Sg[64][64];
+  __shared__ double As[64 * TP];
+  __shared__ double Bs[64 * TP];
+  __shared__ double red[128];
   const int64_t C = F.C;
-  const int c = blockIdx.y, R0 = blockIdx.x * 64, tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const int c = blockIdx.y, R0 = blockIdx.x * 64, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int R = 32 * (wave >> 1), Cc = 32 * (wave & 1);
   const float* __restrict__ W = P.lin_w[L];
   const double* eb = F.eb + (int64_t)c * 64;
   const double* pprev = F.pp + ((int64_t)(L > 0 ? L - 1 : 0) * C + c) * 256 * 64;
   const double* sprev = F.sr + ((int64_t)(L > 0 ? L - 1 : 0) * C + c) * 1024;
   const float* bprev = P.bn_b[L > 0 ? L - 1 : 0];
-  double acc[4][4];
+  f64x4 acc[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
-  for (int k0 = 0; k0 < IN; k0 += 32) {
-    for (int e = tid; e < 2048; e += 256) {
-      const int r = e >> 5, kk = e & 31, k = k0 + kk;
-      As[r][kk] = k < IN ? (double)W[(int64_t)(R0 + r) * IN + k] : 0.0;
-    }
-    for (int e = tid; e < 2048; e += 256) {
-      const int kk = e >> 6, col = e & 63, k = k0 + kk;
+    for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < IN; k0 += 64) {
+    for (int e = tid; e < 4096; e += 256) {
+      const int r = e >> 6, kk = e & 63, k = k0 + kk;
+      As[r * TP + kk] = k < IN ? (double)W[(int64_t)(R0 + r) * IN + k] : 0.0;
+      const int col = kk, kr = k0 + r;   // B row kr, column col
       double v = 0.0;
-      if (k < KE) {
-        v = col < 63 ? (k == col ? 1.0 : 0.0) : eb[k];
-      } else if (k < IN) {
-        const int kh = k - KE;
+      if (kr < KE) {
+        v = col < 63 ? (kr == col ? 1.0 : 0.0) : eb[kr];
+      } else if (kr < IN) {
+        const int kh = kr - KE;
         v = col < 63 ? sprev[kh] * pprev[kh * 64 + col] : (double)bprev[kh];
       }
-      Bs[kk][col] = v;
+      Bs[r * TP + col] = v;
     }
     __syncthreads();
-#pragma unroll 4
-    for (int kk = 0; kk < 32; ++kk) {
-      double a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[16 * i + ty][kk];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][16 * j + tx];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
-    }
+    mfma64_quad<false, false>(As, Bs, R, Cc, lane, acc);
     __syncthreads();
   }
   const int64_t base = (((int64_t)L * C + c) * 256 + R0) * 64;
   double* pp = F.pp + base;
   double* qo = F.q + base;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pp[(16 * i + ty) * 64 + 16 * j + tx] = acc[i][j];
-      Ps[16 * i + ty][16 * j + tx] = acc[i][j];
-    }
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = q_row(R, x, r, lane), col = q_col(Cc, y, lane);
+        pp[row * 64 + col] = acc[x][y][r];
+        As[row * TP + col] = acc[x][y][r];
+      }
   const double* sg = F.sig + (int64_t)c * 4096;
-  for (int e = tid; e < 4096; e += 256) Sg[e >> 6][e & 63] = sg[e];
+  for (int e = tid; e < 4096; e += 256) Bs[(e >> 6) * TP + (e & 63)] = sg[e];
   __syncthreads();
-  double qv[4][4];
+  f64x4 qa[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) qv[i][j] = 0.0;
-#pragma unroll 3
-  for (int k = 0; k < 63; ++k) {
-    double a[4], b[4];
+    for (int y = 0; y < 2; ++y) qa[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+  mfma64_quad<false, false>(As, Bs, R, Cc, lane, qa);
+  double v[2][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = Ps[16 * i + ty][k];
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = Sg[k][16 * j + tx];
+    for (int r = 0; r < 4; ++r) {
+      v[x][r] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) qv[i][j] += a[i] * b[j];
-  }
-  double* sr = F.sr + ((int64_t)L * C + c) * 1024;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    double v = 0.0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      qo[(16 * i + ty) * 64 + 16 * j + tx] = qv[i][j];
-      if (16 * j + tx < 63) v += qv[i][j] * acc[i][j];
+      for (int y = 0; y < 2; ++y) {
+        const int row = q_row(R, x, r, lane), col = q_col(Cc, y, lane);
+        qo[row * 64 + col] = qa[x][y][r];
+        v[x][r] += qa[x][y][r] * acc[x][y][r];   // column 63: Sigma's row 63 is zero, so Q[:, 63] = 0
+      }
     }
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-    if (tx == 0) {
-      const int row = R0 + 16 * i + ty;
-      if (v < 0.0) v = 0.0;
-      const double rinv = 1.0 / sqrt(v + eps);
-      sr[row] = (double)P.bn_w[L][row] * rinv;
-      sr[256 + row] = rinv;
-      sr[512 + row] = Ps[16 * i + ty][63] + (double)P.lin_b[L][row];
-      sr[768 + row] = v;
-    }
+  row_sum_to_lds(v, R, wave, lane, red);
+  __syncthreads();
+  if (tid < 64) {
+    const int row = R0 + tid;
+    double var = red[tid] + red[64 + tid];
+    if (var < 0.0) var = 0.0;
+    const double rinv = 1.0 / sqrt(var + eps);
+    double* sr = F.sr + ((int64_t)L * C + c) * 1024;
+    sr[row] = (double)P.bn_w[L][row] * rinv;
+    sr[256 + row] = rinv;
+    sr[512 + row] = As[tid * TP + 63] + (double)P.lin_b[L][row];
+    sr[768 + row] = var;
   }
 }
 
@@ -398,13 +442,23 @@ __global__ void k_tf_running(NofParamsDev P, FoldDev F, SampleSrc q, double mom)
   const int L = blockIdx.x, k = threadIdx.x;
   if (!P.bn_rm[L]) return;
   float rm = P.bn_rm[L][k], rv = P.bn_rv[L][k];
-  for (int64_t c = 0; c < F.C; ++c) {
-    const double* sr = F.sr + ((int64_t)L * F.C + c) * 1024;
-    const int64_t n = chunk_len(q, c);
-    const double mean = sr[512 + k], var = sr[768 + k];
-    rm = (float)(mom * mean + (1.0 - mom) * (double)rm);
-    const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
-    rv = (float)(mom * unb + (1.0 - mom) * (double)rv);
+  for (int64_t c0 = 0; c0 < F.C; c0 += 8) {   // eight chunks' statistics loaded before the sequential updates
+    double mean[8], var[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t c = c0 + j < F.C ? c0 + j : F.C - 1;
+      const double* sr = F.sr + ((int64_t)L * F.C + c) * 1024;
+      mean[j] = sr[512 + k];
+      var[j] = sr[768 + k];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (c0 + j >= F.C) break;
+      const int64_t n = chunk_len(q, c0 + j);
+      rm = (float)(mom * mean[j] + (1.0 - mom) * (double)rm);
+      const double unb = n > 1 ? var[j] * (double)n / (double)(n - 1) : var[j];
+      rv = (float)(mom * unb + (1.0 - mom) * (double)rv);
+    }
   }
   P.bn_rm[L][k] = rm;
   P.bn_rv[L][k] = rv;
@@ -435,9 +489,9 @@ __global__ __launch_bounds__(256) void k_tf_gmoments(SampleSrc q, FoldDev F, con
   const int64_t t0 = std::min(ntile, (int64_t)w * per), t1 = std::min(ntile, t0 + per);
   float* my = tile[wave];
   double acc = 0.0;
-  for (int64_t base = t0; base < t1; base += 4) {   // same trip count in every wave (barriers below)
-    const int64_t t = base + wave, i = t * 64 + lane;
-    const bool ok = t < t1 && i < n;
+  for (int64_t t = t0 + wave; t < t1; t += 4) {   // waves independent: wave-local LDS tiles
+    const int64_t i = t * 64 + lane;
+    const bool ok = i < n;
     auto put = [&](int f, float v) { my[lane * 65 + f] = ok ? v - sh0[f] : 0.0f; };
     if (q.ein) {
       const float* r = q.ein + (c0 + (ok ? i : 0)) * 63;
@@ -462,10 +516,10 @@ __global__ __launch_bounds__(256) void k_tf_gmoments(SampleSrc q, FoldDev F, con
     }
     my[lane * 65 + 63] = ok ? 1.0f : 0.0f;
     gs[wave][lane] = ok ? fold_logit_grad(g, p, c0 + i) : 0.0f;
-    __syncthreads();
+    wave_lds_sync();
 #pragma unroll 16
     for (int s = 0; s < 64; ++s) acc += (double)gs[wave][s] * (double)my[s * 65 + lane];
-    __syncthreads();
+    wave_lds_sync();
   }
   red[wave][lane] = acc;
   __syncthreads();
@@ -473,13 +527,13 @@ __global__ __launch_bounds__(256) void k_tf_gmoments(SampleSrc q, FoldDev F, con
     F.gm[((int64_t)c * F.wpc + w) * 64 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
 
-// grid C, 256 threads: abar = sum g (d - dbar), gbar = sum g; occ_out / beta_7 gradient partials; the adjoint of
-// P_7 is w_i abar_j, taken through BatchNorm 7 to A'_7 (ab[1]).
+// grid (4, C), 256 threads (rows I0..I0+63 of layer 7): abar = sum g (d - dbar), gbar = sum g; occ_out / beta_7
+// gradient partials; the adjoint of P_7 is w_i abar_j, taken through BatchNorm 7 to A'_7 (ab[1]).
 __global__ __launch_bounds__(256) void k_tf_bwd_out(NofParamsDev P, FoldDev F) {
   __shared__ double ab[64];
-  __shared__ double dot[256], coef[256], dvv[256];
+  __shared__ double dot[64], coef[64], dvv[64];
   __shared__ double gbar_s;
-  const int c = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int c = blockIdx.y, I0 = blockIdx.x * 64, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t C = F.C;
   if (wave == 0) {
     double G = 0.0;
@@ -491,140 +545,138 @@ __global__ __launch_bounds__(256) void k_tf_bwd_out(NofParamsDev P, FoldDev F) {
   __syncthreads();
   const double* pp7 = F.pp + (7 * C + c) * 256 * 64;
   const double* q7 = F.q + (7 * C + c) * 256 * 64;
-  for (int r = wave; r < 256; r += 4) {
-    const double d = wave_sum_d(ab[lane] * pp7[r * 64 + lane]);
+  for (int r = wave; r < 64; r += 4) {
+    const double d = wave_sum_d(ab[lane] * pp7[(I0 + r) * 64 + lane]);
     if (lane == 0) dot[r] = d;
   }
   __syncthreads();
   const double* sr7 = F.sr + (7 * C + c) * 1024;
-  {
-    const int i = tid;
+  if (tid < 64) {
+    const int i = I0 + tid;
     const double gb = gbar_s, s7 = sr7[i], rinv = sr7[256 + i], gam = (double)P.bn_w[7][i];
     const double w = (double)P.out_w[i], beta = (double)P.bn_b[7][i];
     double* v = F.vec + (int64_t)c * 576;
-    v[i] = s7 * dot[i] + beta * gb;
+    v[i] = s7 * dot[tid] + beta * gb;
     v[256 + i] = w * gb;
     if (i == 0) v[512] = gb;
-    const double ds = w * dot[i];
+    const double ds = w * dot[tid];
     F.dg[(7 * C + c) * 256 + i] = ds * rinv;
-    dvv[i] = -0.5 * ds * gam * rinv * rinv * rinv;
-    coef[i] = s7 * w;
+    dvv[tid] = -0.5 * ds * gam * rinv * rinv * rinv;
+    coef[tid] = s7 * w;
   }
   __syncthreads();
   double* out = F.ab + (1 * C + c) * 256 * 64;
-  for (int r = wave; r < 256; r += 4)
-    out[r * 64 + lane] = lane < 63 ? coef[r] * ab[lane] + 2.0 * dvv[r] * q7[r * 64 + lane] : 0.0;
+  for (int r = wave; r < 64; r += 4)
+    out[(I0 + r) * 64 + lane] = lane < 63 ? coef[r] * ab[lane] + 2.0 * dvv[r] * q7[(I0 + r) * 64 + lane] : 0.0;
 }
 
-// grid (4, C), 256 threads: A_{L-1}[k][j] = sum_i W_L[i][OFF + k] A'_L[i][j] for rows k0..k0+63, then BatchNorm
-// L-1's backward to A'_{L-1} (ab[(L-1)&1]) and dgamma_{L-1} per chunk.
+// grid (4, C), 256 threads: A_{L-1}[k][j] = sum_i W_L[i][OFF + k] A'_L[i][j] for rows k0..k0+63 (W staged as
+// [i][k], read transposed), then BatchNorm L-1's backward to A'_{L-1} (ab[(L-1)&1]) and dgamma_{L-1} per chunk.
 template <int L>
 __global__ __launch_bounds__(256) void k_tf_bwd_layer(NofParamsDev P, FoldDev F) {
   constexpr int IN = L == 4 ? 319 : 256, OFF = L == 4 ? 63 : 0;
-  __shared__ double As[64][33];
-  __shared__ double Bs[32][64];
+  constexpr int LP = L - 1;
+  __shared__ double As[64 * TP];
+  __shared__ double Bs[64 * TP];
+  __shared__ double red[128];
   const int64_t C = F.C;
-  const int c = blockIdx.y, K0 = blockIdx.x * 64, tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const int c = blockIdx.y, K0 = blockIdx.x * 64, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int R = 32 * (wave >> 1), Cc = 32 * (wave & 1);
   const float* __restrict__ W = P.lin_w[L];
   const double* abin = F.ab + ((int64_t)(L & 1) * C + c) * 256 * 64;
-  double acc[4][4];
+  f64x4 acc[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
-  for (int i0 = 0; i0 < 256; i0 += 32) {
-    for (int e = tid; e < 2048; e += 256) {
+    for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int i0 = 0; i0 < 256; i0 += 64) {
+    for (int e = tid; e < 4096; e += 256) {
       const int ii = e >> 6, kk = e & 63;
-      As[kk][ii] = (double)W[(int64_t)(i0 + ii) * IN + OFF + K0 + kk];
-    }
-    for (int e = tid; e < 2048; e += 256) {
-      const int ii = e >> 6, j = e & 63;
-      Bs[ii][j] = abin[(i0 + ii) * 64 + j];
+      As[ii * TP + kk] = (double)W[(int64_t)(i0 + ii) * IN + OFF + K0 + kk];
+      Bs[ii * TP + kk] = abin[(i0 + ii) * 64 + kk];
     }
     __syncthreads();
-#pragma unroll 4
-    for (int ii = 0; ii < 32; ++ii) {
-      double a[4], b[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) a[x] = As[16 * x + ty][ii];
-#pragma unroll
-      for (int y = 0; y < 4; ++y) b[y] = Bs[ii][16 * y + tx];
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * b[y];
-    }
+    mfma64_quad<true, false>(As, Bs, R, Cc, lane, acc);
     __syncthreads();
   }
-  constexpr int LP = L - 1;
   const double* ppp = F.pp + ((int64_t)LP * C + c) * 256 * 64;
   const double* qq = F.q + ((int64_t)LP * C + c) * 256 * 64;
   const double* srp = F.sr + ((int64_t)LP * C + c) * 1024;
+  double v[2][4];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[x][r] = 0.0;
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        const int k = K0 + q_row(R, x, r, lane), col = q_col(Cc, y, lane);
+        if (col < 63) v[x][r] += acc[x][y][r] * ppp[k * 64 + col];
+      }
+    }
+  row_sum_to_lds(v, R, wave, lane, red);
+  __syncthreads();
+  if (tid < 64) {
+    const int k = K0 + tid;
+    const double ds = red[tid] + red[64 + tid];
+    F.dg[((int64_t)LP * C + c) * 256 + k] = ds * srp[256 + k];
+    red[tid] = ds;   // this thread's own slot: no other thread reads it before the barrier
+  }
+  __syncthreads();
   double* out = F.ab + ((int64_t)(LP & 1) * C + c) * 256 * 64;
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    const int k = K0 + 16 * x + ty;
-    double ds = 0.0;
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
-      if (16 * y + tx < 63) ds += acc[x][y] * ppp[k * 64 + 16 * y + tx];
+    for (int r = 0; r < 4; ++r) {
+      const int kl = q_row(R, x, r, lane), k = K0 + kl;
+      const double s = srp[k], rinv = srp[256 + k], gam = (double)P.bn_w[LP][k];
+      const double dv = -0.5 * red[kl] * gam * rinv * rinv * rinv;
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) ds += __shfl_xor(ds, o, 64);
-    const double s = srp[k], rinv = srp[256 + k], gam = (double)P.bn_w[LP][k];
-    if (tx == 0) F.dg[((int64_t)LP * C + c) * 256 + k] = ds * rinv;
-    const double dv = -0.5 * ds * gam * rinv * rinv * rinv;
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const int col = 16 * y + tx;
-      out[k * 64 + col] = col < 63 ? s * acc[x][y] + 2.0 * dv * qq[k * 64 + col] : 0.0;
+      for (int y = 0; y < 2; ++y) {
+        const int col = q_col(Cc, y, lane);
+        out[k * 64 + col] = col < 63 ? s * acc[x][y][r] + 2.0 * dv * qq[k * 64 + col] : 0.0;
+      }
     }
-  }
 }
 
 // grid (16, G), 256 threads: partial g of dW_L's h columns, sum over the group's chunks of
-// A'_L[i][j] * s_{L-1,k} P'_{L-1}[k][j] (j < 63), one 64 x 64 tile (rows I0, columns K0) per workgroup.
+// A'_L[i][j] * s_{L-1,k} P'_{L-1}[k][j] (j < 63), one 64 x 64 tile (rows I0, columns K0) per workgroup
+// (both operands staged in their natural [row][j] layout, B read transposed).
 template <int L>
 __global__ __launch_bounds__(256) void k_tf_dw(FoldDev F) {
-  __shared__ double As[64][65];
-  __shared__ double Bs[64][65];
+  __shared__ double As[64 * TP];
+  __shared__ double Bs[64 * TP];
   const int64_t C = F.C;
   const int I0 = (blockIdx.x >> 2) * 64, K0 = (blockIdx.x & 3) * 64, g = blockIdx.y;
-  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int R = 32 * (wave >> 1), Cc = 32 * (wave & 1);
   const int64_t cg0 = C * g / F.G, cg1 = C * (g + 1) / F.G;
-  double acc[4][4];
+  f64x4 acc[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+    for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
   for (int64_t c = cg0; c < cg1; ++c) {
     const double* abin = F.ab + ((int64_t)(L & 1) * C + c) * 256 * 64;
     const double* pp = F.pp + ((int64_t)(L - 1) * C + c) * 256 * 64;
     const double* s = F.sr + ((int64_t)(L - 1) * C + c) * 1024;
     for (int e = tid; e < 4096; e += 256) {
       const int r = e >> 6, j = e & 63;
-      As[r][j] = abin[(I0 + r) * 64 + j];
-      Bs[j][r] = j < 63 ? s[K0 + r] * pp[(K0 + r) * 64 + j] : 0.0;
+      As[r * TP + j] = abin[(I0 + r) * 64 + j];
+      Bs[r * TP + j] = j < 63 ? s[K0 + r] * pp[(K0 + r) * 64 + j] : 0.0;
     }
     __syncthreads();
-#pragma unroll 3
-    for (int j = 0; j < 63; ++j) {
-      double a[4], b[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) a[x] = As[16 * x + ty][j];
-#pragma unroll
-      for (int y = 0; y < 4; ++y) b[y] = Bs[j][16 * y + tx];
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * b[y];
-    }
+    mfma64_quad<false, true>(As, Bs, R, Cc, lane, acc);
     __syncthreads();
   }
   double* out = F.dw + (int64_t)g * 65536;
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y) out[(I0 + 16 * x + ty) * 256 + K0 + 16 * y + tx] = acc[x][y];
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[(I0 + q_row(R, x, r, lane)) * 256 + K0 + q_col(Cc, y, lane)] = acc[x][y][r];
 }
 
 // grid 256 (rows i), 320 threads (columns): dW_L[i][col] += encoding columns: sum_c A'_L[i][col]; h columns: the
@@ -692,6 +744,7 @@ static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, fl
   }
   {
     ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
+    if (F.wpc > 1) hipLaunchKernelGGL(k_tf_msum, dim3(16, (unsigned)F.C), dim3(256), 0, s, F);
     hipLaunchKernelGGL(k_tf_stats, dim3((unsigned)F.C), dim3(256), 0, s, F);
     launch_layer<0>(P, F, ep, s);
     launch_layer<1>(P, F, ep, s);
@@ -731,7 +784,7 @@ static void fold_backward(const SampleSrc& q, const pcnerf_nof_params* params, f
     hipLaunchKernelGGL(k_tf_gmoments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F, g, p);
   }
   ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
-  hipLaunchKernelGGL(k_tf_bwd_out, dim3((unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_out, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
   backward_layer<7>(P, F, G, s);
   backward_layer<6>(P, F, G, s);
   backward_layer<5>(P, F, G, s);
