@@ -470,7 +470,10 @@ def kernel_report(L, a, train_math):
         roof = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": kbytes / max(klaunch, 1),
-                "note": "VALU-bound (60 sincosf per sample); HBM fraction reported as the contract asks"}
+                "note": ("VALU-bound (the encoding's 30 sincosf per sample, recomputed by the moment, query and "
+                         "gradient-moment passes; the per-chunk layer algebra is float64 MFMA); HBM fraction "
+                         "reported as the contract asks") if a.mode in ("train_fwd", "train_step") else
+                        "VALU-bound (60 sincosf per sample); HBM fraction reported as the contract asks"}
     elif split and tag in (1, 2, 3, 11, 14, 15):
         # split-fp16 layer: nterm fp16 MFMA products per fp32 product; 1 KiB in + 1 KiB out per sample: the
         # HBM stream (2 KiB/sample) is the tighter of its two roofs
