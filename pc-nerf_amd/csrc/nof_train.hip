@@ -83,6 +83,12 @@ namespace pcn {
 #ifndef PCN_H_DMA
 #define PCN_H_DMA 0  // hidden layers: k_train_hd (raw tiles by LDS-DMA two tiles ahead)
 #endif
+#ifndef PCN_REV_OWN
+#define PCN_REV_OWN 0   // reversed layers walk each workgroup's own tiles backwards (else the chunk's)
+#endif
+#ifndef PCN_GRAM
+#define PCN_GRAM 1    // with PCN_H1: layer 0 as the encoding's moments (k_enc_gram) instead of its 256-neuron product
+#endif
 #ifndef PCN_H_AHEAD
 #define PCN_H_AHEAD 1  // raw activation loads 1 or 2 tiles ahead
 #endif
@@ -624,7 +630,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   // tile order: odd layers walk the chunk backwards, so a layer first reads the tiles its predecessor wrote last
   // (still in the memory-side cache) -- P maps the loop's tile to the tile of the chunk
   const bool rev = !KE && ((layer >> 8) & 1);   // (the first and skip layers keep the forward walk: registers)
-  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
+  // PCN_REV_OWN: a reversed layer walks its OWN workgroup's tiles backwards (the tiles blockIdx mod gridDim that
+  // the same workgroup index -- the same XCD -- wrote in the previous layer, its last-written first: XCD L2 hits)
+  const int lastb = (int)blockIdx.x + ((nt - 1 - (int)blockIdx.x) / gstride) * gstride;
+  auto P = [&](int x) { return rev ? (PCN_REV_OWN ? lastb + (int)blockIdx.x - x : nt - 1 - x) : x; };
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
   // staging identity: the HBM lane (sample ls + 32 hs) whose float4s this thread stages; PCN_H_LMAP interleaves
   // the halves across neighbouring lanes so each 16-lane group's 8-byte LDS writes cover 128 contiguous bytes
@@ -971,7 +980,8 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
   const bool rev = (layer >> 8) & 1;
-  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
+  const int lastb = (int)blockIdx.x + ((nt - 1 - (int)blockIdx.x) / gstride) * gstride;   // as k_train_h
+  auto P = [&](int x) { return rev ? (PCN_REV_OWN ? lastb + (int)blockIdx.x - x : nt - 1 - x) : x; };
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
   const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
   if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);
@@ -1116,6 +1126,261 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
       a += (double)sred[(wb * 64 + ln) * 8 + ((2 * jj + mo) ^ ((ln >> 1) & 7))][qq];
     }
     atomicAdd(&stats[t], a);
+  }
+}
+
+// ---- layer 0 from the encoding's moments (split forward without activation store, k_train_h1 after it).
+// Layer 0's only remaining outputs there are the chunk's encoding tiles and BatchNorm 0's statistics, and those
+// statistics are exact functions of the chunk's encoding mean ebar and covariance Sigma (models.py:183-203 with
+// identity activations): sum_s (W0 e_s)_i = n w_i.ebar, sum_s (W0 e_s)_i^2 = n (w_i^T Sigma w_i + (w_i.ebar)^2).
+//   k_enc_gram    each sample's encoding once (encode_full: 30 sincosf, not 64 as the per-float4 form of the first
+//                 layer), stored as the chunk's encoding tiles ([tile][g][lane][4]; padded lanes carry the last
+//                 sample, as k_train_h's), and sum d d^T with d = [e - e0, 1] (e0 = the chunk's first encoding, a
+//                 shift against cancellation) in k_tf_moments' form: fp16 hi/mid parts in a wave-private
+//                 [feature][sample] LDS tile, three exact products per pair on v_mfma_f32_32x32x16_f16, fp32 per
+//                 64-sample unit, float64 across units, one partial per workgroup (blocks 00, 01, 11 of 64 x 64);
+//   k_gram_sum    the partials summed in a fixed order;
+//   k_gram_stats  ebar, Sigma and the 256 neurons' sums in float64 -> BatchNorm 0's statistics (bn_coeffs' input).
+// The 256-neuron product of the first layer (99 us per chunk of 262,144, VALU-bound) becomes a 64 x 64 one.
+constexpr int GR_P = 72;          // LDS pitch (halves): 16 lanes' 16-byte operand reads hit disjoint bank groups
+#ifndef PCN_GR_BLOCKS
+#define PCN_GR_BLOCKS 512
+#endif
+#ifndef PCN_GR_ABL
+#define PCN_GR_ABL 0      // timing-only ablations of k_enc_gram: 1 no encoding-tile stores, 2 no moment products
+#endif
+constexpr int GR_BLOCKS = PCN_GR_BLOCKS;    // k_enc_gram workgroups per chunk (two per CU)
+constexpr int GR_PART = 3072;     // doubles per partial: blocks 00, 01, 11 as [block][register 16][lane 64]
+constexpr size_t GR_DOUBLES = (size_t)(GR_BLOCKS + 1) * GR_PART + 64;
+
+// feature f of Embedding(3, 10) at p: encode_full's value, one sincosf per feature (wave-parallel shift vector)
+__device__ __forceinline__ float enc_feat1(const float (&p)[3], int f) {
+  const int fk = f < 3 ? 0 : (f - 3) / 6, fr = f < 3 ? 0 : (f - 3) - 6 * fk;
+  const int m = fr < 3 ? fr : fr - 3;
+  const float pm = m == 0 ? p[0] : m == 1 ? p[1] : p[2];
+  float sn, cs;
+  sincosf(__int_as_float((127 + fk) << 23) * pm, &sn, &cs);
+  const float pf = f == 0 ? p[0] : f == 1 ? p[1] : p[2];
+  return f < 3 ? pf : f >= 63 ? 0.0f : fr < 3 ? sn : cs;
+}
+
+__device__ __forceinline__ void gram_lds_sync() {   // wave-private tiles: order one wave's LDS writes and reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256, 2) void k_enc_gram(const float* __restrict__ rays, int stride,
+                                                     const float* __restrict__ z, int S, int64_t c0,
+                                                     const float* __restrict__ ein, int64_t n,
+                                                     f32x4* __restrict__ etout, double* __restrict__ part,
+                                                     double* __restrict__ e0out) {
+  __shared__ __attribute__((aligned(16))) _Float16 th[4][2][64 * GR_P];
+  __shared__ float sh0[64];
+  static_assert(sizeof(th) >= GR_PART * sizeof(double), "reduction area");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < 64) {   // e0 = the encoding of the chunk's first sample, one feature per lane
+    float v;
+    if (ein) {
+      v = tid < 63 ? ein[c0 * 63 + tid] : 0.0f;
+    } else {
+      float p[3];
+      sample_point(rays + (c0 / S) * stride, z[c0], p);
+      v = enc_feat1(p, tid);
+    }
+    sh0[tid] = v;
+    if (blockIdx.x == 0) e0out[tid] = (double)v;
+  }
+  __syncthreads();
+  const int64_t nu = (n + 63) / 64, ntiles = (n + 31) / 32;
+  f32x16 a00 = {}, a01 = {}, a11 = {};
+  double d00[16], d01[16], d11[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) d00[r] = d01[r] = d11[r] = 0.0;
+  _Float16* const hi = th[wave][0];
+  _Float16* const mi = th[wave][1];
+  for (int64_t u = (int64_t)blockIdx.x * 4 + wave; u < nu; u += (int64_t)gridDim.x * 4) {
+    const int64_t s = u * 64 + lane;
+    const bool ok = s < n;
+    const int64_t se = ok ? s : n - 1;   // padded lanes: the last sample (k_train_h's sample_of)
+    float f[64];
+    if (ein) {
+      const float* r = ein + (c0 + se) * 63;
+#pragma unroll
+      for (int k = 0; k < 63; ++k) f[k] = r[k];
+      f[63] = 0.0f;
+    } else {
+      float p[3];
+      sample_point(rays + ((c0 + se) / S) * stride, z[c0 + se], p);
+      encode_full(p, f);
+    }
+    const int64_t tile = s >> 5;
+    if (!(PCN_GR_ABL & 1) && tile < ntiles) {   // [tile][g][lane (s & 31) + 32 h][4]: features 8 g + 4 h + q
+      f32x4* dst = etout + (size_t)tile * 512 + (lane & 31);
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          dst[g * 64 + 32 * h] = f32x4{f[8 * g + 4 * h], f[8 * g + 4 * h + 1], f[8 * g + 4 * h + 2], f[8 * g + 4 * h + 3]};
+    }
+#pragma unroll
+    for (int k = 0; k < 63; ++k) {
+      const float d = ok ? f[k] - sh0[k] : 0.0f;
+      const _Float16 a = (_Float16)d;
+      hi[k * GR_P + lane] = a;
+      mi[k * GR_P + lane] = (_Float16)(d - (float)a);
+    }
+    hi[63 * GR_P + lane] = ok ? (_Float16)1.0f : (_Float16)0.0f;
+    mi[63 * GR_P + lane] = (_Float16)0.0f;
+    gram_lds_sync();
+#pragma unroll
+    for (int ks = 0; ks < ((PCN_GR_ABL & 2) ? 0 : 4); ++ks) {
+      const int o = (lane & 31) * GR_P + 16 * ks + 8 * (lane >> 5);
+      const f16x8 h0 = *reinterpret_cast<const f16x8*>(hi + o);
+      const f16x8 m0 = *reinterpret_cast<const f16x8*>(mi + o);
+      const f16x8 h1 = *reinterpret_cast<const f16x8*>(hi + 32 * GR_P + o);
+      const f16x8 m1 = *reinterpret_cast<const f16x8*>(mi + 32 * GR_P + o);
+      a00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h0, h0, a00, 0, 0, 0);
+      a01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h0, h1, a01, 0, 0, 0);
+      a11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h1, h1, a11, 0, 0, 0);
+      a00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h0, m0, a00, 0, 0, 0);
+      a01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h0, m1, a01, 0, 0, 0);
+      a11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(h1, m1, a11, 0, 0, 0);
+      a00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m0, h0, a00, 0, 0, 0);
+      a01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m0, h1, a01, 0, 0, 0);
+      a11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m1, h1, a11, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      d00[r] += (double)a00[r];
+      d01[r] += (double)a01[r];
+      d11[r] += (double)a11[r];
+      a00[r] = a01[r] = a11[r] = 0.0f;
+    }
+    gram_lds_sync();
+  }
+  // the four waves' partials summed in a fixed order through LDS (aliasing the tiles), one coalesced store
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(&th[0][0][0]);
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int x = r * 64 + lane;
+        red[x] = wv ? red[x] + d00[r] : d00[r];
+        red[1024 + x] = wv ? red[1024 + x] + d01[r] : d01[r];
+        red[2048 + x] = wv ? red[2048 + x] + d11[r] : d11[r];
+      }
+    }
+    __syncthreads();
+  }
+  double* out = part + (size_t)blockIdx.x * GR_PART;
+  for (int k = tid; k < GR_PART; k += 256) out[k] = red[k];
+}
+
+// grid GR_PART / 16, 512 threads: block x0 owns moments x0 .. x0 + 15; thread (q = tid >> 4, x) sums partials
+// q, q + 32, .. (all its loads in flight at once: the partials were written by every XCD, so each load is a trip
+// to the memory side), then the 32 q-sums are added in order -> mom[x]
+__global__ __launch_bounds__(512) void k_gram_sum(const double* __restrict__ part, int nb, double* __restrict__ mom) {
+  __shared__ double red[32][16];
+  const int xl = threadIdx.x & 15, q = threadIdx.x >> 4, x = blockIdx.x * 16 + xl;
+  double s = 0.0;
+  int b = q;
+  for (; b + 32 * 15 < nb; b += 32 * 16) {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = part[(size_t)(b + 32 * k) * GR_PART + x];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += v[k];
+  }
+  for (; b < nb; b += 32) s += part[(size_t)b * GR_PART + x];
+  red[q][xl] = s;
+  __syncthreads();
+  if (q == 0) {
+    double t = red[0][xl];
+#pragma unroll
+    for (int k = 1; k < 32; ++k) t += red[k][xl];
+    mom[x] = t;
+  }
+}
+
+// grid 32, 256 threads: block b -> neurons 8 b .. 8 b + 7.  M = sum d d^T, n = M[63][63], dbar = M[k][63] / n,
+// Sigma = M / n - dbar dbar^T, ebar = e0 + dbar; neuron i (32 threads, rows k = slice, slice + 32 of Sigma w_i):
+// stats[2i] = n w_i.ebar, stats[2i+1] = n (w_i^T Sigma w_i + (w_i.ebar)^2)   (sums of h - b0, as k_train_h's)
+constexpr int GS_BLOCKS = 32;
+__global__ __launch_bounds__(256) void k_gram_stats(const double* __restrict__ mom, const double* __restrict__ e0,
+                                                    const float* __restrict__ w0, double* __restrict__ stats) {
+  __shared__ double M[64 * 65];
+  __shared__ double Sg[63 * 65];
+  __shared__ double eb[64], db[64];
+  __shared__ float ws[8 * 64];
+  const int tid = threadIdx.x;
+  double mv[GR_PART / 256];   // every load in flight at once
+#pragma unroll
+  for (int j = 0; j < GR_PART / 256; ++j) mv[j] = mom[tid + 256 * j];
+  float wv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int x = tid + 256 * j, i = x >> 6, k = x & 63;
+    wv[j] = k < 63 ? w0[(size_t)(8 * blockIdx.x + i) * 63 + k] : 0.0f;
+  }
+  const double e0v = tid < 63 ? e0[tid] : 0.0;
+#pragma unroll
+  for (int jx = 0; jx < GR_PART / 256; ++jx) {   // blocks 00, 01, 11 -> M (both triangles)
+    const int x = tid + 256 * jx;
+    const int b = x >> 10, r = (x >> 6) & 15, ln = x & 63;
+    const int i = (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5) + (b == 2 ? 32 : 0), j = (ln & 31) + (b ? 32 : 0);
+    M[i * 65 + j] = mv[jx];
+    M[j * 65 + i] = mv[jx];
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) ws[tid + 256 * j] = wv[j];
+  // the chunk's other BatchNorm statistics start from zero (layers 1-7 add to them): the memset of the other path
+  if (tid < 7 * 512 / GS_BLOCKS) stats[512 + (int)blockIdx.x * (7 * 512 / GS_BLOCKS) + tid] = 0.0;
+  __syncthreads();
+  const double n = M[63 * 65 + 63], inv_n = 1.0 / n;
+  if (tid < 64) {
+    db[tid] = tid < 63 ? M[tid * 65 + 63] * inv_n : 0.0;
+    eb[tid] = tid < 63 ? e0v + M[tid * 65 + 63] * inv_n : 0.0;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < (63 * 63 + 255) / 256; ++j) {   // Sigma
+    const int x = tid + 256 * j;
+    if (x < 63 * 63) {
+      const int k = x / 63, l = x - 63 * k;
+      Sg[k * 65 + l] = M[k * 65 + l] * inv_n - db[k] * db[l];
+    }
+  }
+  __syncthreads();
+  const int i = tid >> 5, sl = tid & 31;
+  const float* w = ws + i * 64;
+  double v = 0.0, mu = 0.0;
+#pragma unroll 1
+  for (int k = sl; k < 63; k += 32) {
+    double r[63];   // the row's loads issued together
+#pragma unroll
+    for (int l = 0; l < 63; ++l) r[l] = Sg[k * 65 + l];
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int l = 0; l < 63; l += 3) {
+      t0 += r[l] * (double)w[l];
+      t1 += r[l + 1] * (double)w[l + 1];
+      t2 += r[l + 2] * (double)w[l + 2];
+    }
+    const double wk = (double)w[k];
+    v += wk * ((t0 + t1) + t2);
+    mu += wk * eb[k];
+  }
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    v += __shfl_xor(v, o, 64);
+    mu += __shfl_xor(mu, o, 64);
+  }
+  if (sl == 0) {
+    const int nn = 8 * blockIdx.x + i;
+    stats[2 * nn] = n * mu;
+    stats[2 * nn + 1] = n * (v + mu * mu);
   }
 }
 
@@ -1341,6 +1606,7 @@ struct TrainWs {
   f16x8* wh;    // split-fp16 weight image (train math 1/2)
   int* sw;      // its per-layer scale exponents
   double* stats;
+  double* gram;  // k_enc_gram partials, their slice sums and the chunk's shift e0
   size_t bytes;
 };
 
@@ -1361,6 +1627,7 @@ static TrainWs carve(void* base, int64_t chunk) {
   const size_t oE = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
+  const size_t ogr = take(GR_DOUBLES * sizeof(double));
   char* b = (char*)base;
   TrainWs w;
   w.bufA = (float*)(b + oA);
@@ -1370,6 +1637,7 @@ static TrainWs carve(void* base, int64_t chunk) {
   w.wh = (f16x8*)(b + owh);
   w.sw = (int*)(b + osw);
   w.stats = (double*)(b + ost);
+  w.gram = (double*)(b + ogr);
   w.bytes = off;
   return w;
 }
@@ -1527,7 +1795,6 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     const bool keep = store && ci < store_chunks;
     const StoreChunk sc = keep ? store_chunk(store, chunk, ci) : StoreChunk{};
     double* stats = keep ? sc.stats : ws.stats;
-    PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));
     float* hin = keep ? sc.h[0] : ws.bufA;
     float* hout = keep ? sc.h[1] : ws.bufB;
     // the encoding tiles the skip layer reads back: written by THIS chunk's first-layer launch just below
@@ -1535,7 +1802,20 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     // split math, nothing kept for a backward: layer 0 statistics-only, layer 1 recomputes h0 from the encoding
     // tiles (k_train_h1)
     const bool h1 = PCN_H1 && !keep && g_train_math != 0;
-    {
+    if (!(h1 && PCN_GRAM)) PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));   // (else k_gram_stats)
+    if (h1 && PCN_GRAM) {
+      // algorithmic: the 64 x 64 moment product per sample; 4 B of z in, 256 B of encoding out
+      ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 64 * 64 * dn, (4.0 + 256.0) * dn);
+      const int64_t nu = (n + 63) / 64;
+      const int gb = (int)std::min<int64_t>(GR_BLOCKS, (nu + 3) / 4);
+      double* mom = ws.gram + (size_t)GR_BLOCKS * GR_PART;
+      double* e0 = mom + GR_PART;
+      hipLaunchKernelGGL(k_enc_gram, dim3((unsigned)gb), dim3(256), 0, s, rays, ray_stride, z, n_samples, c0, ein, n,
+                         ws.enc, ws.gram, e0);
+      hipLaunchKernelGGL(k_gram_sum, dim3(GR_PART / 16), dim3(512), 0, s, ws.gram, gb, mom);
+      hipLaunchKernelGGL(k_gram_stats, dim3(GS_BLOCKS), dim3(256), 0, s, mom, e0, P.lin_w[0], stats);
+      enc_of_chunk = ws.enc;
+    } else {
       const BnPrev none{};
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 63 * 256 * dn, (4.0 + (h1 ? 256.0 : 1024.0 + 256.0)) * dn);
       const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};
