@@ -86,6 +86,15 @@ namespace pcn {
 #ifndef PCN_REV_OWN
 #define PCN_REV_OWN 0   // reversed layers walk each workgroup's own tiles backwards (else the chunk's)
 #endif
+#ifndef PCN_INPLACE
+#define PCN_INPLACE 1   // split forward without store: layers overwrite their input buffer (one activation buffer)
+#endif
+#ifndef PCN_XFOLD
+#define PCN_XFOLD 1     // the staging's 2^sx folded into the BatchNorm coefficients (bit-identical)
+#endif
+#ifndef PCN_H_NT
+#define PCN_H_NT 0      // split layers: 1 nontemporal activation loads, 2 nontemporal output stores
+#endif
 #ifndef PCN_GRAM
 #define PCN_GRAM 1    // with PCN_H1: layer 0 as the encoding's moments (k_enc_gram) instead of its 256-neuron product
 #endif
@@ -622,8 +631,13 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
     if (KE && sx > 0) sx = 0;
     sx = sx > 24 ? 24 : sx;
+    if (PCN_XFOLD && t < 256) {   // 2^sx into the BatchNorm coefficients (exact: a power of two)
+      al[t] = ldexpf(al[t], sx);
+      be[t] = ldexpf(be[t], sx);
+    }
   }
   const float xscale = ldexpf(1.0f, sx);
+  const float xs_stage = PCN_XFOLD ? 1.0f : xscale;   // what staging still multiplies by
   const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
@@ -677,7 +691,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * hs);
     f32x4 x;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = (v[m][q] * a[q] + c[q]) * xscale;
+    for (int q = 0; q < 4; ++q) x[q] = PCN_XFOLD ? v[m][q] * a[q] + c[q] : (v[m][q] * a[q] + c[q]) * xs_stage;
     put(b, KE + g, x);
   };
   auto put_enc = [&](int b, const f32x4& e) {   // encoding group t >> 6 (not scaled: sx <= 0 -> x 2^sx only if < 1)
@@ -691,8 +705,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   // the raw activation float4s of a tile this thread stages ([g][HBM lane][4], g = (t >> 6) + 8 m)
   auto load_tile = [&](f32x4 (&v)[4], int tile) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-      v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)P(tile) * TILE_FLOATS)[(t & ~63) + sln + 512 * m];
+    for (int m = 0; m < 4; ++m) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(hin + (size_t)P(tile) * TILE_FLOATS) + (t & ~63) + sln + 512 * m;
+      v[m] = (PCN_H_NT & 1) ? __builtin_nontemporal_load(src) : *src;
+    }
   };
   const int etix = (t & ~63) + sln;   // this thread's encoding float4 in a stored tile [g][HBM lane]
   auto sample_of = [&](int tile) {
@@ -767,7 +783,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       rs[2 * j + 1][q] += dv * dv;
     }
     float* base = hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
-    if (!(PCN_H_ABL & 1)) reinterpret_cast<f32x4*>(base)[lane] = o;
+    if (!(PCN_H_ABL & 1)) {
+      if (PCN_H_NT & 2) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(base) + lane);
+      else reinterpret_cast<f32x4*>(base)[lane] = o;
+    }
   };
   auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile, f32x4 (&vstage)[4], f32x4 (&vload)[4],
                   bool sync) {
@@ -973,6 +992,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
     for (int i = 1; i < 8; ++i) m = fmaxf(m, smax[i]);
     sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
     sx = sx > 24 ? 24 : sx;
+    if (PCN_XFOLD && t < 256) {   // 2^sx into BatchNorm 0's coefficients (exact), as k_train_h
+      al[t] = ldexpf(al[t], sx);
+      be[t] = ldexpf(be[t], sx);
+    }
   }
   const float xscale = ldexpf(1.0f, sx);
   const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
@@ -1039,7 +1062,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float hv = acc[4 * j + q] * unscale0 + bj[q];   // k_train_h's epilogue: o = d + b
-        x[q] = (hv * a[q] + c[q]) * xscale;                   // its staging: (v alpha + beta') 2^sx
+        x[q] = PCN_XFOLD ? hv * a[q] + c[q] : (hv * a[q] + c[q]) * xscale;   // its staging: (v alpha + beta') 2^sx
       }
       putb(xs[b], 4 * blk + j, x);
     }
@@ -1103,7 +1126,9 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
           rs[2 * j][q] += dv;
           rs[2 * j + 1][q] += dv * dv;
         }
-        reinterpret_cast<f32x4*>(hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256)[lane] = o;
+        f32x4* dst = reinterpret_cast<f32x4*>(hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256) + lane;
+        if (PCN_H_NT & 2) __builtin_nontemporal_store(o, dst);
+        else *dst = o;
       }
     }
     if (more) h0_stage(acc, buf ^ 1, buf ^ 1, o0);   // tile + 1's encoding sits in the other slot
@@ -1803,6 +1828,9 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     // tiles (k_train_h1)
     const bool h1 = PCN_H1 && !keep && g_train_math != 0;
     if (!(h1 && PCN_GRAM)) PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));   // (else k_gram_stats)
+    // PCN_INPLACE: every layer of the chunk overwrites its input tile by tile (a tile is read only by the workgroup
+    // that writes its output, which staged it before its MFMAs): one 268 MB footprint instead of two
+    if (h1 && PCN_INPLACE) hout = hin;
     if (h1 && PCN_GRAM) {
       // algorithmic: the 64 x 64 moment product per sample; 4 B of z in, 256 B of encoding out
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 64 * 64 * dn, (4.0 + 256.0) * dn);
