@@ -465,7 +465,7 @@ def kernel_report(L, a, train_math):
     achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
     gbs = kbytes / max(klaunch, 1) / avg_s / 1e9
     traffic, traffic_src = pmc_traffic(kname)
-    nprod = 6 if tag == 14 else nterm   # k_wgrad_b3: six bf16 products per fp32 product
+    nprod = nterm   # k_wgrad_b3 too: f16x2 parts, nterm products (the six-product bf16x3 form is a build option)
     if a.fold:   # no MLP left: the query moves 8 B per sample (+ ray rows) and is bound by its sincos (VALU)
         roof = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -95,6 +95,15 @@ namespace pcn {
 #ifndef PCN_H_NT
 #define PCN_H_NT 0      // split layers: 1 nontemporal activation loads, 2 nontemporal output stores
 #endif
+#ifndef PCN_H1I
+#define PCN_H1I 0       // k_train_h1: the next tile's W0 products inside the W1 k-loop (second accumulator set)
+#endif
+#ifndef PCN_H1I_AT
+#define PCN_H1I_AT 1    // ... at W1 k-steps AT .. AT + 3
+#endif
+#ifndef PCN_H1I_EPI
+#define PCN_H1I_EPI 8   // ... its BatchNorm + split at W1 k-steps EPI .. EPI + 3
+#endif
 #ifndef PCN_GRAM
 #define PCN_GRAM 1    // with PCN_H1: layer 0 as the encoding's moments (k_enc_gram) instead of its 256-neuron product
 #endif
@@ -964,6 +973,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
                                                      double* __restrict__ stats) {
   constexpr int KS = KS_H, XD = PCN_H_XD;
   constexpr int S_ELOAD = 2, S_EPUT = KS - 4;
+  constexpr int H1I_AT = PCN_H1I_AT, H1I_EPI = PCN_H1I_EPI;   // PCN_H1I: W0 k-steps / h0 epilogue parts of tile + 1
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
@@ -1039,6 +1049,26 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
     o[2] = eb[slot][ks][0][lane];
     o[3] = eb[slot][ks][1][lane];
   };
+  // one W0 k-step of h0 (ops: its operands)
+  auto h0_mfma = [&](f32x16& acc, const f16x8 (&o)[4], int ks) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[0], o[2], ks == 0 ? f32x16{} : acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[0], o[3], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[1], o[2], acc, 0, 0, 0);
+    if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[1], o[3], acc, 0, 0, 0);
+  };
+  // h0 part j (accumulator registers 4j..4j+3) + b0, BatchNorm 0, split into B buffer b at group 4 blk + j
+  auto h0_epi = [&](const f32x16& acc, int b, int j) {
+    const int f0 = 32 * blk + 8 * j + 4 * h;
+    const f32x4 bj = *reinterpret_cast<const f32x4*>(b0s + f0);
+    const f32x4 a = *reinterpret_cast<const f32x4*>(al + f0), c = *reinterpret_cast<const f32x4*>(be + f0);
+    f32x4 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float hv = acc[4 * j + q] * unscale0 + bj[q];   // k_train_h's epilogue: o = d + b
+      x[q] = PCN_XFOLD ? hv * a[q] + c[q] : (hv * a[q] + c[q]) * xscale;   // its staging: (v alpha + beta') 2^sx
+    }
+    putb(xs[b], 4 * blk + j, x);
+  };
   // (ops0: k-step 0's operands, read ahead by the caller)
   auto h0_stage = [&](f32x16& acc, int slot, int b, const f16x8 (&ops0)[4]) {
     f16x8 op[2][4];
@@ -1047,25 +1077,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
 #pragma unroll
     for (int ks = 0; ks < KS_E; ++ks) {
       if (ks + 1 < KS_E) h0_ops(op[(ks + 1) & 1], slot, ks + 1);
-      const f16x8 *o = op[ks & 1];
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[0], o[2], ks == 0 ? f32x16{} : acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[0], o[3], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[1], o[2], acc, 0, 0, 0);
-      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[1], o[3], acc, 0, 0, 0);
+      h0_mfma(acc, op[ks & 1], ks);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int f0 = 32 * blk + 8 * j + 4 * h;
-      const f32x4 bj = *reinterpret_cast<const f32x4*>(b0s + f0);
-      const f32x4 a = *reinterpret_cast<const f32x4*>(al + f0), c = *reinterpret_cast<const f32x4*>(be + f0);
-      f32x4 x;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float hv = acc[4 * j + q] * unscale0 + bj[q];   // k_train_h's epilogue: o = d + b
-        x[q] = PCN_XFOLD ? hv * a[q] + c[q] : (hv * a[q] + c[q]) * xscale;   // its staging: (v alpha + beta') 2^sx
-      }
-      putb(xs[b], 4 * blk + j, x);
-    }
+    for (int j = 0; j < 4; ++j) h0_epi(acc, b, j);
   };
   int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
   f32x16 acc;
@@ -1090,6 +1105,9 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
     f16x8 xr[XD][2];
     f32x4 ev;
     f16x8 o0[4];   // W0 k-step 0 operands of tile + 1, read during the last W1 k-step
+    f32x16 acc0;   // PCN_H1I: h0 of tile + 1, its W0 products inside this tile's W1 k-loop
+    f16x8 q0[4];   // ... the operands of its next W0 k-step
+    if (PCN_H1I && more) h0_ops(q0, buf ^ 1, 0);
 #pragma unroll
     for (int d = 0; d < XD - 1; ++d) {
       xr[d][0] = xs[buf][d][0][lane];
@@ -1106,9 +1124,14 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
       if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
+      if (PCN_H1I && more && ks >= H1I_AT && ks < H1I_AT + KS_E) {
+        h0_mfma(acc0, q0, ks - H1I_AT);
+        if (ks - H1I_AT + 1 < KS_E) h0_ops(q0, buf ^ 1, ks - H1I_AT + 1);
+      }
+      if (PCN_H1I && more && ks >= H1I_EPI && ks < H1I_EPI + 4) h0_epi(acc0, buf ^ 1, ks - H1I_EPI);
       if (ks == S_ELOAD && more2) ev = load_enc(nxt2);
       if (ks == S_EPUT && more2) put_enc(buf, ev);   // slot of tile + 2 = this tile's slot (read one tile ago)
-      if (ks == KS - 1) h0_ops(o0, buf ^ 1, 0);
+      if (!PCN_H1I && ks == KS - 1) h0_ops(o0, buf ^ 1, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     {   // epilogue of this tile (as k_train_h's REGSTAT epilogue)
@@ -1131,7 +1154,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
         else *dst = o;
       }
     }
-    if (more) h0_stage(acc, buf ^ 1, buf ^ 1, o0);   // tile + 1's encoding sits in the other slot
+    if (!PCN_H1I && more) h0_stage(acc, buf ^ 1, buf ^ 1, o0);   // tile + 1's encoding sits in the other slot
     __syncthreads();
     buf ^= 1;
     tl = nxt;
@@ -1156,8 +1179,9 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
 
 // ---- layer 0 from the encoding's moments (split forward without activation store, k_train_h1 after it).
 // Layer 0's only remaining outputs there are the chunk's encoding tiles and BatchNorm 0's statistics, and those
-// statistics are exact functions of the chunk's encoding mean ebar and covariance Sigma (models.py:183-203 with
-// identity activations): sum_s (W0 e_s)_i = n w_i.ebar, sum_s (W0 e_s)_i^2 = n (w_i^T Sigma w_i + (w_i.ebar)^2).
+// statistics are exact functions of the chunk's encoding mean ebar and covariance Sigma (h0 = W0 e + b0 feeds
+// BatchNorm 0 directly, models.py:183-203, whatever the activations further on):
+// sum_s (W0 e_s)_i = n w_i.ebar, sum_s (W0 e_s)_i^2 = n (w_i^T Sigma w_i + (w_i.ebar)^2).
 //   k_enc_gram    each sample's encoding once (encode_full: 30 sincosf, not 64 as the per-float4 form of the first
 //                 layer), stored as the chunk's encoding tiles ([tile][g][lane][4]; padded lanes carry the last
 //                 sample, as k_train_h's), and sum d d^T with d = [e - e0, 1] (e0 = the chunk's first encoding, a

@@ -21,4 +21,6 @@ run config4 --config 4 --steps 2 --warmup 1 &&
 run config5 --config 5 --steps 2 --warmup 1 &&
 run val_fold --mode val --fold --steps 5 --warmup 2 &&
 run view_fold --mode view --fold --steps 5 --warmup 2 &&
-run train_step_refcfg --mode train_step --rays 256 --samples 768 --importance 1536 --steps 10 --warmup 2 --cpu-rays 32
+run train_step_refcfg --mode train_step --rays 256 --samples 768 --importance 1536 --steps 10 --warmup 2 --cpu-rays 32 &&
+run train_fwd_fold --fold --steps 10 --warmup 2 &&
+run train_step_fold --mode train_step --fold --steps 5 --warmup 1
