@@ -98,6 +98,9 @@ namespace pcn {
 #ifndef PCN_H1I
 #define PCN_H1I 0       // k_train_h1: the next tile's W0 products inside the W1 k-loop (second accumulator set)
 #endif
+#ifndef PCN_H1_XD
+#define PCN_H1_XD PCN_H_XD   // k_train_h1's B-operand read ring depth
+#endif
 #ifndef PCN_H1I_AT
 #define PCN_H1I_AT 1    // ... at W1 k-steps AT .. AT + 3
 #endif
@@ -971,7 +974,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
                                                      const float* __restrict__ bias, BnPrev prev, float momentum,
                                                      float eps, float* __restrict__ hout,
                                                      double* __restrict__ stats) {
-  constexpr int KS = KS_H, XD = PCN_H_XD;
+  constexpr int KS = KS_H, XD = PCN_H1_XD;
   constexpr int S_ELOAD = 2, S_EPUT = KS - 4;
   constexpr int H1I_AT = PCN_H1I_AT, H1I_EPI = PCN_H1I_EPI;   // PCN_H1I: W0 k-steps / h0 epilogue parts of tile + 1
   __shared__ __attribute__((aligned(16))) float al[256];
