@@ -341,10 +341,11 @@ def main(argv=None):
         return max_over_ranks(el, device=dev), lv
 
     train_math = (("fold" if a.fold else _ops.get_train_math()) if train else None)
+    eval_math = None if (train or a.fold) else _ops.get_eval_math()
     elapsed, loss_val = timed(a.steps, a.warmup)
-    roof, kernels = kernel_report(L, a, train_math)
+    roof, kernels = kernel_report(L, a, train_math, eval_math)
 
-    # the same workload with the train-mode layers on the fp32 MFMA pipe (train_math "fp32"), for comparison
+    # the same workload with the MLP on the fp32 MFMA pipe (train / eval math "fp32"), for comparison
     fp32_line = None
     if train and train_math != "fp32" and not a.no_fp32_line and not a.fold:
         _ops.set_train_math("fp32")
@@ -354,6 +355,15 @@ def main(argv=None):
         fp32_line = {"value": None, "ms_per_step": round(1e3 * el32 / a.steps, 3), "roofline": roof32,
                      "kernels": {k: v for k, v in k32.items() if k.startswith("train")},
                      "note": "the same timed steps with the train-mode Linear layers as fp32 MFMA (v_mfma_f32_32x32x2_f32)"}
+        fp32_elapsed = el32
+    if eval_math not in (None, "fp32") and not a.no_fp32_line:
+        _ops.set_eval_math("fp32")
+        el32, _ = timed(a.steps, 1)
+        roof32, k32 = kernel_report(L, a, None, "fp32")
+        _ops.set_eval_math(eval_math)
+        fp32_line = {"value": None, "ms_per_step": round(1e3 * el32 / a.steps, 3), "roofline": roof32,
+                     "kernels": {k: v for k, v in k32.items() if k.startswith("eval")},
+                     "note": "the same timed steps with the fused eval network as fp32 MFMA (k_nof_eval, v_mfma_f32_32x32x2_f32)"}
         fp32_elapsed = el32
 
     cpu = cdref = None
@@ -418,6 +428,7 @@ def main(argv=None):
                    "parallelism": (f"dp{world}" if a.config == 3 else f"blocks{world}"), "gather": bool(a.gather)},
         "roofline": roof,
         "train_math": train_math,
+        "eval_math": eval_math,
         "fp32_mfma": fp32_line,
         "cpu_baseline": cpu,
         "cd_vs_ref": cdref,
@@ -433,12 +444,13 @@ def main(argv=None):
 FP16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense BF16/FP16 MFMA
 
 
-def kernel_report(L, a, train_math):
+def kernel_report(L, a, train_math, eval_math=None):
     """Kernel breakdown of the last timed step (library HIP events) and the dominant kernel's roofline."""
     split = train_math in ("f16x2_3", "f16x2_4")
-    nterm = 3 if train_math == "f16x2_3" else 4
+    esplit = eval_math == "f16x2_3"
+    nterm = 3 if (train_math == "f16x2_3" or esplit) else 4
     hid = f"k_train_h<0,true,{nterm}>" if split else "k_train_ws<0,true>"
-    knames = {0: "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
+    knames = {0: "k_nof_eval_h" if esplit else "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
               3: f"k_train_h<8,true,{nterm}>" if split else "k_train_ws<8,true>",
               10: "k_wgrad<2>+k_wgrad<1>" if split else "k_wgrad<0>", 11: f"k_dgrad_h<{nterm}>" if split else "k_dgrad_ws",
               13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>",
@@ -474,6 +486,12 @@ def kernel_report(L, a, train_math):
                          "gradient-moment passes; the per-chunk layer algebra is float64 MFMA); HBM fraction "
                          "reported as the contract asks") if a.mode in ("train_fwd", "train_step") else
                         "VALU-bound (60 sincosf per sample); HBM fraction reported as the contract asks"}
+    elif esplit and tag == 0:
+        # split-fp16 eval network: nterm fp16 MFMA products per fp32 product, weights streamed through LDS
+        roof = {"kernel": kname, "bound": "mfma", "achieved": round(nprod * achieved, 1), "peak": FP16_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(nprod * achieved / FP16_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1),
+                "products_per_fp32_product": nprod, "fp32_equivalent_TFLOPs": round(achieved, 2)}
     elif split and tag in (1, 2, 3, 11, 14, 15):
         # split-fp16 layer: nterm fp16 MFMA products per fp32 product; 1 KiB in + 1 KiB out per sample: the
         # HBM stream (2 KiB/sample) is the tighter of its two roofs

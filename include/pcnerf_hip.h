@@ -46,9 +46,17 @@ typedef struct pcnerf_nof_params {
 } pcnerf_nof_params;
 
 /* Eval-mode network image: BatchNorm (running stats) folded into each Linear, weights repacked into the
- * MFMA operand order of the fused query kernel.  Replaces the per-call nn.Module forward in eval mode. */
+ * MFMA operand order of the fused query kernels -- the fp32 image followed by the split-fp16 image (per-layer
+ * power-of-two scales, hi/mid fp16 parts).  Replaces the per-call nn.Module forward in eval mode. */
 size_t pcnerf_nof_eval_packed_floats(void);
 int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* packed, void* stream);
+
+/* Arithmetic of the fused eval-mode query (pcnerf_nof_query_eval / pcnerf_nof_forward_eval), process-wide;
+ * returns the previous mode, or -1 for an invalid one.  0: fp32 MFMA (v_mfma_f32_32x32x2_f32).  1 (default): each
+ * fp32 operand as two fp16 parts (22 significant bits; weights scaled per layer, activations per sample by powers
+ * of two) and hi*hi + hi*mid + mid*hi on v_mfma_f32_32x32x16_f16 (exact products, fp32 accumulation), as
+ * pcnerf_set_train_math mode 1. */
+int pcnerf_set_eval_math(int mode);
 
 /* Fused eval-mode query: for every flattened sample g = ray*n_samples + s computes
  *   p_out[g] = NOF(Embedding(o + d*z[g]))        (render.py:18-25 chunk loop, models.py:27-41, :183-203)

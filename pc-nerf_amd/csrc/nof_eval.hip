@@ -34,7 +34,16 @@ __host__ __device__ constexpr size_t off_w(int layer, bool epart) {
 constexpr size_t OFF_BIAS = 2 * SZ_E + 7 * SZ_H;
 constexpr size_t OFF_WOUT = OFF_BIAS + 8 * 256;
 constexpr size_t OFF_BOUT = OFF_WOUT + 256;
-constexpr size_t EVAL_FLOATS = OFF_BOUT + 4;
+constexpr size_t EVAL_F32_FLOATS = OFF_BOUT + 4;   // the fp32 image (k_nof_eval)
+// split-fp16 image (k_nof_eval_h), appended: [sw: 8 int32 exponents, 16-float aligned][120 k-steps][ob 8][part 2]
+// [lane 64] f16x8 -- the eval network's 120 k-steps of 16 features (layer 0: 4, layers 1-3, 5-7: 16, layer 4: 4 + 16)
+constexpr int EH_KSTEPS = 120;
+constexpr size_t EH_VECS = (size_t)EH_KSTEPS * 8 * 2 * 64;
+constexpr size_t OFF_EH_SW = EVAL_F32_FLOATS;
+constexpr size_t OFF_EH = OFF_EH_SW + 16;
+constexpr size_t EVAL_FLOATS = OFF_EH + EH_VECS * 4;
+static_assert(EVAL_F32_FLOATS % 4 == 0, "f16x8 alignment of the split image");
+__host__ __device__ constexpr int eh_start(int L) { return L == 0 ? 0 : L <= 4 ? 4 + 16 * (L - 1) : 8 + 16 * (L - 1); }
 
 __device__ __forceinline__ int feat_h(int t, int h) {  // accumulator register -> neuron
   return 32 * (t >> 4) + (t & 3) + 8 * ((t & 15) >> 2) + 4 * h;
@@ -174,6 +183,258 @@ __global__ __launch_bounds__(256) void k_nof_eval(const float* __restrict__ rays
   }
   const float logit = part + __shfl_xor(part, 32, 64) + W[OFF_BOUT];
   if (lane < 32 && g < total) p_out[g] = sigmoid_ref(logit);
+}
+
+// ---------------------------------------------------------------------------------- split-fp16 eval query
+// k_nof_eval's fused network with every fp32 product rebuilt from fp16 parts on v_mfma_f32_32x32x16_f16 (the
+// split train math, DESIGN "The split train math"): v = hi + mid (22 significant bits), W x = Wh xh + Wh xm + Wm xh,
+// exact products, fp32 accumulation.  Scales are powers of two undone in each layer's epilogue: per layer for the
+// BatchNorm-folded weights (max |W'| 2^sw in [2^14, 2^15)), per SAMPLE for the activations (max over the sample's
+// features, so a sample's result never depends on the other samples of its tile).
+// One wave owns 32 samples (as k_nof_eval); a block of 4 waves (one per SIMD: 128 accumulator + 128 activation
+// registers per lane) shares the weight stream: each k-step's 16 KiB slice (8 out-blocks x hi/mid) is loaded two
+// k-steps ahead by all 256 threads and published in one of two LDS slots, one barrier per k-step.
+// Operand maps: A (lane l) = W'[32 ob + (l&31)][col(s, l>>5, j)], B (lane l) = x[col(s, l>>5, j)][sample l&31],
+// j = 0..7, with col(s, h, j) = 2 (8 s + j) + h for the encoding (encode_half's e[8 s + j]) and
+// 16 s + 8 (j>>2) + 4 h + (j&3) for the 256 hidden features -- exactly accumulator registers 8 (s&1) + j of
+// block s>>1 of the previous layer, so each layer's B operands are its predecessor's accumulators split in place.
+
+// per-layer weight scale exponents of the BatchNorm-folded weights, stored in the image as int32
+__global__ __launch_bounds__(256) void k_eval_wscale(NofParamsDev P, float* __restrict__ out) {
+  const int L = blockIdx.x;
+  const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < 256 * in_f; i += 256) {
+    const int n = i / in_f;
+    const float alpha = (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
+    m = fmaxf(m, fabsf(alpha * P.lin_w[L][i]));
+  }
+  m = wave_max_f(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    reinterpret_cast<int*>(out + OFF_EH_SW)[L] = m > 0.0f && m == m && m < 3.0e38f ? 14 - ilogbf(m) : 0;
+  }
+}
+
+typedef _Float16 eh_f16x8 __attribute__((ext_vector_type(8)));
+
+__global__ void k_pack_eval_h(NofParamsDev P, float* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= EH_VECS) return;
+  const int lane = (int)(idx & 63), part = (int)((idx >> 6) & 1), ob = (int)((idx >> 7) & 7);
+  const int gk = (int)(idx >> 10);
+  int L = 0;
+  while (L < 7 && gk >= eh_start(L + 1)) ++L;
+  const int s0 = gk - eh_start(L);
+  const bool epart = L == 0 || (L == 4 && s0 < 4);
+  const int s = L == 4 && !epart ? s0 - 4 : s0;
+  const int n = 32 * ob + (lane & 31), h = lane >> 5;
+  const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
+  const float alpha = (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
+  const float sc = ldexpf(1.0f, reinterpret_cast<const int*>(out + OFF_EH_SW)[L]);
+  eh_f16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int col;
+    if (epart) {
+      const int f = 2 * (8 * s + j) + h;
+      col = f < 63 ? f : -1;
+    } else {
+      col = (L == 4 ? 63 : 0) + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+    }
+    const float w = col < 0 ? 0.0f : (alpha * P.lin_w[L][(size_t)n * in_f + col]) * sc;
+    const _Float16 hi = (_Float16)w;
+    v[j] = part == 0 ? hi : (_Float16)(w - (float)hi);
+  }
+  reinterpret_cast<eh_f16x8*>(out + OFF_EH)[idx] = v;
+}
+
+// the per-sample scale exponent for a max |x| (0 for zero / non-finite maxima), clamped so that every unscale
+// factor stays a normal float
+__device__ __forceinline__ int eh_scale(float m) {
+  int e = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
+  return e > 64 ? 64 : e < -64 ? -64 : e;
+}
+
+// 8 values -> hi / mid fp16 parts
+__device__ __forceinline__ void eh_split8(const float (&v)[8], eh_f16x8& hi, eh_f16x8& mid) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 a = (_Float16)v[j];
+    hi[j] = a;
+    mid[j] = (_Float16)(v[j] - (float)a);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__ rays, int stride,
+                                                       const float* __restrict__ z, int64_t total, int S,
+                                                       const float* __restrict__ ein, const float* __restrict__ W,
+                                                       float* __restrict__ p_out) {
+  __shared__ eh_f16x8 wsl[2][8 * 2 * 64];   // two k-step slices of the weight stream
+  __shared__ __attribute__((aligned(16))) float sbias[8 * 256];
+  const int t = threadIdx.x, lane = t & 63, h = lane >> 5;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (t >> 6);
+  const int64_t g = tile * 32 + (lane & 31);
+  const int64_t gc = g < total ? g : total - 1;
+  const eh_f16x8* __restrict__ img = reinterpret_cast<const eh_f16x8*>(W + OFF_EH);
+  int sw[8];
+#pragma unroll
+  for (int L = 0; L < 8; ++L) sw[L] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(W + OFF_EH_SW)[L]);
+  // weight stream: thread t moves vectors t + 256 m of each 1,024-vector slice
+  eh_f16x8 ldA[4], ldB[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) wsl[0][t + 256 * m] = img[t + 256 * m];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) ldA[m] = img[1024 + t + 256 * m];
+  for (int i = t; i < 8 * 256 / 4; i += 256)
+    reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
+  float e[32];
+  if (ein) {
+    load_embedding<0>(ein + gc * 63, h, e);
+  } else {
+    const float* r = rays + (gc / S) * stride;
+    float p[3];
+    sample_point(r, z[gc], p);
+    encode_half(p, h, e);
+  }
+  __syncthreads();
+  int gk = 0;
+  f32x16 acc[8];
+  // one k-step of the current layer: B operands (xh, xm), A operands from the slice in LDS; the loader issues the
+  // slice two k-steps ahead and publishes the next one
+  auto kstep = [&](const eh_f16x8& xh, const eh_f16x8& xm, bool first) {
+    if (gk + 2 < EH_KSTEPS) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) ldB[m] = img[(size_t)(gk + 2) * 1024 + t + 256 * m];
+    }
+    const eh_f16x8* sl = wsl[gk & 1];
+    eh_f16x8 a0 = sl[lane], a1 = sl[64 + lane];
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {
+      eh_f16x8 n0, n1;
+      if (ob + 1 < 8) {
+        n0 = sl[((ob + 1) * 2) * 64 + lane];
+        n1 = sl[((ob + 1) * 2 + 1) * 64 + lane];
+      }
+      acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, xh, first ? f32x16{} : acc[ob], 0, 0, 0);
+      acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, xm, acc[ob], 0, 0, 0);
+      acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, xh, acc[ob], 0, 0, 0);
+      if (ob + 1 < 8) {
+        a0 = n0;
+        a1 = n1;
+      }
+    }
+    if (gk + 1 < EH_KSTEPS) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) wsl[(gk + 1) & 1][t + 256 * m] = ldA[m];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 4; ++m) ldA[m] = ldB[m];
+    ++gk;
+  };
+  // the encoding's B operands at per-sample scale 2^sx
+  eh_f16x8 eh[4], em[4];
+  auto split_e = [&](int sx) {
+    const float xs = ldexpf(1.0f, sx);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = e[8 * s + j] * xs;
+      eh_split8(v, eh[s], em[s]);
+    }
+  };
+  auto max_e = [&]() {
+    float m = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) m = fmaxf(m, fabsf(e[i]));
+    return m;
+  };
+  // layer epilogue: acc <- acc 2^-(sw + sx) + bias (fp32 layer output); returns the lane's max |output|
+  auto epi = [&](int L, int sx) {
+    const float us = ldexpf(1.0f, -(sw[L] + sx));
+    float m = 0.0f;
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + 256 * L + 32 * ob + 8 * gq + 4 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = acc[ob][4 * gq + q] * us + b[q];
+          acc[ob][4 * gq + q] = v;
+          m = fmaxf(m, fabsf(v));
+        }
+      }
+    return m;
+  };
+  eh_f16x8 xh[16], xm[16];   // the hidden B operands
+  auto split_h = [&](int sx) {
+    const float xs = ldexpf(1.0f, sx);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = acc[s >> 1][8 * (s & 1) + j] * xs;
+      eh_split8(v, xh[s], xm[s]);
+    }
+  };
+  auto pair_max = [&](float m) { return fmaxf(m, __shfl_xor(m, 32, 64)); };
+  // layer 0: encoding -> 256
+  int sx = eh_scale(pair_max(max_e()));
+  split_e(sx);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) kstep(eh[s], em[s], s == 0);
+  float mx = epi(0, sx);
+#pragma unroll 1
+  for (int L = 1; L < 8; ++L) {
+    if (L == 4) {   // skip layer: [encoding, h3] share one per-sample scale
+      sx = eh_scale(pair_max(fmaxf(mx, max_e())));
+      split_h(sx);
+      split_e(sx);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kstep(eh[s], em[s], s == 0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) kstep(xh[s], xm[s], false);
+    } else {
+      sx = eh_scale(pair_max(mx));
+      split_h(sx);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) kstep(xh[s], xm[s], s == 0);
+    }
+    mx = epi(L, sx);
+  }
+  // occ_out: Linear(256, 1) + Sigmoid on the fp32 layer-7 output, k_nof_eval's summation order
+  float part = 0.0f;
+#pragma unroll
+  for (int ob = 0; ob < 8; ++ob) {
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(W + OFF_WOUT + 32 * ob + 8 * gq + 4 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part = fmaf(wv[q], acc[ob][4 * gq + q], part);
+    }
+  }
+  const float logit = part + __shfl_xor(part, 32, 64) + W[OFF_BOUT];
+  if (lane < 32 && g < total) p_out[g] = sigmoid_ref(logit);
+}
+
+// Eval-mode MLP arithmetic: 0 = fp32 MFMA (k_nof_eval), 1 = split fp16, 3 products (k_nof_eval_h, default).
+static int g_eval_math = 1;
+
+static void launch_eval(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
+                        const float* W, float* p_out, hipStream_t s) {
+  const int64_t blocks = ((total + 31) / 32 + 3) / 4;
+  if (g_eval_math == 1)
+    hipLaunchKernelGGL(k_nof_eval_h, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
+                       p_out);
+  else
+    hipLaunchKernelGGL(k_nof_eval, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
+                       p_out);
 }
 
 __global__ void k_embed(const float* __restrict__ pts, int64_t n, float* __restrict__ out) {
@@ -396,6 +657,8 @@ extern "C" int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* pack
   const unsigned nb = (unsigned)((OFF_BIAS + 255) / 256);
   hipLaunchKernelGGL(k_pack_eval_weights, dim3(nb), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_pack_eval_vectors, dim3(1), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(k_eval_wscale, dim3(8), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(k_pack_eval_h, dim3((unsigned)((EH_VECS + 255) / 256)), dim3(256), 0, s, P, packed);
   PCN_LAUNCH_CHECK("pcnerf_nof_pack_eval");
   PCN_API_END
 }
@@ -413,9 +676,8 @@ extern "C" int pcnerf_nof_query_eval(const float* rays, int64_t n_rays, int ray_
   {
     // algorithmic work: 982,528 FLOP per sample (9 Linear layers); bytes: z in, p out, ray rows, network image
     ProfScope ps((hipStream_t)stream, PT_EVAL_QUERY, 982528.0 * (double)total,
-                 8.0 * (double)total + 4.0 * ray_stride * (double)n_rays + 4.0 * EVAL_FLOATS);
-    hipLaunchKernelGGL(k_nof_eval, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rays, ray_stride, z,
-                       total, n_samples, (const float*)nullptr, packed, p_out);
+                 8.0 * (double)total + 4.0 * ray_stride * (double)n_rays + 4.0 * EVAL_F32_FLOATS);
+    launch_eval(rays, ray_stride, z, total, n_samples, nullptr, packed, p_out, (hipStream_t)stream);
   }
   PCN_LAUNCH_CHECK("pcnerf_nof_query_eval");
   PCN_API_END
@@ -428,8 +690,17 @@ extern "C" int pcnerf_nof_forward_eval(const float* emb, int64_t n, const float*
   PCN_CHECK(n > 0, "pcnerf_nof_forward_eval: empty input");
   const int64_t blocks = ((n + 31) / 32 + 3) / 4;
   PCN_CHECK(blocks < (int64_t)1 << 31, "pcnerf_nof_forward_eval: too many samples for one launch");
-  hipLaunchKernelGGL(k_nof_eval, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const float*)nullptr, 0,
-                     (const float*)nullptr, n, 1, emb, packed, p_out);
+  launch_eval(nullptr, 0, nullptr, n, 1, emb, packed, p_out, (hipStream_t)stream);
   PCN_LAUNCH_CHECK("pcnerf_nof_forward_eval");
   PCN_API_END
+}
+
+extern "C" int pcnerf_set_eval_math(int mode) {
+  if (mode < 0 || mode > 1) {
+    pcn::set_error("pcnerf_set_eval_math: mode must be 0 (fp32 MFMA) or 1 (split fp16, 3 products)");
+    return -1;
+  }
+  const int prev = pcn::g_eval_math;
+  pcn::g_eval_math = mode;
+  return prev;
 }

@@ -137,6 +137,30 @@ def get_train_math() -> str:
 if os.environ.get("PCNERF_TRAIN_MATH"):
     set_train_math(os.environ["PCNERF_TRAIN_MATH"])
 
+# Arithmetic of the fused eval-mode query (pcnerf_set_eval_math): "f16x2_3" (default; the split products of the
+# train math, weights scaled per layer and activations per sample) or "fp32" (fp32 MFMA).
+EVAL_MATH = {"fp32": 0, "f16x2_3": 1}
+
+
+def set_eval_math(mode: str) -> str:
+    """Select the eval-mode query arithmetic; returns the previous mode's name."""
+    if mode not in EVAL_MATH:
+        raise ValueError(f"eval math must be one of {sorted(EVAL_MATH)}")
+    prev = H.lib().pcnerf_set_eval_math(EVAL_MATH[mode])
+    if prev < 0:
+        raise RuntimeError(H.lib().pcnerf_last_error().decode())
+    return {v: k for k, v in EVAL_MATH.items()}[prev]
+
+
+def get_eval_math() -> str:
+    prev = set_eval_math("fp32")
+    set_eval_math(prev)
+    return prev
+
+
+if os.environ.get("PCNERF_EVAL_MATH"):
+    set_eval_math(os.environ["PCNERF_EVAL_MATH"])
+
 
 # Exact affine fold of the TRAIN-mode network (opt-in; VERDICT r1 item 10): every layer's BatchNorm batch statistics
 # follow from the chunk's encoding mean and covariance, so each chunk's network is sigmoid(a_c . emb + c_c)

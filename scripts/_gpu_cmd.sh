@@ -1,12 +1,7 @@
 export TMPDIR=/tmp
-mkdir -p gpurun_out/prof/r02h_train_step_pmc
-VB_BWD=0 timeout -k 10 300 python scripts/variant_bench.py > gpurun_out/vb_h1i.json 2> gpurun_out/vb_h1i.err
-echo vb rc=$?
-rm -rf pc-nerf_amd/lib/variants
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d gpurun_out/prof/r02h_train_step_pmc/pmc_$C -o run -- \
-    python3 bench.py --no-cpu-baseline --no-fp32-line --mode train_step --rays 16384 --steps 1 --warmup 0 > gpurun_out/prof/r02h_train_step_pmc/pmc_$C.json 2> gpurun_out/prof/r02h_train_step_pmc/pmc_$C.err
-  rc=$?; echo "pmc $C rc=$rc"; [ $rc -ne 0 ] && exit $rc
-  python3 scripts/compact_pmc.py gpurun_out/prof/r02h_train_step_pmc/pmc_$C
-done
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "eval or val or view or render_rays" > gpurun_out/pytest_eval.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_eval.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python bench.py --mode val --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_valh.json 2> gpurun_out/bench_valh.err &&
+timeout -k 10 300 python bench.py --mode view --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_viewh.json 2> gpurun_out/bench_viewh.err
 echo rc=$?

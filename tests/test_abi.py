@@ -25,7 +25,8 @@ def test_library_loads_and_exports_header_symbols():
 def test_size_queries_without_gpu():
     from nof import _hip
     L = _hip.lib()
-    assert L.pcnerf_nof_eval_packed_floats() == 2 * 16384 + 7 * 65536 + 8 * 256 + 256 + 4
+    # the fp32 image, 16 floats of split-image scales, the split image (120 k-steps x 8 x 2 x 64 f16x8)
+    assert L.pcnerf_nof_eval_packed_floats() == 2 * 16384 + 7 * 65536 + 8 * 256 + 256 + 4 + 16 + 120 * 8 * 2 * 64 * 4
     # two chunk-sized activation buffers dominate the train workspace
     assert L.pcnerf_nof_train_workspace_bytes(262144) >= 2 * 262144 * 256 * 4
     assert L.pcnerf_child_loss_workspace_bytes(15333) == 15333 * 3 * 8

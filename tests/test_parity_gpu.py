@@ -44,7 +44,16 @@ def test_embedding():
     close(e, g["embedding"], 0, 2e-6, "embedding")
 
 
-def test_nof_eval_forward():
+@pytest.fixture(params=["f16x2_3", "fp32"])
+def eval_math(request):
+    """The fused eval query's arithmetic (nof._ops.set_eval_math): the default split-fp16 products and fp32 MFMA."""
+    from nof import _ops
+    prev = _ops.set_eval_math(request.param)
+    yield request.param
+    _ops.set_eval_math(prev)
+
+
+def test_nof_eval_forward(eval_math):
     g = golden("nof_eval")
     _, mc, _ = models(False)
     with torch.no_grad():
@@ -93,7 +102,7 @@ def test_sample_pdf():
 
 
 @pytest.mark.parametrize("S", [64, 128])
-def test_render_val(S):
+def test_render_val(S, eval_math):
     g = golden(f"render_val_s{S}")
     emb, mc, mf = models(False)
     with torch.no_grad():
@@ -162,7 +171,7 @@ def test_render_train(name, train_math):
 
 
 @pytest.mark.parametrize("method", [0, 2])
-def test_render_view(method):
+def test_render_view(method, eval_math):
     g = golden(f"render_view_m{method}")
     emb, mc, mf = models(False)
     with torch.no_grad():
@@ -184,7 +193,7 @@ def test_render_view(method):
 
 
 @pytest.mark.parametrize("isval", [0, 1])
-def test_render_rays(isval):
+def test_render_rays(isval, eval_math):
     g = golden(f"render_rays_isval{isval}")
     emb, mc, mf = models(False)
     with torch.no_grad():
@@ -309,7 +318,7 @@ def test_render_train_tiny_and_odd_chunks(chunk, train_math):
     close(running(mc), want, RTOL, 1e-7, "running stats")
 
 
-def test_eval_query_is_per_sample():
+def test_eval_query_is_per_sample(eval_math):
     """Eval mode: a ray rendered alone equals the same ray rendered inside a large batch (bitwise)."""
     rays = torch.from_numpy(syn.make_rays(4096, seed=5)).to(DEV)
     emb, mc, mf = models(False)
