@@ -220,6 +220,15 @@ __global__ __launch_bounds__(256) void k_eval_wscale(NofParamsDev P, float* __re
 }
 
 typedef _Float16 eh_f16x8 __attribute__((ext_vector_type(8)));
+#ifndef PCN_EH_WLATE
+#define PCN_EH_WLATE 1   // publish the next super-slice after this one's MFMAs (else before them)
+#endif
+#ifndef PCN_EH_ORD
+#define PCN_EH_ORD 1   // k_nof_eval_h: MFMAs product-major over the 8 out-blocks (independent accumulators)
+#endif
+#ifndef PCN_EH_KPB
+#define PCN_EH_KPB 1   // k_nof_eval_h: k-steps per weight super-slice (one barrier each)
+#endif
 
 __global__ void k_pack_eval_h(NofParamsDev P, float* __restrict__ out) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -273,7 +282,10 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__
                                                        const float* __restrict__ z, int64_t total, int S,
                                                        const float* __restrict__ ein, const float* __restrict__ W,
                                                        float* __restrict__ p_out) {
-  __shared__ eh_f16x8 wsl[2][8 * 2 * 64];   // two k-step slices of the weight stream
+  // weight stream in super-slices of KPB k-steps (16 KiB each), two LDS slots, one barrier per super-slice
+  constexpr int KPB = PCN_EH_KPB, NV = 4 * KPB;   // vectors per thread per super-slice
+  static_assert(EH_KSTEPS % KPB == 0, "super-slices");
+  __shared__ eh_f16x8 wsl[2][KPB * 8 * 2 * 64];
   __shared__ __attribute__((aligned(16))) float sbias[8 * 256];
   const int t = threadIdx.x, lane = t & 63, h = lane >> 5;
   const int64_t tile = (int64_t)blockIdx.x * 4 + (t >> 6);
@@ -283,12 +295,13 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__
   int sw[8];
 #pragma unroll
   for (int L = 0; L < 8; ++L) sw[L] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(W + OFF_EH_SW)[L]);
-  // weight stream: thread t moves vectors t + 256 m of each 1,024-vector slice
-  eh_f16x8 ldA[4], ldB[4];
+  // thread t moves vectors t + 256 m of each super-slice
+  constexpr int NSS = EH_KSTEPS / KPB;
+  eh_f16x8 ldA[NV], ldB[NV];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) wsl[0][t + 256 * m] = img[t + 256 * m];
+  for (int m = 0; m < NV; ++m) wsl[0][t + 256 * m] = img[t + 256 * m];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) ldA[m] = img[1024 + t + 256 * m];
+  for (int m = 0; m < NV; ++m) ldA[m] = img[(size_t)1024 * KPB + t + 256 * m];
   for (int i = t; i < 8 * 256 / 4; i += 256)
     reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
   float e[32];
@@ -303,37 +316,65 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__
   __syncthreads();
   int gk = 0;
   f32x16 acc[8];
-  // one k-step of the current layer: B operands (xh, xm), A operands from the slice in LDS; the loader issues the
-  // slice two k-steps ahead and publishes the next one
+  // one k-step of the current layer: B operands (xh, xm), A operands from the super-slice in LDS.  The first
+  // k-step of a super-slice issues the loads of the one after next; the next one (loaded a super-slice earlier) is
+  // published into the other slot (last read before the previous barrier) after this super-slice's MFMAs
+  // (PCN_EH_WLATE) or before them; the last k-step ends with the barrier.
   auto kstep = [&](const eh_f16x8& xh, const eh_f16x8& xm, bool first) {
-    if (gk + 2 < EH_KSTEPS) {
+    const int ss = gk / KPB, sub = gk - ss * KPB;
+    if (sub == 0) {
+      if (!PCN_EH_WLATE && ss + 1 < NSS) {
 #pragma unroll
-      for (int m = 0; m < 4; ++m) ldB[m] = img[(size_t)(gk + 2) * 1024 + t + 256 * m];
+        for (int m = 0; m < NV; ++m) wsl[(ss + 1) & 1][t + 256 * m] = ldA[m];
+      }
+      if (ss + 2 < NSS) {
+#pragma unroll
+        for (int m = 0; m < NV; ++m) ldB[m] = img[(size_t)(ss + 2) * 1024 * KPB + t + 256 * m];
+      }
     }
-    const eh_f16x8* sl = wsl[gk & 1];
-    eh_f16x8 a0 = sl[lane], a1 = sl[64 + lane];
+    const eh_f16x8* sl = wsl[ss & 1] + sub * 1024;
+    if (PCN_EH_ORD) {   // product-major: all 16 A operands, then 8 independent MFMAs per product
+      eh_f16x8 aa[8][2];
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob) {
+        aa[ob][0] = sl[(2 * ob) * 64 + lane];
+        aa[ob][1] = sl[(2 * ob + 1) * 64 + lane];
+      }
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob)
+        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[ob][0], xh, first ? f32x16{} : acc[ob], 0, 0, 0);
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob) acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[ob][0], xm, acc[ob], 0, 0, 0);
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob) acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[ob][1], xh, acc[ob], 0, 0, 0);
+    } else {
+    eh_f16x8 a[3][2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      a[d][0] = sl[(2 * d) * 64 + lane];
+      a[d][1] = sl[(2 * d + 1) * 64 + lane];
+    }
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) {
-      eh_f16x8 n0, n1;
-      if (ob + 1 < 8) {
-        n0 = sl[((ob + 1) * 2) * 64 + lane];
-        n1 = sl[((ob + 1) * 2 + 1) * 64 + lane];
+      if (ob + 2 < 8) {
+        a[(ob + 2) % 3][0] = sl[((ob + 2) * 2) * 64 + lane];
+        a[(ob + 2) % 3][1] = sl[((ob + 2) * 2 + 1) * 64 + lane];
       }
+      const eh_f16x8 a0 = a[ob % 3][0], a1 = a[ob % 3][1];
       acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, xh, first ? f32x16{} : acc[ob], 0, 0, 0);
       acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, xm, acc[ob], 0, 0, 0);
       acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, xh, acc[ob], 0, 0, 0);
-      if (ob + 1 < 8) {
-        a0 = n0;
-        a1 = n1;
+    }
+    }
+    if (sub == KPB - 1) {
+      if (PCN_EH_WLATE && ss + 1 < NSS) {
+#pragma unroll
+        for (int m = 0; m < NV; ++m) wsl[(ss + 1) & 1][t + 256 * m] = ldA[m];
       }
-    }
-    if (gk + 1 < EH_KSTEPS) {
+      __syncthreads();
 #pragma unroll
-      for (int m = 0; m < 4; ++m) wsl[(gk + 1) & 1][t + 256 * m] = ldA[m];
+      for (int m = 0; m < NV; ++m) ldA[m] = ldB[m];
     }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 4; ++m) ldA[m] = ldB[m];
     ++gk;
   };
   // the encoding's B operands at per-sample scale 2^sx
