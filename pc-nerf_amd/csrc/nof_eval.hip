@@ -220,6 +220,12 @@ __global__ __launch_bounds__(256) void k_eval_wscale(NofParamsDev P, float* __re
 }
 
 typedef _Float16 eh_f16x8 __attribute__((ext_vector_type(8)));
+#ifndef PCN_EH2
+#define PCN_EH2 1   // split eval query as k_nof_eval_h2 (neuron-split waves, activations through LDS)
+#endif
+#ifndef PCN_EH2_PF
+#define PCN_EH2_PF 0   // k_nof_eval_h2: the next k-step's B operands read during this k-step's MFMAs
+#endif
 #ifndef PCN_EH_WLATE
 #define PCN_EH_WLATE 1   // publish the next super-slice after this one's MFMAs (else before them)
 #endif
@@ -464,13 +470,246 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__
   if (lane < 32 && g < total) p_out[g] = sigmoid_ref(logit);
 }
 
+// ---- k_nof_eval_h2: the same split eval network with the work split over NEURONS inside a block: wave w owns
+// out-blocks 2w, 2w+1 (64 neurons) of every layer for all 96 samples (3 tiles) of its block, so each wave streams
+// only its own 64 neurons' weights from L2 (4 KiB per k-step, three k-steps in flight, no barrier) and each A
+// operand feeds 3 sample tiles; the layer outputs go through LDS as the next layer's split B operands
+// ([k-step][tile][part][lane], 96 KiB), two barriers per layer (per-sample maxima, then the split outputs).
+// The encoding lives in LDS as layer 0's split B operands; layer 4 re-splits it (hi + mid is exact in fp32) at the
+// per-sample scale it shares with h3.
+#ifndef PCN_EH2_T
+#define PCN_EH2_T 3
+#endif
+constexpr int E2_T = PCN_EH2_T;   // sample tiles per block
+__global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict__ rays, int stride,
+                                                        const float* __restrict__ z, int64_t total, int S,
+                                                        const float* __restrict__ ein, const float* __restrict__ W,
+                                                        float* __restrict__ p_out) {
+  __shared__ eh_f16x8 act[16][E2_T][2][64];
+  __shared__ eh_f16x8 eb[4][E2_T][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
+  __shared__ int sx0s[E2_T * 32];
+  __shared__ __attribute__((aligned(16))) float sbias[8 * 256];
+  __shared__ float emax[E2_T * 32];
+  __shared__ float smax[4][E2_T * 32];
+  __shared__ float pdot[4][E2_T * 32];
+  const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int64_t s0 = (int64_t)blockIdx.x * (32 * E2_T);
+  const eh_f16x8* __restrict__ img = reinterpret_cast<const eh_f16x8*>(W + OFF_EH);
+  int sw[8];
+#pragma unroll
+  for (int L = 0; L < 8; ++L) sw[L] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(W + OFF_EH_SW)[L]);
+  // this wave's A operands of k-step gk: out-blocks 2w + o, parts hi / mid
+  auto load_w = [&](eh_f16x8 (&d)[2][2], int gk) {
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) d[o][p] = img[((size_t)(gk * 8 + 2 * w + o) * 2 + p) * 64 + lane];
+  };
+  eh_f16x8 wc[2][2], wn[2][2], wnn[2][2];
+  load_w(wc, 0);
+  load_w(wn, 1);
+  for (int i = t; i < 8 * 256 / 4; i += 256)
+    reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
+  if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
+    int64_t g = s0 + t;
+    if (g >= total) g = total - 1;
+    float f[64];
+    if (ein) {
+#pragma unroll
+      for (int k = 0; k < 63; ++k) f[k] = ein[g * 63 + k];
+      f[63] = 0.0f;
+    } else {
+      float p[3];
+      sample_point(rays + (g / S) * stride, z[g], p);
+      encode_full(p, f);
+    }
+    const int tau = t >> 5, l = t & 31;
+    float m = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 63; ++k) m = fmaxf(m, fabsf(f[k]));
+    const int sx0 = eh_scale(m);
+    const float xs = ldexpf(1.0f, sx0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f[2 * (8 * s + j) + hh] * xs;
+        eh_f16x8 hi, mid;
+        eh_split8(v, hi, mid);
+        eb[s][tau][0][l + 32 * hh] = hi;
+        eb[s][tau][1][l + 32 * hh] = mid;
+      }
+    emax[t] = m;
+    sx0s[t] = sx0;
+  }
+  __syncthreads();
+  int sxl[E2_T];   // the per-sample scale of the current layer's B operands (this lane's sample of each tile)
+#pragma unroll
+  for (int tau = 0; tau < E2_T; ++tau) sxl[tau] = sx0s[32 * tau + li];
+  f32x16 acc[2][E2_T];
+  int gk = 0;
+  // one k-step: B operands of the 3 tiles (from the encoding at the lane's scale, or the split activations),
+  // MFMAs product-major over the 6 accumulators
+  eh_f16x8 pbh[E2_T], pbm[E2_T];   // PCN_EH2_PF: the next hidden k-step's B operands, read during this one
+  auto kstep = [&](int s, bool enc, bool first) {
+    if (gk + 2 < EH_KSTEPS) load_w(wnn, gk + 2);
+    eh_f16x8 bh[E2_T], bm[E2_T];
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau) {
+      if (PCN_EH2_PF && !enc && s > 0) {
+        bh[tau] = pbh[tau];
+        bm[tau] = pbm[tau];
+      } else if (enc) {
+        bh[tau] = eb[s][tau][0][lane];
+        bm[tau] = eb[s][tau][1][lane];
+        const int d = sxl[tau] - sx0s[32 * tau + li];
+        if (d != 0) {   // layer 4: the 22-bit encoding (hi + mid, exact in fp32) re-split at the shared scale
+          const float xs = ldexpf(1.0f, d);
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = ((float)bh[tau][j] + (float)bm[tau][j]) * xs;
+          eh_split8(v, bh[tau], bm[tau]);
+        }
+      } else {
+        bh[tau] = act[s][tau][0][lane];
+        bm[tau] = act[s][tau][1][lane];
+      }
+    }
+    if (PCN_EH2_PF && !enc && s + 1 < 16) {
+#pragma unroll
+      for (int tau = 0; tau < E2_T; ++tau) {
+        pbh[tau] = act[s + 1][tau][0][lane];
+        pbm[tau] = act[s + 1][tau][1][lane];
+      }
+    }
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau)
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+        acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bh[tau], first ? f32x16{} : acc[o][tau], 0, 0, 0);
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau)
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+        acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bm[tau], acc[o][tau], 0, 0, 0);
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau)
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+        acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        wc[o][p] = wn[o][p];
+        wn[o][p] = wnn[o][p];
+      }
+    ++gk;
+  };
+  // epilogue phase 1: acc <- acc 2^-(sw + sx) + bias, this wave's per-sample maxima -> smax[w]
+  auto epi1 = [&](int L) {
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau) {
+      const float us = ldexpf(1.0f, -(sw[L] + sxl[tau]));
+      float m = 0.0f;
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + 256 * L + 32 * (2 * w + o) + 8 * gq + 4 * h);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = acc[o][tau][4 * gq + q] * us + b[q];
+            acc[o][tau][4 * gq + q] = v;
+            m = fmaxf(m, fabsf(v));
+          }
+        }
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      if (h == 0) smax[w][32 * tau + li] = m;
+    }
+  };
+  // phase 2 (after a barrier): the next layer's per-sample scale and this wave's k-steps 4w .. 4w+3 of its B operands
+  auto epi2 = [&](bool with_e) {
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau) {
+      const int sm = 32 * tau + li;
+      float m = fmaxf(fmaxf(smax[0][sm], smax[1][sm]), fmaxf(smax[2][sm], smax[3][sm]));
+      if (with_e) m = fmaxf(m, emax[sm]);
+      sxl[tau] = eh_scale(m);
+      const float xs = ldexpf(1.0f, sxl[tau]);
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = acc[o][tau][8 * k + j] * xs;
+          eh_f16x8 hi, mid;
+          eh_split8(v, hi, mid);
+          const int s = 4 * w + 2 * o + k;
+          act[s][tau][0][lane] = hi;
+          act[s][tau][1][lane] = mid;
+        }
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < 4; ++s) kstep(s, true, s == 0);
+  epi1(0);
+  __syncthreads();
+  epi2(false);
+  __syncthreads();
+#pragma unroll 1
+  for (int L = 1; L < 8; ++L) {
+    if (L == 4) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kstep(s, true, s == 0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) kstep(s, false, false);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) kstep(s, false, s == 0);
+    }
+    epi1(L);
+    __syncthreads();
+    if (L < 7) {
+      epi2(L == 3);
+      __syncthreads();
+    }
+  }
+  // occ_out: this wave's 64 neurons per sample, then the 4 partial sums in order
+#pragma unroll
+  for (int tau = 0; tau < E2_T; ++tau) {
+    float part = 0.0f;
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const f32x4 wv = *reinterpret_cast<const f32x4*>(W + OFF_WOUT + 32 * (2 * w + o) + 8 * gq + 4 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) part = fmaf(wv[q], acc[o][tau][4 * gq + q], part);
+      }
+    part += __shfl_xor(part, 32, 64);
+    if (h == 0) pdot[w][32 * tau + li] = part;
+  }
+  __syncthreads();
+  if (t < 32 * E2_T && s0 + t < total) {
+    const float logit = ((pdot[0][t] + pdot[1][t]) + (pdot[2][t] + pdot[3][t])) + W[OFF_BOUT];
+    p_out[s0 + t] = sigmoid_ref(logit);
+  }
+}
+
 // Eval-mode MLP arithmetic: 0 = fp32 MFMA (k_nof_eval), 1 = split fp16, 3 products (k_nof_eval_h, default).
 static int g_eval_math = 1;
 
 static void launch_eval(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const float* W, float* p_out, hipStream_t s) {
   const int64_t blocks = ((total + 31) / 32 + 3) / 4;
-  if (g_eval_math == 1)
+  if (g_eval_math == 1 && PCN_EH2)
+    hipLaunchKernelGGL(k_nof_eval_h2, dim3((unsigned)((total + 32 * E2_T - 1) / (32 * E2_T))), dim3(256), 0, s, rays,
+                       stride, z, total, S, ein, W, p_out);
+  else if (g_eval_math == 1)
     hipLaunchKernelGGL(k_nof_eval_h, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
                        p_out);
   else

@@ -53,7 +53,7 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     res = {k: {t: [] for t in TAGS} for k in Ls}
     qt = {}
-    outs, gouts = {}, {}
+    outs, gouts, eouts = {}, {}, {}
     bwd = os.environ.get("VB_BWD", "1") == "1"
     if bwd:   # backward on a quarter of the rays (its workspace holds all 8 layers of a chunk)
         rays_b, z_b = rays[: rays_n // 4].contiguous(), z[: rays_n // 4].contiguous()
@@ -82,6 +82,8 @@ def main():
             m.eval()
             L.pcnerf_nof_pack_eval(ctypes.byref(s), packed.data_ptr(), st)
             L.pcnerf_nof_query_eval(rays.data_ptr(), rays_n, 15, z.data_ptr(), S, packed.data_ptr(), p.data_ptr(), st)
+            if rnd == 0:
+                eouts[name] = p.clone()   # eval-mode query output of this variant
             m.train()
             torch.cuda.synchronize()
             if rnd == 0:
@@ -113,6 +115,9 @@ def main():
         for name in Ls:
             d = (outs[name] - ref).abs() / ref.abs().clamp_min(1e-12)
             out[name]["max_rel_diff_vs_base"] = float(d.max())
+            if name in eouts and "base" in eouts:
+                er = eouts["base"]
+                out[name]["eval_max_rel_diff_vs_base"] = float(((eouts[name] - er).abs() / er.abs().clamp_min(1e-12)).max())
             if name in gouts:
                 gr = gouts["base"]
                 out[name]["grad_max_rel_diff_vs_base"] = float(((gouts[name] - gr).abs().max() / gr.abs().max()))
