@@ -107,6 +107,15 @@ namespace pcn {
 #ifndef PCN_H1I_EPI
 #define PCN_H1I_EPI 8   // ... its BatchNorm + split at W1 k-steps EPI .. EPI + 3
 #endif
+#ifndef PCN_H16
+#define PCN_H16 0       // hidden split layers as k_train_h16 (16 waves of 16 neurons, four waves per SIMD)
+#endif
+#ifndef PCN_H16_LOAD
+#define PCN_H16_LOAD 0  // ... k-step of the next tile's raw loads
+#endif
+#ifndef PCN_H16_STAGE
+#define PCN_H16_STAGE 6 // ... k-step of its staging
+#endif
 #ifndef PCN_GRAM
 #define PCN_GRAM 1    // with PCN_H1: layer 0 as the encoding's moments (k_enc_gram) instead of its 256-neuron product
 #endif
@@ -1180,6 +1189,180 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
   }
 }
 
+// ---- k_train_h16<NT>: the hidden split layer with 16 waves of 16 neurons (four waves per SIMD instead of two), on
+// v_mfma_f32_16x16x32_f16: wave b holds the hi/mid weights of neurons 16b..16b+15 (64 registers; image
+// [layer-1][k-step 8][wave 16][part 2][lane 64] f16x8, lane l: neuron 16b + (l&15), features 32s + 8(l>>4) + j),
+// a 32-sample tile is two 16-column blocks, B in LDS as [k-step][block][part][lane] f16x8 (lane l: sample
+// 16 blk + (l&15), features 32s + 8(l>>4) + j), D (reg r, lane l) = neuron 16b + 4(l>>4) + r, sample 16 blk + (l&15)
+// -> one float4 store per block into the [g][lane][4] activation layout.  Same statistics, scales, BatchNorm-on-
+// staging, reversed walks and in-place buffer as k_train_h<0,true,NT>; the running sums per lane cover 4 neurons.
+constexpr size_t H16_LAYER_VECS = (size_t)8 * 16 * 2 * 64;
+constexpr size_t H16_VECS = 7 * H16_LAYER_VECS;   // layers 1..7 (the skip layer's h-part included, unused)
+
+__global__ void k_pack_train_h16(NofParamsDev P, const int* __restrict__ sw, f16x8* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= H16_VECS) return;
+  const int L = 1 + (int)(idx / H16_LAYER_VECS);
+  const size_t j0 = idx % H16_LAYER_VECS;
+  const int lane = (int)(j0 & 63), part = (int)((j0 >> 6) & 1), wb = (int)((j0 >> 7) & 15), ks = (int)(j0 >> 11);
+  const int nn = 16 * wb + (lane & 15);
+  const int in_f = L == 4 ? 319 : 256;
+  const float sc = ldexpf(1.0f, sw[L]);
+  f16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int col = (L == 4 ? 63 : 0) + 32 * ks + 8 * (lane >> 4) + e;
+    const float w = P.lin_w[L][(size_t)nn * in_f + col] * sc;
+    const _Float16 hi = (_Float16)w;
+    v[e] = part == 0 ? hi : (_Float16)(w - (float)hi);
+  }
+  out[idx] = v;
+}
+
+template <int NT>
+__global__ __launch_bounds__(1024, 1) void k_train_h16(const float* __restrict__ hin, int64_t n,
+                                                      const f16x8* __restrict__ Wp, const int* __restrict__ swp,
+                                                      int layer, const float* __restrict__ bias, BnPrev prev,
+                                                      float momentum, float eps, float* __restrict__ hout,
+                                                      double* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) float al[256];
+  __shared__ __attribute__((aligned(16))) float be[256];
+  __shared__ __attribute__((aligned(16))) float bs[256];
+  __shared__ float smax[16];
+  __shared__ f16x8 xs[2][8][2][2][64];   // [buf][k-step][block][part][lane]
+  const int t = threadIdx.x;
+  if (t < 256) {
+    bn_coeffs(prev, n, momentum, eps, al, be);
+    bs[t] = bias[t];
+  }
+  int sx;
+  {
+    float bnd = 0.0f;
+    if (t < 256) bnd = sqrtf((float)n) * fabsf(prev.gamma[t]) + fabsf(prev.beta[t]);
+    bnd = wave_max_f(bnd);
+    if ((t & 63) == 0) smax[t >> 6] = bnd;
+    __syncthreads();
+    float m = smax[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) m = fmaxf(m, smax[i]);
+    sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
+    sx = sx > 24 ? 24 : sx;
+    if (t < 256) {
+      al[t] = ldexpf(al[t], sx);
+      be[t] = ldexpf(be[t], sx);
+    }
+  }
+  const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
+  const int nt = (int)((n + 31) / 32);
+  const int gstride = (int)gridDim.x;
+  const bool rev = (layer >> 8) & 1;
+  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
+  const int lane = t & 63, lq = lane >> 4, lr = lane & 15;
+  const int wb = __builtin_amdgcn_readfirstlane(t >> 6);
+  f16x8 wr[8][2];
+  {
+    const f16x8* __restrict__ w8 = Wp + lane;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 16 + wb) * 2 + p) * 64];
+  }
+  float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f}, rq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  // staging: thread t owns raw float4s u = t + 1024 m of a tile ([g][lane'][4]: features 8g + 4h', sample lane'&31)
+  auto load_tile = [&](f32x4 (&v)[2], int tile) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)P(tile) * TILE_FLOATS)[t + 1024 * m];
+  };
+  auto stage = [&](int b, const f32x4 (&v)[2]) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int u = t + 1024 * m, g = u >> 6, lp = u & 63, smp = lp & 31, hq = lp >> 5;
+      const int f0 = 8 * g + 4 * hq;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(al + f0);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(be + f0);
+      f32x4 x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + c[q];
+      f16x4 hi, mid;
+      split4(x, hi, mid);
+      const int ks = g >> 2, blk = smp >> 4, l = (smp & 15) + 16 * (g & 3);
+      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][ks][blk][0][l]) + 4 * hq) = hi;
+      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][ks][blk][1][l]) + 4 * hq) = mid;
+    }
+  };
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  if (tl < nt) {
+    f32x4 v[2];
+    load_tile(v, tl);
+    stage(0, v);
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);
+  int buf = 0;
+  while (tl < nt) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
+    const bool more = nxt < nt;
+    f32x4 vl[2];
+    f32x4 acc[2];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      if (ks == PCN_H16_LOAD && more) load_tile(vl, nxt);
+      const f16x8 x0h = xs[buf][ks][0][0][lane], x0m = xs[buf][ks][0][1][lane];
+      const f16x8 x1h = xs[buf][ks][1][0][lane], x1m = xs[buf][ks][1][1][lane];
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], x0h, ks == 0 ? f32x4{} : acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], x1h, ks == 0 ? f32x4{} : acc[1], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], x0m, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], x1m, acc[1], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], x0h, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], x1h, acc[1], 0, 0, 0);
+      if (NT == 4) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], x0m, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], x1m, acc[1], 0, 0, 0);
+      }
+      if (ks == PCN_H16_STAGE && more) stage(buf ^ 1, vl);
+    }
+    {   // epilogue: + bias, statistics, one float4 store per block
+      const int tile = P(tl);
+      const int f0 = 16 * wb + 4 * lq;
+      const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + f0);
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        const int smp = 16 * blk + lr;
+        const bool valid = (int64_t)tile * 32 + smp < n;
+        f32x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[blk][r] * unscale;
+          o[r] = d + bj[r];
+          const float dv = valid ? d : 0.0f;
+          rs[r] += dv;
+          rq[r] += dv * dv;
+        }
+        const int g = f0 >> 3, lp = smp + 32 * ((f0 >> 2) & 1);
+        reinterpret_cast<f32x4*>(hout + (size_t)tile * TILE_FLOATS)[g * 64 + lp] = o;
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+    tl = nxt;
+  }
+  // per neuron: the 16 lanes of a quarter-wave hold 16 samples' sums; reduce them in float64, one atomic each
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double a = (double)rs[r], q = (double)rq[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      a += __shfl_xor(a, o, 64);
+      q += __shfl_xor(q, o, 64);
+    }
+    if (lr == 0) {
+      const int nn = 16 * wb + 4 * lq + r;
+      atomicAdd(&stats[2 * nn], a);
+      atomicAdd(&stats[2 * nn + 1], q);
+    }
+  }
+}
+
 // ---- layer 0 from the encoding's moments (split forward without activation store, k_train_h1 after it).
 // Layer 0's only remaining outputs there are the chunk's encoding tiles and BatchNorm 0's statistics, and those
 // statistics are exact functions of the chunk's encoding mean ebar and covariance Sigma (h0 = W0 e + b0 feeds
@@ -1656,6 +1839,7 @@ struct TrainWs {
   f32x4* enc;   // the chunk's encoding tiles: written by the first layer, read by the skip layer
   float* wp;
   f16x8* wh;    // split-fp16 weight image (train math 1/2)
+  f16x8* wh16;  // k_train_h16's image of the 256-input layers
   int* sw;      // its per-layer scale exponents
   double* stats;
   double* gram;  // k_enc_gram partials, their slice sums and the chunk's shift e0
@@ -1680,6 +1864,7 @@ static TrainWs carve(void* base, int64_t chunk) {
   const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
   const size_t ogr = take(GR_DOUBLES * sizeof(double));
+  const size_t oh16 = take(H16_VECS * sizeof(f16x8));
   char* b = (char*)base;
   TrainWs w;
   w.bufA = (float*)(b + oA);
@@ -1690,6 +1875,7 @@ static TrainWs carve(void* base, int64_t chunk) {
   w.sw = (int*)(b + osw);
   w.stats = (double*)(b + ost);
   w.gram = (double*)(b + ogr);
+  w.wh16 = (f16x8*)(b + oh16);
   w.bytes = off;
   return w;
 }
@@ -1837,6 +2023,8 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   hipStream_t s = (hipStream_t)stream;
   pack_weights(P, ws.wp, ws.wh, ws.sw, s);
+  if (PCN_H16 && g_train_math != 0)
+    hipLaunchKernelGGL(k_pack_train_h16, dim3((unsigned)((H16_VECS + 255) / 256)), dim3(256), 0, s, P, ws.sw, ws.wh16);
   for (int64_t c0 = 0; c0 < total; c0 += chunk) {
     const int64_t n = total - c0 < chunk ? total - c0 : chunk;
     const int64_t ntiles = (n + 31) / 32;
@@ -1905,7 +2093,17 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
         const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};
-        launch_layer<0, true>(q, P, ws.wp, ws.wh, ws.sw, L, hin, prev, hout, stats + 512 * L, nullptr, nullptr);
+        if (PCN_H16 && g_train_math != 0) {
+          const f16x8* w16 = ws.wh16 + (size_t)(L - 1) * H16_LAYER_VECS;
+          if (g_train_math == 1)
+            hipLaunchKernelGGL(k_train_h16<3>, dim3(gws), dim3(1024), 0, s, hin, n, w16, ws.sw,
+                               L | (tile_rev(L) << 8), P.lin_b[L], prev, momentum, eps, hout, stats + 512 * L);
+          else
+            hipLaunchKernelGGL(k_train_h16<4>, dim3(gws), dim3(1024), 0, s, hin, n, w16, ws.sw,
+                               L | (tile_rev(L) << 8), P.lin_b[L], prev, momentum, eps, hout, stats + 512 * L);
+        } else {
+          launch_layer<0, true>(q, P, ws.wp, ws.wh, ws.sw, L, hin, prev, hout, stats + 512 * L, nullptr, nullptr);
+        }
       }
       float* t = hin;
       hin = hout;
