@@ -1,4 +1,4 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash scripts/gpu_tests.sh && timeout -k 10 300 python bench.py > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err && timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-echo rc=$?
+VB_BWD=0 timeout -k 10 300 python scripts/variant_bench.py > gpurun_out/vb_grpf.json 2> gpurun_out/vb_grpf.err
+echo vb rc=$?
