@@ -2044,7 +2044,9 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     const bool h1 = PCN_H1 && !keep && g_train_math != 0;
     if (!(h1 && PCN_GRAM)) PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));   // (else k_gram_stats)
     // PCN_INPLACE: every layer of the chunk overwrites its input tile by tile (a tile is read only by the workgroup
-    // that writes its output, which staged it before its MFMAs): one 268 MB footprint instead of two
+    // that writes its output, which staged it before its MFMAs): one 268 MB footprint instead of two.  The kernels'
+    // __restrict__ hin / hout then alias, which stays sound here: a tile's output store depends on its own input
+    // load through LDS and a workgroup barrier (no reordering can cross that), and no other tile is touched twice.
     if (h1 && PCN_INPLACE) hout = hin;
     if (h1 && PCN_GRAM) {
       // algorithmic: the 64 x 64 moment product per sample; 4 B of z in, 256 B of encoding out
