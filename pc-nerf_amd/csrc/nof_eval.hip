@@ -472,7 +472,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__
 
 // ---- k_nof_eval_h2: the same split eval network with the work split over NEURONS inside a block: wave w owns
 // out-blocks 2w, 2w+1 (64 neurons) of every layer for all 96 samples (3 tiles) of its block, so each wave streams
-// only its own 64 neurons' weights from L2 (4 KiB per k-step, three k-steps in flight, no barrier) and each A
+// only its own 64 neurons' weights from L2 (4 KiB per k-step, three k-steps in flight in a 4-slot register ring,
+// no barrier) and each A
 // operand feeds 3 sample tiles; the layer outputs go through LDS as the next layer's split B operands
 // ([k-step][tile][part][lane], 96 KiB), two barriers per layer (per-sample maxima, then the split outputs).
 // The encoding lives in LDS as layer 0's split B operands; layer 4 re-splits it (hi + mid is exact in fp32) at the
@@ -505,9 +506,13 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
 #pragma unroll
       for (int p = 0; p < 2; ++p) d[o][p] = img[((size_t)(gk * 8 + 2 * w + o) * 2 + p) * 64 + lane];
   };
-  eh_f16x8 wc[2][2], wn[2][2], wnn[2][2];
-  load_w(wc, 0);
-  load_w(wn, 1);
+  // ring of 4 k-steps of A operands, slot = k-step index within its layer & 3 (every layer's k-step count and
+  // start are multiples of 4, so the slot is a compile-time index in the unrolled k-loops and no in-flight load's
+  // registers are ever copied): k-step s issues the loads of k-step s + 3 into the slot k-step s - 1 just used
+  eh_f16x8 wr4[4][2][2];
+  load_w(wr4[0], 0);
+  load_w(wr4[1], 1);
+  load_w(wr4[2], 2);
   for (int i = t; i < 8 * 256 / 4; i += 256)
     reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
   if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
@@ -553,8 +558,9 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   // one k-step: B operands of the 3 tiles (from the encoding at the lane's scale, or the split activations),
   // MFMAs product-major over the 6 accumulators
   eh_f16x8 pbh[E2_T], pbm[E2_T];   // PCN_EH2_PF: the next hidden k-step's B operands, read during this one
-  auto kstep = [&](int s, bool enc, bool first) {
-    if (gk + 2 < EH_KSTEPS) load_w(wnn, gk + 2);
+  auto kstep = [&](int s, int pos, bool enc, bool first) {   // pos: the k-step's index within its layer
+    if (gk + 3 < EH_KSTEPS) load_w(wr4[(pos + 3) & 3], gk + 3);
+    const eh_f16x8 (&wc)[2][2] = wr4[pos & 3];
     eh_f16x8 bh[E2_T], bm[E2_T];
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
@@ -599,13 +605,6 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
 #pragma unroll
       for (int o = 0; o < 2; ++o)
         acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
-#pragma unroll
-    for (int o = 0; o < 2; ++o)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        wc[o][p] = wn[o][p];
-        wn[o][p] = wnn[o][p];
-      }
     ++gk;
   };
   // epilogue phase 1: acc <- acc 2^-(sw + sx) + bias, this wave's per-sample maxima -> smax[w]
@@ -655,7 +654,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     }
   };
 #pragma unroll
-  for (int s = 0; s < 4; ++s) kstep(s, true, s == 0);
+  for (int s = 0; s < 4; ++s) kstep(s, s, true, s == 0);
   epi1(0);
   __syncthreads();
   epi2(false);
@@ -664,12 +663,12 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   for (int L = 1; L < 8; ++L) {
     if (L == 4) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) kstep(s, true, s == 0);
+      for (int s = 0; s < 4; ++s) kstep(s, s, true, s == 0);
 #pragma unroll
-      for (int s = 0; s < 16; ++s) kstep(s, false, false);
+      for (int s = 0; s < 16; ++s) kstep(s, 4 + s, false, false);
     } else {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) kstep(s, false, s == 0);
+      for (int s = 0; s < 16; ++s) kstep(s, s, false, s == 0);
     }
     epi1(L);
     __syncthreads();
