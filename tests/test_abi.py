@@ -2,6 +2,8 @@
 import os
 import re
 
+import pytest
+
 from conftest import REPO
 
 
@@ -56,3 +58,17 @@ def test_state_dict_keys_match_reference_layout():
     from nof.networks import NOF_coarse
     keys = set(NOF_coarse().state_dict())
     assert keys == set(syn.init_nof_params(0))
+
+
+def test_math_switches_without_gpu():
+    """pcnerf_set_train_math / pcnerf_set_eval_math: process-wide selectors, previous mode returned, invalid modes
+    refused with a message (no GPU call involved)."""
+    from nof import _ops, _hip
+    assert _ops.get_train_math() == "f16x2_3" and _ops.get_eval_math() == "f16x2_3"
+    assert _ops.set_eval_math("fp32") == "f16x2_3"
+    assert _ops.set_eval_math("f16x2_3") == "fp32"
+    assert _hip.lib().pcnerf_set_eval_math(7) == -1
+    assert b"eval_math" in _hip.lib().pcnerf_last_error()
+    with pytest.raises(ValueError):
+        _ops.set_eval_math("bf16")
+    assert _ops.get_eval_math() == "f16x2_3"
