@@ -107,6 +107,15 @@ namespace pcn {
 #ifndef PCN_H1I_EPI
 #define PCN_H1I_EPI 8   // ... its BatchNorm + split at W1 k-steps EPI .. EPI + 3
 #endif
+#ifndef PCN_H64
+#define PCN_H64 0       // hidden split layers as k_train_h64 (4 waves of 64 neurons, one wave per SIMD)
+#endif
+#ifndef PCN_H64_LOAD
+#define PCN_H64_LOAD 1
+#endif
+#ifndef PCN_H64_STAGE
+#define PCN_H64_STAGE 10
+#endif
 #ifndef PCN_H16
 #define PCN_H16 0       // hidden split layers as k_train_h16 (16 waves of 16 neurons, four waves per SIMD)
 #endif
@@ -1363,6 +1372,161 @@ __global__ __launch_bounds__(1024, 1) void k_train_h16(const float* __restrict__
   }
 }
 
+// ---- k_train_h64<NT>: the hidden split layer with 4 waves of 64 neurons (one wave per SIMD): wave b holds the
+// hi/mid weights of out-blocks 2b, 2b+1 (256 registers, k_pack_train_h's image) and runs two accumulators, so each
+// B fragment read from LDS feeds 6 products instead of 3 -- the CU's LDS B-tile reads halve (128 KiB per tile).
+// Same tiles, layouts, scales, statistics, reversed walks and in-place buffer as k_train_h<0,true,NT>.
+template <int NT>
+__global__ __launch_bounds__(256, 1) void k_train_h64(const float* __restrict__ hin, int64_t n,
+                                                     const f16x8* __restrict__ Wp, const int* __restrict__ swp,
+                                                     int layer, const float* __restrict__ bias, BnPrev prev,
+                                                     float momentum, float eps, float* __restrict__ hout,
+                                                     double* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) float al[256];
+  __shared__ __attribute__((aligned(16))) float be[256];
+  __shared__ __attribute__((aligned(16))) float bs[256];
+  __shared__ float smax[4];
+  __shared__ f16x8 xs[2][KS_H][2][64];
+  const int t = threadIdx.x;
+  bn_coeffs(prev, n, momentum, eps, al, be);
+  bs[t] = bias[t];
+  int sx;
+  {
+    float bnd = sqrtf((float)n) * fabsf(prev.gamma[t]) + fabsf(prev.beta[t]);
+    bnd = wave_max_f(bnd);
+    if ((t & 63) == 0) smax[t >> 6] = bnd;
+    __syncthreads();
+    const float m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
+    sx = sx > 24 ? 24 : sx;
+    al[t] = ldexpf(al[t], sx);
+    be[t] = ldexpf(be[t], sx);
+  }
+  const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
+  const int nt = (int)((n + 31) / 32);
+  const int gstride = (int)gridDim.x;
+  const bool rev = (layer >> 8) & 1;
+  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
+  const int lane = t & 63, h = lane >> 5, li = lane & 31;
+  const int wb = __builtin_amdgcn_readfirstlane(t >> 6);
+  f16x8 wr[2][KS_H][2];
+#pragma unroll
+  for (int o = 0; o < 2; ++o)
+#pragma unroll
+    for (int ks = 0; ks < KS_H; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) wr[o][ks][p] = Wp[((ks * 8 + 2 * wb + o) * 2 + p) * 64 + lane];
+  f32x4 rs[2][8];   // [o][2j + moment]
+#pragma unroll
+  for (int o = 0; o < 2; ++o)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) rs[o][c] = f32x4{};
+  // staging: thread t owns the tile's float4s t + 256 m (m = 0..7): group g = u >> 6, HBM lane u & 63
+  auto load_tile = [&](f32x4 (&v)[8], int tile) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)P(tile) * TILE_FLOATS)[t + 256 * m];
+  };
+  auto stage = [&](int b, const f32x4 (&v)[8], int m0, int m1) {
+#pragma unroll
+    for (int m = m0; m < m1; ++m) {
+      const int g = (t >> 6) + 4 * m;   // feature group (features 8g + 4h .. + 3 of lane t & 63)
+      const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
+      f32x4 x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + c[q];
+      f16x4 hi, mid;
+      split4(x, hi, mid);
+      const int ln = li + 32 * (g & 1);
+      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][g >> 1][0][ln]) + 4 * h) = hi;
+      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][g >> 1][1][ln]) + 4 * h) = mid;
+    }
+  };
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  if (tl < nt) {
+    f32x4 v[8];
+    load_tile(v, tl);
+    stage(0, v, 0, 8);
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);
+  int buf = 0;
+  while (tl < nt) {
+    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
+    const bool more = nxt < nt;
+    f32x4 vl[8];
+    f32x16 acc[2];
+    f16x8 xr[2][2];
+    xr[0][0] = xs[buf][0][0][lane];
+    xr[0][1] = xs[buf][0][1][lane];
+#pragma unroll
+    for (int ks = 0; ks < KS_H; ++ks) {
+      if (ks + 1 < KS_H) {
+        xr[(ks + 1) & 1][0] = xs[buf][ks + 1][0][lane];
+        xr[(ks + 1) & 1][1] = xs[buf][ks + 1][1][lane];
+      }
+      const f16x8 xh = xr[ks & 1][0], xm = xr[ks & 1][1];
+      if (ks == PCN_H64_LOAD && more) load_tile(vl, nxt);
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+        acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[o][ks][0], xh, ks == 0 ? f32x16{} : acc[o], 0, 0, 0);
+#pragma unroll
+      for (int o = 0; o < 2; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[o][ks][0], xm, acc[o], 0, 0, 0);
+#pragma unroll
+      for (int o = 0; o < 2; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[o][ks][1], xh, acc[o], 0, 0, 0);
+      if (NT == 4) {
+#pragma unroll
+        for (int o = 0; o < 2; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[o][ks][1], xm, acc[o], 0, 0, 0);
+      }
+      if (more && ks >= PCN_H64_STAGE && ks < PCN_H64_STAGE + 4) {
+        const int k0 = ks - PCN_H64_STAGE;
+        stage(buf ^ 1, vl, 2 * k0, 2 * k0 + 2);
+      }
+    }
+    {   // epilogue: + bias, statistics, stores straight from the accumulators (as k_train_h)
+      const int tile = P(tl);
+      const bool valid = (int64_t)tile * 32 + li < n;
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+        const int ob = 2 * wb + o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * ob + 8 * j + 4 * h);
+          f32x4 ov;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float d = acc[o][4 * j + q] * unscale;
+            ov[q] = d + bj[q];
+            const float dv = valid ? d : 0.0f;
+            rs[o][2 * j][q] += dv;
+            rs[o][2 * j + 1][q] += dv * dv;
+          }
+          reinterpret_cast<f32x4*>(hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * ob + j) * 256)[lane] = ov;
+        }
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+    tl = nxt;
+  }
+  // per neuron: reduce the 32 lanes of a half wave (the samples) in float64, one atomic per (neuron, moment)
+#pragma unroll
+  for (int o = 0; o < 2; ++o)
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double a = (double)rs[o][c][q];
+#pragma unroll
+        for (int sh = 1; sh < 32; sh <<= 1) a += __shfl_xor(a, sh, 64);
+        if (li == 0) {
+          const int j = c >> 1, mo = c & 1;
+          const int nn = 32 * (2 * wb + o) + 8 * j + 4 * h + q;
+          atomicAdd(&stats[2 * nn + mo], a);
+        }
+      }
+}
+
 // ---- layer 0 from the encoding's moments (split forward without activation store, k_train_h1 after it).
 // Layer 0's only remaining outputs there are the chunk's encoding tiles and BatchNorm 0's statistics, and those
 // statistics are exact functions of the chunk's encoding mean ebar and covariance Sigma (h0 = W0 e + b0 feeds
@@ -2095,7 +2259,15 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
         const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};
-        if (PCN_H16 && g_train_math != 0) {
+        if (PCN_H64 && g_train_math != 0) {
+          const f16x8* wl = ws.wh + off_h(L, false);
+          if (g_train_math == 1)
+            hipLaunchKernelGGL(k_train_h64<3>, dim3(gws), dim3(256), 0, s, hin, n, wl, ws.sw,
+                               L | (tile_rev(L) << 8), P.lin_b[L], prev, momentum, eps, hout, stats + 512 * L);
+          else
+            hipLaunchKernelGGL(k_train_h64<4>, dim3(gws), dim3(256), 0, s, hin, n, wl, ws.sw,
+                               L | (tile_rev(L) << 8), P.lin_b[L], prev, momentum, eps, hout, stats + 512 * L);
+        } else if (PCN_H16 && g_train_math != 0) {
           const f16x8* w16 = ws.wh16 + (size_t)(L - 1) * H16_LAYER_VECS;
           if (g_train_math == 1)
             hipLaunchKernelGGL(k_train_h16<3>, dim3(gws), dim3(1024), 0, s, hin, n, w16, ws.sw,
