@@ -1,4 +1,5 @@
+# the val and training-step profiles at this commit (the training step on 16,384 rays: the same full chunks)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-VB_BWD=0 VB_RAYS=32768 timeout -k 10 300 python scripts/variant_bench.py > gpurun_out/vb_ts.json 2> gpurun_out/vb_ts.err
-echo vb rc=$?
+bash scripts/profile.sh r02k_val --mode val --steps 3 --warmup 1 && bash scripts/profile.sh r02k_train_step --mode train_step --rays 16384 --steps 2 --warmup 1
+echo rc=$?
