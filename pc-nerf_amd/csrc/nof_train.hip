@@ -1622,14 +1622,24 @@ __global__ __launch_bounds__(256, 2) void k_enc_gram(const float* __restrict__ r
         for (int h = 0; h < 2; ++h)
           dst[g * 64 + 32 * h] = f32x4{f[8 * g + 4 * h], f[8 * g + 4 * h + 1], f[8 * g + 4 * h + 2], f[8 * g + 4 * h + 3]};
     }
+    // fp16 range: a unit whose largest |d| reaches 2^15 (positions spread over more than 32 km) is split at 2^-ks,
+    // the count column included, and its products rescaled by 2^(2 ks) in float64 (exact powers of two; ks = 0 for
+    // every realistic scene, so the common path is unchanged)
+    float dm = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 63; ++k) dm = fmaxf(dm, ok ? fabsf(f[k] - sh0[k]) : 0.0f);
+    dm = wave_max_f(dm);
+    int ks = (dm >= 32768.0f && dm < 3.0e38f) ? ilogbf(dm) - 14 : 0;
+    ks = ks > 24 ? 24 : ks;
+    const float dsc = ldexpf(1.0f, -ks);
 #pragma unroll
     for (int k = 0; k < 63; ++k) {
-      const float d = ok ? f[k] - sh0[k] : 0.0f;
+      const float d = ok ? (f[k] - sh0[k]) * dsc : 0.0f;
       const _Float16 a = (_Float16)d;
       hi[k * GR_P + lane] = a;
       mi[k * GR_P + lane] = (_Float16)(d - (float)a);
     }
-    hi[63 * GR_P + lane] = ok ? (_Float16)1.0f : (_Float16)0.0f;
+    hi[63 * GR_P + lane] = ok ? (_Float16)dsc : (_Float16)0.0f;
     mi[63 * GR_P + lane] = (_Float16)0.0f;
     gram_lds_sync();
 #pragma unroll
@@ -1649,11 +1659,12 @@ __global__ __launch_bounds__(256, 2) void k_enc_gram(const float* __restrict__ r
       a01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m0, h1, a01, 0, 0, 0);
       a11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m1, h1, a11, 0, 0, 0);
     }
+    const double usc = ldexp(1.0, 2 * ks);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      d00[r] += (double)a00[r];
-      d01[r] += (double)a01[r];
-      d11[r] += (double)a11[r];
+      d00[r] += (double)a00[r] * usc;
+      d01[r] += (double)a01[r] * usc;
+      d11[r] += (double)a11[r] * usc;
       a00[r] = a01[r] = a11[r] = 0.0f;
     }
     gram_lds_sync();

@@ -74,6 +74,25 @@ def test_nof_train_forward_chunks_and_running_stats(train_math):
     assert int(mc.norms()[0].num_batches_tracked) == -(-len(x) // c)
 
 
+def test_nof_train_forward_far_positions(train_math):
+    """Train-mode NOF.forward on embeddings whose position features spread over 80 km (|e - e0| > 2^15): the
+    split forward's layer-0 moments (k_enc_gram) take their per-unit power-of-two range guard.  Against the float64
+    oracle forward of the same parameters (p within 1e-4, running statistics within 1e-4)."""
+    from oracle import ref_cpu as O
+    gen = torch.Generator().manual_seed(11)
+    e = torch.rand(6000, 63, generator=gen) * 2 - 1
+    e[:, :3] = (torch.rand(6000, 3, generator=gen) * 2 - 1) * 4.0e4
+    _, mc, _ = models(True)
+    with torch.no_grad():
+        p = mc(e.to(DEV))
+    P = {k: v.double() if v.is_floating_point() else v.clone() for k, v in
+         O.params_from_numpy(syn.init_nof_params(SEED_C)).items()}
+    ref = O.nof_forward(P, e.double(), True)
+    close(p, ref.squeeze(-1).numpy() if p.dim() == 1 else ref.numpy(), 1e-4, 1e-6, "p far positions")
+    rs = np.stack([np.stack([P[b + ".running_mean"].numpy(), P[b + ".running_var"].numpy()]) for b in O.BN])
+    close(running(mc), rs, 1e-4, 1e-6, "running stats far positions")
+
+
 def knife_edge(bins, weights, u):
     """Samples whose bin has cdf_hi - cdf_lo within 4 ulp of the reference's 1e-5 threshold (render.py:408): there
     the branch depends on the last bit of the normaliser sum, whose order torch CPU fixes per ISA."""
