@@ -1,4 +1,4 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash scripts/gpu_tests.sh
+timeout -k 10 300 python bench.py > gpurun_out/bench_last.json 2> gpurun_out/bench_last.err
 echo rc=$?
