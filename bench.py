@@ -400,7 +400,8 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
-        "dtype": "fp32",   # every tensor and every accumulation; see train_math for the Linear layers' products
+        # every tensor and every accumulation is fp32; the Linear layers' products as the selected math forms them
+        "dtype": dtype_label(train_math, eval_math, a.fold),
         "data": {2: "synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)",
                  3: "KITTI-00 fixture scene (scans 1151-1156, every 40th point) rays built by nof.dataset, "
                     "262,144-ray batches drawn with replacement; seeded NOF weights",
@@ -440,21 +441,35 @@ def main(argv=None):
         tdist.destroy_process_group()
 
 
+def dtype_label(train_math, eval_math, fold=False):
+    """The arithmetic of the path: fp32 tensors and accumulation, and how the Linear layers' fp32 products are
+    formed (DESIGN.md 'The split train math')."""
+    split = "fp32 (Linear products: fp16 hi/mid split, {} MFMA products, fp32 accumulate)"
+    if train_math in ("f16x2_3", "f16x2_3_fused") or (train_math is None and eval_math == "f16x2_3"):
+        return split.format(3)
+    if train_math == "f16x2_4":
+        return split.format(4)
+    if fold:
+        return "fp32 (float64 {}layer algebra + float64 63-term dot per sample)".format(
+            "per-chunk " if train_math == "fold" else "")
+    return "fp32 (fp32 MFMA)"
+
+
 # ----------------------------------------------------------------------------------------------- roofline
 FP16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense BF16/FP16 MFMA
 
 
 def kernel_report(L, a, train_math, eval_math=None):
     """Kernel breakdown of the last timed step (library HIP events) and the dominant kernel's roofline."""
-    split = train_math in ("f16x2_3", "f16x2_4")
+    split = train_math in ("f16x2_3", "f16x2_4", "f16x2_3_fused")
     esplit = eval_math == "f16x2_3"
-    nterm = 3 if (train_math == "f16x2_3" or esplit) else 4
+    nterm = 3 if (train_math in ("f16x2_3", "f16x2_3_fused") or esplit) else 4
     hid = f"k_train_h<0,true,{nterm}>" if split else "k_train_ws<0,true>"
     knames = {0: "k_nof_eval_h2" if esplit else "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
               3: f"k_train_h<8,true,{nterm}>" if split else "k_train_ws<8,true>",
               10: "k_wgrad<2>+k_wgrad<1>" if split else "k_wgrad<0>", 11: f"k_dgrad_h<{nterm}>" if split else "k_dgrad_ws",
               13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>",
-              16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw"}
+              16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw", 18: "k_nof_eval_h2<true>"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
@@ -463,7 +478,7 @@ def kernel_report(L, a, train_math, eval_math=None):
     for t, nm in ((0, "eval_query"), (1, "train_hidden"), (2, "train_first"), (3, "train_skip"), (4, "train_out"),
                   (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
                   (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold"), (14, "wgrad_b3"),
-                  (15, "train_h1"), (16, "fold_moments"), (17, "fold_algebra")):
+                  (15, "train_h1"), (16, "fold_moments"), (17, "fold_algebra"), (18, "train_query")):
         tm, n, f, b = prof_read(L, t)
         if n:
             tr, src = pmc_traffic(pmc_names.get(t, ""))
@@ -486,8 +501,9 @@ def kernel_report(L, a, train_math, eval_math=None):
                          "gradient-moment passes; the per-chunk layer algebra is float64 MFMA); HBM fraction "
                          "reported as the contract asks") if a.mode in ("train_fwd", "train_step") else
                         "VALU-bound (60 sincosf per sample); HBM fraction reported as the contract asks"}
-    elif esplit and tag == 0:
-        # split-fp16 eval network: nterm fp16 MFMA products per fp32 product, weights streamed through LDS
+    elif (esplit and tag == 0) or tag == 18:
+        # split-fp16 fused network (eval query, or the train-mode query with per-chunk BatchNorm coefficients):
+        # nterm fp16 MFMA products per fp32 product, weights streamed from L2
         roof = {"kernel": kname, "bound": "mfma", "achieved": round(nprod * achieved, 1), "peak": FP16_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(nprod * achieved / FP16_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                 "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1),

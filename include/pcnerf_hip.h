@@ -162,6 +162,20 @@ int pcnerf_nof_query_train_fold_backward(const float* rays, int64_t n_rays, int 
                                          int n_samples, int64_t chunk, const pcnerf_nof_params* params, float eps,
                                          const float* grad_logit, void* state, size_t state_bytes,
                                          const pcnerf_nof_grads* grads, void* stream);
+/* ---------------------------------------------------------------- train-mode query without activations
+ * The render+loss forward's train-mode query (render.py:38-50 chunk loop over models.py:183-203 with BatchNorm batch
+ * statistics per chunk; replaces the layer-by-layer pcnerf_nof_query_train where no backward needs the layer
+ * outputs).  The network is evaluated AS WRITTEN, per sample, in one fused kernel (the 9 Linear layers on split-fp16
+ * products, BatchNorm applied in each layer's epilogue); only the chunk statistics it needs come from the chunk's
+ * encoding moments through the float64 layer algebra above -- exact because every LeakyReLU(True) is the identity
+ * (negative_slope = 1, models.py:72,92).  Running stats are updated chunk by chunk as nn.BatchNorm1d does.  `state`:
+ * pcnerf_nof_train_fold_bytes(total_samples, chunk) bytes of scratch. */
+int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
+                                 int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
+                                 void* state, size_t state_bytes, float* p_out, void* stream);
+/* NOF.forward(emb) in train mode on an embedded batch of n rows (one chunk), the same way. */
+int pcnerf_nof_forward_train_fused(const float* emb, int64_t n, const pcnerf_nof_params* params, float momentum,
+                                   float eps, void* state, size_t state_bytes, float* p_out, void* stream);
 /* NOF.forward(emb) through the fold (one chunk of n rows); grad_p = dL/dp of its output p. */
 int pcnerf_nof_forward_train_fold_backward(const float* emb, int64_t n, const pcnerf_nof_params* params, float eps,
                                            const float* p, const float* grad_p, void* state, size_t state_bytes,

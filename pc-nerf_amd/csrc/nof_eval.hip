@@ -11,6 +11,8 @@
 // so accumulator register R = 16*ob + r of a layer IS the B operand of k-step t = R of the next layer
 // (feature map FEAT_H below): the whole chain runs without LDS or lane shuffles.  The encoding feeds layer 1
 // (and the skip half of layer 5) with feature(t, h) = 2t + h.
+#include <algorithm>
+
 #include "common.h"
 #include "pcnerf_internal.h"
 #include "prof.h"
@@ -199,14 +201,16 @@ __global__ __launch_bounds__(256) void k_nof_eval(const float* __restrict__ rays
 // 16 s + 8 (j>>2) + 4 h + (j&3) for the 256 hidden features -- exactly accumulator registers 8 (s&1) + j of
 // block s>>1 of the previous layer, so each layer's B operands are its predecessor's accumulators split in place.
 
-// per-layer weight scale exponents of the BatchNorm-folded weights, stored in the image as int32
+// per-layer weight scale exponents of the BatchNorm-folded weights (RAW: of the raw weights, for the train-mode
+// query), stored in the image as int32
+template <bool RAW>
 __global__ __launch_bounds__(256) void k_eval_wscale(NofParamsDev P, float* __restrict__ out) {
   const int L = blockIdx.x;
   const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
   float m = 0.0f;
   for (int i = threadIdx.x; i < 256 * in_f; i += 256) {
     const int n = i / in_f;
-    const float alpha = (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
+    const float alpha = RAW ? 1.0f : (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
     m = fmaxf(m, fabsf(alpha * P.lin_w[L][i]));
   }
   m = wave_max_f(m);
@@ -236,6 +240,7 @@ typedef _Float16 eh_f16x8 __attribute__((ext_vector_type(8)));
 #define PCN_EH_KPB 1   // k_nof_eval_h: k-steps per weight super-slice (one barrier each)
 #endif
 
+template <bool RAW>
 __global__ void k_pack_eval_h(NofParamsDev P, float* __restrict__ out) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= EH_VECS) return;
@@ -248,7 +253,7 @@ __global__ void k_pack_eval_h(NofParamsDev P, float* __restrict__ out) {
   const int s = L == 4 && !epart ? s0 - 4 : s0;
   const int n = 32 * ob + (lane & 31), h = lane >> 5;
   const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
-  const float alpha = (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
+  const float alpha = RAW ? 1.0f : (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
   const float sc = ldexpf(1.0f, reinterpret_cast<const int*>(out + OFF_EH_SW)[L]);
   eh_f16x8 v;
 #pragma unroll
@@ -482,19 +487,31 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__
 #define PCN_EH2_T 3
 #endif
 constexpr int E2_T = PCN_EH2_T;   // sample tiles per block
+// TR (the train-mode query, pcnerf_nof_query_train_fused): the image holds the RAW weights (no BatchNorm fold) and
+// each layer's epilogue applies its chunk's BatchNorm as (acc 2^-(sw+sx)) alpha + beta'' -- alpha = fl32(invstd)
+// gamma and beta'' = beta - mean(W x) alpha from the chunk's batch statistics (coef[chunk][L][alpha 256 | beta''
+// 256], nof_fold.hip k_tf_coeffs); blockIdx.y is the BatchNorm chunk, blockIdx.x the 96-sample block inside it, so
+// no block straddles two chunks.
+template <bool TR>
 __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict__ rays, int stride,
                                                         const float* __restrict__ z, int64_t total, int S,
                                                         const float* __restrict__ ein, const float* __restrict__ W,
-                                                        float* __restrict__ p_out) {
+                                                        float* __restrict__ p_out, const float* __restrict__ coef,
+                                                        int64_t chunk) {
   __shared__ eh_f16x8 act[16][E2_T][2][64];
   __shared__ eh_f16x8 eb[4][E2_T][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
   __shared__ int sx0s[E2_T * 32];
-  __shared__ __attribute__((aligned(16))) float sbias[8 * 256];
+  // eval: the 8 layers' folded biases; TR: the chunk's [L][alpha | beta''] BatchNorm coefficients
+  __shared__ __attribute__((aligned(16))) float sbias[(TR ? 16 : 8) * 256];
   __shared__ float emax[E2_T * 32];
   __shared__ float smax[4][E2_T * 32];
   __shared__ float pdot[4][E2_T * 32];
   const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, h = lane >> 5, li = lane & 31;
-  const int64_t s0 = (int64_t)blockIdx.x * (32 * E2_T);
+  // samples [s0, send) of this block
+  const int64_t cb = TR ? (int64_t)blockIdx.y * chunk : 0;
+  const int64_t s0 = cb + (int64_t)blockIdx.x * (32 * E2_T);
+  const int64_t send = TR ? (cb + chunk < total ? cb + chunk : total) : total;
+  if (s0 >= send) return;   // (the last chunk's surplus blocks; uniform over the block, before any barrier)
   const eh_f16x8* __restrict__ img = reinterpret_cast<const eh_f16x8*>(W + OFF_EH);
   int sw[8];
 #pragma unroll
@@ -513,11 +530,16 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   load_w(wr4[0], 0);
   load_w(wr4[1], 1);
   load_w(wr4[2], 2);
-  for (int i = t; i < 8 * 256 / 4; i += 256)
-    reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
+  if (TR) {
+    const f32x4* cf = reinterpret_cast<const f32x4*>(coef + blockIdx.y * (size_t)(16 * 256));
+    for (int i = t; i < 16 * 256 / 4; i += 256) reinterpret_cast<f32x4*>(sbias)[i] = cf[i];
+  } else {
+    for (int i = t; i < 8 * 256 / 4; i += 256)
+      reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
+  }
   if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
     int64_t g = s0 + t;
-    if (g >= total) g = total - 1;
+    if (g >= send) g = send - 1;
     float f[64];
     if (ein) {
 #pragma unroll
@@ -607,7 +629,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
         acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
     ++gk;
   };
-  // epilogue phase 1: acc <- acc 2^-(sw + sx) + bias, this wave's per-sample maxima -> smax[w]
+  // epilogue phase 1: acc <- acc 2^-(sw + sx) + bias (TR: (acc 2^-(sw + sx)) alpha + beta''), this wave's
+  // per-sample maxima -> smax[w]
   auto epi1 = [&](int L) {
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
@@ -617,10 +640,13 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       for (int o = 0; o < 2; ++o)
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + 256 * L + 32 * (2 * w + o) + 8 * gq + 4 * h);
+          const int nb = 32 * (2 * w + o) + 8 * gq + 4 * h;
+          const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + (TR ? 512 * L + 256 : 256 * L) + nb);
+          f32x4 a = {};
+          if (TR) a = *reinterpret_cast<const f32x4*>(sbias + 512 * L + nb);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float v = acc[o][tau][4 * gq + q] * us + b[q];
+            const float v = TR ? (acc[o][tau][4 * gq + q] * us) * a[q] + b[q] : acc[o][tau][4 * gq + q] * us + b[q];
             acc[o][tau][4 * gq + q] = v;
             m = fmaxf(m, fabsf(v));
           }
@@ -693,7 +719,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     if (h == 0) pdot[w][32 * tau + li] = part;
   }
   __syncthreads();
-  if (t < 32 * E2_T && s0 + t < total) {
+  if (t < 32 * E2_T && s0 + t < send) {
     const float logit = ((pdot[0][t] + pdot[1][t]) + (pdot[2][t] + pdot[3][t])) + W[OFF_BOUT];
     p_out[s0 + t] = sigmoid_ref(logit);
   }
@@ -706,8 +732,8 @@ static void launch_eval(const float* rays, int stride, const float* z, int64_t t
                         const float* W, float* p_out, hipStream_t s) {
   const int64_t blocks = ((total + 31) / 32 + 3) / 4;
   if (g_eval_math == 1 && PCN_EH2)
-    hipLaunchKernelGGL(k_nof_eval_h2, dim3((unsigned)((total + 32 * E2_T - 1) / (32 * E2_T))), dim3(256), 0, s, rays,
-                       stride, z, total, S, ein, W, p_out);
+    hipLaunchKernelGGL(k_nof_eval_h2<false>, dim3((unsigned)((total + 32 * E2_T - 1) / (32 * E2_T))), dim3(256), 0,
+                       s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0);
   else if (g_eval_math == 1)
     hipLaunchKernelGGL(k_nof_eval_h, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
                        p_out);
@@ -855,6 +881,25 @@ __global__ __launch_bounds__(256) void k_nof_eval_fold(const float* __restrict__
   p_out[g] = sigmoid_ref((float)acc);
 }
 
+// ---- the train-mode query (nof_fold.hip pcnerf_nof_query_train_fused): raw split weights + occ_out in the eval
+// image layout, then k_nof_eval_h2<true> with one BatchNorm coefficient set per chunk
+size_t train_query_image_floats() { return EVAL_FLOATS; }
+
+void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_eval_vectors, dim3(1), dim3(256), 0, s, P, img);   // (occ_out; biases unused)
+  hipLaunchKernelGGL(k_eval_wscale<true>, dim3(8), dim3(256), 0, s, P, img);
+  hipLaunchKernelGGL(k_pack_eval_h<true>, dim3((unsigned)((EH_VECS + 255) / 256)), dim3(256), 0, s, P, img);
+}
+
+void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
+                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s) {
+  const int64_t C = (total + chunk - 1) / chunk;
+  const int64_t per = (std::min(chunk, total) + 32 * E2_T - 1) / (32 * E2_T);
+  if (C >= 65536 || per >= ((int64_t)1 << 31)) throw std::runtime_error("train query: too many chunks / samples");
+  hipLaunchKernelGGL(k_nof_eval_h2<true>, dim3((unsigned)per, (unsigned)C), dim3(256), 0, s, rays, stride, z, total,
+                     S, ein, img, p_out, coef, chunk);
+}
+
 void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const double* fold, int64_t chunk, float* p_out, hipStream_t s) {
   const int64_t blocks = (total + 255) / 256;
@@ -936,8 +981,8 @@ extern "C" int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* pack
   const unsigned nb = (unsigned)((OFF_BIAS + 255) / 256);
   hipLaunchKernelGGL(k_pack_eval_weights, dim3(nb), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_pack_eval_vectors, dim3(1), dim3(256), 0, s, P, packed);
-  hipLaunchKernelGGL(k_eval_wscale, dim3(8), dim3(256), 0, s, P, packed);
-  hipLaunchKernelGGL(k_pack_eval_h, dim3((unsigned)((EH_VECS + 255) / 256)), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(k_eval_wscale<false>, dim3(8), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(k_pack_eval_h<false>, dim3((unsigned)((EH_VECS + 255) / 256)), dim3(256), 0, s, P, packed);
   PCN_LAUNCH_CHECK("pcnerf_nof_pack_eval");
   PCN_API_END
 }

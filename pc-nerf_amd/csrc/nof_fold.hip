@@ -57,12 +57,15 @@ struct FoldDev {   // device views of the fold state (float64 throughout)
   double* dg;      // [8][C][256] dgamma per chunk
   double* dw;      // [G][256][256] weight-gradient partials (h columns)
   double* vec;     // [C][576] d out_w (256), d beta_7 (256), d out_b (1)
+  float* coef;     // [C][8][alpha 256 | beta'' 256] the chunks' BatchNorm coefficients (train-mode query)
+  float* img;      // the train-mode query's weight image (train_query_image_floats)
 };
 
+constexpr int FOLD_PIECES = 15;
 struct FoldLayout {
   int64_t C;
   int wpc, G;
-  size_t off[13];
+  size_t off[FOLD_PIECES];
   size_t doubles;
 };
 
@@ -73,10 +76,11 @@ static FoldLayout fold_layout(int64_t total, int64_t chunk) {
   F.wpc = (int)std::max<int64_t>(1, std::min<int64_t>(TF_WPC_MAX, tiles / 64));
   F.G = (int)std::min<int64_t>(F.C, TF_G_MAX);
   const size_t C = (size_t)F.C, wpc = (size_t)F.wpc, G = (size_t)F.G;
-  const size_t n[13] = {C * wpc * 4096, C * 4096, C * 64, C * 64, 8 * C * 256 * 64, 8 * C * 256 * 64,
-                        8 * C * 1024, C * 64, C * wpc * 64, 2 * C * 256 * 64, 8 * C * 256, G * 256 * 256, C * 576};
+  const size_t n[FOLD_PIECES] = {C * wpc * 4096, C * 4096, C * 64, C * 64, 8 * C * 256 * 64, 8 * C * 256 * 64,
+                                 8 * C * 1024, C * 64, C * wpc * 64, 2 * C * 256 * 64, 8 * C * 256, G * 256 * 256,
+                                 C * 576, C * 8 * 512 / 2, (train_query_image_floats() + 1) / 2};
   size_t o = 0;
-  for (int i = 0; i < 13; ++i) {
+  for (int i = 0; i < FOLD_PIECES; ++i) {
     F.off[i] = o;
     o += (n[i] + 31) & ~(size_t)31;   // 256-byte aligned pieces
   }
@@ -92,6 +96,8 @@ static FoldDev fold_dev(const FoldLayout& L, void* state) {
   F.G = L.G;
   double** dst[13] = {&F.mom, &F.sig, &F.eb, &F.e0, &F.pp, &F.q, &F.sr, &F.fold, &F.gm, &F.ab, &F.dg, &F.dw, &F.vec};
   for (int i = 0; i < 13; ++i) *dst[i] = b + L.off[i];
+  F.coef = (float*)(b + L.off[13]);
+  F.img = (float*)(b + L.off[14]);
   return F;
 }
 
@@ -164,19 +170,34 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
   for (int64_t t = t0 + wave; t < t1; t += 4) {   // waves independent: wave-local LDS tiles
     const int64_t i = t * 64 + lane;
     const bool ok = i < n;
+    // fp16 range (k_enc_gram's guard): a tile whose largest |d| reaches 2^15 (positions spread over more than
+    // 32 km; the sin/cos features differ by at most 2) is split at 2^-sk, the count column included, and its
+    // products rescaled by 2^(2 sk) in float64 -- exact powers of two, sk = 0 for every realistic scene
+    const float* r = q.ein ? q.ein + (c0 + (ok ? i : 0)) * 63 : nullptr;
+    float p[3] = {0.0f, 0.0f, 0.0f};
+    float dm = 0.0f;
+    if (q.ein) {
+      if (ok)
+        for (int f = 0; f < 63; ++f) dm = fmaxf(dm, fabsf(r[f] - sh0[f]));
+    } else if (ok) {
+      sample_point(q.rays + ((c0 + i) / q.S) * q.stride, q.z[c0 + i], p);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) dm = fmaxf(dm, fabsf(p[m] - sh0[m]));
+    }
+    dm = wave_max_f(dm);
+    int sk = (dm >= 32768.0f && dm < 3.0e38f) ? ilogbf(dm) - 14 : 0;
+    sk = sk > 24 ? 24 : sk;
+    const float dsc = ldexpf(1.0f, -sk);
     auto put = [&](int f, float v) {
-      const float d = ok ? v - sh0[f] : 0.0f;
+      const float d = ok ? (v - sh0[f]) * dsc : 0.0f;
       const _Float16 h = (_Float16)d;
       hi[f * TM_P + lane] = h;
       mi[f * TM_P + lane] = (_Float16)(d - (float)h);
     };
     if (q.ein) {
-      const float* r = q.ein + (c0 + (ok ? i : 0)) * 63;
 #pragma unroll 7
       for (int f = 0; f < 63; ++f) put(f, r[f]);
     } else {
-      float p[3] = {0.0f, 0.0f, 0.0f};
-      if (ok) sample_point(q.rays + ((c0 + i) / q.S) * q.stride, q.z[c0 + i], p);
 #pragma unroll
       for (int m = 0; m < 3; ++m) put(m, p[m]);
 #pragma unroll 2
@@ -191,7 +212,7 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
         }
       }
     }
-    hi[63 * TM_P + lane] = ok ? (_Float16)1.0f : (_Float16)0.0f;
+    hi[63 * TM_P + lane] = ok ? (_Float16)dsc : (_Float16)0.0f;
     mi[63 * TM_P + lane] = (_Float16)0.0f;
     wave_lds_sync();
 #pragma unroll
@@ -211,11 +232,12 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
       a01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m0, h1, a01, 0, 0, 0);
       a11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(m1, h1, a11, 0, 0, 0);
     }
+    const double usc = ldexp(1.0, 2 * sk);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      d00[r] += (double)a00[r];
-      d01[r] += (double)a01[r];
-      d11[r] += (double)a11[r];
+      d00[r] += (double)a00[r] * usc;
+      d01[r] += (double)a01[r] * usc;
+      d11[r] += (double)a11[r] * usc;
       a00[r] = a01[r] = a11[r] = 0.0f;
     }
     wave_lds_sync();
@@ -434,6 +456,24 @@ __global__ __launch_bounds__(256) void k_tf_out(NofParamsDev P, FoldDev F) {
     const double t = wave_sum_d(a * F.eb[(int64_t)c * 64 + lane]);
     F.fold[(int64_t)c * 64 + lane] =
         lane < 63 ? a : ((cw[0] + cw[1]) + (cw[2] + cw[3])) + (double)P.out_b[0] - t;
+  }
+}
+
+// grid C, 256 threads: each chunk's BatchNorm coefficients for the train-mode query, bn_coeffs' (nof_train.hip)
+// arithmetic on the chunk's exact batch statistics: invstd = fl32(1 / sqrt(var + eps)) (biased variance), alpha =
+// invstd * gamma, and beta'' = beta - mean(W x) alpha with mean(W x) = P'[:, 63] -- the Linear's bias cancels
+// inside BatchNorm, so the query's epilogue is (W x) alpha + beta''.
+__global__ __launch_bounds__(256) void k_tf_coeffs(NofParamsDev P, FoldDev F) {
+  const int c = blockIdx.x, k = threadIdx.x;
+  const int64_t C = F.C;
+  for (int L = 0; L < 8; ++L) {
+    const double* sr = F.sr + ((int64_t)L * C + c) * 1024;
+    const double m = F.pp[(((int64_t)L * C + c) * 256 + k) * 64 + 63];
+    const float invstd = (float)(1.0 / sqrt(sr[768 + k] + (double)P.eps));
+    const float a = invstd * P.bn_w[L][k];
+    float* o = F.coef + ((int64_t)c * 8 + L) * 512;
+    o[k] = a;
+    o[256 + k] = (float)((double)P.bn_b[L][k] - m * (double)a);
   }
 }
 
@@ -730,6 +770,8 @@ static void launch_layer(const NofParamsDev& P, const FoldDev& F, double eps, hi
 static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, float momentum, float eps,
                          void* state, size_t state_bytes, float* p_out, hipStream_t s) {
   PCN_CHECK(q.total > 0 && q.chunk > 0, "train fold: empty input");
+  // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
+  PCN_CHECK(q.total % q.chunk != 1 && q.total != 1, "Expected more than 1 value per channel when training");
   const FoldLayout Lo = fold_layout(q.total, q.chunk);
   PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train fold: state buffer too small");
   PCN_CHECK(Lo.C < 65536, "train fold: too many chunks for one query");
@@ -763,6 +805,47 @@ static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, fl
   hipLaunchKernelGGL(k_tf_running, dim3(8), dim3(256), 0, s, P, F, q, (double)momentum);
 }
 
+// The train-mode query evaluated per sample (the network as written, one BatchNorm coefficient set per chunk):
+// the chunk statistics from the encoding moments and the float64 layer algebra above, then k_nof_eval_h2<true>.
+static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, float momentum, float eps,
+                          void* state, size_t state_bytes, float* p_out, hipStream_t s) {
+  PCN_CHECK(q.total > 0 && q.chunk > 0, "train query: empty input");
+  // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
+  PCN_CHECK(q.total % q.chunk != 1 && q.total != 1, "Expected more than 1 value per channel when training");
+  const FoldLayout Lo = fold_layout(q.total, q.chunk);
+  PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train query: state buffer too small");
+  PCN_CHECK(Lo.C < 65536, "train query: too many chunks for one query");
+  NofParamsDev P;
+  PCN_CHECK(to_dev_params(params, eps, &P), "train query: null parameter pointer");
+  const FoldDev F = fold_dev(Lo, state);
+  const double ep = (double)eps;
+  pack_train_query(P, F.img, s);
+  {
+    ProfScope ps(s, PT_FOLD_MOMENTS, 6144.0 * (double)q.total, 4.0 * (double)q.total);
+    hipLaunchKernelGGL(k_tf_moments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F);
+  }
+  {
+    ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
+    if (F.wpc > 1) hipLaunchKernelGGL(k_tf_msum, dim3(16, (unsigned)F.C), dim3(256), 0, s, F);
+    hipLaunchKernelGGL(k_tf_stats, dim3((unsigned)F.C), dim3(256), 0, s, F);
+    launch_layer<0>(P, F, ep, s);
+    launch_layer<1>(P, F, ep, s);
+    launch_layer<2>(P, F, ep, s);
+    launch_layer<3>(P, F, ep, s);
+    launch_layer<4>(P, F, ep, s);
+    launch_layer<5>(P, F, ep, s);
+    launch_layer<6>(P, F, ep, s);
+    launch_layer<7>(P, F, ep, s);
+    hipLaunchKernelGGL(k_tf_coeffs, dim3((unsigned)F.C), dim3(256), 0, s, P, F);
+  }
+  {
+    // algorithmic work: 982,528 FLOP per sample (9 Linear layers); bytes: z in, p out, ray rows
+    ProfScope ps(s, PT_TRAIN_QUERY, 982528.0 * (double)q.total, 8.0 * (double)q.total);
+    launch_train_query(q.rays, q.stride, q.z, q.total, q.S, q.ein, F.img, F.coef, q.chunk, p_out, s);
+  }
+  hipLaunchKernelGGL(k_tf_running, dim3(8), dim3(256), 0, s, P, F, q, (double)momentum);
+}
+
 template <int L>
 static void backward_layer(const NofParamsDev& P, const FoldDev& F, const pcnerf_nof_grads* G, hipStream_t s) {
   if constexpr (L > 0) hipLaunchKernelGGL(k_tf_dw<L>, dim3(16, F.G), dim3(256), 0, s, F);
@@ -774,6 +857,7 @@ static void fold_backward(const SampleSrc& q, const pcnerf_nof_params* params, f
                           const float* p, void* state, size_t state_bytes, const pcnerf_nof_grads* G,
                           hipStream_t s) {
   PCN_CHECK(q.total > 0 && q.chunk > 0, "train fold backward: empty input");
+  PCN_CHECK(q.total % q.chunk != 1 && q.total != 1, "Expected more than 1 value per channel when training");
   const FoldLayout Lo = fold_layout(q.total, q.chunk);
   PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train fold backward: state buffer too small");
   NofParamsDev P;
@@ -803,6 +887,33 @@ using namespace pcn;
 extern "C" size_t pcnerf_nof_train_fold_bytes(int64_t total_samples, int64_t chunk) {
   if (total_samples <= 0 || chunk <= 0) return 0;
   return fold_layout(total_samples, std::min(chunk, total_samples)).doubles * sizeof(double);
+}
+
+extern "C" int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                            int n_samples, int64_t chunk, const pcnerf_nof_params* params,
+                                            float momentum, float eps, void* state, size_t state_bytes, float* p_out,
+                                            void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && state && p_out, "pcnerf_nof_query_train_fused: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_fused: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_fused: ray_stride < 6");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  const SampleSrc q{rays, ray_stride, z, n_samples, nullptr, total, std::min(chunk, total)};
+  fused_forward(q, params, momentum, eps, state, state_bytes, p_out, (hipStream_t)stream);
+  PCN_LAUNCH_CHECK("pcnerf_nof_query_train_fused");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_forward_train_fused(const float* emb, int64_t n, const pcnerf_nof_params* params,
+                                              float momentum, float eps, void* state, size_t state_bytes,
+                                              float* p_out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(emb && params && state && p_out, "pcnerf_nof_forward_train_fused: null argument");
+  PCN_CHECK(n > 1, "pcnerf_nof_forward_train_fused: Expected more than 1 value per channel when training");
+  const SampleSrc q{nullptr, 0, nullptr, 1, emb, n, n};
+  fused_forward(q, params, momentum, eps, state, state_bytes, p_out, (hipStream_t)stream);
+  PCN_LAUNCH_CHECK("pcnerf_nof_forward_train_fused");
+  PCN_API_END
 }
 
 extern "C" int pcnerf_nof_query_train_fold(const float* rays, int64_t n_rays, int ray_stride, const float* z,

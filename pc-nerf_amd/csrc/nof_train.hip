@@ -32,9 +32,6 @@ namespace pcn {
 #ifndef PCN_WS_XD
 #define PCN_WS_XD 4  // k_train_ws / k_dgrad_ws: LDS read ring depth in k-groups
 #endif
-#ifndef PCN_OSTAT1
-#define PCN_OSTAT1 1  // output-layer backward statistics in one pass (k_out_bwd_stats1) instead of four
-#endif
 #ifndef PCN_S12_COPIES
 #define PCN_S12_COPIES 8  // k_wgrad_reduce: copies of the BatchNorm-backward sums (block m adds to copy m % COPIES)
 #endif
@@ -59,18 +56,6 @@ namespace pcn {
 #ifndef PCN_H_PRIO
 #define PCN_H_PRIO 1
 #endif
-#ifndef PCN_H_LMAP
-#define PCN_H_LMAP 0   // staging lane map (conflict-free 8-byte LDS writes)
-#endif
-#ifndef PCN_H_RING4
-#define PCN_H_RING4 0   // hidden layers: four B buffers, staging two tiles ahead, a barrier every second tile (no gain)
-#endif
-#ifndef PCN_H_WLDS
-#define PCN_H_WLDS 0  // hidden layers: k-steps of weights read from LDS instead of registers
-#endif
-#ifndef PCN_H_ABL
-#define PCN_H_ABL 0   // timing-only ablations of the hidden layer: 1 no stores, 2 no loads, 4 no staging, 8 no barrier
-#endif
 #ifndef PCN_H1
 #define PCN_H1 1      // forward without activation store: layer 1 recomputes h0 from the encoding tiles
 #endif
@@ -80,50 +65,11 @@ namespace pcn {
 #ifndef PCN_H_REGSTAT
 #define PCN_H_REGSTAT 1  // hidden layers: running statistics in registers, epilogue after each tile's MFMAs
 #endif
-#ifndef PCN_H_DMA
-#define PCN_H_DMA 0  // hidden layers: k_train_hd (raw tiles by LDS-DMA two tiles ahead)
-#endif
-#ifndef PCN_REV_OWN
-#define PCN_REV_OWN 0   // reversed layers walk each workgroup's own tiles backwards (else the chunk's)
-#endif
 #ifndef PCN_INPLACE
 #define PCN_INPLACE 1   // split forward without store: layers overwrite their input buffer (one activation buffer)
 #endif
-#ifndef PCN_XFOLD
-#define PCN_XFOLD 1     // the staging's 2^sx folded into the BatchNorm coefficients (bit-identical)
-#endif
-#ifndef PCN_H_NT
-#define PCN_H_NT 0      // split layers: 1 nontemporal activation loads, 2 nontemporal output stores
-#endif
-#ifndef PCN_H1I
-#define PCN_H1I 0       // k_train_h1: the next tile's W0 products inside the W1 k-loop (second accumulator set)
-#endif
 #ifndef PCN_H1_XD
 #define PCN_H1_XD PCN_H_XD   // k_train_h1's B-operand read ring depth
-#endif
-#ifndef PCN_H1I_AT
-#define PCN_H1I_AT 1    // ... at W1 k-steps AT .. AT + 3
-#endif
-#ifndef PCN_H1I_EPI
-#define PCN_H1I_EPI 8   // ... its BatchNorm + split at W1 k-steps EPI .. EPI + 3
-#endif
-#ifndef PCN_H64
-#define PCN_H64 0       // hidden split layers as k_train_h64 (4 waves of 64 neurons, one wave per SIMD)
-#endif
-#ifndef PCN_H64_LOAD
-#define PCN_H64_LOAD 1
-#endif
-#ifndef PCN_H64_STAGE
-#define PCN_H64_STAGE 10
-#endif
-#ifndef PCN_H16
-#define PCN_H16 0       // hidden split layers as k_train_h16 (16 waves of 16 neurons, four waves per SIMD)
-#endif
-#ifndef PCN_H16_LOAD
-#define PCN_H16_LOAD 0  // ... k-step of the next tile's raw loads
-#endif
-#ifndef PCN_H16_STAGE
-#define PCN_H16_STAGE 6 // ... k-step of its staging
 #endif
 #ifndef PCN_GRAM
 #define PCN_GRAM 1    // with PCN_H1: layer 0 as the encoding's moments (k_enc_gram) instead of its 256-neuron product
@@ -603,12 +549,14 @@ __device__ __forceinline__ void split4(const f32x4& x, f16x4& hi, f16x4& mid) {
 }
 
 template <int KE, bool HP, int NT>
+// hin / hout are NOT restrict-qualified: the split forward without activation store runs every layer in place
+// (hin == hout, query_train's PCN_INPLACE)
 __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ rays, int stride,
                                                     const float* __restrict__ z, int S, int64_t c0,
-                                                    const float* __restrict__ ein, const float* __restrict__ hin,
+                                                    const float* __restrict__ ein, const float* hin,
                                                     int64_t n, const f16x8* __restrict__ Wp, const int* __restrict__ swp,
                                                     int layer, const float* __restrict__ bias, BnPrev prev,
-                                                    float momentum, float eps, float* __restrict__ hout,
+                                                    float momentum, float eps, float* hout,
                                                     double* __restrict__ stats, const f32x4* __restrict__ etin,
                                                     f32x4* __restrict__ etout) {
   constexpr bool ETIN = KE && HP, ETOUT = KE && !HP;
@@ -625,13 +573,9 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   // which lets the skip layer take the REGSTAT form as well
   constexpr bool WENC = KE && HP && PCN_H_WENC;
   constexpr bool REGSTAT = HP && (!KE || WENC) && PCN_H_REGSTAT;
-  // NWL: k-steps whose weights come from LDS (two k-steps ahead) -- the skip layer's encoding k-steps (WENC), or
-  // the hidden layer's first PCN_H_WLDS (registers for loads two tiles ahead)
-  constexpr int NWL = WENC ? KSE : (HP && !KE) ? PCN_H_WLDS : 0;
-  // RING4 (hidden layers): a ring of four B buffers staged two tiles ahead, so a barrier every second tile suffices
-  // (a buffer is rewritten two tiles after its last read and read two tiles after its staging)
-  constexpr bool RING4 = REGSTAT && !KE && AHEAD == 1 && PCN_H_RING4;
-  constexpr int NBUF = RING4 ? 4 : 2;
+  // NWL: k-steps whose weights come from LDS (two k-steps ahead) -- the skip layer's encoding k-steps (WENC)
+  constexpr int NWL = WENC ? KSE : 0;
+  constexpr int NBUF = 2;
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
@@ -661,27 +605,22 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
     if (KE && sx > 0) sx = 0;
     sx = sx > 24 ? 24 : sx;
-    if (PCN_XFOLD && t < 256) {   // 2^sx into the BatchNorm coefficients (exact: a power of two)
+    if (t < 256) {   // 2^sx into the BatchNorm coefficients (exact: a power of two)
       al[t] = ldexpf(al[t], sx);
       be[t] = ldexpf(be[t], sx);
     }
   }
   const float xscale = ldexpf(1.0f, sx);
-  const float xs_stage = PCN_XFOLD ? 1.0f : xscale;   // what staging still multiplies by
   const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
   // tile order: odd layers walk the chunk backwards, so a layer first reads the tiles its predecessor wrote last
   // (still in the memory-side cache) -- P maps the loop's tile to the tile of the chunk
   const bool rev = !KE && ((layer >> 8) & 1);   // (the first and skip layers keep the forward walk: registers)
-  // PCN_REV_OWN: a reversed layer walks its OWN workgroup's tiles backwards (the tiles blockIdx mod gridDim that
-  // the same workgroup index -- the same XCD -- wrote in the previous layer, its last-written first: XCD L2 hits)
-  const int lastb = (int)blockIdx.x + ((nt - 1 - (int)blockIdx.x) / gstride) * gstride;
-  auto P = [&](int x) { return rev ? (PCN_REV_OWN ? lastb + (int)blockIdx.x - x : nt - 1 - x) : x; };
+  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
-  // staging identity: the HBM lane (sample ls + 32 hs) whose float4s this thread stages; PCN_H_LMAP interleaves
-  // the halves across neighbouring lanes so each 16-lane group's 8-byte LDS writes cover 128 contiguous bytes
-  const int sln = PCN_H_LMAP ? ((lane >> 1) + 32 * (lane & 1)) : lane, ls = sln & 31, hs = sln >> 5;
+  // staging identity: the HBM lane (sample ls + 32 hs) whose float4s this thread stages
+  const int sln = lane, ls = sln & 31, hs = sln >> 5;
   const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
   if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH two-waves item 4
   f16x8 wr[KS][2];
@@ -721,7 +660,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
     const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * hs);
     f32x4 x;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = PCN_XFOLD ? v[m][q] * a[q] + c[q] : (v[m][q] * a[q] + c[q]) * xs_stage;
+    for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + c[q];
     put(b, KE + g, x);
   };
   auto put_enc = [&](int b, const f32x4& e) {   // encoding group t >> 6 (not scaled: sx <= 0 -> x 2^sx only if < 1)
@@ -737,7 +676,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const f32x4* src = reinterpret_cast<const f32x4*>(hin + (size_t)P(tile) * TILE_FLOATS) + (t & ~63) + sln + 512 * m;
-      v[m] = (PCN_H_NT & 1) ? __builtin_nontemporal_load(src) : *src;
+      v[m] = *src;
     }
   };
   const int etix = (t & ~63) + sln;   // this thread's encoding float4 in a stored tile [g][HBM lane]
@@ -753,11 +692,6 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       load_tile(v, tl);
 #pragma unroll
       for (int m = 0; m < 4; ++m) stage(0, v, m);
-      if (RING4 && tl + gstride < nt) {
-        load_tile(v, tl + gstride);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) stage(1, v, m);
-      }
     }
     if (KE) {
       const int64_t gs = sample_of(tl);
@@ -813,18 +747,15 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       rs[2 * j + 1][q] += dv * dv;
     }
     float* base = hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256;
-    if (!(PCN_H_ABL & 1)) {
-      if (PCN_H_NT & 2) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(base) + lane);
-      else reinterpret_cast<f32x4*>(base)[lane] = o;
-    }
+    reinterpret_cast<f32x4*>(base)[lane] = o;
   };
   auto body = [&](f32x16& acc, const f32x16& pacc, int tile, int ptile, f32x4 (&vstage)[4], f32x4 (&vload)[4],
                   bool sync) {
     const int nxt = __builtin_amdgcn_readfirstlane(tile + gstride);
     const bool more = nxt < nt;
     const int nxt2 = __builtin_amdgcn_readfirstlane(tile + 2 * gstride);
-    const int bnext = RING4 ? ((buf + 2) & 3) : (buf ^ 1);   // the buffer this tile stages into
-    const int tst = RING4 ? nxt2 : nxt;                     // ... for this tile
+    const int bnext = buf ^ 1;   // the buffer this tile stages into
+    const int tst = nxt;         // ... for this tile
     const bool mst = tst < nt;
     f16x8 xr[XD][2];
     f32x4 vloc[4];   // AHEAD == 1: this tile's loads of the next tile
@@ -886,20 +817,14 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
           stage(buf ^ 1, vstage, 3);
         }
       } else if constexpr (HP) {
-        if (ks == S_LOAD && mst && !(PCN_H_ABL & 2)) load_tile(vloc, tst);
-        if ((PCN_H_ABL & 2) && ks == S_LOAD) {
-#pragma unroll
-          for (int m = 0; m < 4; ++m) vloc[m] = f32x4{1.0f, 1.0f, 1.0f, 1.0f} * (float)(ks + m);
+        if (ks == S_LOAD && mst) load_tile(vloc, tst);
+        if (ks == S_STAGE0 && mst) {
+          stage(bnext, vloc, 0);
+          stage(bnext, vloc, 1);
         }
-        if (!(PCN_H_ABL & 4)) {
-          if (ks == S_STAGE0 && mst) {
-            stage(bnext, vloc, 0);
-            stage(bnext, vloc, 1);
-          }
-          if (ks == S_STAGE1 && mst) {
-            stage(bnext, vloc, 2);
-            stage(bnext, vloc, 3);
-          }
+        if (ks == S_STAGE1 && mst) {
+          stage(bnext, vloc, 2);
+          stage(bnext, vloc, 3);
         }
       }
       if (KE && ks == KS - 1 && more) {
@@ -923,8 +848,8 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
 #pragma unroll
       for (int j = 0; j < 4; ++j) epir(acc, tile, j);
     }
-    if (!(PCN_H_ABL & 8) && sync) __syncthreads();
-    buf = RING4 ? ((buf + 1) & 3) : (buf ^ 1);
+    if (sync) __syncthreads();
+    buf ^= 1;
   };
   f32x16 accA, accB;
   f32x4 vA[4], vB[4];
@@ -935,7 +860,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   int ptile = -1;
   if (REGSTAT) {
     while (tl < nt) {
-      body(accA, accA, tl, -1, vA, vB, !RING4);
+      body(accA, accA, tl, -1, vA, vB, true);
       tl = __builtin_amdgcn_readfirstlane(tl + gstride);
       if (tl >= nt) break;
       body(accA, accA, tl, -1, vB, vA, true);
@@ -994,7 +919,6 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
                                                      double* __restrict__ stats) {
   constexpr int KS = KS_H, XD = PCN_H1_XD;
   constexpr int S_ELOAD = 2, S_EPUT = KS - 4;
-  constexpr int H1I_AT = PCN_H1I_AT, H1I_EPI = PCN_H1I_EPI;   // PCN_H1I: W0 k-steps / h0 epilogue parts of tile + 1
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
@@ -1023,19 +947,17 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
     for (int i = 1; i < 8; ++i) m = fmaxf(m, smax[i]);
     sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
     sx = sx > 24 ? 24 : sx;
-    if (PCN_XFOLD && t < 256) {   // 2^sx into BatchNorm 0's coefficients (exact), as k_train_h
+    if (t < 256) {   // 2^sx into BatchNorm 0's coefficients (exact), as k_train_h
       al[t] = ldexpf(al[t], sx);
       be[t] = ldexpf(be[t], sx);
     }
   }
-  const float xscale = ldexpf(1.0f, sx);
   const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
   const float unscale0 = ldexpf(1.0f, -swp[0]);   // layer 0: unscaled encoding operand (its sx is 0)
   const int nt = (int)((n + 31) / 32);
   const int gstride = (int)gridDim.x;
   const bool rev = (layer >> 8) & 1;
-  const int lastb = (int)blockIdx.x + ((nt - 1 - (int)blockIdx.x) / gstride) * gstride;   // as k_train_h
-  auto P = [&](int x) { return rev ? (PCN_REV_OWN ? lastb + (int)blockIdx.x - x : nt - 1 - x) : x; };
+  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
   const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
   if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);
@@ -1086,7 +1008,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float hv = acc[4 * j + q] * unscale0 + bj[q];   // k_train_h's epilogue: o = d + b
-      x[q] = PCN_XFOLD ? hv * a[q] + c[q] : (hv * a[q] + c[q]) * xscale;   // its staging: (v alpha + beta') 2^sx
+      x[q] = hv * a[q] + c[q];   // its staging: (v alpha + beta') 2^sx, the scale folded into alpha / beta' 
     }
     putb(xs[b], 4 * blk + j, x);
   };
@@ -1126,9 +1048,6 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
     f16x8 xr[XD][2];
     f32x4 ev;
     f16x8 o0[4];   // W0 k-step 0 operands of tile + 1, read during the last W1 k-step
-    f32x16 acc0;   // PCN_H1I: h0 of tile + 1, its W0 products inside this tile's W1 k-loop
-    f16x8 q0[4];   // ... the operands of its next W0 k-step
-    if (PCN_H1I && more) h0_ops(q0, buf ^ 1, 0);
 #pragma unroll
     for (int d = 0; d < XD - 1; ++d) {
       xr[d][0] = xs[buf][d][0][lane];
@@ -1145,14 +1064,9 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
       if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
-      if (PCN_H1I && more && ks >= H1I_AT && ks < H1I_AT + KS_E) {
-        h0_mfma(acc0, q0, ks - H1I_AT);
-        if (ks - H1I_AT + 1 < KS_E) h0_ops(q0, buf ^ 1, ks - H1I_AT + 1);
-      }
-      if (PCN_H1I && more && ks >= H1I_EPI && ks < H1I_EPI + 4) h0_epi(acc0, buf ^ 1, ks - H1I_EPI);
       if (ks == S_ELOAD && more2) ev = load_enc(nxt2);
       if (ks == S_EPUT && more2) put_enc(buf, ev);   // slot of tile + 2 = this tile's slot (read one tile ago)
-      if (!PCN_H1I && ks == KS - 1) h0_ops(o0, buf ^ 1, 0);
+      if (ks == KS - 1) h0_ops(o0, buf ^ 1, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     {   // epilogue of this tile (as k_train_h's REGSTAT epilogue)
@@ -1171,11 +1085,10 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
           rs[2 * j + 1][q] += dv * dv;
         }
         f32x4* dst = reinterpret_cast<f32x4*>(hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * blk + j) * 256) + lane;
-        if (PCN_H_NT & 2) __builtin_nontemporal_store(o, dst);
-        else *dst = o;
+        *dst = o;
       }
     }
-    if (!PCN_H1I && more) h0_stage(acc, buf ^ 1, buf ^ 1, o0);   // tile + 1's encoding sits in the other slot
+    if (more) h0_stage(acc, buf ^ 1, buf ^ 1, o0);   // tile + 1's encoding sits in the other slot
     __syncthreads();
     buf ^= 1;
     tl = nxt;
@@ -1198,335 +1111,6 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
   }
 }
 
-// ---- k_train_h16<NT>: the hidden split layer with 16 waves of 16 neurons (four waves per SIMD instead of two), on
-// v_mfma_f32_16x16x32_f16: wave b holds the hi/mid weights of neurons 16b..16b+15 (64 registers; image
-// [layer-1][k-step 8][wave 16][part 2][lane 64] f16x8, lane l: neuron 16b + (l&15), features 32s + 8(l>>4) + j),
-// a 32-sample tile is two 16-column blocks, B in LDS as [k-step][block][part][lane] f16x8 (lane l: sample
-// 16 blk + (l&15), features 32s + 8(l>>4) + j), D (reg r, lane l) = neuron 16b + 4(l>>4) + r, sample 16 blk + (l&15)
-// -> one float4 store per block into the [g][lane][4] activation layout.  Same statistics, scales, BatchNorm-on-
-// staging, reversed walks and in-place buffer as k_train_h<0,true,NT>; the running sums per lane cover 4 neurons.
-constexpr size_t H16_LAYER_VECS = (size_t)8 * 16 * 2 * 64;
-constexpr size_t H16_VECS = 7 * H16_LAYER_VECS;   // layers 1..7 (the skip layer's h-part included, unused)
-
-__global__ void k_pack_train_h16(NofParamsDev P, const int* __restrict__ sw, f16x8* __restrict__ out) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= H16_VECS) return;
-  const int L = 1 + (int)(idx / H16_LAYER_VECS);
-  const size_t j0 = idx % H16_LAYER_VECS;
-  const int lane = (int)(j0 & 63), part = (int)((j0 >> 6) & 1), wb = (int)((j0 >> 7) & 15), ks = (int)(j0 >> 11);
-  const int nn = 16 * wb + (lane & 15);
-  const int in_f = L == 4 ? 319 : 256;
-  const float sc = ldexpf(1.0f, sw[L]);
-  f16x8 v;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int col = (L == 4 ? 63 : 0) + 32 * ks + 8 * (lane >> 4) + e;
-    const float w = P.lin_w[L][(size_t)nn * in_f + col] * sc;
-    const _Float16 hi = (_Float16)w;
-    v[e] = part == 0 ? hi : (_Float16)(w - (float)hi);
-  }
-  out[idx] = v;
-}
-
-template <int NT>
-__global__ __launch_bounds__(1024, 1) void k_train_h16(const float* __restrict__ hin, int64_t n,
-                                                      const f16x8* __restrict__ Wp, const int* __restrict__ swp,
-                                                      int layer, const float* __restrict__ bias, BnPrev prev,
-                                                      float momentum, float eps, float* __restrict__ hout,
-                                                      double* __restrict__ stats) {
-  __shared__ __attribute__((aligned(16))) float al[256];
-  __shared__ __attribute__((aligned(16))) float be[256];
-  __shared__ __attribute__((aligned(16))) float bs[256];
-  __shared__ float smax[16];
-  __shared__ f16x8 xs[2][8][2][2][64];   // [buf][k-step][block][part][lane]
-  const int t = threadIdx.x;
-  if (t < 256) {
-    bn_coeffs(prev, n, momentum, eps, al, be);
-    bs[t] = bias[t];
-  }
-  int sx;
-  {
-    float bnd = 0.0f;
-    if (t < 256) bnd = sqrtf((float)n) * fabsf(prev.gamma[t]) + fabsf(prev.beta[t]);
-    bnd = wave_max_f(bnd);
-    if ((t & 63) == 0) smax[t >> 6] = bnd;
-    __syncthreads();
-    float m = smax[0];
-#pragma unroll
-    for (int i = 1; i < 16; ++i) m = fmaxf(m, smax[i]);
-    sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
-    sx = sx > 24 ? 24 : sx;
-    if (t < 256) {
-      al[t] = ldexpf(al[t], sx);
-      be[t] = ldexpf(be[t], sx);
-    }
-  }
-  const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
-  const int nt = (int)((n + 31) / 32);
-  const int gstride = (int)gridDim.x;
-  const bool rev = (layer >> 8) & 1;
-  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
-  const int lane = t & 63, lq = lane >> 4, lr = lane & 15;
-  const int wb = __builtin_amdgcn_readfirstlane(t >> 6);
-  f16x8 wr[8][2];
-  {
-    const f16x8* __restrict__ w8 = Wp + lane;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 16 + wb) * 2 + p) * 64];
-  }
-  float rs[4] = {0.0f, 0.0f, 0.0f, 0.0f}, rq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  // staging: thread t owns raw float4s u = t + 1024 m of a tile ([g][lane'][4]: features 8g + 4h', sample lane'&31)
-  auto load_tile = [&](f32x4 (&v)[2], int tile) {
-#pragma unroll
-    for (int m = 0; m < 2; ++m) v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)P(tile) * TILE_FLOATS)[t + 1024 * m];
-  };
-  auto stage = [&](int b, const f32x4 (&v)[2]) {
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int u = t + 1024 * m, g = u >> 6, lp = u & 63, smp = lp & 31, hq = lp >> 5;
-      const int f0 = 8 * g + 4 * hq;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(al + f0);
-      const f32x4 c = *reinterpret_cast<const f32x4*>(be + f0);
-      f32x4 x;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + c[q];
-      f16x4 hi, mid;
-      split4(x, hi, mid);
-      const int ks = g >> 2, blk = smp >> 4, l = (smp & 15) + 16 * (g & 3);
-      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][ks][blk][0][l]) + 4 * hq) = hi;
-      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][ks][blk][1][l]) + 4 * hq) = mid;
-    }
-  };
-  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
-  if (tl < nt) {
-    f32x4 v[2];
-    load_tile(v, tl);
-    stage(0, v);
-  }
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0);
-  int buf = 0;
-  while (tl < nt) {
-    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
-    const bool more = nxt < nt;
-    f32x4 vl[2];
-    f32x4 acc[2];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      if (ks == PCN_H16_LOAD && more) load_tile(vl, nxt);
-      const f16x8 x0h = xs[buf][ks][0][0][lane], x0m = xs[buf][ks][0][1][lane];
-      const f16x8 x1h = xs[buf][ks][1][0][lane], x1m = xs[buf][ks][1][1][lane];
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], x0h, ks == 0 ? f32x4{} : acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], x1h, ks == 0 ? f32x4{} : acc[1], 0, 0, 0);
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], x0m, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], x1m, acc[1], 0, 0, 0);
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], x0h, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], x1h, acc[1], 0, 0, 0);
-      if (NT == 4) {
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], x0m, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], x1m, acc[1], 0, 0, 0);
-      }
-      if (ks == PCN_H16_STAGE && more) stage(buf ^ 1, vl);
-    }
-    {   // epilogue: + bias, statistics, one float4 store per block
-      const int tile = P(tl);
-      const int f0 = 16 * wb + 4 * lq;
-      const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + f0);
-#pragma unroll
-      for (int blk = 0; blk < 2; ++blk) {
-        const int smp = 16 * blk + lr;
-        const bool valid = (int64_t)tile * 32 + smp < n;
-        f32x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = acc[blk][r] * unscale;
-          o[r] = d + bj[r];
-          const float dv = valid ? d : 0.0f;
-          rs[r] += dv;
-          rq[r] += dv * dv;
-        }
-        const int g = f0 >> 3, lp = smp + 32 * ((f0 >> 2) & 1);
-        reinterpret_cast<f32x4*>(hout + (size_t)tile * TILE_FLOATS)[g * 64 + lp] = o;
-      }
-    }
-    __syncthreads();
-    buf ^= 1;
-    tl = nxt;
-  }
-  // per neuron: the 16 lanes of a quarter-wave hold 16 samples' sums; reduce them in float64, one atomic each
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    double a = (double)rs[r], q = (double)rq[r];
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      a += __shfl_xor(a, o, 64);
-      q += __shfl_xor(q, o, 64);
-    }
-    if (lr == 0) {
-      const int nn = 16 * wb + 4 * lq + r;
-      atomicAdd(&stats[2 * nn], a);
-      atomicAdd(&stats[2 * nn + 1], q);
-    }
-  }
-}
-
-// ---- k_train_h64<NT>: the hidden split layer with 4 waves of 64 neurons (one wave per SIMD): wave b holds the
-// hi/mid weights of out-blocks 2b, 2b+1 (256 registers, k_pack_train_h's image) and runs two accumulators, so each
-// B fragment read from LDS feeds 6 products instead of 3 -- the CU's LDS B-tile reads halve (128 KiB per tile).
-// Same tiles, layouts, scales, statistics, reversed walks and in-place buffer as k_train_h<0,true,NT>.
-template <int NT>
-__global__ __launch_bounds__(256, 1) void k_train_h64(const float* __restrict__ hin, int64_t n,
-                                                     const f16x8* __restrict__ Wp, const int* __restrict__ swp,
-                                                     int layer, const float* __restrict__ bias, BnPrev prev,
-                                                     float momentum, float eps, float* __restrict__ hout,
-                                                     double* __restrict__ stats) {
-  __shared__ __attribute__((aligned(16))) float al[256];
-  __shared__ __attribute__((aligned(16))) float be[256];
-  __shared__ __attribute__((aligned(16))) float bs[256];
-  __shared__ float smax[4];
-  __shared__ f16x8 xs[2][KS_H][2][64];
-  const int t = threadIdx.x;
-  bn_coeffs(prev, n, momentum, eps, al, be);
-  bs[t] = bias[t];
-  int sx;
-  {
-    float bnd = sqrtf((float)n) * fabsf(prev.gamma[t]) + fabsf(prev.beta[t]);
-    bnd = wave_max_f(bnd);
-    if ((t & 63) == 0) smax[t >> 6] = bnd;
-    __syncthreads();
-    const float m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
-    sx = (m > 0.0f && m < 3.0e38f) ? 14 - ilogbf(m) : 0;
-    sx = sx > 24 ? 24 : sx;
-    al[t] = ldexpf(al[t], sx);
-    be[t] = ldexpf(be[t], sx);
-  }
-  const float unscale = ldexpf(1.0f, -(swp[layer & 255] + sx));
-  const int nt = (int)((n + 31) / 32);
-  const int gstride = (int)gridDim.x;
-  const bool rev = (layer >> 8) & 1;
-  auto P = [&](int x) { return rev ? nt - 1 - x : x; };
-  const int lane = t & 63, h = lane >> 5, li = lane & 31;
-  const int wb = __builtin_amdgcn_readfirstlane(t >> 6);
-  f16x8 wr[2][KS_H][2];
-#pragma unroll
-  for (int o = 0; o < 2; ++o)
-#pragma unroll
-    for (int ks = 0; ks < KS_H; ++ks)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) wr[o][ks][p] = Wp[((ks * 8 + 2 * wb + o) * 2 + p) * 64 + lane];
-  f32x4 rs[2][8];   // [o][2j + moment]
-#pragma unroll
-  for (int o = 0; o < 2; ++o)
-#pragma unroll
-    for (int c = 0; c < 8; ++c) rs[o][c] = f32x4{};
-  // staging: thread t owns the tile's float4s t + 256 m (m = 0..7): group g = u >> 6, HBM lane u & 63
-  auto load_tile = [&](f32x4 (&v)[8], int tile) {
-#pragma unroll
-    for (int m = 0; m < 8; ++m) v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)P(tile) * TILE_FLOATS)[t + 256 * m];
-  };
-  auto stage = [&](int b, const f32x4 (&v)[8], int m0, int m1) {
-#pragma unroll
-    for (int m = m0; m < m1; ++m) {
-      const int g = (t >> 6) + 4 * m;   // feature group (features 8g + 4h .. + 3 of lane t & 63)
-      const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
-      const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
-      f32x4 x;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x[q] = v[m][q] * a[q] + c[q];
-      f16x4 hi, mid;
-      split4(x, hi, mid);
-      const int ln = li + 32 * (g & 1);
-      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][g >> 1][0][ln]) + 4 * h) = hi;
-      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&xs[b][g >> 1][1][ln]) + 4 * h) = mid;
-    }
-  };
-  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
-  if (tl < nt) {
-    f32x4 v[8];
-    load_tile(v, tl);
-    stage(0, v, 0, 8);
-  }
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0);
-  int buf = 0;
-  while (tl < nt) {
-    const int nxt = __builtin_amdgcn_readfirstlane(tl + gstride);
-    const bool more = nxt < nt;
-    f32x4 vl[8];
-    f32x16 acc[2];
-    f16x8 xr[2][2];
-    xr[0][0] = xs[buf][0][0][lane];
-    xr[0][1] = xs[buf][0][1][lane];
-#pragma unroll
-    for (int ks = 0; ks < KS_H; ++ks) {
-      if (ks + 1 < KS_H) {
-        xr[(ks + 1) & 1][0] = xs[buf][ks + 1][0][lane];
-        xr[(ks + 1) & 1][1] = xs[buf][ks + 1][1][lane];
-      }
-      const f16x8 xh = xr[ks & 1][0], xm = xr[ks & 1][1];
-      if (ks == PCN_H64_LOAD && more) load_tile(vl, nxt);
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-        acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[o][ks][0], xh, ks == 0 ? f32x16{} : acc[o], 0, 0, 0);
-#pragma unroll
-      for (int o = 0; o < 2; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[o][ks][0], xm, acc[o], 0, 0, 0);
-#pragma unroll
-      for (int o = 0; o < 2; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[o][ks][1], xh, acc[o], 0, 0, 0);
-      if (NT == 4) {
-#pragma unroll
-        for (int o = 0; o < 2; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[o][ks][1], xm, acc[o], 0, 0, 0);
-      }
-      if (more && ks >= PCN_H64_STAGE && ks < PCN_H64_STAGE + 4) {
-        const int k0 = ks - PCN_H64_STAGE;
-        stage(buf ^ 1, vl, 2 * k0, 2 * k0 + 2);
-      }
-    }
-    {   // epilogue: + bias, statistics, stores straight from the accumulators (as k_train_h)
-      const int tile = P(tl);
-      const bool valid = (int64_t)tile * 32 + li < n;
-#pragma unroll
-      for (int o = 0; o < 2; ++o) {
-        const int ob = 2 * wb + o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * ob + 8 * j + 4 * h);
-          f32x4 ov;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float d = acc[o][4 * j + q] * unscale;
-            ov[q] = d + bj[q];
-            const float dv = valid ? d : 0.0f;
-            rs[o][2 * j][q] += dv;
-            rs[o][2 * j + 1][q] += dv * dv;
-          }
-          reinterpret_cast<f32x4*>(hout + (size_t)tile * TILE_FLOATS + (size_t)(4 * ob + j) * 256)[lane] = ov;
-        }
-      }
-    }
-    __syncthreads();
-    buf ^= 1;
-    tl = nxt;
-  }
-  // per neuron: reduce the 32 lanes of a half wave (the samples) in float64, one atomic per (neuron, moment)
-#pragma unroll
-  for (int o = 0; o < 2; ++o)
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double a = (double)rs[o][c][q];
-#pragma unroll
-        for (int sh = 1; sh < 32; sh <<= 1) a += __shfl_xor(a, sh, 64);
-        if (li == 0) {
-          const int j = c >> 1, mo = c & 1;
-          const int nn = 32 * (2 * wb + o) + 8 * j + 4 * h + q;
-          atomicAdd(&stats[2 * nn + mo], a);
-        }
-      }
-}
-
 // ---- layer 0 from the encoding's moments (split forward without activation store, k_train_h1 after it).
 // Layer 0's only remaining outputs there are the chunk's encoding tiles and BatchNorm 0's statistics, and those
 // statistics are exact functions of the chunk's encoding mean ebar and covariance Sigma (h0 = W0 e + b0 feeds
@@ -1544,9 +1128,6 @@ __global__ __launch_bounds__(256, 1) void k_train_h64(const float* __restrict__ 
 constexpr int GR_P = 72;          // LDS pitch (halves): 16 lanes' 16-byte operand reads hit disjoint bank groups
 #ifndef PCN_GR_BLOCKS
 #define PCN_GR_BLOCKS 512
-#endif
-#ifndef PCN_GR_ABL
-#define PCN_GR_ABL 0      // timing-only ablations of k_enc_gram: 1 no encoding-tile stores, 2 no moment products
 #endif
 constexpr int GR_BLOCKS = PCN_GR_BLOCKS;    // k_enc_gram workgroups per chunk (two per CU)
 constexpr int GR_PART = 3072;     // doubles per partial: blocks 00, 01, 11 as [block][register 16][lane 64]
@@ -1614,7 +1195,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_gram(const float* __restrict__ r
       encode_full(p, f);
     }
     const int64_t tile = s >> 5;
-    if (!(PCN_GR_ABL & 1) && tile < ntiles) {   // [tile][g][lane (s & 31) + 32 h][4]: features 8 g + 4 h + q
+    if (tile < ntiles) {   // [tile][g][lane (s & 31) + 32 h][4]: features 8 g + 4 h + q
       f32x4* dst = etout + (size_t)tile * 512 + (lane & 31);
 #pragma unroll
       for (int g = 0; g < 8; ++g)
@@ -1643,7 +1224,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_gram(const float* __restrict__ r
     mi[63 * GR_P + lane] = (_Float16)0.0f;
     gram_lds_sync();
 #pragma unroll
-    for (int ks = 0; ks < ((PCN_GR_ABL & 2) ? 0 : 4); ++ks) {
+    for (int ks = 0; ks < 4; ++ks) {
       const int o = (lane & 31) * GR_P + 16 * ks + 8 * (lane >> 5);
       const f16x8 h0 = *reinterpret_cast<const f16x8*>(hi + o);
       const f16x8 m0 = *reinterpret_cast<const f16x8*>(mi + o);
@@ -1794,191 +1375,6 @@ __global__ __launch_bounds__(256) void k_gram_stats(const double* __restrict__ m
   }
 }
 
-// ---- k_train_hd<NT>: the hidden-layer k_train_h (REGSTAT form) with the raw activation tiles brought in by LDS-DMA
-// (global_load_lds_dwordx4) two tiles ahead into a 2-slot ring, so 64 KiB per CU stay in flight without registers.
-// Iteration i (tile t_i = blockIdx + i G): its start issues tile t_{i+2}'s DMA into slot i & 1 (which held t_i, staged
-// during iteration i-1); its staging point waits (counted vmcnt) for the thread's own DMA of t_{i+1} in slot (i+1) & 1
-// -- every thread reads back exactly the 16-byte pieces it DMA'd (slot layout = the HBM tile's [g][lane][4]), so no
-// barrier is needed for the raw data.  All LDS lives in one __shared__ array and the tile barrier is a raw
-// s_barrier after lgkmcnt(0) (a __syncthreads() would drain the DMA in flight: cdna_hip_programming.md glds rules).
-// Two 16-byte LDS reads (p[0], p[stride]) in inline asm, completed before return: invisible to hipcc's waitcnt
-// pass, which would otherwise wait vmcnt(0) -- every DMA and store in flight -- before reading a DMA-written slot.
-__device__ __forceinline__ void lds_read2_asm(const f32x4* p, int stride, f32x4& a, f32x4& b) {
-  const unsigned ad = (unsigned)(size_t)(const __attribute__((address_space(3))) f32x4*)p;
-  const unsigned bd = ad + (unsigned)stride * 16u;
-  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-               : "=&v"(a), "=&v"(b) : "v"(ad), "v"(bd) : "memory");
-}
-
-template <int NT>
-__global__ __launch_bounds__(512, 1) void k_train_hd(const float* __restrict__ hin, int64_t n,
-                                                     const f16x8* __restrict__ Wp, const int* __restrict__ swp,
-                                                     int layer, const float* __restrict__ bias, BnPrev prev,
-                                                     float momentum, float eps, float* __restrict__ hout,
-                                                     double* __restrict__ stats) {
-  constexpr int KS = KS_H, XD = PCN_H_XD;
-  constexpr int S_STAGE0 = KS - PCN_H_STAGE, S_STAGE1 = S_STAGE0 + 1;
-  constexpr int OFF_AL = 0, OFF_BE = 1024, OFF_BS = 2048, OFF_MAX = 3072, OFF_XS = 4096;
-  constexpr int XS_BYTES = 2 * KS * 2 * 64 * 16, OFF_RAW = OFF_XS + XS_BYTES, RAW_SLOT = 32768;
-  __shared__ __attribute__((aligned(16))) char smem[OFF_RAW + 2 * RAW_SLOT];
-  float* const al = reinterpret_cast<float*>(smem + OFF_AL);
-  float* const be = reinterpret_cast<float*>(smem + OFF_BE);
-  float* const bs = reinterpret_cast<float*>(smem + OFF_BS);
-  float* const smax = reinterpret_cast<float*>(smem + OFF_MAX);
-  f16x8* const xs = reinterpret_cast<f16x8*>(smem + OFF_XS);   // [buf][s][part][lane]
-  f32x4* const raw = reinterpret_cast<f32x4*>(smem + OFF_RAW);  // [slot][2048]
-  auto XS = [&](int b, int s, int p, int l) -> f16x8& { return xs[((b * KS + s) * 2 + p) * 64 + l]; };
-  const int t = threadIdx.x;
-  if (t < 256) {
-    bn_coeffs(prev, n, momentum, eps, al, be);
-    bs[t] = bias[t];
-  }
-  float bnd = t < 256 ? sqrtf((float)n) * fabsf(prev.gamma[t]) + fabsf(prev.beta[t]) : 0.0f;
-  bnd = wave_max_f(bnd);
-  if ((t & 63) == 0) smax[t >> 6] = bnd;
-  __syncthreads();
-  float mb = smax[0];
-#pragma unroll
-  for (int i = 1; i < 8; ++i) mb = fmaxf(mb, smax[i]);
-  int sx = (mb > 0.0f && mb < 3.0e38f) ? 14 - ilogbf(mb) : 0;
-  sx = sx > 24 ? 24 : sx;
-  const float xscale = ldexpf(1.0f, sx);
-  const float unscale = ldexpf(1.0f, -(swp[layer] + sx));
-  const int nt = (int)((n + 31) / 32);
-  const int G = (int)gridDim.x;
-  const int lane = t & 63, h = lane >> 5, li = lane & 31;
-  const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);
-  f16x8 wr[KS][2];
-  {
-    const f16x8* __restrict__ w8 = Wp + lane;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 8 + blk) * 2 + p) * 64];
-  }
-  f32x4 rs[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) rs[c] = f32x4{};
-  // raw tile pieces: this thread's 4 float4 of a tile are [g = (t >> 6) + 8 m][lane] = float4 t + 512 m
-  auto dma = [&](int slot, int tile) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const f32x4*>(hin + (size_t)tile * TILE_FLOATS) +
-                                                          t + 512 * m),
-          (__attribute__((address_space(3))) void*)(raw + slot * 2048 + (t & ~63) + 512 * m), 16, 0, 0);
-  };
-  auto stage = [&](int b, const f32x4& v, int m) {
-    const int g = (t >> 6) + 8 * m;
-    const f32x4 a = *reinterpret_cast<const f32x4*>(al + 8 * g + 4 * h);
-    const f32x4 c = *reinterpret_cast<const f32x4*>(be + 8 * g + 4 * h);
-    f32x4 x;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = (v[q] * a[q] + c[q]) * xscale;
-    f16x4 hi, mid;
-    split4(x, hi, mid);
-    const int s = g >> 1, ln = li + 32 * (g & 1);
-    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&XS(b, s, 0, ln)) + 4 * h) = hi;
-    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(&XS(b, s, 1, ln)) + 4 * h) = mid;
-  };
-  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
-  // prologue: tile t_0 through registers into xs[0]; t_1's DMA into slot 1
-  if (tl < nt) {
-    f32x4 v[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) v[m] = reinterpret_cast<const f32x4*>(hin + (size_t)tl * TILE_FLOATS)[t + 512 * m];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) stage(0, v[m], m);
-  }
-  __builtin_amdgcn_s_waitcnt(0);   // weights and t_0 in registers before any DMA is outstanding
-  if (tl + G < nt) dma(1, tl + G);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  int buf = 0;
-  for (int i = 0; tl < nt; ++i) {
-    const int nxt = __builtin_amdgcn_readfirstlane(tl + G), nxt2 = __builtin_amdgcn_readfirstlane(tl + 2 * G);
-    const bool more = nxt < nt, more2 = nxt2 < nt;
-    if (more2) dma(i & 1, nxt2);
-    f32x16 acc;
-    f16x8 xr[XD][2];
-#pragma unroll
-    for (int d = 0; d < XD - 1; ++d) {
-      xr[d][0] = XS(buf, d, 0, lane);
-      xr[d][1] = XS(buf, d, 1, lane);
-    }
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ks + XD - 1 < KS) {
-        xr[(ks + XD - 1) % XD][0] = XS(buf, ks + XD - 1, 0, lane);
-        xr[(ks + XD - 1) % XD][1] = XS(buf, ks + XD - 1, 1, lane);
-      }
-      const f16x8 xh = xr[ks % XD][0], xm = xr[ks % XD][1];
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xh, ks == 0 ? f32x16{} : acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][0], xm, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xh, acc, 0, 0, 0);
-      if (NT == 4) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wr[ks][1], xm, acc, 0, 0, 0);
-      if (ks == S_STAGE0 && more) {
-        // own DMA of t_{i+1}: younger VMEM ops are iteration i-1's 4 epilogue stores (i > 0) and this
-        // iteration's DMA of t_{i+2} (4, when issued)
-        if (i > 0 && more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (i > 0 || more2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        f32x4 r0, r1;
-        lds_read2_asm(raw + ((i + 1) & 1) * 2048 + t, 512, r0, r1);
-        stage(buf ^ 1, r0, 0);
-        stage(buf ^ 1, r1, 1);
-      }
-      if (ks == S_STAGE1 && more) {
-        f32x4 r2, r3;
-        lds_read2_asm(raw + ((i + 1) & 1) * 2048 + t + 1024, 512, r2, r3);
-        stage(buf ^ 1, r2, 2);
-        stage(buf ^ 1, r3, 3);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // epilogue of this tile: raw h (+ bias) to HBM, running statistics of (h - bias) in registers
-    const bool valid = (int64_t)tl * 32 + li < n;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x4 bj = *reinterpret_cast<const f32x4*>(bs + 32 * blk + 8 * j + 4 * h);
-      f32x4 o;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float d = acc[4 * j + q] * unscale;
-        o[q] = d + bj[q];
-        const float dv = valid ? d : 0.0f;
-        rs[2 * j][q] += dv;
-        rs[2 * j + 1][q] += dv * dv;
-      }
-      reinterpret_cast<f32x4*>(hout + (size_t)tl * TILE_FLOATS + (size_t)(4 * blk + j) * 256)[lane] = o;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    buf ^= 1;
-    tl = nxt;
-  }
-  // per-neuron sums: the per-lane statistics through LDS (the B buffers), one float64 atomic per (neuron, moment)
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  f32x4* const sred = reinterpret_cast<f32x4*>(smem + OFF_XS);
-  const int st_sw = (lane >> 1) & 7;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) sred[(blk * 64 + lane) * 8 + (c ^ st_sw)] = rs[c];
-  __syncthreads();
-  {
-    const int nn = t >> 1, mo = t & 1, ib = nn & 31, wb = nn >> 5;
-    const int hh = (ib >> 2) & 1, jj = ib >> 3, qq = ib & 3;
-    double a = 0.0;
-#pragma unroll 8
-    for (int l = 0; l < 32; ++l) {
-      const int ln = 32 * hh + l;
-      a += (double)sred[(wb * 64 + ln) * 8 + ((2 * jj + mo) ^ ((ln >> 1) & 7))][qq];
-    }
-    atomicAdd(&stats[t], a);
-  }
-}
-
 // occ_out on BatchNorm 8 (applied on load) + sigmoid; one wave per 32-sample tile.
 __global__ __launch_bounds__(256) void k_train_out(const float* __restrict__ hin, int64_t n, BnPrev prev,
                                                    float momentum, float eps, const float* __restrict__ wout,
@@ -2014,7 +1410,6 @@ struct TrainWs {
   f32x4* enc;   // the chunk's encoding tiles: written by the first layer, read by the skip layer
   float* wp;
   f16x8* wh;    // split-fp16 weight image (train math 1/2)
-  f16x8* wh16;  // k_train_h16's image of the 256-input layers
   int* sw;      // its per-layer scale exponents
   double* stats;
   double* gram;  // k_enc_gram partials, their slice sums and the chunk's shift e0
@@ -2039,7 +1434,6 @@ static TrainWs carve(void* base, int64_t chunk) {
   const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
   const size_t ogr = take(GR_DOUBLES * sizeof(double));
-  const size_t oh16 = take(H16_VECS * sizeof(f16x8));
   char* b = (char*)base;
   TrainWs w;
   w.bufA = (float*)(b + oA);
@@ -2050,7 +1444,6 @@ static TrainWs carve(void* base, int64_t chunk) {
   w.sw = (int*)(b + osw);
   w.stats = (double*)(b + ost);
   w.gram = (double*)(b + ogr);
-  w.wh16 = (f16x8*)(b + oh16);
   w.bytes = off;
   return w;
 }
@@ -2106,13 +1499,6 @@ static void launch_layer(const TrainLayerLaunch& q, const NofParamsDev& P, const
   if (m == 0) {
     hipLaunchKernelGGL((k_train_ws<KE, HP>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0, q.ein,
                        hin, q.n, wp + off_w(L, KE != 0), P.lin_b[L], prev, q.mom, q.eps, hout, stats, etin, etout);
-  } else if (PCN_H_DMA && KE == 0 && HP) {
-    if (m == 1)
-      hipLaunchKernelGGL(k_train_hd<3>, dim3(q.gws), dim3(512), 0, q.s, hin, q.n, wh + off_h(L, false), sw, L,
-                         P.lin_b[L], prev, q.mom, q.eps, hout, stats);
-    else
-      hipLaunchKernelGGL(k_train_hd<4>, dim3(q.gws), dim3(512), 0, q.s, hin, q.n, wh + off_h(L, false), sw, L,
-                         P.lin_b[L], prev, q.mom, q.eps, hout, stats);
   } else if (m == 1) {
     hipLaunchKernelGGL((k_train_h<KE, HP, 3>), dim3(q.gws), dim3(512), 0, q.s, q.rays, q.stride, q.z, q.S, q.c0,
                        q.ein, hin, q.n, wh + off_h(L, KE != 0), sw, L | (tile_rev(L) << 8), P.lin_b[L], prev, q.mom,
@@ -2198,8 +1584,6 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   hipStream_t s = (hipStream_t)stream;
   pack_weights(P, ws.wp, ws.wh, ws.sw, s);
-  if (PCN_H16 && g_train_math != 0)
-    hipLaunchKernelGGL(k_pack_train_h16, dim3((unsigned)((H16_VECS + 255) / 256)), dim3(256), 0, s, P, ws.sw, ws.wh16);
   for (int64_t c0 = 0; c0 < total; c0 += chunk) {
     const int64_t n = total - c0 < chunk ? total - c0 : chunk;
     const int64_t ntiles = (n + 31) / 32;
@@ -2219,9 +1603,8 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     const bool h1 = PCN_H1 && !keep && g_train_math != 0;
     if (!(h1 && PCN_GRAM)) PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));   // (else k_gram_stats)
     // PCN_INPLACE: every layer of the chunk overwrites its input tile by tile (a tile is read only by the workgroup
-    // that writes its output, which staged it before its MFMAs): one 268 MB footprint instead of two.  The kernels'
-    // __restrict__ hin / hout then alias, which stays sound here: a tile's output store depends on its own input
-    // load through LDS and a workgroup barrier (no reordering can cross that), and no other tile is touched twice.
+    // that writes its output, which staged it before its MFMAs): one 268 MB footprint instead of two.  k_train_h
+    // declares hin / hout without __restrict__ for this; k_train_h1 reads the encoding tiles, not hin.
     if (h1 && PCN_INPLACE) hout = hin;
     if (h1 && PCN_GRAM) {
       // algorithmic: the 64 x 64 moment product per sample; 4 B of z in, 256 B of encoding out
@@ -2270,25 +1653,7 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
         // algorithmic: 2*256*256 FLOP and 1 KiB in + 1 KiB out per sample
         ProfScope ps(s, PT_TRAIN_HIDDEN, 2.0 * 256 * 256 * dn, 2048.0 * dn);
         const TrainLayerLaunch q{rays, ray_stride, z, n_samples, c0, ein, n, gws, momentum, eps, s};
-        if (PCN_H64 && g_train_math != 0) {
-          const f16x8* wl = ws.wh + off_h(L, false);
-          if (g_train_math == 1)
-            hipLaunchKernelGGL(k_train_h64<3>, dim3(gws), dim3(256), 0, s, hin, n, wl, ws.sw,
-                               L | (tile_rev(L) << 8), P.lin_b[L], prev, momentum, eps, hout, stats + 512 * L);
-          else
-            hipLaunchKernelGGL(k_train_h64<4>, dim3(gws), dim3(256), 0, s, hin, n, wl, ws.sw,
-                               L | (tile_rev(L) << 8), P.lin_b[L], prev, momentum, eps, hout, stats + 512 * L);
-        } else if (PCN_H16 && g_train_math != 0) {
-          const f16x8* w16 = ws.wh16 + (size_t)(L - 1) * H16_LAYER_VECS;
-          if (g_train_math == 1)
-            hipLaunchKernelGGL(k_train_h16<3>, dim3(gws), dim3(1024), 0, s, hin, n, w16, ws.sw,
-                               L | (tile_rev(L) << 8), P.lin_b[L], prev, momentum, eps, hout, stats + 512 * L);
-          else
-            hipLaunchKernelGGL(k_train_h16<4>, dim3(gws), dim3(1024), 0, s, hin, n, w16, ws.sw,
-                               L | (tile_rev(L) << 8), P.lin_b[L], prev, momentum, eps, hout, stats + 512 * L);
-        } else {
-          launch_layer<0, true>(q, P, ws.wp, ws.wh, ws.sw, L, hin, prev, hout, stats + 512 * L, nullptr, nullptr);
-        }
+        launch_layer<0, true>(q, P, ws.wp, ws.wh, ws.sw, L, hin, prev, hout, stats + 512 * L, nullptr, nullptr);
       }
       float* t = hin;
       hin = hout;
@@ -2346,7 +1711,7 @@ extern "C" int pcnerf_nof_forward_train(const float* emb, int64_t n, const pcner
 // dL/dlogit per sample (or dL/dp with p).  Per chunk:
 //   1. the forward's raw h_L of all 8 layers (1 KiB/sample each) and chunk statistics: from the activation store,
 //      or recomputed with k_train_ws (running stats untouched); k_bn_save stores mean/invstd/alpha/beta;
-//   2. occ_out + BatchNorm 8 backward (k_out_bwd_stats, k_out_bwd_grad) -> dL/dh_7;
+//   2. occ_out + BatchNorm 8 backward (k_out_bwd_stats1, k_out_bwd_grad) -> dL/dh_7;
 //   3. for L = 7..1: k_wgrad: G_L = sum_s dL/dh_L[s] (x) (h_{L-1}[s] - mean_{L-1})   (+ the encoding part at L=4)
 //                    on MFMA, partials per block;  k_wgrad_reduce: dW_L = alpha*G + beta (x) db, db_L, and the
 //                    statistics BatchNorm L-1's backward needs, which are algebraic in G and db:
@@ -2399,65 +1764,11 @@ __device__ __forceinline__ float logit_grad(const float* __restrict__ g, const f
   return g[i] * (1.0f - pv) * pv;  // sigmoid backward
 }
 
-// acc[f] += sum_s g_s (h7[s][f] - mean7[f]), acc[256] += sum_s g_s.  Four passes over quarters of the feature
-// groups (32 accumulators per lane over its tiles), each followed by an LDS transpose-reduction across lanes.
-__global__ __launch_bounds__(256) void k_out_bwd_stats(const float* __restrict__ g, const float* __restrict__ pin,
-                                                       const float* __restrict__ h7, int64_t n,
-                                                       const float* __restrict__ coef7, double* __restrict__ acc) {
-  __shared__ float red[4][64 * 33];
-  __shared__ __attribute__((aligned(16))) float mu[256];
-  const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31, wv = t >> 6;
-  mu[t] = coef7[t];
-  __syncthreads();
-  const int64_t ntiles = (n + 31) / 32;
-  const int64_t t0 = (int64_t)blockIdx.x * 4 + wv, ts = (int64_t)gridDim.x * 4;
-  float gs = 0.0f;
-  for (int64_t tile = t0; tile < ntiles; tile += ts) {
-    const int64_t s = tile * 32 + li;
-    if (h == 0 && s < n) gs += logit_grad(g, pin, s);
-  }
-  // thread t reduces feature f = 64*pass + (t & 63) over the 32 lanes of its half, one wave-slice per t>>6
-  for (int pass = 0; pass < 4; ++pass) {
-    float a[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) a[i] = 0.0f;
-    for (int64_t tile = t0; tile < ntiles; tile += ts) {
-      const int64_t s = tile * 32 + li;
-      const float gv = s < n ? logit_grad(g, pin, s) : 0.0f;
-      const f32x4* x4 = reinterpret_cast<const f32x4*>(h7 + tile * TILE_FLOATS) + 8 * pass * 64 + lane;
-#pragma unroll
-      for (int gq = 0; gq < 8; ++gq) {
-        const f32x4 x = x4[gq * 64];
-        const f32x4 m = *reinterpret_cast<const f32x4*>(mu + 8 * (8 * pass + gq) + 4 * h);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a[4 * gq + q] += gv * (x[q] - m[q]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 32; ++i) red[wv][lane * 33 + i] = a[i];
-    __syncthreads();
-    if (t < 64) {
-      const int f = 64 * pass + t;  // feature within this pass: group gq = (f>>3)&7, half (f>>2)&1, q = f&3
-      const int fl = f - 64 * pass, hb = (fl >> 2) & 1, idx = (fl >> 3) * 4 + (fl & 3);
-      double tot = 0.0;
-      for (int w = 0; w < 4; ++w) {
-        float sw = 0.0f;
-        for (int l = 0; l < 32; ++l) sw += red[w][(l + 32 * hb) * 33 + idx];
-        tot += (double)sw;
-      }
-      atomicAdd(&acc[f], tot);
-    }
-    __syncthreads();
-  }
-  gs = wave_sum_f(gs);
-  if (lane == 0) atomicAdd(&acc[256], (double)gs);
-}
-
-// One-pass form of k_out_bwd_stats: each lane keeps all 128 of its half's feature sums over its tiles (two
-// 16-load batches per tile in flight), reduces them across its 32 lanes with shuffles once at the end, and the
+// acc[f] += sum_s g_s (h7[s][f] - mean7[f]), acc[256] += sum_s g_s in one pass: each lane keeps all 128 of its
+// half's feature sums over its tiles (two 16-load batches per tile in flight), reduces them across its 32 lanes with shuffles once at the end, and the
 // block adds its totals to copy (block % OSTAT_COPIES) of acc (fewer blocks per address); k_out_bwd_grad sums the
 // copies.
-constexpr int OSTAT_COPIES = PCN_OSTAT1 ? 8 : 1;
+constexpr int OSTAT_COPIES = 8;
 __global__ __launch_bounds__(256) void k_out_bwd_stats1(const float* __restrict__ g, const float* __restrict__ pin,
                                                         const float* __restrict__ h7, int64_t n,
                                                         const float* __restrict__ coef7, double* __restrict__ acc) {
@@ -3729,12 +3040,9 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
       // 2. occ_out + BatchNorm 8
       PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257 + GMAX_DBL) * sizeof(double), s));  // per chunk
-      if (PCN_OSTAT1) {
+      {
         const unsigned sg = (unsigned)((ntiles + 3) / 4 < 256 ? (ntiles + 3) / 4 : 256);
         hipLaunchKernelGGL(k_out_bwd_stats1, dim3(sg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
-                           ws.coef + 7 * 1024, ws.ostat);
-      } else {
-        hipLaunchKernelGGL(k_out_bwd_stats, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                            ws.coef + 7 * 1024, ws.ostat);
       }
       hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,

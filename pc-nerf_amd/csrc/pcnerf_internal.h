@@ -28,6 +28,13 @@ void set_error(const std::string& msg);
 void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const double* fold, int64_t chunk, float* p_out, hipStream_t s);
 
+// The train-mode query in k_nof_eval_h2's form (nof_eval.hip): the image (train_query_image_floats floats) holds
+// the raw split weights and occ_out; coef[chunk][8][alpha 256 | beta'' 256] each chunk's BatchNorm coefficients.
+size_t train_query_image_floats();
+void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s);
+void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
+                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s);
+
 // p = o + d*z, one rounding per op (render.py:458; built with -ffp-contract=off).
 __device__ __forceinline__ void sample_point(const float* __restrict__ r, float z, float (&p)[3]) {
   p[0] = r[0] + r[3] * z;

@@ -98,6 +98,10 @@ _SIGS = {
                                                      c_float, vp, vp, c_size, ctypes.POINTER(NofGrads), vp]),
     "pcnerf_nof_forward_train_fold_backward": (c_int, [vp, i64, ctypes.POINTER(NofParams), c_float, vp, vp, vp,
                                                        c_size, ctypes.POINTER(NofGrads), vp]),
+    "pcnerf_nof_query_train_fused": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams), c_float,
+                                             c_float, vp, c_size, vp, vp]),
+    "pcnerf_nof_forward_train_fused": (c_int, [vp, i64, ctypes.POINTER(NofParams), c_float, c_float, vp, c_size,
+                                               vp, vp]),
     "pcnerf_nn_distance": (c_int, [vp, i64, vp, i64, vp, vp]),
     "pcnerf_eval_pts_workspace_bytes": (c_size, [i64, i64]),
     "pcnerf_eval_pts": (c_int, [vp, i64, vp, i64, ctypes.c_double, vp, vp, vp]),

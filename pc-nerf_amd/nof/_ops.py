@@ -113,19 +113,26 @@ def fold_eval(model, device) -> torch.Tensor:
 
 # Arithmetic of the train-mode MLP, forward and backward (pcnerf_set_train_math): fp32 operands split into two fp16
 # parts (22 significant bits) with exact products on the fp16 matrix pipe and fp32 accumulation, "f16x2_3"
-# (default: hi*hi + hi*mid + mid*hi) or "f16x2_4" (+ mid*mid) -- the weight gradients under either as three bf16
-# parts and six products -- or "fp32" (fp32 MFMA throughout).
-TRAIN_MATH = {"fp32": 0, "f16x2_3": 1, "f16x2_4": 2}
+# (hi*hi + hi*mid + mid*hi) or "f16x2_4" (+ mid*mid) -- the weight gradients under either as f16x2 / three bf16
+# parts -- or "fp32" (fp32 MFMA throughout).  "f16x2_3_fused" (default): f16x2_3, except that a train-mode query
+# whose layer outputs no backward reads (the render+loss forward, NOF.forward without autograd) runs as ONE fused
+# per-sample kernel with each chunk's BatchNorm batch statistics taken from the chunk's encoding moments
+# (pcnerf_nof_query_train_fused) instead of layer by layer through HBM.
+TRAIN_MATH = {"fp32": 0, "f16x2_3": 1, "f16x2_4": 2, "f16x2_3_fused": 1}
+_TRAIN_FUSED = True   # the library's own default is mode 1 (f16x2_3)
 
 
 def set_train_math(mode: str) -> str:
     """Select the train-mode layer arithmetic; returns the previous mode's name."""
+    global _TRAIN_FUSED
     if mode not in TRAIN_MATH:
         raise ValueError(f"train math must be one of {sorted(TRAIN_MATH)}")
     prev = H.lib().pcnerf_set_train_math(TRAIN_MATH[mode])
     if prev < 0:
         raise RuntimeError(H.lib().pcnerf_last_error().decode())
-    return {v: k for k, v in TRAIN_MATH.items()}[prev]
+    prev_name = "f16x2_3_fused" if (prev == 1 and _TRAIN_FUSED) else {0: "fp32", 1: "f16x2_3", 2: "f16x2_4"}[prev]
+    _TRAIN_FUSED = mode == "f16x2_3_fused"
+    return prev_name
 
 
 def get_train_math() -> str:
@@ -211,6 +218,14 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
                                               ctypes.byref(s), mom, eps, fold.data_ptr(), fold.numel(),
                                               p.data_ptr(), st))
         _track_batches(model, -(-R * S // int(chunk)))
+    elif model.training and _TRAIN_FUSED and (store is None or store.n_chunks == 0):
+        chunk = max(1, min(int(chunk), R * S))
+        mom, eps = _bn_config(model)
+        s, keep = _params(model)
+        ws = _workspace(z.device, int(L.pcnerf_nof_train_fold_bytes(R * S, chunk)))
+        H.check(L.pcnerf_nof_query_train_fused(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                               ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(), p.data_ptr(), st))
+        _track_batches(model, -(-R * S // int(chunk)))
     elif model.training:
         chunk = max(1, min(int(chunk), R * S))   # a larger chunk is the same single BatchNorm chunk
         mom, eps = _bn_config(model)
@@ -255,6 +270,15 @@ def nof_forward_embedded(model, x: torch.Tensor, with_fold_state: bool = False):
         fold = fold_state(x.device, B, B)
         H.check(L.pcnerf_nof_forward_train_fold(x.data_ptr(), B, ctypes.byref(s), mom, eps, fold.data_ptr(),
                                                 fold.numel(), out.data_ptr(), st))
+        _track_batches(model, 1)
+    elif model.training and _TRAIN_FUSED:
+        if B <= 1:
+            raise ValueError("Expected more than 1 value per channel when training")
+        mom, eps = _bn_config(model)
+        s, keep = _params(model)
+        ws = _workspace(x.device, int(L.pcnerf_nof_train_fold_bytes(B, B)))
+        H.check(L.pcnerf_nof_forward_train_fused(x.data_ptr(), B, ctypes.byref(s), mom, eps, ws.data_ptr(),
+                                                 ws.numel(), out.data_ptr(), st))
         _track_batches(model, 1)
     elif model.training:
         if B <= 1:

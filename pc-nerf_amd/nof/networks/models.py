@@ -69,7 +69,10 @@ class _NOFBase(nn.Module):
 
     # ------------------------------------------------------------------ kernel plumbing
     def supported(self) -> bool:
-        return self.feature_size == 256 and self.in_channels_xy == 63 and self.use_skip
+        # the kernels evaluate every LeakyReLU(True) as the identity it is (negative_slope = True = 1); a module
+        # whose activations were changed is not this network
+        slopes_one = all(m.negative_slope == 1.0 for m in self.modules() if isinstance(m, nn.LeakyReLU))
+        return self.feature_size == 256 and self.in_channels_xy == 63 and self.use_skip and slopes_one
 
     def linears(self):
         return [self.layer1[i] for i in (0, 3, 6, 9)] + [self.layer2[i] for i in (0, 2, 4, 6)]

@@ -308,25 +308,90 @@ def grad_summary(m, seed):
 
 def gen_grads():
     """Parameter gradients of the train_kitti.py:117-155 loss through render_rays_train (train-mode BN, several
-    chunks), i.e. what loss.backward() produces in the reference's training step."""
+    chunks), i.e. what loss.backward() produces in the reference's training step.  Each case is run at 1 torch
+    thread and again at 4 (``alt:`` prefix): the reference's own spread under another summation order."""
     for name, (cl, seg, div) in GRAD_CASES.items():
         rays = syn.make_rays(96, seed=71)
-        emb, mc, mf = models(train=True)
-        res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=32, N_samples=64,
-                                  N_importance=128, perturb=0, noise_std=0, chunk=4096, issegmentated=seg,
-                                  childnerf_ratio=0.1, use_child_nerf_divide=div, use_child_nerf_loss=cl)
-        gt = torch.from_numpy(rays[:, 14])
-        lr, lrf = range_losses(res["depth"], res["depth_fine"], gt, torch.from_numpy(rays), div, 32)
-        total = lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"] + \
-            1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"]
-        total.sum().backward()
-        gc = {"c:" + k: v for k, v in grad_summary(mc, 81).items()}
-        gf = {"f:" + k: v for k, v in grad_summary(mf, 82).items()}
+        runs = []
+        for threads in (1, 4):
+            torch.set_num_threads(threads)
+            emb, mc, mf = models(train=True)
+            res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=32, N_samples=64,
+                                      N_importance=128, perturb=0, noise_std=0, chunk=4096, issegmentated=seg,
+                                      childnerf_ratio=0.1, use_child_nerf_divide=div, use_child_nerf_loss=cl)
+            gt = torch.from_numpy(rays[:, 14])
+            lr, lrf = range_losses(res["depth"], res["depth_fine"], gt, torch.from_numpy(rays), div, 32)
+            total = lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"] + \
+                1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"]
+            total.sum().backward()
+            out = {"c:" + k: v for k, v in grad_summary(mc, 81).items()}
+            out.update({"f:" + k: v for k, v in grad_summary(mf, 82).items()})
+            out["loss_total"] = t(total)
+            runs.append(out)
+        torch.set_num_threads(1)
         save(f"grads_{name}", rays=rays, use_child_nerf_loss=cl, issegmentated=seg, use_child_nerf_divide=div,
-             loss_total=t(total), **gc, **gf)
+             **runs[0], **{"alt:" + k: v for k, v in runs[1].items() if not k.endswith("@idx")})
 
 
-METRIC_SCENES = {"kitti": ("logs/kitti00/1151_1200_view/render_result", range(1150, 1200)),
+def grad_sample(m, seed, n=8192):
+    """Every gradient of a NOF: tensors of <= 512 entries in full, each weight matrix by ``n`` fixed entries (the
+    same indices for every run with the same seed) plus its float64 norm."""
+    out = {}
+    rng = np.random.default_rng(seed)
+    for k, p_ in m.named_parameters():
+        gr = p_.grad.detach().numpy()
+        if gr.size <= 512:
+            out[k] = gr
+        else:
+            idx = np.sort(rng.choice(gr.size, size=n, replace=False))
+            out[k + "@idx"] = idx
+            out[k + "@val"] = gr.reshape(-1)[idx]
+            out[k + "@norm"] = np.linalg.norm(gr.astype(np.float64))
+    return out
+
+
+def _grads_chunk(rays, n_child, threads):
+    """loss.backward() of train_kitti.py:117-155 (PC-NeRF shell settings, render.py:38-163 with the production
+    chunk=262,144: one full coarse BatchNorm chunk and three fine ones at 64/128 samples) on torch CPU."""
+    import time
+    torch.set_num_threads(threads)
+    emb, mc, mf = models(train=True)
+    t0 = time.perf_counter()
+    res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=n_child, N_samples=64,
+                              N_importance=128, **PCNERF_TRAIN)
+    gt = torch.from_numpy(rays[:, 14])
+    lr, lrf = range_losses(res["depth"], res["depth_fine"], gt, torch.from_numpy(rays), 0, 0)
+    total = lr + lrf + 1e6 * res["child_free_loss_fine"] + 1e6 * res["child_free_loss"] + \
+        1e5 * res["child_depth_loss_fine"] + 1e5 * res["child_depth_loss"]
+    total.sum().backward()
+    print(f"grads at chunk 262144 ({threads} threads): {time.perf_counter() - t0:.1f} s")
+    out = {"c:" + k: v for k, v in grad_sample(mc, 91).items()}
+    out.update({"f:" + k: v for k, v in grad_sample(mf, 92).items()})
+    out.update(loss_total=t(total), loss_range=t(lr), loss_range_fine=t(lrf), depth=t(res["depth"]),
+               depth_fine=t(res["depth_fine"]), child_free_loss=t(res["child_free_loss"]),
+               child_depth_loss=t(res["child_depth_loss"]), child_free_loss_fine=t(res["child_free_loss_fine"]),
+               child_depth_loss_fine=t(res["child_depth_loss_fine"]))
+    del res, total, mc, mf
+    torch.set_num_threads(1)
+    return out
+
+
+def gen_grads_chunk():
+    """Training-step gradients at the PRODUCTION BatchNorm chunk: 4,096 rays, 64/128 samples,
+    chunk 262,144 -- config 2's synthetic rays (make_rays(4096, seed=73)) and config 3's KITTI fixture rays
+    (scene_rays.npz kitti_train).  Each is run twice, at 8 and at 3 torch threads (the reference's own spread under
+    a different summation order), and both runs are stored (``alt:`` prefix for the second)."""
+    sc = scene_rays()
+    cases = {"grads_chunk_config2": (syn.make_rays(4096, seed=73), 32),
+             "grads_chunk_kitti": (sc["kitti_train"], int(sc["kitti_children"]))}
+    for name, (rays, n_child) in cases.items():
+        a = _grads_chunk(rays, n_child, 8)
+        b = _grads_chunk(rays, n_child, 3)
+        save(name, rays=rays, sub_nerf_test_num=n_child, N_samples=64, N_importance=128, chunk=262144, **a,
+             **{"alt:" + k: v for k, v in b.items() if not k.endswith("@idx")})
+
+
+METRIC_SCENES = {"kitti":("logs/kitti00/1151_1200_view/render_result", range(1150, 1200)),
                  "maicity": ("logs/maicity00/maicity_00_1/render_result", range(0, 50))}
 
 
@@ -496,7 +561,7 @@ def gen_self_spread():
 
 GENERATORS = [gen_maicity_frames, gen_kitti_frames, gen_metrics, gen_grads, gen_aabb, gen_render_rays, gen_nof,
               gen_pdf, gen_val, gen_train, gen_view, gen_pdf_pytest, gen_config1_kitti, gen_config4_maicity,
-              gen_config2_full, gen_self_spread]
+              gen_config2_full, gen_self_spread, gen_grads_chunk]
 
 if __name__ == "__main__":
     # python make_golden.py [name ...]  (names without the gen_ prefix; default: all)

@@ -39,3 +39,61 @@ def check_grads(get, keys, g, prefix, rtol, noise=1e-5):
         except AssertionError as e:
             bad.append(prefix + k + ": " + " ".join(str(e).split())[:300])
     assert not bad, "\n".join(bad)
+
+
+def _report(line):
+    """One JSON line per check into $PCNERF_PARITY_REPORT (the GPU run's parity report), when set."""
+    import json
+    import os
+    path = os.environ.get("PCNERF_PARITY_REPORT")
+    if path:
+        with open(path, "a") as fh:
+            fh.write(json.dumps(line) + "\n")
+
+
+def check_grads_elem(get, keys, g, prefix, case, rtol=1e-4, spread_k=1.5, floor_k=6.0, noise=1e-5):
+    """Per-element gradient parity against a reference run ``g`` that also holds the SAME computation rerun under
+    another summation order (``alt:`` keys: the reference at another torch thread count).  Entry i of a tensor passes
+    when |hip_i - ref_i| <= max(rtol |ref_i|, spread_k |ref_i - alt_i| + floor), floor = floor_k x the RMS over the
+    tensor of |ref - alt| (one rerun samples the reference's rounding noise once per entry; the floor carries its
+    typical size).  Weight matrices are compared on their stored entries and by norm; the mathematically-zero
+    gradients only at noise level.  Returns {tensor: (max err/tol, max |err| / max |ref|)} and reports it."""
+    bad, worst = [], {}
+    nz = noise_level_grads()
+    for k in keys:
+        gr = np.asarray(get(k), dtype=np.float64)
+        try:
+            if k in nz:
+                ref_scale = np.abs(g[prefix + nz[k]]).max()
+                assert np.abs(gr).max() <= noise * ref_scale, (np.abs(gr).max(), ref_scale)
+                continue
+            if prefix + k in g:
+                ref = g[prefix + k].astype(np.float64).ravel()
+                alt = g["alt:" + prefix + k].astype(np.float64).ravel()
+                hip = gr.ravel()
+            else:
+                idx = g[prefix + k + "@idx"]
+                ref = g[prefix + k + "@val"].astype(np.float64)
+                alt = g["alt:" + prefix + k + "@val"].astype(np.float64)
+                hip = gr.reshape(-1)[idx]
+                nr, na = float(g[prefix + k + "@norm"]), float(g["alt:" + prefix + k + "@norm"])
+                assert abs(np.linalg.norm(gr) - nr) <= rtol * nr + spread_k * abs(nr - na), \
+                    ("norm", np.linalg.norm(gr), nr, na)
+            spread = np.abs(ref - alt)
+            floor = floor_k * np.sqrt(np.mean(spread ** 2))
+            tol = np.maximum(rtol * np.abs(ref), spread_k * spread + floor)
+            err = np.abs(hip - ref)
+            ratio = err / np.maximum(tol, 1e-300)
+            i = int(np.argmax(ratio))
+            worst[k] = (float(ratio[i]), float(err.max() / max(np.abs(ref).max(), 1e-300)))
+            assert ratio[i] <= 1.0, (f"entry {i}: hip {hip[i]:.9g} ref {ref[i]:.9g} alt {alt[i]:.9g} tol {tol[i]:.3g}; "
+                                     f"{int((ratio > 1).sum())} of {ratio.size} entries over")
+        except AssertionError as e:
+            bad.append(prefix + k + ": " + " ".join(str(e).split())[:300])
+    if worst:
+        kw = max(worst, key=lambda x: worst[x][0])
+        _report({"case": case, "prefix": prefix, "tensors": len(worst), "max_err_over_tol": worst[kw][0],
+                 "worst_tensor": kw, "max_abs_err_over_tensor_max": max(v[1] for v in worst.values()),
+                 "failed": len(bad)})
+    assert not bad, "\n".join(bad)
+    return worst

@@ -64,7 +64,11 @@ def test_math_switches_without_gpu():
     """pcnerf_set_train_math / pcnerf_set_eval_math: process-wide selectors, previous mode returned, invalid modes
     refused with a message (no GPU call involved)."""
     from nof import _ops, _hip
-    assert _ops.get_train_math() == "f16x2_3" and _ops.get_eval_math() == "f16x2_3"
+    assert _ops.get_train_math() == "f16x2_3_fused" and _ops.get_eval_math() == "f16x2_3"
+    assert _ops.set_train_math("f16x2_3") == "f16x2_3_fused"
+    assert _ops.set_train_math("fp32") == "f16x2_3"
+    assert _ops.set_train_math("f16x2_3_fused") == "fp32"
+    assert _ops.get_train_math() == "f16x2_3_fused"
     assert _ops.set_eval_math("fp32") == "f16x2_3"
     assert _ops.set_eval_math("f16x2_3") == "fp32"
     assert _hip.lib().pcnerf_set_eval_math(7) == -1

@@ -137,7 +137,7 @@ def check_train(res, g, rays, mc, mf, pre="", name="", f64=None, alt=None):
 
 
 # ----------------------------------------------------------------------------------------------- config 2
-@pytest.fixture(params=["f16x2_3", "fp32"])
+@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused"])
 def train_math(request):
     """The train-mode layer arithmetic (nof._ops.set_train_math): the default split-fp16 products and fp32 MFMA."""
     from nof import _ops

@@ -135,7 +135,7 @@ def test_render_val(S, eval_math):
 TRAIN = ["pcnerf", "pcnerf_noseg", "pcnerf_divide", "original", "pcnerf_perturb", "pcnerf_s128"]
 
 
-@pytest.fixture(params=["f16x2_3", "fp32"])
+@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused"])
 def train_math(request):
     """The train-mode layer arithmetic (nof._ops.set_train_math): the default split-fp16 products and fp32 MFMA."""
     from nof import _ops
