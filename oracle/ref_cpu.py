@@ -196,18 +196,24 @@ def child_losses(w, z, rays, near_far_child, ranges, divide, sub_num, eps=1e-10)
 # ----------------------------------------------------------------------------------------------- render paths
 def render_rays_train(Pc, Pf, rays, sub_nerf_test_num=4, N_samples=64, N_importance=128, perturb=0, noise_std=1,
                       chunk=3072, issegmentated=0, childnerf_ratio=0.5, use_child_nerf_divide=0,
-                      use_child_nerf_loss=0, training=True, draws=None):
+                      use_child_nerf_loss=0, training=True, draws=None, f64=False):
     """render.py:416-482 with inference_train (:38-163).  ``draws`` may carry the RNG tensors the reference
-    would consume: ``perturb_rand`` (R,S), ``noise`` (R,S), ``u`` (R,I), ``noise_fine`` (R,S+I)."""
+    would consume: ``perturb_rand`` (R,S), ``noise`` (R,S), ``u`` (R,I), ``noise_fine`` (R,S+I).
+    ``f64``: the float64 evaluation of tests/golden/make_f64.py -- coarse z and points rounded in float32 exactly as
+    the reference rounds them (float32 ``rays``), everything after them (network with float64 ``Pc``/``Pf``,
+    BatchNorm, compositing, losses, sample_pdf, fine points) in float64."""
     draws = draws or {}
     R = rays.shape[0]
     z = coarse_z(rays, N_samples, issegmentated, childnerf_ratio)
     if perturb > 0:
         z = perturb_z(z, perturb, draws["perturb_rand"] if "perturb_rand" in draws else torch.rand(z.shape))
+    pts_c = points(rays, z)
+    if f64:
+        pts_c, z, rays = pts_c.double(), z.double(), rays.double()
     nfc, ranges = rays[:, 10:12], rays[:, 14]
 
-    def pass_(P, z, noise):
-        p = query(P, points(rays, z), training, chunk)
+    def pass_(P, z, noise, pts=None):
+        p = query(P, points(rays, z) if pts is None else pts, training, chunk)
         nz = None if noise_std == 0 else noise * noise_std
         w, depth = composite(p, z, 1e-10, nz)
         if use_child_nerf_loss:
@@ -216,7 +222,7 @@ def render_rays_train(Pc, Pf, rays, sub_nerf_test_num=4, N_samples=64, N_importa
             fl, dl = torch.tensor(0.0), torch.tensor(0.0)
         return w, depth, fl, dl
 
-    w, depth, fl, dl = pass_(Pc, z, draws.get("noise"))
+    w, depth, fl, dl = pass_(Pc, z, draws.get("noise"), pts_c)
     zmid = .5 * (z[..., 1:] + z[..., :-1])
     zs = sample_pdf(zmid, w[..., 1:-1], N_importance, det=(perturb == 0.), u=draws.get("u")).detach()  # :466
     zf = torch.sort(torch.cat([z, zs], -1), -1)[0]

@@ -12,6 +12,7 @@
 // (feature map FEAT_H below): the whole chain runs without LDS or lane shuffles.  The encoding feeds layer 1
 // (and the skip half of layer 5) with feature(t, h) = 2t + h.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "pcnerf_internal.h"
@@ -487,11 +488,41 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__
 #define PCN_EH2_T 3
 #endif
 constexpr int E2_T = PCN_EH2_T;   // sample tiles per block
+#ifndef PCN_EH2_RING
+#define PCN_EH2_RING 4    // k_nof_eval_h2: weight-ring slots (prefetch distance RING - 1 k-steps); 4 or 8
+#endif
+constexpr int RG = PCN_EH2_RING, RD = RG - 1;
+#ifndef PCN_EH2_ROT
+#define PCN_EH2_ROT 0     // TR: each block walks its hidden k-steps rotated by blockIdx (spreads the L2 weight reads)
+#endif
+#ifndef PCN_EH2_ABL
+#define PCN_EH2_ABL 0     // diagnostic timing ablations (wrong results): 1 weights of k-step 0 only, 2 no B re-reads
+#endif
+#ifndef PCN_EH2_STAMP
+#define PCN_EH2_STAMP 0   // diagnostic builds only: per-block phase stamps of k_nof_eval_h2 (pcnerf_debug_eh2_clock)
+#endif
+#if PCN_EH2_STAMP
+// [block][0]: s_memrealtime at entry, [1]: at exit; [2 + i]: s_memtime at phase i (entry, prologue done, layer 0..7
+// done, exit); [13..15]: layer 2's k-loop done, first barrier passed, split outputs written
+__device__ unsigned long long g_eh2_clk[8192][16];
+#define EH2_STAMP(i)                                                                   \
+  if (t == 0 && blockIdx.x < 8192 && blockIdx.y == 0) {                               \
+    g_eh2_clk[blockIdx.x][2 + (i)] = __builtin_amdgcn_s_memtime();                     \
+    if ((i) == 0) g_eh2_clk[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();         \
+    if ((i) == 10) g_eh2_clk[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();        \
+  }
+#else
+#define EH2_STAMP(i)
+#endif
 // TR (the train-mode query, pcnerf_nof_query_train_fused): the image holds the RAW weights (no BatchNorm fold) and
-// each layer's epilogue applies its chunk's BatchNorm as (acc 2^-(sw+sx)) alpha + beta'' -- alpha = fl32(invstd)
-// gamma and beta'' = beta - mean(W x) alpha from the chunk's batch statistics (coef[chunk][L][alpha 256 | beta''
-// 256], nof_fold.hip k_tf_coeffs); blockIdx.y is the BatchNorm chunk, blockIdx.x the 96-sample block inside it, so
-// no block straddles two chunks.
+// each layer's epilogue applies its chunk's BatchNorm -- alpha = fl32(invstd) gamma, beta'' = beta - mean(W x) alpha
+// from the chunk's exact batch statistics (nof_fold.hip k_tf_coeffs) -- as ONE fma per value that also moves the
+// result to the next layer's operand scale: BatchNorm output k of a chunk of n samples has batch mean beta_k and
+// batch variance <= gamma_k^2, so no sample exceeds sqrt(n) |gamma_k| + |beta_k| (Samuelson), and that bound fixes a
+// per-layer power-of-two scale sxB[L] in advance (k_tf_coeffs): no per-sample maxima, no exchange of them between
+// the waves.  Only the encoding (layers 0 and 4) keeps a per-sample scale, min(its own, sxB[3]).  blockIdx.y is the
+// BatchNorm chunk, blockIdx.x the 96-sample block inside it, so no block straddles two chunks.
+// coef per chunk: [L][alpha 256 | beta'' 256] floats, then sxB[8] as int (TQ_COEF_FLOATS floats per chunk).
 template <bool TR>
 __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict__ rays, int stride,
                                                         const float* __restrict__ z, int64_t total, int S,
@@ -501,23 +532,32 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   __shared__ eh_f16x8 act[16][E2_T][2][64];
   __shared__ eh_f16x8 eb[4][E2_T][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
   __shared__ int sx0s[E2_T * 32];
-  // eval: the 8 layers' folded biases; TR: the chunk's [L][alpha | beta''] BatchNorm coefficients
+  // eval: the 8 layers' folded biases; TR: the chunk's [L][A | B] epilogue coefficients (see below)
   __shared__ __attribute__((aligned(16))) float sbias[(TR ? 16 : 8) * 256];
   __shared__ float emax[E2_T * 32];
-  __shared__ float smax[4][E2_T * 32];
+  __shared__ float smax[4][E2_T * 32];   // (eval)
   __shared__ float pdot[4][E2_T * 32];
+  __shared__ float spos[E2_T * 32][3];
   const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, h = lane >> 5, li = lane & 31;
   // samples [s0, send) of this block
   const int64_t cb = TR ? (int64_t)blockIdx.y * chunk : 0;
   const int64_t s0 = cb + (int64_t)blockIdx.x * (32 * E2_T);
   const int64_t send = TR ? (cb + chunk < total ? cb + chunk : total) : total;
   if (s0 >= send) return;   // (the last chunk's surplus blocks; uniform over the block, before any barrier)
+  EH2_STAMP(0);
   const eh_f16x8* __restrict__ img = reinterpret_cast<const eh_f16x8*>(W + OFF_EH);
   int sw[8];
 #pragma unroll
   for (int L = 0; L < 8; ++L) sw[L] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(W + OFF_EH_SW)[L]);
+  int sxB[8];   // TR: the per-layer output scales (layer 7: 0, its output is not split)
+  if (TR) {
+    const int* cs = reinterpret_cast<const int*>(coef + blockIdx.y * (size_t)TQ_COEF_FLOATS + 16 * 256);
+#pragma unroll
+    for (int L = 0; L < 8; ++L) sxB[L] = __builtin_amdgcn_readfirstlane(L < 7 ? cs[L] : 0);
+  }
   // this wave's A operands of k-step gk: out-blocks 2w + o, parts hi / mid
   auto load_w = [&](eh_f16x8 (&d)[2][2], int gk) {
+    if (PCN_EH2_ABL & 1) gk = 0;
 #pragma unroll
     for (int o = 0; o < 2; ++o)
 #pragma unroll
@@ -526,35 +566,81 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   // ring of 4 k-steps of A operands, slot = k-step index within its layer & 3 (every layer's k-step count and
   // start are multiples of 4, so the slot is a compile-time index in the unrolled k-loops and no in-flight load's
   // registers are ever copied): k-step s issues the loads of k-step s + 3 into the slot k-step s - 1 just used
-  eh_f16x8 wr4[4][2][2];
-  load_w(wr4[0], 0);
-  load_w(wr4[1], 1);
-  load_w(wr4[2], 2);
+  // hidden k-steps walked from k-step rot of their layer (TR && PCN_EH2_ROT): the image k-step of processing step q
+  const int rot = (TR && PCN_EH2_ROT) ? (int)(blockIdx.x & 15) : 0;
+  auto kmap = [&](int q) __attribute__((always_inline)) {
+    if (q < 4 || (q >= 52 && q < 56) || q >= EH_KSTEPS) return q < EH_KSTEPS ? q : EH_KSTEPS - 1;
+    const int st = q < 52 ? 4 + ((q - 4) & ~15) : 56 + ((q - 56) & ~15);
+    return st + ((q - st + rot) & 15);
+  };
+  eh_f16x8 wr4[RG][2][2];
+#pragma unroll
+  for (int k = 0; k < RD; ++k) load_w(wr4[k], kmap(k));
   if (TR) {
-    const f32x4* cf = reinterpret_cast<const f32x4*>(coef + blockIdx.y * (size_t)(16 * 256));
-    for (int i = t; i < 16 * 256 / 4; i += 256) reinterpret_cast<f32x4*>(sbias)[i] = cf[i];
+    // the chunk's coefficients as the epilogue's fma operands: A = alpha 2^(sxout - sw_L - sxin_L), B = beta''
+    // 2^sxout, with sxin_L = sxB[L-1] for the uniformly scaled inputs (layers 1-3, 5-7) and 0 for layers 0 and 4,
+    // whose per-sample input scale is removed by an exact multiply first (powers of two: exact)
+    const f32x4* cf = reinterpret_cast<const f32x4*>(coef + blockIdx.y * (size_t)TQ_COEF_FLOATS);
+    f32x4 cv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) cv[m] = cf[t + 256 * m];   // all four loads in flight together
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int i = 4 * (t + 256 * m), L = i >> 9, isb = (i >> 8) & 1;
+      const int sxo = sxB[L], sxi = (L == 0 || L == 4) ? 0 : sxB[L - 1];
+      const int e = isb ? sxo : sxo - sw[L] - sxi;
+      reinterpret_cast<f32x4*>(sbias)[t + 256 * m] =
+          f32x4{ldexpf(cv[m][0], e), ldexpf(cv[m][1], e), ldexpf(cv[m][2], e), ldexpf(cv[m][3], e)};
+    }
   } else {
     for (int i = t; i < 8 * 256 / 4; i += 256)
       reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
   }
+  // prologue: the block's encodings, the 30 sincosf per sample spread over all 256 threads (encode_full's
+  // arithmetic, bit for bit), staged as floats in the (still unused) activation buffer
+  float* const encf = reinterpret_cast<float*>(&act[0][0][0][0]);   // [sample][65]
+  static_assert(sizeof(act) >= 32 * E2_T * 65 * sizeof(float), "encoding staging area");
+  if (!ein) {
+    if (t < 32 * E2_T) {
+      int64_t g = s0 + t;
+      if (g >= send) g = send - 1;
+      float p[3];
+      sample_point(rays + (g / S) * stride, z[g], p);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        spos[t][m] = p[m];
+        encf[t * 65 + m] = p[m];
+      }
+      encf[t * 65 + 63] = 0.0f;
+    }
+    __syncthreads();
+    for (int i = t; i < 32 * E2_T * 30; i += 256) {
+      const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
+      float sv, cv;
+      sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
+      encf[sm * 65 + 3 + 6 * k + m] = sv;
+      encf[sm * 65 + 6 + 6 * k + m] = cv;
+    }
+    __syncthreads();
+  }
   if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
-    int64_t g = s0 + t;
-    if (g >= send) g = send - 1;
     float f[64];
     if (ein) {
+      int64_t g = s0 + t;
+      if (g >= send) g = send - 1;
 #pragma unroll
       for (int k = 0; k < 63; ++k) f[k] = ein[g * 63 + k];
       f[63] = 0.0f;
     } else {
-      float p[3];
-      sample_point(rays + (g / S) * stride, z[g], p);
-      encode_full(p, f);
+#pragma unroll
+      for (int k = 0; k < 64; ++k) f[k] = encf[t * 65 + k];
     }
     const int tau = t >> 5, l = t & 31;
     float m = 0.0f;
 #pragma unroll
     for (int k = 0; k < 63; ++k) m = fmaxf(m, fabsf(f[k]));
-    const int sx0 = eh_scale(m);
+    int sx0 = eh_scale(m);
+    if (TR && sxB[3] < sx0) sx0 = sxB[3];   // the encoding shares layer 4's input scale with h3
     const float xs = ldexpf(1.0f, sx0);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -572,6 +658,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     sx0s[t] = sx0;
   }
   __syncthreads();
+  EH2_STAMP(1);
   int sxl[E2_T];   // the per-sample scale of the current layer's B operands (this lane's sample of each tile)
 #pragma unroll
   for (int tau = 0; tau < E2_T; ++tau) sxl[tau] = sx0s[32 * tau + li];
@@ -580,9 +667,11 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   // one k-step: B operands of the 3 tiles (from the encoding at the lane's scale, or the split activations),
   // MFMAs product-major over the 6 accumulators
   eh_f16x8 pbh[E2_T], pbm[E2_T];   // PCN_EH2_PF: the next hidden k-step's B operands, read during this one
-  auto kstep = [&](int s, int pos, bool enc, bool first) {   // pos: the k-step's index within its layer
-    if (gk + 3 < EH_KSTEPS) load_w(wr4[(pos + 3) & 3], gk + 3);
-    const eh_f16x8 (&wc)[2][2] = wr4[pos & 3];
+  auto kstep = [&](int s, int pos, bool enc, bool first) __attribute__((always_inline)) {   // pos: the k-step's index within its layer
+    // (k-steps past the end reload the last one: unconditional loads keep the ring's registers statically known
+    // to the waitcnt pass -- a conditional load made it wait for every load in flight)
+    load_w(wr4[(pos + RD) & (RG - 1)], kmap(gk + RD));
+    const eh_f16x8 (&wc)[2][2] = wr4[pos & (RG - 1)];
     eh_f16x8 bh[E2_T], bm[E2_T];
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
@@ -592,8 +681,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       } else if (enc) {
         bh[tau] = eb[s][tau][0][lane];
         bm[tau] = eb[s][tau][1][lane];
-        const int d = sxl[tau] - sx0s[32 * tau + li];
-        if (d != 0) {   // layer 4: the 22-bit encoding (hi + mid, exact in fp32) re-split at the shared scale
+        const int d = TR ? 0 : sxl[tau] - sx0s[32 * tau + li];
+        if (d != 0) {   // eval layer 4: the 22-bit encoding (hi + mid, exact in fp32) re-split at the shared scale
           const float xs = ldexpf(1.0f, d);
           float v[8];
 #pragma unroll
@@ -629,9 +718,9 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
         acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
     ++gk;
   };
-  // epilogue phase 1: acc <- acc 2^-(sw + sx) + bias (TR: (acc 2^-(sw + sx)) alpha + beta''), this wave's
-  // per-sample maxima -> smax[w]
-  auto epi1 = [&](int L) {
+  // eval epilogue phase 1: acc <- fl(acc 2^-(sw + sx) + bias) (one fma: the power-of-two product is exact), this
+  // wave's per-sample maxima -> smax[w]
+  auto epi1 = [&](int L) __attribute__((always_inline)) {
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
       const float us = ldexpf(1.0f, -(sw[L] + sxl[tau]));
@@ -640,13 +729,10 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       for (int o = 0; o < 2; ++o)
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          const int nb = 32 * (2 * w + o) + 8 * gq + 4 * h;
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + (TR ? 512 * L + 256 : 256 * L) + nb);
-          f32x4 a = {};
-          if (TR) a = *reinterpret_cast<const f32x4*>(sbias + 512 * L + nb);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + 256 * L + 32 * (2 * w + o) + 8 * gq + 4 * h);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float v = TR ? (acc[o][tau][4 * gq + q] * us) * a[q] + b[q] : acc[o][tau][4 * gq + q] * us + b[q];
+            const float v = __builtin_fmaf(acc[o][tau][4 * gq + q], us, b[q]);
             acc[o][tau][4 * gq + q] = v;
             m = fmaxf(m, fabsf(v));
           }
@@ -655,53 +741,174 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       if (h == 0) smax[w][32 * tau + li] = m;
     }
   };
-  // phase 2 (after a barrier): the next layer's per-sample scale and this wave's k-steps 4w .. 4w+3 of its B operands
-  auto epi2 = [&](bool with_e) {
+  // split of this wave's outputs into the next layer's B operands (k-steps 4w .. 4w+3), at scale xs per tile
+  // (SC false: already at their scale; a compile-time choice, so no select per value)
+  auto split_out = [&](const float (&xs)[E2_T], auto SC) {
 #pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) {
-      const int sm = 32 * tau + li;
-      float m = fmaxf(fmaxf(smax[0][sm], smax[1][sm]), fmaxf(smax[2][sm], smax[3][sm]));
-      if (with_e) m = fmaxf(m, emax[sm]);
-      sxl[tau] = eh_scale(m);
-      const float xs = ldexpf(1.0f, sxl[tau]);
+    for (int tau = 0; tau < E2_T; ++tau)
 #pragma unroll
       for (int o = 0; o < 2; ++o)
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           float v[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = acc[o][tau][8 * k + j] * xs;
+          for (int j = 0; j < 8; ++j) v[j] = decltype(SC)::value ? acc[o][tau][8 * k + j] * xs[tau] : acc[o][tau][8 * k + j];
           eh_f16x8 hi, mid;
           eh_split8(v, hi, mid);
           const int s = 4 * w + 2 * o + k;
           act[s][tau][0][lane] = hi;
           act[s][tau][1][lane] = mid;
         }
+  };
+  // eval phase 2 (after a barrier): the next layer's per-sample scale and this wave's B operands
+  auto epi2 = [&](bool with_e) __attribute__((always_inline)) {
+    float xs[E2_T];
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau) {
+      const int sm = 32 * tau + li;
+      float m = fmaxf(fmaxf(smax[0][sm], smax[1][sm]), fmaxf(smax[2][sm], smax[3][sm]));
+      if (with_e) m = fmaxf(m, emax[sm]);
+      sxl[tau] = eh_scale(m);
+      xs[tau] = ldexpf(1.0f, sxl[tau]);
+    }
+    split_out(xs, std::true_type{});
+  };
+  // TR epilogue: acc <- fma(acc [2^-sx(sample)], A, B) = the next layer's input at its scale (layer 3: times
+  // 2^(sx0(sample) - sxB[3]) where the encoding's own scale is the smaller)
+  auto epi_tr = [&](int L, auto PS) __attribute__((always_inline)) {   // PS: the input has a per-sample scale (layers 0 and 4)
+    constexpr bool ps = decltype(PS)::value;
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau) {
+      const float us = ps ? ldexpf(1.0f, -sxl[tau]) : 1.0f;
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int nb = 32 * (2 * w + o) + 8 * gq + 4 * h;
+          const f32x4 a = *reinterpret_cast<const f32x4*>(sbias + 512 * L + nb);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + 512 * L + 256 + nb);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float v = acc[o][tau][4 * gq + q];
+            if (ps) v *= us;
+            acc[o][tau][4 * gq + q] = __builtin_fmaf(v, a[q], b[q]);
+          }
+        }
+    }
+  };
+  // the 16 hidden k-steps of a layer (B operands in act), software-pipelined: per k-step the products run in the
+  // order Wh.xm, Wh.xh, Wm.xh, and k-step s + 1's xm is read from LDS once Wh.xm of s is issued, its xh once Wm.xh
+  // of s is -- every LDS read has at least six MFMAs in flight to cover it
+  auto hidden_ksteps = [&](int pos0, bool first) __attribute__((always_inline)) {
+    eh_f16x8 bh[E2_T], bm[E2_T];
+#pragma unroll
+    for (int tau = 0; tau < E2_T; ++tau) {
+      bm[tau] = act[rot][tau][1][lane];
+      bh[tau] = act[rot][tau][0][lane];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int pos = pos0 + s;
+      load_w(wr4[(pos + RD) & (RG - 1)], kmap(gk + RD));
+      const eh_f16x8 (&wc)[2][2] = wr4[pos & (RG - 1)];
+#pragma unroll
+      for (int tau = 0; tau < E2_T; ++tau)
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+          acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bm[tau], (first && s == 0) ? f32x16{} : acc[o][tau], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < 16 && !(PCN_EH2_ABL & 2)) {
+#pragma unroll
+        for (int tau = 0; tau < E2_T; ++tau) bm[tau] = act[(s + 1 + rot) & 15][tau][1][lane];
+      }
+      __builtin_amdgcn_sched_barrier(0);   // (else the scheduler sinks the reads down to their use)
+#pragma unroll
+      for (int tau = 0; tau < E2_T; ++tau)
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+          acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bh[tau], acc[o][tau], 0, 0, 0);
+#pragma unroll
+      for (int tau = 0; tau < E2_T; ++tau)
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+          acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < 16 && !(PCN_EH2_ABL & 2)) {
+#pragma unroll
+        for (int tau = 0; tau < E2_T; ++tau) bh[tau] = act[(s + 1 + rot) & 15][tau][0][lane];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      ++gk;
     }
   };
 #pragma unroll
   for (int s = 0; s < 4; ++s) kstep(s, s, true, s == 0);
-  epi1(0);
-  __syncthreads();
-  epi2(false);
-  __syncthreads();
-#pragma unroll 1
-  for (int L = 1; L < 8; ++L) {
-    if (L == 4) {
+  if (TR) {
+    epi_tr(0, std::true_type{});
+    float xs[E2_T];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) kstep(s, s, true, s == 0);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) kstep(s, 4 + s, false, false);
-    } else {
-#pragma unroll
-      for (int s = 0; s < 16; ++s) kstep(s, s, false, s == 0);
+    for (int tau = 0; tau < E2_T; ++tau) {
+      sxl[tau] = sxB[0];
+      xs[tau] = 1.0f;
     }
-    epi1(L);
     __syncthreads();
-    if (L < 7) {
-      epi2(L == 3);
+    split_out(xs, std::false_type{});
+    __syncthreads();
+  } else {
+    epi1(0);
+    __syncthreads();
+    epi2(false);
+    __syncthreads();
+  }
+  EH2_STAMP(2);
+  // epilogue of layers 1-7 (TR: fma to the next operand scale; eval: per-sample scales through smax)
+  auto layer_end = [&](int L) __attribute__((always_inline)) {
+    if (L == 2) EH2_STAMP(11);
+    if (TR) {
+      if (L == 4) epi_tr(4, std::true_type{});
+      else epi_tr(L, std::false_type{});
+      if (L < 7) {
+        float xs[E2_T];
+#pragma unroll
+        for (int tau = 0; tau < E2_T; ++tau) {
+          const int sx0 = sx0s[32 * tau + li];
+          sxl[tau] = L == 3 ? sx0 : sxB[L];
+          xs[tau] = ldexpf(1.0f, sx0 - sxB[3]);
+        }
+        __syncthreads();
+        if (L == 2) EH2_STAMP(12);
+        if (L == 3) split_out(xs, std::true_type{});
+        else split_out(xs, std::false_type{});
+        if (L == 2) EH2_STAMP(13);
+        __syncthreads();
+      }
+    } else {
+      epi1(L);
       __syncthreads();
+      if (L == 2) EH2_STAMP(12);
+      if (L < 7) {
+        epi2(L == 3);
+        if (L == 2) EH2_STAMP(13);
+        __syncthreads();
+      }
     }
+    EH2_STAMP(2 + L);
+  };
+  // the weight ring's slot of global k-step g is g mod RG; each call site below passes its layer's start mod RG
+  // (layer starts: 0, 4, 20, 36, 52 (+4 encoding k-steps), 72, 88, 104), so every slot index is a constant
+#pragma unroll 1
+  for (int L = 1; L <= 3; ++L) {
+    hidden_ksteps(4 % RG, true);
+    layer_end(L);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) kstep(s, 52 % RG + s, true, s == 0);
+  hidden_ksteps(56 % RG, false);
+  layer_end(4);
+#pragma unroll 1
+  for (int L = 5; L <= 7; ++L) {
+    hidden_ksteps(72 % RG, true);
+    layer_end(L);
   }
   // occ_out: this wave's 64 neurons per sample, then the 4 partial sums in order
 #pragma unroll
@@ -723,6 +930,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     const float logit = ((pdot[0][t] + pdot[1][t]) + (pdot[2][t] + pdot[3][t])) + W[OFF_BOUT];
     p_out[s0 + t] = sigmoid_ref(logit);
   }
+  EH2_STAMP(10);
 }
 
 // Eval-mode MLP arithmetic: 0 = fp32 MFMA (k_nof_eval), 1 = split fp16, 3 products (k_nof_eval_h, default).
@@ -1018,6 +1226,33 @@ extern "C" int pcnerf_nof_forward_eval(const float* emb, int64_t n, const float*
   PCN_LAUNCH_CHECK("pcnerf_nof_forward_eval");
   PCN_API_END
 }
+
+#if PCN_EH2_STAMP
+#include <vector>
+// diagnostic builds: out[0] = median in-kernel clock (MHz) of the last k_nof_eval_h2 launch's stamped blocks,
+// out[1 + i] = median cycles of phase i (0 prologue, 1 layer 0, ..., 8 layer 7, 9 occ_out), out[11..13] layer 2's
+// k-loop / epilogue + first barrier / split, out[14] = blocks
+extern "C" int pcnerf_debug_eh2_clock(double* out) {
+  static unsigned long long h[8192][16];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(pcn::g_eh2_clk), sizeof(h)) != hipSuccess) return 1;
+  std::vector<std::vector<double>> ph(14);
+  for (int b = 0; b < 8192; ++b) {
+    if (h[b][1] <= h[b][0] || h[b][12] <= h[b][2]) continue;
+    ph[0].push_back((double)(h[b][12] - h[b][2]) / (double)(h[b][1] - h[b][0]) * 100.0);
+    for (int i = 0; i < 10; ++i) ph[1 + i].push_back((double)(h[b][3 + i] - h[b][2 + i]));
+    ph[11].push_back((double)(h[b][13] - h[b][4]));   // layer 2: k-loop (from layer 1's end)
+    ph[12].push_back((double)(h[b][14] - h[b][13]));  // epilogue 1 + first barrier
+    ph[13].push_back((double)(h[b][15] - h[b][14]));  // scales + split + LDS writes
+  }
+  if (ph[0].empty()) return 2;
+  for (int i = 0; i < 14; ++i) {
+    std::sort(ph[i].begin(), ph[i].end());
+    out[i] = ph[i][ph[i].size() / 2];
+  }
+  out[14] = (double)ph[0].size();
+  return 0;
+}
+#endif
 
 extern "C" int pcnerf_set_eval_math(int mode) {
   if (mode < 0 || mode > 1) {

@@ -57,7 +57,7 @@ struct FoldDev {   // device views of the fold state (float64 throughout)
   double* dg;      // [8][C][256] dgamma per chunk
   double* dw;      // [G][256][256] weight-gradient partials (h columns)
   double* vec;     // [C][576] d out_w (256), d beta_7 (256), d out_b (1)
-  float* coef;     // [C][8][alpha 256 | beta'' 256] the chunks' BatchNorm coefficients (train-mode query)
+  float* coef;     // [C][TQ_COEF_FLOATS] the chunks' BatchNorm coefficients and operand scales (train-mode query)
   float* img;      // the train-mode query's weight image (train_query_image_floats)
 };
 
@@ -78,7 +78,7 @@ static FoldLayout fold_layout(int64_t total, int64_t chunk) {
   const size_t C = (size_t)F.C, wpc = (size_t)F.wpc, G = (size_t)F.G;
   const size_t n[FOLD_PIECES] = {C * wpc * 4096, C * 4096, C * 64, C * 64, 8 * C * 256 * 64, 8 * C * 256 * 64,
                                  8 * C * 1024, C * 64, C * wpc * 64, 2 * C * 256 * 64, 8 * C * 256, G * 256 * 256,
-                                 C * 576, C * 8 * 512 / 2, (train_query_image_floats() + 1) / 2};
+                                 C * 576, C * TQ_COEF_FLOATS / 2, (train_query_image_floats() + 1) / 2};
   size_t o = 0;
   for (int i = 0; i < FOLD_PIECES; ++i) {
     F.off[i] = o;
@@ -462,18 +462,33 @@ __global__ __launch_bounds__(256) void k_tf_out(NofParamsDev P, FoldDev F) {
 // grid C, 256 threads: each chunk's BatchNorm coefficients for the train-mode query, bn_coeffs' (nof_train.hip)
 // arithmetic on the chunk's exact batch statistics: invstd = fl32(1 / sqrt(var + eps)) (biased variance), alpha =
 // invstd * gamma, and beta'' = beta - mean(W x) alpha with mean(W x) = P'[:, 63] -- the Linear's bias cancels
-// inside BatchNorm, so the query's epilogue is (W x) alpha + beta''.
-__global__ __launch_bounds__(256) void k_tf_coeffs(NofParamsDev P, FoldDev F) {
+// inside BatchNorm, so the query's epilogue is (W x) alpha + beta''.  Then the operand scale of each layer's output:
+// BatchNorm output k has batch mean beta_k and batch variance gamma_k^2 var / (var + eps) <= gamma_k^2, so by
+// Samuelson's inequality no sample of the chunk exceeds sqrt(n) |gamma_k| + |beta_k|; sxB[L] puts the layer's
+// largest such bound in [2^14, 2^15) (fp16's range with a factor-2 margin for rounding).
+__global__ __launch_bounds__(256) void k_tf_coeffs(NofParamsDev P, FoldDev F, SampleSrc q) {
+  __shared__ float red[4];
   const int c = blockIdx.x, k = threadIdx.x;
   const int64_t C = F.C;
+  const float rn = sqrtf((float)chunk_len(q, c));
+  float* o = F.coef + (int64_t)c * TQ_COEF_FLOATS;
   for (int L = 0; L < 8; ++L) {
     const double* sr = F.sr + ((int64_t)L * C + c) * 1024;
     const double m = F.pp[(((int64_t)L * C + c) * 256 + k) * 64 + 63];
     const float invstd = (float)(1.0 / sqrt(sr[768 + k] + (double)P.eps));
     const float a = invstd * P.bn_w[L][k];
-    float* o = F.coef + ((int64_t)c * 8 + L) * 512;
-    o[k] = a;
-    o[256 + k] = (float)((double)P.bn_b[L][k] - m * (double)a);
+    o[L * 512 + k] = a;
+    o[L * 512 + 256 + k] = (float)((double)P.bn_b[L][k] - m * (double)a);
+    float bnd = wave_max_f(rn * fabsf(P.bn_w[L][k]) + fabsf(P.bn_b[L][k]));
+    if ((k & 63) == 0) red[k >> 6] = bnd;
+    __syncthreads();
+    if (k == 0) {
+      bnd = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      int sx = (bnd > 0.0f && bnd < 3.0e38f) ? 14 - ilogbf(bnd) : 0;
+      sx = sx > 64 ? 64 : sx < -64 ? -64 : sx;
+      reinterpret_cast<int*>(o + 16 * 256)[L] = sx;
+    }
+    __syncthreads();
   }
 }
 
@@ -836,7 +851,7 @@ static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, f
     launch_layer<5>(P, F, ep, s);
     launch_layer<6>(P, F, ep, s);
     launch_layer<7>(P, F, ep, s);
-    hipLaunchKernelGGL(k_tf_coeffs, dim3((unsigned)F.C), dim3(256), 0, s, P, F);
+    hipLaunchKernelGGL(k_tf_coeffs, dim3((unsigned)F.C), dim3(256), 0, s, P, F, q);
   }
   {
     // algorithmic work: 982,528 FLOP per sample (9 Linear layers); bytes: z in, p out, ray rows

@@ -29,8 +29,10 @@ void launch_fold_logits(const float* rays, int stride, const float* z, int64_t t
                         const double* fold, int64_t chunk, float* p_out, hipStream_t s);
 
 // The train-mode query in k_nof_eval_h2's form (nof_eval.hip): the image (train_query_image_floats floats) holds
-// the raw split weights and occ_out; coef[chunk][8][alpha 256 | beta'' 256] each chunk's BatchNorm coefficients.
+// the raw split weights and occ_out; coef[chunk] (TQ_COEF_FLOATS) each chunk's BatchNorm coefficients and the
+// per-layer operand scales of its bound.
 size_t train_query_image_floats();
+constexpr int TQ_COEF_FLOATS = 16 * 256 + 16;   // per chunk: [L][alpha 256 | beta'' 256], then sxB[8] (int)
 void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s);
 void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s);

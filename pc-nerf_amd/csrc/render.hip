@@ -170,6 +170,181 @@ __device__ __forceinline__ void expand_bounds(const float (&zv)[MAXB], int nb, f
   if (err) *err = 1;
 }
 
+// ATen's KeyValueCompDesc (sort descending): NaN first, then a > b
+__device__ __forceinline__ bool kv_desc(float a, float b) { return (isnan(a) && !isnan(b)) || a > b; }
+
+// torch CPU's argsort(descending=True) (render.py:598) runs libstdc++'s std::sort -- introsort: median-of-three
+// quicksort with unguarded Hoare partitions down to ranges of 16, heapsort past 2 lg n levels, then one insertion
+// sort -- over (value, index) pairs with KeyValueCompDesc; the order it leaves equal keys in is this algorithm's, so
+// it is restated step by step (checked against torch's argsort on tie-heavy rows, tests/test_parity_gpu.py).
+// V / I: the row's values and indices (LDS), n entries; one thread.
+__device__ void introsort_desc(float* V, int* I, int n) {
+  auto swp = [&](int a, int b) {
+    const float tv = V[a];
+    V[a] = V[b];
+    V[b] = tv;
+    const int ti = I[a];
+    I[a] = I[b];
+    I[b] = ti;
+  };
+  auto push_heap = [&](int first, int hole, int top, float vv, int vi) {
+    int parent = (hole - 1) / 2;
+    while (hole > top && kv_desc(V[first + parent], vv)) {
+      V[first + hole] = V[first + parent];
+      I[first + hole] = I[first + parent];
+      hole = parent;
+      parent = (hole - 1) / 2;
+    }
+    V[first + hole] = vv;
+    I[first + hole] = vi;
+  };
+  auto adjust_heap = [&](int first, int hole, int len, float vv, int vi) {
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+      second = 2 * (second + 1);
+      if (kv_desc(V[first + second], V[first + second - 1])) --second;
+      V[first + hole] = V[first + second];
+      I[first + hole] = I[first + second];
+      hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+      second = 2 * (second + 1);
+      V[first + hole] = V[first + second - 1];
+      I[first + hole] = I[first + second - 1];
+      hole = second - 1;
+    }
+    push_heap(first, hole, top, vv, vi);
+  };
+  auto heap_sort = [&](int first, int last) {   // __partial_sort(first, last, last): make_heap + sort_heap
+    const int len = last - first;
+    if (len >= 2) {
+      for (int parent = (len - 2) / 2;; --parent) {
+        adjust_heap(first, parent, len, V[first + parent], I[first + parent]);
+        if (parent == 0) break;
+      }
+    }
+    while (last - first > 1) {
+      --last;
+      const float vv = V[last];
+      const int vi = I[last];
+      V[last] = V[first];
+      I[last] = I[first];
+      adjust_heap(first, 0, last - first, vv, vi);
+    }
+  };
+  auto median_to_first = [&](int res, int a, int b, int c) {
+    if (kv_desc(V[a], V[b])) {
+      if (kv_desc(V[b], V[c])) swp(res, b);
+      else if (kv_desc(V[a], V[c])) swp(res, c);
+      else swp(res, a);
+    } else if (kv_desc(V[a], V[c])) swp(res, a);
+    else if (kv_desc(V[b], V[c])) swp(res, c);
+    else swp(res, b);
+  };
+  auto linear_insert = [&](int last) {   // __unguarded_linear_insert
+    const float vv = V[last];
+    const int vi = I[last];
+    int next = last - 1;
+    while (kv_desc(vv, V[next])) {
+      V[last] = V[next];
+      I[last] = I[next];
+      last = next;
+      --next;
+    }
+    V[last] = vv;
+    I[last] = vi;
+  };
+  auto insertion_sort = [&](int first, int last) {
+    for (int i = first + 1; i < last; ++i) {
+      if (kv_desc(V[i], V[first])) {
+        const float vv = V[i];
+        const int vi = I[i];
+        for (int k = i; k > first; --k) {
+          V[k] = V[k - 1];
+          I[k] = I[k - 1];
+        }
+        V[first] = vv;
+        I[first] = vi;
+      } else {
+        linear_insert(i);
+      }
+    }
+  };
+  if (n < 2) return;
+  // __introsort_loop with its recursion on [cut, last) as an explicit stack (the ranges are disjoint, so the
+  // order they are processed in does not change the result)
+  int sf[64], sl[64], sd[64], sp = 1;
+  sf[0] = 0;
+  sl[0] = n;
+  sd[0] = 2 * (31 - __clz(n));
+  while (sp > 0) {
+    --sp;
+    int first = sf[sp], last = sl[sp], depth = sd[sp];
+    while (last - first > 16) {
+      if (depth == 0) {
+        heap_sort(first, last);
+        break;
+      }
+      --depth;
+      median_to_first(first, first + 1, first + (last - first) / 2, last - 1);
+      int lo = first + 1, hi = last;   // __unguarded_partition(first + 1, last, pivot = first)
+      while (true) {
+        while (kv_desc(V[lo], V[first])) ++lo;
+        --hi;
+        while (kv_desc(V[first], V[hi])) --hi;
+        if (!(lo < hi)) break;
+        swp(lo, hi);
+        ++lo;
+      }
+      if (sp < 64) {
+        sf[sp] = lo;
+        sl[sp] = last;
+        sd[sp] = depth;
+        ++sp;
+      }
+      last = lo;
+    }
+  }
+  if (n > 16) {   // __final_insertion_sort
+    insertion_sort(0, 16);
+    for (int i = 16; i < n; ++i) linear_insert(i);
+  } else {
+    insertion_sort(0, n);
+  }
+}
+
+// render.py:598-600 on the rows where w[S-1] ties with another weight: one wave per row (the others exit at once),
+// the row staged in LDS, lane 0 sorts it as torch does and takes the position of index S-1.
+__global__ __launch_bounds__(256) void k_depth2_ties(const float* __restrict__ W, const float* __restrict__ Z,
+                                                     int64_t n_rays, int S, float* __restrict__ depth2) {
+  extern __shared__ float sm_row[];
+  const int wq = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t ray = (int64_t)blockIdx.x * 4 + wq;
+  if (ray >= n_rays) return;
+  float* V = sm_row + (size_t)wq * S;
+  int* I = reinterpret_cast<int*>(sm_row + (size_t)4 * S) + (size_t)wq * S;
+  const float* wr = W + ray * S;
+  const float wl = wr[S - 1];
+  bool tie = false;
+  for (int j = lane; j < S; j += 64) {
+    const float x = wr[j];
+    V[j] = x;
+    I[j] = j;
+    if (j < S - 1) tie = tie || !(kv_desc(x, wl) || kv_desc(wl, x));
+  }
+  if (__ballot(tie) == 0) return;   // (wave-uniform)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane == 0) {
+    introsort_desc(V, I, S);
+    int pos = 0;
+    while (I[pos] != S - 1) ++pos;
+    depth2[ray] = Z[ray * S + pos];
+  }
+}
+
 template <int MAXB>
 __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, const float* __restrict__ Z,
                                                    int64_t n_rays, int S, const float* __restrict__ noise,
@@ -240,7 +415,9 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
     op = wave_sum_d(op);
     if (lane == 0) opac_row[ray] = op;
   }
-  if (depth2) {  // render.py:598-600: z at the rank of sample S-1 in the (stable) descending weight order
+  if (depth2) {  // render.py:598-600: z at the position of sample S-1 in argsort(w, descending=True)
+    // without a tie of w[S-1], that position is the count of weights ordered before it (any sort agrees);
+    // rows with a tie are redone by k_depth2_ties, which reproduces torch's own order of equal keys
     const int last_lane = (S - 1) / B, last_j = (S - 1) % B;
     float wl = 0.0f;
 #pragma unroll
@@ -250,7 +427,7 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
     int cnt = 0;
 #pragma unroll
     for (int j = 0; j < MAXB; ++j)
-      if (j < nb) cnt += (wv[j] > wl) || (wv[j] == wl && i0 + j < S - 1);
+      if (j < nb) cnt += kv_desc(wv[j], wl);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
     if (lane == 0) depth2[ray] = Z[ray * S + cnt];
@@ -837,6 +1014,7 @@ extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, 
                                 float* sl1_ray, double* opac_row, float* depth2, void* stream) {
   PCN_API_BEGIN
   PCN_CHECK(p && z && depth, "pcnerf_composite: null argument");
+  PCN_CHECK(!depth2 || weights, "pcnerf_composite: depth2 needs the weights output");
   PCN_CHECK(n_rays > 0 && n_samples > 0, "pcnerf_composite: empty input");
   if (rays) {
     PCN_CHECK(free_ray && sl1_ray, "pcnerf_composite: child losses need free_ray and sl1_ray");
@@ -859,6 +1037,10 @@ extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, 
   else if (B <= 256) PCN_COMP(256);
   else PCN_CHECK(false, "pcnerf_composite: more than 16384 samples per ray");
 #undef PCN_COMP
+  if (depth2) {   // rows whose w[S-1] ties: torch's order of equal keys (k_depth2_ties)
+    PCN_CHECK(n_samples <= 2048, "pcnerf_composite: depth2 supports at most 2048 samples per ray");
+    hipLaunchKernelGGL(k_depth2_ties, g, b, (size_t)8 * 4 * n_samples, s, weights, z, n_rays, n_samples, depth2);
+  }
   PCN_LAUNCH_CHECK("pcnerf_composite");
   PCN_API_END
 }

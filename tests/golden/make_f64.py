@@ -13,6 +13,7 @@ HIP depth_fine to 1e-4 of this float64 evaluation, and to the reference within t
     python tests/golden/make_f64.py config1 [--save]   (KITTI-00 4,096-ray batch, 64/128)
     python tests/golden/make_f64.py config4 [--save]   (MaiCity blocks, 128/256)
     python tests/golden/make_f64.py config2 [--save]   (65,536 rays, 128/256; ~10 minutes on 8 cores)
+    python tests/golden/make_f64.py grads [--save]     (float64 gradients of the 96-ray gradient goldens)
 Optional: --hip <npz with depth, depth_fine> compares a HIP run too.
 Test infrastructure (imports the oracle)."""
 import argparse
@@ -61,7 +62,59 @@ def stats(name, a, b):
           f"median {np.median(rel):.3e}  >1e-4: {(rel > 1e-4).mean() * 100:.3f} %")
 
 
+def grads64(save):
+    """Float64 parameter gradients for the 96-ray gradient goldens (grads_<case>.npz, made from the reference by
+    make_golden.gen_grads): the oracle's render_rays_train(f64=True) -- the reference's float32 coarse positions,
+    everything after them in float64 -- with float64 leaves, the train_kitti.py:117-155 loss, backward.  Stored in
+    the same golden file under ``f64:`` keys at the golden's own entry indices: how far the reference's float32
+    gradients sit from the exact evaluation, per entry (the fine network's gradients go through fine samples that
+    sample_pdf places where one float32 ulp of a coarse weight moves them)."""
+    cases = {"pcnerf": 0, "divide": 1, "original": 0}
+    for name, div in cases.items():
+        path = os.path.join(HERE, f"grads_{name}.npz")
+        g = dict(np.load(path, allow_pickle=False))
+        P = {}
+        for pre, seed in (("c:", 1234), ("f:", 5678)):
+            Q = O.params_from_numpy(syn.init_nof_params(seed))
+            Q = {k: (v.double() if v.is_floating_point() else v) for k, v in Q.items()}
+            for k in Q:
+                if k.endswith(".weight") or k.endswith(".bias"):
+                    Q[k].requires_grad_(True)
+            P[pre] = Q
+        rays = torch.from_numpy(g["rays"])
+        cl, seg = int(g["use_child_nerf_loss"]), int(g["issegmentated"])
+        ro = O.render_rays_train(P["c:"], P["f:"], rays, sub_nerf_test_num=32, N_samples=64, N_importance=128,
+                                 perturb=0, noise_std=0, chunk=4096, issegmentated=seg, childnerf_ratio=0.1,
+                                 use_child_nerf_divide=div, use_child_nerf_loss=cl, f64=True)
+        r64 = rays.double()
+        lr, lrf = O.range_losses(ro["depth"], ro["depth_fine"], r64[:, 14], r64, div, 32)
+        tot = O.total_loss(ro, lr, lrf)
+        tot.sum().backward()
+        out = {"f64:loss_total": tot.detach().numpy()}
+        for pre, Q in P.items():
+            for k, t in Q.items():
+                if t.grad is None:
+                    continue
+                gr = t.grad.numpy()
+                if pre + k in g:
+                    out["f64:" + pre + k] = gr
+                elif pre + k + "@idx" in g:
+                    out["f64:" + pre + k + "@val"] = gr.reshape(-1)[g[pre + k + "@idx"]]
+                    out["f64:" + pre + k + "@norm"] = np.linalg.norm(gr)
+        i = list(g["f:layer1.0.weight@idx"]).index(g["f:layer1.0.weight@idx"][0])
+        print(name, "loss ref", float(g["loss_total"].sum()), "f64", float(tot.sum()))
+        if save:
+            g = {k: v for k, v in g.items() if not k.startswith("f64:")}
+            g.update(out)
+            np.savez_compressed(path, **g)
+            print("wrote", path)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "grads":
+        torch.set_num_threads(os.cpu_count() or 1)
+        grads64("--save" in sys.argv)
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("config", choices=["config1", "config2", "config4"])
     ap.add_argument("--hip", default=None)

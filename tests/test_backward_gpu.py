@@ -8,10 +8,13 @@ Pinned two ways:
 Tolerance, PER ELEMENT (gradcheck.check_grads_elem): every golden holds the reference's gradients twice, at two
 torch thread counts (two summation orders), and the oracle cases run the oracle twice the same way; entry i passes
 when |hip_i - ref_i| <= max(1e-4 |ref_i|, 1.5 |ref_i - alt_i| + 6 RMS_tensor(ref - alt)) -- the reference's own
-rounding spread, entry by entry, with its typical size as the floor (6 RMS: the fine network's gradients see fine
-samples that sample_pdf places from the coarse weights, which any two implementations round differently; one
-thread-count rerun samples that perturbation only partly -- measured worst entry at 4 RMS: 1.4x, on the 96-ray
-goldens' fine W0 / W5, both train maths).  The production-chunk goldens
+rounding spread, entry by entry, with its typical size as the floor (6 RMS: the split products' 22-bit operands
+round up to ~4x coarser than float32's 24 bits).  The 96-ray goldens also hold the float64
+evaluation of the same step (make_f64.py grads): there each entry is held to the exact gradient within the
+reference's own distance from it, max(1e-4 |f64_i|, 1.5 |ref_i - f64_i| + 6 RMS_tensor(ref - f64)) -- the fine
+network's gradients go through fine samples that sample_pdf places where one float32 ulp of a coarse weight moves
+them, which a thread-count rerun samples only partly (fine W0 entry 142 of grads_divide: reference 18746.7, rerun
+18747.2, float64 18748.6, this path 18750.2-18750.8).  The production-chunk goldens
 (grads_chunk_*.npz: 4,096 rays, chunk 262,144 = one full coarse BatchNorm chunk and three fine ones, the KITTI
 shell's setting) pin the regime where the split math's chunk-wide dL/dh scale acts.  The mathematically-zero
 gradients (Linear biases before BN, BN shifts before Linear->BN) only at noise level (gradcheck.py).

@@ -226,9 +226,46 @@ def test_render_rays(isval, eval_math):
     # weights in [0, 1]: a fine sample moved by sample_pdf's knife edge (see test_sample_pdf) shifts its
     # neighbours' weights by ~1e-6 absolute
     close(res["weights"], g["weights"], 1e-3, 1e-5, "weights")
-    # depth2 picks a sample by weight rank: allow rows where the ranking flips between near-equal weights
+    # depth2 = z at the position of sample S-1 in argsort(weights, descending=True) (render.py:598-600):
+    # (1) exactly the reference's rule applied to this path's own weights, every row (torch's argsort on the CPU);
+    # (2) exactly the reference's depth2 on every row whose ranking the weights' differences cannot change: the gap
+    #     between w[S-1] and every other weight of the reference row exceeds twice the row's largest |HIP - ref|
+    #     weight difference (a fine sample moved by sample_pdf's knife edge shifts its neighbours' weights)
     d2 = res["depth2"].cpu().numpy()
-    assert np.mean(np.abs(d2 - g["depth2"]) <= 1e-4 * np.abs(g["depth2"]) + 1e-6) >= 0.98
+    wh, zh = res["weights"].cpu(), res["z_vals"].cpu().numpy()
+    S = wh.shape[1]
+    own = zh[wh.argsort(dim=-1, descending=True).eq(S - 1).numpy()]
+    np.testing.assert_array_equal(d2, own)
+    wr = g["weights"].astype(np.float64)
+    gap = np.min(np.abs(wr[:, :-1] - wr[:, -1:]), axis=1)
+    werr = np.max(np.abs(wh.numpy().astype(np.float64) - wr), axis=1)
+    ok = gap > 2 * werr
+    assert ok.mean() >= 0.75, ok.mean()   # (rows the weight differences could re-rank are excluded)
+    rank_h = wh.argsort(dim=-1, descending=True).eq(S - 1).int().argmax(-1).numpy()
+    rank_r = torch.from_numpy(g["weights"]).argsort(dim=-1, descending=True).eq(S - 1).int().argmax(-1).numpy()
+    np.testing.assert_array_equal(rank_h[ok], rank_r[ok])                  # the same sample selected, exactly
+    close(d2[ok], g["depth2"][ok], 1e-5, 1e-5, "depth2")                     # its z within z_vals' tolerance
+
+
+def test_depth2_tie_order():
+    """render.py:598's argsort(descending=True) on rows where w[S-1] ties other weights exactly (p = 0 samples and
+    a p = 1 sample zero every weight after it): torch's order of equal keys is its std::sort's, which
+    k_depth2_ties restates -- the HIP depth2 must equal z at the position torch's own argsort gives, on every row."""
+    from nof import _ops
+    g = torch.Generator().manual_seed(23)
+    for S in (64, 192, 384, 1000):
+        R = 128
+        p = torch.rand(R, S, generator=g)
+        p[torch.rand(R, S, generator=g) < 0.3] = 0.0
+        stop = torch.randint(S // 4, S, (R,), generator=g)
+        for r in range(0, R, 2):
+            p[r, stop[r]] = 1.0                      # every later weight exactly 0, w[S-1] among them
+        p[1::4] = torch.rand(R // 4, S, generator=g) * 0.1 + 1e-3   # rows without ties
+        z = torch.sort(torch.rand(R, S, generator=g) * 30, dim=1).values
+        w, depth, _, _, _, d2 = _ops.composite(p.to(DEV), z.to(DEV), eps=1e-10, extras=True)
+        w = w.cpu()
+        expect = z.numpy()[w.argsort(dim=-1, descending=True).eq(S - 1).numpy()]
+        np.testing.assert_array_equal(d2.cpu().numpy(), expect, err_msg=f"S={S}")
 
 
 def test_view_walk_fallback_matches_parallel():
