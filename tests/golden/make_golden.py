@@ -206,6 +206,32 @@ def gen_view():
              **{k: t(v) for k, v in res.items()})
 
 
+def gen_view_kitti():
+    """Config 5's path on real rows: the reference's render_rays_view_0525_2_2 (render.py:614-699, as
+    eval_kitti_render.py:1148-1161 calls it) on the two-step test rows of the first KITTI fixture test frame
+    (scene_rays.npz kitti_view_*, rebuilt bit for bit by nof.dataset on the GPU side), seeded eval-mode weights
+    (the fixture checkpoint's seeds 11 / 12), 64/128 samples, methods 2 and 0; each run again at 4 torch threads
+    (``alt_`` keys: the reference's own spread)."""
+    sc = scene_rays()
+    rows, other = sc["kitti_view_rows"], sc["kitti_view_other"]
+    out = {"rows": rows, "other": other, "N_samples": 64, "N_importance": 128}
+    for method in (2, 0):
+        for threads, pre in ((1, ""), (4, "alt_")):
+            torch.set_num_threads(threads)
+            emb = Embedding(3, 10)
+            mc = syn.load_into(NOF_coarse(), syn.init_nof_params(11)).eval()
+            mf = syn.load_into(NOF_fine(), syn.init_nof_params(12)).eval()
+            with torch.no_grad():
+                res = R.render_rays_view_0525_2_2(mc, mf, emb, torch.from_numpy(rows), torch.from_numpy(other),
+                                                  N_samples=64, N_importance=128, perturb=0, noise_std=0,
+                                                  chunk=262144, depth_inference_method=method)
+            for k in ("depth", "depth_fine", "points_inference", "points_inference_fine", "rays_effective_flag",
+                      "rays_effective_flag_fine", "opacity", "opacity_fine"):
+                out[f"{pre}m{method}_{k}"] = t(res[k])
+    torch.set_num_threads(1)
+    save("render_view_kitti", **out)
+
+
 def gen_render_rays():
     rays = syn.make_rays(128, seed=51)
     for isval in (False, True):
@@ -561,7 +587,7 @@ def gen_self_spread():
 
 GENERATORS = [gen_maicity_frames, gen_kitti_frames, gen_metrics, gen_grads, gen_aabb, gen_render_rays, gen_nof,
               gen_pdf, gen_val, gen_train, gen_view, gen_pdf_pytest, gen_config1_kitti, gen_config4_maicity,
-              gen_config2_full, gen_self_spread, gen_grads_chunk]
+              gen_config2_full, gen_self_spread, gen_grads_chunk, gen_view_kitti]
 
 if __name__ == "__main__":
     # python make_golden.py [name ...]  (names without the gen_ prefix; default: all)

@@ -15,7 +15,9 @@ Stored (small subsets, the rest is rebuilt on the GPU):
   kitti_train  (4096, 15)  a seeded batch of the train split (DataLoader(shuffle=True) analogue), with its indices;
   kitti_val    (N, 15)     the whole val split;
   maicity_b{0..3}          up to 1024 rows of each of 4 parent blocks (MaiCity bounds [-12,61] split in x), with
-                           the block bounds and each block's child count.
+                           the block bounds and each block's child count;
+  kitti_view_*             the two-step test rows (13 columns), ranges and ray-group column of the first KITTI
+                           fixture test frame (config 5's eval_kitti_render.py path).
 """
 import os
 import sys
@@ -63,6 +65,29 @@ def kitti_rays(tmp):
     return out, len(cen)
 
 
+def kitti_view(tmp):
+    """The two-step test rows of the first KITTI fixture test frame (eval_kitti_render.py:675-803 via
+    oracle/rays_cpu.build_view_rows, method 2), as tests/test_eval_driver.py builds its oracle rows: strict < 120 m
+    scan filter, interest region, raw 1 m child cells of the fused cloud, parent box = the cloud's bounds."""
+    from test_dataset import oracle_poses, write_scene
+    root, pose_path, g = write_scene(tmp)
+    rel = D.relative_poses(D.read_poses(pose_path), DS)
+    cloud = D.fuse_frames(root, rel, DS, DE, "cpu", KW["range_delete"], KW["over_height"], KW["over_low"],
+                          INTEREST, INTEREST).numpy()
+    cells = OD.split_children(cloud)
+    b6 = np.concatenate([np.stack([a for a, _ in cells]), np.stack([b for _, b in cells])], 1)
+    c64 = cloud.astype(np.float64)
+    plo, phi = c64.min(0), c64.max(0)
+    P = oracle_poses(g, pose_path)
+    positions = np.stack([P[k + 1][:3, 3] for k in range(DS, DE)])
+    f = [j + 1 for j in range(DS, DE) if (j + 1 - 3) % 5 == 0][0]
+    p = OD.filter_scan(g[f"f{f}"], KW["range_delete"], KW["over_height"], KW["over_low"], strict_range=True)
+    w = OD.interest_filter(D.to_block(torch.from_numpy(p), torch.from_numpy(P[f])).numpy(), positions, INTEREST,
+                           INTEREST)
+    rows, rng, other, tin = RC.build_view_rows(w, P[f][:3, 3].astype(np.float64), b6, plo, phi, 2)
+    return dict(kitti_view_rows=rows, kitti_view_ranges=rng, kitti_view_other=other, kitti_view_frame=f)
+
+
 def maicity_blocks(tmp):
     from test_dataset import write_maicity
     _, pose_path, g = write_maicity(tmp)
@@ -90,6 +115,7 @@ def main():
     import tempfile
     out = {}
     with tempfile.TemporaryDirectory() as tmp:
+        out.update(kitti_view(os.path.join(tmp, "kitti_view")))
         k, n_children = kitti_rays(os.path.join(tmp, "kitti"))
         idx = np.random.default_rng(0).permutation(len(k["train"]))[:4096]
         out.update(kitti_train=k["train"][idx], kitti_train_idx=idx, kitti_train_total=len(k["train"]),

@@ -116,3 +116,43 @@ def test_view_rows_maicity_on_fixture(tmp_path):
     np.testing.assert_array_equal(rows.cpu().numpy(), orows)
     np.testing.assert_array_equal(other.cpu().numpy(), ooth)
     np.testing.assert_array_equal(ranges.cpu().numpy(), orng)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", [2, 0])
+def test_two_step_render_kitti_rows_vs_reference(method):
+    """Config 5's path on real rows: the two-step test rows of the first KITTI fixture frame
+    (tests/golden/scene_rays.npz kitti_view_*, the oracle rows that test_view_rows_and_render_on_fixture checks the
+    GPU row builder against bit for bit) through render_rays_view_0525_2_2, against the reference's own render of
+    the same rows and weights (tests/golden/make_golden.py gen_view_kitti): effective-row flags bit-equal, depths
+    and points within 1e-4 (the north star), opacities within 1e-5."""
+    from conftest import golden
+    from nof import synthetic as syn
+    from nof.networks import Embedding, NOF_coarse, NOF_fine
+    from nof.render import render_rays_view_0525_2_2
+    g = golden("render_view_kitti")
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(11)).cuda().eval()
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(12)).cuda().eval()
+    with torch.no_grad():
+        res = render_rays_view_0525_2_2(mc, mf, Embedding(3, 10), torch.from_numpy(g["rows"]).cuda(),
+                                        torch.from_numpy(g["other"]).cuda(), N_samples=64, N_importance=128,
+                                        perturb=0, noise_std=0, chunk=262144, depth_inference_method=method)
+    pre = f"m{method}_"
+    for k in ("rays_effective_flag", "rays_effective_flag_fine"):
+        np.testing.assert_array_equal(res[k].cpu().numpy(), g[pre + k], err_msg=k)
+    for k in ("depth", "depth_fine", "points_inference", "points_inference_fine"):
+        np.testing.assert_allclose(res[k].cpu().numpy(), g[pre + k], rtol=1e-4, atol=1e-5, err_msg=k)
+    for k in ("opacity", "opacity_fine"):
+        np.testing.assert_allclose(res[k].cpu().numpy(), g[pre + k], rtol=1e-5, err_msg=k)
+    d, r = res["depth_fine"].cpu().numpy().astype(np.float64), g[pre + "depth_fine"].astype(np.float64)
+    _report({"case": f"config5_kitti_rows_m{method}", "rows": int(len(r)),
+             "depth_fine_max_rel": float(np.max(np.abs(d - r) / np.maximum(np.abs(r), 1e-6))),
+             "flags_equal": True})
+
+
+def _report(line):
+    import json
+    path = os.environ.get("PCNERF_PARITY_REPORT")
+    if path:
+        with open(path, "a") as fh:
+            fh.write(json.dumps(line) + "\n")
