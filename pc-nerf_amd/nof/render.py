@@ -81,9 +81,13 @@ def sample_pdf(bins, weights, N_samples, det=False, pytest=False, *, u=None):
 
     ``pytest=True`` is the reference's test hook (render.py:386-394): ``np.random.seed(0)`` (numpy's global
     generator, as the reference seeds it), then ``u`` = float32 of ``np.linspace(0, 1, N)`` (det) or of
-    ``np.random.rand(R, N)``; the draws are made on the host and uploaded, the sampling itself runs on the device."""
+    ``np.random.rand(R, N)``; the draws are made on the host and uploaded, the sampling itself runs on the device.
+    With ``det`` False the reference first draws (and discards) ``torch.rand`` from torch's CPU generator
+    (render.py:383); that draw is made here too, so torch's global RNG state afterwards is the reference's."""
     if pytest:
         R = bins.shape[0]
+        if not det:   # render.py:383 draws u from torch's CPU generator before the numpy overwrite: consume it too
+            torch.rand((R, N_samples))
         np.random.seed(0)
         if det:
             hu = np.broadcast_to(np.linspace(0., 1., N_samples), (R, N_samples))

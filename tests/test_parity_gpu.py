@@ -454,6 +454,16 @@ def test_sample_pdf_pytest_hook():
         ok = ~knife_edge(bc, wc, torch.from_numpy(np.ascontiguousarray(u, dtype=np.float32)))   # see test_sample_pdf
         assert (~ok).float().mean() < 0.05
         close(got[ok], g[key][ok.numpy()], RTOL, 1e-5, key)
+    # torch's global CPU generator ends where the reference leaves it: one torch.rand(R, N) per det=False call
+    # (render.py:383), none for det=True
+    for det in (True, False):
+        torch.manual_seed(77)
+        R.sample_pdf(b, w, 96, det=det, pytest=True)
+        after = torch.rand(4)
+        torch.manual_seed(77)
+        if not det:
+            torch.rand((R_, 96))
+        np.testing.assert_array_equal(after.numpy(), torch.rand(4).numpy())
 
 
 def test_nan_bounds_sort_like_torch():
