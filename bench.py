@@ -163,8 +163,8 @@ def pmc_traffic(kernel_name: str):
         return None, None
     v = d.get("kernels", d).get(kernel_name, {})
     meta = d.get("_meta", {})
-    return v.get("hbm_bytes_per_launch"), ({"file": "profiles/pmc_traffic.json", "head": meta.get("head"),
-                                            "profile": meta.get("profile")} if v else None)
+    return v.get("hbm_bytes_per_launch"), ({"file": "profiles/pmc_traffic.json", "head": v.get("head", meta.get("head")),
+                                            "profile": v.get("profile", meta.get("profile"))} if v else None)
 
 
 # ----------------------------------------------------------------------------------------------- workloads

@@ -1,5 +1,6 @@
 # rocprofv3 passes for one bench workload: a --kernel-trace --stats pass, then one PMC pass per counter group
-# (FETCH_SIZE and WRITE_SIZE in passes of their own: MI355X_MICROARCH.md rocprofv3 slot limits); outputs under
+# (FETCH_SIZE and WRITE_SIZE in passes of their own: MI355X_MICROARCH.md rocprofv3 slot limits; each PMC pass
+# runs one step, no warmup, whatever steps the stats pass was given); outputs under
 # gpurun_out/prof/<tag>.   usage: bash scripts/profile.sh <tag> [bench args]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -21,7 +22,7 @@ for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_A
          "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
   N=$(echo $C | tr ' ' '_' | cut -c1-40)
   timeout -s KILL 400 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_$N -o run -- \
-    python3 bench.py --no-cpu-baseline --no-fp32-line --steps 1 --warmup 0 "$@" > $OUT/pmc_$N.json 2> $OUT/pmc_$N.err
+    python3 bench.py --no-cpu-baseline --no-fp32-line "$@" --steps 1 --warmup 0 > $OUT/pmc_$N.json 2> $OUT/pmc_$N.err
   rc=$?; echo "pmc $N rc=$rc"; [ $rc -ne 0 ] && exit $rc
   python3 scripts/compact_pmc.py $OUT/pmc_$N
 done

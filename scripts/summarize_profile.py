@@ -67,21 +67,35 @@ for r in stats:
     summary[k] = e
 with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as fh:
     json.dump(summary, fh, indent=1)
-# profiles/pmc_traffic.json: HBM bytes per launch of the CURRENT kernels, rebuilt from this round's profiles
-# (kernels of a profile measured at another commit are dropped; bench.py quotes the file and its commit)
+# profiles/pmc_traffic.json: HBM bytes per launch of the CURRENT kernels.  Each entry records the commit it was
+# summarised at; entries of earlier commits are kept only while pc-nerf_amd/csrc is unchanged since then (so a
+# kernel's bytes always describe the code at HEAD).  bench.py quotes the entry and its commit.
 traffic_path = os.path.join(dst, "pmc_traffic.json")
 traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
 head = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip()
 meta = traffic.get("_meta", {})
-kernels = traffic.get("kernels", {}) if meta.get("head") == head else {}
+
+
+def code_unchanged(since):
+    return bool(since) and subprocess.run(["git", "diff", "--quiet", since, "HEAD", "--", "pc-nerf_amd/csrc"],
+                                          capture_output=True).returncode == 0
+
+
+kernels = {k: e for k, e in traffic.get("kernels", {}).items() if code_unchanged(e.get("head", meta.get("head")))}
+for k, e in kernels.items():
+    e.setdefault("head", meta.get("head"))
 for k, e in summary.items():
     if "hbm_bytes_per_launch" in e:
-        kernels[k] = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "avg_us": e["avg_us"], "profile": tag}
-profs = sorted(set(meta.get("profile", "").split(",")) - {""} | {tag}) if meta.get("head") == head else [tag]
+        kernels[k] = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "avg_us": e["avg_us"], "profile": tag,
+                      "head": head}
+profs = sorted({e["profile"] for e in kernels.values()})
 cmd = open(os.path.join(src, "command.txt")).read().strip() if os.path.exists(os.path.join(src, "command.txt")) else ""
+cmds = {t: c for t, c in meta.get("commands", {}).items() if t in profs}
+cmds[tag] = cmd
 out = {"_meta": {"head": head, "profile": ",".join(profs), "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
-                 "(scripts/profile.sh), bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction)",
-                 "commands": {**meta.get("commands", {}), tag: cmd} if meta.get("head") == head else {tag: cmd}},
+                 "(scripts/profile.sh), bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction); each kernel "
+                 "entry names the commit its profile was summarised at (pc-nerf_amd/csrc unchanged since)",
+                 "commands": cmds},
        "kernels": kernels}
 with open(traffic_path, "w") as fh:
     json.dump(out, fh, indent=1)
