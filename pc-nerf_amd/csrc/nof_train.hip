@@ -16,6 +16,8 @@
 // (the tile's float4 itself), D (reg r, lane l) = out[neuron 32b + (r&3) + 8(r>>2) + 4(l>>5)][sample l&31], so
 // registers 4j..4j+3 are the output tile's float4 at group 4b+j.  feature(t, h) = 8(t>>2) + 4h + (t&3).
 #include <algorithm>
+#include <cstring>
+#include <string>
 #include <type_traits>
 #include <vector>
 
@@ -1413,6 +1415,7 @@ struct TrainWs {
   int* sw;      // its per-layer scale exponents
   double* stats;
   double* gram;  // k_enc_gram partials, their slice sums and the chunk's shift e0
+  unsigned* pbound;   // k_pos_bound's result (float bits)
   size_t bytes;
 };
 
@@ -1433,7 +1436,7 @@ static TrainWs carve(void* base, int64_t chunk) {
   const size_t oE = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ost = take(8 * 512 * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
-  const size_t ogr = take(GR_DOUBLES * sizeof(double));
+  const size_t ogr = take(GR_DOUBLES * sizeof(double)), opb = take(sizeof(unsigned));
   char* b = (char*)base;
   TrainWs w;
   w.bufA = (float*)(b + oA);
@@ -1444,6 +1447,7 @@ static TrainWs carve(void* base, int64_t chunk) {
   w.sw = (int*)(b + osw);
   w.stats = (double*)(b + ost);
   w.gram = (double*)(b + ogr);
+  w.pbound = (unsigned*)(b + opb);
   w.bytes = off;
   return w;
 }
@@ -1572,6 +1576,46 @@ static StoreChunk store_chunk(const void* store, int64_t chunk, int64_t ci) {
   return c;
 }
 
+// fp16 range of the layered split math: k_train_h1, the skip layer and the encoding-column weight gradients split
+// the encoding's xyz features without a scale, so a sample position at or beyond 65,504 (fp16's largest finite
+// value) from the block origin would turn into inf there and NaN downstream.  The fused forward, the eval query
+// and the layer-0 moments scale per sample / per unit and have no such limit.  Before any launch, one pass over
+// the call's sample positions (sample_point's arithmetic, or the embedded batch's xyz columns) is read back and
+// the call raises instead of returning NaN.
+__global__ __launch_bounds__(256) void k_pos_bound(const float* __restrict__ rays, int stride,
+                                                   const float* __restrict__ z, int S, const float* __restrict__ ein,
+                                                   int64_t total, unsigned* __restrict__ out) {
+  float m = 0.0f;
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < total; g += (int64_t)gridDim.x * 256) {
+    float p[3];
+    if (ein) {
+      p[0] = ein[g * 63], p[1] = ein[g * 63 + 1], p[2] = ein[g * 63 + 2];
+    } else {
+      sample_point(rays + (g / S) * stride, z[g], p);
+    }
+    m = fmaxf(m, fmaxf(fabsf(p[0]), fmaxf(fabsf(p[1]), fabsf(p[2]))));   // fmaxf drops NaN positions
+  }
+  m = wave_max_f(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+static void check_split_range(const float* rays, int stride, const float* z, int S, const float* ein, int64_t total,
+                              unsigned* dev, hipStream_t s, const char* who) {
+  if (g_train_math == 0) return;   // fp32 MFMA: no fp16 operand
+  PCN_HIP(hipMemsetAsync(dev, 0, sizeof(unsigned), s));
+  const int64_t blocks = std::min<int64_t>(2048, (total + 255) / 256);
+  hipLaunchKernelGGL(k_pos_bound, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, S, ein, total, dev);
+  unsigned h = 0;
+  PCN_HIP(hipMemcpyAsync(&h, dev, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  PCN_HIP(hipStreamSynchronize(s));
+  float m;
+  memcpy(&m, &h, sizeof(m));
+  if (!(m < 65504.0f))
+    throw std::runtime_error(std::string(who) + ": a sample position lies " + std::to_string(m) +
+                             " from the block origin, beyond fp16's range (65,504) that the layered split train "
+                             "math's encoding operand needs; use set_train_math('fp32') for such blocks");
+}
+
 static void query_train(const float* rays, int ray_stride, const float* z, int n_samples, const float* ein,
                         int64_t total, int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
                         void* workspace, size_t workspace_bytes, float* p_out, void* stream,
@@ -1583,6 +1627,7 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
   // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   hipStream_t s = (hipStream_t)stream;
+  check_split_range(rays, ray_stride, z, n_samples, ein, total, ws.pbound, s, "pcnerf_nof_query_train");
   pack_weights(P, ws.wp, ws.wh, ws.sw, s);
   for (int64_t c0 = 0; c0 < total; c0 += chunk) {
     const int64_t n = total - c0 < chunk ? total - c0 : chunk;
@@ -2878,6 +2923,7 @@ struct BwdWs {
   f16x8* wth;   // split-fp16 W^T image of k_dgrad_h (train math 1/2)
   float* tmax[2];   // per-tile max |dL/dh| of g[0] / g[1] ([tile][8])
   unsigned* gmax;   // per layer L: GMAX_SLOTS partial maxima of the chunk's |dL/dh_L| (float bits; zeroed per chunk)
+  unsigned* pbound;   // k_pos_bound's result (float bits)
   size_t bytes;
 };
 
@@ -2899,6 +2945,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
   const size_t owt = take(7 * HW_H * sizeof(f16x8));
   const size_t otm0 = take(tiles * 8 * sizeof(float)), otm1 = take(tiles * 8 * sizeof(float));
+  const size_t opb = take(sizeof(unsigned));
   char* b = (char*)base;
   BwdWs w;
   w.wth = (f16x8*)(b + owt);
@@ -2918,6 +2965,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.gmax = (unsigned*)(w.ostat + OSTAT_COPIES * 257);
   w.gacc = (double*)(b + oa);
   w.enc = (f32x4*)(b + oenc);
+  w.pbound = (unsigned*)(b + opb);
   w.bytes = off;
   return w;
 }
@@ -2988,6 +3036,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
   PCN_CHECK(to_dev_params(params, eps, &P), "pcnerf_nof_backward: null parameter pointer");
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   const GaccLayout G = gacc_layout();
+  check_split_range(rays, ray_stride, z, n_samples, ein, total, ws.pbound, s, "pcnerf_nof_backward");
   hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wp);
   const bool split = g_train_math != 0;
   if (split) {   // the forward's arithmetic for recomputation, and k_dgrad_h's W^T image

@@ -93,6 +93,35 @@ def test_nof_train_forward_far_positions(train_math):
     close(running(mc), rs, 1e-4, 1e-6, "running stats far positions")
 
 
+def test_layered_split_range_guard():
+    """Positions at or beyond fp16's 65,504 from the block origin: the layered split train math (its encoding operand
+    is split without a scale) raises instead of returning NaN; the fused default and fp32 MFMA evaluate them
+    (p within 1e-4 of the float64 oracle)."""
+    from nof import _ops as ops
+    gen = torch.Generator().manual_seed(12)
+    e = torch.rand(3000, 63, generator=gen) * 2 - 1
+    e[:, :3] = (torch.rand(3000, 3, generator=gen) * 2 - 1) * 6.0e4
+    e[7, 1] = 7.0e4
+    P = {k: v.double() if v.is_floating_point() else v.clone() for k, v in
+         O.params_from_numpy(syn.init_nof_params(SEED_C)).items()}
+    ref = O.nof_forward(P, e.double(), True).reshape(-1).numpy()
+    prev = ops.get_train_math()
+    try:
+        for m in ("f16x2_3", "f16x2_4"):
+            ops.set_train_math(m)
+            _, mc, _ = models(True)
+            with torch.no_grad(), pytest.raises(RuntimeError, match="fp16's range"):
+                mc(e.to(DEV))
+        for m in ("f16x2_3_fused", "fp32"):
+            ops.set_train_math(m)
+            _, mc, _ = models(True)
+            with torch.no_grad():
+                p = mc(e.to(DEV))
+            close(p.reshape(-1), ref, 1e-4, 1e-6, f"p beyond fp16 range ({m})")
+    finally:
+        ops.set_train_math(prev)
+
+
 def knife_edge(bins, weights, u):
     """Samples whose bin has cdf_hi - cdf_lo within 4 ulp of the reference's 1e-5 threshold (render.py:408): there
     the branch depends on the last bit of the normaliser sum, whose order torch CPU fixes per ISA."""
