@@ -280,21 +280,26 @@ __device__ __forceinline__ int eh_scale(float m) {
   return e > 64 ? 64 : e < -64 ? -64 : e;
 }
 
-#ifndef PCN_EH_MIX
-#define PCN_EH_MIX 1   // the split's low part by v_fma_mix (eh_split8m below; bit-identical)
-#endif
-__device__ __forceinline__ void eh_split8m(const float (&v)[8], eh_f16x8& hi, eh_f16x8& mid);
-// 8 values -> hi / mid fp16 parts
+// 8 values -> hi / mid fp16 parts, the low part from ONE mixed-precision fma per value, mid = f16(v - f32(hi))
+// (v_fma_mix{lo,hi}_f16, the f16 operand selected by op_sel): v - hi is exact in fp32 (hi is v rounded to 11 bits),
+// so this is the same single rounding as converting the fp32 difference -- bit for bit (scripts/micro/split_mix.hip
+// checks it on the GPU over 67M values) -- in 3 instructions per pair instead of 5 (query time -0.6 %)
 __device__ __forceinline__ void eh_split8(const float (&v)[8], eh_f16x8& hi, eh_f16x8& mid) {
-  if (PCN_EH_MIX) {
-    eh_split8m(v, hi, mid);
-    return;
-  }
+  typedef _Float16 eh_f16x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const _Float16 a = (_Float16)v[j];
-    hi[j] = a;
-    mid[j] = (_Float16)(v[j] - (float)a);
+  for (int p = 0; p < 4; ++p) {
+    eh_f16x2 hp;
+    hp[0] = (_Float16)v[2 * p];
+    hp[1] = (_Float16)v[2 * p + 1];
+    const unsigned hb = __builtin_bit_cast(unsigned, hp);
+    unsigned mb;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(mb) : "v"(hb), "v"(v[2 * p]));
+    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(mb) : "v"(hb), "v"(v[2 * p + 1]));
+    const eh_f16x2 mp = __builtin_bit_cast(eh_f16x2, mb);
+    hi[2 * p] = hp[0];
+    hi[2 * p + 1] = hp[1];
+    mid[2 * p] = mp[0];
+    mid[2 * p + 1] = mp[1];
   }
 }
 
@@ -499,41 +504,12 @@ constexpr int E2_T = PCN_EH2_T;   // sample tiles per block
 #ifndef PCN_EH2_RING
 #define PCN_EH2_RING 4    // k_nof_eval_h2: weight-ring slots (prefetch distance RING - 1 k-steps); 4 or 8
 #endif
-#ifndef PCN_EH2_PIPE
-#define PCN_EH2_PIPE 0    // TR: layer transitions overlap the split of tile tau+1 with tile tau's first MFMAs (below)
-#endif
-constexpr int RG_EVAL = PCN_EH2_RING;   // (the PIPE train query uses 8 slots: see the transition)
-
-// 8 values -> hi / mid fp16 parts with the low part from ONE mixed-precision fma per value, mid = f16(v - f32(hi))
-// (v_fma_mix{lo,hi}_f16, the f16 operand selected by op_sel): v - hi is exact in fp32 (hi is v rounded to 11 bits),
-// so this is the same single rounding as eh_split8's conversion of the fp32 difference -- bit for bit
-// (scripts/micro/split_mix.hip checks it on the GPU) -- in 3 instructions per pair instead of 5
-__device__ __forceinline__ void eh_split8m(const float (&v)[8], eh_f16x8& hi, eh_f16x8& mid) {
-  typedef _Float16 eh_f16x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    eh_f16x2 hp;
-    hp[0] = (_Float16)v[2 * p];
-    hp[1] = (_Float16)v[2 * p + 1];
-    const unsigned hb = __builtin_bit_cast(unsigned, hp);
-    unsigned mb;
-    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(mb) : "v"(hb), "v"(v[2 * p]));
-    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(mb) : "v"(hb), "v"(v[2 * p + 1]));
-    const eh_f16x2 mp = __builtin_bit_cast(eh_f16x2, mb);
-    hi[2 * p] = hp[0];
-    hi[2 * p + 1] = hp[1];
-    mid[2 * p] = mp[0];
-    mid[2 * p + 1] = mp[1];
-  }
-}
+constexpr int RG = PCN_EH2_RING, RD = RG - 1;
 #ifndef PCN_EH2_ROT
 #define PCN_EH2_ROT 0     // TR: each block walks its hidden k-steps rotated by blockIdx (spreads the L2 weight reads)
 #endif
 #ifndef PCN_EH2_ABL
 #define PCN_EH2_ABL 0     // diagnostic timing ablations (wrong results): 1 weights of k-step 0 only, 2 no B re-reads
-#endif
-#ifndef PCN_EH2_TABL
-#define PCN_EH2_TABL 0    // diagnostic timing ablations of the PIPE transition (wrong results): 1 no split, 2 no MFMAs
 #endif
 #ifndef PCN_EH2_STAMP
 #define PCN_EH2_STAMP 0   // diagnostic builds only: per-block phase stamps of k_nof_eval_h2 (pcnerf_debug_eh2_clock)
@@ -604,20 +580,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   // start are multiples of 4, so the slot is a compile-time index in the unrolled k-loops and no in-flight load's
   // registers are ever copied): k-step s issues the loads of k-step s + 3 into the slot k-step s - 1 just used
   // hidden k-steps walked from k-step rot of their layer (TR && PCN_EH2_ROT): the image k-step of processing step q
-  // TR && PCN_EH2_PIPE: every hidden layer starts at the wave's OWN k-steps 4w..4w+3 (its own outputs of the layer
-  // before); layer 4 walks own h3 k-steps, its 4 encoding k-steps, then the other 12
-  constexpr bool PIPE = TR && PCN_EH2_PIPE;
-  constexpr int RG = PIPE ? 8 : RG_EVAL, RD = RG - 1;
-  const int rot = PIPE ? 4 * w : (TR && PCN_EH2_ROT) ? (int)(blockIdx.x & 15) : 0;
+  const int rot = (TR && PCN_EH2_ROT) ? (int)(blockIdx.x & 15) : 0;
   auto kmap = [&](int q) __attribute__((always_inline)) {
-    if (PIPE) {   // every case computed and selected (uniform scalar selects, no branch splitting the schedule)
-      q = q < EH_KSTEPS ? q : EH_KSTEPS - 1;
-      const int i = q - 52;
-      const int r4 = i < 4 ? 56 + ((rot + i) & 15) : i < 8 ? 48 + i : 56 + ((rot + i - 4) & 15);
-      const int base = q < 52 ? 4 : 72, st = base + ((q - base) & ~15);
-      const int rh = st + ((q - st + rot) & 15);
-      return q < 4 ? q : (unsigned)i < 20u ? r4 : rh;
-    }
     if (q < 4 || (q >= 52 && q < 56) || q >= EH_KSTEPS) return q < EH_KSTEPS ? q : EH_KSTEPS - 1;
     const int st = q < 52 ? 4 + ((q - 4) & ~15) : 56 + ((q - 56) & ~15);
     return st + ((q - st + rot) & 15);
@@ -848,36 +812,18 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   // the 16 hidden k-steps of a layer (B operands in act), software-pipelined: per k-step the products run in the
   // order Wh.xm, Wh.xh, Wm.xh, and k-step s + 1's xm is read from LDS once Wh.xm of s is issued, its xh once Wm.xh
   // of s is -- every LDS read has at least six MFMAs in flight to cover it
-  // (s0: the first processing step; PIPE layers enter at 4, their own k-steps done by the transition)
-  auto no_hook = []() {};
-  // (TM: the last k-step runs tile-major, so tile 0's accumulators are final first; pre_last runs before it)
-  auto hidden_ksteps = [&](int pos0, bool first, int s0, auto TM, auto pre_last) __attribute__((always_inline)) {
-    constexpr bool tm = decltype(TM)::value;
+  auto hidden_ksteps = [&](int pos0, bool first) __attribute__((always_inline)) {
     eh_f16x8 bh[E2_T], bm[E2_T];
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
-      bm[tau] = act[(s0 + rot) & 15][tau][1][lane];
-      bh[tau] = act[(s0 + rot) & 15][tau][0][lane];
+      bm[tau] = act[rot][tau][1][lane];
+      bh[tau] = act[rot][tau][0][lane];
     }
 #pragma unroll
-    for (int s = s0; s < 16; ++s) {
+    for (int s = 0; s < 16; ++s) {
       const int pos = pos0 + s;
       load_w(wr4[(pos + RD) & (RG - 1)], kmap(gk + RD));
       const eh_f16x8 (&wc)[2][2] = wr4[pos & (RG - 1)];
-      if (tm && s == 15) {
-        pre_last();
-#pragma unroll
-        for (int tau = 0; tau < E2_T; ++tau) {
-#pragma unroll
-          for (int o = 0; o < 2; ++o) acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bm[tau], acc[o][tau], 0, 0, 0);
-#pragma unroll
-          for (int o = 0; o < 2; ++o) acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bh[tau], acc[o][tau], 0, 0, 0);
-#pragma unroll
-          for (int o = 0; o < 2; ++o) acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
-        }
-        ++gk;
-        continue;
-      }
 #pragma unroll
       for (int tau = 0; tau < E2_T; ++tau)
 #pragma unroll
@@ -908,141 +854,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       ++gk;
     }
   };
-  // PIPE transition from layer L to L+1 (posn: layer L+1's first processing step mod RG; gk is that step).  Per
-  // tile: layer L's epilogue (the chunk's BatchNorm fma, as epi_tr) and the split of this wave's 64 outputs -- the
-  // B operands of layer L+1's k-steps 4w..4w+3 -- stored to act for the other waves AND used from registers at
-  // once by this wave's first 4 k-steps of layer L+1 on that tile (24 MFMAs), so the split of tile tau+1 issues
-  // beside the MFMAs of tile tau.  The caller's barrier before it ends every wave's reads of layer L's act; the
-  // barrier at its end publishes the split outputs.  Own k-steps' weights stay in the ring for all tiles (RG = 8:
-  // the next k-steps' loads are already in flight), so the loads into their slots wait until the last tile.
-  // MODE (compile-time): 0 plain, 1 the input has a per-sample scale (layers 0 and 4: unscaled first, exact), 2
-  // layer 3 (outputs moved to the per-sample scale layer 4 shares with the encoding)
-  f32x4 ca[4][2], cbv[4][2];   // (PIPE) the finished layer's coefficients of this lane's 32 neurons
-  auto read_coef = [&](int L) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int nb = 512 * L + 32 * (2 * w + (j >> 1)) + 16 * (j & 1) + 4 * h;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        ca[j][u] = *reinterpret_cast<const f32x4*>(sbias + nb + 8 * u);
-        cbv[j][u] = *reinterpret_cast<const f32x4*>(sbias + nb + 256 + 8 * u);
-      }
-    }
-  };
-  // MODE (compile-time): 0 plain, 1 the input has a per-sample scale (layers 0 and 4: unscaled first, exact), 2
-  // layer 3 (outputs moved to the per-sample scale layer 4 shares with the encoding).  B1: the barrier that ends
-  // every wave's reads of layer L's act, placed after tile 0's split values are formed (none for layer 0).  The
-  // coefficients (ca, cbv) were read by read_coef before the layer's last k-step.
-  auto transition = [&](int L, int posn, auto MODE, bool B1) __attribute__((always_inline)) {
-    constexpr int md = decltype(MODE)::value;
-    load_w(wr4[(posn + RD) & (RG - 1)], kmap(gk + RD));
-    eh_f16x8 bh[2][4], bm[2][4];   // split outputs of tiles tau (being multiplied) and tau + 1 (being split)
-    auto split_tile = [&](int tau, eh_f16x8 (&xh)[4], eh_f16x8 (&xm)[4], bool store) __attribute__((always_inline)) {
-      const float us = md == 1 ? ldexpf(1.0f, -sxl[tau]) : 1.0f;
-      const float xs3 = md == 2 ? ldexpf(1.0f, sx0s[32 * tau + li] - sxB[3]) : 1.0f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int o = j >> 1, k = j & 1;
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float x = acc[o][tau][8 * k + e];
-          if (md == 1) x *= us;
-          v[e] = __builtin_fmaf(x, ca[j][e >> 2][e & 3], cbv[j][e >> 2][e & 3]);
-          if (md == 2) v[e] *= xs3;
-        }
-#if PCN_EH2_TABL & 1
-        xh[j] = __builtin_bit_cast(eh_f16x8, f32x4{v[0], v[1], v[2], v[3]});
-        xm[j] = __builtin_bit_cast(eh_f16x8, f32x4{v[4], v[5], v[6], v[7]});
-#else
-        eh_split8m(v, xh[j], xm[j]);
-#endif
-        if (store) {
-          act[4 * w + j][tau][0][lane] = xh[j];
-          act[4 * w + j][tau][1][lane] = xm[j];
-        }
-      }
-    };
-    auto mfma_tile = [&](int tau, const eh_f16x8 (&xh)[4], const eh_f16x8 (&xm)[4]) __attribute__((always_inline)) {
-      if (PCN_EH2_TABL & 2) return;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const eh_f16x8 (&wc)[2][2] = wr4[(posn + j) & (RG - 1)];
-#pragma unroll
-        for (int o = 0; o < 2; ++o)
-          acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], xm[j], j == 0 ? f32x16{} : acc[o][tau], 0, 0, 0);
-#pragma unroll
-        for (int o = 0; o < 2; ++o) acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], xh[j], acc[o][tau], 0, 0, 0);
-#pragma unroll
-        for (int o = 0; o < 2; ++o) acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], xh[j], acc[o][tau], 0, 0, 0);
-      }
-    };
-    split_tile(0, bh[0], bm[0], false);
-    if (B1) __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      act[4 * w + j][0][0][lane] = bh[0][j];
-      act[4 * w + j][0][1][lane] = bm[0][j];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) {
-      mfma_tile(tau, bh[tau & 1], bm[tau & 1]);
-      if (tau + 1 < E2_T) {
-        split_tile(tau + 1, bh[(tau + 1) & 1], bm[(tau + 1) & 1], true);
-        // tile tau+1's epilogue / split beside tile tau's 24 MFMAs: 4 vector instructions per MFMA gap, its 8 LDS
-        // stores spread over the gaps
-#pragma unroll
-        for (int i = 0; i < 24; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-          if (i % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int j = 1; j < 4; ++j) load_w(wr4[(posn + RD + j) & (RG - 1)], kmap(gk + RD + j));
-    gk += 4;
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) sxl[tau] = md == 2 ? sx0s[32 * tau + li] : sxB[L];
-    if (L == 2) EH2_STAMP(13);
-    __syncthreads();
-  };
-
 #pragma unroll
   for (int s = 0; s < 4; ++s) kstep(s, s, true, s == 0);
-  if (PIPE) {
-    using TMy = std::true_type;
-    read_coef(0);
-    // layer 0 read no act (its B operands are eb), so no barrier before the first transition
-    transition(0, 4 % RG, std::integral_constant<int, 1>{}, false);
-    EH2_STAMP(2);
-    // the weight ring's slot of processing step g is g mod RG: layer starts 4, 20, 36, 52 ≡ 4 and 72, 88, 104 ≡ 0
-#pragma unroll 1
-    for (int L = 1; L <= 3; ++L) {
-      hidden_ksteps(4 % RG, false, 4, TMy{}, [&]() { read_coef(L); });
-      if (L == 2) EH2_STAMP(11);
-      if (L == 2) EH2_STAMP(12);
-      if (L == 3) transition(L, 4 % RG, std::integral_constant<int, 2>{}, true);
-      else transition(L, 4 % RG, std::integral_constant<int, 0>{}, true);
-      EH2_STAMP(2 + L);
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) kstep(s, 56 % RG + s, true, false);   // layer 4's encoding k-steps
-    hidden_ksteps(56 % RG, false, 4, TMy{}, [&]() { read_coef(4); });
-    transition(4, 72 % RG, std::integral_constant<int, 1>{}, true);
-    EH2_STAMP(6);
-#pragma unroll 1
-    for (int L = 5; L <= 6; ++L) {
-      hidden_ksteps(72 % RG, false, 4, TMy{}, [&]() { read_coef(L); });
-      transition(L, 72 % RG, std::integral_constant<int, 0>{}, true);
-      EH2_STAMP(2 + L);
-    }
-    hidden_ksteps(72 % RG, false, 4, std::false_type{}, no_hook);
-    epi_tr(7, std::false_type{});
-    EH2_STAMP(9);
-  } else {
   if (TR) {
     epi_tr(0, std::true_type{});
     float xs[E2_T];
@@ -1098,18 +911,17 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   // (layer starts: 0, 4, 20, 36, 52 (+4 encoding k-steps), 72, 88, 104), so every slot index is a constant
 #pragma unroll 1
   for (int L = 1; L <= 3; ++L) {
-    hidden_ksteps(4 % RG, true, 0, std::false_type{}, no_hook);
+    hidden_ksteps(4 % RG, true);
     layer_end(L);
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) kstep(s, 52 % RG + s, true, s == 0);
-  hidden_ksteps(56 % RG, false, 0, std::false_type{}, no_hook);
+  hidden_ksteps(56 % RG, false);
   layer_end(4);
 #pragma unroll 1
   for (int L = 5; L <= 7; ++L) {
-    hidden_ksteps(72 % RG, true, 0, std::false_type{}, no_hook);
+    hidden_ksteps(72 % RG, true);
     layer_end(L);
-  }
   }
   // occ_out: this wave's 64 neurons per sample, then the 4 partial sums in order
 #pragma unroll
