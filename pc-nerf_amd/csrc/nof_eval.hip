@@ -611,6 +611,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   }
   // prologue: the block's encodings, the 30 sincosf per sample spread over all 256 threads (encode_full's
   // arithmetic, bit for bit), staged as floats in the (still unused) activation buffer
+  if (PCN_EH2_STAMP == 2) EH2_STAMP(11);
   float* const encf = reinterpret_cast<float*>(&act[0][0][0][0]);   // [sample][65]
   static_assert(sizeof(act) >= 32 * E2_T * 65 * sizeof(float), "encoding staging area");
   if (!ein) {
@@ -627,6 +628,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       encf[t * 65 + 63] = 0.0f;
     }
     __syncthreads();
+    if (PCN_EH2_STAMP == 2) EH2_STAMP(12);
     for (int i = t; i < 32 * E2_T * 30; i += 256) {
       const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
       float sv, cv;
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       encf[sm * 65 + 6 + 6 * k + m] = cv;
     }
     __syncthreads();
+    if (PCN_EH2_STAMP == 2) EH2_STAMP(13);
   }
   if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
     float f[64];
@@ -876,7 +879,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   EH2_STAMP(2);
   // epilogue of layers 1-7 (TR: fma to the next operand scale; eval: per-sample scales through smax)
   auto layer_end = [&](int L) __attribute__((always_inline)) {
-    if (L == 2) EH2_STAMP(11);
+    if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(11);
     if (TR) {
       if (L == 4) epi_tr(4, std::true_type{});
       else epi_tr(L, std::false_type{});
@@ -889,19 +892,19 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
           xs[tau] = ldexpf(1.0f, sx0 - sxB[3]);
         }
         __syncthreads();
-        if (L == 2) EH2_STAMP(12);
+        if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(12);
         if (L == 3) split_out(xs, std::true_type{});
         else split_out(xs, std::false_type{});
-        if (L == 2) EH2_STAMP(13);
+        if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(13);
         __syncthreads();
       }
     } else {
       epi1(L);
       __syncthreads();
-      if (L == 2) EH2_STAMP(12);
+      if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(12);
       if (L < 7) {
         epi2(L == 3);
-        if (L == 2) EH2_STAMP(13);
+        if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(13);
         __syncthreads();
       }
     }
@@ -1253,9 +1256,16 @@ extern "C" int pcnerf_debug_eh2_clock(double* out) {
     if (h[b][1] <= h[b][0] || h[b][12] <= h[b][2]) continue;
     ph[0].push_back((double)(h[b][12] - h[b][2]) / (double)(h[b][1] - h[b][0]) * 100.0);
     for (int i = 0; i < 10; ++i) ph[1 + i].push_back((double)(h[b][3 + i] - h[b][2 + i]));
+#if PCN_EH2_STAMP == 2
+    // prologue: coefficients / ring loads issued; sample positions + barrier; sincosf + barrier; B-order split
+    ph[11].push_back((double)(h[b][13] - h[b][2]));
+    ph[12].push_back((double)(h[b][14] - h[b][13]));
+    ph[13].push_back((double)(h[b][15] - h[b][14]));
+#else
     ph[11].push_back((double)(h[b][13] - h[b][4]));   // layer 2: k-loop (from layer 1's end)
     ph[12].push_back((double)(h[b][14] - h[b][13]));  // epilogue 1 + first barrier
     ph[13].push_back((double)(h[b][15] - h[b][14]));  // scales + split + LDS writes
+#endif
   }
   if (ph[0].empty()) return 2;
   for (int i = 0; i < 14; ++i) {
