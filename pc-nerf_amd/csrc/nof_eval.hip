@@ -511,6 +511,9 @@ constexpr int RG = PCN_EH2_RING, RD = RG - 1;
 #ifndef PCN_EH2_ABL
 #define PCN_EH2_ABL 0     // diagnostic timing ablations (wrong results): 1 weights of k-step 0 only, 2 no B re-reads
 #endif
+#ifndef PCN_EH2_BSPLIT
+#define PCN_EH2_BSPLIT 1   // the prologue's B-order split of the encodings over all 256 threads
+#endif
 #ifndef PCN_EH2_STAMP
 #define PCN_EH2_STAMP 0   // diagnostic builds only: per-block phase stamps of k_nof_eval_h2 (pcnerf_debug_eh2_clock)
 #endif
@@ -639,7 +642,49 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     __syncthreads();
     if (PCN_EH2_STAMP == 2) EH2_STAMP(13);
   }
-  if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
+  if (!ein && PCN_EH2_BSPLIT) {
+    // the encodings' B-order split over all 256 threads: unit u = (sample u >> 3, k-step (u >> 1) & 3, lane half
+    // u & 1) holds 8 features; the sample's scale from the maxima of its 8 units (fmaxf: the same value as one
+    // thread's max over the 63 features, so the same scale and bits as below)
+    float* const umax = encf + 32 * E2_T * 65;
+    static_assert(sizeof(act) >= 32 * E2_T * (65 + 8) * sizeof(float), "unit maxima");
+    constexpr int NU = 32 * E2_T * 8 / 256;
+    static_assert(32 * E2_T * 8 % 256 == 0, "whole units per thread");
+    float uv[NU][8];
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      const int u = t + 256 * q, sm = u >> 3, sq = (u >> 1) & 3, hh = u & 1;
+      float m = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uv[q][j] = encf[sm * 65 + 2 * (8 * sq + j) + hh];
+        m = fmaxf(m, fabsf(uv[q][j]));
+      }
+      umax[u] = m;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      const int u = t + 256 * q, sm = u >> 3, sq = (u >> 1) & 3, hh = u & 1;
+      const f32x4 m0 = *reinterpret_cast<const f32x4*>(umax + 8 * sm);
+      const f32x4 m1 = *reinterpret_cast<const f32x4*>(umax + 8 * sm + 4);
+      const float m = fmaxf(fmaxf(fmaxf(m0[0], m0[1]), fmaxf(m0[2], m0[3])), fmaxf(fmaxf(m1[0], m1[1]), fmaxf(m1[2], m1[3])));
+      int sx0 = eh_scale(m);
+      if (TR && sxB[3] < sx0) sx0 = sxB[3];   // the encoding shares layer 4's input scale with h3
+      const float xs = ldexpf(1.0f, sx0);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = uv[q][j] * xs;
+      eh_f16x8 hi, mid;
+      eh_split8(v, hi, mid);
+      eb[sq][sm >> 5][0][(sm & 31) + 32 * hh] = hi;
+      eb[sq][sm >> 5][1][(sm & 31) + 32 * hh] = mid;
+      if ((u & 7) == 0) {
+        emax[sm] = m;
+        sx0s[sm] = sx0;
+      }
+    }
+  } else if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
     float f[64];
     if (ein) {
       int64_t g = s0 + t;
