@@ -511,8 +511,11 @@ constexpr int RG = PCN_EH2_RING, RD = RG - 1;
 #ifndef PCN_EH2_ABL
 #define PCN_EH2_ABL 0     // diagnostic timing ablations (wrong results): 1 weights of k-step 0 only, 2 no B re-reads
 #endif
-#ifndef PCN_EH2_BSPLIT
-#define PCN_EH2_BSPLIT 1   // the prologue's B-order split of the encodings over all 256 threads
+#ifndef PCN_EH2_EARLY
+#define PCN_EH2_EARLY 1   // prologue: the samples' z and ray rows loaded before the weight-ring / coefficient loads
+#endif
+#ifndef PCN_EH2_SCU
+#define PCN_EH2_SCU 0     // prologue: the sincosf loop fully unrolled
 #endif
 #ifndef PCN_EH2_STAMP
 #define PCN_EH2_STAMP 0   // diagnostic builds only: per-block phase stamps of k_nof_eval_h2 (pcnerf_debug_eh2_clock)
@@ -544,7 +547,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
                                                         const float* __restrict__ z, int64_t total, int S,
                                                         const float* __restrict__ ein, const float* __restrict__ W,
                                                         float* __restrict__ p_out, const float* __restrict__ coef,
-                                                        int64_t chunk) {
+                                                        int64_t chunk, const float* __restrict__ encu,
+                                                        const float* __restrict__ emx) {
   __shared__ eh_f16x8 act[16][E2_T][2][64];
   __shared__ eh_f16x8 eb[4][E2_T][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
   __shared__ int sx0s[E2_T * 32];
@@ -561,6 +565,36 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   const int64_t send = TR ? (cb + chunk < total ? cb + chunk : total) : total;
   if (s0 >= send) return;   // (the last chunk's surplus blocks; uniform over the block, before any barrier)
   EH2_STAMP(0);
+  // this thread's sample (threads < 96): its z and ray row loaded first, so their latency overlaps the weight-ring
+  // and coefficient loads below (PCN_EH2_EARLY; the prologue otherwise waits for the two in turn)
+  float rz = 0.0f, rr[6] = {};
+  // TR with encu (nof_fold.hip EncUnits): the block's 768 encoding units (8 features each) and their samples' max
+  // |feature| come from the moment pass; thread t splits units t, t + 256, t + 512 (loads issued here, first)
+  constexpr int NU = 32 * E2_T * 8 / 256;
+  static_assert(32 * E2_T * 8 % 256 == 0 && 32 * E2_T == 96, "encoding units: nof_fold.hip EU_BLOCK");
+  const bool units = TR && encu != nullptr;
+  f32x4 uva[NU], uvb[NU];
+  float umx[NU];
+  if (units) {
+    const int64_t bidx = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const int last = (int)(send - 1 - s0);   // padded samples take the block's last valid one (as below)
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      const int u = t + 256 * q, sm = u % (32 * E2_T), smc = sm < last ? sm : last;
+      const f32x4* up = reinterpret_cast<const f32x4*>(encu + ((bidx * 768) + (u - sm) + smc) * 8);
+      uva[q] = up[0];
+      uvb[q] = up[1];
+      umx[q] = emx[bidx * (32 * E2_T) + smc];
+    }
+  }
+  if (PCN_EH2_EARLY && !ein && !units && t < 32 * E2_T) {
+    int64_t g = s0 + t;
+    if (g >= send) g = send - 1;
+    const float* r = rays + (g / S) * stride;
+    rz = z[g];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) rr[m] = r[m];
+  }
   const eh_f16x8* __restrict__ img = reinterpret_cast<const eh_f16x8*>(W + OFF_EH);
   int sw[8];
 #pragma unroll
@@ -617,12 +651,39 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   if (PCN_EH2_STAMP == 2) EH2_STAMP(11);
   float* const encf = reinterpret_cast<float*>(&act[0][0][0][0]);   // [sample][65]
   static_assert(sizeof(act) >= 32 * E2_T * 65 * sizeof(float), "encoding staging area");
+  if (units) {
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      const int u = t + 256 * q, sm = u % (32 * E2_T), sq = u / (64 * E2_T), hh = (u / (32 * E2_T)) & 1;
+      int sx0 = eh_scale(umx[q]);
+      if (sxB[3] < sx0) sx0 = sxB[3];   // the encoding shares layer 4's input scale with h3
+      const float xs = ldexpf(1.0f, sx0);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = uva[q][j] * xs;
+        v[4 + j] = uvb[q][j] * xs;
+      }
+      eh_f16x8 hi, mid;
+      eh_split8(v, hi, mid);
+      eb[sq][sm >> 5][0][(sm & 31) + 32 * hh] = hi;
+      eb[sq][sm >> 5][1][(sm & 31) + 32 * hh] = mid;
+      if (u < 32 * E2_T) {
+        emax[sm] = umx[q];
+        sx0s[sm] = sx0;
+      }
+    }
+  } else {
   if (!ein) {
     if (t < 32 * E2_T) {
-      int64_t g = s0 + t;
-      if (g >= send) g = send - 1;
       float p[3];
-      sample_point(rays + (g / S) * stride, z[g], p);
+      if (PCN_EH2_EARLY) {
+        sample_point(rr, rz, p);
+      } else {
+        int64_t g = s0 + t;
+        if (g >= send) g = send - 1;
+        sample_point(rays + (g / S) * stride, z[g], p);
+      }
 #pragma unroll
       for (int m = 0; m < 3; ++m) {
         spos[t][m] = p[m];
@@ -632,59 +693,34 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     }
     __syncthreads();
     if (PCN_EH2_STAMP == 2) EH2_STAMP(12);
-    for (int i = t; i < 32 * E2_T * 30; i += 256) {
-      const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
-      float sv, cv;
-      sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
-      encf[sm * 65 + 3 + 6 * k + m] = sv;
-      encf[sm * 65 + 6 + 6 * k + m] = cv;
+    // fully unrolled (PCN_EH2_SCU): the iterations' LDS reads and sincosf chains interleave instead of running one
+    // dependent chain after another at one wave per SIMD
+    if (PCN_EH2_SCU) {
+      constexpr int NI = (32 * E2_T * 30 + 255) / 256;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int i = t + 256 * j;
+        if (i < 32 * E2_T * 30) {
+          const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
+          float sv, cv;
+          sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
+          encf[sm * 65 + 3 + 6 * k + m] = sv;
+          encf[sm * 65 + 6 + 6 * k + m] = cv;
+        }
+      }
+    } else {
+      for (int i = t; i < 32 * E2_T * 30; i += 256) {
+        const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
+        float sv, cv;
+        sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
+        encf[sm * 65 + 3 + 6 * k + m] = sv;
+        encf[sm * 65 + 6 + 6 * k + m] = cv;
+      }
     }
     __syncthreads();
     if (PCN_EH2_STAMP == 2) EH2_STAMP(13);
   }
-  if (!ein && PCN_EH2_BSPLIT) {
-    // the encodings' B-order split over all 256 threads: unit u = (sample u >> 3, k-step (u >> 1) & 3, lane half
-    // u & 1) holds 8 features; the sample's scale from the maxima of its 8 units (fmaxf: the same value as one
-    // thread's max over the 63 features, so the same scale and bits as below)
-    float* const umax = encf + 32 * E2_T * 65;
-    static_assert(sizeof(act) >= 32 * E2_T * (65 + 8) * sizeof(float), "unit maxima");
-    constexpr int NU = 32 * E2_T * 8 / 256;
-    static_assert(32 * E2_T * 8 % 256 == 0, "whole units per thread");
-    float uv[NU][8];
-#pragma unroll
-    for (int q = 0; q < NU; ++q) {
-      const int u = t + 256 * q, sm = u >> 3, sq = (u >> 1) & 3, hh = u & 1;
-      float m = 0.0f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        uv[q][j] = encf[sm * 65 + 2 * (8 * sq + j) + hh];
-        m = fmaxf(m, fabsf(uv[q][j]));
-      }
-      umax[u] = m;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < NU; ++q) {
-      const int u = t + 256 * q, sm = u >> 3, sq = (u >> 1) & 3, hh = u & 1;
-      const f32x4 m0 = *reinterpret_cast<const f32x4*>(umax + 8 * sm);
-      const f32x4 m1 = *reinterpret_cast<const f32x4*>(umax + 8 * sm + 4);
-      const float m = fmaxf(fmaxf(fmaxf(m0[0], m0[1]), fmaxf(m0[2], m0[3])), fmaxf(fmaxf(m1[0], m1[1]), fmaxf(m1[2], m1[3])));
-      int sx0 = eh_scale(m);
-      if (TR && sxB[3] < sx0) sx0 = sxB[3];   // the encoding shares layer 4's input scale with h3
-      const float xs = ldexpf(1.0f, sx0);
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = uv[q][j] * xs;
-      eh_f16x8 hi, mid;
-      eh_split8(v, hi, mid);
-      eb[sq][sm >> 5][0][(sm & 31) + 32 * hh] = hi;
-      eb[sq][sm >> 5][1][(sm & 31) + 32 * hh] = mid;
-      if ((u & 7) == 0) {
-        emax[sm] = m;
-        sx0s[sm] = sx0;
-      }
-    }
-  } else if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
+  if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
     float f[64];
     if (ein) {
       int64_t g = s0 + t;
@@ -717,6 +753,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       }
     emax[t] = m;
     sx0s[t] = sx0;
+  }
   }
   __syncthreads();
   EH2_STAMP(1);
@@ -1002,7 +1039,7 @@ static void launch_eval(const float* rays, int stride, const float* z, int64_t t
   const int64_t blocks = ((total + 31) / 32 + 3) / 4;
   if (g_eval_math == 1 && PCN_EH2)
     hipLaunchKernelGGL(k_nof_eval_h2<false>, dim3((unsigned)((total + 32 * E2_T - 1) / (32 * E2_T))), dim3(256), 0,
-                       s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0);
+                       s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0, nullptr, nullptr);
   else if (g_eval_math == 1)
     hipLaunchKernelGGL(k_nof_eval_h, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
                        p_out);
@@ -1161,12 +1198,13 @@ void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s) {
 }
 
 void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
-                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s) {
+                        const float* img, const float* coef, int64_t chunk, const float* encu, const float* emx,
+                        float* p_out, hipStream_t s) {
   const int64_t C = (total + chunk - 1) / chunk;
   const int64_t per = (std::min(chunk, total) + 32 * E2_T - 1) / (32 * E2_T);
   if (C >= 65536 || per >= ((int64_t)1 << 31)) throw std::runtime_error("train query: too many chunks / samples");
   hipLaunchKernelGGL(k_nof_eval_h2<true>, dim3((unsigned)per, (unsigned)C), dim3(256), 0, s, rays, stride, z, total,
-                     S, ein, img, p_out, coef, chunk);
+                     S, ein, img, p_out, coef, chunk, PCN_EH2_UNITS ? encu : nullptr, emx);
 }
 
 void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,

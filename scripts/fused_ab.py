@@ -42,7 +42,7 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     p = torch.empty_like(z)
     first = next(iter(Ls.values()))
-    ws = torch.empty(first.pcnerf_nof_train_fold_bytes(n * S, chunk), dtype=torch.uint8, device=dev)
+    ws = torch.empty(first.pcnerf_nof_train_fused_bytes(n * S, chunk), dtype=torch.uint8, device=dev)
     packed = torch.empty(first.pcnerf_nof_eval_packed_floats(), device=dev)
     times = {k: {"train": [], "eval": []} for k in Ls}
     outs = {}
