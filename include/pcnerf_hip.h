@@ -169,9 +169,7 @@ int pcnerf_nof_query_train_fold_backward(const float* rays, int64_t n_rays, int 
  * products, BatchNorm applied in each layer's epilogue); only the chunk statistics it needs come from the chunk's
  * encoding moments through the float64 layer algebra above -- exact because every LeakyReLU(True) is the identity
  * (negative_slope = 1, models.py:72,92).  Running stats are updated chunk by chunk as nn.BatchNorm1d does.  `state`:
- * pcnerf_nof_train_fused_bytes(total_samples, chunk) bytes of scratch (or pcnerf_nof_train_fold_bytes: then the
- * fused kernel evaluates the encodings itself instead of taking them from the moment pass; same results). */
-size_t pcnerf_nof_train_fused_bytes(int64_t total_samples, int64_t chunk);
+ * pcnerf_nof_train_fold_bytes(total_samples, chunk) bytes of scratch. */
 int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
                                  int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
                                  void* state, size_t state_bytes, float* p_out, void* stream);

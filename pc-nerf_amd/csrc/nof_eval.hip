@@ -514,9 +514,6 @@ constexpr int RG = PCN_EH2_RING, RD = RG - 1;
 #ifndef PCN_EH2_EARLY
 #define PCN_EH2_EARLY 1   // prologue: the samples' z and ray rows loaded before the weight-ring / coefficient loads
 #endif
-#ifndef PCN_EH2_SCU
-#define PCN_EH2_SCU 0     // prologue: the sincosf loop fully unrolled
-#endif
 #ifndef PCN_EH2_STAMP
 #define PCN_EH2_STAMP 0   // diagnostic builds only: per-block phase stamps of k_nof_eval_h2 (pcnerf_debug_eh2_clock)
 #endif
@@ -547,8 +544,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
                                                         const float* __restrict__ z, int64_t total, int S,
                                                         const float* __restrict__ ein, const float* __restrict__ W,
                                                         float* __restrict__ p_out, const float* __restrict__ coef,
-                                                        int64_t chunk, const float* __restrict__ encu,
-                                                        const float* __restrict__ emx) {
+                                                        int64_t chunk) {
   __shared__ eh_f16x8 act[16][E2_T][2][64];
   __shared__ eh_f16x8 eb[4][E2_T][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
   __shared__ int sx0s[E2_T * 32];
@@ -568,26 +564,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   // this thread's sample (threads < 96): its z and ray row loaded first, so their latency overlaps the weight-ring
   // and coefficient loads below (PCN_EH2_EARLY; the prologue otherwise waits for the two in turn)
   float rz = 0.0f, rr[6] = {};
-  // TR with encu (nof_fold.hip EncUnits): the block's 768 encoding units (8 features each) and their samples' max
-  // |feature| come from the moment pass; thread t splits units t, t + 256, t + 512 (loads issued here, first)
-  constexpr int NU = 32 * E2_T * 8 / 256;
-  static_assert(32 * E2_T * 8 % 256 == 0 && 32 * E2_T == 96, "encoding units: nof_fold.hip EU_BLOCK");
-  const bool units = TR && encu != nullptr;
-  f32x4 uva[NU], uvb[NU];
-  float umx[NU];
-  if (units) {
-    const int64_t bidx = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-    const int last = (int)(send - 1 - s0);   // padded samples take the block's last valid one (as below)
-#pragma unroll
-    for (int q = 0; q < NU; ++q) {
-      const int u = t + 256 * q, sm = u % (32 * E2_T), smc = sm < last ? sm : last;
-      const f32x4* up = reinterpret_cast<const f32x4*>(encu + ((bidx * 768) + (u - sm) + smc) * 8);
-      uva[q] = up[0];
-      uvb[q] = up[1];
-      umx[q] = emx[bidx * (32 * E2_T) + smc];
-    }
-  }
-  if (PCN_EH2_EARLY && !ein && !units && t < 32 * E2_T) {
+  if (PCN_EH2_EARLY && !ein && t < 32 * E2_T) {
     int64_t g = s0 + t;
     if (g >= send) g = send - 1;
     const float* r = rays + (g / S) * stride;
@@ -651,29 +628,6 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   if (PCN_EH2_STAMP == 2) EH2_STAMP(11);
   float* const encf = reinterpret_cast<float*>(&act[0][0][0][0]);   // [sample][65]
   static_assert(sizeof(act) >= 32 * E2_T * 65 * sizeof(float), "encoding staging area");
-  if (units) {
-#pragma unroll
-    for (int q = 0; q < NU; ++q) {
-      const int u = t + 256 * q, sm = u % (32 * E2_T), sq = u / (64 * E2_T), hh = (u / (32 * E2_T)) & 1;
-      int sx0 = eh_scale(umx[q]);
-      if (sxB[3] < sx0) sx0 = sxB[3];   // the encoding shares layer 4's input scale with h3
-      const float xs = ldexpf(1.0f, sx0);
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = uva[q][j] * xs;
-        v[4 + j] = uvb[q][j] * xs;
-      }
-      eh_f16x8 hi, mid;
-      eh_split8(v, hi, mid);
-      eb[sq][sm >> 5][0][(sm & 31) + 32 * hh] = hi;
-      eb[sq][sm >> 5][1][(sm & 31) + 32 * hh] = mid;
-      if (u < 32 * E2_T) {
-        emax[sm] = umx[q];
-        sx0s[sm] = sx0;
-      }
-    }
-  } else {
   if (!ein) {
     if (t < 32 * E2_T) {
       float p[3];
@@ -693,29 +647,12 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     }
     __syncthreads();
     if (PCN_EH2_STAMP == 2) EH2_STAMP(12);
-    // fully unrolled (PCN_EH2_SCU): the iterations' LDS reads and sincosf chains interleave instead of running one
-    // dependent chain after another at one wave per SIMD
-    if (PCN_EH2_SCU) {
-      constexpr int NI = (32 * E2_T * 30 + 255) / 256;
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int i = t + 256 * j;
-        if (i < 32 * E2_T * 30) {
-          const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
-          float sv, cv;
-          sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
-          encf[sm * 65 + 3 + 6 * k + m] = sv;
-          encf[sm * 65 + 6 + 6 * k + m] = cv;
-        }
-      }
-    } else {
-      for (int i = t; i < 32 * E2_T * 30; i += 256) {
-        const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
-        float sv, cv;
-        sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
-        encf[sm * 65 + 3 + 6 * k + m] = sv;
-        encf[sm * 65 + 6 + 6 * k + m] = cv;
-      }
+    for (int i = t; i < 32 * E2_T * 30; i += 256) {
+      const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
+      float sv, cv;
+      sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
+      encf[sm * 65 + 3 + 6 * k + m] = sv;
+      encf[sm * 65 + 6 + 6 * k + m] = cv;
     }
     __syncthreads();
     if (PCN_EH2_STAMP == 2) EH2_STAMP(13);
@@ -753,7 +690,6 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       }
     emax[t] = m;
     sx0s[t] = sx0;
-  }
   }
   __syncthreads();
   EH2_STAMP(1);
@@ -1039,7 +975,7 @@ static void launch_eval(const float* rays, int stride, const float* z, int64_t t
   const int64_t blocks = ((total + 31) / 32 + 3) / 4;
   if (g_eval_math == 1 && PCN_EH2)
     hipLaunchKernelGGL(k_nof_eval_h2<false>, dim3((unsigned)((total + 32 * E2_T - 1) / (32 * E2_T))), dim3(256), 0,
-                       s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0, nullptr, nullptr);
+                       s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0);
   else if (g_eval_math == 1)
     hipLaunchKernelGGL(k_nof_eval_h, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
                        p_out);
@@ -1198,13 +1134,12 @@ void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s) {
 }
 
 void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
-                        const float* img, const float* coef, int64_t chunk, const float* encu, const float* emx,
-                        float* p_out, hipStream_t s) {
+                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s) {
   const int64_t C = (total + chunk - 1) / chunk;
   const int64_t per = (std::min(chunk, total) + 32 * E2_T - 1) / (32 * E2_T);
   if (C >= 65536 || per >= ((int64_t)1 << 31)) throw std::runtime_error("train query: too many chunks / samples");
   hipLaunchKernelGGL(k_nof_eval_h2<true>, dim3((unsigned)per, (unsigned)C), dim3(256), 0, s, rays, stride, z, total,
-                     S, ein, img, p_out, coef, chunk, PCN_EH2_UNITS ? encu : nullptr, emx);
+                     S, ein, img, p_out, coef, chunk);
 }
 
 void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,

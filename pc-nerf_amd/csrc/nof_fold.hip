@@ -110,18 +110,6 @@ struct SampleSrc {   // the query's flattened ray-major samples (rays + z) or an
   int64_t total, chunk;
 };
 
-// The fused query's encoding units (k_nof_eval_h2<true>'s layer-0 / layer-4 operands, nof_eval.hip): k_tf_moments,
-// which evaluates every sample's encoding anyway, also writes it as fp32 in the query's B-operand unit order --
-// per chunk, per 96-sample block, unit u = (2 k-step + lane half) * 96 + sample, 8 features 2 (8 k-step + j) + half
-// (feature 63 = 0) -- and each sample's max |feature|; the query's prologue then splits them instead of evaluating
-// 30 sincosf per sample at one wave per SIMD.  u == nullptr: the query evaluates the encodings itself.
-struct EncUnits {
-  float* u;     // [C][nb][768][8]
-  float* mx;    // [C][nb * 96]
-  int64_t nb;   // 96-sample blocks per chunk
-};
-constexpr int EU_BLOCK = 96;   // = 32 * E2_T of nof_eval.hip (checked there)
-
 __device__ __forceinline__ void sample_enc(const SampleSrc& q, int64_t g, float (&f)[64]) {
   if (q.ein) {
     const float* r = q.ein + g * 63;
@@ -157,7 +145,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 constexpr int TM_P = 72;
 
-__global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F, EncUnits E) {
+__global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
   __shared__ __attribute__((aligned(16))) _Float16 th[4][2][64 * TM_P];
   __shared__ float sh0[64];
   const int c = blockIdx.y, w = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -200,15 +188,7 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F, EncU
     int sk = (dm >= 32768.0f && dm < 3.0e38f) ? ilogbf(dm) - 14 : 0;
     sk = sk > 24 ? 24 : sk;
     const float dsc = ldexpf(1.0f, -sk);
-    // (E.u: this sample's encoding also stored in the fused query's unit order; only with positions, not ein)
-    float* const ub = (E.u && ok && !q.ein) ? E.u + ((c * E.nb + i / EU_BLOCK) * 768) * 8 + (i % EU_BLOCK) * 8
-                                           : nullptr;
-    float emx = 0.0f;
     auto put = [&](int f, float v) {
-      if (ub) {
-        ub[((f >> 4) * 2 + (f & 1)) * EU_BLOCK * 8 + ((f >> 1) & 7)] = v;
-        emx = fmaxf(emx, fabsf(v));
-      }
       const float d = ok ? (v - sh0[f]) * dsc : 0.0f;
       const _Float16 h = (_Float16)d;
       hi[f * TM_P + lane] = h;
@@ -231,10 +211,6 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F, EncU
           put(6 + 6 * k + m, cv);
         }
       }
-    }
-    if (ub) {
-      ub[(3 * 2 + 1) * EU_BLOCK * 8 + 7] = 0.0f;   // feature 63 (zero padding)
-      E.mx[c * E.nb * EU_BLOCK + i] = emx;
     }
     hi[63 * TM_P + lane] = ok ? (_Float16)dsc : (_Float16)0.0f;
     mi[63 * TM_P + lane] = (_Float16)0.0f;
@@ -818,11 +794,10 @@ static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, fl
   PCN_CHECK(to_dev_params(params, eps, &P), "train fold: null parameter pointer");
   const FoldDev F = fold_dev(Lo, state);
   const double ep = (double)eps;
-  const EncUnits E{};
   {
     // algorithmic work per sample: the encoding + 3 x 32 x 32 x 2 flops per k-step pair; bytes: z in, ray rows
     ProfScope ps(s, PT_FOLD_MOMENTS, 6144.0 * (double)q.total, 4.0 * (double)q.total);
-    hipLaunchKernelGGL(k_tf_moments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F, E);
+    hipLaunchKernelGGL(k_tf_moments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F);
   }
   {
     ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
@@ -845,11 +820,6 @@ static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, fl
   hipLaunchKernelGGL(k_tf_running, dim3(8), dim3(256), 0, s, P, F, q, (double)momentum);
 }
 
-static size_t enc_units_bytes(int64_t total, int64_t chunk) {
-  const int64_t C = (total + chunk - 1) / chunk, nb = (std::min(chunk, total) + EU_BLOCK - 1) / EU_BLOCK;
-  return (size_t)C * nb * EU_BLOCK * (64 + 1) * sizeof(float);
-}
-
 // The train-mode query evaluated per sample (the network as written, one BatchNorm coefficient set per chunk):
 // the chunk statistics from the encoding moments and the float64 layer algebra above, then k_nof_eval_h2<true>.
 static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, float momentum, float eps,
@@ -864,18 +834,10 @@ static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, f
   PCN_CHECK(to_dev_params(params, eps, &P), "train query: null parameter pointer");
   const FoldDev F = fold_dev(Lo, state);
   const double ep = (double)eps;
-  // the encoding units behind the fold layout when the state has room for them (pcnerf_nof_train_fused_bytes);
-  // else (a state of pcnerf_nof_train_fold_bytes) the query evaluates the encodings in its prologue
-  EncUnits E{};
-  if (PCN_EH2_UNITS && !q.ein && state_bytes >= Lo.doubles * sizeof(double) + enc_units_bytes(q.total, q.chunk)) {
-    E.nb = (std::min(q.chunk, q.total) + EU_BLOCK - 1) / EU_BLOCK;
-    E.u = reinterpret_cast<float*>(static_cast<double*>(state) + Lo.doubles);
-    E.mx = E.u + (size_t)Lo.C * E.nb * 768 * 8;
-  }
   pack_train_query(P, F.img, s);
   {
     ProfScope ps(s, PT_FOLD_MOMENTS, 6144.0 * (double)q.total, 4.0 * (double)q.total);
-    hipLaunchKernelGGL(k_tf_moments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F, E);
+    hipLaunchKernelGGL(k_tf_moments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F);
   }
   {
     ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
@@ -894,7 +856,7 @@ static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, f
   {
     // algorithmic work: 982,528 FLOP per sample (9 Linear layers); bytes: z in, p out, ray rows
     ProfScope ps(s, PT_TRAIN_QUERY, 982528.0 * (double)q.total, 8.0 * (double)q.total);
-    launch_train_query(q.rays, q.stride, q.z, q.total, q.S, q.ein, F.img, F.coef, q.chunk, E.u, E.mx, p_out, s);
+    launch_train_query(q.rays, q.stride, q.z, q.total, q.S, q.ein, F.img, F.coef, q.chunk, p_out, s);
   }
   hipLaunchKernelGGL(k_tf_running, dim3(8), dim3(256), 0, s, P, F, q, (double)momentum);
 }
@@ -940,12 +902,6 @@ using namespace pcn;
 extern "C" size_t pcnerf_nof_train_fold_bytes(int64_t total_samples, int64_t chunk) {
   if (total_samples <= 0 || chunk <= 0) return 0;
   return fold_layout(total_samples, std::min(chunk, total_samples)).doubles * sizeof(double);
-}
-
-extern "C" size_t pcnerf_nof_train_fused_bytes(int64_t total_samples, int64_t chunk) {
-  if (total_samples <= 0 || chunk <= 0) return 0;
-  chunk = std::min(chunk, total_samples);
-  return fold_layout(total_samples, chunk).doubles * sizeof(double) + enc_units_bytes(total_samples, chunk);
 }
 
 extern "C" int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z,

@@ -33,13 +33,9 @@ void launch_fold_logits(const float* rays, int stride, const float* z, int64_t t
 // per-layer operand scales of its bound.
 size_t train_query_image_floats();
 constexpr int TQ_COEF_FLOATS = 16 * 256 + 16;   // per chunk: [L][alpha 256 | beta'' 256], then sxB[8] (int)
-#ifndef PCN_EH2_UNITS
-#define PCN_EH2_UNITS 0   // the fused train query takes the encodings from the moment pass (nof_fold.hip EncUnits)
-#endif
 void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s);
 void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
-                        const float* img, const float* coef, int64_t chunk, const float* encu, const float* emx,
-                        float* p_out, hipStream_t s);
+                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s);
 
 // p = o + d*z, one rounding per op (render.py:458; built with -ffp-contract=off).
 __device__ __forceinline__ void sample_point(const float* __restrict__ r, float z, float (&p)[3]) {

@@ -222,7 +222,7 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
         chunk = max(1, min(int(chunk), R * S))
         mom, eps = _bn_config(model)
         s, keep = _params(model)
-        ws = _workspace(z.device, int(L.pcnerf_nof_train_fused_bytes(R * S, chunk)))
+        ws = _workspace(z.device, int(L.pcnerf_nof_train_fold_bytes(R * S, chunk)))
         H.check(L.pcnerf_nof_query_train_fused(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
                                                ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(), p.data_ptr(), st))
         _track_batches(model, -(-R * S // int(chunk)))

@@ -42,9 +42,11 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     p = torch.empty_like(z)
     first = next(iter(Ls.values()))
-    ws = torch.empty(first.pcnerf_nof_train_fused_bytes(n * S, chunk), dtype=torch.uint8, device=dev)
+    ws = torch.empty(first.pcnerf_nof_train_fold_bytes(n * S, chunk), dtype=torch.uint8, device=dev)
     packed = torch.empty(first.pcnerf_nof_eval_packed_floats(), device=dev)
     times = {k: {"train": [], "eval": []} for k in Ls}
+    tags = {16: "moments", 17: "algebra", 18: "train_query"}   # prof.h: per-kernel HIP events of the train query
+    ktimes = {k: {v: [] for v in tags.values()} for k in Ls}
     outs = {}
     for rnd in range(rounds):
         for name, L in Ls.items():
@@ -57,6 +59,7 @@ def main():
                     s, keep = _ops._params(m)
                     assert L.pcnerf_nof_pack_eval(ctypes.byref(s), packed.data_ptr(), st) == 0
                 torch.cuda.synchronize()
+                L.pcnerf_prof_enable(1 if mode == "train" else 0)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 if mode == "train":
@@ -73,6 +76,13 @@ def main():
                     outs[(name, mode)] = p.clone()
                 else:
                     times[name][mode].append(e0.elapsed_time(e1))
+                    if mode == "train":
+                        for tg, nm in tags.items():
+                            tm, nn, fl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+                            L.pcnerf_prof_read(tg, ctypes.byref(tm), ctypes.byref(nn), ctypes.byref(fl), ctypes.byref(by))
+                            if nn.value:
+                                ktimes[name][nm].append(tm.value)
+                L.pcnerf_prof_enable(0)
     res = {}
     for name in Ls:
         r = {}
@@ -83,6 +93,9 @@ def main():
                 ref = outs[("base", mode)]
                 d = (outs[(name, mode)] - ref).abs() / ref.abs().clamp_min(1e-12)
                 r[mode + "_max_rel_vs_base"] = float(d.max())
+        for nm, v in ktimes[name].items():
+            if v:
+                r[nm + "_ms"] = round(sorted(v)[len(v) // 2], 3)
         res[name] = r
     print(json.dumps({"rays": n, "S": S, "chunk": chunk, "variants": res}, indent=1))
 
