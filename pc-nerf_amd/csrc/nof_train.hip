@@ -1772,6 +1772,9 @@ constexpr size_t DGRAD_W_FLOATS = 7 * SZ_H;
 constexpr int GMAX_SLOTS = 64;                     // per layer: atomicMax targets of the |dL/dh| maxima
 constexpr int GMAX_DBL = 8 * GMAX_SLOTS / 2;       // their doubles in the per-chunk s12 region
 constexpr int WG_BLOCKS = 256;  // weight-gradient partials per chunk (one 8-wave block per CU)
+#ifndef PCN_WB3_L0X2
+#define PCN_WB3_L0X2 1             // layer 0's encoding-column weight gradient at two workgroups per CU
+#endif
 
 __host__ __device__ constexpr int in_features(int L) { return L == 0 ? 63 : L == 4 ? 319 : 256; }
 
@@ -3146,19 +3149,24 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       }
       cur ^= 1;
     }
-    // 4. layer 0 on the encoding
+    // 4. layer 0 on the encoding.  Under the split math at TWO workgroups per CU (PCN_WB3_L0X2): the
+    // encoding-column launch is latency-bound on its sincosf staging at one 8-wave workgroup per CU, and its
+    // 127 VGPRs and 66 KiB of LDS let a second one share the CU (its partials: 2 x WG_BLOCKS slots of k_wgrad<1>'s
+    // layout, within the buffer sized for WG_BLOCKS of k_wgrad<2>'s)
+    static_assert(2 * WG_BLOCKS * WgradCfg<1>::PART <= WG_BLOCKS * WgradCfg<2>::PART, "layer-0 partial slots");
+    const unsigned wb0 = (split && PCN_WB3_L0X2) ? (unsigned)std::min<int64_t>(2 * ntiles, 2 * WG_BLOCKS) : wblocks;
     {
       ProfScope ps(s, split ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
       if (split)
-        launch_wgrad_b3<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
+        launch_wgrad_b3<1>(wb0, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
                            ws.gmax + 0 * GMAX_SLOTS, ws.part);
       else
         launch_wgrad<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
                         ws.part);
     }
     {
-      ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<1>::PART * 4.0);
-      hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)wblocks,
+      ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wb0 * WgradCfg<1>::PART * 4.0);
+      hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)wb0,
                          P.lin_w[0], (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr);
     }
   }
