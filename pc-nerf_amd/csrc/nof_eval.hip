@@ -38,7 +38,7 @@ constexpr size_t OFF_BIAS = 2 * SZ_E + 7 * SZ_H;
 constexpr size_t OFF_WOUT = OFF_BIAS + 8 * 256;
 constexpr size_t OFF_BOUT = OFF_WOUT + 256;
 constexpr size_t EVAL_F32_FLOATS = OFF_BOUT + 4;   // the fp32 image (k_nof_eval)
-// split-fp16 image (k_nof_eval_h), appended: [sw: 8 int32 exponents, 16-float aligned][120 k-steps][ob 8][part 2]
+// split-fp16 image (k_nof_eval_h2), appended: [sw: 8 int32 exponents, 16-float aligned][120 k-steps][ob 8][part 2]
 // [lane 64] f16x8 -- the eval network's 120 k-steps of 16 features (layer 0: 4, layers 1-3, 5-7: 16, layer 4: 4 + 16)
 constexpr int EH_KSTEPS = 120;
 constexpr size_t EH_VECS = (size_t)EH_KSTEPS * 8 * 2 * 64;
@@ -225,21 +225,6 @@ __global__ __launch_bounds__(256) void k_eval_wscale(NofParamsDev P, float* __re
 }
 
 typedef _Float16 eh_f16x8 __attribute__((ext_vector_type(8)));
-#ifndef PCN_EH2
-#define PCN_EH2 1   // split eval query as k_nof_eval_h2 (neuron-split waves, activations through LDS)
-#endif
-#ifndef PCN_EH2_PF
-#define PCN_EH2_PF 0   // k_nof_eval_h2: the next k-step's B operands read during this k-step's MFMAs
-#endif
-#ifndef PCN_EH_WLATE
-#define PCN_EH_WLATE 1   // publish the next super-slice after this one's MFMAs (else before them)
-#endif
-#ifndef PCN_EH_ORD
-#define PCN_EH_ORD 1   // k_nof_eval_h: MFMAs product-major over the 8 out-blocks (independent accumulators)
-#endif
-#ifndef PCN_EH_KPB
-#define PCN_EH_KPB 1   // k_nof_eval_h: k-steps per weight super-slice (one barrier each)
-#endif
 
 template <bool RAW>
 __global__ void k_pack_eval_h(NofParamsDev P, float* __restrict__ out) {
@@ -303,192 +288,6 @@ __device__ __forceinline__ void eh_split8(const float (&v)[8], eh_f16x8& hi, eh_
   }
 }
 
-__global__ __launch_bounds__(256, 1) void k_nof_eval_h(const float* __restrict__ rays, int stride,
-                                                       const float* __restrict__ z, int64_t total, int S,
-                                                       const float* __restrict__ ein, const float* __restrict__ W,
-                                                       float* __restrict__ p_out) {
-  // weight stream in super-slices of KPB k-steps (16 KiB each), two LDS slots, one barrier per super-slice
-  constexpr int KPB = PCN_EH_KPB, NV = 4 * KPB;   // vectors per thread per super-slice
-  static_assert(EH_KSTEPS % KPB == 0, "super-slices");
-  __shared__ eh_f16x8 wsl[2][KPB * 8 * 2 * 64];
-  __shared__ __attribute__((aligned(16))) float sbias[8 * 256];
-  const int t = threadIdx.x, lane = t & 63, h = lane >> 5;
-  const int64_t tile = (int64_t)blockIdx.x * 4 + (t >> 6);
-  const int64_t g = tile * 32 + (lane & 31);
-  const int64_t gc = g < total ? g : total - 1;
-  const eh_f16x8* __restrict__ img = reinterpret_cast<const eh_f16x8*>(W + OFF_EH);
-  int sw[8];
-#pragma unroll
-  for (int L = 0; L < 8; ++L) sw[L] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(W + OFF_EH_SW)[L]);
-  // thread t moves vectors t + 256 m of each super-slice
-  constexpr int NSS = EH_KSTEPS / KPB;
-  eh_f16x8 ldA[NV], ldB[NV];
-#pragma unroll
-  for (int m = 0; m < NV; ++m) wsl[0][t + 256 * m] = img[t + 256 * m];
-#pragma unroll
-  for (int m = 0; m < NV; ++m) ldA[m] = img[(size_t)1024 * KPB + t + 256 * m];
-  for (int i = t; i < 8 * 256 / 4; i += 256)
-    reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
-  float e[32];
-  if (ein) {
-    load_embedding<0>(ein + gc * 63, h, e);
-  } else {
-    const float* r = rays + (gc / S) * stride;
-    float p[3];
-    sample_point(r, z[gc], p);
-    encode_half(p, h, e);
-  }
-  __syncthreads();
-  int gk = 0;
-  f32x16 acc[8];
-  // one k-step of the current layer: B operands (xh, xm), A operands from the super-slice in LDS.  The first
-  // k-step of a super-slice issues the loads of the one after next; the next one (loaded a super-slice earlier) is
-  // published into the other slot (last read before the previous barrier) after this super-slice's MFMAs
-  // (PCN_EH_WLATE) or before them; the last k-step ends with the barrier.
-  auto kstep = [&](const eh_f16x8& xh, const eh_f16x8& xm, bool first) {
-    const int ss = gk / KPB, sub = gk - ss * KPB;
-    if (sub == 0) {
-      if (!PCN_EH_WLATE && ss + 1 < NSS) {
-#pragma unroll
-        for (int m = 0; m < NV; ++m) wsl[(ss + 1) & 1][t + 256 * m] = ldA[m];
-      }
-      if (ss + 2 < NSS) {
-#pragma unroll
-        for (int m = 0; m < NV; ++m) ldB[m] = img[(size_t)(ss + 2) * 1024 * KPB + t + 256 * m];
-      }
-    }
-    const eh_f16x8* sl = wsl[ss & 1] + sub * 1024;
-    if (PCN_EH_ORD) {   // product-major: all 16 A operands, then 8 independent MFMAs per product
-      eh_f16x8 aa[8][2];
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob) {
-        aa[ob][0] = sl[(2 * ob) * 64 + lane];
-        aa[ob][1] = sl[(2 * ob + 1) * 64 + lane];
-      }
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob)
-        acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[ob][0], xh, first ? f32x16{} : acc[ob], 0, 0, 0);
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob) acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[ob][0], xm, acc[ob], 0, 0, 0);
-#pragma unroll
-      for (int ob = 0; ob < 8; ++ob) acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[ob][1], xh, acc[ob], 0, 0, 0);
-    } else {
-    eh_f16x8 a[3][2];
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      a[d][0] = sl[(2 * d) * 64 + lane];
-      a[d][1] = sl[(2 * d + 1) * 64 + lane];
-    }
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) {
-      if (ob + 2 < 8) {
-        a[(ob + 2) % 3][0] = sl[((ob + 2) * 2) * 64 + lane];
-        a[(ob + 2) % 3][1] = sl[((ob + 2) * 2 + 1) * 64 + lane];
-      }
-      const eh_f16x8 a0 = a[ob % 3][0], a1 = a[ob % 3][1];
-      acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, xh, first ? f32x16{} : acc[ob], 0, 0, 0);
-      acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, xm, acc[ob], 0, 0, 0);
-      acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, xh, acc[ob], 0, 0, 0);
-    }
-    }
-    if (sub == KPB - 1) {
-      if (PCN_EH_WLATE && ss + 1 < NSS) {
-#pragma unroll
-        for (int m = 0; m < NV; ++m) wsl[(ss + 1) & 1][t + 256 * m] = ldA[m];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int m = 0; m < NV; ++m) ldA[m] = ldB[m];
-    }
-    ++gk;
-  };
-  // the encoding's B operands at per-sample scale 2^sx
-  eh_f16x8 eh[4], em[4];
-  auto split_e = [&](int sx) {
-    const float xs = ldexpf(1.0f, sx);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = e[8 * s + j] * xs;
-      eh_split8(v, eh[s], em[s]);
-    }
-  };
-  auto max_e = [&]() {
-    float m = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) m = fmaxf(m, fabsf(e[i]));
-    return m;
-  };
-  // layer epilogue: acc <- acc 2^-(sw + sx) + bias (fp32 layer output); returns the lane's max |output|
-  auto epi = [&](int L, int sx) {
-    const float us = ldexpf(1.0f, -(sw[L] + sx));
-    float m = 0.0f;
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + 256 * L + 32 * ob + 8 * gq + 4 * h);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float v = acc[ob][4 * gq + q] * us + b[q];
-          acc[ob][4 * gq + q] = v;
-          m = fmaxf(m, fabsf(v));
-        }
-      }
-    return m;
-  };
-  eh_f16x8 xh[16], xm[16];   // the hidden B operands
-  auto split_h = [&](int sx) {
-    const float xs = ldexpf(1.0f, sx);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = acc[s >> 1][8 * (s & 1) + j] * xs;
-      eh_split8(v, xh[s], xm[s]);
-    }
-  };
-  auto pair_max = [&](float m) { return fmaxf(m, __shfl_xor(m, 32, 64)); };
-  // layer 0: encoding -> 256
-  int sx = eh_scale(pair_max(max_e()));
-  split_e(sx);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) kstep(eh[s], em[s], s == 0);
-  float mx = epi(0, sx);
-#pragma unroll 1
-  for (int L = 1; L < 8; ++L) {
-    if (L == 4) {   // skip layer: [encoding, h3] share one per-sample scale
-      sx = eh_scale(pair_max(fmaxf(mx, max_e())));
-      split_h(sx);
-      split_e(sx);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) kstep(eh[s], em[s], s == 0);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) kstep(xh[s], xm[s], false);
-    } else {
-      sx = eh_scale(pair_max(mx));
-      split_h(sx);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) kstep(xh[s], xm[s], s == 0);
-    }
-    mx = epi(L, sx);
-  }
-  // occ_out: Linear(256, 1) + Sigmoid on the fp32 layer-7 output, k_nof_eval's summation order
-  float part = 0.0f;
-#pragma unroll
-  for (int ob = 0; ob < 8; ++ob) {
-#pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      const f32x4 wv = *reinterpret_cast<const f32x4*>(W + OFF_WOUT + 32 * ob + 8 * gq + 4 * h);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) part = fmaf(wv[q], acc[ob][4 * gq + q], part);
-    }
-  }
-  const float logit = part + __shfl_xor(part, 32, 64) + W[OFF_BOUT];
-  if (lane < 32 && g < total) p_out[g] = sigmoid_ref(logit);
-}
-
 // ---- k_nof_eval_h2: the same split eval network with the work split over NEURONS inside a block: wave w owns
 // out-blocks 2w, 2w+1 (64 neurons) of every layer for all 96 samples (3 tiles) of its block, so each wave streams
 // only its own 64 neurons' weights from L2 (4 KiB per k-step, three k-steps in flight in a 4-slot register ring,
@@ -505,15 +304,6 @@ constexpr int E2_T = PCN_EH2_T;   // sample tiles per block
 #define PCN_EH2_RING 4    // k_nof_eval_h2: weight-ring slots (prefetch distance RING - 1 k-steps); 4 or 8
 #endif
 constexpr int RG = PCN_EH2_RING, RD = RG - 1;
-#ifndef PCN_EH2_ROT
-#define PCN_EH2_ROT 0     // TR: each block walks its hidden k-steps rotated by blockIdx (spreads the L2 weight reads)
-#endif
-#ifndef PCN_EH2_ABL
-#define PCN_EH2_ABL 0     // diagnostic timing ablations (wrong results): 1 weights of k-step 0 only, 2 no B re-reads
-#endif
-#ifndef PCN_EH2_EARLY
-#define PCN_EH2_EARLY 1   // prologue: the samples' z and ray rows loaded before the weight-ring / coefficient loads
-#endif
 #ifndef PCN_EH2_STAMP
 #define PCN_EH2_STAMP 0   // diagnostic builds only: per-block phase stamps of k_nof_eval_h2 (pcnerf_debug_eh2_clock)
 #endif
@@ -562,9 +352,9 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   if (s0 >= send) return;   // (the last chunk's surplus blocks; uniform over the block, before any barrier)
   EH2_STAMP(0);
   // this thread's sample (threads < 96): its z and ray row loaded first, so their latency overlaps the weight-ring
-  // and coefficient loads below (PCN_EH2_EARLY; the prologue otherwise waits for the two in turn)
+  // and coefficient loads below (the prologue otherwise waits for the two in turn: -0.7 %)
   float rz = 0.0f, rr[6] = {};
-  if (PCN_EH2_EARLY && !ein && t < 32 * E2_T) {
+  if (!ein && t < 32 * E2_T) {
     int64_t g = s0 + t;
     if (g >= send) g = send - 1;
     const float* r = rays + (g / S) * stride;
@@ -584,7 +374,6 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   }
   // this wave's A operands of k-step gk: out-blocks 2w + o, parts hi / mid
   auto load_w = [&](eh_f16x8 (&d)[2][2], int gk) {
-    if (PCN_EH2_ABL & 1) gk = 0;
 #pragma unroll
     for (int o = 0; o < 2; ++o)
 #pragma unroll
@@ -593,8 +382,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   // ring of 4 k-steps of A operands, slot = k-step index within its layer & 3 (every layer's k-step count and
   // start are multiples of 4, so the slot is a compile-time index in the unrolled k-loops and no in-flight load's
   // registers are ever copied): k-step s issues the loads of k-step s + 3 into the slot k-step s - 1 just used
-  // hidden k-steps walked from k-step rot of their layer (TR && PCN_EH2_ROT): the image k-step of processing step q
-  const int rot = (TR && PCN_EH2_ROT) ? (int)(blockIdx.x & 15) : 0;
+  const int rot = 0;   // (the first hidden k-step read of each layer)
   auto kmap = [&](int q) __attribute__((always_inline)) {
     if (q < 4 || (q >= 52 && q < 56) || q >= EH_KSTEPS) return q < EH_KSTEPS ? q : EH_KSTEPS - 1;
     const int st = q < 52 ? 4 + ((q - 4) & ~15) : 56 + ((q - 56) & ~15);
@@ -631,13 +419,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   if (!ein) {
     if (t < 32 * E2_T) {
       float p[3];
-      if (PCN_EH2_EARLY) {
-        sample_point(rr, rz, p);
-      } else {
-        int64_t g = s0 + t;
-        if (g >= send) g = send - 1;
-        sample_point(rays + (g / S) * stride, z[g], p);
-      }
+      sample_point(rr, rz, p);
 #pragma unroll
       for (int m = 0; m < 3; ++m) {
         spos[t][m] = p[m];
@@ -700,7 +482,6 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   int gk = 0;
   // one k-step: B operands of the 3 tiles (from the encoding at the lane's scale, or the split activations),
   // MFMAs product-major over the 6 accumulators
-  eh_f16x8 pbh[E2_T], pbm[E2_T];   // PCN_EH2_PF: the next hidden k-step's B operands, read during this one
   auto kstep = [&](int s, int pos, bool enc, bool first) __attribute__((always_inline)) {   // pos: the k-step's index within its layer
     // (k-steps past the end reload the last one: unconditional loads keep the ring's registers statically known
     // to the waitcnt pass -- a conditional load made it wait for every load in flight)
@@ -709,10 +490,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     eh_f16x8 bh[E2_T], bm[E2_T];
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
-      if (PCN_EH2_PF && !enc && s > 0) {
-        bh[tau] = pbh[tau];
-        bm[tau] = pbm[tau];
-      } else if (enc) {
+      if (enc) {
         bh[tau] = eb[s][tau][0][lane];
         bm[tau] = eb[s][tau][1][lane];
         const int d = TR ? 0 : sxl[tau] - sx0s[32 * tau + li];
@@ -726,13 +504,6 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       } else {
         bh[tau] = act[s][tau][0][lane];
         bm[tau] = act[s][tau][1][lane];
-      }
-    }
-    if (PCN_EH2_PF && !enc && s + 1 < 16) {
-#pragma unroll
-      for (int tau = 0; tau < E2_T; ++tau) {
-        pbh[tau] = act[s + 1][tau][0][lane];
-        pbm[tau] = act[s + 1][tau][1][lane];
       }
     }
 #pragma unroll
@@ -851,7 +622,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
         for (int o = 0; o < 2; ++o)
           acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bm[tau], (first && s == 0) ? f32x16{} : acc[o][tau], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < 16 && !(PCN_EH2_ABL & 2)) {
+      if (s + 1 < 16) {
 #pragma unroll
         for (int tau = 0; tau < E2_T; ++tau) bm[tau] = act[(s + 1 + rot) & 15][tau][1][lane];
       }
@@ -867,7 +638,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
         for (int o = 0; o < 2; ++o)
           acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < 16 && !(PCN_EH2_ABL & 2)) {
+      if (s + 1 < 16) {
 #pragma unroll
         for (int tau = 0; tau < E2_T; ++tau) bh[tau] = act[(s + 1 + rot) & 15][tau][0][lane];
       }
@@ -967,21 +738,19 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   EH2_STAMP(10);
 }
 
-// Eval-mode MLP arithmetic: 0 = fp32 MFMA (k_nof_eval), 1 = split fp16, 3 products (k_nof_eval_h, default).
+// Eval-mode MLP arithmetic: 0 = fp32 MFMA (k_nof_eval), 1 = split fp16, 3 products (k_nof_eval_h2, default).
 static int g_eval_math = 1;
 
 static void launch_eval(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const float* W, float* p_out, hipStream_t s) {
-  const int64_t blocks = ((total + 31) / 32 + 3) / 4;
-  if (g_eval_math == 1 && PCN_EH2)
+  if (g_eval_math == 1) {
     hipLaunchKernelGGL(k_nof_eval_h2<false>, dim3((unsigned)((total + 32 * E2_T - 1) / (32 * E2_T))), dim3(256), 0,
                        s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0);
-  else if (g_eval_math == 1)
-    hipLaunchKernelGGL(k_nof_eval_h, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
-                       p_out);
-  else
+  } else {
+    const int64_t blocks = ((total + 31) / 32 + 3) / 4;
     hipLaunchKernelGGL(k_nof_eval, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
                        p_out);
+  }
 }
 
 __global__ void k_embed(const float* __restrict__ pts, int64_t n, float* __restrict__ out) {
