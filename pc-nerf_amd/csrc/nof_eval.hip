@@ -300,11 +300,6 @@ __device__ __forceinline__ void eh_split8(const float (&v)[8], eh_f16x8& hi, eh_
 #define PCN_EH2_T 3
 #endif
 constexpr int E2_T = PCN_EH2_T;   // sample tiles per block
-#ifndef PCN_EH2_TALIAS
-#define PCN_EH2_TALIAS 0   // diagnostic timing builds only (WRONG results): LDS tiles >= 3 alias tile 0, so
-#endif                     // PCN_EH2_T=4 runs its instruction mix within the 3-tile LDS footprint
-constexpr int ET = PCN_EH2_TALIAS && E2_T > 3 ? 3 : E2_T;   // LDS sample tiles
-#define TSL(x) ((x) < ET ? (x) : 0)
 #ifndef PCN_EH2_RING
 #define PCN_EH2_RING 4    // k_nof_eval_h2: weight-ring slots (prefetch distance RING - 1 k-steps); 4 or 8
 #endif
@@ -340,8 +335,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
                                                         const float* __restrict__ ein, const float* __restrict__ W,
                                                         float* __restrict__ p_out, const float* __restrict__ coef,
                                                         int64_t chunk) {
-  __shared__ eh_f16x8 act[16][ET][2][64];
-  __shared__ eh_f16x8 eb[4][ET][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
+  __shared__ eh_f16x8 act[16][E2_T][2][64];
+  __shared__ eh_f16x8 eb[4][E2_T][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
   __shared__ int sx0s[E2_T * 32];
   // eval: the 8 layers' folded biases; TR: the chunk's [L][A | B] epilogue coefficients (see below)
   __shared__ __attribute__((aligned(16))) float sbias[(TR ? 16 : 8) * 256];
@@ -472,8 +467,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
         for (int j = 0; j < 8; ++j) v[j] = f[2 * (8 * s + j) + hh] * xs;
         eh_f16x8 hi, mid;
         eh_split8(v, hi, mid);
-        eb[s][TSL(tau)][0][l + 32 * hh] = hi;
-        eb[s][TSL(tau)][1][l + 32 * hh] = mid;
+        eb[s][tau][0][l + 32 * hh] = hi;
+        eb[s][tau][1][l + 32 * hh] = mid;
       }
     emax[t] = m;
     sx0s[t] = sx0;
@@ -496,8 +491,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
       if (enc) {
-        bh[tau] = eb[s][TSL(tau)][0][lane];
-        bm[tau] = eb[s][TSL(tau)][1][lane];
+        bh[tau] = eb[s][tau][0][lane];
+        bm[tau] = eb[s][tau][1][lane];
         const int d = TR ? 0 : sxl[tau] - sx0s[32 * tau + li];
         if (d != 0) {   // eval layer 4: the 22-bit encoding (hi + mid, exact in fp32) re-split at the shared scale
           const float xs = ldexpf(1.0f, d);
@@ -507,8 +502,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
           eh_split8(v, bh[tau], bm[tau]);
         }
       } else {
-        bh[tau] = act[s][TSL(tau)][0][lane];
-        bm[tau] = act[s][TSL(tau)][1][lane];
+        bh[tau] = act[s][tau][0][lane];
+        bm[tau] = act[s][tau][1][lane];
       }
     }
 #pragma unroll
@@ -566,8 +561,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
           eh_f16x8 hi, mid;
           eh_split8(v, hi, mid);
           const int s = 4 * w + 2 * o + k;
-          act[s][TSL(tau)][0][lane] = hi;
-          act[s][TSL(tau)][1][lane] = mid;
+          act[s][tau][0][lane] = hi;
+          act[s][tau][1][lane] = mid;
         }
   };
   // eval phase 2 (after a barrier): the next layer's per-sample scale and this wave's B operands
@@ -613,8 +608,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
     eh_f16x8 bh[E2_T], bm[E2_T];
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
-      bm[tau] = act[rot][TSL(tau)][1][lane];
-      bh[tau] = act[rot][TSL(tau)][0][lane];
+      bm[tau] = act[rot][tau][1][lane];
+      bh[tau] = act[rot][tau][0][lane];
     }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
@@ -629,7 +624,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < 16) {
 #pragma unroll
-        for (int tau = 0; tau < E2_T; ++tau) bm[tau] = act[(s + 1 + rot) & 15][TSL(tau)][1][lane];
+        for (int tau = 0; tau < E2_T; ++tau) bm[tau] = act[(s + 1 + rot) & 15][tau][1][lane];
       }
       __builtin_amdgcn_sched_barrier(0);   // (else the scheduler sinks the reads down to their use)
 #pragma unroll
@@ -645,7 +640,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < 16) {
 #pragma unroll
-        for (int tau = 0; tau < E2_T; ++tau) bh[tau] = act[(s + 1 + rot) & 15][TSL(tau)][0][lane];
+        for (int tau = 0; tau < E2_T; ++tau) bh[tau] = act[(s + 1 + rot) & 15][tau][0][lane];
       }
       __builtin_amdgcn_sched_barrier(0);
       ++gk;

@@ -39,7 +39,7 @@ def main():
         m.train()
         s, keep = _ops._params(m)
         chunk = int(os.environ.get("EH_CHUNK", "262144"))
-        ws = torch.empty(L.pcnerf_nof_train_fold_bytes(n * S, chunk), dtype=torch.uint8, device=dev)
+        ws = torch.empty((getattr(L, 'pcnerf_nof_train_fused_bytes', None) or L.pcnerf_nof_train_fold_bytes)(n * S, chunk), dtype=torch.uint8, device=dev)
 
     def run():
         if train:

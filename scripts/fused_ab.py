@@ -20,8 +20,9 @@ from nof.networks import NOF_coarse  # noqa: E402
 def load(path):
     L = ctypes.CDLL(path)
     for name, (res, args) in H._SIGS.items():
-        f = getattr(L, name)
-        f.restype, f.argtypes = res, args
+        f = getattr(L, name, None)
+        if f is not None:
+            f.restype, f.argtypes = res, args
     return L
 
 
@@ -42,7 +43,11 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     p = torch.empty_like(z)
     first = next(iter(Ls.values()))
-    ws = torch.empty(first.pcnerf_nof_train_fold_bytes(n * S, chunk), dtype=torch.uint8, device=dev)
+    def need(L):   # the fused query's state (pcnerf_nof_train_fused_bytes where the library has it)
+        f = getattr(L, "pcnerf_nof_train_fused_bytes", None) or L.pcnerf_nof_train_fold_bytes
+        f.restype, f.argtypes = ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64]
+        return f(n * S, chunk)
+    ws = torch.empty(max(need(L) for L in Ls.values()), dtype=torch.uint8, device=dev)
     packed = torch.empty(first.pcnerf_nof_eval_packed_floats(), device=dev)
     times = {k: {"train": [], "eval": []} for k in Ls}
     tags = {16: "moments", 17: "algebra", 18: "train_query"}   # prof.h: per-kernel HIP events of the train query
