@@ -315,6 +315,8 @@ def main(argv=None):
 
     L = _hip.lib()
 
+    breakdown = {}   # wall time of the instrumented (last) step, the one the kernel breakdown comes from
+
     def timed(steps, warmup):
         """warmup, barrier, ``steps`` timed steps (HIP events on the last), barrier; max over ranks."""
         with (torch.enable_grad() if grad else torch.no_grad()):
@@ -325,14 +327,22 @@ def main(argv=None):
                 tdist.barrier()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
+            eb0 = eb1 = None
             for i in range(steps):
                 # per-kernel HIP events (kernel breakdown + roofline) around every launch of the LAST timed step
                 # only: their own cost (two hipEventRecord per launch) then weighs 1/steps on the timed region
                 if i == steps - 1:
                     L.pcnerf_prof_enable(1)
+                    eb0 = torch.cuda.Event(enable_timing=True)
+                    eb0.record()
                 loss = step()
+            if eb0 is not None:
+                eb1 = torch.cuda.Event(enable_timing=True)
+                eb1.record()
             torch.cuda.synchronize(dev)
             el = time.perf_counter() - t0
+            if eb0 is not None:
+                breakdown["ms"] = eb0.elapsed_time(eb1)
             if dist:
                 tdist.barrier()
             lv = float(loss)
@@ -343,6 +353,7 @@ def main(argv=None):
     train_math = (("fold" if a.fold else _ops.get_train_math()) if train else None)
     eval_math = None if (train or a.fold) else _ops.get_eval_math()
     elapsed, loss_val = timed(a.steps, a.warmup)
+    kstep_ms = breakdown.get("ms", 0.0)
     roof, kernels = kernel_report(L, a, train_math, eval_math)
 
     # the same workload with the MLP on the fp32 MFMA pipe (train / eval math "fp32"), for comparison
@@ -435,6 +446,7 @@ def main(argv=None):
         "cd_vs_ref": cdref,
         "loss": loss_val,
         "kernels": kernels,
+        "kernels_step_ms": round(kstep_ms, 3),   # the instrumented last step's own time (the kernels' step)
     }
     print(json.dumps(out), flush=True)
     if dist:
