@@ -173,6 +173,13 @@ int pcnerf_nof_query_train_fold_backward(const float* rays, int64_t n_rays, int 
 int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
                                  int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
                                  void* state, size_t state_bytes, float* p_out, void* stream);
+/* The same query writing chunks 0..store_chunks-1 into an activation store (pcnerf_nof_store_bytes(chunk) bytes per
+ * chunk, the layout pcnerf_nof_query_train_store writes: raw layer outputs W_L x and BatchNorm sums) for
+ * pcnerf_nof_query_train_backward_store. */
+int pcnerf_nof_query_train_fused_store(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                       int n_samples, int64_t chunk, const pcnerf_nof_params* params, float momentum,
+                                       float eps, void* state, size_t state_bytes, float* p_out, void* store,
+                                       int64_t store_chunks, void* stream);
 /* NOF.forward(emb) in train mode on an embedded batch of n rows (one chunk), the same way. */
 int pcnerf_nof_forward_train_fused(const float* emb, int64_t n, const pcnerf_nof_params* params, float momentum,
                                    float eps, void* state, size_t state_bytes, float* p_out, void* stream);

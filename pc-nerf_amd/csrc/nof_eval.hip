@@ -80,9 +80,15 @@ __global__ void k_pack_eval_weights(NofParamsDev P, float* __restrict__ out) {
   out[idx] = col < 0 ? 0.0f : alpha * P.lin_w[layer][(size_t)n * in_f + col];
 }
 
+// RAW (the train query's image): the Linear biases as they are (its activation-store writes add them to W x)
+template <bool RAW>
 __global__ void k_pack_eval_vectors(NofParamsDev P, float* __restrict__ out) {
   const int n = threadIdx.x;  // 256 threads
   for (int layer = 0; layer < 8; ++layer) {
+    if (RAW) {
+      out[OFF_BIAS + layer * 256 + n] = P.lin_b[layer][n];
+      continue;
+    }
     const float alpha = (1.0f / sqrtf(P.bn_rv[layer][n] + P.eps)) * P.bn_w[layer][n];
     const float beta = P.bn_b[layer][n] - P.bn_rm[layer][n] * alpha;
     out[OFF_BIAS + layer * 256 + n] = alpha * P.lin_b[layer][n] + beta;
@@ -334,7 +340,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
                                                         const float* __restrict__ z, int64_t total, int S,
                                                         const float* __restrict__ ein, const float* __restrict__ W,
                                                         float* __restrict__ p_out, const float* __restrict__ coef,
-                                                        int64_t chunk) {
+                                                        int64_t chunk, float* __restrict__ hst, int64_t hst_chunk,
+                                                        int64_t hst_layer, int64_t store_chunks) {
   __shared__ eh_f16x8 act[16][E2_T][2][64];
   __shared__ eh_f16x8 eb[4][E2_T][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
   __shared__ int sx0s[E2_T * 32];
@@ -580,11 +587,35 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   };
   // TR epilogue: acc <- fma(acc [2^-sx(sample)], A, B) = the next layer's input at its scale (layer 3: times
   // 2^(sx0(sample) - sxB[3]) where the encoding's own scale is the smaller)
+  // TR with an activation store (hst, chunks below store_chunks): each layer's raw output W_L x + b_L (the layered
+  // kernels' stored h, nof_train.hip StoreChunk) is written before the BatchNorm fma -- the accumulator times
+  // 2^-(sw_L + the input's scale), exact, plus the bias -- as the store's [32-sample tile][k-group][lane][4] float4s: the
+  // accumulator registers 4gq..4gq+3 of out-block ob ARE k-group 4 ob + gq of the lane's sample (1 KiB per wave
+  // store instruction)
+  const bool storing = TR && hst != nullptr && (int64_t)blockIdx.y < store_chunks;
+  auto store_raw = [&](int L, int tau, int o, int gq, float sc) __attribute__((always_inline)) {
+    const int64_t tile = (int64_t)blockIdx.x * E2_T + tau;
+    if (tile * 32 >= send - cb) return;   // (tiles past the chunk's end: none in the store's layout)
+    // the store holds h = W x + b (its BatchNorm sums are of W x: nof_train.hip BnPrev)
+    const f32x4 b = *reinterpret_cast<const f32x4*>(W + OFF_BIAS + 256 * L + 32 * (2 * w + o) + 8 * gq + 4 * h);
+    const f32x4 v = {acc[o][tau][4 * gq] * sc + b[0], acc[o][tau][4 * gq + 1] * sc + b[1],
+                     acc[o][tau][4 * gq + 2] * sc + b[2], acc[o][tau][4 * gq + 3] * sc + b[3]};
+    float* dst = hst + (int64_t)blockIdx.y * hst_chunk + (int64_t)L * hst_layer +
+                 ((tile * 32 + 4 * (2 * w + o) + gq) * 64 + lane) * 4;
+    *reinterpret_cast<f32x4*>(dst) = v;
+  };
   auto epi_tr = [&](int L, auto PS) __attribute__((always_inline)) {   // PS: the input has a per-sample scale (layers 0 and 4)
     constexpr bool ps = decltype(PS)::value;
 #pragma unroll
     for (int tau = 0; tau < E2_T; ++tau) {
       const float us = ps ? ldexpf(1.0f, -sxl[tau]) : 1.0f;
+      if (storing) {
+        const float sc = ldexpf(1.0f, -(sw[L] + (ps ? sxl[tau] : (L > 0 ? sxB[L - 1] : 0))));
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) store_raw(L, tau, o, gq, sc);
+      }
 #pragma unroll
       for (int o = 0; o < 2; ++o)
 #pragma unroll
@@ -745,7 +776,8 @@ static void launch_eval(const float* rays, int stride, const float* z, int64_t t
                         const float* W, float* p_out, hipStream_t s) {
   if (g_eval_math == 1) {
     hipLaunchKernelGGL(k_nof_eval_h2<false>, dim3((unsigned)((total + 32 * E2_T - 1) / (32 * E2_T))), dim3(256), 0,
-                       s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0);
+                       s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0, nullptr, (int64_t)0,
+                       (int64_t)0, (int64_t)0);
   } else {
     const int64_t blocks = ((total + 31) / 32 + 3) / 4;
     hipLaunchKernelGGL(k_nof_eval, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
@@ -897,18 +929,19 @@ __global__ __launch_bounds__(256) void k_nof_eval_fold(const float* __restrict__
 size_t train_query_image_floats() { return EVAL_FLOATS; }
 
 void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s) {
-  hipLaunchKernelGGL(k_pack_eval_vectors, dim3(1), dim3(256), 0, s, P, img);   // (occ_out; biases unused)
+  hipLaunchKernelGGL(k_pack_eval_vectors<true>, dim3(1), dim3(256), 0, s, P, img);   // occ_out, raw biases
   hipLaunchKernelGGL(k_eval_wscale<true>, dim3(8), dim3(256), 0, s, P, img);
   hipLaunchKernelGGL(k_pack_eval_h<true>, dim3((unsigned)((EH_VECS + 255) / 256)), dim3(256), 0, s, P, img);
 }
 
 void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
-                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s) {
+                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s,
+                        float* hst, int64_t hst_chunk, int64_t hst_layer, int64_t store_chunks) {
   const int64_t C = (total + chunk - 1) / chunk;
   const int64_t per = (std::min(chunk, total) + 32 * E2_T - 1) / (32 * E2_T);
   if (C >= 65536 || per >= ((int64_t)1 << 31)) throw std::runtime_error("train query: too many chunks / samples");
   hipLaunchKernelGGL(k_nof_eval_h2<true>, dim3((unsigned)per, (unsigned)C), dim3(256), 0, s, rays, stride, z, total,
-                     S, ein, img, p_out, coef, chunk);
+                     S, ein, img, p_out, coef, chunk, hst, hst_chunk, hst_layer, store_chunks);
 }
 
 void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
@@ -991,7 +1024,7 @@ extern "C" int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* pack
   hipStream_t s = (hipStream_t)stream;
   const unsigned nb = (unsigned)((OFF_BIAS + 255) / 256);
   hipLaunchKernelGGL(k_pack_eval_weights, dim3(nb), dim3(256), 0, s, P, packed);
-  hipLaunchKernelGGL(k_pack_eval_vectors, dim3(1), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(k_pack_eval_vectors<false>, dim3(1), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_eval_wscale<false>, dim3(8), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_pack_eval_h<false>, dim3((unsigned)((EH_VECS + 255) / 256)), dim3(256), 0, s, P, packed);
   PCN_LAUNCH_CHECK("pcnerf_nof_pack_eval");

@@ -492,6 +492,22 @@ __global__ __launch_bounds__(256) void k_tf_coeffs(NofParamsDev P, FoldDev F, Sa
   }
 }
 
+// grid (8 layers, store_chunks), 256 threads: a stored chunk's BatchNorm sums in the activation store's layout
+// (nof_train.hip k_bn_save reads them): sum h and sum h^2 of the raw layer output h = W x (no Linear bias) over the
+// chunk's n samples, from the exact statistics the query's coefficients come from (mean = P'_L's column 63, biased
+// variance): n m and n (var + m^2) in float64.
+__global__ void k_tf_store_stats(FoldDev F, SampleSrc q, char* __restrict__ store, size_t chunk_bytes,
+                                 size_t stats_off) {
+  const int L = blockIdx.x, k = threadIdx.x;
+  const int64_t c = blockIdx.y, C = F.C;
+  const double n = (double)chunk_len(q, c);
+  const double m = F.pp[(((int64_t)L * C + c) * 256 + k) * 64 + 63];
+  const double var = F.sr[((int64_t)L * C + c) * 1024 + 768 + k];
+  double* st = reinterpret_cast<double*>(store + (size_t)c * chunk_bytes + stats_off);
+  st[512 * L + 2 * k] = n * m;
+  st[512 * L + 2 * k + 1] = n * (var + m * m);
+}
+
 // grid 8, 256 threads: running stats chunk by chunk, bn_coeffs' arithmetic (float64 update, stored as float).
 __global__ void k_tf_running(NofParamsDev P, FoldDev F, SampleSrc q, double mom) {
   const int L = blockIdx.x, k = threadIdx.x;
@@ -823,7 +839,8 @@ static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, fl
 // The train-mode query evaluated per sample (the network as written, one BatchNorm coefficient set per chunk):
 // the chunk statistics from the encoding moments and the float64 layer algebra above, then k_nof_eval_h2<true>.
 static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, float momentum, float eps,
-                          void* state, size_t state_bytes, float* p_out, hipStream_t s) {
+                          void* state, size_t state_bytes, float* p_out, hipStream_t s, void* store = nullptr,
+                          int64_t store_chunks = 0) {
   PCN_CHECK(q.total > 0 && q.chunk > 0, "train query: empty input");
   // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
   PCN_CHECK(q.total % q.chunk != 1 && q.total != 1, "Expected more than 1 value per channel when training");
@@ -856,7 +873,13 @@ static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, f
   {
     // algorithmic work: 982,528 FLOP per sample (9 Linear layers); bytes: z in, p out, ray rows
     ProfScope ps(s, PT_TRAIN_QUERY, 982528.0 * (double)q.total, 8.0 * (double)q.total);
-    launch_train_query(q.rays, q.stride, q.z, q.total, q.S, q.ein, F.img, F.coef, q.chunk, p_out, s);
+    const int64_t sc = store ? std::min<int64_t>(store_chunks, F.C) : 0;
+    const size_t cb = pcnerf_nof_store_bytes(q.chunk), lb = store_layer_bytes(q.chunk);
+    launch_train_query(q.rays, q.stride, q.z, q.total, q.S, q.ein, F.img, F.coef, q.chunk, p_out, s,
+                       sc > 0 ? static_cast<float*>(store) : nullptr, (int64_t)(cb / 4), (int64_t)(lb / 4), sc);
+    if (sc > 0)
+      hipLaunchKernelGGL(k_tf_store_stats, dim3(8, (unsigned)sc), dim3(256), 0, s, F, q, static_cast<char*>(store),
+                         cb, 8 * lb);
   }
   hipLaunchKernelGGL(k_tf_running, dim3(8), dim3(256), 0, s, P, F, q, (double)momentum);
 }
@@ -916,6 +939,22 @@ extern "C" int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, i
   const SampleSrc q{rays, ray_stride, z, n_samples, nullptr, total, std::min(chunk, total)};
   fused_forward(q, params, momentum, eps, state, state_bytes, p_out, (hipStream_t)stream);
   PCN_LAUNCH_CHECK("pcnerf_nof_query_train_fused");
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_query_train_fused_store(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                                  int n_samples, int64_t chunk, const pcnerf_nof_params* params,
+                                                  float momentum, float eps, void* state, size_t state_bytes,
+                                                  float* p_out, void* store, int64_t store_chunks, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && state && p_out, "pcnerf_nof_query_train_fused_store: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_fused_store: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_fused_store: ray_stride < 6");
+  PCN_CHECK(store_chunks == 0 || store, "pcnerf_nof_query_train_fused_store: store_chunks > 0 needs a store");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  const SampleSrc q{rays, ray_stride, z, n_samples, nullptr, total, std::min(chunk, total)};
+  fused_forward(q, params, momentum, eps, state, state_bytes, p_out, (hipStream_t)stream, store, store_chunks);
+  PCN_LAUNCH_CHECK("pcnerf_nof_query_train_fused_store");
   PCN_API_END
 }
 

@@ -1560,9 +1560,7 @@ struct StoreChunk {
   double* stats;
 };
 
-static size_t store_layer_bytes(int64_t chunk) {
-  return ((size_t)((chunk + 31) / 32) * TILE_FLOATS * 4 + 255) & ~(size_t)255;
-}
+static_assert(TILE_FLOATS == 32 * 256, "store_layer_bytes (pcnerf_internal.h) assumes 32-sample tiles of 256");
 
 extern "C" size_t pcnerf_nof_store_bytes(int64_t chunk) {
   return 8 * store_layer_bytes(chunk) + ((8 * 512 * 8 + 255) & ~(size_t)255);

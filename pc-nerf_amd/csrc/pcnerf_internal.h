@@ -32,10 +32,17 @@ void launch_fold_logits(const float* rays, int stride, const float* z, int64_t t
 // the raw split weights and occ_out; coef[chunk] (TQ_COEF_FLOATS) each chunk's BatchNorm coefficients and the
 // per-layer operand scales of its bound.
 size_t train_query_image_floats();
+// the activation store's bytes per layer of a chunk ([tile of 32 samples][32 k-groups][64 lanes][4] floats, 256-B
+// aligned; nof_train.hip StoreChunk, pcnerf_nof_store_bytes)
+inline size_t store_layer_bytes(int64_t chunk) {
+  return ((size_t)((chunk + 31) / 32) * (32 * 256) * 4 + 255) & ~(size_t)255;
+}
 constexpr int TQ_COEF_FLOATS = 16 * 256 + 16;   // per chunk: [L][alpha 256 | beta'' 256], then sxB[8] (int)
 void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s);
 void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
-                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s);
+                        const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s,
+                        float* hst = nullptr, int64_t hst_chunk = 0, int64_t hst_layer = 0,
+                        int64_t store_chunks = 0);
 
 // p = o + d*z, one rounding per op (render.py:458; built with -ffp-contract=off).
 __device__ __forceinline__ void sample_point(const float* __restrict__ r, float z, float (&p)[3]) {

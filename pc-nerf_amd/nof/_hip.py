@@ -86,6 +86,8 @@ _SIGS = {
     "pcnerf_nof_store_bytes": (c_size, [i64]),
     "pcnerf_nof_query_train_store": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams), c_float,
                                              c_float, vp, c_size, vp, vp, i64, vp]),
+    "pcnerf_nof_query_train_fused_store": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams),
+                                                   c_float, c_float, vp, c_size, vp, vp, i64, vp]),
     "pcnerf_nof_query_train_backward_store": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams),
                                                       c_float, vp, vp, c_size, ctypes.POINTER(NofGrads), vp, i64,
                                                       vp]),

@@ -218,13 +218,22 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
                                               ctypes.byref(s), mom, eps, fold.data_ptr(), fold.numel(),
                                               p.data_ptr(), st))
         _track_batches(model, -(-R * S // int(chunk)))
-    elif model.training and _TRAIN_FUSED and (store is None or store.n_chunks == 0):
+    elif model.training and _TRAIN_FUSED:
+        # the network per sample in one fused kernel; with an activation store it also writes the stored chunks'
+        # raw layer outputs and BatchNorm sums for the backward (the layered store forward's layout)
         chunk = max(1, min(int(chunk), R * S))
         mom, eps = _bn_config(model)
         s, keep = _params(model)
         ws = _workspace(z.device, int(L.pcnerf_nof_train_fold_bytes(R * S, chunk)))
-        H.check(L.pcnerf_nof_query_train_fused(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
-                                               ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(), p.data_ptr(), st))
+        if store is not None and store.n_chunks > 0:
+            H.check(L.pcnerf_nof_query_train_fused_store(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S,
+                                                         int(chunk), ctypes.byref(s), mom, eps, ws.data_ptr(),
+                                                         ws.numel(), p.data_ptr(), store.buf.data_ptr(),
+                                                         store.n_chunks, st))
+        else:
+            H.check(L.pcnerf_nof_query_train_fused(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                                   ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(),
+                                                   p.data_ptr(), st))
         _track_batches(model, -(-R * S // int(chunk)))
     elif model.training:
         chunk = max(1, min(int(chunk), R * S))   # a larger chunk is the same single BatchNorm chunk

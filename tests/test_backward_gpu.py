@@ -67,7 +67,7 @@ def named(m):
     return dict(m.named_parameters())
 
 
-@pytest.fixture(params=["f16x2_3", "fp32"])
+@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused"])
 def train_math(request):
     from nof import _ops
     prev = _ops.set_train_math(request.param)
