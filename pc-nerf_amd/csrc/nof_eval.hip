@@ -769,13 +769,463 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
   EH2_STAMP(10);
 }
 
+// ---- k_nof_eval_h3: k_nof_eval_h2's block (96 samples, wave w owns neurons 64w .. 64w + 63 of every layer, its
+// weights streamed from L2 through a register ring, the layer outputs through LDS as the next layer's split B
+// operands) on v_mfma_f32_16x16x32_f16 instead of 32x32x16: the same products and bytes per k-step in 16x16
+// blocks -- 4 neuron blocks x 6 sample blocks of 16, k-steps of 32 features.  At the same issue rate the smaller
+// shape draws less power per FLOP (scripts/micro/mfma_f16_shape.hip with LDS B operands: 1.79 PF at 1.80 GHz vs
+// 1.63 PF at 1.61 GHz), and this kernel runs power-limited (DESIGN (f)).
+// Operand maps (16x16x32: lane l = column l & 15, k-group g = l >> 4 holding k = 8g .. 8g + 7; D reg r of lane l =
+// row 4g + r, column l & 15):
+//   accumulator acc[j][sb] reg r, lane l = neuron 64w + 16j + 4g + r of sample 16sb + (l & 15);
+//   a layer's output in LDS: act[2w + jp][sb][part][l] = (acc[2jp][sb][0..3], acc[2jp + 1][sb][0..3]) of lane l, so
+//   hidden k-step s, k-group g, element e is input neuron 32s + 16(e >> 2) + 4g + (e & 3) (the image's column map);
+//   the encoding: eb[s][sb][part][l] element e = feature 32s + 8g + e (63: zero padding).
+// Image: [60 k-steps][16 neuron blocks][part 2][lane 64] f16x8 (layer 0: 2 k-steps, 1-3 / 5-7: 8, layer 4: 2 + 8),
+// the same 1.97 MB as k_nof_eval_h2's.
+__host__ __device__ constexpr int eh3_start(int L) { return L == 0 ? 0 : L <= 4 ? 2 + 8 * (L - 1) : 4 + 8 * (L - 1); }
+constexpr int EH3_KSTEPS = 60;
+static_assert((size_t)EH3_KSTEPS * 16 * 2 * 64 == EH_VECS, "the 16x16 image fills the split image area");
+
+template <bool RAW>
+__global__ void k_pack_eval_h3(NofParamsDev P, float* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= EH_VECS) return;
+  const int lane = (int)(idx & 63), part = (int)((idx >> 6) & 1), nb = (int)((idx >> 7) & 15);
+  const int gk = (int)(idx >> 11);
+  int L = 0;
+  while (L < 7 && gk >= eh3_start(L + 1)) ++L;
+  const int s0 = gk - eh3_start(L);
+  const bool epart = L == 0 || (L == 4 && s0 < 2);
+  const int s = L == 4 && !epart ? s0 - 2 : s0;
+  const int n = 16 * nb + (lane & 15), g = lane >> 4;
+  const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
+  const float alpha = RAW ? 1.0f : (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
+  const float sc = ldexpf(1.0f, reinterpret_cast<const int*>(out + OFF_EH_SW)[L]);
+  eh_f16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    int col;
+    if (epart) {
+      const int f = 32 * s + 8 * g + e;
+      col = f < 63 ? f : -1;
+    } else {
+      col = (L == 4 ? 63 : 0) + 32 * s + 16 * (e >> 2) + 4 * g + (e & 3);
+    }
+    const float w = col < 0 ? 0.0f : (alpha * P.lin_w[L][(size_t)n * in_f + col]) * sc;
+    const _Float16 hi = (_Float16)w;
+    v[e] = part == 0 ? hi : (_Float16)(w - (float)hi);
+  }
+  reinterpret_cast<eh_f16x8*>(out + OFF_EH)[idx] = v;
+}
+
+#ifndef PCN_EH3_SB
+#define PCN_EH3_SB 6      // k_nof_eval_h3: 16-sample blocks per workgroup (LDS: 20.5 KiB each; 7 fills the 160 KiB)
+#endif
+constexpr int EH3_NS = 16 * PCN_EH3_SB;   // samples per workgroup
+#ifndef PCN_EH3_RING
+#define PCN_EH3_RING 2    // k_nof_eval_h3: weight-ring slots (prefetch distance RING - 1 k-steps of 32); 2 or 4
+#endif
+// TR, coef, the activation store and the scales: as k_nof_eval_h2
+template <bool TR>
+__global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict__ rays, int stride,
+                                                        const float* __restrict__ z, int64_t total, int S,
+                                                        const float* __restrict__ ein, const float* __restrict__ W,
+                                                        float* __restrict__ p_out, const float* __restrict__ coef,
+                                                        int64_t chunk, float* __restrict__ hst, int64_t hst_chunk,
+                                                        int64_t hst_layer, int64_t store_chunks) {
+  constexpr int SB = PCN_EH3_SB, NS = EH3_NS, R3 = PCN_EH3_RING, D3 = R3 - 1;
+  typedef float f32x4_ __attribute__((ext_vector_type(4)));
+  __shared__ eh_f16x8 act[8][SB][2][64];
+  __shared__ eh_f16x8 eb[2][SB][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
+  __shared__ int sx0s[NS];
+  __shared__ __attribute__((aligned(16))) float sbias[(TR ? 16 : 8) * 256];
+  __shared__ float emax[NS];
+  __shared__ float smax[4][NS];   // (eval)
+  __shared__ float pdot[4][NS];
+  __shared__ float spos[NS][3];
+  const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, g = lane >> 4, li = lane & 15;
+  const int64_t cb = TR ? (int64_t)blockIdx.y * chunk : 0;
+  const int64_t s0 = cb + (int64_t)blockIdx.x * NS;
+  const int64_t send = TR ? (cb + chunk < total ? cb + chunk : total) : total;
+  if (s0 >= send) return;   // (the last chunk's surplus blocks; uniform over the block, before any barrier)
+  float rz = 0.0f, rr[6] = {};
+  if (!ein && t < NS) {
+    int64_t gs = s0 + t;
+    if (gs >= send) gs = send - 1;
+    const float* r = rays + (gs / S) * stride;
+    rz = z[gs];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) rr[m] = r[m];
+  }
+  const eh_f16x8* __restrict__ img = reinterpret_cast<const eh_f16x8*>(W + OFF_EH);
+  int sw[8];
+#pragma unroll
+  for (int L = 0; L < 8; ++L) sw[L] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(W + OFF_EH_SW)[L]);
+  int sxB[8];
+  if (TR) {
+    const int* cs = reinterpret_cast<const int*>(coef + blockIdx.y * (size_t)TQ_COEF_FLOATS + 16 * 256);
+#pragma unroll
+    for (int L = 0; L < 8; ++L) sxB[L] = __builtin_amdgcn_readfirstlane(L < 7 ? cs[L] : 0);
+  }
+  // this wave's A operands of k-step gk: neuron blocks 4w + j, parts hi / mid
+  auto load_w = [&](eh_f16x8 (&d)[4][2], int gk) __attribute__((always_inline)) {
+    gk = gk < EH3_KSTEPS ? gk : EH3_KSTEPS - 1;   // (past the end: reload the last k-step, see k_nof_eval_h2)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) d[j][p] = img[((size_t)(gk * 16 + 4 * w + j) * 2 + p) * 64 + lane];
+  };
+  eh_f16x8 wr[R3][4][2];
+#pragma unroll
+  for (int k = 0; k < D3; ++k) load_w(wr[k], k);
+  if (TR) {
+    const f32x4_* cf = reinterpret_cast<const f32x4_*>(coef + blockIdx.y * (size_t)TQ_COEF_FLOATS);
+    f32x4_ cv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) cv[m] = cf[t + 256 * m];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int i = 4 * (t + 256 * m), L = i >> 9, isb = (i >> 8) & 1;
+      const int sxo = sxB[L], sxi = (L == 0 || L == 4) ? 0 : sxB[L - 1];
+      const int e = isb ? sxo : sxo - sw[L] - sxi;
+      reinterpret_cast<f32x4_*>(sbias)[t + 256 * m] =
+          f32x4_{ldexpf(cv[m][0], e), ldexpf(cv[m][1], e), ldexpf(cv[m][2], e), ldexpf(cv[m][3], e)};
+    }
+  } else {
+    for (int i = t; i < 8 * 256 / 4; i += 256)
+      reinterpret_cast<f32x4_*>(sbias)[i] = reinterpret_cast<const f32x4_*>(W + OFF_BIAS)[i];
+  }
+  float* const encf = reinterpret_cast<float*>(&act[0][0][0][0]);   // [sample][65]
+  static_assert(sizeof(act) >= NS * 65 * sizeof(float), "encoding staging area");
+  if (!ein) {
+    if (t < NS) {
+      float p[3];
+      sample_point(rr, rz, p);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        spos[t][m] = p[m];
+        encf[t * 65 + m] = p[m];
+      }
+      encf[t * 65 + 63] = 0.0f;
+    }
+    __syncthreads();
+    for (int i = t; i < NS * 30; i += 256) {
+      const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
+      float sv, cv;
+      sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
+      encf[sm * 65 + 3 + 6 * k + m] = sv;
+      encf[sm * 65 + 6 + 6 * k + m] = cv;
+    }
+    __syncthreads();
+  }
+  if (t < NS) {   // one sample's encoding per thread, stored in B order
+    float f[64];
+    if (ein) {
+      int64_t gs = s0 + t;
+      if (gs >= send) gs = send - 1;
+#pragma unroll
+      for (int k = 0; k < 63; ++k) f[k] = ein[gs * 63 + k];
+      f[63] = 0.0f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 64; ++k) f[k] = encf[t * 65 + k];
+    }
+    float m = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 63; ++k) m = fmaxf(m, fabsf(f[k]));
+    int sx0 = eh_scale(m);
+    if (TR && sxB[3] < sx0) sx0 = sxB[3];
+    const float xs = ldexpf(1.0f, sx0);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f[32 * s + 8 * gg + e] * xs;
+        eh_f16x8 hi, mid;
+        eh_split8(v, hi, mid);
+        eb[s][t >> 4][0][(t & 15) + 16 * gg] = hi;
+        eb[s][t >> 4][1][(t & 15) + 16 * gg] = mid;
+      }
+    if (!TR) emax[t] = m;
+    sx0s[t] = sx0;
+  }
+  __syncthreads();
+  int sxl[SB];   // the per-sample scale of the current layer's B operands (this lane's sample of each block)
+#pragma unroll
+  for (int sb = 0; sb < SB; ++sb) sxl[sb] = sx0s[16 * sb + li];
+  f32x4_ acc[4][SB];
+  int gk = 0;
+  // one encoding k-step (layers 0 and 4)
+  auto kstep_enc = [&](int s, int pos, bool first) __attribute__((always_inline)) {
+    load_w(wr[(pos + D3) & (R3 - 1)], gk + D3);
+    const eh_f16x8 (&wc)[4][2] = wr[pos & (R3 - 1)];
+    eh_f16x8 bh[SB], bm[SB];
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+      bh[sb] = eb[s][sb][0][lane];
+      bm[sb] = eb[s][sb][1][lane];
+      const int d = TR ? 0 : sxl[sb] - sx0s[16 * sb + li];
+      if (d != 0) {   // eval layer 4: the 22-bit encoding (hi + mid, exact in fp32) re-split at the shared scale
+        const float xs = ldexpf(1.0f, d);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ((float)bh[sb][e] + (float)bm[sb][e]) * xs;
+        eh_split8(v, bh[sb], bm[sb]);
+      }
+    }
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][0], bm[sb], first ? f32x4_{} : acc[j][sb], 0, 0, 0);
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][0], bh[sb], acc[j][sb], 0, 0, 0);
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][1], bh[sb], acc[j][sb], 0, 0, 0);
+    ++gk;
+  };
+  // the 8 hidden k-steps of a layer, software-pipelined as k_nof_eval_h2's: products Wh.xm, Wh.xh, Wm.xh; k-step
+  // s + 1's xm read once Wh.xm of s is issued, its xh once Wm.xh of s is
+  auto hidden_ksteps = [&](int pos0, bool first) __attribute__((always_inline)) {
+    eh_f16x8 bh[SB], bm[SB];
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+      bm[sb] = act[0][sb][1][lane];
+      bh[sb] = act[0][sb][0][lane];
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int pos = pos0 + s;
+      load_w(wr[(pos + D3) & (R3 - 1)], gk + D3);
+      const eh_f16x8 (&wc)[4][2] = wr[pos & (R3 - 1)];
+#pragma unroll
+      for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][0], bm[sb], (first && s == 0) ? f32x4_{} : acc[j][sb], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < 8) {
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) bm[sb] = act[s + 1][sb][1][lane];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][0], bh[sb], acc[j][sb], 0, 0, 0);
+#pragma unroll
+      for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][1], bh[sb], acc[j][sb], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < 8) {
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) bh[sb] = act[s + 1][sb][0][lane];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      ++gk;
+    }
+  };
+  // eval epilogue phase 1: acc <- fl(acc 2^-(sw + sx) + bias), this wave's per-sample maxima -> smax[w]
+  auto epi1 = [&](int L) __attribute__((always_inline)) {
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+      const float us = ldexpf(1.0f, -(sw[L] + sxl[sb]));
+      float m = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4_ b = *reinterpret_cast<const f32x4_*>(sbias + 256 * L + 64 * w + 16 * j + 4 * g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = __builtin_fmaf(acc[j][sb][q], us, b[q]);
+          acc[j][sb][q] = v;
+          m = fmaxf(m, fabsf(v));
+        }
+      }
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      if (g == 0) smax[w][16 * sb + li] = m;
+    }
+  };
+  // this wave's outputs as the next layer's B operands (k-steps 2w, 2w + 1), at scale xs per sample block
+  auto split_out = [&](const float (&xs)[SB], auto SC) {
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = acc[2 * jp + (e >> 2)][sb][e & 3];
+          v[e] = decltype(SC)::value ? a * xs[sb] : a;
+        }
+        eh_f16x8 hi, mid;
+        eh_split8(v, hi, mid);
+        act[2 * w + jp][sb][0][lane] = hi;
+        act[2 * w + jp][sb][1][lane] = mid;
+      }
+  };
+  auto epi2 = [&](bool with_e) __attribute__((always_inline)) {
+    float xs[SB];
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+      const int sm = 16 * sb + li;
+      float m = fmaxf(fmaxf(smax[0][sm], smax[1][sm]), fmaxf(smax[2][sm], smax[3][sm]));
+      if (with_e) m = fmaxf(m, emax[sm]);
+      sxl[sb] = eh_scale(m);
+      xs[sb] = ldexpf(1.0f, sxl[sb]);
+    }
+    split_out(xs, std::true_type{});
+  };
+  // TR: the activation store (the layered kernels' [32-sample tile][k-group][lane][4] layout): accumulator
+  // acc[j][sb] of lane l is neurons 64w + 16j + 4g .. + 3 = k-group 8w + 2j + (g >> 1), half g & 1, of sample
+  // 16(q & 1) + (l & 15) of tile q >> 1, q = SB blockIdx.x + sb the 16-sample block within the chunk
+  const bool storing = TR && hst != nullptr && (int64_t)blockIdx.y < store_chunks;
+  auto store_raw = [&](int L, int sb, int j, float sc) __attribute__((always_inline)) {
+    const int64_t q = (int64_t)blockIdx.x * SB + sb, tile = q >> 1;
+    if (tile * 32 >= send - cb) return;
+    const int n0 = 64 * w + 16 * j + 4 * g;
+    const f32x4_ b = *reinterpret_cast<const f32x4_*>(W + OFF_BIAS + 256 * L + n0);
+    const f32x4_ v = {acc[j][sb][0] * sc + b[0], acc[j][sb][1] * sc + b[1], acc[j][sb][2] * sc + b[2],
+                      acc[j][sb][3] * sc + b[3]};
+    const int sl = 16 * (int)(q & 1) + li + 32 * (g & 1);
+    float* dst = hst + (int64_t)blockIdx.y * hst_chunk + (int64_t)L * hst_layer +
+                 ((tile * 32 + (n0 >> 3)) * 64 + sl) * 4;
+    *reinterpret_cast<f32x4_*>(dst) = v;
+  };
+  auto epi_tr = [&](int L, auto PS) __attribute__((always_inline)) {
+    constexpr bool ps = decltype(PS)::value;
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+      const float us = ps ? ldexpf(1.0f, -sxl[sb]) : 1.0f;
+      if (storing) {
+        const float sc = ldexpf(1.0f, -(sw[L] + (ps ? sxl[sb] : (L > 0 ? sxB[L - 1] : 0))));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) store_raw(L, sb, j, sc);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nb = 64 * w + 16 * j + 4 * g;
+        const f32x4_ a = *reinterpret_cast<const f32x4_*>(sbias + 512 * L + nb);
+        const f32x4_ b = *reinterpret_cast<const f32x4_*>(sbias + 512 * L + 256 + nb);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = acc[j][sb][q];
+          if (ps) v *= us;
+          acc[j][sb][q] = __builtin_fmaf(v, a[q], b[q]);
+        }
+      }
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < 2; ++s) kstep_enc(s, s, s == 0);
+  if (TR) {
+    epi_tr(0, std::true_type{});
+    float xs[SB];
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+      sxl[sb] = sxB[0];
+      xs[sb] = 1.0f;
+    }
+    __syncthreads();
+    split_out(xs, std::false_type{});
+    __syncthreads();
+  } else {
+    epi1(0);
+    __syncthreads();
+    epi2(false);
+    __syncthreads();
+  }
+  auto layer_end = [&](int L) __attribute__((always_inline)) {
+    if (TR) {
+      if (L == 4) epi_tr(4, std::true_type{});
+      else epi_tr(L, std::false_type{});
+      if (L < 7) {
+        float xs[SB];
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+          const int sx0 = sx0s[16 * sb + li];
+          sxl[sb] = L == 3 ? sx0 : sxB[L];
+          xs[sb] = ldexpf(1.0f, sx0 - sxB[3]);
+        }
+        __syncthreads();
+        if (L == 3) split_out(xs, std::true_type{});
+        else split_out(xs, std::false_type{});
+        __syncthreads();
+      }
+    } else {
+      epi1(L);
+      __syncthreads();
+      if (L < 7) {
+        epi2(L == 3);
+        __syncthreads();
+      }
+    }
+  };
+  // ring slots: layer starts 0, 2, 10, 18, 26 (+2 encoding k-steps), 36, 44, 52 -- every call site's position is a
+  // compile-time constant mod the ring
+  static_assert(eh3_start(1) % R3 == eh3_start(2) % R3 && eh3_start(2) % R3 == eh3_start(3) % R3, "ring slots");
+  static_assert((eh3_start(4) + 2) % R3 == eh3_start(5) % R3 && eh3_start(5) % R3 == eh3_start(6) % R3 &&
+                eh3_start(6) % R3 == eh3_start(7) % R3, "ring slots");
+#pragma unroll 1
+  for (int L = 1; L <= 3; ++L) {
+    hidden_ksteps(eh3_start(1) % R3, true);
+    layer_end(L);
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) kstep_enc(s, eh3_start(4) % R3 + s, s == 0);
+  hidden_ksteps((eh3_start(4) + 2) % R3, false);
+  layer_end(4);
+#pragma unroll 1
+  for (int L = 5; L <= 7; ++L) {
+    hidden_ksteps(eh3_start(5) % R3, true);
+    layer_end(L);
+  }
+  // occ_out: this wave's 64 neurons per sample, then the 4 partial sums in order
+#pragma unroll
+  for (int sb = 0; sb < SB; ++sb) {
+    float part = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4_ wv = *reinterpret_cast<const f32x4_*>(W + OFF_WOUT + 64 * w + 16 * j + 4 * g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part = fmaf(wv[q], acc[j][sb][q], part);
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    if (g == 0) pdot[w][16 * sb + li] = part;
+  }
+  __syncthreads();
+  if (t < NS && s0 + t < send) {
+    const float logit = ((pdot[0][t] + pdot[1][t]) + (pdot[2][t] + pdot[3][t])) + W[OFF_BOUT];
+    p_out[s0 + t] = sigmoid_ref(logit);
+  }
+}
+
+#ifndef PCN_EH3
+#define PCN_EH3 1   // split query on v_mfma_f32_16x16x32_f16 (k_nof_eval_h3) instead of 32x32x16 (k_nof_eval_h2)
+#endif
+
 // Eval-mode MLP arithmetic: 0 = fp32 MFMA (k_nof_eval), 1 = split fp16, 3 products (k_nof_eval_h2, default).
 static int g_eval_math = 1;
 
 static void launch_eval(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const float* W, float* p_out, hipStream_t s) {
   if (g_eval_math == 1) {
-    hipLaunchKernelGGL(k_nof_eval_h2<false>, dim3((unsigned)((total + 32 * E2_T - 1) / (32 * E2_T))), dim3(256), 0,
+    const int64_t ns = PCN_EH3 ? EH3_NS : 32 * E2_T;
+    hipLaunchKernelGGL(PCN_EH3 ? k_nof_eval_h3<false> : k_nof_eval_h2<false>,
+                       dim3((unsigned)((total + ns - 1) / ns)), dim3(256), 0,
                        s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0, nullptr, (int64_t)0,
                        (int64_t)0, (int64_t)0);
   } else {
@@ -931,16 +1381,19 @@ size_t train_query_image_floats() { return EVAL_FLOATS; }
 void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s) {
   hipLaunchKernelGGL(k_pack_eval_vectors<true>, dim3(1), dim3(256), 0, s, P, img);   // occ_out, raw biases
   hipLaunchKernelGGL(k_eval_wscale<true>, dim3(8), dim3(256), 0, s, P, img);
-  hipLaunchKernelGGL(k_pack_eval_h<true>, dim3((unsigned)((EH_VECS + 255) / 256)), dim3(256), 0, s, P, img);
+  hipLaunchKernelGGL(PCN_EH3 ? k_pack_eval_h3<true> : k_pack_eval_h<true>, dim3((unsigned)((EH_VECS + 255) / 256)),
+                     dim3(256), 0, s, P, img);
 }
 
 void launch_train_query(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s,
                         float* hst, int64_t hst_chunk, int64_t hst_layer, int64_t store_chunks) {
   const int64_t C = (total + chunk - 1) / chunk;
-  const int64_t per = (std::min(chunk, total) + 32 * E2_T - 1) / (32 * E2_T);
+  const int64_t ns = PCN_EH3 ? EH3_NS : 32 * E2_T;
+  const int64_t per = (std::min(chunk, total) + ns - 1) / ns;
   if (C >= 65536 || per >= ((int64_t)1 << 31)) throw std::runtime_error("train query: too many chunks / samples");
-  hipLaunchKernelGGL(k_nof_eval_h2<true>, dim3((unsigned)per, (unsigned)C), dim3(256), 0, s, rays, stride, z, total,
+  hipLaunchKernelGGL(PCN_EH3 ? k_nof_eval_h3<true> : k_nof_eval_h2<true>, dim3((unsigned)per, (unsigned)C), dim3(256),
+                     0, s, rays, stride, z, total,
                      S, ein, img, p_out, coef, chunk, hst, hst_chunk, hst_layer, store_chunks);
 }
 
@@ -1026,7 +1479,8 @@ extern "C" int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* pack
   hipLaunchKernelGGL(k_pack_eval_weights, dim3(nb), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_pack_eval_vectors<false>, dim3(1), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_eval_wscale<false>, dim3(8), dim3(256), 0, s, P, packed);
-  hipLaunchKernelGGL(k_pack_eval_h<false>, dim3((unsigned)((EH_VECS + 255) / 256)), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(PCN_EH3 ? k_pack_eval_h3<false> : k_pack_eval_h<false>, dim3((unsigned)((EH_VECS + 255) / 256)),
+                     dim3(256), 0, s, P, packed);
   PCN_LAUNCH_CHECK("pcnerf_nof_pack_eval");
   PCN_API_END
 }
