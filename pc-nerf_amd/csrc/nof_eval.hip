@@ -38,15 +38,15 @@ constexpr size_t OFF_BIAS = 2 * SZ_E + 7 * SZ_H;
 constexpr size_t OFF_WOUT = OFF_BIAS + 8 * 256;
 constexpr size_t OFF_BOUT = OFF_WOUT + 256;
 constexpr size_t EVAL_F32_FLOATS = OFF_BOUT + 4;   // the fp32 image (k_nof_eval)
-// split-fp16 image (k_nof_eval_h2), appended: [sw: 8 int32 exponents, 16-float aligned][120 k-steps][ob 8][part 2]
+// split-fp16 image (k_nof_eval_h3), appended: [sw: 8 int32 exponents, 16-float aligned][60 k-steps][16 neuron
+// blocks][part 2][lane 64] f16x8 (see k_nof_eval_h3)
 // [lane 64] f16x8 -- the eval network's 120 k-steps of 16 features (layer 0: 4, layers 1-3, 5-7: 16, layer 4: 4 + 16)
-constexpr int EH_KSTEPS = 120;
-constexpr size_t EH_VECS = (size_t)EH_KSTEPS * 8 * 2 * 64;
+constexpr int EH3_KSTEPS = 60;
+constexpr size_t EH_VECS = (size_t)EH3_KSTEPS * 16 * 2 * 64;
 constexpr size_t OFF_EH_SW = EVAL_F32_FLOATS;
 constexpr size_t OFF_EH = OFF_EH_SW + 16;
 constexpr size_t EVAL_FLOATS = OFF_EH + EH_VECS * 4;
 static_assert(EVAL_F32_FLOATS % 4 == 0, "f16x8 alignment of the split image");
-__host__ __device__ constexpr int eh_start(int L) { return L == 0 ? 0 : L <= 4 ? 4 + 16 * (L - 1) : 8 + 16 * (L - 1); }
 
 __device__ __forceinline__ int feat_h(int t, int h) {  // accumulator register -> neuron
   return 32 * (t >> 4) + (t & 3) + 8 * ((t & 15) >> 2) + 4 * h;
@@ -232,38 +232,6 @@ __global__ __launch_bounds__(256) void k_eval_wscale(NofParamsDev P, float* __re
 
 typedef _Float16 eh_f16x8 __attribute__((ext_vector_type(8)));
 
-template <bool RAW>
-__global__ void k_pack_eval_h(NofParamsDev P, float* __restrict__ out) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= EH_VECS) return;
-  const int lane = (int)(idx & 63), part = (int)((idx >> 6) & 1), ob = (int)((idx >> 7) & 7);
-  const int gk = (int)(idx >> 10);
-  int L = 0;
-  while (L < 7 && gk >= eh_start(L + 1)) ++L;
-  const int s0 = gk - eh_start(L);
-  const bool epart = L == 0 || (L == 4 && s0 < 4);
-  const int s = L == 4 && !epart ? s0 - 4 : s0;
-  const int n = 32 * ob + (lane & 31), h = lane >> 5;
-  const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
-  const float alpha = RAW ? 1.0f : (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
-  const float sc = ldexpf(1.0f, reinterpret_cast<const int*>(out + OFF_EH_SW)[L]);
-  eh_f16x8 v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    int col;
-    if (epart) {
-      const int f = 2 * (8 * s + j) + h;
-      col = f < 63 ? f : -1;
-    } else {
-      col = (L == 4 ? 63 : 0) + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
-    }
-    const float w = col < 0 ? 0.0f : (alpha * P.lin_w[L][(size_t)n * in_f + col]) * sc;
-    const _Float16 hi = (_Float16)w;
-    v[j] = part == 0 ? hi : (_Float16)(w - (float)hi);
-  }
-  reinterpret_cast<eh_f16x8*>(out + OFF_EH)[idx] = v;
-}
-
 // the per-sample scale exponent for a max |x| (0 for zero / non-finite maxima), clamped so that every unscale
 // factor stays a normal float
 __device__ __forceinline__ int eh_scale(float m) {
@@ -294,487 +262,18 @@ __device__ __forceinline__ void eh_split8(const float (&v)[8], eh_f16x8& hi, eh_
   }
 }
 
-// ---- k_nof_eval_h2: the same split eval network with the work split over NEURONS inside a block: wave w owns
-// out-blocks 2w, 2w+1 (64 neurons) of every layer for all 96 samples (3 tiles) of its block, so each wave streams
-// only its own 64 neurons' weights from L2 (4 KiB per k-step, three k-steps in flight in a 4-slot register ring,
-// no barrier) and each A
-// operand feeds 3 sample tiles; the layer outputs go through LDS as the next layer's split B operands
-// ([k-step][tile][part][lane], 96 KiB), two barriers per layer (per-sample maxima, then the split outputs).
-// The encoding lives in LDS as layer 0's split B operands; layer 4 re-splits it (hi + mid is exact in fp32) at the
-// per-sample scale it shares with h3.
-#ifndef PCN_EH2_T
-#define PCN_EH2_T 3
-#endif
-constexpr int E2_T = PCN_EH2_T;   // sample tiles per block
-#ifndef PCN_EH2_RING
-#define PCN_EH2_RING 4    // k_nof_eval_h2: weight-ring slots (prefetch distance RING - 1 k-steps); 4 or 8
-#endif
-constexpr int RG = PCN_EH2_RING, RD = RG - 1;
-#ifndef PCN_EH2_STAMP
-#define PCN_EH2_STAMP 0   // diagnostic builds only: per-block phase stamps of k_nof_eval_h2 (pcnerf_debug_eh2_clock)
-#endif
-#if PCN_EH2_STAMP
-// [block][0]: s_memrealtime at entry, [1]: at exit; [2 + i]: s_memtime at phase i (entry, prologue done, layer 0..7
-// done, exit); [13..15]: layer 2's k-loop done, first barrier passed, split outputs written
-__device__ unsigned long long g_eh2_clk[8192][16];
-#define EH2_STAMP(i)                                                                   \
-  if (t == 0 && blockIdx.x < 8192 && blockIdx.y == 0) {                               \
-    g_eh2_clk[blockIdx.x][2 + (i)] = __builtin_amdgcn_s_memtime();                     \
-    if ((i) == 0) g_eh2_clk[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();         \
-    if ((i) == 10) g_eh2_clk[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();        \
-  }
-#else
-#define EH2_STAMP(i)
-#endif
-// TR (the train-mode query, pcnerf_nof_query_train_fused): the image holds the RAW weights (no BatchNorm fold) and
-// each layer's epilogue applies its chunk's BatchNorm -- alpha = fl32(invstd) gamma, beta'' = beta - mean(W x) alpha
-// from the chunk's exact batch statistics (nof_fold.hip k_tf_coeffs) -- as ONE fma per value that also moves the
-// result to the next layer's operand scale: BatchNorm output k of a chunk of n samples has batch mean beta_k and
-// batch variance <= gamma_k^2, so no sample exceeds sqrt(n) |gamma_k| + |beta_k| (Samuelson), and that bound fixes a
-// per-layer power-of-two scale sxB[L] in advance (k_tf_coeffs): no per-sample maxima, no exchange of them between
-// the waves.  Only the encoding (layers 0 and 4) keeps a per-sample scale, min(its own, sxB[3]).  blockIdx.y is the
-// BatchNorm chunk, blockIdx.x the 96-sample block inside it, so no block straddles two chunks.
-// coef per chunk: [L][alpha 256 | beta'' 256] floats, then sxB[8] as int (TQ_COEF_FLOATS floats per chunk).
-template <bool TR>
-__global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict__ rays, int stride,
-                                                        const float* __restrict__ z, int64_t total, int S,
-                                                        const float* __restrict__ ein, const float* __restrict__ W,
-                                                        float* __restrict__ p_out, const float* __restrict__ coef,
-                                                        int64_t chunk, float* __restrict__ hst, int64_t hst_chunk,
-                                                        int64_t hst_layer, int64_t store_chunks) {
-  __shared__ eh_f16x8 act[16][E2_T][2][64];
-  __shared__ eh_f16x8 eb[4][E2_T][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
-  __shared__ int sx0s[E2_T * 32];
-  // eval: the 8 layers' folded biases; TR: the chunk's [L][A | B] epilogue coefficients (see below)
-  __shared__ __attribute__((aligned(16))) float sbias[(TR ? 16 : 8) * 256];
-  __shared__ float emax[E2_T * 32];
-  __shared__ float smax[4][E2_T * 32];   // (eval)
-  __shared__ float pdot[4][E2_T * 32];
-  __shared__ float spos[E2_T * 32][3];
-  const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, h = lane >> 5, li = lane & 31;
-  // samples [s0, send) of this block
-  const int64_t cb = TR ? (int64_t)blockIdx.y * chunk : 0;
-  const int64_t s0 = cb + (int64_t)blockIdx.x * (32 * E2_T);
-  const int64_t send = TR ? (cb + chunk < total ? cb + chunk : total) : total;
-  if (s0 >= send) return;   // (the last chunk's surplus blocks; uniform over the block, before any barrier)
-  EH2_STAMP(0);
-  // this thread's sample (threads < 96): its z and ray row loaded first, so their latency overlaps the weight-ring
-  // and coefficient loads below (the prologue otherwise waits for the two in turn: -0.7 %)
-  float rz = 0.0f, rr[6] = {};
-  if (!ein && t < 32 * E2_T) {
-    int64_t g = s0 + t;
-    if (g >= send) g = send - 1;
-    const float* r = rays + (g / S) * stride;
-    rz = z[g];
-#pragma unroll
-    for (int m = 0; m < 6; ++m) rr[m] = r[m];
-  }
-  const eh_f16x8* __restrict__ img = reinterpret_cast<const eh_f16x8*>(W + OFF_EH);
-  int sw[8];
-#pragma unroll
-  for (int L = 0; L < 8; ++L) sw[L] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(W + OFF_EH_SW)[L]);
-  int sxB[8];   // TR: the per-layer output scales (layer 7: 0, its output is not split)
-  if (TR) {
-    const int* cs = reinterpret_cast<const int*>(coef + blockIdx.y * (size_t)TQ_COEF_FLOATS + 16 * 256);
-#pragma unroll
-    for (int L = 0; L < 8; ++L) sxB[L] = __builtin_amdgcn_readfirstlane(L < 7 ? cs[L] : 0);
-  }
-  // this wave's A operands of k-step gk: out-blocks 2w + o, parts hi / mid
-  auto load_w = [&](eh_f16x8 (&d)[2][2], int gk) {
-#pragma unroll
-    for (int o = 0; o < 2; ++o)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) d[o][p] = img[((size_t)(gk * 8 + 2 * w + o) * 2 + p) * 64 + lane];
-  };
-  // ring of 4 k-steps of A operands, slot = k-step index within its layer & 3 (every layer's k-step count and
-  // start are multiples of 4, so the slot is a compile-time index in the unrolled k-loops and no in-flight load's
-  // registers are ever copied): k-step s issues the loads of k-step s + 3 into the slot k-step s - 1 just used
-  const int rot = 0;   // (the first hidden k-step read of each layer)
-  auto kmap = [&](int q) __attribute__((always_inline)) {
-    if (q < 4 || (q >= 52 && q < 56) || q >= EH_KSTEPS) return q < EH_KSTEPS ? q : EH_KSTEPS - 1;
-    const int st = q < 52 ? 4 + ((q - 4) & ~15) : 56 + ((q - 56) & ~15);
-    return st + ((q - st + rot) & 15);
-  };
-  eh_f16x8 wr4[RG][2][2];
-#pragma unroll
-  for (int k = 0; k < RD; ++k) load_w(wr4[k], kmap(k));
-  if (TR) {
-    // the chunk's coefficients as the epilogue's fma operands: A = alpha 2^(sxout - sw_L - sxin_L), B = beta''
-    // 2^sxout, with sxin_L = sxB[L-1] for the uniformly scaled inputs (layers 1-3, 5-7) and 0 for layers 0 and 4,
-    // whose per-sample input scale is removed by an exact multiply first (powers of two: exact)
-    const f32x4* cf = reinterpret_cast<const f32x4*>(coef + blockIdx.y * (size_t)TQ_COEF_FLOATS);
-    f32x4 cv[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) cv[m] = cf[t + 256 * m];   // all four loads in flight together
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int i = 4 * (t + 256 * m), L = i >> 9, isb = (i >> 8) & 1;
-      const int sxo = sxB[L], sxi = (L == 0 || L == 4) ? 0 : sxB[L - 1];
-      const int e = isb ? sxo : sxo - sw[L] - sxi;
-      reinterpret_cast<f32x4*>(sbias)[t + 256 * m] =
-          f32x4{ldexpf(cv[m][0], e), ldexpf(cv[m][1], e), ldexpf(cv[m][2], e), ldexpf(cv[m][3], e)};
-    }
-  } else {
-    for (int i = t; i < 8 * 256 / 4; i += 256)
-      reinterpret_cast<f32x4*>(sbias)[i] = reinterpret_cast<const f32x4*>(W + OFF_BIAS)[i];
-  }
-  // prologue: the block's encodings, the 30 sincosf per sample spread over all 256 threads (encode_full's
-  // arithmetic, bit for bit), staged as floats in the (still unused) activation buffer
-  if (PCN_EH2_STAMP == 2) EH2_STAMP(11);
-  float* const encf = reinterpret_cast<float*>(&act[0][0][0][0]);   // [sample][65]
-  static_assert(sizeof(act) >= 32 * E2_T * 65 * sizeof(float), "encoding staging area");
-  if (!ein) {
-    if (t < 32 * E2_T) {
-      float p[3];
-      sample_point(rr, rz, p);
-#pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        spos[t][m] = p[m];
-        encf[t * 65 + m] = p[m];
-      }
-      encf[t * 65 + 63] = 0.0f;
-    }
-    __syncthreads();
-    if (PCN_EH2_STAMP == 2) EH2_STAMP(12);
-    for (int i = t; i < 32 * E2_T * 30; i += 256) {
-      const int sm = i / 30, r = i - 30 * sm, k = r / 3, m = r - 3 * k;
-      float sv, cv;
-      sincosf((float)(1 << k) * spos[sm][m], &sv, &cv);
-      encf[sm * 65 + 3 + 6 * k + m] = sv;
-      encf[sm * 65 + 6 + 6 * k + m] = cv;
-    }
-    __syncthreads();
-    if (PCN_EH2_STAMP == 2) EH2_STAMP(13);
-  }
-  if (t < 32 * E2_T) {   // one sample's encoding per thread, stored in B order
-    float f[64];
-    if (ein) {
-      int64_t g = s0 + t;
-      if (g >= send) g = send - 1;
-#pragma unroll
-      for (int k = 0; k < 63; ++k) f[k] = ein[g * 63 + k];
-      f[63] = 0.0f;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 64; ++k) f[k] = encf[t * 65 + k];
-    }
-    const int tau = t >> 5, l = t & 31;
-    float m = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 63; ++k) m = fmaxf(m, fabsf(f[k]));
-    int sx0 = eh_scale(m);
-    if (TR && sxB[3] < sx0) sx0 = sxB[3];   // the encoding shares layer 4's input scale with h3
-    const float xs = ldexpf(1.0f, sx0);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = f[2 * (8 * s + j) + hh] * xs;
-        eh_f16x8 hi, mid;
-        eh_split8(v, hi, mid);
-        eb[s][tau][0][l + 32 * hh] = hi;
-        eb[s][tau][1][l + 32 * hh] = mid;
-      }
-    emax[t] = m;
-    sx0s[t] = sx0;
-  }
-  __syncthreads();
-  EH2_STAMP(1);
-  int sxl[E2_T];   // the per-sample scale of the current layer's B operands (this lane's sample of each tile)
-#pragma unroll
-  for (int tau = 0; tau < E2_T; ++tau) sxl[tau] = sx0s[32 * tau + li];
-  f32x16 acc[2][E2_T];
-  int gk = 0;
-  // one k-step: B operands of the 3 tiles (from the encoding at the lane's scale, or the split activations),
-  // MFMAs product-major over the 6 accumulators
-  auto kstep = [&](int s, int pos, bool enc, bool first) __attribute__((always_inline)) {   // pos: the k-step's index within its layer
-    // (k-steps past the end reload the last one: unconditional loads keep the ring's registers statically known
-    // to the waitcnt pass -- a conditional load made it wait for every load in flight)
-    load_w(wr4[(pos + RD) & (RG - 1)], kmap(gk + RD));
-    const eh_f16x8 (&wc)[2][2] = wr4[pos & (RG - 1)];
-    eh_f16x8 bh[E2_T], bm[E2_T];
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) {
-      if (enc) {
-        bh[tau] = eb[s][tau][0][lane];
-        bm[tau] = eb[s][tau][1][lane];
-        const int d = TR ? 0 : sxl[tau] - sx0s[32 * tau + li];
-        if (d != 0) {   // eval layer 4: the 22-bit encoding (hi + mid, exact in fp32) re-split at the shared scale
-          const float xs = ldexpf(1.0f, d);
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = ((float)bh[tau][j] + (float)bm[tau][j]) * xs;
-          eh_split8(v, bh[tau], bm[tau]);
-        }
-      } else {
-        bh[tau] = act[s][tau][0][lane];
-        bm[tau] = act[s][tau][1][lane];
-      }
-    }
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau)
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-        acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bh[tau], first ? f32x16{} : acc[o][tau], 0, 0, 0);
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau)
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-        acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bm[tau], acc[o][tau], 0, 0, 0);
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau)
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-        acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
-    ++gk;
-  };
-  // eval epilogue phase 1: acc <- fl(acc 2^-(sw + sx) + bias) (one fma: the power-of-two product is exact), this
-  // wave's per-sample maxima -> smax[w]
-  auto epi1 = [&](int L) __attribute__((always_inline)) {
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) {
-      const float us = ldexpf(1.0f, -(sw[L] + sxl[tau]));
-      float m = 0.0f;
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + 256 * L + 32 * (2 * w + o) + 8 * gq + 4 * h);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float v = __builtin_fmaf(acc[o][tau][4 * gq + q], us, b[q]);
-            acc[o][tau][4 * gq + q] = v;
-            m = fmaxf(m, fabsf(v));
-          }
-        }
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      if (h == 0) smax[w][32 * tau + li] = m;
-    }
-  };
-  // split of this wave's outputs into the next layer's B operands (k-steps 4w .. 4w+3), at scale xs per tile
-  // (SC false: already at their scale; a compile-time choice, so no select per value)
-  auto split_out = [&](const float (&xs)[E2_T], auto SC) {
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau)
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = decltype(SC)::value ? acc[o][tau][8 * k + j] * xs[tau] : acc[o][tau][8 * k + j];
-          eh_f16x8 hi, mid;
-          eh_split8(v, hi, mid);
-          const int s = 4 * w + 2 * o + k;
-          act[s][tau][0][lane] = hi;
-          act[s][tau][1][lane] = mid;
-        }
-  };
-  // eval phase 2 (after a barrier): the next layer's per-sample scale and this wave's B operands
-  auto epi2 = [&](bool with_e) __attribute__((always_inline)) {
-    float xs[E2_T];
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) {
-      const int sm = 32 * tau + li;
-      float m = fmaxf(fmaxf(smax[0][sm], smax[1][sm]), fmaxf(smax[2][sm], smax[3][sm]));
-      if (with_e) m = fmaxf(m, emax[sm]);
-      sxl[tau] = eh_scale(m);
-      xs[tau] = ldexpf(1.0f, sxl[tau]);
-    }
-    split_out(xs, std::true_type{});
-  };
-  // TR epilogue: acc <- fma(acc [2^-sx(sample)], A, B) = the next layer's input at its scale (layer 3: times
-  // 2^(sx0(sample) - sxB[3]) where the encoding's own scale is the smaller)
-  // TR with an activation store (hst, chunks below store_chunks): each layer's raw output W_L x + b_L (the layered
-  // kernels' stored h, nof_train.hip StoreChunk) is written before the BatchNorm fma -- the accumulator times
-  // 2^-(sw_L + the input's scale), exact, plus the bias -- as the store's [32-sample tile][k-group][lane][4] float4s: the
-  // accumulator registers 4gq..4gq+3 of out-block ob ARE k-group 4 ob + gq of the lane's sample (1 KiB per wave
-  // store instruction)
-  const bool storing = TR && hst != nullptr && (int64_t)blockIdx.y < store_chunks;
-  auto store_raw = [&](int L, int tau, int o, int gq, float sc) __attribute__((always_inline)) {
-    const int64_t tile = (int64_t)blockIdx.x * E2_T + tau;
-    if (tile * 32 >= send - cb) return;   // (tiles past the chunk's end: none in the store's layout)
-    // the store holds h = W x + b (its BatchNorm sums are of W x: nof_train.hip BnPrev)
-    const f32x4 b = *reinterpret_cast<const f32x4*>(W + OFF_BIAS + 256 * L + 32 * (2 * w + o) + 8 * gq + 4 * h);
-    const f32x4 v = {acc[o][tau][4 * gq] * sc + b[0], acc[o][tau][4 * gq + 1] * sc + b[1],
-                     acc[o][tau][4 * gq + 2] * sc + b[2], acc[o][tau][4 * gq + 3] * sc + b[3]};
-    float* dst = hst + (int64_t)blockIdx.y * hst_chunk + (int64_t)L * hst_layer +
-                 ((tile * 32 + 4 * (2 * w + o) + gq) * 64 + lane) * 4;
-    *reinterpret_cast<f32x4*>(dst) = v;
-  };
-  auto epi_tr = [&](int L, auto PS) __attribute__((always_inline)) {   // PS: the input has a per-sample scale (layers 0 and 4)
-    constexpr bool ps = decltype(PS)::value;
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) {
-      const float us = ps ? ldexpf(1.0f, -sxl[tau]) : 1.0f;
-      if (storing) {
-        const float sc = ldexpf(1.0f, -(sw[L] + (ps ? sxl[tau] : (L > 0 ? sxB[L - 1] : 0))));
-#pragma unroll
-        for (int o = 0; o < 2; ++o)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) store_raw(L, tau, o, gq, sc);
-      }
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int nb = 32 * (2 * w + o) + 8 * gq + 4 * h;
-          const f32x4 a = *reinterpret_cast<const f32x4*>(sbias + 512 * L + nb);
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sbias + 512 * L + 256 + nb);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float v = acc[o][tau][4 * gq + q];
-            if (ps) v *= us;
-            acc[o][tau][4 * gq + q] = __builtin_fmaf(v, a[q], b[q]);
-          }
-        }
-    }
-  };
-  // the 16 hidden k-steps of a layer (B operands in act), software-pipelined: per k-step the products run in the
-  // order Wh.xm, Wh.xh, Wm.xh, and k-step s + 1's xm is read from LDS once Wh.xm of s is issued, its xh once Wm.xh
-  // of s is -- every LDS read has at least six MFMAs in flight to cover it
-  auto hidden_ksteps = [&](int pos0, bool first) __attribute__((always_inline)) {
-    eh_f16x8 bh[E2_T], bm[E2_T];
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) {
-      bm[tau] = act[rot][tau][1][lane];
-      bh[tau] = act[rot][tau][0][lane];
-    }
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int pos = pos0 + s;
-      load_w(wr4[(pos + RD) & (RG - 1)], kmap(gk + RD));
-      const eh_f16x8 (&wc)[2][2] = wr4[pos & (RG - 1)];
-#pragma unroll
-      for (int tau = 0; tau < E2_T; ++tau)
-#pragma unroll
-        for (int o = 0; o < 2; ++o)
-          acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bm[tau], (first && s == 0) ? f32x16{} : acc[o][tau], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < 16) {
-#pragma unroll
-        for (int tau = 0; tau < E2_T; ++tau) bm[tau] = act[(s + 1 + rot) & 15][tau][1][lane];
-      }
-      __builtin_amdgcn_sched_barrier(0);   // (else the scheduler sinks the reads down to their use)
-#pragma unroll
-      for (int tau = 0; tau < E2_T; ++tau)
-#pragma unroll
-        for (int o = 0; o < 2; ++o)
-          acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][0], bh[tau], acc[o][tau], 0, 0, 0);
-#pragma unroll
-      for (int tau = 0; tau < E2_T; ++tau)
-#pragma unroll
-        for (int o = 0; o < 2; ++o)
-          acc[o][tau] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wc[o][1], bh[tau], acc[o][tau], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < 16) {
-#pragma unroll
-        for (int tau = 0; tau < E2_T; ++tau) bh[tau] = act[(s + 1 + rot) & 15][tau][0][lane];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      ++gk;
-    }
-  };
-#pragma unroll
-  for (int s = 0; s < 4; ++s) kstep(s, s, true, s == 0);
-  if (TR) {
-    epi_tr(0, std::true_type{});
-    float xs[E2_T];
-#pragma unroll
-    for (int tau = 0; tau < E2_T; ++tau) {
-      sxl[tau] = sxB[0];
-      xs[tau] = 1.0f;
-    }
-    __syncthreads();
-    split_out(xs, std::false_type{});
-    __syncthreads();
-  } else {
-    epi1(0);
-    __syncthreads();
-    epi2(false);
-    __syncthreads();
-  }
-  EH2_STAMP(2);
-  // epilogue of layers 1-7 (TR: fma to the next operand scale; eval: per-sample scales through smax)
-  auto layer_end = [&](int L) __attribute__((always_inline)) {
-    if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(11);
-    if (TR) {
-      if (L == 4) epi_tr(4, std::true_type{});
-      else epi_tr(L, std::false_type{});
-      if (L < 7) {
-        float xs[E2_T];
-#pragma unroll
-        for (int tau = 0; tau < E2_T; ++tau) {
-          const int sx0 = sx0s[32 * tau + li];
-          sxl[tau] = L == 3 ? sx0 : sxB[L];
-          xs[tau] = ldexpf(1.0f, sx0 - sxB[3]);
-        }
-        __syncthreads();
-        if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(12);
-        if (L == 3) split_out(xs, std::true_type{});
-        else split_out(xs, std::false_type{});
-        if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(13);
-        __syncthreads();
-      }
-    } else {
-      epi1(L);
-      __syncthreads();
-      if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(12);
-      if (L < 7) {
-        epi2(L == 3);
-        if (L == 2 && PCN_EH2_STAMP == 1) EH2_STAMP(13);
-        __syncthreads();
-      }
-    }
-    EH2_STAMP(2 + L);
-  };
-  // the weight ring's slot of global k-step g is g mod RG; each call site below passes its layer's start mod RG
-  // (layer starts: 0, 4, 20, 36, 52 (+4 encoding k-steps), 72, 88, 104), so every slot index is a constant
-#pragma unroll 1
-  for (int L = 1; L <= 3; ++L) {
-    hidden_ksteps(4 % RG, true);
-    layer_end(L);
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) kstep(s, 52 % RG + s, true, s == 0);
-  hidden_ksteps(56 % RG, false);
-  layer_end(4);
-#pragma unroll 1
-  for (int L = 5; L <= 7; ++L) {
-    hidden_ksteps(72 % RG, true);
-    layer_end(L);
-  }
-  // occ_out: this wave's 64 neurons per sample, then the 4 partial sums in order
-#pragma unroll
-  for (int tau = 0; tau < E2_T; ++tau) {
-    float part = 0.0f;
-#pragma unroll
-    for (int o = 0; o < 2; ++o)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const f32x4 wv = *reinterpret_cast<const f32x4*>(W + OFF_WOUT + 32 * (2 * w + o) + 8 * gq + 4 * h);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) part = fmaf(wv[q], acc[o][tau][4 * gq + q], part);
-      }
-    part += __shfl_xor(part, 32, 64);
-    if (h == 0) pdot[w][32 * tau + li] = part;
-  }
-  __syncthreads();
-  if (t < 32 * E2_T && s0 + t < send) {
-    const float logit = ((pdot[0][t] + pdot[1][t]) + (pdot[2][t] + pdot[3][t])) + W[OFF_BOUT];
-    p_out[s0 + t] = sigmoid_ref(logit);
-  }
-  EH2_STAMP(10);
-}
-
-// ---- k_nof_eval_h3: k_nof_eval_h2's block (96 samples, wave w owns neurons 64w .. 64w + 63 of every layer, its
-// weights streamed from L2 through a register ring, the layer outputs through LDS as the next layer's split B
-// operands) on v_mfma_f32_16x16x32_f16 instead of 32x32x16: the same products and bytes per k-step in 16x16
-// blocks -- 4 neuron blocks x 6 sample blocks of 16, k-steps of 32 features.  At the same issue rate the smaller
-// shape draws less power per FLOP (scripts/micro/mfma_f16_shape.hip with LDS B operands: 1.79 PF at 1.80 GHz vs
-// 1.63 PF at 1.61 GHz), and this kernel runs power-limited (DESIGN (f)).
+// ---- k_nof_eval_h3: the split network (every fp32 product as hi*hi + hi*mid + mid*hi of fp16 parts, fp32
+// accumulation), fused over all 9 layers for a block of 96 samples with the work split over NEURONS: wave w owns
+// neurons 64w .. 64w + 63 of every layer for all 96 samples, so each wave streams only its own neurons' weights
+// from L2 (a 2-slot register ring, one k-step of prefetch, no barrier) and each A operand feeds 6 sample blocks;
+// the layer outputs go through LDS as the next layer's split B operands ([k-step][sample block][part][lane],
+// 96 KiB), two barriers per layer.  The encoding lives in LDS as layer 0's split B operands; layer 4 re-splits it
+// (hi + mid is exact in fp32) at the per-sample scale it shares with h3.
+// On v_mfma_f32_16x16x32_f16: 4 neuron blocks x 6 sample blocks of 16, k-steps of 32 features.  Against the same
+// block on 32x32x16 (2 x 3 blocks of 32, k-steps of 16; round 3's k_nof_eval_h2, in git history) it is 4-7 %
+// faster in the train query and 1-2 % in the eval query (profiles/r03l_variants_eval_*.json): the kernel runs
+// power-limited (DESIGN (f)), and at the same issue rate the smaller shape draws less power per FLOP
+// (scripts/micro/mfma_f16_shape.hip with LDS B operands: 1.79 PF at 1.80 GHz vs 1.63 PF at 1.61 GHz).
 // Operand maps (16x16x32: lane l = column l & 15, k-group g = l >> 4 holding k = 8g .. 8g + 7; D reg r of lane l =
 // row 4g + r, column l & 15):
 //   accumulator acc[j][sb] reg r, lane l = neuron 64w + 16j + 4g + r of sample 16sb + (l & 15);
@@ -782,10 +281,9 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h2(const float* __restrict_
 //   hidden k-step s, k-group g, element e is input neuron 32s + 16(e >> 2) + 4g + (e & 3) (the image's column map);
 //   the encoding: eb[s][sb][part][l] element e = feature 32s + 8g + e (63: zero padding).
 // Image: [60 k-steps][16 neuron blocks][part 2][lane 64] f16x8 (layer 0: 2 k-steps, 1-3 / 5-7: 8, layer 4: 2 + 8),
-// the same 1.97 MB as k_nof_eval_h2's.
+// 1.97 MB.
 __host__ __device__ constexpr int eh3_start(int L) { return L == 0 ? 0 : L <= 4 ? 2 + 8 * (L - 1) : 4 + 8 * (L - 1); }
-constexpr int EH3_KSTEPS = 60;
-static_assert((size_t)EH3_KSTEPS * 16 * 2 * 64 == EH_VECS, "the 16x16 image fills the split image area");
+static_assert(eh3_start(7) + 8 == EH3_KSTEPS, "k-steps of the image");
 
 template <bool RAW>
 __global__ void k_pack_eval_h3(NofParamsDev P, float* __restrict__ out) {
@@ -819,14 +317,27 @@ __global__ void k_pack_eval_h3(NofParamsDev P, float* __restrict__ out) {
   reinterpret_cast<eh_f16x8*>(out + OFF_EH)[idx] = v;
 }
 
-#ifndef PCN_EH3_SB
-#define PCN_EH3_SB 6      // k_nof_eval_h3: 16-sample blocks per workgroup (LDS: 20.5 KiB each; 7 fills the 160 KiB)
-#endif
-constexpr int EH3_NS = 16 * PCN_EH3_SB;   // samples per workgroup
+// 16-sample blocks per workgroup (LDS: 20.5 KiB each).  Measured in one process against 6: 7 (the most the 160 KiB
+// hold, 14 % less weight stream per sample) -2 % / +1 % on the train query on two boxes and +7 % on the eval query
+// (profiles/r03l_variants_eval_sb7.json, _sb.json), 5: +3 % / +9 %
+constexpr int EH3_SB = 6;
 #ifndef PCN_EH3_RING
 #define PCN_EH3_RING 2    // k_nof_eval_h3: weight-ring slots (prefetch distance RING - 1 k-steps of 32); 2 or 4
 #endif
-// TR, coef, the activation store and the scales: as k_nof_eval_h2
+// Scales (eval): each layer's weights at 2^sw[L] (k_eval_wscale), each sample's B operands at the power of two
+// that puts its largest |x| in [2^14, 2^15) (eh_scale; exchanged between the waves through smax), undone by one
+// exact fma with the bias in the epilogue.
+// TR (the train-mode query, pcnerf_nof_query_train_fused): the image holds the RAW weights (no BatchNorm fold) and
+// each layer's epilogue applies its chunk's BatchNorm -- alpha = fl32(invstd) gamma, beta'' = beta - mean(W x) alpha
+// from the chunk's exact batch statistics (nof_fold.hip k_tf_coeffs) -- as ONE fma per value that also moves the
+// result to the next layer's operand scale: BatchNorm output k of a chunk of n samples has batch mean beta_k and
+// batch variance <= gamma_k^2, so no sample exceeds sqrt(n) |gamma_k| + |beta_k| (Samuelson), and that bound fixes a
+// per-layer power-of-two scale sxB[L] in advance (k_tf_coeffs): no per-sample maxima, no exchange of them between
+// the waves.  Only the encoding (layers 0 and 4) keeps a per-sample scale, min(its own, sxB[3]).  blockIdx.y is the
+// BatchNorm chunk, blockIdx.x the 96-sample block inside it, so no block straddles two chunks.
+// coef per chunk: [L][alpha 256 | beta'' 256] floats, then sxB[8] as int (TQ_COEF_FLOATS floats per chunk).
+// TR with an activation store (hst, chunks below store_chunks): each layer's raw output W_L x + b_L (the layered
+// kernels' stored h, nof_train.hip StoreChunk) is written before the BatchNorm fma.
 template <bool TR>
 __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict__ rays, int stride,
                                                         const float* __restrict__ z, int64_t total, int S,
@@ -834,7 +345,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
                                                         float* __restrict__ p_out, const float* __restrict__ coef,
                                                         int64_t chunk, float* __restrict__ hst, int64_t hst_chunk,
                                                         int64_t hst_layer, int64_t store_chunks) {
-  constexpr int SB = PCN_EH3_SB, NS = EH3_NS, R3 = PCN_EH3_RING, D3 = R3 - 1;
+  constexpr int SB = EH3_SB, NS = 16 * SB, R3 = PCN_EH3_RING, D3 = R3 - 1;
   typedef float f32x4_ __attribute__((ext_vector_type(4)));
   __shared__ eh_f16x8 act[8][SB][2][64];
   __shared__ eh_f16x8 eb[2][SB][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
@@ -870,7 +381,9 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
   }
   // this wave's A operands of k-step gk: neuron blocks 4w + j, parts hi / mid
   auto load_w = [&](eh_f16x8 (&d)[4][2], int gk) __attribute__((always_inline)) {
-    gk = gk < EH3_KSTEPS ? gk : EH3_KSTEPS - 1;   // (past the end: reload the last k-step, see k_nof_eval_h2)
+    // (k-steps past the end reload the last one: unconditional loads keep the ring's registers statically known to
+    // the waitcnt pass -- a conditional load made it wait for every load in flight)
+    gk = gk < EH3_KSTEPS ? gk : EH3_KSTEPS - 1;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -993,8 +506,9 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
         acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][1], bh[sb], acc[j][sb], 0, 0, 0);
     ++gk;
   };
-  // the 8 hidden k-steps of a layer, software-pipelined as k_nof_eval_h2's: products Wh.xm, Wh.xh, Wm.xh; k-step
-  // s + 1's xm read once Wh.xm of s is issued, its xh once Wm.xh of s is
+  // the 8 hidden k-steps of a layer, software-pipelined: per k-step the products run in the order Wh.xm, Wh.xh,
+  // Wm.xh, and k-step s + 1's xm is read from LDS once Wh.xm of s is issued, its xh once Wm.xh of s is -- every LDS
+  // read has at least 24 MFMAs in flight to cover it
   auto hidden_ksteps = [&](int pos0, bool first) __attribute__((always_inline)) {
     eh_f16x8 bh[SB], bm[SB];
 #pragma unroll
@@ -1213,18 +727,14 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
   }
 }
 
-#ifndef PCN_EH3
-#define PCN_EH3 1   // split query on v_mfma_f32_16x16x32_f16 (k_nof_eval_h3) instead of 32x32x16 (k_nof_eval_h2)
-#endif
-
-// Eval-mode MLP arithmetic: 0 = fp32 MFMA (k_nof_eval), 1 = split fp16, 3 products (k_nof_eval_h2, default).
+// Eval-mode MLP arithmetic: 0 = fp32 MFMA (k_nof_eval), 1 = split fp16, 3 products (k_nof_eval_h3, default).
 static int g_eval_math = 1;
 
 static void launch_eval(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const float* W, float* p_out, hipStream_t s) {
   if (g_eval_math == 1) {
-    const int64_t ns = PCN_EH3 ? EH3_NS : 32 * E2_T;
-    hipLaunchKernelGGL(PCN_EH3 ? k_nof_eval_h3<false> : k_nof_eval_h2<false>,
+    const int64_t ns = 16 * EH3_SB;
+    hipLaunchKernelGGL(k_nof_eval_h3<false>,
                        dim3((unsigned)((total + ns - 1) / ns)), dim3(256), 0,
                        s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0, nullptr, (int64_t)0,
                        (int64_t)0, (int64_t)0);
@@ -1375,13 +885,13 @@ __global__ __launch_bounds__(256) void k_nof_eval_fold(const float* __restrict__
 }
 
 // ---- the train-mode query (nof_fold.hip pcnerf_nof_query_train_fused): raw split weights + occ_out in the eval
-// image layout, then k_nof_eval_h2<true> with one BatchNorm coefficient set per chunk
+// image layout, then k_nof_eval_h3<true> with one BatchNorm coefficient set per chunk
 size_t train_query_image_floats() { return EVAL_FLOATS; }
 
 void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s) {
   hipLaunchKernelGGL(k_pack_eval_vectors<true>, dim3(1), dim3(256), 0, s, P, img);   // occ_out, raw biases
   hipLaunchKernelGGL(k_eval_wscale<true>, dim3(8), dim3(256), 0, s, P, img);
-  hipLaunchKernelGGL(PCN_EH3 ? k_pack_eval_h3<true> : k_pack_eval_h<true>, dim3((unsigned)((EH_VECS + 255) / 256)),
+  hipLaunchKernelGGL(k_pack_eval_h3<true>, dim3((unsigned)((EH_VECS + 255) / 256)),
                      dim3(256), 0, s, P, img);
 }
 
@@ -1389,10 +899,10 @@ void launch_train_query(const float* rays, int stride, const float* z, int64_t t
                         const float* img, const float* coef, int64_t chunk, float* p_out, hipStream_t s,
                         float* hst, int64_t hst_chunk, int64_t hst_layer, int64_t store_chunks) {
   const int64_t C = (total + chunk - 1) / chunk;
-  const int64_t ns = PCN_EH3 ? EH3_NS : 32 * E2_T;
+  const int64_t ns = 16 * EH3_SB;
   const int64_t per = (std::min(chunk, total) + ns - 1) / ns;
   if (C >= 65536 || per >= ((int64_t)1 << 31)) throw std::runtime_error("train query: too many chunks / samples");
-  hipLaunchKernelGGL(PCN_EH3 ? k_nof_eval_h3<true> : k_nof_eval_h2<true>, dim3((unsigned)per, (unsigned)C), dim3(256),
+  hipLaunchKernelGGL(k_nof_eval_h3<true>, dim3((unsigned)per, (unsigned)C), dim3(256),
                      0, s, rays, stride, z, total,
                      S, ein, img, p_out, coef, chunk, hst, hst_chunk, hst_layer, store_chunks);
 }
@@ -1479,7 +989,7 @@ extern "C" int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* pack
   hipLaunchKernelGGL(k_pack_eval_weights, dim3(nb), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_pack_eval_vectors<false>, dim3(1), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_eval_wscale<false>, dim3(8), dim3(256), 0, s, P, packed);
-  hipLaunchKernelGGL(PCN_EH3 ? k_pack_eval_h3<false> : k_pack_eval_h<false>, dim3((unsigned)((EH_VECS + 255) / 256)),
+  hipLaunchKernelGGL(k_pack_eval_h3<false>, dim3((unsigned)((EH_VECS + 255) / 256)),
                      dim3(256), 0, s, P, packed);
   PCN_LAUNCH_CHECK("pcnerf_nof_pack_eval");
   PCN_API_END
@@ -1517,39 +1027,6 @@ extern "C" int pcnerf_nof_forward_eval(const float* emb, int64_t n, const float*
   PCN_API_END
 }
 
-#if PCN_EH2_STAMP
-#include <vector>
-// diagnostic builds: out[0] = median in-kernel clock (MHz) of the last k_nof_eval_h2 launch's stamped blocks,
-// out[1 + i] = median cycles of phase i (0 prologue, 1 layer 0, ..., 8 layer 7, 9 occ_out), out[11..13] layer 2's
-// k-loop / epilogue + first barrier / split, out[14] = blocks
-extern "C" int pcnerf_debug_eh2_clock(double* out) {
-  static unsigned long long h[8192][16];
-  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(pcn::g_eh2_clk), sizeof(h)) != hipSuccess) return 1;
-  std::vector<std::vector<double>> ph(14);
-  for (int b = 0; b < 8192; ++b) {
-    if (h[b][1] <= h[b][0] || h[b][12] <= h[b][2]) continue;
-    ph[0].push_back((double)(h[b][12] - h[b][2]) / (double)(h[b][1] - h[b][0]) * 100.0);
-    for (int i = 0; i < 10; ++i) ph[1 + i].push_back((double)(h[b][3 + i] - h[b][2 + i]));
-#if PCN_EH2_STAMP == 2
-    // prologue: coefficients / ring loads issued; sample positions + barrier; sincosf + barrier; B-order split
-    ph[11].push_back((double)(h[b][13] - h[b][2]));
-    ph[12].push_back((double)(h[b][14] - h[b][13]));
-    ph[13].push_back((double)(h[b][15] - h[b][14]));
-#else
-    ph[11].push_back((double)(h[b][13] - h[b][4]));   // layer 2: k-loop (from layer 1's end)
-    ph[12].push_back((double)(h[b][14] - h[b][13]));  // epilogue 1 + first barrier
-    ph[13].push_back((double)(h[b][15] - h[b][14]));  // scales + split + LDS writes
-#endif
-  }
-  if (ph[0].empty()) return 2;
-  for (int i = 0; i < 14; ++i) {
-    std::sort(ph[i].begin(), ph[i].end());
-    out[i] = ph[i][ph[i].size() / 2];
-  }
-  out[14] = (double)ph[0].size();
-  return 0;
-}
-#endif
 
 extern "C" int pcnerf_set_eval_math(int mode) {
   if (mode < 0 || mode > 1) {

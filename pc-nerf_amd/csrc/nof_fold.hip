@@ -837,7 +837,7 @@ static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, fl
 }
 
 // The train-mode query evaluated per sample (the network as written, one BatchNorm coefficient set per chunk):
-// the chunk statistics from the encoding moments and the float64 layer algebra above, then k_nof_eval_h2<true>.
+// the chunk statistics from the encoding moments and the float64 layer algebra above, then k_nof_eval_h3<true>.
 static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, float momentum, float eps,
                           void* state, size_t state_bytes, float* p_out, hipStream_t s, void* store = nullptr,
                           int64_t store_chunks = 0) {

@@ -28,7 +28,7 @@ void set_error(const std::string& msg);
 void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,
                         const double* fold, int64_t chunk, float* p_out, hipStream_t s);
 
-// The train-mode query in k_nof_eval_h2's form (nof_eval.hip): the image (train_query_image_floats floats) holds
+// The train-mode query in k_nof_eval_h3's form (nof_eval.hip): the image (train_query_image_floats floats) holds
 // the raw split weights and occ_out; coef[chunk] (TQ_COEF_FLOATS) each chunk's BatchNorm coefficients and the
 // per-layer operand scales of its bound.
 size_t train_query_image_floats();

@@ -23,7 +23,7 @@ enum ProfTag {
   PT_TRAIN_H1 = 15,    // k_train_h1: layer 1 from the encoding tiles (h0 recomputed)
   PT_FOLD_MOMENTS = 16,// train fold: k_tf_moments / k_tf_gmoments (per-sample encoding moments)
   PT_FOLD_ALGEBRA = 17,// train fold: the per-chunk float64 layer algebra (forward or backward)
-  PT_TRAIN_QUERY = 18, // k_nof_eval_h2<true>: the fused train-mode query (per-chunk BatchNorm coefficients)
+  PT_TRAIN_QUERY = 18, // k_nof_eval_h3<true>: the fused train-mode query (per-chunk BatchNorm coefficients)
 };
 extern bool g_prof_on;
 class ProfScope {

@@ -1,5 +1,5 @@
-"""A/B timing of the fused train-mode query (pcnerf_nof_query_train_fused, k_nof_eval_h2<true>) and the split eval
-query (k_nof_eval_h2<false>) across variant libraries (pc-nerf_amd/lib/variants/*.so) in ONE process, interleaved
+"""A/B timing of the fused train-mode query (pcnerf_nof_query_train_fused, k_nof_eval_h3<true>) and the split eval
+query (k_nof_eval_h3<false>) across variant libraries (pc-nerf_amd/lib/variants/*.so) in ONE process, interleaved
 rounds on the same inputs (cdna_hip_programming.md 5.4 rule 24).  Prints per-variant median times and the max
 relative output difference against the 'base' variant.   env: FA_RAYS, FA_S, FA_CHUNK, FA_ROUNDS, VB_ONLY."""
 import ctypes
