@@ -321,6 +321,10 @@ __global__ void k_pack_eval_h3(NofParamsDev P, float* __restrict__ out) {
 // hold, 14 % less weight stream per sample) -2 % / +1 % on the train query on two boxes and +7 % on the eval query
 // (profiles/r03l_variants_eval_sb7.json, _sb.json), 5: +3 % / +9 %
 constexpr int EH3_SB = 6;
+#ifndef PCN_EH3_NTSTORE
+#define PCN_EH3_NTSTORE 1   // activation-store writes nontemporal (streamed past L2, which holds the weight image):
+                            // the store-writing train query -3.8 % (profiles/r03n_variants_eval_ntstore.json)
+#endif
 #ifndef PCN_EH3_RING
 #define PCN_EH3_RING 2    // k_nof_eval_h3: weight-ring slots (prefetch distance RING - 1 k-steps of 32); 2 or 4
 #endif
@@ -616,7 +620,11 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
     const int sl = 16 * (int)(q & 1) + li + 32 * (g & 1);
     float* dst = hst + (int64_t)blockIdx.y * hst_chunk + (int64_t)L * hst_layer +
                  ((tile * 32 + (n0 >> 3)) * 64 + sl) * 4;
+#if PCN_EH3_NTSTORE
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4_*>(dst));
+#else
     *reinterpret_cast<f32x4_*>(dst) = v;
+#endif
   };
   auto epi_tr = [&](int L, auto PS) __attribute__((always_inline)) {
     constexpr bool ps = decltype(PS)::value;

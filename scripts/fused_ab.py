@@ -1,7 +1,8 @@
 """A/B timing of the fused train-mode query (pcnerf_nof_query_train_fused, k_nof_eval_h3<true>) and the split eval
 query (k_nof_eval_h3<false>) across variant libraries (pc-nerf_amd/lib/variants/*.so) in ONE process, interleaved
 rounds on the same inputs (cdna_hip_programming.md 5.4 rule 24).  Prints per-variant median times and the max
-relative output difference against the 'base' variant.   env: FA_RAYS, FA_S, FA_CHUNK, FA_ROUNDS, VB_ONLY."""
+relative output difference against the 'base' variant.   env: FA_RAYS, FA_S, FA_CHUNK, FA_ROUNDS, VB_ONLY, FA_STORE
+(1: the train query writes the activation store of every chunk, pcnerf_nof_query_train_fused_store)."""
 import ctypes
 import glob
 import json
@@ -48,6 +49,8 @@ def main():
         f.restype, f.argtypes = ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64]
         return f(n * S, chunk)
     ws = torch.empty(max(need(L) for L in Ls.values()), dtype=torch.uint8, device=dev)
+    nst = (n * S + chunk - 1) // chunk if os.environ.get("FA_STORE") == "1" else 0   # activation store: all chunks
+    store = torch.empty(nst * first.pcnerf_nof_store_bytes(chunk), dtype=torch.uint8, device=dev) if nst else None
     packed = torch.empty(first.pcnerf_nof_eval_packed_floats(), device=dev)
     times = {k: {"train": [], "eval": []} for k in Ls}
     tags = {16: "moments", 17: "algebra", 18: "train_query"}   # prof.h: per-kernel HIP events of the train query
@@ -67,7 +70,11 @@ def main():
                 L.pcnerf_prof_enable(1 if mode == "train" else 0)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                if mode == "train":
+                if mode == "train" and nst:
+                    rc = L.pcnerf_nof_query_train_fused_store(rays.data_ptr(), n, rays.shape[1], z.data_ptr(), S,
+                                                              chunk, ctypes.byref(s), 0.0, 1e-5, ws.data_ptr(),
+                                                              ws.numel(), p.data_ptr(), store.data_ptr(), nst, st)
+                elif mode == "train":
                     rc = L.pcnerf_nof_query_train_fused(rays.data_ptr(), n, rays.shape[1], z.data_ptr(), S, chunk,
                                                         ctypes.byref(s), 0.0, 1e-5, ws.data_ptr(), ws.numel(),
                                                         p.data_ptr(), st)
