@@ -325,6 +325,11 @@ constexpr int EH3_SB = 6;
 #define PCN_EH3_NTSTORE 1   // activation-store writes nontemporal (streamed past L2, which holds the weight image):
                             // the store-writing train query -3.8 % (profiles/r03n_variants_eval_ntstore.json)
 #endif
+#ifndef PCN_EH3_ORD_TR
+#define PCN_EH3_ORD_TR 1  // k_nof_eval_h3<true>: MFMAs of a product group neuron-block-outer (1) or sample-block-outer
+                          // (0, the eval kernel's order): -0.9 % / -1.4 % in two same-process A/Bs, bit-identical
+                          // (profiles/r03l_variants_eval_order.json, r03q_variants_eval_order_tr.json)
+#endif
 #ifndef PCN_EH3_RING
 #define PCN_EH3_RING 2    // k_nof_eval_h3: weight-ring slots (prefetch distance RING - 1 k-steps of 32); 2 or 4
 #endif
@@ -350,6 +355,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
                                                         int64_t chunk, float* __restrict__ hst, int64_t hst_chunk,
                                                         int64_t hst_layer, int64_t store_chunks) {
   constexpr int SB = EH3_SB, NS = 16 * SB, R3 = PCN_EH3_RING, D3 = R3 - 1;
+  constexpr bool ORD = TR && PCN_EH3_ORD_TR;
   typedef float f32x4_ __attribute__((ext_vector_type(4)));
   __shared__ eh_f16x8 act[8][SB][2][64];
   __shared__ eh_f16x8 eb[2][SB][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
@@ -494,20 +500,26 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
       }
     }
 #pragma unroll
-    for (int sb = 0; sb < SB; ++sb)
+    for (int o1 = 0; o1 < (ORD ? 4 : SB); ++o1)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int o2 = 0; o2 < (ORD ? SB : 4); ++o2) {
+        const int sb = ORD ? o2 : o1, j = ORD ? o1 : o2;
         acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][0], bm[sb], first ? f32x4_{} : acc[j][sb], 0, 0, 0);
+      }
 #pragma unroll
-    for (int sb = 0; sb < SB; ++sb)
+    for (int o1 = 0; o1 < (ORD ? 4 : SB); ++o1)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int o2 = 0; o2 < (ORD ? SB : 4); ++o2) {
+        const int sb = ORD ? o2 : o1, j = ORD ? o1 : o2;
         acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][0], bh[sb], acc[j][sb], 0, 0, 0);
+      }
 #pragma unroll
-    for (int sb = 0; sb < SB; ++sb)
+    for (int o1 = 0; o1 < (ORD ? 4 : SB); ++o1)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int o2 = 0; o2 < (ORD ? SB : 4); ++o2) {
+        const int sb = ORD ? o2 : o1, j = ORD ? o1 : o2;
         acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][1], bh[sb], acc[j][sb], 0, 0, 0);
+      }
     ++gk;
   };
   // the 8 hidden k-steps of a layer, software-pipelined: per k-step the products run in the order Wh.xm, Wh.xh,
@@ -526,10 +538,12 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
       load_w(wr[(pos + D3) & (R3 - 1)], gk + D3);
       const eh_f16x8 (&wc)[4][2] = wr[pos & (R3 - 1)];
 #pragma unroll
-      for (int sb = 0; sb < SB; ++sb)
+      for (int o1 = 0; o1 < (ORD ? 4 : SB); ++o1)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int o2 = 0; o2 < (ORD ? SB : 4); ++o2) {
+          const int sb = ORD ? o2 : o1, j = ORD ? o1 : o2;
           acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][0], bm[sb], (first && s == 0) ? f32x4_{} : acc[j][sb], 0, 0, 0);
+        }
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < 8) {
 #pragma unroll
@@ -537,15 +551,19 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int sb = 0; sb < SB; ++sb)
+      for (int o1 = 0; o1 < (ORD ? 4 : SB); ++o1)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int o2 = 0; o2 < (ORD ? SB : 4); ++o2) {
+          const int sb = ORD ? o2 : o1, j = ORD ? o1 : o2;
           acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][0], bh[sb], acc[j][sb], 0, 0, 0);
+        }
 #pragma unroll
-      for (int sb = 0; sb < SB; ++sb)
+      for (int o1 = 0; o1 < (ORD ? 4 : SB); ++o1)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int o2 = 0; o2 < (ORD ? SB : 4); ++o2) {
+          const int sb = ORD ? o2 : o1, j = ORD ? o1 : o2;
           acc[j][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wc[j][1], bh[sb], acc[j][sb], 0, 0, 0);
+        }
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < 8) {
 #pragma unroll
