@@ -24,6 +24,12 @@ and relays rank 0's line; under an external torchrun ``--gpus`` must equal WORLD
 RCCL; the timed region is bracketed by barriers and the time is the max over ranks.  ``--dry-run`` exercises the
 launcher and the distributed timing on CPU (gloo), with no GPU.
 
+The default run (N=1, config 2, train_fwd) also times, in the same process and as extra keys of its one line, the
+training step (``train_step``: config 2 with backward + Adam), the reference's own shell setting of it
+(``train_step_refcfg``: 256 rays at 768 + 1536 samples, chunk 262,144, shells/pretraining/KITTI00_pcnerf_train.bash),
+``val`` and the two-step ``view``, each with its own ms_per_step, roofline, cpu_baseline and cd_vs_ref (--no-extra
+skips them), and measures what the fp16 matrix pipe sustains on the board (``mfma_ceiling_measured``, 1 s).
+
 Prints ONE JSON line (rank 0) with the throughput, the dominant kernel's roofline (HIP events over the timed
 region, on the kernels' own stream) and a CPU baseline (the CPU oracle on a bounded sample, rank 0 at N=1 only).
 """
@@ -76,6 +82,9 @@ def parse(argv=None):
     ap.add_argument("--gather", action="store_true",
                     help="gather every block's depth_fine to rank 0 inside each step (eval-driver output path; on "
                          "by default for configs 4 and 5)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="default run only: skip the extra lines (train_step, train_step_refcfg, val, view)")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the measured fp16 MFMA ceiling (1 s)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / distributed-timing check on CPU (gloo): no GPU, no render")
     a = ap.parse_args(argv)
@@ -224,6 +233,18 @@ def make_blocks(a, rank, world, dev, syn):
     return out
 
 
+# The default N=1 run also times these lines in the same process, as extra keys of the one JSON line (the headline
+# value stays the render+loss forward): the whole training step at config 2 and at the reference's own shell setting
+# (shells/pretraining/KITTI00_pcnerf_train.bash:8-10: 256 rays, 768 + 1536 samples, chunk 262,144 -- the setting of
+# the reference's published 779 rays/s), render_rays_val and the two-step inference.
+EXTRA_LINES = {
+    "train_step": dict(mode="train_step", rays=65536, samples=128, importance=256, cpu_rays=512),
+    "train_step_refcfg": dict(mode="train_step", rays=256, samples=768, importance=1536, cpu_rays=64),
+    "val": dict(mode="val", rays=65536, samples=128, importance=256, cpu_rays=2048),
+    "view": dict(mode="view", rays=16384, samples=128, importance=256, cpu_rays=512),
+}
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
@@ -243,12 +264,70 @@ def main(argv=None):
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    from nof import _hip
+    L = _hip.lib()
 
-    from nof import _hip, _ops, synthetic as syn
+    head = run_line(a, L, dev, rank, world)
+
+    # what the fp16 matrix pipe sustains on this board, measured in this process
+    ceiling = None
+    if not a.no_ceiling:
+        tf, mhz = ctypes.c_double(), ctypes.c_double()
+        _hip.check(L.pcnerf_mfma_ceiling(1.0, ctypes.byref(tf), ctypes.byref(mhz),
+                                         torch.cuda.current_stream(dev).cuda_stream))
+        ceiling = {"TFLOPs": round(tf.value, 1), "clock_MHz": round(mhz.value), "seconds": 1.0,
+                   "kernel": "bare v_mfma_f32_16x16x32_f16 loop, B from LDS, random fp16 operands, 1 wave/SIMD"}
+    extras = {}
+    if world == 1 and a.config == 2 and a.mode == "train_fwd" and not a.fold and not a.no_extra:
+        for name, over in EXTRA_LINES.items():
+            b = argparse.Namespace(**{**vars(a), **over, "no_fp32_line": True, "gather": False})
+            extras[name] = run_line(b, L, dev, rank, world)
+    if rank != 0:
+        if dist:
+            tdist.destroy_process_group()
+        return
+    for ln in [head] + list(extras.values()):
+        add_ceiling(ln["roofline"], ceiling)
+        if ln.get("fp32_mfma"):
+            add_ceiling(ln["fp32_mfma"]["roofline"], ceiling)
+    out = line_json(a, world, head)
+    out["mfma_ceiling_measured"] = ceiling
+    for name, ln in extras.items():
+        b = argparse.Namespace(**{**vars(a), **EXTRA_LINES[name]})
+        e = line_json(b, world, ln)
+        out[name] = {k: e[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
+                                        "roofline", "cpu_baseline", "cd_vs_ref", "loss", "kernels",
+                                        "kernels_step_ms")}
+    print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+def add_ceiling(roof, ceiling):
+    """The algorithmic fraction (fp32-equivalent FLOP of the network as written / the fp16 dense peak the split
+    products run on) beside the issued-products ``frac``, and the issued rate against the measured ceiling."""
+    if roof is None or roof.get("unit") != "TFLOP/s":
+        return
+    fp32eq = roof.get("fp32_equivalent_TFLOPs")
+    if fp32eq is not None:
+        roof["frac_algorithmic"] = round(fp32eq / FP16_MFMA_PEAK_TFLOPS, 4)
+    if ceiling and roof.get("products_per_fp32_product"):
+        roof["ceiling_measured_TFLOPs"] = ceiling["TFLOPs"]
+        roof["frac_of_measured_ceiling"] = round(roof["achieved"] / ceiling["TFLOPs"], 4)
+
+
+def run_line(a, L, dev, rank, world):
+    """One bench line: ``a.warmup`` untimed + ``a.steps`` timed steps of ``a.mode`` on this rank's blocks, the
+    kernel breakdown / roofline of the last step, the fp32-MFMA comparison and (rank 0, N=1) the CPU baseline."""
+    import gc
+    from nof import _ops, synthetic as syn
     from nof.blocks import allreduce_grads, gather_rows, max_over_ranks
     from nof.criteria import nof_loss
     from nof.networks import Embedding, NOF_coarse, NOF_fine
     from nof.render import render_rays_train, render_rays_val, render_rays_view_0525_2_2
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
 
     view = a.mode == "view"
     train = a.mode in ("train_fwd", "train_step")
@@ -258,8 +337,8 @@ def main(argv=None):
             _ops.set_train_fold(True)
         else:
             _ops.set_eval_fold(True)
-    if grad:   # this caller allocates nothing between forward and backward: let the store take the free HBM
-        _ops.set_activation_store_budget(1 << 62)
+    # this caller allocates nothing between forward and backward: let the store take the free HBM
+    prev_budget = _ops.set_activation_store_budget(1 << 62) if grad else None
     blocks = make_blocks(a, rank, world, dev, syn)
     for blk in blocks:
         blk["mc"] = syn.load_into(NOF_coarse(), syn.init_nof_params(blk["seeds"][0])).to(dev).train(train)
@@ -312,8 +391,6 @@ def main(argv=None):
                 allreduce_grads(opt.param_groups[0]["params"])
             opt.step()
         return torch.stack(losses).sum() if losses else torch.zeros((), device=dev)
-
-    L = _hip.lib()
 
     breakdown = {}   # wall time of the instrumented (last) step, the one the kernel breakdown comes from
 
@@ -377,42 +454,66 @@ def main(argv=None):
                      "note": "the same timed steps with the fused eval network as fp32 MFMA (k_nof_eval, v_mfma_f32_32x32x2_f32)"}
         fp32_elapsed = el32
 
+    # rays processed per step by the whole job (weak scaling: every rank its own blocks / batch)
+    # (view: LiDAR rays = ray groups, a.rays per block; otherwise the rays of the block's batch)
+    n_local = a.rays * len(blocks) if view else sum(blk["rays"].shape[0] for blk in blocks)
+    blocks_rank0 = [blk["block"] for blk in blocks]
+    sample = {k: blocks[0][k] for k in ("block", "rays", "seeds", "sub_num")}
+    del blocks, opt, step, block_step
+    gc.collect()
+    torch.cuda.empty_cache()
+    if grad:
+        _ops.set_activation_store_budget(prev_budget)
+    if a.fold:
+        _ops.set_train_fold(False)
+        _ops.set_eval_fold(False)
+
     cpu = cdref = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline belongs to the N=1 line only
         if a.cpu_rays is None:
             a.cpu_rays = 512 if view else 256 if a.config == 3 else 1024 if grad else 4096
-        sample = blocks[0]
+        if a.fold:
+            (_ops.set_train_fold if train else _ops.set_eval_fold)(True)
         cpu, ext = cpu_baseline(a, syn, sample)
         cdref = (cd_vs_ref_view if view else cd_vs_ref)(a, syn, ext, dev, sample)
+        if a.fold:
+            _ops.set_train_fold(False)
+            _ops.set_eval_fold(False)
+        del ext
+        gc.collect()
+        torch.cuda.empty_cache()
 
-    # rays processed per step by the whole job (weak scaling: every rank its own blocks / batch)
-    # (view: LiDAR rays = ray groups, a.rays per block; otherwise the rays of the block's batch)
-    n_local = a.rays * len(blocks) if view else sum(blk["rays"].shape[0] for blk in blocks)
     n_tot = torch.tensor([float(n_local)], dtype=torch.float64, device=dev)
     if dist:
         tdist.all_reduce(n_tot)
     rays_per_step = float(n_tot)
-    if rank != 0:
-        if dist:
-            tdist.destroy_process_group()
-        return
     value = rays_per_step * a.steps / elapsed
     if fp32_line is not None:
         fp32_line["value"] = round(rays_per_step * a.steps / fp32_elapsed, 1)
+    return {"value": value, "elapsed": elapsed, "rays_per_step": rays_per_step, "roofline": roof,
+            "kernels": kernels, "kstep_ms": kstep_ms, "fp32_mfma": fp32_line, "cpu_baseline": cpu,
+            "cd_vs_ref": cdref, "loss": loss_val, "train_math": train_math, "eval_math": eval_math,
+            "blocks_rank0": blocks_rank0}
+
+
+def line_json(a, world, ln):
+    """The JSON object of one bench line."""
+    view = a.mode == "view"
+    train = a.mode in ("train_fwd", "train_step")
     scaling = "strong" if a.config in (4, 5) else "weak"
-    out = {
+    return {
         "metric": "LiDAR rays/s (render+loss) at 128 samples/ray; CD vs ref depth",
-        "value": round(value, 1),
+        "value": round(ln["value"], 1),
         "unit": "rays/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+        "ms_per_step": round(1e3 * ln["elapsed"] / a.steps, 3),
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
         # every tensor and every accumulation is fp32; the Linear layers' products as the selected math forms them
-        "dtype": dtype_label(train_math, eval_math, a.fold),
+        "dtype": dtype_label(ln["train_math"], ln["eval_math"], a.fold),
         "data": {2: "synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)",
                  3: "KITTI-00 fixture scene (scans 1151-1156, every 40th point) rays built by nof.dataset, "
                     "262,144-ray batches drawn with replacement; seeded NOF weights",
@@ -430,27 +531,24 @@ def main(argv=None):
                                               "(opt-in)" if train else " -- exact affine fold of the eval network "
                                               "(opt-in)") if a.fold else ""),
                    "baseline_config": a.config,
-                   "rays_per_step": int(rays_per_step), "rays_per_block": a.rays,
-                   "blocks_rank0": [blk["block"] for blk in blocks],
+                   "rays_per_step": int(ln["rays_per_step"]), "rays_per_block": a.rays,
+                   "blocks_rank0": ln["blocks_rank0"],
                    "N_samples": a.samples, "N_importance": a.importance,
                    "mlp_samples_per_ray": a.samples + a.samples + a.importance, "chunk": a.chunk,
                    "batchnorm": "train (batch stats per chunk)" if train else "eval (folded)",
                    "network": "affine fold (sigmoid(a.e + c))" if a.fold else "9 Linear layers as written",
                    "segmented_ratio": 0.1 if train else None, "perturb": 1 if train else 0,
                    "parallelism": (f"dp{world}" if a.config == 3 else f"blocks{world}"), "gather": bool(a.gather)},
-        "roofline": roof,
-        "train_math": train_math,
-        "eval_math": eval_math,
-        "fp32_mfma": fp32_line,
-        "cpu_baseline": cpu,
-        "cd_vs_ref": cdref,
-        "loss": loss_val,
-        "kernels": kernels,
-        "kernels_step_ms": round(kstep_ms, 3),   # the instrumented last step's own time (the kernels' step)
+        "roofline": ln["roofline"],
+        "train_math": ln["train_math"],
+        "eval_math": ln["eval_math"],
+        "fp32_mfma": ln["fp32_mfma"],
+        "cpu_baseline": ln["cpu_baseline"],
+        "cd_vs_ref": ln["cd_vs_ref"],
+        "loss": ln["loss"],
+        "kernels": ln["kernels"],
+        "kernels_step_ms": round(ln["kstep_ms"], 3),   # the instrumented last step's own time (the kernels' step)
     }
-    print(json.dumps(out), flush=True)
-    if dist:
-        tdist.destroy_process_group()
 
 
 def dtype_label(train_math, eval_math, fold=False):

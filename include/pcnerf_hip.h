@@ -169,7 +169,9 @@ int pcnerf_nof_query_train_fold_backward(const float* rays, int64_t n_rays, int 
  * products, BatchNorm applied in each layer's epilogue); only the chunk statistics it needs come from the chunk's
  * encoding moments through the float64 layer algebra above -- exact because every LeakyReLU(True) is the identity
  * (negative_slope = 1, models.py:72,92).  Running stats are updated chunk by chunk as nn.BatchNorm1d does.  `state`:
- * pcnerf_nof_train_fold_bytes(total_samples, chunk) bytes of scratch. */
+ * pcnerf_nof_train_fused_bytes(total_samples, chunk) bytes of scratch (the fold's forward pieces only: no
+ * backward state). */
+size_t pcnerf_nof_train_fused_bytes(int64_t total_samples, int64_t chunk);
 int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z, int n_samples,
                                  int64_t chunk, const pcnerf_nof_params* params, float momentum, float eps,
                                  void* state, size_t state_bytes, float* p_out, void* stream);
@@ -211,6 +213,10 @@ int pcnerf_composite(const float* p, const float* z, int64_t n_rays, int n_sampl
                      float* sl1_ray, double* opac_row, float* depth2, void* stream);
 /* (opac_row, nullable: per-ray sum of log(0.1+p)+log(1.1-p)+2.20727, render.py:224; depth2, nullable: z at the
  * rank of the last sample in the descending weight order, render.py:598-600.) */
+/* depth2's order of equal weights (render.py:598 argsort(descending=True)): 0 (default) = stable, as torch sorts
+ * these rows on the GPU where the reference runs render_rays (rows > 32 long: merge / radix sort); 1 = torch CPU's
+ * std::sort (introsort) order, reproduced per tied row (at most 2048 samples per ray; checked before any launch). */
+int pcnerf_set_depth2_order(int order);
 /* mean = sum(x[0:n]) / denom, one float written to out (used for the opacity means). */
 int pcnerf_mean_f64(const double* x, int64_t n, double denom, float* out, void* stream);
 
@@ -337,6 +343,12 @@ int pcnerf_range_metrics(const float* pred, const float* gt, const float* origin
  * the summed duration, launch count and algorithmic FLOPs / bytes of those launches. */
 int pcnerf_prof_enable(int on);
 int pcnerf_prof_read(int tag, double* total_ms, int64_t* launches, double* flops, double* bytes);
+
+/* What the fp16 matrix pipe sustains on this board: the headline query's instruction (v_mfma_f32_16x16x32_f16, B
+ * operands from LDS, one wave per SIMD, 24 accumulators per wave) in a bare loop on random operands, launched back
+ * to back for `seconds` (settle for the first half, timed with HIP events over the second).  *tflops = dense fp16
+ * TFLOP/s, *clock_mhz = median shader clock of the timed launches.  No reference counterpart (measurement only). */
+int pcnerf_mfma_ceiling(double seconds, double* tflops, double* clock_mhz, void* stream);
 
 #ifdef __cplusplus
 }

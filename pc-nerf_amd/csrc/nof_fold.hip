@@ -69,16 +69,20 @@ struct FoldLayout {
   size_t doubles;
 };
 
-static FoldLayout fold_layout(int64_t total, int64_t chunk) {
+// fwd_only: the fused train query's state (pcnerf_nof_train_fused_bytes) -- the backward-only pieces (gm, ab, dg, dw,
+// vec: about 2.5 MB per chunk) and the fold's logits are empty, so its size does not grow with them
+static FoldLayout fold_layout(int64_t total, int64_t chunk, bool fwd_only = false) {
   FoldLayout F{};
   F.C = (total + chunk - 1) / chunk;
   const int64_t tiles = (std::min(chunk, total) + 63) / 64;
   F.wpc = (int)std::max<int64_t>(1, std::min<int64_t>(TF_WPC_MAX, tiles / 64));
   F.G = (int)std::min<int64_t>(F.C, TF_G_MAX);
   const size_t C = (size_t)F.C, wpc = (size_t)F.wpc, G = (size_t)F.G;
+  const size_t b = fwd_only ? 0 : 1;
   const size_t n[FOLD_PIECES] = {C * wpc * 4096, C * 4096, C * 64, C * 64, 8 * C * 256 * 64, 8 * C * 256 * 64,
-                                 8 * C * 1024, C * 64, C * wpc * 64, 2 * C * 256 * 64, 8 * C * 256, G * 256 * 256,
-                                 C * 576, C * TQ_COEF_FLOATS / 2, (train_query_image_floats() + 1) / 2};
+                                 8 * C * 1024, b * C * 64, b * C * wpc * 64, b * 2 * C * 256 * 64, b * 8 * C * 256,
+                                 b * G * 256 * 256, b * C * 576, C * TQ_COEF_FLOATS / 2,
+                                 (train_query_image_floats() + 1) / 2};
   size_t o = 0;
   for (int i = 0; i < FOLD_PIECES; ++i) {
     F.off[i] = o;
@@ -844,7 +848,7 @@ static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, f
   PCN_CHECK(q.total > 0 && q.chunk > 0, "train query: empty input");
   // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
   PCN_CHECK(q.total % q.chunk != 1 && q.total != 1, "Expected more than 1 value per channel when training");
-  const FoldLayout Lo = fold_layout(q.total, q.chunk);
+  const FoldLayout Lo = fold_layout(q.total, q.chunk, true);
   PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train query: state buffer too small");
   PCN_CHECK(Lo.C < 65536, "train query: too many chunks for one query");
   NofParamsDev P;
@@ -925,6 +929,11 @@ using namespace pcn;
 extern "C" size_t pcnerf_nof_train_fold_bytes(int64_t total_samples, int64_t chunk) {
   if (total_samples <= 0 || chunk <= 0) return 0;
   return fold_layout(total_samples, std::min(chunk, total_samples)).doubles * sizeof(double);
+}
+
+extern "C" size_t pcnerf_nof_train_fused_bytes(int64_t total_samples, int64_t chunk) {
+  if (total_samples <= 0 || chunk <= 0) return 0;
+  return fold_layout(total_samples, std::min(chunk, total_samples), true).doubles * sizeof(double);
 }
 
 extern "C" int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z,

@@ -416,8 +416,10 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
     if (lane == 0) opac_row[ray] = op;
   }
   if (depth2) {  // render.py:598-600: z at the position of sample S-1 in argsort(w, descending=True)
-    // without a tie of w[S-1], that position is the count of weights ordered before it (any sort agrees);
-    // rows with a tie are redone by k_depth2_ties, which reproduces torch's own order of equal keys
+    // the count of weights a stable descending sort orders before it: every greater weight, and every equal one
+    // (all have smaller indices) -- torch's sort on the GPU, where the reference runs this (the rows it sorts are
+    // > 32 long: merge / radix sort, stable).  Under pcnerf_set_depth2_order(1) rows with a tie are redone by
+    // k_depth2_ties (torch CPU's std::sort order of equal keys)
     const int last_lane = (S - 1) / B, last_j = (S - 1) % B;
     float wl = 0.0f;
 #pragma unroll
@@ -427,7 +429,7 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
     int cnt = 0;
 #pragma unroll
     for (int j = 0; j < MAXB; ++j)
-      if (j < nb) cnt += kv_desc(wv[j], wl);
+      if (j < nb && i0 + j < S - 1) cnt += kv_desc(wv[j], wl) || !kv_desc(wl, wv[j]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
     if (lane == 0) depth2[ray] = Z[ray * S + cnt];
@@ -1008,6 +1010,16 @@ extern "C" int pcnerf_perturb(const float* z, int64_t n_rays, int n_samples, flo
   PCN_API_END
 }
 
+// render_rays' depth2 tie order: 0 = stable (torch's sort on the GPU, default), 1 = torch CPU's std::sort
+static int g_depth2_order = 0;
+
+extern "C" int pcnerf_set_depth2_order(int order) {
+  PCN_API_BEGIN
+  PCN_CHECK(order == 0 || order == 1, "pcnerf_set_depth2_order: order must be 0 (stable) or 1 (torch CPU)");
+  g_depth2_order = order;
+  PCN_API_END
+}
+
 extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, int n_samples, const float* noise,
                                 float noise_std, float eps, const float* rays, int ray_stride, int child_near_col,
                                 int child_far_col, int range_col, float* weights, float* depth, float* free_ray,
@@ -1021,6 +1033,9 @@ extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, 
     PCN_CHECK(child_near_col < ray_stride && child_far_col < ray_stride && range_col < ray_stride,
               "pcnerf_composite: column outside ray row");
   }
+  PCN_CHECK(!depth2 || g_depth2_order == 0 || n_samples <= 2048,
+            "pcnerf_composite: depth2 in torch CPU's tie order (pcnerf_set_depth2_order(1)) supports at most 2048 "
+            "samples per ray");
   const int B = (n_samples + 63) / 64;
   hipStream_t s = (hipStream_t)stream;
   const dim3 g(nblk(n_rays, 4)), b(256);
@@ -1037,10 +1052,8 @@ extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, 
   else if (B <= 256) PCN_COMP(256);
   else PCN_CHECK(false, "pcnerf_composite: more than 16384 samples per ray");
 #undef PCN_COMP
-  if (depth2) {   // rows whose w[S-1] ties: torch's order of equal keys (k_depth2_ties)
-    PCN_CHECK(n_samples <= 2048, "pcnerf_composite: depth2 supports at most 2048 samples per ray");
+  if (depth2 && g_depth2_order == 1)   // rows whose w[S-1] ties: torch CPU's order of equal keys
     hipLaunchKernelGGL(k_depth2_ties, g, b, (size_t)8 * 4 * n_samples, s, weights, z, n_rays, n_samples, depth2);
-  }
   PCN_LAUNCH_CHECK("pcnerf_composite");
   PCN_API_END
 }

@@ -50,6 +50,7 @@ _SIGS = {
     "pcnerf_perturb": (c_int, [vp, i64, c_int, c_float, vp, vp, vp]),
     "pcnerf_composite": (c_int, [vp, vp, i64, c_int, vp, c_float, c_float, vp, c_int, c_int, c_int, c_int, vp, vp,
                                  vp, vp, vp, vp, vp]),
+    "pcnerf_set_depth2_order": (c_int, [c_int]),
     "pcnerf_mean_f64": (c_int, [vp, i64, ctypes.c_double, vp, vp]),
     "pcnerf_resample": (c_int, [vp, vp, i64, c_int, c_int, vp, vp, vp]),
     "pcnerf_sample_pdf": (c_int, [vp, vp, i64, c_int, c_int, vp, vp, vp]),
@@ -73,6 +74,8 @@ _SIGS = {
     "pcnerf_prof_enable": (c_int, [c_int]),
     "pcnerf_prof_read": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "pcnerf_mfma_ceiling": (c_int, [ctypes.c_double, ctypes.POINTER(ctypes.c_double),
+                                    ctypes.POINTER(ctypes.c_double), vp]),
     "pcnerf_nof_forward_eval": (c_int, [vp, i64, vp, vp, vp]),
     "pcnerf_nof_fold_eval": (c_int, [ctypes.POINTER(NofParams), vp, vp]),
     "pcnerf_nof_query_eval_fold": (c_int, [vp, i64, c_int, vp, c_int, vp, vp, vp]),
@@ -92,6 +95,7 @@ _SIGS = {
                                                       c_float, vp, vp, c_size, ctypes.POINTER(NofGrads), vp, i64,
                                                       vp]),
     "pcnerf_nof_train_fold_bytes": (c_size, [i64, i64]),
+    "pcnerf_nof_train_fused_bytes": (c_size, [i64, i64]),
     "pcnerf_nof_query_train_fold": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams), c_float,
                                             c_float, vp, c_size, vp, vp]),
     "pcnerf_nof_forward_train_fold": (c_int, [vp, i64, ctypes.POINTER(NofParams), c_float, c_float, vp, c_size, vp,

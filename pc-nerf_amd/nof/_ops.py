@@ -169,6 +169,25 @@ if os.environ.get("PCNERF_EVAL_MATH"):
     set_eval_math(os.environ["PCNERF_EVAL_MATH"])
 
 
+# render_rays' depth2 (render.py:598-600) ranks the last sample in argsort(weights, descending=True); where weights
+# tie exactly (every weight after an opaque sample is 0) the order of equal keys decides.  "stable" (default): the
+# order torch's sort gives on the GPU, where the reference runs render_rays (it moves the draws to cuda:0,
+# render.py:397) -- rows longer than 32 go through torch's merge / radix sort, which are stable.  "cpu": torch CPU's
+# std::sort (introsort) order, for comparing with CPU runs of the reference (the committed goldens).
+_DEPTH2_ORDER = {"stable": 0, "cpu": 1}
+_depth2_order = "stable"
+
+
+def set_depth2_order(order: str) -> str:
+    """Select depth2's order of equal weights; returns the previous one."""
+    global _depth2_order
+    if order not in _DEPTH2_ORDER:
+        raise ValueError(f"depth2 order must be one of {sorted(_DEPTH2_ORDER)}")
+    H.check(H.lib().pcnerf_set_depth2_order(_DEPTH2_ORDER[order]))
+    prev, _depth2_order = _depth2_order, order
+    return prev
+
+
 # Exact affine fold of the TRAIN-mode network (opt-in; VERDICT r1 item 10): every layer's BatchNorm batch statistics
 # follow from the chunk's encoding mean and covariance, so each chunk's network is sigmoid(a_c . emb + c_c)
 # (csrc/nof_fold.hip).  Off by default: the drop-in evaluates the module as written.
@@ -224,7 +243,7 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
         chunk = max(1, min(int(chunk), R * S))
         mom, eps = _bn_config(model)
         s, keep = _params(model)
-        ws = _workspace(z.device, int(L.pcnerf_nof_train_fold_bytes(R * S, chunk)))
+        ws = _workspace(z.device, int(L.pcnerf_nof_train_fused_bytes(R * S, chunk)))
         if store is not None and store.n_chunks > 0:
             H.check(L.pcnerf_nof_query_train_fused_store(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S,
                                                          int(chunk), ctypes.byref(s), mom, eps, ws.data_ptr(),
@@ -285,7 +304,7 @@ def nof_forward_embedded(model, x: torch.Tensor, with_fold_state: bool = False):
             raise ValueError("Expected more than 1 value per channel when training")
         mom, eps = _bn_config(model)
         s, keep = _params(model)
-        ws = _workspace(x.device, int(L.pcnerf_nof_train_fold_bytes(B, B)))
+        ws = _workspace(x.device, int(L.pcnerf_nof_train_fused_bytes(B, B)))
         H.check(L.pcnerf_nof_forward_train_fused(x.data_ptr(), B, ctypes.byref(s), mom, eps, ws.data_ptr(),
                                                  ws.numel(), out.data_ptr(), st))
         _track_batches(model, 1)
@@ -588,6 +607,11 @@ def composite_backward(p, z, noise, noise_std, eps, rays, sub_nerf_test_num, g_d
 
 # Activation-store budget (bytes) of one train-mode pass; None = the default policy below.
 _STORE_BUDGET = None
+# The default cap when the caller set none: a bounded amount, so a drop-in caller that never asked for the store
+# does not find most of the HBM held between its forward and backward (the reference holds only autograd's own
+# tensors).  32 GiB keeps 14 chunks of 262,144 samples -- every chunk of the reference's shell setting (256 rays x
+# 3072 samples = 3 chunks) -- and callers that want the whole step kept opt in (bench.py: free HBM - 4 GiB).
+DEFAULT_STORE_CAP = 32 << 30
 
 
 def set_activation_store_budget(nbytes):
@@ -599,35 +623,39 @@ def set_activation_store_budget(nbytes):
     return prev
 
 
+def store_budget(device, reserve: int) -> int:
+    """Bytes the activation store of one train-mode pass may take (ActivationStore's policy, below)."""
+    import os
+    if os.environ.get("PCNERF_ACT_STORE", "1") == "0":
+        return 0
+    free, _ = torch.cuda.mem_get_info(device)
+    free += torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+    avail = max(0, free - int(reserve))
+    cap = os.environ.get("PCNERF_ACT_STORE_GB")
+    if _STORE_BUDGET is not None:
+        return min(avail, _STORE_BUDGET)
+    if cap is not None:
+        return min(avail, int(float(cap) * (1 << 30)))
+    return min(avail // 2, DEFAULT_STORE_CAP)
+
+
 class ActivationStore:
     """Device buffer for the first ``n_chunks`` chunks' layer outputs + BatchNorm statistics of one train-mode
     query (pcnerf_nof_store_bytes per chunk), so its backward skips their recomputation.
 
     Budget, in order: ``PCNERF_ACT_STORE=0`` disables it; ``set_activation_store_budget(n)`` or
-    ``PCNERF_ACT_STORE_GB`` set an explicit cap; otherwise the DEFAULT is half of the HBM free at the forward
-    (driver-free + torch's cached-but-unused) after ``reserve`` bytes -- the other half stays free for whatever
-    the caller allocates between forward and backward (a drop-in under Lightning: logging, other modules).  The
-    store never takes more than free HBM minus ``reserve``; chunks beyond the budget are recomputed in the
-    backward (same gradients)."""
+    ``PCNERF_ACT_STORE_GB`` set an explicit cap; otherwise the DEFAULT is ``DEFAULT_STORE_CAP`` (32 GiB), and never
+    more than half of the HBM free at the forward (driver-free + torch's cached-but-unused) after ``reserve``
+    bytes -- the rest stays free for whatever the caller allocates between forward and backward (a drop-in under
+    Lightning: logging, other modules).  The store never takes more than free HBM minus ``reserve``; chunks beyond
+    the budget are recomputed in the backward (same gradients)."""
 
     def __init__(self, device, total_samples: int, chunk: int, reserve: int):
-        import os
         L = H.lib()
         self.per_chunk = int(L.pcnerf_nof_store_bytes(int(chunk)))
         n_chunks = -(-int(total_samples) // int(chunk))
-        budget = 0
-        if os.environ.get("PCNERF_ACT_STORE", "1") != "0" and n_chunks > 0:
-            free, _ = torch.cuda.mem_get_info(device)
-            free += torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
-            avail = max(0, free - int(reserve))
-            cap = os.environ.get("PCNERF_ACT_STORE_GB")
-            if _STORE_BUDGET is not None:
-                budget = min(avail, _STORE_BUDGET)
-            elif cap is not None:
-                budget = min(avail, int(float(cap) * (1 << 30)))
-            else:
-                budget = avail // 2
-        self.n_chunks = min(n_chunks, budget // self.per_chunk)
+        self.budget = store_budget(device, reserve) if n_chunks > 0 else 0
+        self.n_chunks = min(n_chunks, self.budget // self.per_chunk)
         self.buf = None
         while self.n_chunks > 0:
             try:

@@ -76,3 +76,32 @@ def test_math_switches_without_gpu():
     with pytest.raises(ValueError):
         _ops.set_eval_math("bf16")
     assert _ops.get_eval_math() == "f16x2_3"
+
+
+def test_activation_store_default_is_bounded(monkeypatch):
+    """The drop-in's default activation-store budget is DEFAULT_STORE_CAP (32 GiB) however much HBM is free, at most
+    half of what is free, and callers opt into more (set_activation_store_budget / PCNERF_ACT_STORE_GB)."""
+    import torch
+    from nof import _ops
+    gib = 1 << 30
+    free = {"v": 280 * gib}
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (free["v"], 288 * gib))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda dev=None: 0)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda dev=None: 0)
+    monkeypatch.delenv("PCNERF_ACT_STORE", raising=False)
+    monkeypatch.delenv("PCNERF_ACT_STORE_GB", raising=False)
+    prev = _ops.set_activation_store_budget(None)
+    try:
+        assert _ops.DEFAULT_STORE_CAP == 32 * gib
+        assert _ops.store_budget("cuda:0", 4 * gib) == 32 * gib
+        free["v"] = 40 * gib   # little free: half of what is left after the reserve
+        assert _ops.store_budget("cuda:0", 4 * gib) == 18 * gib
+        free["v"] = 280 * gib
+        monkeypatch.setenv("PCNERF_ACT_STORE_GB", "100")
+        assert _ops.store_budget("cuda:0", 4 * gib) == 100 * gib
+        _ops.set_activation_store_budget(1 << 62)   # bench.py's opt-in: everything but the reserve
+        assert _ops.store_budget("cuda:0", 4 * gib) == 276 * gib
+        monkeypatch.setenv("PCNERF_ACT_STORE", "0")
+        assert _ops.store_budget("cuda:0", 4 * gib) == 0
+    finally:
+        _ops.set_activation_store_budget(prev)
