@@ -303,6 +303,11 @@ def main(argv=None):
         tdist.destroy_process_group()
 
 
+def log(msg):
+    """Progress on stderr (a long default run keeps showing signs of life)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def add_ceiling(roof, ceiling):
     """The algorithmic fraction (fp32-equivalent FLOP of the network as written / the fp16 dense peak the split
     products run on) beside the issued-products ``frac``, and the issued rate against the measured ceiling."""
@@ -429,7 +434,9 @@ def run_line(a, L, dev, rank, world):
 
     train_math = (("fold" if a.fold else _ops.get_train_math()) if train else None)
     eval_math = None if (train or a.fold) else _ops.get_eval_math()
+    log(f"{a.mode} ({a.rays} rays, {a.samples}/{a.importance}): {a.warmup} + {a.steps} steps")
     elapsed, loss_val = timed(a.steps, a.warmup)
+    log(f"{a.mode}: {1e3 * elapsed / a.steps:.2f} ms/step")
     kstep_ms = breakdown.get("ms", 0.0)
     roof, kernels = kernel_report(L, a, train_math, eval_math)
 
@@ -474,8 +481,10 @@ def run_line(a, L, dev, rank, world):
             a.cpu_rays = 512 if view else 256 if a.config == 3 else 1024 if grad else 4096
         if a.fold:
             (_ops.set_train_fold if train else _ops.set_eval_fold)(True)
+        log(f"{a.mode}: CPU baseline on {a.cpu_rays} rays")
         cpu, ext = cpu_baseline(a, syn, sample)
         cdref = (cd_vs_ref_view if view else cd_vs_ref)(a, syn, ext, dev, sample)
+        log(f"{a.mode}: CPU baseline {cpu['value']} rays/s")
         if a.fold:
             _ops.set_train_fold(False)
             _ops.set_eval_fold(False)
