@@ -283,7 +283,10 @@ def test_render_rays(isval, eval_math):
              "same_order_rows": float(ok.mean()), "tied_rows": int(tied.sum()),
              "tied_same_order": int((ok & tied).sum())})
     assert ok.mean() >= 0.9, ok.mean()
-    np.testing.assert_array_equal(d2[ok], g["depth2"][ok])
+    rank_h = wh.argsort(dim=-1, descending=True).eq(S - 1).int().argmax(-1).numpy()
+    rank_r = wr.argsort(dim=-1, descending=True).eq(S - 1).int().argmax(-1).numpy()
+    np.testing.assert_array_equal(rank_h[ok], rank_r[ok])                  # the same sample selected, exactly
+    close(d2[ok], g["depth2"][ok], 1e-5, 1e-5, "depth2")                     # its z within z_vals' tolerance
 
 
 @pytest.mark.parametrize("order", ["stable", "cpu"])
