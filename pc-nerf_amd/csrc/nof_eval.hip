@@ -321,18 +321,12 @@ __global__ void k_pack_eval_h3(NofParamsDev P, float* __restrict__ out) {
 // hold, 14 % less weight stream per sample) -2 % / +1 % on the train query on two boxes and +7 % on the eval query
 // (profiles/r03l_variants_eval_sb7.json, _sb.json), 5: +3 % / +9 %
 constexpr int EH3_SB = 6;
-#ifndef PCN_EH3_NTSTORE
-#define PCN_EH3_NTSTORE 1   // activation-store writes nontemporal (streamed past L2, which holds the weight image):
-                            // the store-writing train query -3.8 % (profiles/r03n_variants_eval_ntstore.json)
-#endif
-#ifndef PCN_EH3_ORD_TR
-#define PCN_EH3_ORD_TR 1  // k_nof_eval_h3<true>: MFMAs of a product group neuron-block-outer (1) or sample-block-outer
-                          // (0, the eval kernel's order): -0.9 % / -1.4 % in two same-process A/Bs, bit-identical
-                          // (profiles/r03l_variants_eval_order.json, r03q_variants_eval_order_tr.json)
-#endif
-#ifndef PCN_EH3_RING
-#define PCN_EH3_RING 2    // k_nof_eval_h3: weight-ring slots (prefetch distance RING - 1 k-steps of 32); 2 or 4
-#endif
+// k_nof_eval_h3: weight-ring slots (prefetch distance EH3_RING - 1 k-steps of 32; a 4-slot ring: +7 %)
+constexpr int EH3_RING = 2;
+// The store-writing train query writes the activation store nontemporal (streamed past L2, which holds the weight
+// image): -3.8 % (profiles/r03n_variants_eval_ntstore.json).  k_nof_eval_h3<true> issues the MFMAs of a product
+// group neuron-block-outer, the eval query sample-block-outer: -0.9 % / -1.4 % and +4.2 % in same-process A/Bs,
+// bit-identical (profiles/r03l_variants_eval_order.json, r03q_variants_eval_order_tr.json).
 // Scales (eval): each layer's weights at 2^sw[L] (k_eval_wscale), each sample's B operands at the power of two
 // that puts its largest |x| in [2^14, 2^15) (eh_scale; exchanged between the waves through smax), undone by one
 // exact fma with the bias in the epilogue.
@@ -354,8 +348,8 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
                                                         float* __restrict__ p_out, const float* __restrict__ coef,
                                                         int64_t chunk, float* __restrict__ hst, int64_t hst_chunk,
                                                         int64_t hst_layer, int64_t store_chunks) {
-  constexpr int SB = EH3_SB, NS = 16 * SB, R3 = PCN_EH3_RING, D3 = R3 - 1;
-  constexpr bool ORD = TR && PCN_EH3_ORD_TR;
+  constexpr int SB = EH3_SB, NS = 16 * SB, R3 = EH3_RING, D3 = R3 - 1;
+  constexpr bool ORD = TR;
   typedef float f32x4_ __attribute__((ext_vector_type(4)));
   __shared__ eh_f16x8 act[8][SB][2][64];
   __shared__ eh_f16x8 eb[2][SB][2][64];   // the encoding's B operands at the layer-0 scale (sx0)
@@ -638,11 +632,7 @@ __global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict_
     const int sl = 16 * (int)(q & 1) + li + 32 * (g & 1);
     float* dst = hst + (int64_t)blockIdx.y * hst_chunk + (int64_t)L * hst_layer +
                  ((tile * 32 + (n0 >> 3)) * 64 + sl) * 4;
-#if PCN_EH3_NTSTORE
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4_*>(dst));
-#else
-    *reinterpret_cast<f32x4_*>(dst) = v;
-#endif
   };
   auto epi_tr = [&](int L, auto PS) __attribute__((always_inline)) {
     constexpr bool ps = decltype(PS)::value;

@@ -27,77 +27,17 @@
 
 namespace pcn {
 
-// tuning knobs (variant builds for A/B timing; defaults are the shipped configuration)
-#ifndef PCN_WS_XD_SKIP
-#define PCN_WS_XD_SKIP 2  // the same for the skip layer
-#endif
-#ifndef PCN_WS_XD
-#define PCN_WS_XD 4  // k_train_ws / k_dgrad_ws: LDS read ring depth in k-groups
-#endif
-#ifndef PCN_S12_COPIES
-#define PCN_S12_COPIES 8  // k_wgrad_reduce: copies of the BatchNorm-backward sums (block m adds to copy m % COPIES)
-#endif
-
-// k_train_h schedule (A/B knobs): ring depth of B-operand reads, k-step of the next tile's raw loads, staging
-// k-steps counted from the end, k-step of the previous tile's epilogue, static priority for waves 4-7
-#ifndef PCN_H_XD
-#define PCN_H_XD 3
-#endif
-#ifndef PCN_H_XD_SKIP
-#define PCN_H_XD_SKIP 2
-#endif
-#ifndef PCN_H_LOAD
-#define PCN_H_LOAD 2
-#endif
-#ifndef PCN_H_STAGE
-#define PCN_H_STAGE 4
-#endif
-#ifndef PCN_H_EPI
-#define PCN_H_EPI 1
-#endif
-#ifndef PCN_H_PRIO
-#define PCN_H_PRIO 1
-#endif
-#ifndef PCN_H1
-#define PCN_H1 1      // forward without activation store: layer 1 recomputes h0 from the encoding tiles
-#endif
-#ifndef PCN_H_WENC
-#define PCN_H_WENC 1  // skip layer: encoding weights in LDS, REGSTAT form
-#endif
-#ifndef PCN_H_REGSTAT
-#define PCN_H_REGSTAT 1  // hidden layers: running statistics in registers, epilogue after each tile's MFMAs
-#endif
-#ifndef PCN_INPLACE
-#define PCN_INPLACE 1   // split forward without store: layers overwrite their input buffer (one activation buffer)
-#endif
-#ifndef PCN_H1_XD
-#define PCN_H1_XD PCN_H_XD   // k_train_h1's B-operand read ring depth
-#endif
-#ifndef PCN_GRAM
-#define PCN_GRAM 1    // with PCN_H1: layer 0 as the encoding's moments (k_enc_gram) instead of its 256-neuron product
-#endif
-#ifndef PCN_H_AHEAD
-#define PCN_H_AHEAD 1  // raw activation loads 1 or 2 tiles ahead
-#endif
-// k_wgrad_b3 schedule (column blocks of a half tile)
-#ifndef PCN_WB3_AREAD
-#define PCN_WB3_AREAD 3   // column block that reads the next half tile's A values (split two blocks later)
-#endif
-#ifndef PCN_WB3_STAGE
-#define PCN_WB3_STAGE 0   // column block of the first staging piece
-#endif
-#ifndef PCN_WGRAD_H2
-#define PCN_WGRAD_H2 1    // split-math weight gradients as f16x2 (else three bf16 parts)
-#endif
-#ifndef PCN_WB3_RB
-#define PCN_WB3_RB 1      // row blocks of 32 per wave (8 / RB waves per workgroup)
-#endif
-#ifndef PCN_WB3_SGB
-#define PCN_WB3_SGB 0     // > 0: sched_group_barrier interleave with this many VALU per MFMA
-#endif
-#ifndef PCN_WB3_SPACE
-#define PCN_WB3_SPACE 2   // column blocks between staging pieces
-#endif
+// Schedule constants (each measured against its alternatives in same-process A/Bs; DESIGN.md, git history):
+constexpr int WS_XD_SKIP = 2;    // k_train_ws, skip layer: LDS read ring depth in k-groups
+constexpr int WS_XD = 4;         // k_train_ws / k_dgrad_ws: LDS read ring depth in k-groups
+constexpr int S12_COPIES = 8;    // k_wgrad_reduce: copies of the BatchNorm-backward sums (block m adds to copy m % COPIES)
+// k_train_h: ring depth of B-operand reads (hidden / skip), k-step of the next tile's raw loads, staging k-steps
+// counted from the end, k-step of the previous tile's epilogue, raw loads one tile ahead
+constexpr int H_XD = 3, H_XD_SKIP = 2, H_LOAD = 2, H_STAGE = 4, H_EPI = 1, H_AHEAD = 1;
+constexpr int H1_XD = H_XD;      // k_train_h1's B-operand read ring depth
+// k_wgrad_b3 schedule (column blocks of a half tile): the block that reads the next half tile's A values (split two
+// blocks later), the block of the first staging piece, the blocks between staging pieces
+constexpr int WB3_AREAD = 3, WB3_STAGE = 0, WB3_SPACE = 2;
 
 #ifndef PCN_CLOCK_STAMP
 #define PCN_CLOCK_STAMP 0  // diagnostic builds only: phase stamps of 1 k_train_ws, 2 k_wgrad (pcnerf_debug_clock)
@@ -199,7 +139,6 @@ __device__ __forceinline__ void bn_coeffs(const BnPrev& B, int64_t n, float mome
   }
 }
 
-constexpr int WS_XD = PCN_WS_XD;
 
 // Encoding feature group g (features 8g + 4h + q, q = 0..3) of a sample at p for lane half h: Embedding(3, 10) as
 // in encode_half (2^k * x exact, full-range sincosf), computed per feature so one thread stages one float4.
@@ -265,7 +204,7 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
   // caller runs the first layer of the chunk before its skip layer with the same buffer)
   constexpr bool ETIN = KE && HP, ETOUT = KE && !HP;
   constexpr int KGT = KE + (HP ? KG_H : 0);
-  constexpr int XD = (KE && HP) ? PCN_WS_XD_SKIP : WS_XD;   // the skip layer's 160 weight registers leave less
+  constexpr int XD = (KE && HP) ? WS_XD_SKIP : WS_XD;   // the skip layer's 160 weight registers leave less
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
   __shared__ __attribute__((aligned(16))) float bs[256];
@@ -552,7 +491,7 @@ __device__ __forceinline__ void split4(const f32x4& x, f16x4& hi, f16x4& mid) {
 
 template <int KE, bool HP, int NT>
 // hin / hout are NOT restrict-qualified: the split forward without activation store runs every layer in place
-// (hin == hout, query_train's PCN_INPLACE)
+// (hin == hout, query_train's in-place forward)
 __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ rays, int stride,
                                                     const float* __restrict__ z, int S, int64_t c0,
                                                     const float* __restrict__ ein, const float* hin,
@@ -564,17 +503,17 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   constexpr bool ETIN = KE && HP, ETOUT = KE && !HP;
   constexpr int KSE = KE ? KS_E : 0;               // encoding k-steps
   constexpr int KS = KSE + (HP ? KS_H : 0);        // k-steps of 16 features
-  constexpr int XD = (KE && HP) ? PCN_H_XD_SKIP : PCN_H_XD;   // LDS read ring depth in k-steps
+  constexpr int XD = (KE && HP) ? H_XD_SKIP : H_XD;   // LDS read ring depth in k-steps
   // HP: the next tile's raw loads, their staging (BatchNorm + split + LDS), the previous tile's epilogue
-  constexpr int S_LOAD = PCN_H_LOAD, S_STAGE0 = KS - PCN_H_STAGE, S_STAGE1 = S_STAGE0 + 1;
-  constexpr int S_EPI = PCN_H_EPI;
-  constexpr int AHEAD = (KE && HP) ? 1 : PCN_H_AHEAD;   // the skip layer's weight registers leave no room
+  constexpr int S_LOAD = H_LOAD, S_STAGE0 = KS - H_STAGE, S_STAGE1 = S_STAGE0 + 1;
+  constexpr int S_EPI = H_EPI;
+  constexpr int AHEAD = (KE && HP) ? 1 : H_AHEAD;   // the skip layer's weight registers leave no room
   // REGSTAT: each tile's epilogue right after its MFMAs, the per-lane running statistics in registers (no LDS
   // read-modify-write per tile, one accumulator set); the B buffers double as the final reduction area
   // WENC (skip layer): the encoding k-steps' weights live in LDS, read two k-steps ahead, instead of 32 registers --
   // which lets the skip layer take the REGSTAT form as well
-  constexpr bool WENC = KE && HP && PCN_H_WENC;
-  constexpr bool REGSTAT = HP && (!KE || WENC) && PCN_H_REGSTAT;
+  constexpr bool WENC = KE && HP;   // skip layer: encoding weights in LDS
+  constexpr bool REGSTAT = HP;      // running statistics in registers, epilogue after each tile's MFMAs
   // NWL: k-steps whose weights come from LDS (two k-steps ahead) -- the skip layer's encoding k-steps (WENC)
   constexpr int NWL = WENC ? KSE : 0;
   constexpr int NBUF = 2;
@@ -624,7 +563,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
   // staging identity: the HBM lane (sample ls + 32 hs) whose float4s this thread stages
   const int sln = lane, ls = sln & 31, hs = sln >> 5;
   const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH two-waves item 4
+  if (blk >= 4) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH two-waves item 4
   f16x8 wr[KS][2];
   {
     const f16x8* __restrict__ w8 = Wp + lane;
@@ -919,7 +858,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
                                                      const float* __restrict__ bias, BnPrev prev, float momentum,
                                                      float eps, float* __restrict__ hout,
                                                      double* __restrict__ stats) {
-  constexpr int KS = KS_H, XD = PCN_H1_XD;
+  constexpr int KS = KS_H, XD = H1_XD;
   constexpr int S_ELOAD = 2, S_EPUT = KS - 4;
   __shared__ __attribute__((aligned(16))) float al[256];
   __shared__ __attribute__((aligned(16))) float be[256];
@@ -962,7 +901,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
   auto P = [&](int x) { return rev ? nt - 1 - x : x; };
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
   const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);
+  if (blk >= 4) __builtin_amdgcn_s_setprio(1);
   f16x8 wr[KS][2];
   {
     const f16x8* __restrict__ w8 = W1p + lane;
@@ -1128,10 +1067,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h1(const f32x4* __restrict__ e
 //   k_gram_stats  ebar, Sigma and the 256 neurons' sums in float64 -> BatchNorm 0's statistics (bn_coeffs' input).
 // The 256-neuron product of the first layer (99 us per chunk of 262,144, VALU-bound) becomes a 64 x 64 one.
 constexpr int GR_P = 72;          // LDS pitch (halves): 16 lanes' 16-byte operand reads hit disjoint bank groups
-#ifndef PCN_GR_BLOCKS
-#define PCN_GR_BLOCKS 512
-#endif
-constexpr int GR_BLOCKS = PCN_GR_BLOCKS;    // k_enc_gram workgroups per chunk (two per CU)
+constexpr int GR_BLOCKS = 512;    // k_enc_gram workgroups per chunk (two per CU)
 constexpr int GR_PART = 3072;     // doubles per partial: blocks 00, 01, 11 as [block][register 16][lane 64]
 constexpr size_t GR_DOUBLES = (size_t)(GR_BLOCKS + 1) * GR_PART + 64;
 
@@ -1483,17 +1419,9 @@ struct TrainLayerLaunch {
   hipStream_t s;
 };
 
-// Tile order of the split train layers: bit L of the mask reverses layer L's walk over its chunk (default: the
-// odd hidden layers, so each hidden layer first reads the tiles its predecessor wrote last); PCNERF_TILE_REV
-// overrides it (A/B runs).
-static int tile_rev(int L) {
-  static int mask = -1;
-  if (mask < 0) {
-    const char* e = getenv("PCNERF_TILE_REV");
-    mask = e ? (int)strtol(e, nullptr, 0) : 0xAA;
-  }
-  return (mask >> L) & 1;
-}
+// Tile order of the split train layers: the odd hidden layers walk their chunk backwards, so each hidden layer
+// first reads the tiles its predecessor wrote last.
+static int tile_rev(int L) { return (0xAA >> L) & 1; }
 
 template <int KE, bool HP>
 static void launch_layer(const TrainLayerLaunch& q, const NofParamsDev& P, const float* wp, const f16x8* wh,
@@ -1643,13 +1571,13 @@ static void query_train(const float* rays, int ray_stride, const float* z, int n
     const f32x4* enc_of_chunk = nullptr;
     // split math, nothing kept for a backward: layer 0 statistics-only, layer 1 recomputes h0 from the encoding
     // tiles (k_train_h1)
-    const bool h1 = PCN_H1 && !keep && g_train_math != 0;
-    if (!(h1 && PCN_GRAM)) PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));   // (else k_gram_stats)
-    // PCN_INPLACE: every layer of the chunk overwrites its input tile by tile (a tile is read only by the workgroup
+    const bool h1 = !keep && g_train_math != 0;
+    if (!h1) PCN_HIP(hipMemsetAsync(stats, 0, 8 * 512 * sizeof(double), s));   // (else k_gram_stats)
+    // in place: every layer of the chunk overwrites its input tile by tile (a tile is read only by the workgroup
     // that writes its output, which staged it before its MFMAs): one 268 MB footprint instead of two.  k_train_h
     // declares hin / hout without __restrict__ for this; k_train_h1 reads the encoding tiles, not hin.
-    if (h1 && PCN_INPLACE) hout = hin;
-    if (h1 && PCN_GRAM) {
+    if (h1) hout = hin;
+    if (h1) {
       // algorithmic: the 64 x 64 moment product per sample; 4 B of z in, 256 B of encoding out
       ProfScope ps(s, PT_TRAIN_FIRST, 2.0 * 64 * 64 * dn, (4.0 + 256.0) * dn);
       const int64_t nu = (n + 63) / 64;
@@ -1770,9 +1698,6 @@ constexpr size_t DGRAD_W_FLOATS = 7 * SZ_H;
 constexpr int GMAX_SLOTS = 64;                     // per layer: atomicMax targets of the |dL/dh| maxima
 constexpr int GMAX_DBL = 8 * GMAX_SLOTS / 2;       // their doubles in the per-chunk s12 region
 constexpr int WG_BLOCKS = 256;  // weight-gradient partials per chunk (one 8-wave block per CU)
-#ifndef PCN_WB3_L0X2
-#define PCN_WB3_L0X2 1             // layer 0's encoding-column weight gradient at two workgroups per CU
-#endif
 
 __host__ __device__ constexpr int in_features(int L) { return L == 0 ? 63 : L == 4 ? 319 : 256; }
 
@@ -2135,7 +2060,7 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__
     const size_t wi = (size_t)m * in_f + wcol_h + nn;
     dW[wi] += (double)coefp[512 + nn] * G + (double)coefp[768 + nn] * dbm;
     const double w = (double)W[wi];
-    double* s12c = s12 + (m % PCN_S12_COPIES) * 512;   // 256 / COPIES blocks per address instead of 256
+    double* s12c = s12 + (m % S12_COPIES) * 512;   // 256 / COPIES blocks per address instead of 256
     atomicAdd(&s12c[2 * nn], w * dbm);
     atomicAdd(&s12c[2 * nn + 1], w * G);
   }
@@ -2164,7 +2089,7 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_ws(
     const int k = t;
     double S1 = 0.0, dotp = 0.0;
 #pragma unroll
-    for (int c = 0; c < PCN_S12_COPIES; ++c) {
+    for (int c = 0; c < S12_COPIES; ++c) {
       S1 += s12[512 * c + 2 * k];
       dotp += s12[512 * c + 2 * k + 1];
     }
@@ -2327,9 +2252,9 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
     const double* __restrict__ s12, const float* __restrict__ coefp, const float* __restrict__ gamma,
     double* __restrict__ d_gamma, double* __restrict__ d_beta, float* __restrict__ gout,
     float* __restrict__ tmax_out, unsigned* __restrict__ gmax_out) {
-  constexpr int KS = KS_H, XD = PCN_H_XD;
+  constexpr int KS = KS_H, XD = H_XD;
   float gm = 0.0f;   // the wave's largest |dL/dh_{L-1}| over its tiles (k_wgrad_b3's chunk-wide scale)
-  constexpr int S_LOAD = PCN_H_LOAD, S_STAGE0 = KS - PCN_H_STAGE, S_STAGE1 = S_STAGE0 + 1, S_HX = 8;
+  constexpr int S_LOAD = H_LOAD, S_STAGE0 = KS - H_STAGE, S_STAGE1 = S_STAGE0 + 1, S_HX = 8;
   __shared__ __attribute__((aligned(16))) float cgm[256];
   __shared__ __attribute__((aligned(16))) float ckk[256];
   __shared__ __attribute__((aligned(16))) float cmu[256];
@@ -2341,7 +2266,7 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
     const int k = t;
     double S1 = 0.0, dotp = 0.0;
 #pragma unroll
-    for (int c = 0; c < PCN_S12_COPIES; ++c) {
+    for (int c = 0; c < S12_COPIES; ++c) {
       S1 += s12[512 * c + 2 * k];
       dotp += s12[512 * c + 2 * k + 1];
     }
@@ -2361,7 +2286,7 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
   const int gstride = (int)gridDim.x;
   const int lane = t & 63, h = lane >> 5, li = lane & 31;
   const int blk = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (PCN_H_PRIO && blk >= 4) __builtin_amdgcn_s_setprio(1);
+  if (blk >= 4) __builtin_amdgcn_s_setprio(1);
   f16x8 wr[KS][2];
   {
     const f16x8* __restrict__ w8 = Wt + lane;
@@ -2792,9 +2717,9 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     }
   if (2 < nh) load_half(rv, tile_of(2), 0);
   __syncthreads();
-  constexpr int S_PD = NBLK / NP < PCN_WB3_SPACE ? NBLK / NP : PCN_WB3_SPACE;
-  constexpr int S_P0 = PCN_WB3_STAGE + (NP - 1) * S_PD < NBLK ? PCN_WB3_STAGE : 0;
-  constexpr int S_APF = PCN_WB3_AREAD < NBLK ? PCN_WB3_AREAD : NBLK - 1;
+  constexpr int S_PD = NBLK / NP < WB3_SPACE ? NBLK / NP : WB3_SPACE;
+  constexpr int S_P0 = WB3_STAGE + (NP - 1) * S_PD < NBLK ? WB3_STAGE : 0;
+  constexpr int S_APF = WB3_AREAD < NBLK ? WB3_AREAD : NBLK - 1;
   constexpr int S_ASP = S_APF + 2 < NBLK ? S_APF + 2 : NBLK - 1;
   P8 Acur[RB][NPART], Anext[RB][NPART], B[2][NPART];
   if (nh > 0) {
@@ -2905,7 +2830,7 @@ static GaccLayout gacc_layout() {
   return G;
 }
 
-constexpr int S12_LAYER = PCN_S12_COPIES * 512;
+constexpr int S12_LAYER = S12_COPIES * 512;
 
 struct BwdWs {
   float* h[8];
@@ -2989,7 +2914,7 @@ template <int MODE, int LAY, bool H2, int NTP>
 static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                                 int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
                                 const float* mu, const unsigned* gmax, float* part) {
-  constexpr int RB = MODE == 0 ? PCN_WB3_RB : 1;
+  constexpr int RB = 1;
   using Cfg = Wb3Cfg<MODE, H2>;
   constexpr size_t lds = 3 * Cfg::BUF + (H2 ? 2 * Cfg::NBLK * 32 * sizeof(float) : 0);
   static_assert(lds <= 160 * 1024, "LDS");
@@ -3003,20 +2928,17 @@ static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* ray
                      c0, ein, gin, hprev, mu, n, gmax, part);
 }
 
-// the weight-gradient partials of k_wgrad<MODE> under the split train math: f16x2 (PCN_WGRAD_H2, with the
-// forward's product count) or three bf16 parts
+// the weight-gradient partials of k_wgrad<MODE> under the split train math: f16x2 with the forward's product count
 template <int MODE>
 static void launch_wgrad_b3(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                             int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
                             const float* mu, const unsigned* gmax, float* part) {
   auto one = [&](auto mode, auto lay) {
     constexpr int M = decltype(mode)::value, LY = decltype(lay)::value;
-    if (PCN_WGRAD_H2 && g_train_math == 1)
+    if (g_train_math == 1)
       launch_wgrad_b3_one<M, LY, true, 3>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
-    else if (PCN_WGRAD_H2)
-      launch_wgrad_b3_one<M, LY, true, 4>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
     else
-      launch_wgrad_b3_one<M, LY, false, 3>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
+      launch_wgrad_b3_one<M, LY, true, 4>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
   };
   if constexpr (MODE != 1) one(std::integral_constant<int, 0>{}, std::integral_constant<int, MODE>{});
   if constexpr (MODE != 0) one(std::integral_constant<int, 1>{}, std::integral_constant<int, MODE>{});
@@ -3147,12 +3069,12 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       }
       cur ^= 1;
     }
-    // 4. layer 0 on the encoding.  Under the split math at TWO workgroups per CU (PCN_WB3_L0X2): the
+    // 4. layer 0 on the encoding.  Under the split math at TWO workgroups per CU: the
     // encoding-column launch is latency-bound on its sincosf staging at one 8-wave workgroup per CU, and its
     // 127 VGPRs and 66 KiB of LDS let a second one share the CU (its partials: 2 x WG_BLOCKS slots of k_wgrad<1>'s
     // layout, within the buffer sized for WG_BLOCKS of k_wgrad<2>'s)
     static_assert(2 * WG_BLOCKS * WgradCfg<1>::PART <= WG_BLOCKS * WgradCfg<2>::PART, "layer-0 partial slots");
-    const unsigned wb0 = (split && PCN_WB3_L0X2) ? (unsigned)std::min<int64_t>(2 * ntiles, 2 * WG_BLOCKS) : wblocks;
+    const unsigned wb0 = split ? (unsigned)std::min<int64_t>(2 * ntiles, 2 * WG_BLOCKS) : wblocks;
     {
       ProfScope ps(s, split ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
       if (split)
