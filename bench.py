@@ -588,7 +588,8 @@ def kernel_report(L, a, train_math, eval_math=None):
               3: f"k_train_h<8,true,{nterm}>" if split else "k_train_ws<8,true>",
               10: "k_wgrad<2>+k_wgrad<1>" if split else "k_wgrad<0>", 11: f"k_dgrad_h<{nterm}>" if split else "k_dgrad_ws",
               13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>",
-              16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw", 18: "k_nof_eval_h3<true>"}
+              16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw", 18: "k_nof_eval_h3<true>",
+              19: "k_bwd_fused<0>"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
@@ -597,7 +598,8 @@ def kernel_report(L, a, train_math, eval_math=None):
     for t, nm in ((0, "eval_query"), (1, "train_hidden"), (2, "train_first"), (3, "train_skip"), (4, "train_out"),
                   (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
                   (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold"), (14, "wgrad_b3"),
-                  (15, "train_h1"), (16, "fold_moments"), (17, "fold_algebra"), (18, "train_query")):
+                  (15, "train_h1"), (16, "fold_moments"), (17, "fold_algebra"), (18, "train_query"),
+                  (19, "bwd_fused")):
         tm, n, f, b = prof_read(L, t)
         if n:
             tr, src = pmc_traffic(pmc_names.get(t, ""))
@@ -627,7 +629,7 @@ def kernel_report(L, a, train_math, eval_math=None):
                 "unit": "TFLOP/s", "frac": round(nprod * achieved / FP16_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                 "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1),
                 "products_per_fp32_product": nprod, "fp32_equivalent_TFLOPs": round(achieved, 2)}
-    elif split and tag in (1, 2, 3, 11, 14, 15):
+    elif split and tag in (1, 2, 3, 11, 14, 15, 19):
         # split-fp16 layer: nterm fp16 MFMA products per fp32 product; 1 KiB in + 1 KiB out per sample: the
         # HBM stream (2 KiB/sample) is the tighter of its two roofs
         roof = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

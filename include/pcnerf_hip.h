@@ -177,11 +177,23 @@ int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stri
                                  void* state, size_t state_bytes, float* p_out, void* stream);
 /* The same query writing chunks 0..store_chunks-1 into an activation store (pcnerf_nof_store_bytes(chunk) bytes per
  * chunk, the layout pcnerf_nof_query_train_store writes: raw layer outputs W_L x and BatchNorm sums) for
- * pcnerf_nof_query_train_backward_store. */
+ * pcnerf_nof_query_train_backward_fused (or _store).  Here `state` is pcnerf_nof_train_fold_bytes(total_samples,
+ * chunk) bytes and must stay untouched until that backward: it holds the chunks' encoding moments and layer maps. */
 int pcnerf_nof_query_train_fused_store(const float* rays, int64_t n_rays, int ray_stride, const float* z,
                                        int n_samples, int64_t chunk, const pcnerf_nof_params* params, float momentum,
                                        float eps, void* state, size_t state_bytes, float* p_out, void* store,
                                        int64_t store_chunks, void* stream);
+/* The training backward after pcnerf_nof_query_train_fused_store (the autograd of render.py:47-50 / models.py:183-203
+ * in train_kitti.py:155's loss.backward(), as pcnerf_nof_query_train_backward): `state` is that forward's state.
+ * Each stored chunk's layers run ONE pass each (data gradient, BatchNorm backward and weight gradient together,
+ * g_{L-1} written over h_{L-1} in the store, which the call consumes); the BatchNorm-backward statistics per chunk
+ * come from the state (the chunk's encoding and gradient moments, float64).  Chunks beyond store_chunks are
+ * recomputed and take the two-pass backward.  Gradients are ADDED to `grads`. */
+int pcnerf_nof_query_train_backward_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                          int n_samples, int64_t chunk, const pcnerf_nof_params* params, float eps,
+                                          const float* grad_logit, void* state, size_t state_bytes, void* workspace,
+                                          size_t workspace_bytes, const pcnerf_nof_grads* grads, const void* store,
+                                          int64_t store_chunks, void* stream);
 /* NOF.forward(emb) in train mode on an embedded batch of n rows (one chunk), the same way. */
 int pcnerf_nof_forward_train_fused(const float* emb, int64_t n, const pcnerf_nof_params* params, float momentum,
                                    float eps, void* state, size_t state_bytes, float* p_out, void* stream);

@@ -59,9 +59,10 @@ struct FoldDev {   // device views of the fold state (float64 throughout)
   double* vec;     // [C][576] d out_w (256), d beta_7 (256), d out_b (1)
   float* coef;     // [C][TQ_COEF_FLOATS] the chunks' BatchNorm coefficients and operand scales (train-mode query)
   float* img;      // the train-mode query's weight image (train_query_image_floats)
+  double* oacc;    // [C][257] sum_s g_s (h_7 - mean_7) and sum_s g_s (the per-sample backward's occ_out statistics)
 };
 
-constexpr int FOLD_PIECES = 15;
+constexpr int FOLD_PIECES = 16;
 struct FoldLayout {
   int64_t C;
   int wpc, G;
@@ -82,7 +83,7 @@ static FoldLayout fold_layout(int64_t total, int64_t chunk, bool fwd_only = fals
   const size_t n[FOLD_PIECES] = {C * wpc * 4096, C * 4096, C * 64, C * 64, 8 * C * 256 * 64, 8 * C * 256 * 64,
                                  8 * C * 1024, b * C * 64, b * C * wpc * 64, b * 2 * C * 256 * 64, b * 8 * C * 256,
                                  b * G * 256 * 256, b * C * 576, C * TQ_COEF_FLOATS / 2,
-                                 (train_query_image_floats() + 1) / 2};
+                                 (train_query_image_floats() + 1) / 2, b * C * 257};
   size_t o = 0;
   for (int i = 0; i < FOLD_PIECES; ++i) {
     F.off[i] = o;
@@ -102,6 +103,7 @@ static FoldDev fold_dev(const FoldLayout& L, void* state) {
   for (int i = 0; i < 13; ++i) *dst[i] = b + L.off[i];
   F.coef = (float*)(b + L.off[13]);
   F.img = (float*)(b + L.off[14]);
+  F.oacc = b + L.off[15];
   return F;
 }
 
@@ -636,6 +638,10 @@ __global__ __launch_bounds__(256) void k_tf_bwd_out(NofParamsDev P, FoldDev F) {
     if (i == 0) v[512] = gb;
     const double ds = w * dot[tid];
     F.dg[(7 * C + c) * 256 + i] = ds * rinv;
+    if (F.oacc) {   // sum_s g_s (h_7 - mean_7)_i and sum_s g_s, for the per-sample backward (nof_train.hip)
+      F.oacc[c * 257 + i] = dot[tid];
+      if (i == 0) F.oacc[c * 257 + 256] = gb;
+    }
     dvv[tid] = -0.5 * ds * gam * rinv * rinv * rinv;
     coef[tid] = s7 * w;
   }
@@ -848,7 +854,8 @@ static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, f
   PCN_CHECK(q.total > 0 && q.chunk > 0, "train query: empty input");
   // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
   PCN_CHECK(q.total % q.chunk != 1 && q.total != 1, "Expected more than 1 value per channel when training");
-  const FoldLayout Lo = fold_layout(q.total, q.chunk, true);
+  // with an activation store the state is the backward's too (fold_bn_backward): the full layout
+  const FoldLayout Lo = fold_layout(q.total, q.chunk, store == nullptr);
   PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train query: state buffer too small");
   PCN_CHECK(Lo.C < 65536, "train query: too many chunks for one query");
   NofParamsDev P;
@@ -920,6 +927,34 @@ static void fold_backward(const SampleSrc& q, const pcnerf_nof_params* params, f
   backward_layer<1>(P, F, G, s);
   backward_layer<0>(P, F, G, s);
   hipLaunchKernelGGL(k_tf_vec_reduce, dim3(10), dim3(256), 0, s, F, *G);
+}
+
+// The per-sample training backward's BatchNorm statistics (nof_train.hip, backward_train with a fold state): the
+// state the store-writing fused forward left (full layout), the gradient moments of g_logit, and the fold's layer
+// algebra down to every BatchNorm's dgamma per chunk (Sigma_s dL/dy (h - mean) / sqrt(var + eps)) and the occ_out
+// statistics -- no weight gradient (the per-sample passes compute those as written).
+FoldBnBwd fold_bn_backward(const float* rays, int stride, const float* z, int S, int64_t total, int64_t chunk,
+                           const NofParamsDev& P, const float* g_logit, void* state, size_t state_bytes,
+                           hipStream_t s) {
+  const SampleSrc q{rays, stride, z, S, nullptr, total, std::min(chunk, total)};
+  const FoldLayout Lo = fold_layout(q.total, q.chunk);
+  PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train backward: fold state buffer too small");
+  const FoldDev F = fold_dev(Lo, state);
+  {
+    ProfScope ps(s, PT_FOLD_MOMENTS, 126.0 * (double)q.total, 8.0 * (double)q.total);
+    hipLaunchKernelGGL(k_tf_gmoments, dim3(F.wpc, (unsigned)F.C), dim3(256), 0, s, q, F, g_logit,
+                       (const float*)nullptr);
+  }
+  ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
+  hipLaunchKernelGGL(k_tf_bwd_out, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer<7>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer<6>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer<5>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer<4>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer<3>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer<2>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer<1>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  return FoldBnBwd{F.dg, F.sr, F.oacc, F.C};
 }
 
 }  // namespace pcn

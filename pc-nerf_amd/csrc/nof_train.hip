@@ -1525,12 +1525,17 @@ __global__ __launch_bounds__(256) void k_pos_bound(const float* __restrict__ ray
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-static void check_split_range(const float* rays, int stride, const float* z, int S, const float* ein, int64_t total,
-                              unsigned* dev, hipStream_t s, const char* who) {
-  if (g_train_math == 0) return;   // fp32 MFMA: no fp16 operand
+static void pos_bound_async(const float* rays, int stride, const float* z, int S, const float* ein, int64_t total,
+                            unsigned* dev, hipStream_t s) {
   PCN_HIP(hipMemsetAsync(dev, 0, sizeof(unsigned), s));
   const int64_t blocks = std::min<int64_t>(2048, (total + 255) / 256);
   hipLaunchKernelGGL(k_pos_bound, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, S, ein, total, dev);
+}
+
+static void check_split_range(const float* rays, int stride, const float* z, int S, const float* ein, int64_t total,
+                              unsigned* dev, hipStream_t s, const char* who) {
+  if (g_train_math == 0) return;   // fp32 MFMA: no fp16 operand
+  pos_bound_async(rays, stride, z, S, ein, total, dev, s);
   unsigned h = 0;
   PCN_HIP(hipMemcpyAsync(&h, dev, sizeof(unsigned), hipMemcpyDeviceToHost, s));
   PCN_HIP(hipStreamSynchronize(s));
@@ -1801,7 +1806,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
                                                       double* __restrict__ d_gamma, double* __restrict__ d_beta,
                                                       double* __restrict__ d_wout, double* __restrict__ d_bout,
                                                       float* __restrict__ gout, float* __restrict__ tmax,
-                                                      unsigned* __restrict__ gmax) {
+                                                      unsigned* __restrict__ gmax, int ncopies) {
   __shared__ __attribute__((aligned(16))) float cgm[256];
   __shared__ __attribute__((aligned(16))) float ckk[256];
   __shared__ __attribute__((aligned(16))) float cmu[256];
@@ -1812,7 +1817,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
     const int k = threadIdx.x;
     double A = 0.0, G0 = 0.0;
 #pragma unroll
-    for (int c = 0; c < OSTAT_COPIES; ++c) {   // k_out_bwd_stats1's copies
+    for (int c = 0; c < ncopies; ++c) {   // k_out_bwd_stats1's copies (or the fold's one)
       A += acc[257 * c + k];
       G0 += acc[257 * c + 256];
     }
@@ -2020,7 +2025,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__ part, int nblk, const float* __restrict__ W,
                                const float* __restrict__ coefp, double* __restrict__ dW, double* __restrict__ db,
-                               double* __restrict__ s12) {
+                               double* __restrict__ s12, int nblk_e) {
   using Cfg = WgradCfg<MODE>;
   constexpr int C = Cfg::C;
   constexpr int SPLIT = Cfg::SPLIT;
@@ -2039,7 +2044,8 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__
   // 8 independent loads in flight per thread (the sum is latency-bound otherwise)
   double Gp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   const float* pc = part + (size_t)m * C + t;
-  const int b0 = sl * ((nblk + SPLIT - 1) / SPLIT), b1 = min(nblk, b0 + (nblk + SPLIT - 1) / SPLIT);
+  const int nbc = (Cfg::EX && t < 64) ? nblk_e : nblk;   // the encoding columns' own partial count (MODE 2)
+  const int b0 = sl * ((nbc + SPLIT - 1) / SPLIT), b1 = min(nbc, b0 + (nbc + SPLIT - 1) / SPLIT);
   int b = b0;
   for (; b + 8 <= b1; b += 8) {
 #pragma unroll
@@ -2501,7 +2507,8 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
                                                           const float* __restrict__ hprev,
                                                           const float* __restrict__ mu, int64_t n,
                                                           const unsigned* __restrict__ gmax,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part,
+                                                          const unsigned* __restrict__ pbound) {
   using Cfg = Wb3Cfg<MODE, H2>;
   constexpr int NPART = Cfg::NPART;
   constexpr bool HX = Cfg::HX, EX = Cfg::EX;
@@ -2519,7 +2526,13 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     for (int c = t; c < NBLK * 32; c += 512 / RB) {
       int e;
       if (EX && c < 64) {
-        e = (c >= 3 && c < 63) ? 14 : 0;   // |sin|, |cos| <= 1; xyz unscaled
+        // |sin|, |cos| <= 1; xyz by the call's largest |position| (k_pos_bound, on the device: no host sync)
+        e = (c >= 3 && c < 63) ? 14 : 0;
+        if (c < 3 && pbound) {
+          const float pm = __uint_as_float(*pbound);
+          e = (pm > 0.0f && pm < 3.0e38f) ? 14 - ilogbf(pm) : 0;
+          e = e < -60 ? -60 : e > 60 ? 60 : e;
+        }
       } else {
         const float invstd = mu[256 + (c - HOFF)];
         const float bnd = sqrtf((float)n) / invstd;   // Samuelson: |h - mean| <= sqrt(n) sigma
@@ -2793,6 +2806,300 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   }
 }
 
+// ---- k_bwd_fused: one layer's backward over a chunk of stored tiles in ONE pass -- the data gradient with the
+// BatchNorm backward below it AND the weight gradient (5 -> 3 KiB of HBM per sample and layer).
+// What used to force two passes is the chunk-wide statistics of BatchNorm L-1's backward, Sigma_s dL/dy and
+// Sigma_s dL/dy (h - mean), which the weight-gradient GEMM's result gave; here they come before the backward from
+// the fused forward's fold state (fold_bn_backward: exact float64 functions of the chunk's encoding and gradient
+// moments -- the premise, identity activations, the forward's statistics already rest on), so each tile's
+//   dy = W_L^T g_L  (data gradient)   ->   g_{L-1} = ((dy - mean dy) - (h - mean) kk) invstd gamma
+// is final in the tile's epilogue, and G_L += g_L (x) (h_{L-1} - mean) (weight gradient) uses the same operands.
+//
+// Work split: the 256 input features i of layer L in two halves; a PAIR of workgroups (blocks b and b + 8: the same
+// XCD, so the second read of a g tile is an L2 hit) takes the same tiles, each computing its half of dy and of G's
+// columns -- W^T for 16 features per wave stays in 64 registers and G's 32 x 128 slice per wave in 64, which two
+// waves per SIMD can hold.  8 waves; per 32-sample tile and wave: 48 v_mfma_f32_16x16x32_f16 of data gradient (its
+// 16 features x 2 sample blocks, 8 k-steps of 32 neurons, 3 products) + 48 of weight gradient (2 x 8 blocks of
+// 16 x 16 over the tile's 32 samples, 3 products).  Operands in LDS per tile (double-buffered, one barrier a tile):
+// g_L scaled by its chunk-wide 2^sg (the producer's gmax) and h - mean per column by 2^sx (Samuelson), each split
+// into fp16 hi + mid, stored [sample][feature] with 16-byte chunks swizzled by row (fb_off): conflict-free for the
+// data gradient's 16-byte reads (8 neurons of a sample) and the weight gradient's transposed ds_read_b64_tr_b16
+// reads (8 samples of a feature).  g_{L-1} is written in place over h_{L-1} (each workgroup reads exactly the
+// columns it writes); the weight-gradient partial per pair in k_wgrad<LAY>'s layout (k_wgrad_reduce sums them).
+constexpr int FB_GP = 512, FB_XP = 256;                   // g / x part row bytes (256 / 128 halves)
+constexpr int FB_GPART = 32 * FB_GP, FB_XPART = 32 * FB_XP;
+constexpr int FB_BUF = 2 * FB_GPART + 2 * FB_XPART;       // 48 KiB per tile
+constexpr int FB_PAIRS = 128;
+constexpr size_t FB_LDS = 2 * (size_t)FB_BUF + 6 * 128 * sizeof(float);
+
+__device__ __forceinline__ int fb_swz(int r) { return 2 * ((r & 3) | ((r & 8) >> 1)); }
+template <int P>
+__device__ __forceinline__ int fb_off(int r, int c) {   // 16-bit element c of row r
+  return r * P + 16 * ((c >> 3) ^ fb_swz(r)) + 2 * (c & 7);
+}
+__device__ __forceinline__ s16x4 fb_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(__attribute__((address_space(3))) void*)(p));
+}
+
+// W_L^T image for k_bwd_fused: layer L (1..7) at (L-1) HW_H, [ks 8][input block 16][part 2][lane 64] f16x8: row
+// i = 16 iblk + (lane & 15) (input feature of layer L, the skip layer's h columns), k = neuron 32 ks + 8 (lane >> 4)
+// + e; scaled by 2^sw[L] like the forward
+__global__ void k_pack_dgrad_h16(NofParamsDev P, const int* __restrict__ sw, f16x8* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 7 * HW_H) return;
+  const int L = 1 + (int)(idx / HW_H);
+  const size_t j = idx % HW_H;
+  const int lane = (int)(j & 63), part = (int)((j >> 6) & 1), ib = (int)((j >> 7) & 15), ks = (int)(j >> 11);
+  const int i = 16 * ib + (lane & 15), in_f = in_features(L), col = (L == 4 ? 63 : 0) + i;
+  const float sc = ldexpf(1.0f, sw[L]);
+  f16x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 32 * ks + 8 * (lane >> 4) + e;
+    const float w = P.lin_w[L][(size_t)k * in_f + col] * sc;
+    const _Float16 hi = (_Float16)w;
+    v[e] = part == 0 ? hi : (_Float16)(w - (float)hi);
+  }
+  out[idx] = v;
+}
+
+// BatchNorm k's backward constants for a chunk, k = 0..6 (grid 7 x 256 threads): mean(dL/dy) = 0 (exactly: dL/dy =
+// W_{k+1}^T g_{k+1} and g_{k+1} is a BatchNorm backward's output, zero-mean over the chunk), and
+// kk = Sigma dL/dy (h - mean) invstd^2 / n with Sigma dL/dy (h - mean) = dgamma / fl64(1/sqrt(var+eps)) from the fold
+// -- k_dgrad_h's ckk arithmetic on it; dgamma_k += that sum x invstd (k_dgrad_h's d_gamma), dbeta_k += 0.
+struct GammaOff {
+  int64_t g[8];
+};
+__global__ void k_fb_bnb(FoldBnBwd F, int64_t c, int64_t n, const float* __restrict__ coef,
+                         float* __restrict__ bnb, double* __restrict__ gacc, GammaOff go) {
+  const int k = blockIdx.x, i = threadIdx.x;
+  const double rinv = F.sr[((int64_t)k * F.C + c) * 1024 + 256 + i];
+  const double dotp = F.dg[((int64_t)k * F.C + c) * 256 + i] / rinv;
+  const float invstd = coef[1024 * k + 256 + i];
+  bnb[512 * k + i] = 0.0f;
+  bnb[512 * k + 256 + i] = (((float)dotp * invstd) * invstd) / (float)n;
+  gacc[go.g[k] + i] += dotp * (double)invstd;
+}
+
+template <int LAY>
+__global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ gin, float* hio,
+                                                       const f16x8* __restrict__ wt, const int* __restrict__ sw,
+                                                       int layer, int64_t n, const float* __restrict__ coefp,
+                                                       const float* __restrict__ bnb,
+                                                       const float* __restrict__ gamma,
+                                                       const unsigned* __restrict__ gmax_in,
+                                                       unsigned* __restrict__ gmax_out, float* __restrict__ part) {
+  constexpr int C = WgradCfg<LAY>::C, COL = LAY == 2 ? 64 : 0;
+  extern __shared__ __attribute__((aligned(16))) char fb[];
+  float* const cst = reinterpret_cast<float*>(fb + 2 * FB_BUF);   // [csc | cun | gm | kk | invstd | gamma][128]
+  const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int bid = (int)blockIdx.x, hf = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
+  const int npair = (int)gridDim.x >> 1;
+  const int nt = (int)((n + 31) / 32);
+  if (t < 128) {
+    const int c = 128 * hf + t;
+    const float invstd = coefp[256 + c];
+    const float bnd = sqrtf((float)n) / invstd;   // Samuelson: |h - mean| <= sqrt(n) sigma
+    int e = (bnd > 0.0f && bnd < 3.0e38f) ? 14 - ilogbf(bnd) : 0;
+    e = e < -60 ? -60 : e > 60 ? 60 : e;
+    cst[t] = ldexpf(1.0f, e);
+    cst[128 + t] = ldexpf(1.0f, -e);
+    cst[256 + t] = bnb[c];
+    cst[384 + t] = bnb[256 + c];
+    cst[512 + t] = invstd;
+    cst[640 + t] = gamma[c];
+  }
+  unsigned gmx = 0;
+  for (int i = 0; i < GMAX_SLOTS; ++i) gmx = max(gmx, gmax_in[i]);   // (uniform loads)
+  const int eg = tile_scale_exp(__uint_as_float(gmx));
+  const float gsc = ldexpf(1.0f, eg), gun = ldexpf(1.0f, -eg);
+  const float dun = ldexpf(1.0f, -sw[layer]) * gun;   // data-gradient accumulator -> dL/dy
+  // this wave's W^T rows: input features 128 hf + 16 wv + (lane & 15), all 8 k-steps, hi / mid
+  f16x8 wr[8][2];
+  {
+    const f16x8* __restrict__ w8 = wt + lane;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 16 + 8 * hf + wv) * 2 + p) * 64];
+  }
+  // staging map: g float4 t + 512 m (m < 4): feature group (t >> 6) + 8 m, sample (t & 31), half (t >> 5) & 1;
+  // x float4 t + 512 m (m < 2) of this half: group 16 hf + (t >> 6) + 8 m
+  const int ss = t & 31, sh = (t >> 5) & 1, sg0 = t >> 6;
+  f32x4 mu2[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+    mu2[m] = *reinterpret_cast<const f32x4*>(coefp + 8 * (16 * hf + sg0 + 8 * m) + 4 * sh);
+  __syncthreads();
+  f32x4 csc2[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) csc2[m] = *reinterpret_cast<const f32x4*>(cst + 8 * (sg0 + 8 * m) + 4 * sh);
+  f32x4 rg[4], rx[2];
+  auto load_tile = [&](int tl) {
+    const f32x4* g4 = reinterpret_cast<const f32x4*>(gin + (size_t)tl * TILE_FLOATS);
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(hio + (size_t)tl * TILE_FLOATS) + 1024 * hf;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) rg[m] = g4[t + 512 * m];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) rx[m] = x4[t + 512 * m];
+  };
+  auto stage = [&](int bb, int tl) {
+    char* gb = fb + (size_t)bb * FB_BUF;
+    char* xb = gb + 2 * FB_GPART;
+    const bool valid = (int64_t)tl * 32 + ss < n;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      f32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = valid ? rg[m][q] * gsc : 0.0f;
+      s16x4 p0, p1;
+      split2_x4(v, p0, p1);
+      const int o = fb_off<FB_GP>(ss, 8 * (sg0 + 8 * m) + 4 * sh);
+      *reinterpret_cast<s16x4*>(gb + o) = p0;
+      *reinterpret_cast<s16x4*>(gb + FB_GPART + o) = p1;
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      f32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = valid ? (rx[m][q] - mu2[m][q]) * csc2[m][q] : 0.0f;
+      s16x4 p0, p1;
+      split2_x4(v, p0, p1);
+      const int o = fb_off<FB_XP>(ss, 8 * (sg0 + 8 * m) + 4 * sh);
+      *reinterpret_cast<s16x4*>(xb + o) = p0;
+      *reinterpret_cast<s16x4*>(xb + FB_XPART + o) = p1;
+    }
+  };
+  f32x4 aw[2][8];
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+    for (int ib = 0; ib < 8; ++ib) aw[jb][ib] = f32x4{};
+  float dbacc[2] = {0.0f, 0.0f};
+  float gmo = 0.0f;
+  // transposed reads: lane lm = 4 q + pp of 16-lane group kg supplies sample row 8 kg + q (+ 4), columns + 4 pp
+  const int trq = lm >> 2, trp = lm & 3;
+  int tl = pr;
+  if (tl < nt) {
+    load_tile(tl);
+    stage(0, tl);
+  }
+  __syncthreads();
+  int bb = 0;
+  while (tl < nt) {
+    const int nxt = tl + npair;
+    if (nxt < nt) load_tile(nxt);
+    const char* gb = fb + (size_t)bb * FB_BUF;
+    const char* xb = gb + 2 * FB_GPART;
+    // data gradient: this wave's 16 input features x 32 samples
+    f32x4 ad[2] = {f32x4{}, f32x4{}};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int o = fb_off<FB_GP>(16 * sb + lm, 32 * ks + 8 * kg);
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(gb + o);
+        const f16x8 bm = *reinterpret_cast<const f16x8*>(gb + FB_GPART + o);
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bh, ad[sb], 0, 0, 0);
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bm, ad[sb], 0, 0, 0);
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], bh, ad[sb], 0, 0, 0);
+      }
+    }
+    // weight gradient: rows j = 32 wv + 16 jb + lm, the tile's 32 samples, 8 column blocks of this half
+    f16x8 A[2][2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const char* pb = gb + p * FB_GPART;
+        const int col = 32 * wv + 16 * jb + 4 * trp;
+        const s16x4 v0 = fb_tr(pb + fb_off<FB_GP>(8 * kg + trq, col));
+        const s16x4 v1 = fb_tr(pb + fb_off<FB_GP>(8 * kg + 4 + trq, col));
+        A[jb][p] = __builtin_bit_cast(f16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    if (hf == 0) {
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dbacc[jb] += (float)A[jb][0][e] + (float)A[jb][1][e];
+    }
+#pragma unroll
+    for (int ib = 0; ib < 8; ++ib) {
+      f16x8 B[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const char* pb = xb + p * FB_XPART;
+        const int col = 16 * ib + 4 * trp;
+        const s16x4 v0 = fb_tr(pb + fb_off<FB_XP>(8 * kg + trq, col));
+        const s16x4 v1 = fb_tr(pb + fb_off<FB_XP>(8 * kg + 4 + trq, col));
+        B[p] = __builtin_bit_cast(f16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B[0], aw[jb][ib], 0, 0, 0);
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B[1], aw[jb][ib], 0, 0, 0);
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B[0], aw[jb][ib], 0, 0, 0);
+      }
+    }
+    // epilogue: dL/dy -> BatchNorm L-1 backward -> g_{L-1} over this tile's h_{L-1} (input features
+    // 128 hf + 16 wv + 4 kg .. + 3 of sample 16 sb + lm)
+    {
+      const int il = 16 * wv + 4 * kg;   // column within the half
+      const f32x4 cun = *reinterpret_cast<const f32x4*>(cst + 128 + il);
+      const f32x4 cgm = *reinterpret_cast<const f32x4*>(cst + 256 + il);
+      const f32x4 ckk = *reinterpret_cast<const f32x4*>(cst + 384 + il);
+      const f32x4 cis = *reinterpret_cast<const f32x4*>(cst + 512 + il);
+      const f32x4 cga = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+      const int i = 128 * hf + il;
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int sm = 16 * sb + lm;
+        const bool valid = (int64_t)tl * 32 + sm < n;
+        const int o = fb_off<FB_XP>(sm, il);
+        const f16x4 xh = *reinterpret_cast<const f16x4*>(xb + o);
+        const f16x4 xm = *reinterpret_cast<const f16x4*>(xb + FB_XPART + o);
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float d = ad[sb][q] * dun;
+          const float xc = ((float)xh[q] + (float)xm[q]) * cun[q];   // h - mean (hi + mid: 22 bits)
+          v[q] = valid ? ((d - cgm[q]) - xc * ckk[q]) * cis[q] * cga[q] : 0.0f;
+          gmo = fmaxf(gmo, fabsf(v[q]));
+        }
+        reinterpret_cast<f32x4*>(hio + (size_t)tl * TILE_FLOATS)[(i >> 3) * 64 + sm + 32 * ((i >> 2) & 1)] = v;
+      }
+    }
+    if (nxt < nt) stage(bb ^ 1, nxt);
+    __syncthreads();
+    bb ^= 1;
+    tl = nxt;
+  }
+  gmo = wave_max_f(gmo);
+  if (lane == 0) atomicMax(gmax_out + ((bid * 8 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
+  // G partial of pair pr: rows j = 32 wv + 16 jb + 4 kg + r, columns 128 hf + 16 ib + lm (x scale undone per column)
+  float* pb = part + (size_t)pr * WgradCfg<LAY>::PART;
+#pragma unroll
+  for (int ib = 0; ib < 8; ++ib) {
+    const float cu = cst[128 + 16 * ib + lm] * gun;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pb[(size_t)(32 * wv + 16 * jb + 4 * kg + r) * C + COL + 128 * hf + 16 * ib + lm] = aw[jb][ib][r] * cu;
+  }
+  if (hf == 0) {
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      float d = dbacc[jb];
+      d += __shfl_xor(d, 16, 64);
+      d += __shfl_xor(d, 32, 64);
+      if (kg == 0) pb[(size_t)256 * C + 32 * wv + 16 * jb + lm] = d * gun;
+    }
+  }
+}
+
 struct GradTable {
   float* dst[34];
   int64_t off[34];
@@ -2850,6 +3157,8 @@ struct BwdWs {
   float* tmax[2];   // per-tile max |dL/dh| of g[0] / g[1] ([tile][8])
   unsigned* gmax;   // per layer L: GMAX_SLOTS partial maxima of the chunk's |dL/dh_L| (float bits; zeroed per chunk)
   unsigned* pbound;   // k_pos_bound's result (float bits)
+  f16x8* wth16;       // W^T image of k_bwd_fused (7 layers)
+  float* bnb;         // BatchNorm 0..6 backward constants of the chunk (k_fb_bnb)
   size_t bytes;
 };
 
@@ -2872,6 +3181,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t owt = take(7 * HW_H * sizeof(f16x8));
   const size_t otm0 = take(tiles * 8 * sizeof(float)), otm1 = take(tiles * 8 * sizeof(float));
   const size_t opb = take(sizeof(unsigned));
+  const size_t owt16 = take(7 * HW_H * sizeof(f16x8)), obnb = take(7 * 512 * sizeof(float));
   char* b = (char*)base;
   BwdWs w;
   w.wth = (f16x8*)(b + owt);
@@ -2892,6 +3202,8 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.gacc = (double*)(b + oa);
   w.enc = (f32x4*)(b + oenc);
   w.pbound = (unsigned*)(b + opb);
+  w.wth16 = (f16x8*)(b + owt16);
+  w.bnb = (float*)(b + obnb);
   w.bytes = off;
   return w;
 }
@@ -2913,7 +3225,7 @@ static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int 
 template <int MODE, int LAY, bool H2, int NTP>
 static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                                 int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
-                                const float* mu, const unsigned* gmax, float* part) {
+                                const float* mu, const unsigned* gmax, float* part, const unsigned* pbound) {
   constexpr int RB = 1;
   using Cfg = Wb3Cfg<MODE, H2>;
   constexpr size_t lds = 3 * Cfg::BUF + (H2 ? 2 * Cfg::NBLK * 32 * sizeof(float) : 0);
@@ -2925,41 +3237,125 @@ static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* ray
     attr = true;
   }
   hipLaunchKernelGGL((k_wgrad_b3<RB, MODE, LAY, H2, NTP>), dim3(blocks), dim3(512 / RB), lds, s, rays, stride, z, S,
-                     c0, ein, gin, hprev, mu, n, gmax, part);
+                     c0, ein, gin, hprev, mu, n, gmax, part, pbound);
 }
 
 // the weight-gradient partials of k_wgrad<MODE> under the split train math: f16x2 with the forward's product count
 template <int MODE>
 static void launch_wgrad_b3(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                             int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
-                            const float* mu, const unsigned* gmax, float* part) {
+                            const float* mu, const unsigned* gmax, float* part, const unsigned* pbound,
+                            bool h_cols = true, bool e_cols = true) {
   auto one = [&](auto mode, auto lay) {
     constexpr int M = decltype(mode)::value, LY = decltype(lay)::value;
     if (g_train_math == 1)
-      launch_wgrad_b3_one<M, LY, true, 3>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
+      launch_wgrad_b3_one<M, LY, true, 3>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part,
+                                          pbound);
     else
-      launch_wgrad_b3_one<M, LY, true, 4>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part);
+      launch_wgrad_b3_one<M, LY, true, 4>(blocks, s, rays, stride, z, S, c0, n, ein, gin, hprev, mu, gmax, part,
+                                          pbound);
   };
-  if constexpr (MODE != 1) one(std::integral_constant<int, 0>{}, std::integral_constant<int, MODE>{});
-  if constexpr (MODE != 0) one(std::integral_constant<int, 1>{}, std::integral_constant<int, MODE>{});
+  if constexpr (MODE != 1) if (h_cols) one(std::integral_constant<int, 0>{}, std::integral_constant<int, MODE>{});
+  if constexpr (MODE != 0) if (e_cols) one(std::integral_constant<int, 1>{}, std::integral_constant<int, MODE>{});
 }
 
 }  // namespace pcn
 
 extern "C" size_t pcnerf_nof_backward_workspace_bytes(int64_t chunk) { return carve_bwd(nullptr, chunk).bytes; }
 
+// One stored chunk through the one-pass backward: BatchNorm coefficients from the chunk's stored statistics, the
+// BatchNorm-backward constants from the fold (k_fb_bnb), occ_out + BatchNorm 7 (k_out_bwd_grad on the fold's occ_out
+// statistics: no statistics pass), then layers 7..1 each in ONE k_bwd_fused launch (g_{L-1} in place over
+// h_{L-1}) + the partial reduction, the skip layer's and layer 0's encoding columns (k_wgrad_b3 MODE 1 on g_4 and
+// g_0, which stay in their store slots).
+static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs& ws, const FoldBnBwd& FB, int64_t ci,
+                        int64_t c0, int64_t n, const double* stats, float* const (&hh)[8], const float* rays,
+                        int ray_stride, const float* z, int n_samples, const float* ein, float eps, const float* grad,
+                        hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)FB_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)FB_LDS));
+    attr = true;
+  }
+  const double dn = (double)n;
+  const int64_t ntiles = (n + 31) / 32;
+  const unsigned wblocks = (unsigned)(ntiles < WG_BLOCKS ? ntiles : WG_BLOCKS);
+  const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
+  {
+    ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
+    hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
+    GammaOff go;
+    for (int L = 0; L < 8; ++L) go.g[L] = G.g[L];
+    hipLaunchKernelGGL(k_fb_bnb, dim3(7), dim3(256), 0, s, FB, ci, n, ws.coef, ws.bnb, ws.gacc, go);
+    PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257 + GMAX_DBL) * sizeof(double), s));
+    hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, (const float*)nullptr, hh[7], n,
+                       ws.coef + 7 * 1024, P.bn_w[7], P.out_w, FB.oacc + ci * 257, ws.gacc + G.g[7],
+                       ws.gacc + G.be[7], ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0], (float*)nullptr,
+                       ws.gmax + 7 * GMAX_SLOTS, 1);
+  }
+  const unsigned fbg = (unsigned)(2 * FB_PAIRS);
+  for (int L = 7; L >= 1; --L) {
+    const float* coefp = ws.coef + 1024 * (L - 1);
+    const float* gin = L == 7 ? ws.g[0] : hh[L];
+    {
+      ProfScope ps(s, PT_BWD_FUSED, 2.0 * 2.0 * 256.0 * 256.0 * dn, 3072.0 * dn);
+      if (L == 4)
+        hipLaunchKernelGGL(k_bwd_fused<2>, dim3(fbg), dim3(512), FB_LDS, s, gin, hh[L - 1],
+                           ws.wth16 + (size_t)(L - 1) * HW_H, ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1),
+                           P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS, ws.gmax + (L - 1) * GMAX_SLOTS, ws.part);
+      else
+        hipLaunchKernelGGL(k_bwd_fused<0>, dim3(fbg), dim3(512), FB_LDS, s, gin, hh[L - 1],
+                           ws.wth16 + (size_t)(L - 1) * HW_H, ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1),
+                           P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS, ws.gmax + (L - 1) * GMAX_SLOTS, ws.part);
+    }
+    if (L == 4) {   // the skip layer's encoding columns on g_4 (its store slot), into the same partials
+      ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
+      launch_wgrad_b3<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[4], hh[3], coefp,
+                         ws.gmax + 4 * GMAX_SLOTS, ws.part, ws.pbound, false, true);
+    }
+    ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0);
+    if (L == 4)
+      hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[4],
+                         coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + S12_LAYER * L, (int)wblocks);
+    else
+      hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[L],
+                         coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12 + S12_LAYER * L, FB_PAIRS);
+  }
+  // layer 0 on the encoding (g_0 in its store slot), two workgroups per CU
+  const unsigned wb0 = (unsigned)std::min<int64_t>(2 * ntiles, 2 * WG_BLOCKS);
+  {
+    ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
+    launch_wgrad_b3<1>(wb0, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[0], nullptr, nullptr,
+                       ws.gmax + 0 * GMAX_SLOTS, ws.part, ws.pbound);
+  }
+  ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wb0 * WgradCfg<1>::PART * 4.0);
+  hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)wb0, P.lin_w[0],
+                     (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr, (int)wb0);
+}
+
 static void backward_train(const float* rays, int ray_stride, const float* z, int n_samples, const float* ein,
                            int64_t total, int64_t chunk, const pcnerf_nof_params* params, float eps,
                            const float* grad, const float* p, void* workspace, size_t workspace_bytes,
                            const pcnerf_nof_grads* grads, hipStream_t s, const void* store = nullptr,
-                           int64_t store_chunks = 0) {
+                           int64_t store_chunks = 0, void* fstate = nullptr, size_t fstate_bytes = 0) {
   const BwdWs ws = carve_bwd(workspace, chunk);
   PCN_CHECK(workspace_bytes >= ws.bytes, "pcnerf_nof_backward: workspace too small");
   NofParamsDev P;
   PCN_CHECK(to_dev_params(params, eps, &P), "pcnerf_nof_backward: null parameter pointer");
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   const GaccLayout G = gacc_layout();
-  check_split_range(rays, ray_stride, z, n_samples, ein, total, ws.pbound, s, "pcnerf_nof_backward");
+  const int64_t n_chunks = (total + chunk - 1) / chunk;
+  // the one-pass backward (k_bwd_fused) on the chunks the fused forward stored, under the split math of the fused
+  // forward (f16x2, 3 products); every other chunk (recomputed) and every other math: the two-pass backward
+  const bool fused = fstate && store && g_train_math == 1;
+  const bool recompute = !store || store_chunks < n_chunks || !fused;
+  // the encoding operand's xyz columns are scaled by the largest |position| (device-side, k_pos_bound); the
+  // layered forward that recomputes chunks splits them unscaled and needs the host-side range check
+  if (recompute) check_split_range(rays, ray_stride, z, n_samples, ein, total, ws.pbound, s, "pcnerf_nof_backward");
+  else pos_bound_async(rays, ray_stride, z, n_samples, ein, total, ws.pbound, s);
   hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wp);
   const bool split = g_train_math != 0;
   if (split) {   // the forward's arithmetic for recomputation, and k_dgrad_h's W^T image
@@ -2968,6 +3364,12 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
   }
   hipLaunchKernelGGL(k_pack_dgrad, dim3((unsigned)((DGRAD_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, ws.wt);
   PCN_HIP(hipMemsetAsync(ws.gacc, 0, (size_t)G.total * 8, s));
+  FoldBnBwd FB{};
+  if (fused) {
+    hipLaunchKernelGGL(k_pack_dgrad_h16, dim3((unsigned)((7 * HW_H + 255) / 256)), dim3(256), 0, s, P, ws.sw,
+                       ws.wth16);
+    FB = fold_bn_backward(rays, ray_stride, z, n_samples, total, chunk, P, grad, fstate, fstate_bytes, s);
+  }
   const float mom = 0.0f;  // unused: the recomputation passes no running stats
   for (int64_t c0 = 0; c0 < total; c0 += chunk) {
     const int64_t n = total - c0 < chunk ? total - c0 : chunk;
@@ -2983,6 +3385,10 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     float* hh[8];
     for (int L = 0; L < 8; ++L) hh[L] = kept ? sc.h[L] : ws.h[L];
     const double* stats = kept ? sc.stats : ws.stats;
+    if (kept && fused) {
+      fused_chunk(P, G, ws, FB, ci, c0, n, stats, hh, rays, ray_stride, z, n_samples, ein, eps, grad, s);
+      continue;
+    }
     if (!kept) PCN_HIP(hipMemsetAsync(ws.stats, 0, 8 * 512 * sizeof(double), s));
     const f32x4* enc_of_chunk = nullptr;   // written by this chunk's recomputed first layer, read by its skip layer
     if (!kept) {
@@ -3020,7 +3426,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, p ? p + c0 : nullptr, hh[7], n,
                          ws.coef + 7 * 1024, P.bn_w[7], P.out_w, ws.ostat, ws.gacc + G.g[7], ws.gacc + G.be[7],
                          ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0], split ? ws.tmax[0] : nullptr,
-                         split ? ws.gmax + 7 * GMAX_SLOTS : nullptr);
+                         split ? ws.gmax + 7 * GMAX_SLOTS : nullptr, OSTAT_COPIES);
     }
     // 3. layers 7..1
     int cur = 0;
@@ -3031,10 +3437,10 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
                      2048.0 * dn);
         if (split && L == 4)
           launch_wgrad_b3<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp,
-                             ws.gmax + L * GMAX_SLOTS, ws.part);
+                             ws.gmax + L * GMAX_SLOTS, ws.part, ws.pbound);
         else if (split)
           launch_wgrad_b3<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
-                             ws.gmax + L * GMAX_SLOTS, ws.part);
+                             ws.gmax + L * GMAX_SLOTS, ws.part, ws.pbound);
         else if (L == 4)
           launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
         else
@@ -3045,10 +3451,10 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
         ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wblocks * WgradCfg<0>::PART * 4.0);
         if (L == 4)
           hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::RT), 0, s, ws.part, (int)wblocks,
-                             P.lin_w[4], coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + S12_LAYER * L);
+                             P.lin_w[4], coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + S12_LAYER * L, (int)wblocks);
         else
           hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::RT), 0, s, ws.part, (int)wblocks,
-                             P.lin_w[L], coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12 + S12_LAYER * L);
+                             P.lin_w[L], coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12 + S12_LAYER * L, (int)wblocks);
       }
       {
         ProfScope ps(s, PT_BWD_DGRAD, 2.0 * 256 * 256 * dn, 3072.0 * dn);
@@ -3079,7 +3485,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
       ProfScope ps(s, split ? PT_BWD_WGRAD_H : PT_BWD_WGRAD, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
       if (split)
         launch_wgrad_b3<1>(wb0, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
-                           ws.gmax + 0 * GMAX_SLOTS, ws.part);
+                           ws.gmax + 0 * GMAX_SLOTS, ws.part, ws.pbound);
       else
         launch_wgrad<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
                         ws.part);
@@ -3087,7 +3493,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     {
       ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wb0 * WgradCfg<1>::PART * 4.0);
       hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)wb0,
-                         P.lin_w[0], (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr);
+                         P.lin_w[0], (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr, (int)wb0);
     }
   }
   GradTable T;
@@ -3118,6 +3524,25 @@ extern "C" int pcnerf_nof_query_train_backward_store(const float* rays, int64_t 
   PCN_CHECK(store_chunks == 0 || store, "pcnerf_nof_query_train_backward_store: store_chunks > 0 needs a store");
   backward_train(rays, ray_stride, z, n_samples, nullptr, n_rays * (int64_t)n_samples, chunk, params, eps,
                  grad_logit, nullptr, workspace, workspace_bytes, grads, (hipStream_t)stream, store, store_chunks);
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_query_train_backward_fused(const float* rays, int64_t n_rays, int ray_stride,
+                                                     const float* z, int n_samples, int64_t chunk,
+                                                     const pcnerf_nof_params* params, float eps,
+                                                     const float* grad_logit, void* state, size_t state_bytes,
+                                                     void* workspace, size_t workspace_bytes,
+                                                     const pcnerf_nof_grads* grads, const void* store,
+                                                     int64_t store_chunks, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && grad_logit && state && workspace && grads,
+            "pcnerf_nof_query_train_backward_fused: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_backward_fused: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_backward_fused: ray_stride < 6");
+  PCN_CHECK(store_chunks == 0 || store, "pcnerf_nof_query_train_backward_fused: store_chunks > 0 needs a store");
+  backward_train(rays, ray_stride, z, n_samples, nullptr, n_rays * (int64_t)n_samples, chunk, params, eps,
+                 grad_logit, nullptr, workspace, workspace_bytes, grads, (hipStream_t)stream, store, store_chunks,
+                 state, state_bytes);
   PCN_API_END
 }
 

@@ -44,6 +44,19 @@ void launch_train_query(const float* rays, int stride, const float* z, int64_t t
                         float* hst = nullptr, int64_t hst_chunk = 0, int64_t hst_layer = 0,
                         int64_t store_chunks = 0);
 
+// The per-sample training backward's BatchNorm statistics from the fused forward's fold state (nof_fold.hip):
+// dg [8][C][256] each BatchNorm's dgamma per chunk, sr [8][C][1024] (s, 1/sqrt(var+eps), mean, var per layer and
+// chunk), oacc [C][257] (sum_s g_s (h_7 - mean_7), sum_s g_s).
+struct FoldBnBwd {
+  const double* dg;
+  const double* sr;
+  const double* oacc;
+  int64_t C;
+};
+FoldBnBwd fold_bn_backward(const float* rays, int stride, const float* z, int S, int64_t total, int64_t chunk,
+                           const NofParamsDev& P, const float* g_logit, void* state, size_t state_bytes,
+                           hipStream_t s);
+
 // p = o + d*z, one rounding per op (render.py:458; built with -ffp-contract=off).
 __device__ __forceinline__ void sample_point(const float* __restrict__ r, float z, float (&p)[3]) {
   p[0] = r[0] + r[3] * z;

@@ -24,6 +24,7 @@ enum ProfTag {
   PT_FOLD_MOMENTS = 16,// train fold: k_tf_moments / k_tf_gmoments (per-sample encoding moments)
   PT_FOLD_ALGEBRA = 17,// train fold: the per-chunk float64 layer algebra (forward or backward)
   PT_TRAIN_QUERY = 18, // k_nof_eval_h3<true>: the fused train-mode query (per-chunk BatchNorm coefficients)
+  PT_BWD_FUSED = 19,   // k_bwd_fused: one layer's data + weight gradient in one pass (stored chunks)
 };
 extern bool g_prof_on;
 class ProfScope {

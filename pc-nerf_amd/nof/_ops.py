@@ -243,13 +243,15 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
         chunk = max(1, min(int(chunk), R * S))
         mom, eps = _bn_config(model)
         s, keep = _params(model)
-        ws = _workspace(z.device, int(L.pcnerf_nof_train_fused_bytes(R * S, chunk)))
         if store is not None and store.n_chunks > 0:
+            # the state (the chunks' encoding moments and layer maps) is the backward's too: kept with the store
+            store.fstate = fold_state(z.device, R * S, chunk)
             H.check(L.pcnerf_nof_query_train_fused_store(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S,
-                                                         int(chunk), ctypes.byref(s), mom, eps, ws.data_ptr(),
-                                                         ws.numel(), p.data_ptr(), store.buf.data_ptr(),
-                                                         store.n_chunks, st))
+                                                         int(chunk), ctypes.byref(s), mom, eps,
+                                                         store.fstate.data_ptr(), store.fstate.numel(), p.data_ptr(),
+                                                         store.buf.data_ptr(), store.n_chunks, st))
         else:
+            ws = _workspace(z.device, int(L.pcnerf_nof_train_fused_bytes(R * S, chunk)))
             H.check(L.pcnerf_nof_query_train_fused(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
                                                    ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(),
                                                    p.data_ptr(), st))
@@ -657,6 +659,7 @@ class ActivationStore:
         self.budget = store_budget(device, reserve) if n_chunks > 0 else 0
         self.n_chunks = min(n_chunks, self.budget // self.per_chunk)
         self.buf = None
+        self.fstate = None   # the fused forward's state (query), read by the one-pass backward
         while self.n_chunks > 0:
             try:
                 self.buf = torch.empty((self.n_chunks * self.per_chunk,), dtype=torch.uint8, device=device)
@@ -666,6 +669,7 @@ class ActivationStore:
 
     def release(self):
         self.buf = None
+        self.fstate = None
         self.n_chunks = 0
 
 
@@ -678,7 +682,15 @@ def nof_query_backward(model, rays, z, chunk: int, g_logit, store=None) -> list:
     s, keep = _params(model)
     gs, out = _grads_struct(model, z.device)
     ws = _workspace(z.device, L.pcnerf_nof_backward_workspace_bytes(int(chunk)))
-    if store is not None and store.n_chunks > 0:
+    fstate = getattr(store, "fstate", None) if store is not None else None
+    if store is not None and store.n_chunks > 0 and fstate is not None:
+        # the fused forward's store: one pass per layer (pcnerf_nof_query_train_backward_fused)
+        H.check(L.pcnerf_nof_query_train_backward_fused(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S,
+                                                        int(chunk), ctypes.byref(s), eps, _f32(g_logit).data_ptr(),
+                                                        fstate.data_ptr(), fstate.numel(), ws.data_ptr(), ws.numel(),
+                                                        ctypes.byref(gs), store.buf.data_ptr(), store.n_chunks,
+                                                        _stream(z)))
+    elif store is not None and store.n_chunks > 0:
         H.check(L.pcnerf_nof_query_train_backward_store(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S,
                                                         int(chunk), ctypes.byref(s), eps, _f32(g_logit).data_ptr(),
                                                         ws.data_ptr(), ws.numel(), ctypes.byref(gs),

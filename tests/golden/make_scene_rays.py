@@ -13,6 +13,7 @@ bit for bit before rendering.
 
 Stored (small subsets, the rest is rebuilt on the GPU):
   kitti_train  (4096, 15)  a seeded batch of the train split (DataLoader(shuffle=True) analogue), with its indices;
+  kitti_train_all          the whole train split (config 3 draws its 262,144-ray batch from it with replacement);
   kitti_val    (N, 15)     the whole val split;
   maicity_b{0..3}          up to 1024 rows of each of 4 parent blocks (MaiCity bounds [-12,61] split in x), with
                            the block bounds and each block's child count;
@@ -119,6 +120,7 @@ def main():
         k, n_children = kitti_rays(os.path.join(tmp, "kitti"))
         idx = np.random.default_rng(0).permutation(len(k["train"]))[:4096]
         out.update(kitti_train=k["train"][idx], kitti_train_idx=idx, kitti_train_total=len(k["train"]),
+                   kitti_train_all=k["train"],
                    kitti_val=k["val"], kitti_children=n_children)
         for b, (lo, hi, rows, nc) in enumerate(maicity_blocks(os.path.join(tmp, "maicity"))):
             out[f"maicity_b{b}"] = rows[:1024]
