@@ -1860,10 +1860,10 @@ __global__ __launch_bounds__(256) void k_out_bwd_grad(const float* __restrict__ 
       }
       o4[gq * 64] = o;
     }
-    if (tmax) {   // the tile's largest |dL/dh_7| (k_dgrad_h's operand scale), one wave per tile
+    if (tmax || gmax) {   // the tile's largest |dL/dh_7| (k_dgrad_h's per-tile operand scale) and the chunk's
       float mx = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
       mx = wave_max_f(mx);
-      if (lane < 8) tmax[tile * 8 + lane] = mx;
+      if (tmax && lane < 8) tmax[tile * 8 + lane] = mx;
       gm = fmaxf(gm, mx);
     }
   }
