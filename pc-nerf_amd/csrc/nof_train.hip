@@ -16,6 +16,7 @@
 // (the tile's float4 itself), D (reg r, lane l) = out[neuron 32b + (r&3) + 8(r>>2) + 4(l>>5)][sample l&31], so
 // registers 4j..4j+3 are the output tile's float4 at group 4b+j.  feature(t, h) = 8(t>>2) + 4h + (t&3).
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -2830,16 +2831,30 @@ constexpr int FB_GP = 512, FB_XP = 256;                   // g / x part row byte
 constexpr int FB_GPART = 32 * FB_GP, FB_XPART = 32 * FB_XP;
 constexpr int FB_BUF = 2 * FB_GPART + 2 * FB_XPART;       // 48 KiB per tile
 constexpr int FB_PAIRS = 128;
-constexpr size_t FB_LDS = 2 * (size_t)FB_BUF + 6 * 128 * sizeof(float);
+constexpr size_t FB_LDS = 3 * (size_t)FB_BUF + 7 * 128 * sizeof(float);   // split + 2 raw tiles + constants
 
 __device__ __forceinline__ int fb_swz(int r) { return 2 * ((r & 3) | ((r & 8) >> 1)); }
 template <int P>
 __device__ __forceinline__ int fb_off(int r, int c) {   // 16-bit element c of row r
   return r * P + 16 * ((c >> 3) ^ fb_swz(r)) + 2 * (c & 7);
 }
-__device__ __forceinline__ s16x4 fb_tr(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)(__attribute__((address_space(3))) void*)(p));
+// ds_read_b64_tr_b16 of four 16-bit elements at p (LDS) + OFF.  Inline asm: hipcc waits vmcnt(0) before every
+// ds_read_tr16 builtin while an LDS-DMA is in flight (it cannot tell the DMA's destination from the read's), which
+// would drain k_bwd_fused's two-tiles-ahead prefetch.  The compiler does not count these reads: the caller waits
+// lgkmcnt before using the result (fb_lgkm).
+typedef int fb_i32x2 __attribute__((ext_vector_type(2)));
+template <int OFF>
+__device__ __forceinline__ s16x4 fb_tr(unsigned addr) {
+  fb_i32x2 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return __builtin_bit_cast(s16x4, r);
+}
+template <int N>
+__device__ __forceinline__ void fb_lgkm() {   // s_waitcnt lgkmcnt(N)
+  __builtin_amdgcn_s_waitcnt(0xC07F & ~0x0F00 | (N << 8));
+}
+__device__ __forceinline__ unsigned fb_lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
 // W_L^T image for k_bwd_fused: layer L (1..7) at (L-1) HW_H, [ks 8][input block 16][part 2][lane 64] f16x8: row
@@ -2882,6 +2897,11 @@ __global__ void k_fb_bnb(FoldBnBwd F, int64_t c, int64_t n, const float* __restr
   gacc[go.g[k] + i] += dotp * (double)invstd;
 }
 
+__device__ __forceinline__ void fb_glds16(const void* g, void* l) {   // 16 B per lane -> l + 16 lane (LDS-DMA)
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
 template <int LAY>
 __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ gin, float* hio,
                                                        const f16x8* __restrict__ wt, const int* __restrict__ sw,
@@ -2892,12 +2912,14 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
                                                        unsigned* __restrict__ gmax_out, float* __restrict__ part) {
   constexpr int C = WgradCfg<LAY>::C, COL = LAY == 2 ? 64 : 0;
   extern __shared__ __attribute__((aligned(16))) char fb[];
-  float* const cst = reinterpret_cast<float*>(fb + 2 * FB_BUF);   // [csc | cun | gm | kk | invstd | gamma][128]
+  char* const sp = fb;                                              // the split operands of the current tile
+  float* const cst = reinterpret_cast<float*>(fb + 3 * FB_BUF);     // [csc | cun | gm | kk | invstd | gamma | mu][128]
   const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int bid = (int)blockIdx.x, hf = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
   const int npair = (int)gridDim.x >> 1;
   const int nt = (int)((n + 31) / 32);
+  const int nk = pr < nt ? (nt - 1 - pr) / npair + 1 : 0;   // this pair's tiles: pr + k npair, k < nk
   if (t < 128) {
     const int c = 128 * hf + t;
     const float invstd = coefp[256 + c];
@@ -2910,6 +2932,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     cst[384 + t] = bnb[256 + c];
     cst[512 + t] = invstd;
     cst[640 + t] = gamma[c];
+    cst[768 + t] = coefp[c];
   }
   unsigned gmx = 0;
   for (int i = 0; i < GMAX_SLOTS; ++i) gmx = max(gmx, gmax_in[i]);   // (uniform loads)
@@ -2925,51 +2948,51 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
 #pragma unroll
       for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 16 + 8 * hf + wv) * 2 + p) * 64];
   }
-  // staging map: g float4 t + 512 m (m < 4): feature group (t >> 6) + 8 m, sample (t & 31), half (t >> 5) & 1;
-  // x float4 t + 512 m (m < 2) of this half: group 16 hf + (t >> 6) + 8 m
-  const int ss = t & 31, sh = (t >> 5) & 1, sg0 = t >> 6;
-  f32x4 mu2[2];
+  // Raw tiles by LDS-DMA, two ahead: raw buffer k & 1 holds the pair's tile k as it lies in HBM -- 32 rows (feature
+  // groups) of 1 KiB of g_L, then the 16 rows of this half's h_{L-1}.  Wave w moves rows w + 8 m and later splits
+  // exactly those rows (thread t: row (t >> 6) + 8 m, HBM lane t & 63), so a wave waits only for its own DMA.
+  auto issue_raw = [&](int k) {
+    const int tl = pr + k * npair;
+    char* rb = fb + (size_t)(1 + (k & 1)) * FB_BUF;
+    const float* gsrc = gin + (size_t)tl * TILE_FLOATS + lane * 4;
+    const float* xsrc = hio + (size_t)tl * TILE_FLOATS + 16 * hf * 256 + lane * 4;
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-    mu2[m] = *reinterpret_cast<const f32x4*>(coefp + 8 * (16 * hf + sg0 + 8 * m) + 4 * sh);
-  __syncthreads();
-  f32x4 csc2[2];
+    for (int m = 0; m < 4; ++m) fb_glds16(gsrc + (wv + 8 * m) * 256, rb + (wv + 8 * m) * 1024);
 #pragma unroll
-  for (int m = 0; m < 2; ++m) csc2[m] = *reinterpret_cast<const f32x4*>(cst + 8 * (sg0 + 8 * m) + 4 * sh);
-  f32x4 rg[4], rx[2];
-  auto load_tile = [&](int tl) {
-    const f32x4* g4 = reinterpret_cast<const f32x4*>(gin + (size_t)tl * TILE_FLOATS);
-    const f32x4* x4 = reinterpret_cast<const f32x4*>(hio + (size_t)tl * TILE_FLOATS) + 1024 * hf;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) rg[m] = g4[t + 512 * m];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) rx[m] = x4[t + 512 * m];
+    for (int m = 0; m < 2; ++m) fb_glds16(xsrc + (wv + 8 * m) * 256, rb + 32 * 1024 + (wv + 8 * m) * 1024);
   };
-  auto stage = [&](int bb, int tl) {
-    char* gb = fb + (size_t)bb * FB_BUF;
-    char* xb = gb + 2 * FB_GPART;
+  const int ss = t & 31, sh = (t >> 5) & 1, sg0 = t >> 6;
+  auto convert = [&](int k) {   // raw tile k -> split operands (this wave's rows)
+    const int tl = pr + k * npair;
+    const char* rb = fb + (size_t)(1 + (k & 1)) * FB_BUF;
     const bool valid = (int64_t)tl * 32 + ss < n;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
+      const int row = sg0 + 8 * m;
+      const f32x4 r = *reinterpret_cast<const f32x4*>(rb + (row * 64 + lane) * 16);
       f32x4 v;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = valid ? rg[m][q] * gsc : 0.0f;
+      for (int q = 0; q < 4; ++q) v[q] = valid ? r[q] * gsc : 0.0f;
       s16x4 p0, p1;
       split2_x4(v, p0, p1);
-      const int o = fb_off<FB_GP>(ss, 8 * (sg0 + 8 * m) + 4 * sh);
-      *reinterpret_cast<s16x4*>(gb + o) = p0;
-      *reinterpret_cast<s16x4*>(gb + FB_GPART + o) = p1;
+      const int o = fb_off<FB_GP>(ss, 8 * row + 4 * sh);
+      *reinterpret_cast<s16x4*>(sp + o) = p0;
+      *reinterpret_cast<s16x4*>(sp + FB_GPART + o) = p1;
     }
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
+      const int row = sg0 + 8 * m, cl = 8 * row + 4 * sh;   // column within the half
+      const f32x4 r = *reinterpret_cast<const f32x4*>(rb + 32 * 1024 + (row * 64 + lane) * 16);
+      const f32x4 mu = *reinterpret_cast<const f32x4*>(cst + 768 + cl);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(cst + cl);
       f32x4 v;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = valid ? (rx[m][q] - mu2[m][q]) * csc2[m][q] : 0.0f;
+      for (int q = 0; q < 4; ++q) v[q] = valid ? (r[q] - mu[q]) * sc[q] : 0.0f;
       s16x4 p0, p1;
       split2_x4(v, p0, p1);
-      const int o = fb_off<FB_XP>(ss, 8 * (sg0 + 8 * m) + 4 * sh);
-      *reinterpret_cast<s16x4*>(xb + o) = p0;
-      *reinterpret_cast<s16x4*>(xb + FB_XPART + o) = p1;
+      const int o = fb_off<FB_XP>(ss, cl);
+      *reinterpret_cast<s16x4*>(sp + 2 * FB_GPART + o) = p0;
+      *reinterpret_cast<s16x4*>(sp + 2 * FB_GPART + FB_XPART + o) = p1;
     }
   };
   f32x4 aw[2][8];
@@ -2979,20 +3002,21 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     for (int ib = 0; ib < 8; ++ib) aw[jb][ib] = f32x4{};
   float dbacc[2] = {0.0f, 0.0f};
   float gmo = 0.0f;
-  // transposed reads: lane lm = 4 q + pp of 16-lane group kg supplies sample row 8 kg + q (+ 4), columns + 4 pp
-  const int trq = lm >> 2, trp = lm & 3;
-  int tl = pr;
-  if (tl < nt) {
-    load_tile(tl);
-    stage(0, tl);
-  }
-  __syncthreads();
-  int bb = 0;
-  while (tl < nt) {
-    const int nxt = tl + npair;
-    if (nxt < nt) load_tile(nxt);
-    const char* gb = fb + (size_t)bb * FB_BUF;
-    const char* xb = gb + 2 * FB_GPART;
+  const int trq = lm >> 2, trp = lm & 3;   // transposed reads: lane lm = 4 q + pp of 16-lane group kg
+  __syncthreads();   // cst
+  if (nk > 0) issue_raw(0);
+  if (nk > 1) issue_raw(1);
+  if (nk > 1) __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6): tile 0's six DMAs landed (tile 1's in flight)
+  else __builtin_amdgcn_s_waitcnt(0x0F70);
+  if (nk > 0) convert(0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  for (int k = 0; k < nk; ++k) {
+    const int tl = pr + k * npair;
+    const bool more2 = k + 2 < nk;
+    if (more2) issue_raw(k + 2);   // into the raw buffer tile k came from
+    const char* gb = sp;
+    const char* xb = sp + 2 * FB_GPART;
     // data gradient: this wave's 16 input features x 32 samples
     f32x4 ad[2] = {f32x4{}, f32x4{}};
 #pragma unroll
@@ -3007,18 +3031,34 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
         ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], bh, ad[sb], 0, 0, 0);
       }
     }
-    // weight gradient: rows j = 32 wv + 16 jb + lm, the tile's 32 samples, 8 column blocks of this half
-    f16x8 A[2][2];
+    // weight gradient: rows j = 32 wv + 16 jb + lm, the tile's 32 samples, 8 column blocks of this half.  Operands
+    // by transposed reads (rows +4: the same swizzle, so an immediate offset; the mid part FB_*PART further), the
+    // next column block's read while the current one multiplies
+    auto read8 = [&](unsigned a, auto pitch, auto part) {
+      constexpr int P = decltype(pitch)::value, Q = decltype(part)::value;
+      const s16x4 h0 = fb_tr<0>(a), h1 = fb_tr<4 * P>(a), m0 = fb_tr<Q>(a), m1 = fb_tr<Q + 4 * P>(a);
+      return std::array<s16x4, 4>{h0, h1, m0, m1};
+    };
+    auto join = [](const s16x4& a, const s16x4& b) {
+      return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    using PG = std::integral_constant<int, FB_GP>;
+    using PX = std::integral_constant<int, FB_XP>;
+    using QG = std::integral_constant<int, FB_GPART>;
+    using QX = std::integral_constant<int, FB_XPART>;
+    const unsigned ga = fb_lds_addr(gb), xa = fb_lds_addr(xb);
+    std::array<s16x4, 4> ra[2], rbx[2];
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
+      ra[jb] = read8(ga + fb_off<FB_GP>(8 * kg + trq, 32 * wv + 16 * jb + 4 * trp), PG{}, QG{});
+    rbx[0] = read8(xa + fb_off<FB_XP>(8 * kg + trq, 4 * trp), PX{}, QX{});
+    fb_lgkm<4>();   // A landed (the first column block's four reads may still fly)
+    f16x8 A[2][2];
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const char* pb = gb + p * FB_GPART;
-        const int col = 32 * wv + 16 * jb + 4 * trp;
-        const s16x4 v0 = fb_tr(pb + fb_off<FB_GP>(8 * kg + trq, col));
-        const s16x4 v1 = fb_tr(pb + fb_off<FB_GP>(8 * kg + 4 + trq, col));
-        A[jb][p] = __builtin_bit_cast(f16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
+    for (int jb = 0; jb < 2; ++jb) {
+      A[jb][0] = join(ra[jb][0], ra[jb][1]);
+      A[jb][1] = join(ra[jb][2], ra[jb][3]);
+    }
     if (hf == 0) {
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb)
@@ -3027,24 +3067,22 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     }
 #pragma unroll
     for (int ib = 0; ib < 8; ++ib) {
-      f16x8 B[2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const char* pb = xb + p * FB_XPART;
-        const int col = 16 * ib + 4 * trp;
-        const s16x4 v0 = fb_tr(pb + fb_off<FB_XP>(8 * kg + trq, col));
-        const s16x4 v1 = fb_tr(pb + fb_off<FB_XP>(8 * kg + 4 + trq, col));
-        B[p] = __builtin_bit_cast(f16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+      if (ib + 1 < 8) {
+        rbx[(ib + 1) & 1] = read8(xa + fb_off<FB_XP>(8 * kg + trq, 16 * (ib + 1) + 4 * trp), PX{}, QX{});
+        fb_lgkm<4>();
+      } else {
+        fb_lgkm<0>();
       }
+      const f16x8 B0 = join(rbx[ib & 1][0], rbx[ib & 1][1]), B1 = join(rbx[ib & 1][2], rbx[ib & 1][3]);
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
-        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B[0], aw[jb][ib], 0, 0, 0);
-        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B[1], aw[jb][ib], 0, 0, 0);
-        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B[0], aw[jb][ib], 0, 0, 0);
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B0, aw[jb][ib], 0, 0, 0);
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B1, aw[jb][ib], 0, 0, 0);
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B0, aw[jb][ib], 0, 0, 0);
       }
     }
     // epilogue: dL/dy -> BatchNorm L-1 backward -> g_{L-1} over this tile's h_{L-1} (input features
-    // 128 hf + 16 wv + 4 kg .. + 3 of sample 16 sb + lm)
+    // 128 hf + 16 wv + 4 kg .. + 3 of sample 16 sb + lm): two 16-byte stores per lane
     {
       const int il = 16 * wv + 4 * kg;   // column within the half
       const f32x4 cun = *reinterpret_cast<const f32x4*>(cst + 128 + il);
@@ -3071,10 +3109,14 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
         reinterpret_cast<f32x4*>(hio + (size_t)tl * TILE_FLOATS)[(i >> 3) * 64 + sm + 32 * ((i >> 2) & 1)] = v;
       }
     }
-    if (nxt < nt) stage(bb ^ 1, nxt);
-    __syncthreads();
-    bb ^= 1;
-    tl = nxt;
+    // tile k + 1's DMAs landed (this wave's: the ones issued before tile k + 2's six and this tile's two stores)
+    if (more2) __builtin_amdgcn_s_waitcnt(0x0F78);   // vmcnt(8)
+    else __builtin_amdgcn_s_waitcnt(0x0F72);         // vmcnt(2)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();   // every wave done with tile k's split operands
+    if (k + 1 < nk) convert(k + 1);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
   }
   gmo = wave_max_f(gmo);
   if (lane == 0) atomicMax(gmax_out + ((bid * 8 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
