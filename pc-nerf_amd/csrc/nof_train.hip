@@ -2849,9 +2849,19 @@ __device__ __forceinline__ s16x4 fb_tr(unsigned addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
   return __builtin_bit_cast(s16x4, r);
 }
-template <int N>
-__device__ __forceinline__ void fb_lgkm() {   // s_waitcnt lgkmcnt(N)
-  __builtin_amdgcn_s_waitcnt(0xC07F & ~0x0F00 | (N << 8));
+// s_waitcnt lgkmcnt(N), then the values that wait made ready pass through an (ordered) empty asm: the compiler
+// cannot read their registers before the wait
+template <int N, size_t K>
+__device__ __forceinline__ void fb_lgkm(std::array<s16x4, 4> (&ready)[K]) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N));
+#pragma unroll
+  for (size_t k = 0; k < K; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fb_i32x2 v = __builtin_bit_cast(fb_i32x2, ready[k][i]);
+      asm volatile("" : "+v"(v));
+      ready[k][i] = __builtin_bit_cast(s16x4, v);
+    }
 }
 __device__ __forceinline__ unsigned fb_lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
@@ -3052,7 +3062,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     for (int jb = 0; jb < 2; ++jb)
       ra[jb] = read8(ga + fb_off<FB_GP>(8 * kg + trq, 32 * wv + 16 * jb + 4 * trp), PG{}, QG{});
     rbx[0] = read8(xa + fb_off<FB_XP>(8 * kg + trq, 4 * trp), PX{}, QX{});
-    fb_lgkm<4>();   // A landed (the first column block's four reads may still fly)
+    fb_lgkm<4>(ra);   // A landed (the first column block's four reads may still fly)
     f16x8 A[2][2];
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb) {
@@ -3067,12 +3077,14 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     }
 #pragma unroll
     for (int ib = 0; ib < 8; ++ib) {
+      std::array<s16x4, 4> cur[1] = {rbx[ib & 1]};
       if (ib + 1 < 8) {
         rbx[(ib + 1) & 1] = read8(xa + fb_off<FB_XP>(8 * kg + trq, 16 * (ib + 1) + 4 * trp), PX{}, QX{});
-        fb_lgkm<4>();
+        fb_lgkm<4>(cur);
       } else {
-        fb_lgkm<0>();
+        fb_lgkm<0>(cur);
       }
+      rbx[ib & 1] = cur[0];
       const f16x8 B0 = join(rbx[ib & 1][0], rbx[ib & 1][1]), B1 = join(rbx[ib & 1][2], rbx[ib & 1][3]);
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
