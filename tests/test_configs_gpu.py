@@ -5,8 +5,8 @@
             compared with the reference's outputs on those rows (tests/golden/config1_kitti.npz);
   config 2  the headline workload at FULL size: 65,536 rays, 128/256 samples, chunk 262,144 (32 coarse + 96 fine
             BatchNorm chunks), child losses, against the reference run on the same rays (config2_full.npz);
-  config 3  the KITTI training loop at 262,144 rays/iter (64/128 samples): a full-size training step (forward,
-            losses, backward, Adam), property-checked (no CPU run of this size exists);
+  config 3  the KITTI training loop at 262,144 rays/iter (64/128 samples): the full-size step's forward against the
+            reference run on the same rays (config3_kitti.npz), then forward, losses, backward, Adam, properties;
   config 4  MaiCity-00 in 4 parent blocks, each with its own weights (config4_maicity.npz);
   the training driver: k steps of Adam + MultiStepLR through train_kitti.fit() against the oracle's autograd +
             torch.optim.Adam (parameters and per-step losses), once with BatchNorm inputs whose |mean|/std >> 1.
@@ -230,14 +230,19 @@ def test_config4_maicity_blocks(tmp_path):
 # ----------------------------------------------------------------------------------------------- config 3
 def test_config3_training_step_262144_rays(tmp_path):
     """The KITTI training loop's step at 262,144 rays/iter (64/128 samples, chunk 262,144: 64 coarse + 192 fine
-    BatchNorm chunks, more than the activation store holds, so the backward recomputes part of the forward):
-    a batch drawn (with replacement) from the KITTI fixture scene's train rays; three steps of forward, range +
-    child losses, backward, Adam.  Properties: finite losses that decrease on the repeated batch, finite non-zero
-    gradients on both networks, running statistics and parameters updated."""
+    BatchNorm chunks, more than the default activation store holds, so the backward recomputes part of the
+    forward): a batch drawn (with replacement, numpy seed 3) from the KITTI fixture scene's whole train split, rebuilt
+    on the GPU and checked bit for bit against tests/golden/scene_rays.npz.  The first step's forward (depths, child
+    and range losses, total, running statistics) against the reference run on the same 262,144 rays
+    (config3_kitti.npz, make_golden.gen_config3_kitti) with check_train's tolerances -- depth_fine against the float64
+    evaluation and the reference's own spread (config3_kitti_f64.npz, _alt.npz); then three steps of forward,
+    losses, backward, Adam: finite losses that decrease on the repeated batch, finite non-zero gradients on both
+    networks, running statistics and parameters updated."""
     tr, _ = kitti_scene(tmp_path)
-    gen = torch.Generator(device=DEV).manual_seed(0)
-    idx = torch.randint(0, tr.rays.shape[0], (262144,), device=DEV, generator=gen)
-    rays = tr.rays[idx].contiguous()
+    sc, g3 = golden("scene_rays"), golden("config3_kitti")
+    np.testing.assert_array_equal(tr.rays.cpu().numpy(), sc["kitti_train_all"])
+    idx = np.random.default_rng(int(g3["seed"])).integers(0, tr.rays.shape[0], int(g3["n_rays"]))
+    rays = tr.rays[torch.from_numpy(idx).to(DEV)].contiguous()
     emb, mc, mf = models(True)
     params = list(mc.parameters()) + list(mf.parameters())
     opt = torch.optim.Adam(params, lr=5e-4, eps=1e-8, weight_decay=1e-3)
@@ -246,10 +251,13 @@ def test_config3_training_step_262144_rays(tmp_path):
     losses = []
     for _ in range(3):
         opt.zero_grad(set_to_none=True)
-        res = R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=1171, N_samples=64, N_importance=128,
-                                  **PCNERF_TRAIN)
+        res = R.render_rays_train(mc, mf, emb, rays, sub_nerf_test_num=int(g3["sub_nerf_test_num"]), N_samples=64,
+                                  N_importance=128, **PCNERF_TRAIN)
         for k in ("depth", "depth_fine"):
             assert torch.isfinite(res[k]).all()
+        if not losses:   # the first step's forward against the reference
+            check_train({k: v.detach() for k, v in res.items()}, g3, rays, mc, mf, name="config3_kitti",
+                        f64=golden("config3_kitti_f64"), alt=golden("config3_kitti_alt"))
         gt = rays[:, 14]
         loss = (1e-1 * loss_fn(1e1 * res["depth"], 1e1 * gt) + 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
                 + 1e6 * (res["child_free_loss"] + res["child_free_loss_fine"])
