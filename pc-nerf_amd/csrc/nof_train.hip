@@ -2833,7 +2833,14 @@ constexpr int FB_BUF = 2 * FB_GPART + 2 * FB_XPART;       // 48 KiB per tile
 constexpr int FB_PAIRS = 128;
 constexpr size_t FB_LDS = 3 * (size_t)FB_BUF + 7 * 128 * sizeof(float);   // split + 2 raw tiles + constants
 
-__device__ __forceinline__ int fb_swz(int r) { return 2 * ((r & 3) | ((r & 8) >> 1)); }
+// 16-byte chunk c of row r sits at c ^ f(r), f(r) = 2 (r & 3 | b << 2) | p with p = bit 2 of r and b = bit 2 ^ bit 3:
+// sixteen distinct values over a row block of 16 (the split writes: 32 lanes = 16 rows x two 8-byte halves of one
+// chunk), distinct f >> 1 over rows {0..3, 8..11} and over {4..7, 12..15} (the transposed reads: 8 rows x 2 chunks),
+// and {f(A)} u {f(B) ^ 1} distinct for A = {0..3, 12..15}, B = {4..11} (the 16-byte reads' lane groups of 16, two
+// k-groups each) -- every pattern conflict-free (scripts/micro/lds_fb.hip)
+__device__ __forceinline__ int fb_swz(int r) {
+  return 2 * ((r & 3) | ((((r >> 2) ^ (r >> 3)) & 1) << 2)) | ((r >> 2) & 1);
+}
 template <int P>
 __device__ __forceinline__ int fb_off(int r, int c) {   // 16-bit element c of row r
   return r * P + 16 * ((c >> 3) ^ fb_swz(r)) + 2 * (c & 7);
@@ -2959,40 +2966,43 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
       for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 16 + 8 * hf + wv) * 2 + p) * 64];
   }
   // Raw tiles by LDS-DMA, two ahead: raw buffer k & 1 holds the pair's tile k as it lies in HBM -- 32 rows (feature
-  // groups) of 1 KiB of g_L, then the 16 rows of this half's h_{L-1}.  Wave w moves rows w + 8 m and later splits
-  // exactly those rows (thread t: row (t >> 6) + 8 m, HBM lane t & 63), so a wave waits only for its own DMA.
+  // groups) of 1 KiB of g_L, then the 16 rows of this half's h_{L-1}.  Wave w moves g rows 4 w + m and x rows
+  // 2 w + m and later splits exactly those rows, so a wave waits only for its own DMA.  Split map of wave w's
+  // instruction m: lane l takes sample 16 sb + (l & 15) (sb = m & 1), half (l >> 4) & 1 of row 4 w + 2 (m >> 1) +
+  // (l >> 5) (g) or 2 w + (l >> 5) (x, sb = m): the raw reads and the split writes conflict-free
   auto issue_raw = [&](int k) {
     const int tl = pr + k * npair;
     char* rb = fb + (size_t)(1 + (k & 1)) * FB_BUF;
     const float* gsrc = gin + (size_t)tl * TILE_FLOATS + lane * 4;
     const float* xsrc = hio + (size_t)tl * TILE_FLOATS + 16 * hf * 256 + lane * 4;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) fb_glds16(gsrc + (wv + 8 * m) * 256, rb + (wv + 8 * m) * 1024);
+    for (int m = 0; m < 4; ++m) fb_glds16(gsrc + (4 * wv + m) * 256, rb + (4 * wv + m) * 1024);
 #pragma unroll
-    for (int m = 0; m < 2; ++m) fb_glds16(xsrc + (wv + 8 * m) * 256, rb + 32 * 1024 + (wv + 8 * m) * 1024);
+    for (int m = 0; m < 2; ++m) fb_glds16(xsrc + (2 * wv + m) * 256, rb + 32 * 1024 + (2 * wv + m) * 1024);
   };
-  const int ss = t & 31, sh = (t >> 5) & 1, sg0 = t >> 6;
+  const int sl = lane & 15, sh = (lane >> 4) & 1, sr = lane >> 5;
   auto convert = [&](int k) {   // raw tile k -> split operands (this wave's rows)
     const int tl = pr + k * npair;
     const char* rb = fb + (size_t)(1 + (k & 1)) * FB_BUF;
-    const bool valid = (int64_t)tl * 32 + ss < n;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const int row = sg0 + 8 * m;
-      const f32x4 r = *reinterpret_cast<const f32x4*>(rb + (row * 64 + lane) * 16);
+      const int row = 4 * wv + 2 * (m >> 1) + sr, sm = 16 * (m & 1) + sl;
+      const bool valid = (int64_t)tl * 32 + sm < n;
+      const f32x4 r = *reinterpret_cast<const f32x4*>(rb + (row * 64 + sm + 32 * sh) * 16);
       f32x4 v;
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = valid ? r[q] * gsc : 0.0f;
       s16x4 p0, p1;
       split2_x4(v, p0, p1);
-      const int o = fb_off<FB_GP>(ss, 8 * row + 4 * sh);
+      const int o = fb_off<FB_GP>(sm, 8 * row + 4 * sh);
       *reinterpret_cast<s16x4*>(sp + o) = p0;
       *reinterpret_cast<s16x4*>(sp + FB_GPART + o) = p1;
     }
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      const int row = sg0 + 8 * m, cl = 8 * row + 4 * sh;   // column within the half
-      const f32x4 r = *reinterpret_cast<const f32x4*>(rb + 32 * 1024 + (row * 64 + lane) * 16);
+      const int row = 2 * wv + sr, sm = 16 * m + sl, cl = 8 * row + 4 * sh;   // column within the half
+      const bool valid = (int64_t)tl * 32 + sm < n;
+      const f32x4 r = *reinterpret_cast<const f32x4*>(rb + 32 * 1024 + (row * 64 + sm + 32 * sh) * 16);
       const f32x4 mu = *reinterpret_cast<const f32x4*>(cst + 768 + cl);
       const f32x4 sc = *reinterpret_cast<const f32x4*>(cst + cl);
       f32x4 v;
@@ -3000,7 +3010,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
       for (int q = 0; q < 4; ++q) v[q] = valid ? (r[q] - mu[q]) * sc[q] : 0.0f;
       s16x4 p0, p1;
       split2_x4(v, p0, p1);
-      const int o = fb_off<FB_XP>(ss, cl);
+      const int o = fb_off<FB_XP>(sm, cl);
       *reinterpret_cast<s16x4*>(sp + 2 * FB_GPART + o) = p0;
       *reinterpret_cast<s16x4*>(sp + 2 * FB_GPART + FB_XPART + o) = p1;
     }
@@ -3044,24 +3054,29 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     // weight gradient: rows j = 32 wv + 16 jb + lm, the tile's 32 samples, 8 column blocks of this half.  Operands
     // by transposed reads (rows +4: the same swizzle, so an immediate offset; the mid part FB_*PART further), the
     // next column block's read while the current one multiplies
-    auto read8 = [&](unsigned a, auto pitch, auto part) {
-      constexpr int P = decltype(pitch)::value, Q = decltype(part)::value;
-      const s16x4 h0 = fb_tr<0>(a), h1 = fb_tr<4 * P>(a), m0 = fb_tr<Q>(a), m1 = fb_tr<Q + 4 * P>(a);
+    auto read8 = [&](unsigned a0, unsigned a1, auto part) {   // rows 8 kg + q (a0) and + 4 (a1), hi and mid
+      constexpr int Q = decltype(part)::value;
+      const s16x4 h0 = fb_tr<0>(a0), h1 = fb_tr<0>(a1), m0 = fb_tr<Q>(a0), m1 = fb_tr<Q>(a1);
       return std::array<s16x4, 4>{h0, h1, m0, m1};
     };
     auto join = [](const s16x4& a, const s16x4& b) {
       return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
     };
-    using PG = std::integral_constant<int, FB_GP>;
-    using PX = std::integral_constant<int, FB_XP>;
     using QG = std::integral_constant<int, FB_GPART>;
     using QX = std::integral_constant<int, FB_XPART>;
     const unsigned ga = fb_lds_addr(gb), xa = fb_lds_addr(xb);
+    const int tr0 = 8 * kg + trq, tr1 = tr0 + 4;
+    auto xrd = [&](int ib) {
+      const int col = 16 * ib + 4 * trp;
+      return read8(xa + fb_off<FB_XP>(tr0, col), xa + fb_off<FB_XP>(tr1, col), QX{});
+    };
     std::array<s16x4, 4> ra[2], rbx[2];
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-      ra[jb] = read8(ga + fb_off<FB_GP>(8 * kg + trq, 32 * wv + 16 * jb + 4 * trp), PG{}, QG{});
-    rbx[0] = read8(xa + fb_off<FB_XP>(8 * kg + trq, 4 * trp), PX{}, QX{});
+    for (int jb = 0; jb < 2; ++jb) {
+      const int col = 32 * wv + 16 * jb + 4 * trp;
+      ra[jb] = read8(ga + fb_off<FB_GP>(tr0, col), ga + fb_off<FB_GP>(tr1, col), QG{});
+    }
+    rbx[0] = xrd(0);
     fb_lgkm<4>(ra);   // A landed (the first column block's four reads may still fly)
     f16x8 A[2][2];
 #pragma unroll
@@ -3079,7 +3094,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     for (int ib = 0; ib < 8; ++ib) {
       std::array<s16x4, 4> cur[1] = {rbx[ib & 1]};
       if (ib + 1 < 8) {
-        rbx[(ib + 1) & 1] = read8(xa + fb_off<FB_XP>(8 * kg + trq, 16 * (ib + 1) + 4 * trp), PX{}, QX{});
+        rbx[(ib + 1) & 1] = xrd(ib + 1);
         fb_lgkm<4>(cur);
       } else {
         fb_lgkm<0>(cur);

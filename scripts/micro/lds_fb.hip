@@ -12,6 +12,10 @@ __device__ __forceinline__ int off(int r, int c, int mode) {
     const int swz = 2 * ((r & 3) | ((r & 8) >> 1));
     return r * P + 16 * ((c >> 3) ^ swz) + 2 * (c & 7);
   }
+  if (mode == 3) {   // nof_train.hip's fb_swz (round 4 final)
+    const int f = 2 * ((r & 3) | ((((r >> 2) ^ (r >> 3)) & 1) << 2)) | ((r >> 2) & 1);
+    return r * P + 16 * ((c >> 3) ^ f) + 2 * (c & 7);
+  }
   // mode 1: rows padded by 16 B, no swizzle; mode 2: rows padded by 16 B + the XOR swizzle
   const int swz = mode == 2 ? 2 * ((r & 3) | ((r & 8) >> 1)) : 0;
   return r * (P + 16) + 16 * ((c >> 3) ^ swz) + 2 * (c & 7);
@@ -31,7 +35,8 @@ __global__ __launch_bounds__(256, 1) void k(int pattern, int mode, unsigned long
   if (pattern == 0) a0 = off<512>(lm, 8 * kg, mode);                                  // dgrad b128 (ks 0, sb 0)
   else if (pattern == 1) a0 = off<512>(8 * kg + (lm >> 2), 32 * wv + 4 * (lm & 3), mode);   // tr read, g
   else if (pattern == 2) a0 = off<256>(8 * kg + (lm >> 2), 4 * (lm & 3), mode);       // tr read, x
-  else if (pattern == 3) a0 = off<512>(lane & 31, 8 * wv + 4 * ((lane >> 5) & 1), mode);   // split write, g
+  else if (pattern == 3 && mode < 3) a0 = off<512>(lane & 31, 8 * wv + 4 * ((lane >> 5) & 1), mode);   // split write, g
+  else if (pattern == 3) a0 = off<512>(lm, 8 * (4 * wv + (lane >> 5)) + 4 * ((lane >> 4) & 1), mode);   // its final map
   else a0 = off<256>(lm, 16 * wv + 4 * kg, mode);                                      // epilogue read x
   const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
   const unsigned addr = base + a0;
@@ -70,7 +75,7 @@ int main() {
   (void)hipMalloc(&out, 256 * 4 * 8);
   (void)hipMalloc(&sink, 256 * 256 * 4);
   const char* names[] = {"dgrad ds_read_b128", "tr read g", "tr read x", "split ds_write_b64", "epilogue ds_read_b64"};
-  for (int mode = 0; mode < 3; ++mode)
+  for (int mode = 0; mode < 4; ++mode)
     for (int p = 0; p < 5; ++p) {
       hipLaunchKernelGGL(k, dim3(256), dim3(256), 0, 0, p, mode, out, sink);
       (void)hipDeviceSynchronize();
