@@ -2923,8 +2923,12 @@ __device__ __forceinline__ constexpr int fb_vmcnt(int n) {   // s_waitcnt vmcnt(
   return (n & 15) | ((n >> 4) << 14) | 0x0F70;
 }
 
+#ifndef FB_ABL
+#define FB_ABL 0   // diagnostic ablations (timing only): 1 no data-gradient MFMA, 2 no weight-gradient MFMA, 4 no
+                   // split conversion, 8 no epilogue stores, 16 no DMA in the loop
+#endif
 template <int LAY>
-__global__ __launch_bounds__(256, 1) void k_bwd_fused(const float* __restrict__ gin, float* hio,
+__global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ gin, float* hio,
                                                        const f16x8* __restrict__ wt, const int* __restrict__ sw,
                                                        int layer, int64_t n, const float* __restrict__ coefp,
                                                        const float* __restrict__ bnb,
@@ -2933,7 +2937,7 @@ __global__ __launch_bounds__(256, 1) void k_bwd_fused(const float* __restrict__ 
                                                        unsigned* __restrict__ gmax_out, float* __restrict__ part) {
   constexpr int C = WgradCfg<LAY>::C, COL = LAY == 2 ? 64 : 0;
   extern __shared__ __attribute__((aligned(16))) char fb[];
-  char* const sp = fb;                                              // the split operands of the current tile
+  // LDS: split operands of tiles k & 1 (two buffers), the raw tile (one buffer), constants
   float* const cst = reinterpret_cast<float*>(fb + 3 * FB_BUF);     // [csc | cun | gm | kk | invstd | gamma | mu][128]
   const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2960,39 +2964,38 @@ __global__ __launch_bounds__(256, 1) void k_bwd_fused(const float* __restrict__ 
   const int eg = tile_scale_exp(__uint_as_float(gmx));
   const float gsc = ldexpf(1.0f, eg), gun = ldexpf(1.0f, -eg);
   const float dun = ldexpf(1.0f, -sw[layer]) * gun;   // data-gradient accumulator -> dL/dy
-  // this wave's W^T rows: input features 128 hf + 32 wv + 16 ib + (lane & 15), ib < 2, all 8 k-steps, hi / mid
-  f16x8 wr[2][8][2];
+  // this wave's W^T rows: input features 128 hf + 16 wv + (lane & 15), all 8 k-steps, hi / mid
+  f16x8 wr[8][2];
   {
     const f16x8* __restrict__ w8 = wt + lane;
 #pragma unroll
-    for (int ib = 0; ib < 2; ++ib)
+    for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) wr[ib][ks][p] = w8[((ks * 16 + 8 * hf + 2 * wv + ib) * 2 + p) * 64];
+      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 16 + 8 * hf + wv) * 2 + p) * 64];
   }
   // Raw tiles by LDS-DMA, two ahead: raw buffer k & 1 holds the pair's tile k as it lies in HBM -- 32 rows (feature
-  // groups) of 1 KiB of g_L, then the 16 rows of this half's h_{L-1}.  Wave w moves g rows 8 w + m and x rows
-  // 4 w + m and later splits exactly those rows, so a wave waits only for its own DMA.  Split map of instruction m:
-  // lane l takes sample 16 (m & 1) + (l & 15), half (l >> 4) & 1 of row 8 w + 2 (m >> 1) + (l >> 5) (g) or
-  // 4 w + 2 (m >> 1) + (l >> 5) (x): the raw reads and the split writes conflict-free
+  // groups) of 1 KiB of g_L, then the 16 rows of this half's h_{L-1}.  Wave w moves g rows 4 w + m and x rows
+  // 2 w + m and later splits exactly those rows, so a wave waits only for its own DMA.  Split map of wave w's
+  // instruction m: lane l takes sample 16 sb + (l & 15) (sb = m & 1), half (l >> 4) & 1 of row 4 w + 2 (m >> 1) +
+  // (l >> 5) (g) or 2 w + (l >> 5) (x, sb = m): the raw reads and the split writes conflict-free
   auto issue_raw = [&](int k) {
     const int tl = pr + k * npair;
-    char* rb = fb + (size_t)(1 + (k & 1)) * FB_BUF;
+    char* rb = fb + 2 * (size_t)FB_BUF;
     const float* gsrc = gin + (size_t)tl * TILE_FLOATS + lane * 4;
     const float* xsrc = hio + (size_t)tl * TILE_FLOATS + 16 * hf * 256 + lane * 4;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) fb_glds16(gsrc + (8 * wv + m) * 256, rb + (8 * wv + m) * 1024);
+    for (int m = 0; m < 4; ++m) fb_glds16(gsrc + (4 * wv + m) * 256, rb + (4 * wv + m) * 1024);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) fb_glds16(xsrc + (4 * wv + m) * 256, rb + 32 * 1024 + (4 * wv + m) * 1024);
+    for (int m = 0; m < 2; ++m) fb_glds16(xsrc + (2 * wv + m) * 256, rb + 32 * 1024 + (2 * wv + m) * 1024);
   };
   const int sl = lane & 15, sh = (lane >> 4) & 1, sr = lane >> 5;
-  auto convert = [&](int k) {   // raw tile k -> split operands (this wave's rows)
+  auto convert = [&](int k) {   // raw tile k -> split buffer k & 1 (this wave's rows)
     const int tl = pr + k * npair;
-    const char* rb = fb + (size_t)(1 + (k & 1)) * FB_BUF;
+    const char* rb = fb + 2 * (size_t)FB_BUF;
+    char* const sp = fb + (size_t)(k & 1) * FB_BUF;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int row = 8 * wv + 2 * (m >> 1) + sr, sm = 16 * (m & 1) + sl;
+    for (int m = 0; m < 4; ++m) {
+      const int row = 4 * wv + 2 * (m >> 1) + sr, sm = 16 * (m & 1) + sl;
       const bool valid = (int64_t)tl * 32 + sm < n;
       const f32x4 r = *reinterpret_cast<const f32x4*>(rb + (row * 64 + sm + 32 * sh) * 16);
       f32x4 v;
@@ -3005,8 +3008,8 @@ __global__ __launch_bounds__(256, 1) void k_bwd_fused(const float* __restrict__ 
       *reinterpret_cast<s16x4*>(sp + FB_GPART + o) = p1;
     }
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int row = 4 * wv + 2 * (m >> 1) + sr, sm = 16 * (m & 1) + sl, cl = 8 * row + 4 * sh;
+    for (int m = 0; m < 2; ++m) {
+      const int row = 2 * wv + sr, sm = 16 * m + sl, cl = 8 * row + 4 * sh;   // column within the half
       const bool valid = (int64_t)tl * 32 + sm < n;
       const f32x4 r = *reinterpret_cast<const f32x4*>(rb + 32 * 1024 + (row * 64 + sm + 32 * sh) * 16);
       const f32x4 mu = *reinterpret_cast<const f32x4*>(cst + 768 + cl);
@@ -3021,46 +3024,33 @@ __global__ __launch_bounds__(256, 1) void k_bwd_fused(const float* __restrict__ 
       *reinterpret_cast<s16x4*>(sp + 2 * FB_GPART + FB_XPART + o) = p1;
     }
   };
-  f32x4 aw[4][8];
+  f32x4 aw[2][8];
 #pragma unroll
-  for (int jb = 0; jb < 4; ++jb)
+  for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
     for (int ib = 0; ib < 8; ++ib) aw[jb][ib] = f32x4{};
-  float dbacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float dbacc[2] = {0.0f, 0.0f};
   float gmo = 0.0f;
   const int trq = lm >> 2, trp = lm & 3;   // transposed reads: lane lm = 4 q + pp of 16-lane group kg
-  const int tr0 = 8 * kg + trq, tr1 = tr0 + 4;
   __syncthreads();   // cst
-  if (nk > 0) issue_raw(0);
-  if (nk > 1) issue_raw(1);
-  if (nk > 1) __builtin_amdgcn_s_waitcnt(fb_vmcnt(12));   // tile 0's twelve DMAs landed (tile 1's in flight)
-  else __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
-  if (nk > 0) convert(0);
+  // Pipeline, one barrier per tile: tile k computes from split buffer k & 1 while each wave splits ITS rows of tile
+  // k + 1 (raw, DMA'd during tile k - 1) into buffer (k + 1) & 1 between the data- and weight-gradient MFMAs, then
+  // DMAs its rows of tile k + 2 into the raw buffer it has just read
+  if (nk > 0) {
+    issue_raw(0);
+    __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+    convert(0);
+    if (nk > 1) issue_raw(1);
+  }
   __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
   __builtin_amdgcn_s_barrier();
-  const unsigned ga = fb_lds_addr(sp), xa = fb_lds_addr(sp + 2 * FB_GPART);
-  using QG = std::integral_constant<int, FB_GPART>;
-  using QX = std::integral_constant<int, FB_XPART>;
-  auto read8 = [&](unsigned a0, unsigned a1, auto part) {   // rows 8 kg + q (a0) and + 4 (a1), hi and mid
-    constexpr int Q = decltype(part)::value;
-    const s16x4 h0 = fb_tr<0>(a0), h1 = fb_tr<0>(a1), m0 = fb_tr<Q>(a0), m1 = fb_tr<Q>(a1);
-    return std::array<s16x4, 4>{h0, h1, m0, m1};
-  };
-  auto join = [](const s16x4& a, const s16x4& b) {
-    return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  auto xrd = [&](int ib) {
-    const int col = 16 * ib + 4 * trp;
-    return read8(xa + fb_off<FB_XP>(tr0, col), xa + fb_off<FB_XP>(tr1, col), QX{});
-  };
   for (int k = 0; k < nk; ++k) {
     const int tl = pr + k * npair;
-    const bool more2 = k + 2 < nk;
-    if (more2) issue_raw(k + 2);   // into the raw buffer tile k came from
+    const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
     const char* gb = sp;
     const char* xb = sp + 2 * FB_GPART;
-    // data gradient: this wave's 32 input features x 32 samples
-    f32x4 ad[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+    // data gradient: this wave's 16 input features x 32 samples
+    f32x4 ad[2] = {f32x4{}, f32x4{}};
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
@@ -3068,33 +3058,57 @@ __global__ __launch_bounds__(256, 1) void k_bwd_fused(const float* __restrict__ 
         const int o = fb_off<FB_GP>(16 * sb + lm, 32 * ks + 8 * kg);
         const f16x8 bh = *reinterpret_cast<const f16x8*>(gb + o);
         const f16x8 bm = *reinterpret_cast<const f16x8*>(gb + FB_GPART + o);
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-          ad[ib][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ib][ks][0], bh, ad[ib][sb], 0, 0, 0);
-          ad[ib][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ib][ks][0], bm, ad[ib][sb], 0, 0, 0);
-          ad[ib][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ib][ks][1], bh, ad[ib][sb], 0, 0, 0);
+        if (FB_ABL & 1) {
+          ad[sb][0] += (float)bh[0] + (float)bm[1];
+          continue;
         }
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bh, ad[sb], 0, 0, 0);
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bm, ad[sb], 0, 0, 0);
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], bh, ad[sb], 0, 0, 0);
       }
     }
-    // weight gradient: rows j = 64 wv + 16 jb + lm (jb < 4), the tile's 32 samples, 8 column blocks of this half;
-    // the next column block's transposed reads while the current one multiplies
-    std::array<s16x4, 4> ra[4], rbx[2];
+    if (k + 1 < nk) {   // this wave's rows of tile k + 1 (its DMA, then the stores of tile k - 1: vmcnt(2))
+      __builtin_amdgcn_s_waitcnt(k > 0 ? fb_vmcnt(2) : fb_vmcnt(0));
+      if (!(FB_ABL & 4)) convert(k + 1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // its raw reads done before the raw buffer is refilled
+      if (k + 2 < nk && !(FB_ABL & 16)) issue_raw(k + 2);
+    }
+    // weight gradient: rows j = 32 wv + 16 jb + lm, the tile's 32 samples, 8 column blocks of this half.  Operands
+    // by transposed reads (rows +4: the same swizzle, so an immediate offset; the mid part FB_*PART further), the
+    // next column block's read while the current one multiplies
+    auto read8 = [&](unsigned a0, unsigned a1, auto part) {   // rows 8 kg + q (a0) and + 4 (a1), hi and mid
+      constexpr int Q = decltype(part)::value;
+      const s16x4 h0 = fb_tr<0>(a0), h1 = fb_tr<0>(a1), m0 = fb_tr<Q>(a0), m1 = fb_tr<Q>(a1);
+      return std::array<s16x4, 4>{h0, h1, m0, m1};
+    };
+    auto join = [](const s16x4& a, const s16x4& b) {
+      return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    using QG = std::integral_constant<int, FB_GPART>;
+    using QX = std::integral_constant<int, FB_XPART>;
+    const unsigned ga = fb_lds_addr(gb), xa = fb_lds_addr(xb);
+    const int tr0 = 8 * kg + trq, tr1 = tr0 + 4;
+    auto xrd = [&](int ib) {
+      const int col = 16 * ib + 4 * trp;
+      return read8(xa + fb_off<FB_XP>(tr0, col), xa + fb_off<FB_XP>(tr1, col), QX{});
+    };
+    std::array<s16x4, 4> ra[2], rbx[2];
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) {
-      const int col = 64 * wv + 16 * jb + 4 * trp;
+    for (int jb = 0; jb < 2; ++jb) {
+      const int col = 32 * wv + 16 * jb + 4 * trp;
       ra[jb] = read8(ga + fb_off<FB_GP>(tr0, col), ga + fb_off<FB_GP>(tr1, col), QG{});
     }
     rbx[0] = xrd(0);
     fb_lgkm<4>(ra);   // A landed (the first column block's four reads may still fly)
-    f16x8 A[4][2];
+    f16x8 A[2][2];
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) {
+    for (int jb = 0; jb < 2; ++jb) {
       A[jb][0] = join(ra[jb][0], ra[jb][1]);
       A[jb][1] = join(ra[jb][2], ra[jb][3]);
     }
     if (hf == 0) {
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
+      for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
         for (int e = 0; e < 8; ++e) dbacc[jb] += (float)A[jb][0][e] + (float)A[jb][1][e];
     }
@@ -3107,19 +3121,23 @@ __global__ __launch_bounds__(256, 1) void k_bwd_fused(const float* __restrict__ 
       } else {
         fb_lgkm<0>(cur);
       }
-      const f16x8 B0 = join(cur[0][0], cur[0][1]), B1 = join(cur[0][2], cur[0][3]);
+      rbx[ib & 1] = cur[0];
+      const f16x8 B0 = join(rbx[ib & 1][0], rbx[ib & 1][1]), B1 = join(rbx[ib & 1][2], rbx[ib & 1][3]);
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb) {
+      for (int jb = 0; jb < 2; ++jb) {
+        if (FB_ABL & 2) {
+          aw[jb][ib][0] += (float)A[jb][0][0] + (float)B0[1] + (float)B1[2];
+          continue;
+        }
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B0, aw[jb][ib], 0, 0, 0);
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B1, aw[jb][ib], 0, 0, 0);
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B0, aw[jb][ib], 0, 0, 0);
       }
     }
     // epilogue: dL/dy -> BatchNorm L-1 backward -> g_{L-1} over this tile's h_{L-1} (input features
-    // 128 hf + 32 wv + 16 ib + 4 kg .. + 3 of sample 16 sb + lm): four 16-byte stores per lane
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) {
-      const int il = 32 * wv + 16 * ib + 4 * kg;   // column within the half
+    // 128 hf + 16 wv + 4 kg .. + 3 of sample 16 sb + lm): two 16-byte stores per lane
+    {
+      const int il = 16 * wv + 4 * kg;   // column within the half
       const f32x4 cun = *reinterpret_cast<const f32x4*>(cst + 128 + il);
       const f32x4 cgm = *reinterpret_cast<const f32x4*>(cst + 256 + il);
       const f32x4 ckk = *reinterpret_cast<const f32x4*>(cst + 384 + il);
@@ -3136,43 +3154,38 @@ __global__ __launch_bounds__(256, 1) void k_bwd_fused(const float* __restrict__ 
         f32x4 v;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float d = ad[ib][sb][q] * dun;
+          const float d = ad[sb][q] * dun;
           const float xc = ((float)xh[q] + (float)xm[q]) * cun[q];   // h - mean (hi + mid: 22 bits)
           v[q] = valid ? ((d - cgm[q]) - xc * ckk[q]) * cis[q] * cga[q] : 0.0f;
           gmo = fmaxf(gmo, fabsf(v[q]));
         }
-        reinterpret_cast<f32x4*>(hio + (size_t)tl * TILE_FLOATS)[(i >> 3) * 64 + sm + 32 * ((i >> 2) & 1)] = v;
+        if (!(FB_ABL & 8))
+          reinterpret_cast<f32x4*>(hio + (size_t)tl * TILE_FLOATS)[(i >> 3) * 64 + sm + 32 * ((i >> 2) & 1)] = v;
       }
     }
-    // tile k + 1's DMAs landed (this wave's: the ones issued before tile k + 2's twelve and this tile's four stores)
-    if (more2) __builtin_amdgcn_s_waitcnt(fb_vmcnt(16));
-    else __builtin_amdgcn_s_waitcnt(fb_vmcnt(4));
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();   // every wave done with tile k's split operands
-    if (k + 1 < nk) convert(k + 1);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();   // every wave done with split buffer k & 1 and has filled (k + 1) & 1
   }
   gmo = wave_max_f(gmo);
-  if (lane == 0) atomicMax(gmax_out + ((bid * 4 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
-  // G partial of pair pr: rows j = 64 wv + 16 jb + 4 kg + r, columns 128 hf + 16 ib + lm (x scale undone per column)
+  if (lane == 0) atomicMax(gmax_out + ((bid * 8 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
+  // G partial of pair pr: rows j = 32 wv + 16 jb + 4 kg + r, columns 128 hf + 16 ib + lm (x scale undone per column)
   float* pb = part + (size_t)pr * WgradCfg<LAY>::PART;
 #pragma unroll
   for (int ib = 0; ib < 8; ++ib) {
     const float cu = cst[128 + 16 * ib + lm] * gun;
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
+    for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        pb[(size_t)(64 * wv + 16 * jb + 4 * kg + r) * C + COL + 128 * hf + 16 * ib + lm] = aw[jb][ib][r] * cu;
+        pb[(size_t)(32 * wv + 16 * jb + 4 * kg + r) * C + COL + 128 * hf + 16 * ib + lm] = aw[jb][ib][r] * cu;
   }
   if (hf == 0) {
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) {
+    for (int jb = 0; jb < 2; ++jb) {
       float d = dbacc[jb];
       d += __shfl_xor(d, 16, 64);
       d += __shfl_xor(d, 32, 64);
-      if (kg == 0) pb[(size_t)256 * C + 64 * wv + 16 * jb + lm] = d * gun;
+      if (kg == 0) pb[(size_t)256 * C + 32 * wv + 16 * jb + lm] = d * gun;
     }
   }
 }
@@ -3380,11 +3393,11 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
     {
       ProfScope ps(s, PT_BWD_FUSED, 2.0 * 2.0 * 256.0 * 256.0 * dn, 3072.0 * dn);
       if (L == 4)
-        hipLaunchKernelGGL(k_bwd_fused<2>, dim3(fbg), dim3(256), FB_LDS, s, gin, hh[L - 1],
+        hipLaunchKernelGGL(k_bwd_fused<2>, dim3(fbg), dim3(512), FB_LDS, s, gin, hh[L - 1],
                            ws.wth16 + (size_t)(L - 1) * HW_H, ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1),
                            P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS, ws.gmax + (L - 1) * GMAX_SLOTS, ws.part);
       else
-        hipLaunchKernelGGL(k_bwd_fused<0>, dim3(fbg), dim3(256), FB_LDS, s, gin, hh[L - 1],
+        hipLaunchKernelGGL(k_bwd_fused<0>, dim3(fbg), dim3(512), FB_LDS, s, gin, hh[L - 1],
                            ws.wth16 + (size_t)(L - 1) * HW_H, ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1),
                            P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS, ws.gmax + (L - 1) * GMAX_SLOTS, ws.part);
     }
