@@ -3068,7 +3068,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
       }
     }
     if (k + 1 < nk) {   // this wave's rows of tile k + 1 (its DMA, then the stores of tile k - 1: vmcnt(2))
-      __builtin_amdgcn_s_waitcnt(k > 0 ? fb_vmcnt(2) : fb_vmcnt(0));
+      if (k > 0) __builtin_amdgcn_s_waitcnt(fb_vmcnt(2));
+      else __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
       if (!(FB_ABL & 4)) convert(k + 1);
       __builtin_amdgcn_s_waitcnt(0xC07F);   // its raw reads done before the raw buffer is refilled
       if (k + 2 < nk && !(FB_ABL & 16)) issue_raw(k + 2);
