@@ -326,27 +326,36 @@ def test_fit_trajectory_vs_oracle(tmp_path, stress):
     hip_losses = [r["train/loss"] for r in map(json.loads, open(log)) if "train/loss" in r]
     assert len(hip_losses) == epochs
 
-    # the oracle, fed the same batches in fit()'s order
-    gen = torch.Generator(device=DEV).manual_seed(int(h.seed))
-    Pc, Pf = O.params_from_numpy(pc_np), O.params_from_numpy(pf_np)
-    leaves = [P[k].requires_grad_(True) for P in (Pc, Pf) for k in P if k.endswith((".weight", ".bias"))]
-    opt = torch.optim.Adam(leaves, lr=5e-4, eps=1e-8, weight_decay=1e-3)
-    sched = torch.optim.lr_scheduler.MultiStepLR(opt, milestones=[5, 120, 256], gamma=0.2)
-    rays_c = torch.from_numpy(rays_np)
-    ref_losses = []
-    for _ in range(epochs):
-        perm = torch.randperm(n, device=DEV, generator=gen).cpu()
-        r = rays_c[perm]
-        opt.zero_grad()
-        res = O.render_rays_train(Pc, Pf, r, sub_nerf_test_num=32, N_samples=64, N_importance=128, perturb=0,
-                                  noise_std=0, chunk=8192, issegmentated=1, childnerf_ratio=0.1,
-                                  use_child_nerf_divide=0, use_child_nerf_loss=1)
-        lr, lrf = O.range_losses(res["depth"], res["depth_fine"], r[:, 14])
-        loss = O.total_loss(res, lr, lrf)
-        loss.backward()
-        opt.step()
-        sched.step()
-        ref_losses.append(float(loss))
+    # the oracle, fed the same batches in fit()'s order -- in float32 (the reference's arithmetic) and in float64
+    # (the same trajectory evaluated exactly, from the same float32 coarse positions)
+    def oracle_fit(f64):
+        gen = torch.Generator(device=DEV).manual_seed(int(h.seed))
+        Pc, Pf = O.params_from_numpy(pc_np), O.params_from_numpy(pf_np)
+        if f64:
+            Pc, Pf = ({k: (v.double() if v.is_floating_point() else v) for k, v in P.items()} for P in (Pc, Pf))
+        leaves = [P[k].requires_grad_(True) for P in (Pc, Pf) for k in P if k.endswith((".weight", ".bias"))]
+        opt = torch.optim.Adam(leaves, lr=5e-4, eps=1e-8, weight_decay=1e-3)
+        sched = torch.optim.lr_scheduler.MultiStepLR(opt, milestones=[5, 120, 256], gamma=0.2)
+        rays_c = torch.from_numpy(rays_np)
+        ref_losses = []
+        for _ in range(epochs):
+            perm = torch.randperm(n, device=DEV, generator=gen).cpu()
+            r = rays_c[perm]
+            opt.zero_grad()
+            res = O.render_rays_train(Pc, Pf, r, sub_nerf_test_num=32, N_samples=64, N_importance=128, perturb=0,
+                                      noise_std=0, chunk=8192, issegmentated=1, childnerf_ratio=0.1,
+                                      use_child_nerf_divide=0, use_child_nerf_loss=1, f64=f64)
+            rr = r.double() if f64 else r
+            lr, lrf = O.range_losses(res["depth"], res["depth_fine"], rr[:, 14])
+            loss = O.total_loss(res, lr, lrf)
+            loss.backward()
+            opt.step()
+            sched.step()
+            ref_losses.append(float(loss))
+        return Pc, Pf, ref_losses
+
+    Pc, Pf, ref_losses = oracle_fit(False)
+    Pc64, Pf64, _ = oracle_fit(True)
     np.testing.assert_allclose(hip_losses, ref_losses, rtol=RTOL)
     # Adam normalises every element's step (lr * m / sqrt(v)): an element whose gradient is at rounding-noise level
     # -- the mathematically-zero gradients of noise_level_grads, or single weights with a near-zero gradient --
@@ -354,13 +363,15 @@ def test_fit_trajectory_vs_oracle(tmp_path, stress):
     # within Adam's largest possible movement; each tensor's update (final - initial) matching the reference's
     # to 1 % in norm (the trajectory); a running mean follows the
     # bias / previous BN shift feeding its Linear, so it gets that drift through the Linear as tolerance; running
-    # variances of the drifted network within 5e-3.
+    # variances of the drifted network within 5e-3.  A tensor whose update the reference's own float32 rounding
+    # moves by more than 1 % (its float64 trajectory's distance: the occ_out bias under the x30 BatchNorm stress,
+    # whose Adam steps nearly cancel, 1.5 %) is held to 1.5 x that distance instead.
     nz = noise_level_grads()
     adam_max = 2 * 3.2 * 5e-4 * epochs
     init = {("c", k): v for k, v in pc_np.items()}
     init.update({("f", k): v for k, v in pf_np.items()})
     worst, worst_nz, worst_rm, worst_rv = 0.0, 0.0, 0.0, 0.0
-    for tag, m, P in (("c", system.nof_coarse, Pc), ("f", system.nof_fine, Pf)):
+    for tag, m, P, P64 in (("c", system.nof_coarse, Pc, Pc64), ("f", system.nof_fine, Pf, Pf64)):
         sd = m.state_dict()
         for k, v in sd.items():
             if k.endswith("num_batches_tracked"):
@@ -386,7 +397,8 @@ def test_fit_trajectory_vs_oracle(tmp_path, stress):
                     continue
                 upd = np.linalg.norm(want - init[(tag, k)].astype(np.float64))
                 ratio = float(np.linalg.norm(err) / upd)
-                assert ratio <= 1e-2, (tag + k, ratio)
+                spread = float(np.linalg.norm(want - P64[k].detach().numpy()) / upd)
+                assert ratio <= max(1e-2, 1.5 * spread), (tag + k, ratio, spread)
                 worst = max(worst, ratio)
     report(f"fit_trajectory_stress{stress:g}", max_update_err_rel_norm=worst, max_noise_param_drift=worst_nz,
            max_running_mean_err=worst_rm, max_running_var_rel=worst_rv,
