@@ -2923,10 +2923,6 @@ __device__ __forceinline__ constexpr int fb_vmcnt(int n) {   // s_waitcnt vmcnt(
   return (n & 15) | ((n >> 4) << 14) | 0x0F70;
 }
 
-#ifndef FB_ABL
-#define FB_ABL 0   // diagnostic ablations (timing only): 1 no data-gradient MFMA, 2 no weight-gradient MFMA, 4 no
-                   // split conversion, 8 no epilogue stores, 16 no DMA in the loop
-#endif
 template <int LAY>
 __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ gin, float* hio,
                                                        const f16x8* __restrict__ wt, const int* __restrict__ sw,
@@ -3058,10 +3054,6 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
         const int o = fb_off<FB_GP>(16 * sb + lm, 32 * ks + 8 * kg);
         const f16x8 bh = *reinterpret_cast<const f16x8*>(gb + o);
         const f16x8 bm = *reinterpret_cast<const f16x8*>(gb + FB_GPART + o);
-        if (FB_ABL & 1) {
-          ad[sb][0] += (float)bh[0] + (float)bm[1];
-          continue;
-        }
         ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bh, ad[sb], 0, 0, 0);
         ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bm, ad[sb], 0, 0, 0);
         ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], bh, ad[sb], 0, 0, 0);
@@ -3070,9 +3062,9 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     if (k + 1 < nk) {   // this wave's rows of tile k + 1 (its DMA, then the stores of tile k - 1: vmcnt(2))
       if (k > 0) __builtin_amdgcn_s_waitcnt(fb_vmcnt(2));
       else __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
-      if (!(FB_ABL & 4)) convert(k + 1);
+      convert(k + 1);
       __builtin_amdgcn_s_waitcnt(0xC07F);   // its raw reads done before the raw buffer is refilled
-      if (k + 2 < nk && !(FB_ABL & 16)) issue_raw(k + 2);
+      if (k + 2 < nk) issue_raw(k + 2);
     }
     // weight gradient: rows j = 32 wv + 16 jb + lm, the tile's 32 samples, 8 column blocks of this half.  Operands
     // by transposed reads (rows +4: the same swizzle, so an immediate offset; the mid part FB_*PART further), the
@@ -3126,10 +3118,6 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
       const f16x8 B0 = join(rbx[ib & 1][0], rbx[ib & 1][1]), B1 = join(rbx[ib & 1][2], rbx[ib & 1][3]);
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
-        if (FB_ABL & 2) {
-          aw[jb][ib][0] += (float)A[jb][0][0] + (float)B0[1] + (float)B1[2];
-          continue;
-        }
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B0, aw[jb][ib], 0, 0, 0);
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B1, aw[jb][ib], 0, 0, 0);
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B0, aw[jb][ib], 0, 0, 0);
@@ -3160,8 +3148,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
           v[q] = valid ? ((d - cgm[q]) - xc * ckk[q]) * cis[q] * cga[q] : 0.0f;
           gmo = fmaxf(gmo, fabsf(v[q]));
         }
-        if (!(FB_ABL & 8))
-          reinterpret_cast<f32x4*>(hio + (size_t)tl * TILE_FLOATS)[(i >> 3) * 64 + sm + 32 * ((i >> 2) & 1)] = v;
+        reinterpret_cast<f32x4*>(hio + (size_t)tl * TILE_FLOATS)[(i >> 3) * 64 + sm + 32 * ((i >> 2) & 1)] = v;
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
