@@ -2832,6 +2832,8 @@ constexpr int FB_GPART = 32 * FB_GP, FB_XPART = 32 * FB_XP;
 constexpr int FB_BUF = 2 * FB_GPART + 2 * FB_XPART;       // 48 KiB per tile
 constexpr int FB_PAIRS = 128;
 constexpr size_t FB_LDS = 3 * (size_t)FB_BUF + 7 * 128 * sizeof(float);   // split + 2 raw tiles + constants
+constexpr size_t FB_LDS_OUT = FB_LDS + (4 * 256 + 8 * 64) * sizeof(float);  // + occ_out / BatchNorm 7 constants,
+                                                                            //   dL/dlogit slots
 
 // 16-byte chunk c of row r sits at c ^ f(r), f(r) = 2 (r & 3 | b << 2) | p with p = bit 2 of r and b = bit 2 ^ bit 3:
 // sixteen distinct values over a row block of 16 (the split writes: 32 lanes = 16 rows x two 8-byte halves of one
@@ -2903,6 +2905,48 @@ __global__ void k_pack_dgrad_h16(NofParamsDev P, const int* __restrict__ sw, f16
 struct GammaOff {
   int64_t g[8];
 };
+
+// max |dL/dlogit| over the chunk (float bits, into a zeroed word): k_out_prep's bound on |g_7|
+__global__ __launch_bounds__(256) void k_out_gabs(const float* __restrict__ g, int64_t n, unsigned* __restrict__ out) {
+  float m = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    m = fmaxf(m, fabsf(g[i]));
+  m = wave_max_f(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// occ_out + BatchNorm 7 backward constants for k_bwd_fused<0, true> (one block of 256 threads: k_out_bwd_grad's
+// prologue on the fold's occ_out statistics acc = (Sigma dL/dlogit (h_7 - mean_7), Sigma dL/dlogit)), the output
+// layer's and BatchNorm 7's parameter gradients, and the bound |g_7[f]| <= ((|gvmax w_out| + |gm|) + sqrt(n) sigma
+// |kk|) invstd |gamma| (|h_7 - mean_7| <= sqrt(n) sigma, Samuelson) as the layer's operand-scale maximum
+__global__ __launch_bounds__(256) void k_out_prep(const float* __restrict__ coef7, const float* __restrict__ gamma,
+                                                  const float* __restrict__ wout, const double* __restrict__ acc,
+                                                  int64_t n, double* __restrict__ d_gamma, double* __restrict__ d_beta,
+                                                  double* __restrict__ d_wout, double* __restrict__ d_bout,
+                                                  const unsigned* __restrict__ gvmax, float* __restrict__ ocst,
+                                                  unsigned* __restrict__ gmax7) {
+  __shared__ float wmax[4];
+  const int k = threadIdx.x;
+  const double A = acc[k], G0 = acc[256];
+  const float wo = wout[k], invstd = coef7[256 + k], ga = gamma[k];
+  const double S1 = (double)wo * G0, dotp = (double)wo * A;
+  const float gm = (float)(S1 / (double)n), kk = (((float)dotp * invstd) * invstd) / (float)n;
+  const float sg = invstd * ga;
+  ocst[k] = wo * sg;
+  ocst[256 + k] = gm * sg;
+  ocst[512 + k] = coef7[k];
+  ocst[768 + k] = kk * sg;
+  d_gamma[k] += dotp * (double)invstd;
+  d_beta[k] += S1;
+  d_wout[k] += (double)coef7[512 + k] * A + (double)coef7[768 + k] * G0;
+  if (k == 0) d_bout[0] += G0;
+  const float gvm = __uint_as_float(*gvmax);
+  float b = ((fabsf(gvm * wo) + fabsf(gm)) + sqrtf((float)n) / invstd * fabsf(kk)) * invstd * fabsf(ga) * 1.001f;
+  b = wave_max_f(b);
+  if ((k & 63) == 0) wmax[k >> 6] = b;
+  __syncthreads();
+  if (k == 0) *gmax7 = __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
+}
 __global__ void k_fb_bnb(FoldBnBwd F, int64_t c, int64_t n, const float* __restrict__ coef,
                          float* __restrict__ bnb, double* __restrict__ gacc, GammaOff go) {
   const int k = blockIdx.x, i = threadIdx.x;
@@ -2923,18 +2967,26 @@ __device__ __forceinline__ constexpr int fb_vmcnt(int n) {   // s_waitcnt vmcnt(
   return (n & 15) | ((n >> 4) << 14) | 0x0F70;
 }
 
-template <int LAY>
+// OUT (layer 7 only): g_7 = dL/dh_7 is not read from HBM but made in LDS from h_7 (gin, DMA'd as the raw tile) and
+// the chunk's dL/dlogit (ograd): g_7 = (dL/dlogit A - B) - (h_7 - mean_7) K with k_out_prep's per-column A = w_out s,
+// B = gm s, K = kk s, s = invstd gamma_7 (k_out_bwd_grad's terms, the same cancellation order), and the operand scale
+// comes from k_out_prep's bound on |g_7| instead of a recorded maximum: 1 KiB per sample less written and read than
+// producing g_7 first.
+template <int LAY, bool OUT>
 __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ gin, float* hio,
                                                        const f16x8* __restrict__ wt, const int* __restrict__ sw,
                                                        int layer, int64_t n, const float* __restrict__ coefp,
                                                        const float* __restrict__ bnb,
                                                        const float* __restrict__ gamma,
                                                        const unsigned* __restrict__ gmax_in,
-                                                       unsigned* __restrict__ gmax_out, float* __restrict__ part) {
+                                                       unsigned* __restrict__ gmax_out, float* __restrict__ part,
+                                                       const float* __restrict__ ograd,
+                                                       const float* __restrict__ ocst) {
   constexpr int C = WgradCfg<LAY>::C, COL = LAY == 2 ? 64 : 0;
   extern __shared__ __attribute__((aligned(16))) char fb[];
   // LDS: split operands of tiles k & 1 (two buffers), the raw tile (one buffer), constants
   float* const cst = reinterpret_cast<float*>(fb + 3 * FB_BUF);     // [csc | cun | gm | kk | invstd | gamma | mu][128]
+  float* const ocs = cst + 7 * 128;   // OUT: [A | B | mean | K][256], then per wave 64 dL/dlogit
   const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int bid = (int)blockIdx.x, hf = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
@@ -2955,6 +3007,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     cst[640 + t] = gamma[c];
     cst[768 + t] = coefp[c];
   }
+  if constexpr (OUT)
+    for (int i = t; i < 4 * 256; i += 512) ocs[i] = ocst[i];
   unsigned gmx = 0;
   for (int i = 0; i < GMAX_SLOTS; ++i) gmx = max(gmx, gmax_in[i]);   // (uniform loads)
   const int eg = tile_scale_exp(__uint_as_float(gmx));
@@ -2974,11 +3028,20 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
   // 2 w + m and later splits exactly those rows, so a wave waits only for its own DMA.  Split map of wave w's
   // instruction m: lane l takes sample 16 sb + (l & 15) (sb = m & 1), half (l >> 4) & 1 of row 4 w + 2 (m >> 1) +
   // (l >> 5) (g) or 2 w + (l >> 5) (x, sb = m): the raw reads and the split writes conflict-free
+  // OUT: the tile's 32 dL/dlogit, DMA'd with the raw rows into this wave's own 256-byte slot (lane l: sample l & 31)
+  float* const gvs = ocs + 4 * 256 + 64 * wv;
   auto issue_raw = [&](int k) {
     const int tl = pr + k * npair;
     char* rb = fb + 2 * (size_t)FB_BUF;
-    const float* gsrc = gin + (size_t)tl * TILE_FLOATS + lane * 4;
-    const float* xsrc = hio + (size_t)tl * TILE_FLOATS + 16 * hf * 256 + lane * 4;
+    int ln = lane;
+    if constexpr (OUT) {
+      asm volatile("" : "+v"(ln));   // (OUT: lane addresses recomputed per tile -- its extra registers would spill)
+      const int64_t s0 = (int64_t)tl * 32 + (ln & 31);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ograd + (s0 < n ? s0 : n - 1)),
+                                       (__attribute__((address_space(3))) void*)gvs, 4, 0, 0);
+    }
+    const float* gsrc = gin + (size_t)tl * TILE_FLOATS + ln * 4;
+    const float* xsrc = hio + (size_t)tl * TILE_FLOATS + 16 * hf * 256 + ln * 4;
 #pragma unroll
     for (int m = 0; m < 4; ++m) fb_glds16(gsrc + (4 * wv + m) * 256, rb + (4 * wv + m) * 1024);
 #pragma unroll
@@ -3020,6 +3083,26 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
       *reinterpret_cast<s16x4*>(sp + 2 * FB_GPART + FB_XPART + o) = p1;
     }
   };
+  // OUT: this wave's raw rows of tile k (h_7, as DMA'd) -> g_7 in place, before convert splits them; run where
+  // the data-gradient accumulators are not live yet (the top of the tile before k)
+  auto out_rows = [&]() {
+    char* rb = fb + 2 * (size_t)FB_BUF;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));   // addresses recomputed here, not held in registers across the tile loop
+    const float gv = gvs[ln & 31];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 4 * wv + j, f = 8 * row + 4 * (ln >> 5);
+      f32x4* rp = reinterpret_cast<f32x4*>(rb + (row * 64 + ln) * 16);
+      const f32x4 r = *rp;
+      const f32x4 ca = *reinterpret_cast<const f32x4*>(ocs + f), cb = *reinterpret_cast<const f32x4*>(ocs + 256 + f);
+      const f32x4 mu = *reinterpret_cast<const f32x4*>(ocs + 512 + f), ck = *reinterpret_cast<const f32x4*>(ocs + 768 + f);
+      f32x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (gv * ca[q] - cb[q]) - (r[q] - mu[q]) * ck[q];
+      *rp = o;
+    }
+  };
   f32x4 aw[2][8];
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb)
@@ -3035,6 +3118,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
   if (nk > 0) {
     issue_raw(0);
     __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+    if constexpr (OUT) out_rows();
     convert(0);
     if (nk > 1) issue_raw(1);
   }
@@ -3045,6 +3129,13 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
     const char* gb = sp;
     const char* xb = sp + 2 * FB_GPART;
+    if constexpr (OUT) {   // tile k + 1's g_7 rows (its DMA, then the stores of tile k - 1: vmcnt(2))
+      if (k + 1 < nk) {
+        if (k > 0) __builtin_amdgcn_s_waitcnt(fb_vmcnt(2));
+        else __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+        out_rows();
+      }
+    }
     // data gradient: this wave's 16 input features x 32 samples
     f32x4 ad[2] = {f32x4{}, f32x4{}};
 #pragma unroll
@@ -3237,6 +3328,7 @@ struct BwdWs {
   unsigned* pbound;   // k_pos_bound's result (float bits)
   f16x8* wth16;       // W^T image of k_bwd_fused (7 layers)
   float* bnb;         // BatchNorm 0..6 backward constants of the chunk (k_fb_bnb)
+  float* ocst;        // occ_out / BatchNorm 7 backward constants of the chunk (k_out_prep: [A | B | mean | K][256])
   size_t bytes;
 };
 
@@ -3260,6 +3352,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t otm0 = take(tiles * 8 * sizeof(float)), otm1 = take(tiles * 8 * sizeof(float));
   const size_t opb = take(sizeof(unsigned));
   const size_t owt16 = take(7 * HW_H * sizeof(f16x8)), obnb = take(7 * 512 * sizeof(float));
+  const size_t oocst = take(4 * 256 * sizeof(float));
   char* b = (char*)base;
   BwdWs w;
   w.wth = (f16x8*)(b + owt);
@@ -3282,6 +3375,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.pbound = (unsigned*)(b + opb);
   w.wth16 = (f16x8*)(b + owt16);
   w.bnb = (float*)(b + obnb);
+  w.ocst = (float*)(b + oocst);
   w.bytes = off;
   return w;
 }
@@ -3352,10 +3446,12 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                         hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)FB_LDS));
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)FB_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)FB_LDS_OUT));
     attr = true;
   }
   const double dn = (double)n;
@@ -3369,25 +3465,32 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
     for (int L = 0; L < 8; ++L) go.g[L] = G.g[L];
     hipLaunchKernelGGL(k_fb_bnb, dim3(7), dim3(256), 0, s, FB, ci, n, ws.coef, ws.bnb, ws.gacc, go);
     PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257 + GMAX_DBL) * sizeof(double), s));
-    hipLaunchKernelGGL(k_out_bwd_grad, dim3(eg), dim3(256), 0, s, grad + c0, (const float*)nullptr, hh[7], n,
-                       ws.coef + 7 * 1024, P.bn_w[7], P.out_w, FB.oacc + ci * 257, ws.gacc + G.g[7],
-                       ws.gacc + G.be[7], ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0], (float*)nullptr,
-                       ws.gmax + 7 * GMAX_SLOTS, 1);
+    // occ_out + BatchNorm 7 on the fold's occ_out statistics; g_7 itself is made inside layer 7's k_bwd_fused.
+    // max |dL/dlogit| goes to the first word of the output-statistics copies (zeroed above; the one-pass backward
+    // takes those statistics from the fold)
+    unsigned* gvmax = reinterpret_cast<unsigned*>(ws.ostat);
+    hipLaunchKernelGGL(k_out_gabs, dim3(eg < 256 ? eg : 256), dim3(256), 0, s, grad + c0, n, gvmax);
+    hipLaunchKernelGGL(k_out_prep, dim3(1), dim3(256), 0, s, ws.coef + 7 * 1024, P.bn_w[7], P.out_w,
+                       FB.oacc + ci * 257, n, ws.gacc + G.g[7], ws.gacc + G.be[7], ws.gacc + G.wo, ws.gacc + G.bo,
+                       gvmax, ws.ocst, ws.gmax + 7 * GMAX_SLOTS);
   }
   const unsigned fbg = (unsigned)(2 * FB_PAIRS);
   for (int L = 7; L >= 1; --L) {
     const float* coefp = ws.coef + 1024 * (L - 1);
-    const float* gin = L == 7 ? ws.g[0] : hh[L];
+    const float* gin = hh[L];   // layer 7: h_7, from which k_bwd_fused<0, true> makes g_7
     {
       ProfScope ps(s, PT_BWD_FUSED, 2.0 * 2.0 * 256.0 * 256.0 * dn, 3072.0 * dn);
-      if (L == 4)
-        hipLaunchKernelGGL(k_bwd_fused<2>, dim3(fbg), dim3(512), FB_LDS, s, gin, hh[L - 1],
-                           ws.wth16 + (size_t)(L - 1) * HW_H, ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1),
-                           P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS, ws.gmax + (L - 1) * GMAX_SLOTS, ws.part);
+      auto launch = [&](auto kern, size_t lds) {
+        hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), lds, s, gin, hh[L - 1], ws.wth16 + (size_t)(L - 1) * HW_H,
+                           ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1), P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS,
+                           ws.gmax + (L - 1) * GMAX_SLOTS, ws.part, grad + c0, (const float*)ws.ocst);
+      };
+      if (L == 7)
+        launch(k_bwd_fused<0, true>, FB_LDS_OUT);
+      else if (L == 4)
+        launch(k_bwd_fused<2, false>, FB_LDS);
       else
-        hipLaunchKernelGGL(k_bwd_fused<0>, dim3(fbg), dim3(512), FB_LDS, s, gin, hh[L - 1],
-                           ws.wth16 + (size_t)(L - 1) * HW_H, ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1),
-                           P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS, ws.gmax + (L - 1) * GMAX_SLOTS, ws.part);
+        launch(k_bwd_fused<0, false>, FB_LDS);
     }
     if (L == 4) {   // the skip layer's encoding columns on g_4 (its store slot), into the same partials
       ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
