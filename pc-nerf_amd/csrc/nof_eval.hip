@@ -263,13 +263,14 @@ __device__ __forceinline__ void eh_split8(const float (&v)[8], eh_f16x8& hi, eh_
 }
 
 // ---- k_nof_eval_h3: the split network (every fp32 product as hi*hi + hi*mid + mid*hi of fp16 parts, fp32
-// accumulation), fused over all 9 layers for a block of 96 samples with the work split over NEURONS: wave w owns
-// neurons 64w .. 64w + 63 of every layer for all 96 samples, so each wave streams only its own neurons' weights
-// from L2 (a 2-slot register ring, one k-step of prefetch, no barrier) and each A operand feeds 6 sample blocks;
+// accumulation), fused over all 9 layers for a block of 16 EH3_SB samples (48) with the work split over NEURONS: wave w
+// owns neurons 64w .. 64w + 63 of every layer for all the block's samples, so each wave streams only its own neurons'
+// weights from L2 (a 2-slot register ring, one k-step of prefetch, no barrier) and each A operand feeds EH3_SB sample
+// blocks; two workgroups per CU;
 // the layer outputs go through LDS as the next layer's split B operands ([k-step][sample block][part][lane],
-// 96 KiB), two barriers per layer.  The encoding lives in LDS as layer 0's split B operands; layer 4 re-splits it
+// 16 KiB per sample block), two barriers per layer.  The encoding lives in LDS as layer 0's split B operands; layer 4 re-splits it
 // (hi + mid is exact in fp32) at the per-sample scale it shares with h3.
-// On v_mfma_f32_16x16x32_f16: 4 neuron blocks x 6 sample blocks of 16, k-steps of 32 features.  Against the same
+// On v_mfma_f32_16x16x32_f16: 4 neuron blocks x EH3_SB sample blocks of 16, k-steps of 32 features.  Against the same
 // block on 32x32x16 (2 x 3 blocks of 32, k-steps of 16; round 3's k_nof_eval_h2, in git history) it is 4-7 %
 // faster in the train query and 1-2 % in the eval query (profiles/r03l_variants_eval_*.json): the kernel runs
 // power-limited (DESIGN (f)), and at the same issue rate the smaller shape draws less power per FLOP
@@ -317,10 +318,14 @@ __global__ void k_pack_eval_h3(NofParamsDev P, float* __restrict__ out) {
   reinterpret_cast<eh_f16x8*>(out + OFF_EH)[idx] = v;
 }
 
-// 16-sample blocks per workgroup (LDS: 20.5 KiB each).  Measured in one process against 6: 7 (the most the 160 KiB
-// hold, 14 % less weight stream per sample) -2 % / +1 % on the train query on two boxes and +7 % on the eval query
-// (profiles/r03l_variants_eval_sb7.json, _sb.json), 5: +3 % / +9 %
-constexpr int EH3_SB = 6;
+// 16-sample blocks per workgroup, and workgroups per CU.  Three blocks (77.5 KiB of LDS in the train form) let TWO
+// workgroups share a CU (two waves per SIMD, <= 256 registers each, no spills), so one workgroup's layer transitions
+// (barriers, epilogue, split) and prologue run under the other's MFMAs: against one workgroup of 6 blocks per CU,
+// store-writing train query 87.5 -> 78.6 ms and eval query 64.0 -> 61.7 ms at 25.2M samples, bit-identical; MfmaUtil
+// 38.9 -> 55.3 % / 49.4 -> 61.7 % (profiles/r04_occupancy_*.json; the clock drops ~20 %: the board's power limit).
+// One workgroup per CU: 5, 7 or 3 blocks all slower than 6 (profiles/r03l_variants_eval_sb*.json, r04_occupancy_ab).
+constexpr int EH3_SB = 3;
+constexpr int EH3_WG_PER_CU = 2;
 // k_nof_eval_h3: weight-ring slots (prefetch distance EH3_RING - 1 k-steps of 32; a 4-slot ring: +7 %)
 constexpr int EH3_RING = 2;
 // The store-writing train query writes the activation store nontemporal (streamed past L2, which holds the weight
@@ -337,12 +342,12 @@ constexpr int EH3_RING = 2;
 // batch variance <= gamma_k^2, so no sample exceeds sqrt(n) |gamma_k| + |beta_k| (Samuelson), and that bound fixes a
 // per-layer power-of-two scale sxB[L] in advance (k_tf_coeffs): no per-sample maxima, no exchange of them between
 // the waves.  Only the encoding (layers 0 and 4) keeps a per-sample scale, min(its own, sxB[3]).  blockIdx.y is the
-// BatchNorm chunk, blockIdx.x the 96-sample block inside it, so no block straddles two chunks.
+// BatchNorm chunk, blockIdx.x the 16 EH3_SB-sample block inside it, so no block straddles two chunks.
 // coef per chunk: [L][alpha 256 | beta'' 256] floats, then sxB[8] as int (TQ_COEF_FLOATS floats per chunk).
 // TR with an activation store (hst, chunks below store_chunks): each layer's raw output W_L x + b_L (the layered
 // kernels' stored h, nof_train.hip StoreChunk) is written before the BatchNorm fma.
 template <bool TR>
-__global__ __launch_bounds__(256, 1) void k_nof_eval_h3(const float* __restrict__ rays, int stride,
+__global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float* __restrict__ rays, int stride,
                                                         const float* __restrict__ z, int64_t total, int S,
                                                         const float* __restrict__ ein, const float* __restrict__ W,
                                                         float* __restrict__ p_out, const float* __restrict__ coef,

@@ -3345,7 +3345,8 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   for (int i = 0; i < 2; ++i) og[i] = take(tiles * TILE_FLOATS * 4);
   const size_t oenc = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
-  const size_t oc = take(8 * 1024 * 4), op = take(WG_BLOCKS * WgradCfg<2>::PART * 4);
+  // partials: up to 2 WG_BLOCKS records of the skip layer's layout (its encoding columns, two workgroups per CU)
+  const size_t oc = take(8 * 1024 * 4), op = take(2 * WG_BLOCKS * WgradCfg<2>::PART * 4);
   const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257 + GMAX_DBL) * 8), oa = take((size_t)gacc_layout().total * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
   const size_t owt = take(7 * HW_H * sizeof(f16x8));
@@ -3456,7 +3457,7 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   }
   const double dn = (double)n;
   const int64_t ntiles = (n + 31) / 32;
-  const unsigned wblocks = (unsigned)(ntiles < WG_BLOCKS ? ntiles : WG_BLOCKS);
+  const unsigned wb0 = (unsigned)std::min<int64_t>(2 * ntiles, 2 * WG_BLOCKS);   // encoding-column workgroups
   const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
   {
     ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
@@ -3492,21 +3493,21 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
       else
         launch(k_bwd_fused<0, false>, FB_LDS);
     }
-    if (L == 4) {   // the skip layer's encoding columns on g_4 (its store slot), into the same partials
+    if (L == 4) {   // the skip layer's encoding columns on g_4 (its store slot), into the same partials, two
+                    // workgroups per CU like layer 0's
       ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
-      launch_wgrad_b3<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[4], hh[3], coefp,
+      launch_wgrad_b3<2>(wb0, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[4], hh[3], coefp,
                          ws.gmax + 4 * GMAX_SLOTS, ws.part, ws.pbound, false, true);
     }
     ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0);
     if (L == 4)
       hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[4],
-                         coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + S12_LAYER * L, (int)wblocks);
+                         coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + S12_LAYER * L, (int)wb0);
     else
       hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[L],
                          coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12 + S12_LAYER * L, FB_PAIRS);
   }
   // layer 0 on the encoding (g_0 in its store slot), two workgroups per CU
-  const unsigned wb0 = (unsigned)std::min<int64_t>(2 * ntiles, 2 * WG_BLOCKS);
   {
     ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
     launch_wgrad_b3<1>(wb0, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[0], nullptr, nullptr,

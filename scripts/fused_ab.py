@@ -44,8 +44,10 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     p = torch.empty_like(z)
     first = next(iter(Ls.values()))
-    def need(L):   # the fused query's state (pcnerf_nof_train_fused_bytes where the library has it)
-        f = getattr(L, "pcnerf_nof_train_fused_bytes", None) or L.pcnerf_nof_train_fold_bytes
+    def need(L):   # the fused query's state: the fold's full layout when the store is written (the backward reads
+        # it), else pcnerf_nof_train_fused_bytes where the library has it
+        f = None if os.environ.get("FA_STORE") == "1" else getattr(L, "pcnerf_nof_train_fused_bytes", None)
+        f = f or L.pcnerf_nof_train_fold_bytes
         f.restype, f.argtypes = ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64]
         return f(n * S, chunk)
     ws = torch.empty(max(need(L) for L in Ls.values()), dtype=torch.uint8, device=dev)
