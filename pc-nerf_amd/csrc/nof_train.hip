@@ -3034,8 +3034,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     const int tl = pr + k * npair;
     char* rb = fb + 2 * (size_t)FB_BUF;
     int ln = lane;
+    asm volatile("" : "+v"(ln));   // lane addresses recomputed per tile: held across the loop they would spill
     if constexpr (OUT) {
-      asm volatile("" : "+v"(ln));   // (OUT: lane addresses recomputed per tile -- its extra registers would spill)
       const int64_t s0 = (int64_t)tl * 32 + (ln & 31);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ograd + (s0 < n ? s0 : n - 1)),
                                        (__attribute__((address_space(3))) void*)gvs, 4, 0, 0);
