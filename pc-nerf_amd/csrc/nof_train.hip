@@ -2958,9 +2958,10 @@ __global__ void k_fb_bnb(FoldBnBwd F, int64_t c, int64_t n, const float* __restr
   gacc[go.g[k] + i] += dotp * (double)invstd;
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void fb_glds16(const void* g, void* l) {   // 16 B per lane -> l + 16 lane (LDS-DMA)
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, AUX);
 }
 
 __device__ __forceinline__ constexpr int fb_vmcnt(int n) {   // s_waitcnt vmcnt(n) alone (gfx9 encoding)
@@ -3045,7 +3046,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
 #pragma unroll
     for (int m = 0; m < 4; ++m) fb_glds16(gsrc + (4 * wv + m) * 256, rb + (4 * wv + m) * 1024);
 #pragma unroll
-    for (int m = 0; m < 2; ++m) fb_glds16(xsrc + (2 * wv + m) * 256, rb + 32 * 1024 + (2 * wv + m) * 1024);
+    for (int m = 0; m < 2; ++m)
+      fb_glds16<2>(xsrc + (2 * wv + m) * 256, rb + 32 * 1024 + (2 * wv + m) * 1024);   // (nt: read once)
   };
   const int sl = lane & 15, sh = (lane >> 4) & 1, sr = lane >> 5;
   auto convert = [&](int k) {   // raw tile k -> split buffer k & 1 (this wave's rows)
@@ -3124,7 +3126,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
   __builtin_amdgcn_s_barrier();
-  for (int k = 0; k < nk; ++k) {
+  // one tile: data gradient, split of tile k + 1, weight gradient, epilogue (the second wave of each SIMD running
+  // the phases in another order -- weight gradient first, or split first -- measured +2 %,
+  // profiles/r04_variants_bwd_*.txt)
+  auto tile = [&](int k) {
     const int tl = pr + k * npair;
     const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
     const char* gb = sp;
@@ -3138,6 +3143,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     }
     // data gradient: this wave's 16 input features x 32 samples
     f32x4 ad[2] = {f32x4{}, f32x4{}};
+    auto dgrad = [&]() {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
@@ -3150,6 +3156,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
         ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], bh, ad[sb], 0, 0, 0);
       }
     }
+    };
+    auto split_next = [&]() {
     if (k + 1 < nk) {   // this wave's rows of tile k + 1 (its DMA, then the stores of tile k - 1: vmcnt(2))
       if (k > 0) __builtin_amdgcn_s_waitcnt(fb_vmcnt(2));
       else __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
@@ -3157,6 +3165,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
       __builtin_amdgcn_s_waitcnt(0xC07F);   // its raw reads done before the raw buffer is refilled
       if (k + 2 < nk) issue_raw(k + 2);
     }
+    };
+    auto wgrad = [&]() {
     // weight gradient: rows j = 32 wv + 16 jb + lm, the tile's 32 samples, 8 column blocks of this half.  Operands
     // by transposed reads (rows +4: the same swizzle, so an immediate offset; the mid part FB_*PART further), the
     // next column block's read while the current one multiplies
@@ -3214,6 +3224,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B0, aw[jb][ib], 0, 0, 0);
       }
     }
+    };
+    auto epilogue = [&]() {
     // epilogue: dL/dy -> BatchNorm L-1 backward -> g_{L-1} over this tile's h_{L-1} (input features
     // 128 hf + 16 wv + 4 kg .. + 3 of sample 16 sb + lm): two 16-byte stores per lane
     {
@@ -3239,12 +3251,19 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
           v[q] = valid ? ((d - cgm[q]) - xc * ckk[q]) * cis[q] * cga[q] : 0.0f;
           gmo = fmaxf(gmo, fabsf(v[q]));
         }
-        reinterpret_cast<f32x4*>(hio + (size_t)tl * TILE_FLOATS)[(i >> 3) * 64 + sm + 32 * ((i >> 2) & 1)] = v;
+        f32x4* dst = reinterpret_cast<f32x4*>(hio + (size_t)tl * TILE_FLOATS) + (i >> 3) * 64 + sm + 32 * ((i >> 2) & 1);
+        __builtin_nontemporal_store(v, dst);   // streamed past L2, which keeps the g tiles for the pair
       }
     }
+    };
+    dgrad();
+    split_next();
+    wgrad();
+    epilogue();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();   // every wave done with split buffer k & 1 and has filled (k + 1) & 1
-  }
+    };
+  for (int k = 0; k < nk; ++k) tile(k);
   gmo = wave_max_f(gmo);
   if (lane == 0) atomicMax(gmax_out + ((bid * 8 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
   // G partial of pair pr: rows j = 32 wv + 16 jb + 4 kg + r, columns 128 hf + 16 ib + lm (x scale undone per column)
