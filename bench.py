@@ -161,16 +161,19 @@ def prof_read(L, tag):
     return t.value, n.value, f.value, b.value
 
 
-def pmc_traffic(kernel_name: str):
+def pmc_traffic(kernel_name: str, line: str = None):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json) and
-    where they come from (profile file + the commit it was measured at), or (None, None)."""
+    where they come from (profile file + the commit it was measured at), or (None, None).  ``line``: the bench line
+    whose profile to prefer (``<kernel>@<line>`` entries: the same kernel moves different bytes in different lines,
+    e.g. the train query with and without the activation store)."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
         return None, None
-    v = d.get("kernels", d).get(kernel_name, {})
+    ks = d.get("kernels", d)
+    v = ks.get(f"{kernel_name}@{line}") or ks.get(kernel_name, {}) if line else ks.get(kernel_name, {})
     meta = d.get("_meta", {})
     return v.get("hbm_bytes_per_launch"), ({"file": "profiles/pmc_traffic.json", "head": v.get("head", meta.get("head")),
                                             "profile": v.get("profile", meta.get("profile"))} if v else None)
@@ -602,7 +605,7 @@ def kernel_report(L, a, train_math, eval_math=None):
                   (19, "bwd_fused")):
         tm, n, f, b = prof_read(L, t)
         if n:
-            tr, src = pmc_traffic(pmc_names.get(t, ""))
+            tr, src = pmc_traffic(pmc_names.get(t, ""), a.mode)
             kernels[nm] = {"kernel": pmc_names.get(t), "ms_per_step": round(tm, 3), "launches_per_step": n,
                            "avg_us": round(1e3 * tm / n, 2),
                            "TFLOP/s": round(f / (tm * 1e-3) / 1e12, 2) if f else None,
@@ -612,7 +615,7 @@ def kernel_report(L, a, train_math, eval_math=None):
     avg_s = ktime_ms * 1e-3 / max(klaunch, 1)
     achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
     gbs = kbytes / max(klaunch, 1) / avg_s / 1e9
-    traffic, traffic_src = pmc_traffic(kname)
+    traffic, traffic_src = pmc_traffic(kname, a.mode)
     nprod = nterm   # k_wgrad_b3 too: f16x2 parts, nterm products (the six-product bf16x3 form is a build option)
     if a.fold:   # no MLP left: the query moves 8 B per sample (+ ray rows) and is bound by its sincos (VALU)
         roof = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

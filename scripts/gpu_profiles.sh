@@ -3,8 +3,8 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${TAG:-r03m}
-bash scripts/profile.sh ${TAG}_train_fwd --steps 3 --warmup 1 && \
-bash scripts/profile.sh ${TAG}_val --mode val --steps 3 --warmup 1 && \
-bash scripts/profile.sh ${TAG}_train_step --mode train_step --steps 2 --warmup 1
+bash scripts/profile.sh ${TAG}_train_fwd --steps 3 --warmup 1 --no-extra --no-ceiling && \
+bash scripts/profile.sh ${TAG}_val --mode val --steps 3 --warmup 1 --no-ceiling && \
+bash scripts/profile.sh ${TAG}_train_step --mode train_step --steps 2 --warmup 1 --no-ceiling
 rc=$?; echo "prof rc=$rc"
 exit $rc

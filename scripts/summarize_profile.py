@@ -84,10 +84,13 @@ def code_unchanged(since):
 kernels = {k: e for k, e in traffic.get("kernels", {}).items() if code_unchanged(e.get("head", meta.get("head")))}
 for k, e in kernels.items():
     e.setdefault("head", meta.get("head"))
+line = tag.split("_", 1)[1] if "_" in tag else None   # <prefix>_<bench line>, e.g. r04b_train_step
 for k, e in summary.items():
     if "hbm_bytes_per_launch" in e:
-        kernels[k] = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "avg_us": e["avg_us"], "profile": tag,
-                      "head": head}
+        ent = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"], "avg_us": e["avg_us"], "profile": tag, "head": head}
+        kernels[k] = ent
+        if line:   # the same kernel can move different bytes in different lines (bench.py prefers this entry)
+            kernels[f"{k}@{line}"] = dict(ent)
 profs = sorted({e["profile"] for e in kernels.values()})
 cmd = open(os.path.join(src, "command.txt")).read().strip() if os.path.exists(os.path.join(src, "command.txt")) else ""
 cmds = {t: c for t, c in meta.get("commands", {}).items() if t in profs}
