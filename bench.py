@@ -592,7 +592,7 @@ def kernel_report(L, a, train_math, eval_math=None):
               10: "k_wgrad<2>+k_wgrad<1>" if split else "k_wgrad<0>", 11: f"k_dgrad_h<{nterm}>" if split else "k_dgrad_ws",
               13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>",
               16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw", 18: "k_nof_eval_h3<true>",
-              19: "k_bwd_fused<0>"}
+              19: "k_bwd_fused<0,false>"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]

@@ -2066,10 +2066,12 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__
     const int nn = t - col_h;
     const size_t wi = (size_t)m * in_f + wcol_h + nn;
     dW[wi] += (double)coefp[512 + nn] * G + (double)coefp[768 + nn] * dbm;
-    const double w = (double)W[wi];
-    double* s12c = s12 + (m % S12_COPIES) * 512;   // 256 / COPIES blocks per address instead of 256
-    atomicAdd(&s12c[2 * nn], w * dbm);
-    atomicAdd(&s12c[2 * nn + 1], w * G);
+    if (s12) {   // (the two-pass backward's BatchNorm-backward sums; the one-pass backward passes none)
+      const double w = (double)W[wi];
+      double* s12c = s12 + (m % S12_COPIES) * 512;   // 256 / COPIES blocks per address instead of 256
+      atomicAdd(&s12c[2 * nn], w * dbm);
+      atomicAdd(&s12c[2 * nn + 1], w * G);
+    }
   }
   if (t == 0) db[m] += dbm;
 }
@@ -2898,15 +2900,7 @@ __global__ void k_pack_dgrad_h16(NofParamsDev P, const int* __restrict__ sw, f16
   out[idx] = v;
 }
 
-// BatchNorm k's backward constants for a chunk, k = 0..6 (grid 7 x 256 threads): mean(dL/dy) = 0 (exactly: dL/dy =
-// W_{k+1}^T g_{k+1} and g_{k+1} is a BatchNorm backward's output, zero-mean over the chunk), and
-// kk = Sigma dL/dy (h - mean) invstd^2 / n with Sigma dL/dy (h - mean) = dgamma / fl64(1/sqrt(var+eps)) from the fold
-// -- k_dgrad_h's ckk arithmetic on it; dgamma_k += that sum x invstd (k_dgrad_h's d_gamma), dbeta_k += 0.
-struct GammaOff {
-  int64_t g[8];
-};
-
-// max |dL/dlogit| over the chunk (float bits, into a zeroed word): k_out_prep's bound on |g_7|
+// max |dL/dlogit| over the chunk (float bits, into a zeroed word): k_fb_prep's bound on |g_7|
 __global__ __launch_bounds__(256) void k_out_gabs(const float* __restrict__ g, int64_t n, unsigned* __restrict__ out) {
   float m = 0.0f;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
@@ -2915,47 +2909,70 @@ __global__ __launch_bounds__(256) void k_out_gabs(const float* __restrict__ g, i
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-// occ_out + BatchNorm 7 backward constants for k_bwd_fused<0, true> (one block of 256 threads: k_out_bwd_grad's
-// prologue on the fold's occ_out statistics acc = (Sigma dL/dlogit (h_7 - mean_7), Sigma dL/dlogit)), the output
-// layer's and BatchNorm 7's parameter gradients, and the bound |g_7[f]| <= ((|gvmax w_out| + |gm|) + sqrt(n) sigma
-// |kk|) invstd |gamma| (|h_7 - mean_7| <= sqrt(n) sigma, Samuelson) as the layer's operand-scale maximum
-__global__ __launch_bounds__(256) void k_out_prep(const float* __restrict__ coef7, const float* __restrict__ gamma,
-                                                  const float* __restrict__ wout, const double* __restrict__ acc,
-                                                  int64_t n, double* __restrict__ d_gamma, double* __restrict__ d_beta,
-                                                  double* __restrict__ d_wout, double* __restrict__ d_bout,
-                                                  const unsigned* __restrict__ gvmax, float* __restrict__ ocst,
-                                                  unsigned* __restrict__ gmax7) {
+// Everything a stored chunk's one-pass backward needs before its first layer, in ONE launch of 8 blocks x 256
+// threads (block L, thread k = neuron k of layer L): BatchNorm L's forward coefficients from the chunk's stored
+// statistics (k_bn_save's arithmetic), then
+//   L < 7: BatchNorm L's backward constants from the fold (mean(dL/dy) = 0 exactly: dL/dy = W_{L+1}^T g_{L+1} and
+//          g_{L+1} is a BatchNorm backward's output, zero-mean over the chunk; kk = Sigma dL/dy (h - mean) invstd^2 / n
+//          with Sigma dL/dy (h - mean) = dgamma / fl64(1/sqrt(var+eps)) from the fold; dgamma_L += that sum x invstd),
+//   L = 7: occ_out + BatchNorm 7 (k_out_bwd_grad's prologue on the fold's occ_out statistics acc = (Sigma dL/dlogit
+//          (h_7 - mean_7), Sigma dL/dlogit)): k_bwd_fused<0, true>'s per-column constants, the output layer's and
+//          BatchNorm 7's parameter gradients, and the bound |g_7[f]| <= ((|gvmax w_out| + |gm|) + sqrt(n) sigma |kk|)
+//          invstd |gamma| (|h_7 - mean_7| <= sqrt(n) sigma, Samuelson) as layer 7's operand-scale maximum;
+// and layer L's |dL/dh| maximum slots zeroed for this chunk (block 7 after reading gvmax also re-zeroes it for the
+// next chunk's k_out_gabs).
+struct FbPrepOut {
+  int64_t g[8];                        // gacc offsets of dgamma per layer
+  double *d_beta7, *d_wout, *d_bout;   // occ_out / BatchNorm 7 parameter gradients
+};
+__global__ __launch_bounds__(256) void k_fb_prep(NofParamsDev P, const double* __restrict__ stats, int64_t n,
+                                                 float eps, float* __restrict__ coef, FoldBnBwd F, int64_t c,
+                                                 float* __restrict__ bnb, double* __restrict__ gacc, FbPrepOut o,
+                                                 const double* __restrict__ oacc, unsigned* __restrict__ gvmax,
+                                                 float* __restrict__ ocst, unsigned* __restrict__ gmax) {
   __shared__ float wmax[4];
-  const int k = threadIdx.x;
-  const double A = acc[k], G0 = acc[256];
-  const float wo = wout[k], invstd = coef7[256 + k], ga = gamma[k];
+  const int L = blockIdx.x, k = threadIdx.x;
+  const double s1 = stats[512 * L + 2 * k], s2 = stats[512 * L + 2 * k + 1];
+  const double m = s1 / (double)n;
+  double var = s2 / (double)n - m * m;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  float* cf = coef + 1024 * L;
+  cf[k] = (float)((double)P.lin_b[L][k] + m);
+  cf[256 + k] = invstd;
+  cf[512 + k] = invstd * P.bn_w[L][k];
+  cf[768 + k] = P.bn_b[L][k];
+  if (k < GMAX_SLOTS) gmax[L * GMAX_SLOTS + k] = 0u;
+  if (L < 7) {
+    const double rinv = F.sr[((int64_t)L * F.C + c) * 1024 + 256 + k];
+    const double dotp = F.dg[((int64_t)L * F.C + c) * 256 + k] / rinv;
+    bnb[512 * L + k] = 0.0f;
+    bnb[512 * L + 256 + k] = (((float)dotp * invstd) * invstd) / (float)n;
+    gacc[o.g[L] + k] += dotp * (double)invstd;
+    return;
+  }
+  const double A = oacc[k], G0 = oacc[256];
+  const float wo = P.out_w[k], ga = P.bn_w[7][k], mu = cf[k], al = cf[512 + k], be = cf[768 + k];
   const double S1 = (double)wo * G0, dotp = (double)wo * A;
   const float gm = (float)(S1 / (double)n), kk = (((float)dotp * invstd) * invstd) / (float)n;
   const float sg = invstd * ga;
   ocst[k] = wo * sg;
   ocst[256 + k] = gm * sg;
-  ocst[512 + k] = coef7[k];
+  ocst[512 + k] = mu;
   ocst[768 + k] = kk * sg;
-  d_gamma[k] += dotp * (double)invstd;
-  d_beta[k] += S1;
-  d_wout[k] += (double)coef7[512 + k] * A + (double)coef7[768 + k] * G0;
-  if (k == 0) d_bout[0] += G0;
+  gacc[o.g[7] + k] += dotp * (double)invstd;
+  o.d_beta7[k] += S1;
+  o.d_wout[k] += (double)al * A + (double)be * G0;
+  if (k == 0) o.d_bout[0] += G0;
   const float gvm = __uint_as_float(*gvmax);
-  float b = ((fabsf(gvm * wo) + fabsf(gm)) + sqrtf((float)n) / invstd * fabsf(kk)) * invstd * fabsf(ga) * 1.001f;
-  b = wave_max_f(b);
-  if ((k & 63) == 0) wmax[k >> 6] = b;
-  __syncthreads();
-  if (k == 0) *gmax7 = __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
-}
-__global__ void k_fb_bnb(FoldBnBwd F, int64_t c, int64_t n, const float* __restrict__ coef,
-                         float* __restrict__ bnb, double* __restrict__ gacc, GammaOff go) {
-  const int k = blockIdx.x, i = threadIdx.x;
-  const double rinv = F.sr[((int64_t)k * F.C + c) * 1024 + 256 + i];
-  const double dotp = F.dg[((int64_t)k * F.C + c) * 256 + i] / rinv;
-  const float invstd = coef[1024 * k + 256 + i];
-  bnb[512 * k + i] = 0.0f;
-  bnb[512 * k + 256 + i] = (((float)dotp * invstd) * invstd) / (float)n;
-  gacc[go.g[k] + i] += dotp * (double)invstd;
+  float bd = ((fabsf(gvm * wo) + fabsf(gm)) + sqrtf((float)n) / invstd * fabsf(kk)) * invstd * fabsf(ga) * 1.001f;
+  bd = wave_max_f(bd);
+  if ((k & 63) == 0) wmax[k >> 6] = bd;
+  __syncthreads();   // (also: every thread has read gvmax)
+  if (k == 0) {
+    gmax[7 * GMAX_SLOTS] = __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
+    *gvmax = 0u;
+  }
 }
 
 template <int AUX = 0>
@@ -2969,9 +2986,9 @@ __device__ __forceinline__ constexpr int fb_vmcnt(int n) {   // s_waitcnt vmcnt(
 }
 
 // OUT (layer 7 only): g_7 = dL/dh_7 is not read from HBM but made in LDS from h_7 (gin, DMA'd as the raw tile) and
-// the chunk's dL/dlogit (ograd): g_7 = (dL/dlogit A - B) - (h_7 - mean_7) K with k_out_prep's per-column A = w_out s,
+// the chunk's dL/dlogit (ograd): g_7 = (dL/dlogit A - B) - (h_7 - mean_7) K with k_fb_prep's per-column A = w_out s,
 // B = gm s, K = kk s, s = invstd gamma_7 (k_out_bwd_grad's terms, the same cancellation order), and the operand scale
-// comes from k_out_prep's bound on |g_7| instead of a recorded maximum: 1 KiB per sample less written and read than
+// comes from k_fb_prep's bound on |g_7| instead of a recorded maximum: 1 KiB per sample less written and read than
 // producing g_7 first.
 template <int LAY, bool OUT>
 __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ gin, float* hio,
@@ -3134,13 +3151,6 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
     const char* gb = sp;
     const char* xb = sp + 2 * FB_GPART;
-    if constexpr (OUT) {   // tile k + 1's g_7 rows (its DMA, then the stores of tile k - 1: vmcnt(2))
-      if (k + 1 < nk) {
-        if (k > 0) __builtin_amdgcn_s_waitcnt(fb_vmcnt(2));
-        else __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
-        out_rows();
-      }
-    }
     // data gradient: this wave's 16 input features x 32 samples
     f32x4 ad[2] = {f32x4{}, f32x4{}};
     auto dgrad = [&]() {
@@ -3161,6 +3171,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
     if (k + 1 < nk) {   // this wave's rows of tile k + 1 (its DMA, then the stores of tile k - 1: vmcnt(2))
       if (k > 0) __builtin_amdgcn_s_waitcnt(fb_vmcnt(2));
       else __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+      if constexpr (OUT) out_rows();   // (OUT: g_7 rows of tile k + 1 from its h_7 rows, in place)
       convert(k + 1);
       __builtin_amdgcn_s_waitcnt(0xC07F);   // its raw reads done before the raw buffer is refilled
       if (k + 2 < nk) issue_raw(k + 2);
@@ -3346,8 +3357,8 @@ struct BwdWs {
   unsigned* gmax;   // per layer L: GMAX_SLOTS partial maxima of the chunk's |dL/dh_L| (float bits; zeroed per chunk)
   unsigned* pbound;   // k_pos_bound's result (float bits)
   f16x8* wth16;       // W^T image of k_bwd_fused (7 layers)
-  float* bnb;         // BatchNorm 0..6 backward constants of the chunk (k_fb_bnb)
-  float* ocst;        // occ_out / BatchNorm 7 backward constants of the chunk (k_out_prep: [A | B | mean | K][256])
+  float* bnb;         // BatchNorm 0..6 backward constants of the chunk (k_fb_prep)
+  float* ocst;        // occ_out / BatchNorm 7 backward constants of the chunk (k_fb_prep: [A | B | mean | K][256])
   size_t bytes;
 };
 
@@ -3455,11 +3466,11 @@ static void launch_wgrad_b3(unsigned blocks, hipStream_t s, const float* rays, i
 
 extern "C" size_t pcnerf_nof_backward_workspace_bytes(int64_t chunk) { return carve_bwd(nullptr, chunk).bytes; }
 
-// One stored chunk through the one-pass backward: BatchNorm coefficients from the chunk's stored statistics, the
-// BatchNorm-backward constants from the fold (k_fb_bnb), occ_out + BatchNorm 7 (k_out_bwd_grad on the fold's occ_out
-// statistics: no statistics pass), then layers 7..1 each in ONE k_bwd_fused launch (g_{L-1} in place over
-// h_{L-1}) + the partial reduction, the skip layer's and layer 0's encoding columns (k_wgrad_b3 MODE 1 on g_4 and
-// g_0, which stay in their store slots).
+// One stored chunk through the one-pass backward: max |dL/dlogit| (k_out_gabs), then in one launch (k_fb_prep) the
+// BatchNorm coefficients from the chunk's stored statistics, the BatchNorm-backward constants from the fold and
+// occ_out + BatchNorm 7 on the fold's occ_out statistics (no statistics pass); then layers 7..1 each in ONE
+// k_bwd_fused launch (g_{L-1} in place over h_{L-1}; layer 7 makes g_7 from h_7) + the partial reduction, the skip
+// layer's and layer 0's encoding columns (k_wgrad_b3 MODE 1 on g_4 and g_0, which stay in their store slots).
 static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs& ws, const FoldBnBwd& FB, int64_t ci,
                         int64_t c0, int64_t n, const double* stats, float* const (&hh)[8], const float* rays,
                         int ray_stride, const float* z, int n_samples, const float* ein, float eps, const float* grad,
@@ -3479,20 +3490,20 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   const unsigned wb0 = (unsigned)std::min<int64_t>(2 * ntiles, 2 * WG_BLOCKS);   // encoding-column workgroups
   const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
   {
+    // max |dL/dlogit| (into the first word of the output-statistics copies, which the one-pass backward does not
+    // use: it takes those statistics from the fold; zero before the first chunk, re-zeroed by k_fb_prep), then
+    // every constant of the chunk's layers in one launch (k_fb_prep); g_7 itself is made inside layer 7's
+    // k_bwd_fused
     ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
-    hipLaunchKernelGGL(k_bn_save, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef);
-    GammaOff go;
-    for (int L = 0; L < 8; ++L) go.g[L] = G.g[L];
-    hipLaunchKernelGGL(k_fb_bnb, dim3(7), dim3(256), 0, s, FB, ci, n, ws.coef, ws.bnb, ws.gacc, go);
-    PCN_HIP(hipMemsetAsync(ws.s12, 0, (8 * S12_LAYER + OSTAT_COPIES * 257 + GMAX_DBL) * sizeof(double), s));
-    // occ_out + BatchNorm 7 on the fold's occ_out statistics; g_7 itself is made inside layer 7's k_bwd_fused.
-    // max |dL/dlogit| goes to the first word of the output-statistics copies (zeroed above; the one-pass backward
-    // takes those statistics from the fold)
     unsigned* gvmax = reinterpret_cast<unsigned*>(ws.ostat);
     hipLaunchKernelGGL(k_out_gabs, dim3(eg < 256 ? eg : 256), dim3(256), 0, s, grad + c0, n, gvmax);
-    hipLaunchKernelGGL(k_out_prep, dim3(1), dim3(256), 0, s, ws.coef + 7 * 1024, P.bn_w[7], P.out_w,
-                       FB.oacc + ci * 257, n, ws.gacc + G.g[7], ws.gacc + G.be[7], ws.gacc + G.wo, ws.gacc + G.bo,
-                       gvmax, ws.ocst, ws.gmax + 7 * GMAX_SLOTS);
+    FbPrepOut po;
+    for (int L = 0; L < 8; ++L) po.g[L] = G.g[L];
+    po.d_beta7 = ws.gacc + G.be[7];
+    po.d_wout = ws.gacc + G.wo;
+    po.d_bout = ws.gacc + G.bo;
+    hipLaunchKernelGGL(k_fb_prep, dim3(8), dim3(256), 0, s, P, stats, n, eps, ws.coef, FB, ci, ws.bnb, ws.gacc, po,
+                       FB.oacc + ci * 257, gvmax, ws.ocst, ws.gmax);
   }
   const unsigned fbg = (unsigned)(2 * FB_PAIRS);
   for (int L = 7; L >= 1; --L) {
@@ -3521,10 +3532,10 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
     ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0);
     if (L == 4)
       hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[4],
-                         coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], ws.s12 + S12_LAYER * L, (int)wb0);
+                         coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], (double*)nullptr, (int)wb0);
     else
       hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[L],
-                         coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], ws.s12 + S12_LAYER * L, FB_PAIRS);
+                         coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], (double*)nullptr, FB_PAIRS);
   }
   // layer 0 on the encoding (g_0 in its store slot), two workgroups per CU
   {
@@ -3552,6 +3563,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
   // the one-pass backward (k_bwd_fused) on the chunks the fused forward stored, under the split math of the fused
   // forward (f16x2, 3 products); every other chunk (recomputed) and every other math: the two-pass backward
   const bool fused = fstate && store && g_train_math == 1;
+  bool fused_zeroed = false;
   const bool recompute = !store || store_chunks < n_chunks || !fused;
   // the encoding operand's xyz columns are scaled by the largest |position| (device-side, k_pos_bound); the
   // layered forward that recomputes chunks splits them unscaled and needs the host-side range check
@@ -3587,6 +3599,10 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
     for (int L = 0; L < 8; ++L) hh[L] = kept ? sc.h[L] : ws.h[L];
     const double* stats = kept ? sc.stats : ws.stats;
     if (kept && fused) {
+      if (!fused_zeroed) {   // k_out_gabs's word (k_fb_prep re-zeroes it after every chunk)
+        PCN_HIP(hipMemsetAsync(ws.ostat, 0, sizeof(unsigned), s));
+        fused_zeroed = true;
+      }
       fused_chunk(P, G, ws, FB, ci, c0, n, stats, hh, rays, ray_stride, z, n_samples, ein, eps, grad, s);
       continue;
     }
