@@ -2582,8 +2582,13 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     if constexpr (EX) {   // the sample's ray origin, direction and z
       if (ein) return;
       const int64_t gs = sample_of(tile, hs);
-      const float* r = rays + (gs / S) * stride;
-      rv[2 * NI] = f32x4{r[0], r[1], r[2], r[3]};
+      // (32-bit division when it fits: the 64-bit one is a long emulated sequence per thread and half tile; the
+      // ray row's first four floats as one 4-byte-aligned vector load)
+      const int64_t ray = gs < 0x7fffffff ? (int64_t)((unsigned)gs / (unsigned)S) : gs / S;
+      const float* r = rays + ray * stride;
+      typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+      const f32x4u r4 = *reinterpret_cast<const f32x4u*>(r);
+      rv[2 * NI] = f32x4{r4[0], r4[1], r4[2], r4[3]};
       rv[2 * NI + 1] = f32x4{r[4], r[5], z[gs], 0.0f};
     }
   };
