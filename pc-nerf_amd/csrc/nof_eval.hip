@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void k_nof_eval(const float* __restrict__ rays
   if (ein) {
     load_embedding<0>(ein + gc * 63, h, e);
   } else {
-    const float* r = rays + (gc / S) * stride;
+    const float* r = rays + ray_of(gc, S) * stride;
     float p[3];
     sample_point(r, z[gc], p);
     encode_half(p, h, e);
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float*
   if (!ein && t < NS) {
     int64_t gs = s0 + t;
     if (gs >= send) gs = send - 1;
-    const float* r = rays + (gs / S) * stride;
+    const float* r = rays + ray_of(gs, S) * stride;
     rz = z[gs];
 #pragma unroll
     for (int m = 0; m < 6; ++m) rr[m] = r[m];
@@ -882,7 +882,7 @@ __global__ __launch_bounds__(256) void k_nof_eval_fold(const float* __restrict__
   } else {
     // the Embedding's 63 features (encode_half's arithmetic, each sincosf once) straight into the dot product
     float p[3];
-    sample_point(rays + (g / S) * stride, z[g], p);
+    sample_point(rays + ray_of(g, S) * stride, z[g], p);
     double part[6];   // six independent chains (sin / cos per coordinate), summed at the end
 #pragma unroll
     for (int m = 0; m < 3; ++m) {

@@ -124,7 +124,7 @@ __device__ __forceinline__ void sample_enc(const SampleSrc& q, int64_t g, float 
     f[63] = 0.0f;
   } else {
     float p[3];
-    sample_point(q.rays + (g / q.S) * q.stride, q.z[g], p);
+    sample_point(q.rays + ray_of(g, q.S) * q.stride, q.z[g], p);
     encode_full(p, f);
   }
 }
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
       if (ok)
         for (int f = 0; f < 63; ++f) dm = fmaxf(dm, fabsf(r[f] - sh0[f]));
     } else if (ok) {
-      sample_point(q.rays + ((c0 + i) / q.S) * q.stride, q.z[c0 + i], p);
+      sample_point(q.rays + ray_of(c0 + i, q.S) * q.stride, q.z[c0 + i], p);
 #pragma unroll
       for (int m = 0; m < 3; ++m) dm = fmaxf(dm, fabsf(p[m] - sh0[m]));
     }
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(256) void k_tf_gmoments(SampleSrc q, FoldDev F, con
       for (int f = 0; f < 63; ++f) put(f, r[f]);
     } else {
       float pt[3] = {0.0f, 0.0f, 0.0f};
-      if (ok) sample_point(q.rays + ((c0 + i) / q.S) * q.stride, q.z[c0 + i], pt);
+      if (ok) sample_point(q.rays + ray_of(c0 + i, q.S) * q.stride, q.z[c0 + i], pt);
 #pragma unroll
       for (int m = 0; m < 3; ++m) put(m, pt[m]);
 #pragma unroll 2

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
         e = enc_feats_row(ein + gs * 63, h, t >> 6);
       } else {
         float p[3];
-        sample_point(rays + (gs / S) * stride, z[gs], p);
+        sample_point(rays + ray_of(gs, S) * stride, z[gs], p);
         e = enc_feats(p, h, t >> 6);
       }
       xs[0][t] = e;
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(512, 1) void k_train_ws(const float* __restrict__ r
       if (ETIN && kg == KGT - 8 && more) ev = etin[(size_t)nxt * 512 + t];
       if (ETOUT && kg == 0 && more && !ein) {   // after the activations' registers are free
         const int64_t gs = sample_of(nxt);
-        const float* r = rays + (gs / S) * stride;
+        const float* r = rays + ray_of(gs, S) * stride;
 #pragma unroll
         for (int c = 0; c < 6; ++c) rr[c] = r[c];
         rr[6] = z[gs];
@@ -644,7 +644,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
         e = enc_feats_row(ein + gs * 63, hs, t >> 6);
       } else {
         float p[3];
-        sample_point(rays + (gs / S) * stride, z[gs], p);
+        sample_point(rays + ray_of(gs, S) * stride, z[gs], p);
         e = enc_feats(p, hs, t >> 6);
       }
       put_enc(0, e);
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(512, 1) void k_train_h(const float* __restrict__ ra
       if (ETIN && ks == KS - 4 && more) ev = etin[(size_t)P(nxt) * 512 + etix];
       if (ETOUT && ks == 0 && more && !ein) {
         const int64_t gs = sample_of(nxt);
-        const float* r = rays + (gs / S) * stride;
+        const float* r = rays + ray_of(gs, S) * stride;
 #pragma unroll
         for (int c = 0; c < 6; ++c) rr[c] = r[c];
         rr[6] = z[gs];
@@ -1104,7 +1104,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_gram(const float* __restrict__ r
       v = tid < 63 ? ein[c0 * 63 + tid] : 0.0f;
     } else {
       float p[3];
-      sample_point(rays + (c0 / S) * stride, z[c0], p);
+      sample_point(rays + ray_of(c0, S) * stride, z[c0], p);
       v = enc_feat1(p, tid);
     }
     sh0[tid] = v;
@@ -1130,7 +1130,7 @@ __global__ __launch_bounds__(256, 2) void k_enc_gram(const float* __restrict__ r
       f[63] = 0.0f;
     } else {
       float p[3];
-      sample_point(rays + ((c0 + se) / S) * stride, z[c0 + se], p);
+      sample_point(rays + ray_of(c0 + se, S) * stride, z[c0 + se], p);
       encode_full(p, f);
     }
     const int64_t tile = s >> 5;
@@ -1518,7 +1518,7 @@ __global__ __launch_bounds__(256) void k_pos_bound(const float* __restrict__ ray
     if (ein) {
       p[0] = ein[g * 63], p[1] = ein[g * 63 + 1], p[2] = ein[g * 63 + 2];
     } else {
-      sample_point(rays + (g / S) * stride, z[g], p);
+      sample_point(rays + ray_of(g, S) * stride, z[g], p);
     }
     m = fmaxf(m, fmaxf(fabsf(p[0]), fmaxf(fabsf(p[1]), fabsf(p[2]))));   // fmaxf drops NaN positions
   }
@@ -1955,7 +1955,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
         for (int f = jj; f < 64; f += 16) row[f] = f < 63 ? er[f] : 0.0f;
       } else {
         float p[3];
-        sample_point(rays + (gi / S) * stride, z[gi], p);
+        sample_point(rays + ray_of(gi, S) * stride, z[gi], p);
         if (jj == 0) {
           row[0] = p[0];
           row[1] = p[1];
@@ -2584,7 +2584,7 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       const int64_t gs = sample_of(tile, hs);
       // (32-bit division when it fits: the 64-bit one is a long emulated sequence per thread and half tile; the
       // ray row's first four floats as one 4-byte-aligned vector load)
-      const int64_t ray = gs < 0x7fffffff ? (int64_t)((unsigned)gs / (unsigned)S) : gs / S;
+      const int64_t ray = ray_of(gs, S);
       const float* r = rays + ray * stride;
       typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
       const f32x4u r4 = *reinterpret_cast<const f32x4u*>(r);

@@ -58,6 +58,11 @@ FoldBnBwd fold_bn_backward(const float* rays, int stride, const float* z, int S,
                            hipStream_t s);
 
 // p = o + d*z, one rounding per op (render.py:458; built with -ffp-contract=off).
+// ray of flattened sample g (ray-major, S samples per ray): a 32-bit division when g fits (the 64-bit one is a long
+// emulated sequence)
+__device__ __forceinline__ int64_t ray_of(int64_t g, int S) {
+  return g < 0x7fffffff ? (int64_t)((unsigned)g / (unsigned)S) : g / S;
+}
 __device__ __forceinline__ void sample_point(const float* __restrict__ r, float z, float (&p)[3]) {
   p[0] = r[0] + r[3] * z;
   p[1] = r[1] + r[4] * z;
