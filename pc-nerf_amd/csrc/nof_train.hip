@@ -2026,11 +2026,13 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__ part, int nblk, const float* __restrict__ W,
                                const float* __restrict__ coefp, double* __restrict__ dW, double* __restrict__ db,
-                               double* __restrict__ s12, int nblk_e) {
+                               double* __restrict__ s12, int nblk_e, int ldw = 0) {
+  // ldw: dW's row stride when it is not the layer's own (MODE 1 summing the skip layer's encoding columns: 319);
+  // db may be null (no bias sum)
   using Cfg = WgradCfg<MODE>;
   constexpr int C = Cfg::C;
   constexpr int SPLIT = Cfg::SPLIT;
-  constexpr int in_f = MODE == 0 ? 256 : MODE == 1 ? 63 : 319;
+  const int in_f = ldw > 0 ? ldw : MODE == 0 ? 256 : MODE == 1 ? 63 : 319;
   constexpr int wcol_h = MODE == 2 ? 63 : 0, col_h = Cfg::EX ? 64 : 0;
   __shared__ double red[C * SPLIT];
   const int m = blockIdx.x, tt = threadIdx.x, t = tt % C, sl = tt / C;
@@ -2073,7 +2075,7 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__
       atomicAdd(&s12c[2 * nn + 1], w * G);
     }
   }
-  if (t == 0) db[m] += dbm;
+  if (t == 0 && db) db[m] += dbm;
 }
 
 // ---- k_dgrad_ws: the data gradient in the weight-stationary form of k_train_ws<0,true>.  A workgroup of 8 waves (two per
@@ -2432,14 +2434,18 @@ __global__ __launch_bounds__(512, 1) void k_dgrad_h(
 //   dL/dh (A operand, read by its wave only): copied raw ([g][half][sample ^ c][4], c = 2 (g & 3) + half:
 //     conflict-free 4-byte reads), each wave splitting its 8 values per half tile itself.
 // One barrier per half tile.  Partials and db in k_wgrad<MODE>'s layout (k_wgrad_reduce<MODE> sums them).
+// MODE 3 (DUAL): the encoding columns of TWO layers in one pass -- layer 0's G on dL/dh_0 (gin) and the skip layer's
+// encoding columns on dL/dh_4 (gin2, a second partial set part2 in layer 0's layout, no db) -- sharing the staged
+// encoding (one sincos pass) and each half tile's barrier.
 template <int MODE, bool H2 = false>
 struct Wb3Cfg {
-  static constexpr bool HX = MODE != 1, EX = MODE != 0;
+  static constexpr bool HX = MODE != 1 && MODE != 3, EX = MODE != 0, DUAL = MODE == 3;
   static constexpr int NPART = H2 ? 2 : 3;                         // operand parts: f16 hi/mid or bf16 hi/mid/lo
   static constexpr int NBLK = (EX ? 2 : 0) + (HX ? 8 : 0);        // 32-column blocks of G
   static constexpr int PITCH = 64 * NBLK + 64;                     // x row bytes: 576, 192, 704
   static constexpr int XPART = 16 * PITCH;
-  static constexpr int GB = 16 * 256 * 4;                          // raw dL/dh bytes per half tile
+  static constexpr int GB1 = 16 * 256 * 4;                         // raw dL/dh bytes per half tile (per source)
+  static constexpr int GB = (DUAL ? 2 : 1) * GB1;
   static constexpr size_t BUF = (size_t)GB + NPART * XPART;
   static constexpr size_t LDS = 3 * BUF;
 };
@@ -2511,10 +2517,14 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
                                                           const float* __restrict__ mu, int64_t n,
                                                           const unsigned* __restrict__ gmax,
                                                           float* __restrict__ part,
-                                                          const unsigned* __restrict__ pbound) {
+                                                          const unsigned* __restrict__ pbound,
+                                                          const float* __restrict__ gin2,
+                                                          const unsigned* __restrict__ gmax2,
+                                                          float* __restrict__ part2) {
   using Cfg = Wb3Cfg<MODE, H2>;
   constexpr int NPART = Cfg::NPART;
-  constexpr bool HX = Cfg::HX, EX = Cfg::EX;
+  constexpr bool HX = Cfg::HX, EX = Cfg::EX, DUAL = Cfg::DUAL;
+  constexpr int GB1 = Cfg::GB1;
   constexpr int NBLK = Cfg::NBLK, PITCH = Cfg::PITCH, XPART = Cfg::XPART, GB = Cfg::GB;
   constexpr int NT = 512 / RB, NI = 2 * RB;   // threads; float4 per thread per operand and half tile
   constexpr int HOFF = EX ? 64 : 0;           // first h feature column in the x image
@@ -2524,7 +2534,7 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   // H2: per-column scales of G (x operand) after the three buffers; dL/dh's chunk-wide scale
   float* const csc = wb3 + 3 * Cfg::BUF / 4;
   float* const cun = csc + NBLK * 32;
-  float gsc = 1.0f, gun = 1.0f;
+  float gsc = 1.0f, gun = 1.0f, gsc2 = 1.0f, gun2 = 1.0f;
   if constexpr (H2) {
     for (int c = t; c < NBLK * 32; c += 512 / RB) {
       int e;
@@ -2550,6 +2560,13 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     const int eg = tile_scale_exp(__uint_as_float(gm));
     gsc = ldexpf(1.0f, eg);
     gun = ldexpf(1.0f, -eg);
+    if constexpr (DUAL) {
+      unsigned gm2 = 0;
+      for (int i = 0; i < GMAX_SLOTS; ++i) gm2 = max(gm2, gmax2[i]);
+      const int eg2 = tile_scale_exp(__uint_as_float(gm2));
+      gsc2 = ldexpf(1.0f, eg2);
+      gun2 = ldexpf(1.0f, -eg2);
+    }
     __syncthreads();
   }
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2562,8 +2579,8 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   // encoding staging (EX): row er = t & 15, sincos task ej = t >> 4
   const int er = t & 15, ej = t >> 4;
   const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)gin, (short)0, nt * tb, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rx =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(HX ? hprev : gin), (short)0, nt * tb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =   // (DUAL: the second dL/dh)
+      __builtin_amdgcn_make_buffer_rsrc((void*)(HX ? hprev : DUAL ? gin2 : gin), (short)0, nt * tb, 0x00020000);
   const int voff = (sg0 * 64 + 32 * shh + sl) * 16;
   constexpr int NR = 2 * NI + (EX ? 2 : 0);   // staging registers (float4): dL/dh, x, ray row + z
   auto sample_of = [&](int tile, int hs) {
@@ -2576,7 +2593,7 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       rv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, voff, so + NT * 32 * i, 0));
-      if (HX)
+      if (HX || DUAL)
         rv[NI + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, so + NT * 32 * i, 0));
     }
     if constexpr (EX) {   // the sample's ray origin, direction and z
@@ -2598,13 +2615,15 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     mu2[i] = HX ? *reinterpret_cast<const f32x4*>(mu + 8 * (sg0 + (NT / 32) * i) + 4 * shh) : f32x4{};
   // staging pieces of a half tile: k < NI the dL/dh float4 k; NI <= k < 2 NI the x float4 k - NI (HX); the
   // encoding piece last (EX)
-  constexpr int NP = NI * (HX ? 2 : 1) + (EX ? 1 : 0);
+  constexpr int NP = NI * (HX || DUAL ? 2 : 1) + (EX ? 1 : 0);
   auto stage_piece = [&](int b, const f32x4 (&rv)[NR], int tile, int hs, int k) {
     char* base = reinterpret_cast<char*>(wb3) + (size_t)b * Cfg::BUF;
     char* xb = base + GB;
-    if (k < NI) {
-      const int g = sg0 + (NT / 32) * k, c = 2 * (g & 3) + shh;
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + g * 128 + shh * 64 + (sl ^ c) * 4) = rv[k];
+    if (k < NI || (DUAL && k < 2 * NI)) {   // raw dL/dh (DUAL: the second source GB1 further)
+      const int kk = k < NI ? k : k - NI;
+      const int g = sg0 + (NT / 32) * kk, c = 2 * (g & 3) + shh;
+      char* bb = base + (k < NI ? 0 : GB1);
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(bb) + g * 128 + shh * 64 + (sl ^ c) * 4) = rv[k];
       return;
     }
     s16x4 p0 = {}, p1 = {}, p2 = {};
@@ -2670,11 +2689,16 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     *reinterpret_cast<s16x4*>(xb + XPART + off) = p1;
     if (!H2) *reinterpret_cast<s16x4*>(xb + 2 * XPART + off) = p2;
   };
-  f32x16 acc[RB][NBLK];
+  f32x16 acc[RB][NBLK], acc2[DUAL ? RB : 1][DUAL ? NBLK : 1];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int nb = 0; nb < NBLK; ++nb) acc[rb][nb] = f32x16{};
+  if constexpr (DUAL)
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int nb = 0; nb < NBLK; ++nb) acc2[rb][nb] = f32x16{};
   float dbacc[RB] = {};
   // A read: feature m = 32 (RB wv + rb) + li -> g = 4 (RB wv + rb) + (li >> 3), half (li >> 2) & 1, q = li & 3;
   // row 8 h + j (the swizzle c = 2 (g & 3) + half does not depend on rb)
@@ -2691,14 +2715,14 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   const int nh = tl0 < nt ? 2 * ((nt - 1 - tl0) / gstride + 1) : 0;
   auto tile_of = [&](int u) { return tl0 + (u >> 1) * gstride; };
   auto bufp = [&](int b) { return reinterpret_cast<const char*>(wb3) + (size_t)b * Cfg::BUF; };
-  auto readA = [&](float (&av)[RB][8], int b) {
-    const float* gbuf = reinterpret_cast<const float*>(bufp(b));
+  auto readA = [&](float (&av)[RB][8], int b, int src = 0) {
+    const float* gbuf = reinterpret_cast<const float*>(bufp(b) + src * GB1);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int j = 0; j < 8; ++j) av[rb][j] = gbuf[abase + 512 * rb + ((8 * h + j) ^ ac) * 4];
   };
-  auto splitA = [&](float (&av)[RB][8], P8 (&a)[RB][NPART], bool count) {
+  auto splitA = [&](float (&av)[RB][8], P8 (&a)[RB][NPART], bool count, float sc) {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
@@ -2706,7 +2730,7 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       if constexpr (H2) {
         float sv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sv[j] = av[rb][j] * gsc;
+        for (int j = 0; j < 8; ++j) sv[j] = av[rb][j] * sc;
         split2_f16(sv, a[rb][0], a[rb][1]);
       } else {
         split3_bf16(av[rb], a[rb][0], a[rb][1], a[rb][2]);
@@ -2743,10 +2767,15 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   constexpr int S_APF = WB3_AREAD < NBLK ? WB3_AREAD : NBLK - 1;
   constexpr int S_ASP = S_APF + 2 < NBLK ? S_APF + 2 : NBLK - 1;
   P8 Acur[RB][NPART], Anext[RB][NPART], B[2][NPART];
+  P8 Acur2[DUAL ? RB : 1][NPART], Anext2[DUAL ? RB : 1][NPART];
   if (nh > 0) {
     float av[RB][8];
     readA(av, 0);
-    splitA(av, Acur, true);
+    splitA(av, Acur, true, gsc);
+    if constexpr (DUAL) {
+      readA(av, 0, 1);
+      splitA(av, Acur2, false, gsc2);
+    }
     readB(B[0], 0, 0);
   }
   int bcur = 0;
@@ -2756,14 +2785,31 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   for (int u = 0; u < nh; ++u) {
     const int bn1 = bcur == 2 ? 0 : bcur + 1, bn2 = bcur == 0 ? 2 : bcur - 1;
     const int u2 = u + 2 < nh ? u + 2 : nh - 1, u3 = u + 3 < nh ? u + 3 : nh - 1;
-    float av[RB][8];
+    float av[RB][8], av2[RB][8];
 #pragma unroll
     for (int nb = 0; nb < NBLK; ++nb) {
       if (nb + 1 < NBLK) readB(B[(nb + 1) & 1], bcur, nb + 1);
       else readB(B[0], bn1, 0);
-      if (nb == S_APF) readA(av, bn1);
-      if (nb == S_ASP) splitA(av, Anext, u + 1 < nh);
+      if (nb == S_APF) {
+        readA(av, bn1);
+        if constexpr (DUAL) readA(av2, bn1, 1);
+      }
+      if (nb == S_ASP) {
+        splitA(av, Anext, u + 1 < nh, gsc);
+        if constexpr (DUAL) splitA(av2, Anext2, false, gsc2);
+      }
       const P8* bo = B[nb & 1];
+      if constexpr (DUAL)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          const P8* a = Acur2[rb];
+          f32x16 c = acc2[rb][nb];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bo[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bo[1], c, 0, 0, 0);
+          if (NTP == 4) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bo[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bo[0], c, 0, 0, 0);
+          acc2[rb][nb] = c;
+        }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
         const P8* a = Acur[rb];
@@ -2793,10 +2839,14 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int p = 0; p < NPART; ++p) Acur[rb][p] = Anext[rb][p];
+      for (int p = 0; p < NPART; ++p) {
+        Acur[rb][p] = Anext[rb][p];
+        if constexpr (DUAL) Acur2[rb][p] = Anext2[rb][p];
+      }
     bcur = bn1;
   }
-  static_assert(MODE != 2 && (LAY == MODE || LAY == 2), "partial layouts");
+  static_assert(!DUAL || (H2 && LAY == 1), "the two-layer encoding form: f16x2, both partial sets in layer 0's layout");
+  static_assert(MODE != 2 && (LAY == MODE || LAY == 2 || DUAL), "partial layouts");
   constexpr int C = WgradCfg<LAY>::C, COL = (LAY == 2 && MODE == 0) ? 64 : 0;
   constexpr bool DB = MODE == 0 || LAY == 1;
   float* pb = part + (size_t)blockIdx.x * WgradCfg<LAY>::PART;
@@ -2811,6 +2861,18 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
     }
     float d = dbacc[rb] + __shfl_xor(dbacc[rb], 32, 64);
     if (DB && h == 0) pb[(size_t)256 * C + 32 * (RB * wv + rb) + li] = d;
+  }
+  if constexpr (DUAL) {   // the skip layer's encoding columns (no db: its dL/dh_4 sum comes with its h columns)
+    float* pb2 = part2 + (size_t)blockIdx.x * WgradCfg<LAY>::PART;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int m = 32 * (RB * wv + rb) + (rr & 3) + 8 * (rr >> 2) + 4 * h;
+#pragma unroll
+        for (int nb = 0; nb < NBLK; ++nb)
+          pb2[(size_t)m * C + 32 * nb + li] = (acc2[rb][nb][rr] * gun2) * cun[32 * nb + li];
+      }
   }
 }
 
@@ -3433,7 +3495,9 @@ static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int 
 template <int MODE, int LAY, bool H2, int NTP>
 static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                                 int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
-                                const float* mu, const unsigned* gmax, float* part, const unsigned* pbound) {
+                                const float* mu, const unsigned* gmax, float* part, const unsigned* pbound,
+                                const float* gin2 = nullptr, const unsigned* gmax2 = nullptr,
+                                float* part2 = nullptr) {
   constexpr int RB = 1;
   using Cfg = Wb3Cfg<MODE, H2>;
   constexpr size_t lds = 3 * Cfg::BUF + (H2 ? 2 * Cfg::NBLK * 32 * sizeof(float) : 0);
@@ -3445,7 +3509,7 @@ static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* ray
     attr = true;
   }
   hipLaunchKernelGGL((k_wgrad_b3<RB, MODE, LAY, H2, NTP>), dim3(blocks), dim3(512 / RB), lds, s, rays, stride, z, S,
-                     c0, ein, gin, hprev, mu, n, gmax, part, pbound);
+                     c0, ein, gin, hprev, mu, n, gmax, part, pbound, gin2, gmax2, part2);
 }
 
 // the weight-gradient partials of k_wgrad<MODE> under the split train math: f16x2 with the forward's product count
@@ -3492,7 +3556,6 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   }
   const double dn = (double)n;
   const int64_t ntiles = (n + 31) / 32;
-  const unsigned wb0 = (unsigned)std::min<int64_t>(2 * ntiles, 2 * WG_BLOCKS);   // encoding-column workgroups
   const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
   {
     // max |dL/dlogit| (into the first word of the output-statistics copies, which the one-pass backward does not
@@ -3528,29 +3591,30 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
       else
         launch(k_bwd_fused<0, false>, FB_LDS);
     }
-    if (L == 4) {   // the skip layer's encoding columns on g_4 (its store slot), into the same partials, two
-                    // workgroups per CU like layer 0's
-      ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
-      launch_wgrad_b3<2>(wb0, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[4], hh[3], coefp,
-                         ws.gmax + 4 * GMAX_SLOTS, ws.part, ws.pbound, false, true);
-    }
     ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0);
-    if (L == 4)
+    if (L == 4)   // (its encoding columns come with layer 0's at the end: no encoding-column partials here)
       hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[4],
-                         coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], (double*)nullptr, (int)wb0);
+                         coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], (double*)nullptr, 0);
     else
       hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[L],
                          coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], (double*)nullptr, FB_PAIRS);
   }
-  // layer 0 on the encoding (g_0 in its store slot), two workgroups per CU
+  // layer 0 and the skip layer's encoding columns in ONE pass over the staged encoding (k_wgrad_b3 MODE 3: g_0 and
+  // g_4 in their store slots), one workgroup per CU, two partial sets in layer 0's layout
+  const unsigned we = (unsigned)std::min<int64_t>(ntiles, WG_BLOCKS);
+  float* part_e4 = ws.part + (size_t)WG_BLOCKS * WgradCfg<1>::PART;
   {
-    ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, 1024.0 * dn);
-    launch_wgrad_b3<1>(wb0, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[0], nullptr, nullptr,
-                       ws.gmax + 0 * GMAX_SLOTS, ws.part, ws.pbound);
+    ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 2.0 * 256.0 * 64 * dn, 2048.0 * dn);
+    launch_wgrad_b3_one<3, 1, true, 3>(we, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[0], nullptr, nullptr,
+                                       ws.gmax + 0 * GMAX_SLOTS, ws.part, ws.pbound, hh[4], ws.gmax + 4 * GMAX_SLOTS,
+                                       part_e4);
   }
-  ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wb0 * WgradCfg<1>::PART * 4.0);
-  hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)wb0, P.lin_w[0],
-                     (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr, (int)wb0);
+  ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * we * WgradCfg<1>::PART * 4.0);
+  hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)we, P.lin_w[0],
+                     (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr, (int)we, 0);
+  hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, part_e4, (int)we, P.lin_w[4],
+                     (const float*)nullptr, ws.gacc + G.w[4], (double*)nullptr, (double*)nullptr, (int)we,
+                     in_features(4));
 }
 
 static void backward_train(const float* rays, int ray_stride, const float* z, int n_samples, const float* ein,
