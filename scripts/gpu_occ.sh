@@ -1,6 +1,7 @@
 # Forward occupancy experiment: the store-writing train query and the eval query of variant
-# libraries built with PCN_EH3_SB / PCN_EH3_MINB (base: 6 sample blocks, one block per CU; sb3x2: 3 sample blocks, two
-# blocks per CU; sb3x1: 3 sample blocks, one block per CU) -- same-process A/B, then one PMC pass per variant.
+# libraries built with EH3_SB / EH3_WG_PER_CU of csrc/nof_eval.hip set per variant (base: 6 sample blocks, one block
+# per CU; sb3x2: 3 sample blocks, two blocks per CU -- adopted; sb3x1: 3 sample blocks, one block per CU; the run in
+# profiles/r04_occupancy_* used -D macros for the two constants) -- same-process A/B, then one PMC pass per variant.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
