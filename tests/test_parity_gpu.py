@@ -307,7 +307,7 @@ def test_render_rays(isval, eval_math):
     _report({"case": f"render_rays_isval{isval}_depth2_{eval_math}", "rows": int(ok.size),
              "same_order_rows": float(ok.mean()), "tied_rows": int(tied.sum()),
              "tied_same_order": int((ok & tied).sum())})
-    assert ok.mean() >= 0.9, ok.mean()
+    assert ok.mean() >= 0.98, ok.mean()   # (measured: every row, both maths)
     rank_h = wh.argsort(dim=-1, descending=True).eq(S - 1).int().argmax(-1).numpy()
     rank_r = wr.argsort(dim=-1, descending=True).eq(S - 1).int().argmax(-1).numpy()
     np.testing.assert_array_equal(rank_h[ok], rank_r[ok])                  # the same sample selected, exactly
