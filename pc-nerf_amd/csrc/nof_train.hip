@@ -3405,258 +3405,6 @@ static GaccLayout gacc_layout() {
 
 constexpr int S12_LAYER = S12_COPIES * 512;
 
-// ---- k_enc_wgrad: the encoding columns' weight gradients of layer 0 (G0 = sum_s g_0 (x) e) and of the skip layer
-// (G4e = sum_s g_4 (x) e) in ONE pass over a stored chunk, in k_bwd_fused's form: per 32-sample tile the raw g_0 and
-// g_4 tiles arrive by LDS-DMA one tile ahead; each wave splits ITS 32 features of both (fp16 hi + mid, chunk-wide
-// 2^sg scales from the producers' maxima) into a wave-private split image read back by transposed reads; all waves
-// build the tile's encoding (sample positions from the ray rows, or the stored embedding rows) split per column
-// (2^14 for sin / cos, the positions' bound for xyz) into a shared image; then per wave 2 x (2 row blocks x 4 column
-// blocks x 3 products) v_mfma_f32_16x16x32_f16.  Two barriers per tile (the encoding image is single-buffered).
-// 8 waves, one workgroup per CU (152.5 KiB of LDS); partials per workgroup in k_wgrad<1>'s layout (part0 with db,
-// part4 without).
-constexpr int EW_BUF = 2 * FB_GPART;                       // split or raw g of one source (32 KiB)
-constexpr size_t EW_LDS = 4 * (size_t)EW_BUF + 2 * FB_XPART + 2 * 64 * sizeof(float) + 8 * 1024;
-__global__ __launch_bounds__(512, 1) void k_enc_wgrad(const float* __restrict__ rays, int stride,
-                                                       const float* __restrict__ z, int S, int64_t c0, int64_t n,
-                                                       const float* __restrict__ ein, const float* __restrict__ g0,
-                                                       const float* __restrict__ g4, const unsigned* __restrict__ gmax0,
-                                                       const unsigned* __restrict__ gmax4,
-                                                       const unsigned* __restrict__ pbound, float* __restrict__ part0,
-                                                       float* __restrict__ part4) {
-  extern __shared__ __attribute__((aligned(16))) char ew[];
-  char* const spl = ew;                            // [source 2][part 2][sample 32][512 B] (fb_off<FB_GP>)
-  char* const raw = ew + 2 * EW_BUF;               // [source 2][g 32][lane 64][16 B]
-  char* const enc = ew + 4 * EW_BUF;               // [part 2][sample 32][256 B] (fb_off<FB_XP>, 64 columns used)
-  float* const csc = reinterpret_cast<float*>(ew + 4 * EW_BUF + 2 * FB_XPART);
-  float* const cun = csc + 64;
-  char* const rows = reinterpret_cast<char*>(cun + 64) + 0;   // per wave [component 7][sample 32] (+32 spare) floats
-  const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int bid = (int)blockIdx.x, nb = (int)gridDim.x;
-  const int nt = (int)((n + 31) / 32);
-  const int nk = bid < nt ? (nt - 1 - bid) / nb + 1 : 0;   // this workgroup's tiles: bid + k nb
-  if (t < 64) {   // column scales: |sin|, |cos| <= 1; xyz by the call's largest |position| (k_pos_bound)
-    int e = (t >= 3 && t < 63) ? 14 : 0;
-    if (t < 3 && pbound) {
-      const float pm = __uint_as_float(*pbound);
-      e = (pm > 0.0f && pm < 3.0e38f) ? 14 - ilogbf(pm) : 0;
-      e = e < -60 ? -60 : e > 60 ? 60 : e;
-    }
-    csc[t] = ldexpf(1.0f, e);
-    cun[t] = ldexpf(1.0f, -e);
-  }
-  unsigned m0 = 0, m4 = 0;
-  for (int i = 0; i < GMAX_SLOTS; ++i) {   // (uniform loads)
-    m0 = max(m0, gmax0[i]);
-    m4 = max(m4, gmax4[i]);
-  }
-  const int e0 = tile_scale_exp(__uint_as_float(m0)), e4 = tile_scale_exp(__uint_as_float(m4));
-  const float gsc[2] = {ldexpf(1.0f, e0), ldexpf(1.0f, e4)}, gun[2] = {ldexpf(1.0f, -e0), ldexpf(1.0f, -e4)};
-  // raw DMA: wave w moves rows 4 w + m (m < 4) of both sources, which it alone splits
-  auto issue_raw = [&](int k) {
-    const int tl = bid + k * nb;
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-#pragma unroll
-    for (int src = 0; src < 2; ++src) {
-      const float* gsrc = (src ? g4 : g0) + (size_t)tl * TILE_FLOATS + ln * 4;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) fb_glds16(gsrc + (4 * wv + m) * 256, raw + src * EW_BUF + (4 * wv + m) * 1024);
-    }
-  };
-  const int sl = lane & 15, sh = (lane >> 4) & 1, sr = lane >> 5;
-  auto convert = [&](int k) {   // raw tile k of both sources -> this wave's rows of the split images
-    const int tl = bid + k * nb;
-#pragma unroll
-    for (int src = 0; src < 2; ++src)
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int row = 4 * wv + 2 * (m >> 1) + sr, sm = 16 * (m & 1) + sl;
-        const bool valid = (int64_t)tl * 32 + sm < n;
-        const f32x4 r = *reinterpret_cast<const f32x4*>(raw + src * EW_BUF + (row * 64 + sm + 32 * sh) * 16);
-        f32x4 v;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = valid ? r[q] * gsc[src] : 0.0f;
-        s16x4 p0, p1;
-        split2_x4(v, p0, p1);
-        const int o = fb_off<FB_GP>(sm, 8 * row + 4 * sh);
-        *reinterpret_cast<s16x4*>(spl + src * EW_BUF + o) = p0;
-        *reinterpret_cast<s16x4*>(spl + src * EW_BUF + FB_GPART + o) = p1;
-      }
-  };
-  // encoding of a tile: thread t = sample es (t & 31), tasks et = t >> 5 (0..15): sincos tasks et and et + 16 (< 30,
-  // task j = 3 k + m -> features 3 + 6 k + m (sin) and 6 + 6 k + m (cos)); et == 14 also the positions (0..2) and
-  // et == 15 the zero pad 63.  Ray row and z loaded one tile ahead into registers
-  const int es = t & 31, et = t >> 5;
-  // the tile's ray rows and z by LDS-DMA into this wave's own slot (4 dword pieces: float q = 32 c + sample for
-  // component c < 6 of the ray row, c = 6 for z; the last 32 lanes repeat the previous ones into the spare)
-  auto load_rows = [&](int k) {
-    if (ein) return;
-    char* const slot = rows + wv * 1024;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int q = 64 * i + lane;
-      if (q >= 224) q -= 32;
-      const int c = q >> 5, sidx = q & 31;
-      int64_t sm = (int64_t)(bid + k * nb) * 32 + sidx;
-      if (sm >= n) sm = n - 1;
-      const int64_t gs = c0 + sm;
-      const float* src = c < 6 ? rays + ray_of(gs, S) * stride + c : z + gs;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(slot + i * 256), 4, 0, 0);
-    }
-  };
-  auto put1 = [&](int f, float v, bool valid) {
-    const float x = valid ? v * csc[f] : 0.0f;
-    const _Float16 h = (_Float16)x;
-    const int o = fb_off<FB_XP>(es, f);
-    *reinterpret_cast<_Float16*>(enc + o) = h;
-    *reinterpret_cast<_Float16*>(enc + FB_XPART + o) = (_Float16)(x - (float)h);
-  };
-  auto build_enc = [&](int k) {
-    int64_t s = (int64_t)(bid + k * nb) * 32 + es;
-    const bool valid = s < n;
-    if (s >= n) s = n - 1;
-    float pp[3];
-    const float* er = ein ? ein + (c0 + s) * 63 : nullptr;
-    if (!ein) {
-      const float* slot = reinterpret_cast<const float*>(rows + wv * 1024);
-      float rv[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) rv[i] = slot[32 * i + es];
-      sample_point(rv, slot[32 * 6 + es], pp);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int j = et + 16 * u;
-      if (j < 30) {
-        const int kf = j / 3, m = j - 3 * kf;
-        float sn, cs;
-        if (ein) {
-          sn = er[3 + 6 * kf + m];
-          cs = er[6 + 6 * kf + m];
-        } else {
-          const float pm = m == 0 ? pp[0] : m == 1 ? pp[1] : pp[2];
-          sincosf(__int_as_float((127 + kf) << 23) * pm, &sn, &cs);   // encode_half's (float)(1 << k) * p[m]
-        }
-        put1(3 + 6 * kf + m, sn, valid);
-        put1(6 + 6 * kf + m, cs, valid);
-      }
-    }
-    if (et == 14)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) put1(c, ein ? er[c] : pp[c], valid);
-    if (et == 15) put1(63, 0.0f, false);
-  };
-  f32x4 aw[2][2][4];
-#pragma unroll
-  for (int src = 0; src < 2; ++src)
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib) aw[src][jb][ib] = f32x4{};
-  float dbacc[2] = {0.0f, 0.0f};
-  const int trq = lm >> 2, trp = lm & 3, tr0 = 8 * kg + trq, tr1 = tr0 + 4;
-  using QG = std::integral_constant<int, FB_GPART>;
-  using QX = std::integral_constant<int, FB_XPART>;
-  auto read8 = [&](unsigned a0, unsigned a1, auto part) {
-    constexpr int Q = decltype(part)::value;
-    const s16x4 h0 = fb_tr<0>(a0), h1 = fb_tr<0>(a1), m0 = fb_tr<Q>(a0), m1 = fb_tr<Q>(a1);
-    return std::array<s16x4, 4>{h0, h1, m0, m1};
-  };
-  auto join = [](const s16x4& a, const s16x4& b) {
-    return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  const unsigned xa = fb_lds_addr(enc);
-  __syncthreads();   // csc
-  if (nk > 0) {
-    issue_raw(0);
-    load_rows(0);
-  }
-  for (int k = 0; k < nk; ++k) {
-    // raw tile k and its ray rows (both DMA'd one tile ago)
-    __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
-    convert(k);
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // its raw reads done before the raw rows are refilled
-    if (k + 1 < nk) issue_raw(k + 1);     // (in flight during the encoding and the MFMAs)
-    build_enc(k);
-    if (k + 1 < nk) load_rows(k + 1);     // (after build_enc has read this wave's row slot)
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // the encoding image of tile k is complete
-#pragma unroll
-    for (int src = 0; src < 2; ++src) {
-      const unsigned ga = fb_lds_addr(spl + src * EW_BUF);
-      std::array<s16x4, 4> ra[2], rbx[2];
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        const int col = 32 * wv + 16 * jb + 4 * trp;
-        ra[jb] = read8(ga + fb_off<FB_GP>(tr0, col), ga + fb_off<FB_GP>(tr1, col), QG{});
-      }
-      auto xrd = [&](int ib) {
-        const int col = 16 * ib + 4 * trp;
-        return read8(xa + fb_off<FB_XP>(tr0, col), xa + fb_off<FB_XP>(tr1, col), QX{});
-      };
-      rbx[0] = xrd(0);
-      fb_lgkm<4>(ra);
-      f16x8 A[2][2];
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        A[jb][0] = join(ra[jb][0], ra[jb][1]);
-        A[jb][1] = join(ra[jb][2], ra[jb][3]);
-      }
-      if (src == 0) {
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) dbacc[jb] += (float)A[jb][0][e] + (float)A[jb][1][e];
-      }
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib) {
-        std::array<s16x4, 4> cur[1] = {rbx[ib & 1]};
-        if (ib + 1 < 4) {
-          rbx[(ib + 1) & 1] = xrd(ib + 1);
-          fb_lgkm<4>(cur);
-        } else {
-          fb_lgkm<0>(cur);
-        }
-        const f16x8 B0 = join(cur[0][0], cur[0][1]), B1 = join(cur[0][2], cur[0][3]);
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-          aw[src][jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B0, aw[src][jb][ib], 0, 0, 0);
-          aw[src][jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B1, aw[src][jb][ib], 0, 0, 0);
-          aw[src][jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B0, aw[src][jb][ib], 0, 0, 0);
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // every wave done with the encoding image before the next tile's
-  }
-  // partials: rows j = 32 wv + 16 jb + 4 kg + r, columns 16 ib + lm (scales undone)
-  constexpr int C = WgradCfg<1>::C;
-#pragma unroll
-  for (int src = 0; src < 2; ++src) {
-    float* pb = (src ? part4 : part0) + (size_t)bid * WgradCfg<1>::PART;
-#pragma unroll
-    for (int ib = 0; ib < 4; ++ib) {
-      const float cu = cun[16 * ib + lm] * gun[src];
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          pb[(size_t)(32 * wv + 16 * jb + 4 * kg + r) * C + 16 * ib + lm] = aw[src][jb][ib][r] * cu;
-    }
-  }
-#pragma unroll
-  for (int jb = 0; jb < 2; ++jb) {
-    float d = dbacc[jb];
-    d += __shfl_xor(d, 16, 64);
-    d += __shfl_xor(d, 32, 64);
-    if (kg == 0) part0[(size_t)bid * WgradCfg<1>::PART + (size_t)256 * C + 32 * wv + 16 * jb + lm] = d * gun[0];
-  }
-}
-
 struct BwdWs {
   float* h[8];
   float* g[2];
@@ -3857,24 +3605,9 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   float* part_e4 = ws.part + (size_t)WG_BLOCKS * WgradCfg<1>::PART;
   {
     ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 2.0 * 256.0 * 64 * dn, 2048.0 * dn);
-#ifndef PCN_ENC_NEW
-#define PCN_ENC_NEW 1
-#endif
-    if (PCN_ENC_NEW) {
-      static bool eattr = false;
-      if (!eattr) {
-        PCN_HIP(hipFuncSetAttribute((const void*)k_enc_wgrad, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)EW_LDS));
-        eattr = true;
-      }
-      hipLaunchKernelGGL(k_enc_wgrad, dim3(we), dim3(512), EW_LDS, s, rays, ray_stride, z, n_samples, c0, n, ein,
-                         hh[0], hh[4], ws.gmax + 0 * GMAX_SLOTS, ws.gmax + 4 * GMAX_SLOTS, ws.pbound, ws.part,
-                         part_e4);
-    } else {
-      launch_wgrad_b3_one<3, 1, true, 3>(we, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[0], nullptr, nullptr,
-                                         ws.gmax + 0 * GMAX_SLOTS, ws.part, ws.pbound, hh[4],
-                                         ws.gmax + 4 * GMAX_SLOTS, part_e4);
-    }
+    launch_wgrad_b3_one<3, 1, true, 3>(we, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[0], nullptr, nullptr,
+                                       ws.gmax + 0 * GMAX_SLOTS, ws.part, ws.pbound, hh[4], ws.gmax + 4 * GMAX_SLOTS,
+                                       part_e4);
   }
   ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * we * WgradCfg<1>::PART * 4.0);
   hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)we, P.lin_w[0],
