@@ -326,6 +326,7 @@ __global__ void k_pack_eval_h3(NofParamsDev P, float* __restrict__ out) {
 // One workgroup per CU: 5, 7 or 3 blocks all slower than 6 (profiles/r03l_variants_eval_sb*.json, r04_occupancy_ab).
 constexpr int EH3_SB = 3;
 constexpr int EH3_WG_PER_CU = 2;
+static_assert(96 % (16 * EH3_SB) == 0, "store_layer_bytes (pcnerf_internal.h) pads a chunk to whole 96-sample blocks");
 // k_nof_eval_h3: weight-ring slots (prefetch distance EH3_RING - 1 k-steps of 32; a 4-slot ring: +7 %)
 constexpr int EH3_RING = 2;
 // The store-writing train query writes the activation store nontemporal (streamed past L2, which holds the weight
@@ -344,15 +345,18 @@ constexpr int EH3_RING = 2;
 // the waves.  Only the encoding (layers 0 and 4) keeps a per-sample scale, min(its own, sxB[3]).  blockIdx.y is the
 // BatchNorm chunk, blockIdx.x the 16 EH3_SB-sample block inside it, so no block straddles two chunks.
 // coef per chunk: [L][alpha 256 | beta'' 256] floats, then sxB[8] as int (TQ_COEF_FLOATS floats per chunk).
-// TR with an activation store (hst, chunks below store_chunks): each layer's raw output W_L x + b_L (the layered
-// kernels' stored h, nof_train.hip StoreChunk) is written before the BatchNorm fma.
-template <bool TR>
+// TR with an activation store (ST; launch_train_query runs the stored chunks as their own launch, blockIdx.y + cy0 is
+// the chunk): each layer's raw output W_L x + b_L (the layered kernels' stored h, nof_train.hip StoreChunk) is written
+// before the BatchNorm fma, whole 32-sample tiles (the store pads a chunk to 96 samples), its raw bias from LDS
+// (loaded one layer ahead): a global bias load there waited for the previous sample block's stores.  Compile-time
+// store + LDS bias: store-writing query -3.3 % (profiles/r04_variants_store_query.json).
+template <bool TR, bool ST = false>
 __global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float* __restrict__ rays, int stride,
                                                         const float* __restrict__ z, int64_t total, int S,
                                                         const float* __restrict__ ein, const float* __restrict__ W,
                                                         float* __restrict__ p_out, const float* __restrict__ coef,
                                                         int64_t chunk, float* __restrict__ hst, int64_t hst_chunk,
-                                                        int64_t hst_layer, int64_t store_chunks) {
+                                                        int64_t hst_layer, int cy0) {
   constexpr int SB = EH3_SB, NS = 16 * SB, R3 = EH3_RING, D3 = R3 - 1;
   constexpr bool ORD = TR;
   typedef float f32x4_ __attribute__((ext_vector_type(4)));
@@ -364,11 +368,15 @@ __global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float*
   __shared__ float smax[4][NS];   // (eval)
   __shared__ float pdot[4][NS];
   __shared__ float spos[NS][3];
+  // TR with the store: the raw biases of two consecutive layers (slot L & 1), each loaded one layer ahead
+  __shared__ __attribute__((aligned(16))) float sbraw[TR ? 2 : 1][TR ? 256 : 4];
   const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, g = lane >> 4, li = lane & 15;
-  const int64_t cb = TR ? (int64_t)blockIdx.y * chunk : 0;
+  const int cy = (int)blockIdx.y + cy0;   // the BatchNorm chunk
+  const int64_t cb = TR ? (int64_t)cy * chunk : 0;
   const int64_t s0 = cb + (int64_t)blockIdx.x * NS;
   const int64_t send = TR ? (cb + chunk < total ? cb + chunk : total) : total;
   if (s0 >= send) return;   // (the last chunk's surplus blocks; uniform over the block, before any barrier)
+  constexpr bool storing = TR && ST;
   float rz = 0.0f, rr[6] = {};
   if (!ein && t < NS) {
     int64_t gs = s0 + t;
@@ -384,7 +392,7 @@ __global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float*
   for (int L = 0; L < 8; ++L) sw[L] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(W + OFF_EH_SW)[L]);
   int sxB[8];
   if (TR) {
-    const int* cs = reinterpret_cast<const int*>(coef + blockIdx.y * (size_t)TQ_COEF_FLOATS + 16 * 256);
+    const int* cs = reinterpret_cast<const int*>(coef + cy * (size_t)TQ_COEF_FLOATS + 16 * 256);
 #pragma unroll
     for (int L = 0; L < 8; ++L) sxB[L] = __builtin_amdgcn_readfirstlane(L < 7 ? cs[L] : 0);
   }
@@ -401,8 +409,12 @@ __global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float*
   eh_f16x8 wr[R3][4][2];
 #pragma unroll
   for (int k = 0; k < D3; ++k) load_w(wr[k], k);
+  if (storing) {
+    sbraw[0][t] = W[OFF_BIAS + t];
+    sbraw[TR ? 1 : 0][t] = W[OFF_BIAS + 256 + t];
+  }
   if (TR) {
-    const f32x4_* cf = reinterpret_cast<const f32x4_*>(coef + blockIdx.y * (size_t)TQ_COEF_FLOATS);
+    const f32x4_* cf = reinterpret_cast<const f32x4_*>(coef + cy * (size_t)TQ_COEF_FLOATS);
     f32x4_ cv[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) cv[m] = cf[t + 256 * m];
@@ -626,18 +638,19 @@ __global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float*
   // TR: the activation store (the layered kernels' [32-sample tile][k-group][lane][4] layout): accumulator
   // acc[j][sb] of lane l is neurons 64w + 16j + 4g .. + 3 = k-group 8w + 2j + (g >> 1), half g & 1, of sample
   // 16(q & 1) + (l & 15) of tile q >> 1, q = SB blockIdx.x + sb the 16-sample block within the chunk
-  const bool storing = TR && hst != nullptr && (int64_t)blockIdx.y < store_chunks;
   auto store_raw = [&](int L, int sb, int j, float sc) __attribute__((always_inline)) {
     const int64_t q = (int64_t)blockIdx.x * SB + sb, tile = q >> 1;
-    if (tile * 32 >= send - cb) return;
     const int n0 = 64 * w + 16 * j + 4 * g;
-    const f32x4_ b = *reinterpret_cast<const f32x4_*>(W + OFF_BIAS + 256 * L + n0);
+    const f32x4_ b = *reinterpret_cast<const f32x4_*>(&sbraw[TR ? L & 1 : 0][TR ? n0 : 0]);
     const f32x4_ v = {acc[j][sb][0] * sc + b[0], acc[j][sb][1] * sc + b[1], acc[j][sb][2] * sc + b[2],
                       acc[j][sb][3] * sc + b[3]};
     const int sl = 16 * (int)(q & 1) + li + 32 * (g & 1);
-    float* dst = hst + (int64_t)blockIdx.y * hst_chunk + (int64_t)L * hst_layer +
-                 ((tile * 32 + (n0 >> 3)) * 64 + sl) * 4;
-    __builtin_nontemporal_store(v, reinterpret_cast<f32x4_*>(dst));
+    // a uniform layer base and a 32-bit byte offset (launch_train_query checks a layer's region is < 4 GiB): the
+    // stores take the scalar-base form, one offset register per sample block
+    char* const hb = reinterpret_cast<char*>(hst + (int64_t)cy * hst_chunk + (int64_t)L * hst_layer);
+    const uint32_t off = ((uint32_t)tile * 32u + (uint32_t)(8 * w + (g >> 1))) * 1024u + (uint32_t)sl * 16u +
+                         (uint32_t)j * 2048u;
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4_*>(hb + off));
   };
   auto epi_tr = [&](int L, auto PS) __attribute__((always_inline)) {
     constexpr bool ps = decltype(PS)::value;
@@ -682,8 +695,14 @@ __global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float*
     epi2(false);
     __syncthreads();
   }
+  // the next layer's raw bias, loaded at the start of layer L (bnext) and written to its slot before L's epilogue
+  float bnext = 0.0f;
+  auto bias_load = [&](int L) __attribute__((always_inline)) {
+    if (storing && L < 7) bnext = W[OFF_BIAS + 256 * (L + 1) + t];
+  };
   auto layer_end = [&](int L) __attribute__((always_inline)) {
     if (TR) {
+      if (storing && L < 7) sbraw[TR ? (L + 1) & 1 : 0][TR ? t : 0] = bnext;
       if (L == 4) epi_tr(4, std::true_type{});
       else epi_tr(L, std::false_type{});
       if (L < 7) {
@@ -715,15 +734,18 @@ __global__ __launch_bounds__(256, EH3_WG_PER_CU) void k_nof_eval_h3(const float*
                 eh3_start(6) % R3 == eh3_start(7) % R3, "ring slots");
 #pragma unroll 1
   for (int L = 1; L <= 3; ++L) {
+    if (TR) bias_load(L);
     hidden_ksteps(eh3_start(1) % R3, true);
     layer_end(L);
   }
+  if (TR) bias_load(4);
 #pragma unroll
   for (int s = 0; s < 2; ++s) kstep_enc(s, eh3_start(4) % R3 + s, s == 0);
   hidden_ksteps((eh3_start(4) + 2) % R3, false);
   layer_end(4);
 #pragma unroll 1
   for (int L = 5; L <= 7; ++L) {
+    if (TR) bias_load(L);
     hidden_ksteps(eh3_start(5) % R3, true);
     layer_end(L);
   }
@@ -758,7 +780,7 @@ static void launch_eval(const float* rays, int stride, const float* z, int64_t t
     hipLaunchKernelGGL(k_nof_eval_h3<false>,
                        dim3((unsigned)((total + ns - 1) / ns)), dim3(256), 0,
                        s, rays, stride, z, total, S, ein, W, p_out, nullptr, (int64_t)0, nullptr, (int64_t)0,
-                       (int64_t)0, (int64_t)0);
+                       (int64_t)0, 0);
   } else {
     const int64_t blocks = ((total + 31) / 32 + 3) / 4;
     hipLaunchKernelGGL(k_nof_eval, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, total, S, ein, W,
@@ -923,9 +945,16 @@ void launch_train_query(const float* rays, int stride, const float* z, int64_t t
   const int64_t ns = 16 * EH3_SB;
   const int64_t per = (std::min(chunk, total) + ns - 1) / ns;
   if (C >= 65536 || per >= ((int64_t)1 << 31)) throw std::runtime_error("train query: too many chunks / samples");
-  hipLaunchKernelGGL(k_nof_eval_h3<true>, dim3((unsigned)per, (unsigned)C), dim3(256),
-                     0, s, rays, stride, z, total,
-                     S, ein, img, p_out, coef, chunk, hst, hst_chunk, hst_layer, store_chunks);
+  // the stored chunks [0, Cs) and the rest as two launches: the store is compile-time in the kernel (a runtime
+  // branch around the stores made every layer's first weight-ring wait drain them)
+  const int64_t Cs = hst ? std::min(store_chunks, C) : 0;
+  if (Cs > 0 && hst_layer * sizeof(float) > 0xffffffffull) throw std::runtime_error("train query: store layer >= 4 GiB");
+  if (Cs > 0)
+    hipLaunchKernelGGL((k_nof_eval_h3<true, true>), dim3((unsigned)per, (unsigned)Cs), dim3(256), 0, s, rays,
+                       stride, z, total, S, ein, img, p_out, coef, chunk, hst, hst_chunk, hst_layer, 0);
+  if (C > Cs)
+    hipLaunchKernelGGL((k_nof_eval_h3<true, false>), dim3((unsigned)per, (unsigned)(C - Cs)), dim3(256), 0, s, rays,
+                       stride, z, total, S, ein, img, p_out, coef, chunk, nullptr, (int64_t)0, (int64_t)0, (int)Cs);
 }
 
 void launch_fold_logits(const float* rays, int stride, const float* z, int64_t total, int S, const float* ein,

@@ -33,9 +33,10 @@ void launch_fold_logits(const float* rays, int stride, const float* z, int64_t t
 // per-layer operand scales of its bound.
 size_t train_query_image_floats();
 // the activation store's bytes per layer of a chunk ([tile of 32 samples][32 k-groups][64 lanes][4] floats, 256-B
-// aligned; nof_train.hip StoreChunk, pcnerf_nof_store_bytes)
+// aligned; nof_train.hip StoreChunk, pcnerf_nof_store_bytes): the chunk rounded up to 96 samples, so the train
+// query's 48-sample blocks write whole tiles unconditionally (the tail's extra tiles are never read)
 inline size_t store_layer_bytes(int64_t chunk) {
-  return ((size_t)((chunk + 31) / 32) * (32 * 256) * 4 + 255) & ~(size_t)255;
+  return (size_t)((chunk + 95) / 96) * 3 * (32 * 256) * 4;
 }
 constexpr int TQ_COEF_FLOATS = 16 * 256 + 16;   // per chunk: [L][alpha 256 | beta'' 256], then sxB[8] (int)
 void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s);
