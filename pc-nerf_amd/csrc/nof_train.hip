@@ -2044,12 +2044,19 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__
   const int nred = nblk < C * SPLIT ? nblk : C * SPLIT;   // only the first nblk threads summed anything
   for (int i = 0; i < nred; ++i) dbm += red[i];
   __syncthreads();
-  // 8 independent loads in flight per thread (the sum is latency-bound otherwise)
+  // 32 loads per thread in flight at once (the sum is latency-bound otherwise)
   double Gp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   const float* pc = part + (size_t)m * C + t;
   const int nbc = (Cfg::EX && t < 64) ? nblk_e : nblk;   // the encoding columns' own partial count (MODE 2)
   const int b0 = sl * ((nbc + SPLIT - 1) / SPLIT), b1 = min(nbc, b0 + (nbc + SPLIT - 1) / SPLIT);
   int b = b0;
+  for (; b + 32 <= b1; b += 32) {
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = pc[(size_t)(b + j) * Cfg::PART];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) Gp[j & 7] += (double)v[j];
+  }
   for (; b + 8 <= b1; b += 8) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) Gp[j] += (double)pc[(size_t)(b + j) * Cfg::PART];
@@ -2968,12 +2975,16 @@ __global__ void k_pack_dgrad_h16(NofParamsDev P, const int* __restrict__ sw, f16
 }
 
 // max |dL/dlogit| over the chunk (float bits, into a zeroed word): k_fb_prep's bound on |g_7|
+// (one atomic per workgroup: 4 per workgroup onto the one word cost ~10 us per chunk in L2 serialisation)
 __global__ __launch_bounds__(256) void k_out_gabs(const float* __restrict__ g, int64_t n, unsigned* __restrict__ out) {
+  __shared__ float wm[4];
   float m = 0.0f;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     m = fmaxf(m, fabsf(g[i]));
   m = wave_max_f(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
 
 // Everything a stored chunk's one-pass backward needs before its first layer, in ONE launch of 8 blocks x 256
