@@ -2024,9 +2024,10 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
 // layer puts ~1024 threads, 8 loads each in flight, on the latency-bound sum), accumulate dW/db in float64 and the
 // statistics of the BatchNorm below: s12[n] = (sum_m W[m][n] db[m], sum_m W[m][n] G[m][n]).
 template <int MODE>
-__global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__ part, int nblk, const float* __restrict__ W,
-                               const float* __restrict__ coefp, double* __restrict__ dW, double* __restrict__ db,
-                               double* __restrict__ s12, int nblk_e, int ldw = 0) {
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part, int nblk, const float* __restrict__ W,
+                                                  const float* __restrict__ coefp, double* __restrict__ dW,
+                                                  double* __restrict__ db, double* __restrict__ s12, int nblk_e,
+                                                  int ldw) {
   // ldw: dW's row stride when it is not the layer's own (MODE 1 summing the skip layer's encoding columns: 319);
   // db may be null (no bias sum)
   using Cfg = WgradCfg<MODE>;
@@ -2083,6 +2084,26 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__
     }
   }
   if (t == 0 && db) db[m] += dbm;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__ part, int nblk, const float* __restrict__ W,
+                               const float* __restrict__ coefp, double* __restrict__ dW, double* __restrict__ db,
+                               double* __restrict__ s12, int nblk_e, int ldw = 0) {
+  wgrad_reduce_body<MODE>(part, nblk, W, coefp, dW, db, s12, nblk_e, ldw);
+}
+
+// The one-pass backward's last sums of a chunk in one launch (blockIdx.y): layer 1's partials (k_wgrad_reduce<0>),
+// layer 0's and the skip layer's encoding columns (k_wgrad_reduce<1>, the latter into rows of 319)
+__global__ __launch_bounds__(1024) void k_fb_reduce_tail(const float* __restrict__ part1, const float* __restrict__ coef1,
+                                                         double* __restrict__ dW1, double* __restrict__ db1,
+                                                         const float* __restrict__ pe0, double* __restrict__ dW0,
+                                                         double* __restrict__ db0, const float* __restrict__ pe4,
+                                                         double* __restrict__ dW4, int np, int we) {
+  static_assert(WgradCfg<0>::RT == 1024 && WgradCfg<1>::RT == 1024, "one block size for both sums");
+  if (blockIdx.y == 0) wgrad_reduce_body<0>(part1, np, nullptr, coef1, dW1, db1, nullptr, np, 0);
+  else if (blockIdx.y == 1) wgrad_reduce_body<1>(pe0, we, nullptr, nullptr, dW0, db0, nullptr, we, 0);
+  else wgrad_reduce_body<1>(pe4, we, nullptr, nullptr, dW4, nullptr, nullptr, we, in_features(4));
 }
 
 // ---- k_dgrad_ws: the data gradient in the weight-stationary form of k_train_ws<0,true>.  A workgroup of 8 waves (two per
@@ -3063,6 +3084,52 @@ __device__ __forceinline__ constexpr int fb_vmcnt(int n) {   // s_waitcnt vmcnt(
   return (n & 15) | ((n >> 4) << 14) | 0x0F70;
 }
 
+// The previous layer's weight-gradient partials, summed in a k_bwd_fused launch's prologue (k_wgrad_reduce's sum,
+// one row per workgroup of the 256) instead of by a launch of its own: mode 0 none, 1 the 256-column layout
+// (WgradCfg<0>), 2 the skip layer's (WgradCfg<2>: hidden columns at 64, dW rows of 319)
+struct FbRed {
+  const float* part;
+  const float* coef;   // that layer's coefp (alpha at 512, beta'' at 768)
+  double* dW;
+  double* db;
+  int mode;
+};
+
+// Row m = blockIdx.x of dW += alpha G + beta'' (x) db over FB_PAIRS partials; red: 640 doubles of LDS
+__device__ __forceinline__ void fb_reduce_row(const FbRed& R, double* red, int t) {
+  const int m = (int)blockIdx.x;
+  const int C = R.mode == 2 ? WgradCfg<2>::C : WgradCfg<0>::C, colh = R.mode == 2 ? 64 : 0;
+  const size_t PART = (size_t)256 * C + 256;
+  const int c = t & 255, hv = t >> 8;
+  const float* pc = R.part + (size_t)m * C + colh + c;
+  double Gp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int b0 = 0; b0 < FB_PAIRS / 2; b0 += 32) {
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = pc[(size_t)(FB_PAIRS / 2 * hv + b0 + j) * PART];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) Gp[j & 7] += (double)v[j];
+  }
+  red[t] = ((Gp[0] + Gp[1]) + (Gp[2] + Gp[3])) + ((Gp[4] + Gp[5]) + (Gp[6] + Gp[7]));
+  if (t < FB_PAIRS) {
+    double d = (double)R.part[(size_t)t * PART + (size_t)256 * C + m];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    if ((t & 63) == 0) red[512 + (t >> 6)] = d;
+  }
+  __syncthreads();
+  if (t < 256) {
+    const double dbm = red[512] + red[513];
+    const double G = red[t] + red[t + 256];
+    const int in_f = R.mode == 2 ? 319 : 256, wcol = R.mode == 2 ? 63 : 0;
+    R.dW[(size_t)m * in_f + wcol + c] += (double)R.coef[512 + c] * G + (double)R.coef[768 + c] * dbm;
+    if (t == 0) R.db[m] += dbm;
+  }
+  __syncthreads();
+}
+static_assert(FB_PAIRS == 128 && 2 * FB_PAIRS == 256, "fb_reduce_row: one row per workgroup, two 64-pair halves");
+
 // OUT (layer 7 only): g_7 = dL/dh_7 is not read from HBM but made in LDS from h_7 (gin, DMA'd as the raw tile) and
 // the chunk's dL/dlogit (ograd): g_7 = (dL/dlogit A - B) - (h_7 - mean_7) K with k_fb_prep's per-column A = w_out s,
 // B = gm s, K = kk s, s = invstd gamma_7 (k_out_bwd_grad's terms, the same cancellation order), and the operand scale
@@ -3077,7 +3144,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
                                                        const unsigned* __restrict__ gmax_in,
                                                        unsigned* __restrict__ gmax_out, float* __restrict__ part,
                                                        const float* __restrict__ ograd,
-                                                       const float* __restrict__ ocst) {
+                                                       const float* __restrict__ ocst, FbRed red) {
   constexpr int C = WgradCfg<LAY>::C, COL = LAY == 2 ? 64 : 0;
   extern __shared__ __attribute__((aligned(16))) char fb[];
   // LDS: split operands of tiles k & 1 (two buffers), the raw tile (one buffer), constants
@@ -3212,8 +3279,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
   // Pipeline, one barrier per tile: tile k computes from split buffer k & 1 while each wave splits ITS rows of tile
   // k + 1 (raw, DMA'd during tile k - 1) into buffer (k + 1) & 1 between the data- and weight-gradient MFMAs, then
   // DMAs its rows of tile k + 2 into the raw buffer it has just read
+  if (nk > 0) issue_raw(0);
+  // the previous layer's partials (split buffer 0 as scratch: convert(0) writes it after the reduction's barriers)
+  if (red.mode != 0) fb_reduce_row(red, reinterpret_cast<double*>(fb), t);
   if (nk > 0) {
-    issue_raw(0);
     __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
     if constexpr (OUT) out_rows();
     convert(0);
@@ -3454,6 +3523,10 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t oenc = take(tiles * 512 * sizeof(f32x4));
   const size_t ow = take(TRAIN_W_FLOATS * 4), ot = take(DGRAD_W_FLOATS * 4), ost = take(8 * 512 * 8);
   // partials: up to 2 WG_BLOCKS records of the skip layer's layout (its encoding columns, two workgroups per CU)
+  // partials: the layered path's 2 x WG_BLOCKS sets; the one-pass path's two hidden-layer sets (FB_PAIRS each) and
+  // the two encoding-column sets (WG_BLOCKS each) fit in the same space
+  static_assert(2 * FB_PAIRS * WgradCfg<2>::PART + 2 * WG_BLOCKS * WgradCfg<1>::PART <= 2 * WG_BLOCKS * WgradCfg<2>::PART,
+                "one-pass backward partial sets");
   const size_t oc = take(8 * 1024 * 4), op = take(2 * WG_BLOCKS * WgradCfg<2>::PART * 4);
   const size_t os = take((8 * S12_LAYER + OSTAT_COPIES * 257 + GMAX_DBL) * 8), oa = take((size_t)gacc_layout().total * 8);
   const size_t owh = take(TRAIN_H_VECS * sizeof(f16x8)), osw = take(16 * sizeof(int));
@@ -3585,47 +3658,42 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                        FB.oacc + ci * 257, gvmax, ws.ocst, ws.gmax);
   }
   const unsigned fbg = (unsigned)(2 * FB_PAIRS);
+  // two partial sets, by layer parity: layer L's launch writes set L & 1 and sums layer L + 1's set in its prologue
+  float* const pset[2] = {ws.part, ws.part + (size_t)FB_PAIRS * WgradCfg<2>::PART};
   for (int L = 7; L >= 1; --L) {
     const float* coefp = ws.coef + 1024 * (L - 1);
     const float* gin = hh[L];   // layer 7: h_7, from which k_bwd_fused<0, true> makes g_7
-    {
-      ProfScope ps(s, PT_BWD_FUSED, 2.0 * 2.0 * 256.0 * 256.0 * dn, 3072.0 * dn);
-      auto launch = [&](auto kern, size_t lds) {
-        hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), lds, s, gin, hh[L - 1], ws.wth16 + (size_t)(L - 1) * HW_H,
-                           ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1), P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS,
-                           ws.gmax + (L - 1) * GMAX_SLOTS, ws.part, grad + c0, (const float*)ws.ocst);
-      };
-      if (L == 7)
-        launch(k_bwd_fused<0, true>, FB_LDS_OUT);
-      else if (L == 4)
-        launch(k_bwd_fused<2, false>, FB_LDS);
-      else
-        launch(k_bwd_fused<0, false>, FB_LDS);
-    }
-    ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0);
-    if (L == 4)   // (its encoding columns come with layer 0's at the end: no encoding-column partials here)
-      hipLaunchKernelGGL(k_wgrad_reduce<2>, dim3(256), dim3(WgradCfg<2>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[4],
-                         coefp, ws.gacc + G.w[4], ws.gacc + G.b[4], (double*)nullptr, 0);
+    FbRed red{nullptr, nullptr, nullptr, nullptr, 0};
+    if (L < 7)
+      red = FbRed{pset[(L + 1) & 1], ws.coef + 1024 * L, ws.gacc + G.w[L + 1], ws.gacc + G.b[L + 1], L + 1 == 4 ? 2 : 1};
+    ProfScope ps(s, PT_BWD_FUSED, 2.0 * 2.0 * 256.0 * 256.0 * dn, 3072.0 * dn);
+    auto launch = [&](auto kern, size_t lds) {
+      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), lds, s, gin, hh[L - 1], ws.wth16 + (size_t)(L - 1) * HW_H,
+                         ws.sw, L, n, coefp, ws.bnb + 512 * (L - 1), P.bn_w[L - 1], ws.gmax + L * GMAX_SLOTS,
+                         ws.gmax + (L - 1) * GMAX_SLOTS, pset[L & 1], grad + c0, (const float*)ws.ocst, red);
+    };
+    if (L == 7)
+      launch(k_bwd_fused<0, true>, FB_LDS_OUT);
+    else if (L == 4)
+      launch(k_bwd_fused<2, false>, FB_LDS);
     else
-      hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(256), dim3(WgradCfg<0>::RT), 0, s, ws.part, FB_PAIRS, P.lin_w[L],
-                         coefp, ws.gacc + G.w[L], ws.gacc + G.b[L], (double*)nullptr, FB_PAIRS);
+      launch(k_bwd_fused<0, false>, FB_LDS);
   }
   // layer 0 and the skip layer's encoding columns in ONE pass over the staged encoding (k_wgrad_b3 MODE 3: g_0 and
-  // g_4 in their store slots), one workgroup per CU, two partial sets in layer 0's layout
+  // g_4 in their store slots), one workgroup per CU, two partial sets in layer 0's layout (after the two hidden sets)
   const unsigned we = (unsigned)std::min<int64_t>(ntiles, WG_BLOCKS);
-  float* part_e4 = ws.part + (size_t)WG_BLOCKS * WgradCfg<1>::PART;
+  float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
+  float* const part_e4 = part_e0 + (size_t)WG_BLOCKS * WgradCfg<1>::PART;
   {
     ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 2.0 * 256.0 * 64 * dn, 2048.0 * dn);
     launch_wgrad_b3_one<3, 1, true, 3>(we, s, rays, ray_stride, z, n_samples, c0, n, ein, hh[0], nullptr, nullptr,
-                                       ws.gmax + 0 * GMAX_SLOTS, ws.part, ws.pbound, hh[4], ws.gmax + 4 * GMAX_SLOTS,
+                                       ws.gmax + 0 * GMAX_SLOTS, part_e0, ws.pbound, hh[4], ws.gmax + 4 * GMAX_SLOTS,
                                        part_e4);
   }
-  ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * we * WgradCfg<1>::PART * 4.0);
-  hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, ws.part, (int)we, P.lin_w[0],
-                     (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr, (int)we, 0);
-  hipLaunchKernelGGL(k_wgrad_reduce<1>, dim3(256), dim3(WgradCfg<1>::RT), 0, s, part_e4, (int)we, P.lin_w[4],
-                     (const float*)nullptr, ws.gacc + G.w[4], (double*)nullptr, (double*)nullptr, (int)we,
-                     in_features(4));
+  ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0 + 2.0 * we * WgradCfg<1>::PART * 4.0);
+  hipLaunchKernelGGL(k_fb_reduce_tail, dim3(256, 3), dim3(1024), 0, s, pset[1], (const float*)ws.coef,
+                     ws.gacc + G.w[1], ws.gacc + G.b[1], part_e0, ws.gacc + G.w[0], ws.gacc + G.b[0], part_e4,
+                     ws.gacc + G.w[4], FB_PAIRS, (int)we);
 }
 
 static void backward_train(const float* rays, int ray_stride, const float* z, int n_samples, const float* ein,
