@@ -587,11 +587,13 @@ def kernel_report(L, a, train_math, eval_math=None):
     esplit = eval_math == "f16x2_3"
     nterm = 3 if (train_math in ("f16x2_3", "f16x2_3_fused") or esplit) else 4
     hid = f"k_train_h<0,true,{nterm}>" if split else "k_train_ws<0,true>"
-    knames = {0: "k_nof_eval_h3<false>" if esplit else "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
+    knames = {0: "k_nof_eval_h3<false,false>" if esplit else "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
               3: f"k_train_h<8,true,{nterm}>" if split else "k_train_ws<8,true>",
               10: "k_wgrad<2>+k_wgrad<1>" if split else "k_wgrad<0>", 11: f"k_dgrad_h<{nterm}>" if split else "k_dgrad_ws",
               13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>",
-              16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw", 18: "k_nof_eval_h3<true>",
+              16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw",
+              # (the train query writing the activation store is its own instantiation)
+              18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" else "k_nof_eval_h3<true,false>",
               19: "k_bwd_fused<0,false>"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
