@@ -3084,7 +3084,7 @@ __device__ __forceinline__ constexpr int fb_vmcnt(int n) {   // s_waitcnt vmcnt(
   return (n & 15) | ((n >> 4) << 14) | 0x0F70;
 }
 
-// The previous layer's weight-gradient partials, summed in a k_bwd_fused launch's prologue (k_wgrad_reduce's sum,
+// The previous layer's weight-gradient partials, summed at the end of a k_bwd_fused launch (k_wgrad_reduce's sum,
 // one row per workgroup of the 256) instead of by a launch of its own: mode 0 none, 1 the 256-column layout
 // (WgradCfg<0>), 2 the skip layer's (WgradCfg<2>: hidden columns at 64, dW rows of 319)
 struct FbRed {
@@ -3103,13 +3103,12 @@ __device__ __forceinline__ void fb_reduce_row(const FbRed& R, double* red, int t
   const int c = t & 255, hv = t >> 8;
   const float* pc = R.part + (size_t)m * C + colh + c;
   double Gp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  {   // all 64 of the thread's loads in flight (32 at a time: +0.3 % step)
+    float v[FB_PAIRS / 2];
 #pragma unroll
-  for (int b0 = 0; b0 < FB_PAIRS / 2; b0 += 32) {
-    float v[32];
+    for (int j = 0; j < FB_PAIRS / 2; ++j) v[j] = pc[(size_t)(FB_PAIRS / 2 * hv + j) * PART];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = pc[(size_t)(FB_PAIRS / 2 * hv + b0 + j) * PART];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) Gp[j & 7] += (double)v[j];
+    for (int j = 0; j < FB_PAIRS / 2; ++j) Gp[j & 7] += (double)v[j];
   }
   red[t] = ((Gp[0] + Gp[1]) + (Gp[2] + Gp[3])) + ((Gp[4] + Gp[5]) + (Gp[6] + Gp[7]));
   if (t < FB_PAIRS) {
@@ -3280,8 +3279,6 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
   // k + 1 (raw, DMA'd during tile k - 1) into buffer (k + 1) & 1 between the data- and weight-gradient MFMAs, then
   // DMAs its rows of tile k + 2 into the raw buffer it has just read
   if (nk > 0) issue_raw(0);
-  // the previous layer's partials (split buffer 0 as scratch: convert(0) writes it after the reduction's barriers)
-  if (red.mode != 0) fb_reduce_row(red, reinterpret_cast<double*>(fb), t);
   if (nk > 0) {
     __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
     if constexpr (OUT) out_rows();
@@ -3444,6 +3441,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
       if (kg == 0) pb[(size_t)256 * C + 32 * wv + 16 * jb + lm] = d * gun;
     }
   }
+  // the previous layer's partials (split buffer 0 as scratch; after the loop, where the registers are free and
+  // other workgroups' loops still run: -0.3 % step against the prologue, profiles/r04_variants_bwd_reductions.txt)
+  __syncthreads();
+  if (red.mode != 0) fb_reduce_row(red, reinterpret_cast<double*>(fb), t);
 }
 
 struct GradTable {
