@@ -3278,8 +3278,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
   // Pipeline, one barrier per tile: tile k computes from split buffer k & 1 while each wave splits ITS rows of tile
   // k + 1 (raw, DMA'd during tile k - 1) into buffer (k + 1) & 1 between the data- and weight-gradient MFMAs, then
   // DMAs its rows of tile k + 2 into the raw buffer it has just read
-  if (nk > 0) issue_raw(0);
   if (nk > 0) {
+    issue_raw(0);
     __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
     if constexpr (OUT) out_rows();
     convert(0);
