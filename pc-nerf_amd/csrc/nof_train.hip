@@ -2780,7 +2780,10 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   // Pipeline: half tile u computes from buffer u % 3 while half tile u + 2 is staged into buffer (u + 2) % 3 from
   // registers loaded during u - 1 (pieces at column blocks S_P0 + k S_PD), the loads of u + 3 go out after the last
   // piece, and u + 1's A operand and first B block are read (already staged and fenced) before the barrier.
-  f32x4 rv[NR];
+  // DEEP (the two-layer encoding form): two register sets, the loads of half tile u + 4 issued at u (two half tiles
+  // of latency instead of one; nh is even): 131.3 -> 128.1 us per launch (profiles/r04_variants_enc_wgrad_deep.txt)
+  constexpr bool DEEP = DUAL;
+  f32x4 rv[NR], rv1[DEEP ? NR : 1];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
     if (u < nh) {
@@ -2789,6 +2792,8 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       for (int k = 0; k < NP; ++k) stage_piece(u, rv, tile_of(u), u & 1, k);
     }
   if (2 < nh) load_half(rv, tile_of(2), 0);
+  if constexpr (DEEP)
+    if (3 < nh) load_half(rv1, tile_of(3), 1);
   __syncthreads();
   constexpr int S_PD = NBLK / NP < WB3_SPACE ? NBLK / NP : WB3_SPACE;
   constexpr int S_P0 = WB3_STAGE + (NP - 1) * S_PD < NBLK ? WB3_STAGE : 0;
@@ -2809,10 +2814,10 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
   int bcur = 0;
   // the loop body is branch-free (a branch would split the scheduling regions the MFMA chains are interleaved in):
   // past the end, the reads of half tile u + 1 and the staging of u + 2 touch buffers nobody reads afterwards, and
-  // the loads of u + 3 re-read the last half tile
-  for (int u = 0; u < nh; ++u) {
+  // the loads of u + 3 (DEEP: u + 4) re-read the last half tile
+  auto body = [&](int u, f32x4 (&rvs)[NR]) __attribute__((always_inline)) {
     const int bn1 = bcur == 2 ? 0 : bcur + 1, bn2 = bcur == 0 ? 2 : bcur - 1;
-    const int u2 = u + 2 < nh ? u + 2 : nh - 1, u3 = u + 3 < nh ? u + 3 : nh - 1;
+    const int u2 = u + 2 < nh ? u + 2 : nh - 1, u3 = u + (DEEP ? 4 : 3) < nh ? u + (DEEP ? 4 : 3) : nh - 1;
     float av[RB][8], av2[RB][8];
 #pragma unroll
     for (int nb = 0; nb < NBLK; ++nb) {
@@ -2859,8 +2864,8 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
       }
 #pragma unroll
       for (int k = 0; k < NP; ++k)
-        if (nb == S_P0 + k * S_PD) stage_piece(bn2, rv, tile_of(u2), u2 & 1, k);
-      if (nb == S_P0 + (NP - 1) * S_PD) load_half(rv, tile_of(u3), u3 & 1);
+        if (nb == S_P0 + k * S_PD) stage_piece(bn2, rvs, tile_of(u2), u2 & 1, k);
+      if (nb == S_P0 + (NP - 1) * S_PD) load_half(rvs, tile_of(u3), u3 & 1);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
@@ -2872,6 +2877,14 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
         if constexpr (DUAL) Acur2[rb][p] = Anext2[rb][p];
       }
     bcur = bn1;
+  };
+  if constexpr (DEEP) {
+    for (int u = 0; u < nh; u += 2) {   // (half tiles u and u + 1: the register sets by parity)
+      body(u, rv);
+      body(u + 1, rv1);
+    }
+  } else {
+    for (int u = 0; u < nh; ++u) body(u, rv);
   }
   static_assert(!DUAL || (H2 && LAY == 1), "the two-layer encoding form: f16x2, both partial sets in layer 0's layout");
   static_assert(MODE != 2 && (LAY == MODE || LAY == 2 || DUAL), "partial layouts");
