@@ -2936,7 +2936,8 @@ __global__ __launch_bounds__(512 / RB, 1) void k_wgrad_b3(const float* __restric
 // into fp16 hi + mid, stored [sample][feature] with 16-byte chunks swizzled by row (fb_off): conflict-free for the
 // data gradient's 16-byte reads (8 neurons of a sample) and the weight gradient's transposed ds_read_b64_tr_b16
 // reads (8 samples of a feature).  g_{L-1} is written in place over h_{L-1} (each workgroup reads exactly the
-// columns it writes); the weight-gradient partial per pair in k_wgrad<LAY>'s layout (k_wgrad_reduce sums them).
+// columns it writes); the weight-gradient partial per pair in k_wgrad<LAY>'s layout (summed at the end of the next
+// layer's launch, fb_reduce_row; layer 1's by k_fb_reduce_tail).
 constexpr int FB_GP = 512, FB_XP = 256;                   // g / x part row bytes (256 / 128 halves)
 constexpr int FB_GPART = 32 * FB_GP, FB_XPART = 32 * FB_XP;
 constexpr int FB_BUF = 2 * FB_GPART + 2 * FB_XPART;       // 48 KiB per tile
