@@ -3425,9 +3425,15 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
       }
     }
     };
+    // the MFMA phases at raised wave priority, so a SIMD's other wave (in its split / epilogue) does not delay their
+    // issue: -1.0 % per launch (the split and epilogue raised instead: +0.3 %; profiles/r04_variants_bwd_prio.txt)
+    __builtin_amdgcn_s_setprio(1);
     dgrad();
+    __builtin_amdgcn_s_setprio(0);
     split_next();
+    __builtin_amdgcn_s_setprio(1);
     wgrad();
+    __builtin_amdgcn_s_setprio(0);
     epilogue();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();   // every wave done with split buffer k & 1 and has filled (k + 1) & 1
