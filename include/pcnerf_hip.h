@@ -194,6 +194,22 @@ int pcnerf_nof_query_train_backward_fused(const float* rays, int64_t n_rays, int
                                           const float* grad_logit, void* state, size_t state_bytes, void* workspace,
                                           size_t workspace_bytes, const pcnerf_nof_grads* grads, const void* store,
                                           int64_t store_chunks, void* stream);
+/* The training step's forward and backward without any activation store (the default training path since round 5;
+ * replaces the autograd of render.py:47-50 / models.py:183-203 that train_kitti.py:155's loss.backward() runs).
+ * pcnerf_nof_query_train_fused_state: the fused query above, keeping its `state` (pcnerf_nof_train_fold_bytes
+ * (total_samples, chunk) bytes: the chunks' encoding moments and layer maps) for the backward; nothing else is
+ * written.  pcnerf_nof_query_train_backward_remat: every chunk's layers in ONE pass each (data gradient, BatchNorm
+ * backward, weight gradient), each layer's input h_{L-1} - mean rematerialised per tile from the chunk's encoding
+ * through its exact layer map P'_{L-1} (identity activations, models.py:72: the premise of the statistics); `state`
+ * is consumed (its Sigma products are overwritten), `workspace` is pcnerf_nof_backward_workspace_bytes(chunk) bytes;
+ * train math 1 (f16x2_3) only.  Gradients are ADDED to `grads`. */
+int pcnerf_nof_query_train_fused_state(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                       int n_samples, int64_t chunk, const pcnerf_nof_params* params, float momentum,
+                                       float eps, void* state, size_t state_bytes, float* p_out, void* stream);
+int pcnerf_nof_query_train_backward_remat(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                          int n_samples, int64_t chunk, const pcnerf_nof_params* params, float eps,
+                                          const float* grad_logit, void* state, size_t state_bytes, void* workspace,
+                                          size_t workspace_bytes, const pcnerf_nof_grads* grads, void* stream);
 /* NOF.forward(emb) in train mode on an embedded batch of n rows (one chunk), the same way. */
 int pcnerf_nof_forward_train_fused(const float* emb, int64_t n, const pcnerf_nof_params* params, float momentum,
                                    float eps, void* state, size_t state_bytes, float* p_out, void* stream);

@@ -850,12 +850,13 @@ static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, fl
 // the chunk statistics from the encoding moments and the float64 layer algebra above, then k_nof_eval_h3<true>.
 static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, float momentum, float eps,
                           void* state, size_t state_bytes, float* p_out, hipStream_t s, void* store = nullptr,
-                          int64_t store_chunks = 0) {
+                          int64_t store_chunks = 0, bool keep = false) {
   PCN_CHECK(q.total > 0 && q.chunk > 0, "train query: empty input");
   // nn.BatchNorm1d raises for a chunk of one sample (render.py:47-50 would hit it on a 1-sample tail)
   PCN_CHECK(q.total % q.chunk != 1 && q.total != 1, "Expected more than 1 value per channel when training");
-  // with an activation store the state is the backward's too (fold_bn_backward): the full layout
-  const FoldLayout Lo = fold_layout(q.total, q.chunk, store == nullptr);
+  // with an activation store, or kept for the rematerialised backward (keep), the state is the backward's too
+  // (fold_bn_backward): the full layout
+  const FoldLayout Lo = fold_layout(q.total, q.chunk, store == nullptr && !keep);
   PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "train query: state buffer too small");
   PCN_CHECK(Lo.C < 65536, "train query: too many chunks for one query");
   NofParamsDev P;
@@ -954,7 +955,7 @@ FoldBnBwd fold_bn_backward(const float* rays, int stride, const float* z, int S,
   hipLaunchKernelGGL(k_tf_bwd_layer<3>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
   hipLaunchKernelGGL(k_tf_bwd_layer<2>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
   hipLaunchKernelGGL(k_tf_bwd_layer<1>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
-  return FoldBnBwd{F.dg, F.sr, F.oacc, F.C};
+  return FoldBnBwd{F.dg, F.sr, F.oacc, F.C, F.pp, F.eb, F.q};
 }
 
 }  // namespace pcn
@@ -983,6 +984,23 @@ extern "C" int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, i
   const SampleSrc q{rays, ray_stride, z, n_samples, nullptr, total, std::min(chunk, total)};
   fused_forward(q, params, momentum, eps, state, state_bytes, p_out, (hipStream_t)stream);
   PCN_LAUNCH_CHECK("pcnerf_nof_query_train_fused");
+  PCN_API_END
+}
+
+// The training step's forward: the fused query, its state in the full layout (pcnerf_nof_train_fold_bytes) kept for
+// pcnerf_nof_query_train_backward_remat -- nothing else is written for the backward.
+extern "C" int pcnerf_nof_query_train_fused_state(const float* rays, int64_t n_rays, int ray_stride, const float* z,
+                                                  int n_samples, int64_t chunk, const pcnerf_nof_params* params,
+                                                  float momentum, float eps, void* state, size_t state_bytes,
+                                                  float* p_out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && state && p_out, "pcnerf_nof_query_train_fused_state: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_fused_state: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_fused_state: ray_stride < 6");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  const SampleSrc q{rays, ray_stride, z, n_samples, nullptr, total, std::min(chunk, total)};
+  fused_forward(q, params, momentum, eps, state, state_bytes, p_out, (hipStream_t)stream, nullptr, 0, true);
+  PCN_LAUNCH_CHECK("pcnerf_nof_query_train_fused_state");
   PCN_API_END
 }
 

@@ -2946,6 +2946,15 @@ constexpr size_t FB_LDS = 3 * (size_t)FB_BUF + 7 * 128 * sizeof(float);   // spl
 constexpr size_t FB_LDS_OUT = FB_LDS + (4 * 256 + 8 * 64) * sizeof(float);  // + occ_out / BatchNorm 7 constants,
                                                                             //   dL/dlogit slots
 
+// The rematerialised backward (k_bwd_remat, the default since round 5) moves g between layers PRE-SPLIT: a tile's
+// g as the split buffer's g half holds it ([part 2][sample 32][feature 256] fp16 at fb_off<FB_GP>, 32 KiB), scaled
+// by 2^gexp[L], so the consumer DMAs it straight into its split buffer; and the chunk's encoding image (FB_ENC bytes
+// per tile, k_remat_enc) the same way.  Encoding row r's 16-byte chunk ch sits at ch ^ ((r >> 1) & 7): the x
+// product's 16-byte B-operand reads (8 features of one sample, lanes = 16 samples x 4 chunks) are conflict-free.
+constexpr int FB_ENC = 8192;
+constexpr int GS_TILE = 2 * FB_GPART;
+__device__ __forceinline__ int fb_eoff(int r, int ch) { return r * 128 + 16 * (ch ^ ((r >> 1) & 7)); }
+
 // 16-byte chunk c of row r sits at c ^ f(r), f(r) = 2 (r & 3 | b << 2) | p with p = bit 2 of r and b = bit 2 ^ bit 3:
 // sixteen distinct values over a row block of 16 (the split writes: 32 lanes = 16 rows x two 8-byte halves of one
 // chunk), distinct f >> 1 over rows {0..3, 8..11} and over {4..7, 12..15} (the transposed reads: 8 rows x 2 chunks),
@@ -3045,9 +3054,15 @@ __global__ __launch_bounds__(256) void k_fb_prep(NofParamsDev P, const double* _
                                                  float* __restrict__ ocst, unsigned* __restrict__ gmax) {
   __shared__ float wmax[4];
   const int L = blockIdx.x, k = threadIdx.x;
-  const double s1 = stats[512 * L + 2 * k], s2 = stats[512 * L + 2 * k + 1];
-  const double m = s1 / (double)n;
-  double var = s2 / (double)n - m * m;
+  double m, var;
+  if (stats) {
+    const double s1 = stats[512 * L + 2 * k], s2 = stats[512 * L + 2 * k + 1];
+    m = s1 / (double)n;
+    var = s2 / (double)n - m * m;
+  } else {   // no store (rematerialised backward): the fold's exact statistics, as the forward's coefficients
+    m = F.pp[(((int64_t)L * F.C + c) * 256 + k) * 64 + 63];
+    var = F.sr[((int64_t)L * F.C + c) * 1024 + 768 + k];
+  }
   if (var < 0.0) var = 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   float* cf = coef + 1024 * L;
@@ -3086,6 +3101,107 @@ __global__ __launch_bounds__(256) void k_fb_prep(NofParamsDev P, const double* _
     gmax[7 * GMAX_SLOTS] = __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
     *gvmax = 0u;
   }
+}
+
+// The rematerialised backward's operand images (k_bwd_fused<., ., true>).  Column scale 2^s_k of the encoding
+// image: the sin / cos features (and their chunk means) lie in [-1, 1], so |e - ebar| <= 2 -> 2^13; the xyz features
+// |e - ebar| <= 2 max |position| (k_pos_bound) -> 2^(13 - ilogb max|position|); every scaled value below 2^15.
+__device__ __forceinline__ int remat_sx(int k, float pmax) {
+  if (k >= 3) return 13;
+  int e = (pmax > 0.0f && pmax < 3.0e38f) ? 13 - ilogbf(pmax) : 13;
+  return e < -60 ? -60 : e > 60 ? 60 : e;
+}
+
+// grid (8 layers, C chunks), 256 threads (row i of P'_L for chunk c): the row scaled by 2^(t_i - s_k), t_i putting
+// its largest entry in [2^14, 2^15), split into fp16 hi / mid in k_bwd_fused's A-operand order, and 2^-t_i
+__global__ __launch_bounds__(256) void k_remat_pimg(FoldBnBwd F, const unsigned* __restrict__ pbound,
+                                                    f16x8* __restrict__ img, float* __restrict__ scl) {
+  const int L = blockIdx.x, i = threadIdx.x;
+  const int64_t c = blockIdx.y, li = ((int64_t)L * F.C + c) * 256 + i;
+  const int sxyz = remat_sx(0, __uint_as_float(*pbound));
+  const double* row = F.pp + li * 64;
+  double mx = 0.0;
+  for (int k = 0; k < 63; ++k) mx = fmax(mx, fabs(ldexp(row[k], -(k < 3 ? sxyz : 13))));
+  int t = (mx > 0.0 && mx < 1.0e300) ? 14 - ilogb(mx) : 0;
+  t = t < -100 ? -100 : t > 100 ? 100 : t;
+  scl[li] = ldexpf(1.0f, -t);
+  f16x8* o = img + li * 16;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int kg = 0; kg < 4; ++kg) {
+      f16x8 h, m;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = 32 * ks + 8 * kg + e;
+        const float a = k < 63 ? (float)ldexp(row[k], t - (k < 3 ? sxyz : 13)) : 0.0f;
+        h[e] = (_Float16)a;
+        m[e] = (_Float16)(a - (float)h[e]);
+      }
+      o[(2 * ks) * 4 + kg] = h;
+      o[(2 * ks + 1) * 4 + kg] = m;
+    }
+}
+
+// One chunk's encoding image: per sample d = fl32(e - ebar) (encode_full, the forward's features; ebar float64),
+// times 2^s_k, split into fp16 hi / mid at [tile][part][row = sample & 31][chunk ch ^ ((row >> 1) & 7)][8]; samples
+// past the chunk (the last tile's tail) are zero.  One thread per sample; a workgroup's four tiles are assembled in
+// LDS and written as whole 16-byte lanes (1 KiB per wave store).  Block 0 also zeroes k_g7's |g_7| slots (gm7) for
+// this chunk (the previous chunk's layer 7 has read them: stream order).
+constexpr int RE_TILES = 4;
+__global__ __launch_bounds__(32 * RE_TILES) void k_remat_enc(const float* __restrict__ rays, int stride,
+                                                           const float* __restrict__ z, int S, int64_t c0, int64_t n,
+                                                           const double* __restrict__ eb,
+                                                           const unsigned* __restrict__ pbound,
+                                                           char* __restrict__ out, unsigned* __restrict__ gm7) {
+  __shared__ __attribute__((aligned(16))) char img[RE_TILES * FB_ENC];
+  __shared__ double ebs[64];
+  const int t = threadIdx.x;
+  if (t < 64) ebs[t] = t < 63 ? eb[t] : 0.0;
+  if (blockIdx.x == 0 && t < GMAX_SLOTS) gm7[t] = 0u;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * (32 * RE_TILES) + t;
+  const int64_t nrow = (n + 31) / 32 * 32;
+  float f[64];
+  if (i < n) {
+    float p[3];
+    sample_point(rays + ray_of(c0 + i, S) * stride, z[c0 + i], p);
+    encode_full(p, f);
+  }
+  const int sxyz = remat_sx(0, __uint_as_float(*pbound));
+  char* tb = img + (t >> 5) * FB_ENC;
+  const int r = t & 31;
+#pragma unroll
+  for (int ch = 0; ch < 8; ++ch) {
+    f16x8 h, m;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * ch + e;
+      const float d = (i < n && k < 63) ? (float)((double)f[k] - ebs[k]) : 0.0f;
+      const float a = ldexpf(d, k < 3 ? sxyz : 13);
+      h[e] = (_Float16)a;
+      m[e] = (_Float16)(a - (float)h[e]);
+    }
+    *reinterpret_cast<f16x8*>(tb + fb_eoff(r, ch)) = h;
+    *reinterpret_cast<f16x8*>(tb + FB_ENC / 2 + fb_eoff(r, ch)) = m;
+  }
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * RE_TILES * FB_ENC;
+  const int64_t bend = nrow / 32 * FB_ENC;
+#pragma unroll
+  for (int j = 0; j < RE_TILES * FB_ENC / 16 / (32 * RE_TILES); ++j) {
+    const int o = 16 * (t + 32 * RE_TILES * j);
+    if (b0 + o < bend) *reinterpret_cast<f32x4*>(out + b0 + o) = *reinterpret_cast<const f32x4*>(img + o);
+  }
+}
+
+// grid 7 (layers 1..7), 256 threads: sum_j |W_L[j][i]| over the 256 outputs j, for the 256 input columns i that
+// k_bwd_remat's data gradient takes (the skip layer's h columns) -- its bound on |W_L^T g_L|
+__global__ __launch_bounds__(256) void k_wcol(NofParamsDev P, float* __restrict__ wcol) {
+  const int L = 1 + blockIdx.x, i = threadIdx.x, in_f = in_features(L), col = (L == 4 ? 63 : 0) + i;
+  float s = 0.0f;
+  for (int j = 0; j < 256; ++j) s += fabsf(P.lin_w[L][(size_t)j * in_f + col]);
+  wcol[(L - 1) * 256 + i] = s;
 }
 
 template <int AUX = 0>
@@ -3467,6 +3583,419 @@ __global__ __launch_bounds__(512, 1) void k_bwd_fused(const float* __restrict__ 
   if (red.mode != 0) fb_reduce_row(red, reinterpret_cast<double*>(fb), t);
 }
 
+// ---- The rematerialised backward (the default training backward since round 5; no activation store).
+//
+// Every layer input is made per tile from the chunk's encoding instead of read from a store:
+//   h_{L-1} - mean_{L-1} = P'_{L-1} (e - ebar),   P'_L = W_L P_{L-1}   (the fold state's float64 layer maps)
+// -- the identity-activation premise (models.py:72) the BatchNorm statistics already rest on -- so the forward
+// writes nothing for the backward and every chunk takes this path whatever its size.  Operands: the encoding image
+// (k_remat_enc: d = e - ebar scaled by 2^s_k, fp16 hi / mid, 256 B per sample) and P' rows scaled by 2^(t_i - s_k)
+// and split (k_remat_pimg); the product d -> x is 3 fp16 products per fp32 product like every other.
+//
+// k_g7: g_7 = dL/dh_7 per tile, (dL/dlogit A - B) - (h_7 - mean_7) K (k_out_bwd_grad's terms and order; A, B, K
+// from k_fb_prep), h_7 - mean_7 = P'_7 d on the matrix pipe (wave w: features 32 w .. + 31, 24 MFMAs a tile, P'_7's
+// rows in registers, the encoding by LDS-DMA into two slots), written pre-split at 2^gexp[7] (k_fb_prep's bound on
+// |g_7|), its largest |g_7| recorded (gm7) for layer 7's bound on g_6.
+__global__ __launch_bounds__(512, 1) void k_g7(const char* __restrict__ enc, const float* __restrict__ ograd,
+                                               int64_t n, const f16x8* __restrict__ p7, const float* __restrict__ p7s,
+                                               const float* __restrict__ ocst, const unsigned* __restrict__ gbound,
+                                               int* __restrict__ gexp, unsigned* __restrict__ gm7,
+                                               char* __restrict__ gout) {
+  extern __shared__ __attribute__((aligned(16))) char g7l[];
+  float* const ocs = reinterpret_cast<float*>(g7l + 2 * FB_ENC);   // [A | B | 2^-t | K][256]
+  const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nt = (int)((n + 31) / 32), grid = (int)gridDim.x, bid = (int)blockIdx.x;
+  const int nk = bid < nt ? (nt - 1 - bid) / grid + 1 : 0;
+  for (int i = t; i < 1024; i += 512) ocs[i] = (i >= 512 && i < 768) ? p7s[i - 512] : ocst[i];
+  const int eg = tile_scale_exp(__uint_as_float(*gbound));
+  const float gsc = ldexpf(1.0f, eg);
+  if (bid == 0 && t == 0) gexp[7] = eg;
+  f16x8 pa[2][2][2];   // [rb][ks][part]: rows 32 wv + 16 rb + lm
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) pa[rb][ks][p] = p7[((size_t)(32 * wv + 16 * rb + lm) * 4 + 2 * ks + p) * 4 + kg];
+  auto dma = [&](int k) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    fb_glds16(enc + (size_t)(bid + k * grid) * FB_ENC + wv * 1024 + ln * 16, g7l + (k & 1) * FB_ENC + wv * 1024);
+  };
+  if (nk > 0) dma(0);
+  __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+  __syncthreads();
+  float gmo = 0.0f;
+  for (int k = 0; k < nk; ++k) {
+    const int tl = bid + k * grid;
+    float gv[2];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      const int64_t s = (int64_t)tl * 32 + 16 * sb + lm;
+      gv[sb] = ograd[s < n ? s : n - 1];
+    }
+    if (k + 1 < nk) dma(k + 1);   // slot (k + 1) & 1: tile k - 1's, read before the last barrier
+    const char* eb = g7l + (k & 1) * FB_ENC;
+    f32x4 ah[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int o = fb_eoff(16 * sb + lm, 4 * ks + kg);
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(eb + o);
+        const f16x8 bm = *reinterpret_cast<const f16x8*>(eb + FB_ENC / 2 + o);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          ah[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][ks][0], bh, ah[rb][sb], 0, 0, 0);
+          ah[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][ks][0], bm, ah[rb][sb], 0, 0, 0);
+          ah[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][ks][1], bh, ah[rb][sb], 0, 0, 0);
+        }
+      }
+    char* gt = gout + (size_t)tl * GS_TILE;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      const int sm = 16 * sb + lm;
+      const bool valid = (int64_t)tl * 32 + sm < n;
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int f = 32 * wv + 16 * rb + 4 * kg;
+        const f32x4 ca = *reinterpret_cast<const f32x4*>(ocs + f), cb = *reinterpret_cast<const f32x4*>(ocs + 256 + f);
+        const f32x4 ts = *reinterpret_cast<const f32x4*>(ocs + 512 + f), ck = *reinterpret_cast<const f32x4*>(ocs + 768 + f);
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float g7 = (gv[sb] * ca[q] - cb[q]) - (ah[rb][sb][q] * ts[q]) * ck[q];
+          v[q] = valid ? g7 : 0.0f;
+          gmo = fmaxf(gmo, fabsf(v[q]));
+          v[q] *= gsc;
+        }
+        s16x4 p0, p1;
+        split2_x4(v, p0, p1);
+        *reinterpret_cast<s16x4*>(gt + sm * FB_GP + 2 * f) = p0;
+        *reinterpret_cast<s16x4*>(gt + FB_GPART + sm * FB_GP + 2 * f) = p1;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(fb_vmcnt(8));   // this wave's DMA of tile k + 1 (the 8 stores may still fly)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+  }
+  gmo = wave_max_f(gmo);
+  if (lane == 0) atomicMax(gm7 + ((bid * 8 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
+}
+constexpr size_t G7_LDS = 2 * FB_ENC + 1024 * sizeof(float);
+
+// k_bwd_remat<LAY, GOUT>: one layer's backward over a chunk in one pass, as k_bwd_fused (a pair of workgroups per
+// tile, halves of the input features, 8 waves; W_L^T rows in registers; one barrier a tile), with
+//   * g_L arriving PRE-SPLIT by LDS-DMA straight into the tile's split buffer (no raw buffer, no conversion: its
+//     producer wrote it at 2^gexp[L]), one tile ahead;
+//   * the layer input x = h_{L-1} - mean made on the matrix pipe from the encoding image (two LDS slots, one tile
+//     deeper) and the half's P'_{L-1} rows (LDS, staged once: 12 MFMAs per wave and tile), split into the x half of
+//     the next tile's buffer between the data- and weight-gradient MFMAs;
+//   * g_{L-1} = ((dy - gm) - x kk) invstd gamma written pre-split (GOUT 0), as fp32 tiles (1: g_0, read by the
+//     encoding-column launch), or both (2: g_4), at 2^gexp[L-1] from a bound fixed in the prologue:
+//     |g_{L-1,i}| <= (sum_j |W_L[j][i]| max|g_L| + |gm_i| + sqrt(n) sigma_i |kk_i|) invstd_i |gamma_i|.
+// HBM per sample: 1 KiB of g_L, 256 B of encoding in, 1 KiB of g_{L-1} out (2.25 KiB; the store path moved 3).
+constexpr size_t RB_PX = 128 * 256;   // the half's P' rows (128 x 16 f16x8), slot q of row r at q ^ (r & 15)
+constexpr size_t RB_LDS = 2 * (size_t)FB_BUF + 2 * FB_ENC + RB_PX + 8 * 128 * sizeof(float);
+static_assert(RB_LDS <= 160 * 1024, "k_bwd_remat LDS");
+template <int LAY, int GOUT>
+__global__ __launch_bounds__(512, 1) void k_bwd_remat(const char* __restrict__ gin, char* __restrict__ gout,
+                                                       float* __restrict__ gout32, const f16x8* __restrict__ wt,
+                                                       const int* __restrict__ sw, int layer, int64_t n,
+                                                       const float* __restrict__ coefp, const float* __restrict__ bnb,
+                                                       const float* __restrict__ gamma, int* __restrict__ gexp,
+                                                       const float* __restrict__ wcol,
+                                                       const unsigned* __restrict__ gmax_in,
+                                                       unsigned* __restrict__ gmax_out, float* __restrict__ part,
+                                                       FbRed red, const char* __restrict__ enc,
+                                                       const f16x8* __restrict__ px, const float* __restrict__ pxs) {
+  constexpr int C = WgradCfg<LAY>::C, COL = LAY == 2 ? 64 : 0;
+  constexpr int NST = (GOUT != 1 ? 4 : 0) + (GOUT != 0 ? 2 : 0);   // global stores per wave and tile
+  extern __shared__ __attribute__((aligned(16))) char fb[];
+  char* const enb = fb + 2 * FB_BUF;
+  char* const pxl = enb + 2 * FB_ENC;
+  float* const cst = reinterpret_cast<float*>(pxl + RB_PX);   // [csc | cun | gm | kk | invstd | gamma | xs | bound]
+  const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int bid = (int)blockIdx.x, hf = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
+  const int npair = (int)gridDim.x >> 1;
+  const int nt = (int)((n + 31) / 32);
+  const int nk = pr < nt ? (nt - 1 - pr) / npair + 1 : 0;   // this pair's tiles: pr + k npair, k < nk
+  const float rn = sqrtf((float)n);
+  if (t < 128) {
+    const int c = 128 * hf + t;
+    const float invstd = coefp[256 + c];
+    const float bnd = rn / invstd;   // Samuelson: |h - mean| <= sqrt(n) sigma
+    int e = (bnd > 0.0f && bnd < 3.0e38f) ? 14 - ilogbf(bnd) : 0;
+    e = e < -60 ? -60 : e > 60 ? 60 : e;
+    cst[t] = ldexpf(1.0f, e);
+    cst[128 + t] = ldexpf(1.0f, -e);
+    cst[256 + t] = bnb[c];
+    cst[384 + t] = bnb[256 + c];
+    cst[512 + t] = invstd;
+    cst[640 + t] = gamma[c];
+    cst[768 + t] = ldexpf(pxs[c], e);   // x accumulator (P' rows at 2^t_i) -> x at its split scale
+  }
+  unsigned gmx = 0;
+  for (int i = 0; i < GMAX_SLOTS; ++i) gmx = max(gmx, gmax_in[i]);   // (uniform loads)
+  {   // the bound on |g_{L-1}| over all 256 columns (every workgroup computes the same value)
+    const int c = t & 255;
+    const float invstd = coefp[256 + c];
+    float ob = ((wcol[c] * __uint_as_float(gmx) + fabsf(bnb[c])) + rn / invstd * fabsf(bnb[256 + c])) * invstd *
+               fabsf(gamma[c]) * 1.01f;
+    ob = wave_max_f(ob);
+    if (lane == 0) cst[896 + wv] = ob;
+  }
+  for (int j = t; j < 128 * 16; j += 512) {   // the half's P' rows, slot-swizzled by row
+    const int r = j >> 4, q = j & 15;
+    *reinterpret_cast<f16x8*>(pxl + r * 256 + 16 * (q ^ (r & 15))) = px[(size_t)(128 * hf + r) * 16 + q];
+  }
+  const int eg = gexp[layer];
+  const float gun = ldexpf(1.0f, -eg);
+  const float dun = ldexpf(1.0f, -sw[layer]) * gun;   // data-gradient accumulator -> dL/dy
+  f16x8 wr[8][2];
+  {
+    const f16x8* __restrict__ w8 = wt + lane;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 16 + 8 * hf + wv) * 2 + p) * 64];
+  }
+  __syncthreads();
+  float obm = cst[896];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) obm = fmaxf(obm, cst[896 + i]);
+  const int eo = tile_scale_exp(obm);
+  const float gso = ldexpf(1.0f, eo);
+  if (bid == 0 && t == 0) gexp[layer - 1] = eo;
+  // g_L of tile k (pre-split image, rows of 512 B per part) -> split buffer k & 1: wave w moves rows 4w .. 4w+3 of
+  // both parts, lane l of instruction m row 4 w + 2 (m & 1) + (l >> 5), LDS chunk l & 31 <- image chunk ^ fb_swz
+  auto dma_g = [&](int k) {
+    const int tl = pr + k * npair;
+    char* const sb = fb + (size_t)(k & 1) * FB_BUF;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));   // lane addresses recomputed per tile: held across the loop they would spill
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int p = m >> 1, r0 = 4 * wv + 2 * (m & 1), r = r0 + (ln >> 5), c = (ln & 31) ^ fb_swz(r);
+      fb_glds16(gin + (size_t)tl * GS_TILE + p * FB_GPART + r * FB_GP + 16 * c, sb + p * FB_GPART + r0 * FB_GP);
+    }
+  };
+  auto dma_enc = [&](int k) {   // tile k's encoding image -> slot k & 1 (1 KiB per wave)
+    const int tl = pr + k * npair;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    fb_glds16(enc + (size_t)tl * FB_ENC + wv * 1024 + ln * 16, enb + (k & 1) * FB_ENC + wv * 1024);
+  };
+  // x of tile k (this wave's 16 columns il .. il + 15 of the half) from slot k & 1 -> split buffer k & 1's x half
+  auto remat_x = [&](int k) {
+    const char* eb = enb + (k & 1) * FB_ENC;
+    char* const xb = fb + (size_t)(k & 1) * FB_BUF + 2 * FB_GPART;
+    const int r = 16 * wv + lm;
+    f16x8 pa[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int q = (2 * ks + p) * 4 + kg;
+        pa[ks][p] = *reinterpret_cast<const f16x8*>(pxl + r * 256 + 16 * (q ^ (r & 15)));
+      }
+    f32x4 ax[2] = {f32x4{}, f32x4{}};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int o = fb_eoff(16 * sb + lm, 4 * ks + kg);
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(eb + o);
+        const f16x8 bm = *reinterpret_cast<const f16x8*>(eb + FB_ENC / 2 + o);
+        ax[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[ks][0], bh, ax[sb], 0, 0, 0);
+        ax[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[ks][0], bm, ax[sb], 0, 0, 0);
+        ax[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[ks][1], bh, ax[sb], 0, 0, 0);
+      }
+    const int il = 16 * wv + 4 * kg;
+    const f32x4 xs = *reinterpret_cast<const f32x4*>(cst + 768 + il);
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      f32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = ax[sb][q] * xs[q];   // (the image is zero past the chunk)
+      s16x4 p0, p1;
+      split2_x4(v, p0, p1);
+      const int o = fb_off<FB_XP>(16 * sb + lm, il);
+      *reinterpret_cast<s16x4*>(xb + o) = p0;
+      *reinterpret_cast<s16x4*>(xb + FB_XPART + o) = p1;
+    }
+  };
+  f32x4 aw[2][8];
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+    for (int ib = 0; ib < 8; ++ib) aw[jb][ib] = f32x4{};
+  float dbacc[2] = {0.0f, 0.0f};
+  float gmo = 0.0f;
+  const int trq = lm >> 2, trp = lm & 3;   // transposed reads: lane lm = 4 q + pp of 16-lane group kg
+  if (nk > 0) {
+    dma_g(0);
+    dma_enc(0);
+    if (nk > 1) dma_enc(1);
+    __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+    __builtin_amdgcn_s_barrier();   // every wave's part of tile 0's encoding (and the P' rows, constants)
+    remat_x(0);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  auto tile = [&](int k) {
+    const int tl = pr + k * npair;
+    if (k + 1 < nk) dma_g(k + 1);     // into split buffer (k + 1) & 1, free since the last barrier
+    if (k + 2 < nk) dma_enc(k + 2);   // into slot k & 1, read by remat_x(k) before the last barrier
+    const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
+    const char* gb = sp;
+    const char* xb = sp + 2 * FB_GPART;
+    f32x4 ad[2] = {f32x4{}, f32x4{}};
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int o = fb_off<FB_GP>(16 * sb + lm, 32 * ks + 8 * kg);
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(gb + o);
+        const f16x8 bm = *reinterpret_cast<const f16x8*>(gb + FB_GPART + o);
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bh, ad[sb], 0, 0, 0);
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bm, ad[sb], 0, 0, 0);
+        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], bh, ad[sb], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (k + 1 < nk) remat_x(k + 1);   // slot (k + 1) & 1: DMA'd a tile ago, every wave's part waited before the barrier
+    __builtin_amdgcn_s_setprio(1);
+    {   // weight gradient (k_bwd_fused's: transposed operand reads, next column block's read under the current)
+      auto read8 = [&](unsigned a0, unsigned a1, auto partc) {
+        constexpr int Q = decltype(partc)::value;
+        const s16x4 h0 = fb_tr<0>(a0), h1 = fb_tr<0>(a1), m0 = fb_tr<Q>(a0), m1 = fb_tr<Q>(a1);
+        return std::array<s16x4, 4>{h0, h1, m0, m1};
+      };
+      auto join = [](const s16x4& a, const s16x4& b) {
+        return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      using QG = std::integral_constant<int, FB_GPART>;
+      using QX = std::integral_constant<int, FB_XPART>;
+      const unsigned ga = fb_lds_addr(gb), xa = fb_lds_addr(xb);
+      const int tr0 = 8 * kg + trq, tr1 = tr0 + 4;
+      auto xrd = [&](int ib) {
+        const int col = 16 * ib + 4 * trp;
+        return read8(xa + fb_off<FB_XP>(tr0, col), xa + fb_off<FB_XP>(tr1, col), QX{});
+      };
+      std::array<s16x4, 4> ra[2], rbx[2];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int col = 32 * wv + 16 * jb + 4 * trp;
+        ra[jb] = read8(ga + fb_off<FB_GP>(tr0, col), ga + fb_off<FB_GP>(tr1, col), QG{});
+      }
+      rbx[0] = xrd(0);
+      fb_lgkm<4>(ra);
+      f16x8 A[2][2];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        A[jb][0] = join(ra[jb][0], ra[jb][1]);
+        A[jb][1] = join(ra[jb][2], ra[jb][3]);
+      }
+      if (hf == 0) {
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dbacc[jb] += (float)A[jb][0][e] + (float)A[jb][1][e];
+      }
+#pragma unroll
+      for (int ib = 0; ib < 8; ++ib) {
+        std::array<s16x4, 4> cur[1] = {rbx[ib & 1]};
+        if (ib + 1 < 8) {
+          rbx[(ib + 1) & 1] = xrd(ib + 1);
+          fb_lgkm<4>(cur);
+        } else {
+          fb_lgkm<0>(cur);
+        }
+        rbx[ib & 1] = cur[0];
+        const f16x8 B0 = join(rbx[ib & 1][0], rbx[ib & 1][1]), B1 = join(rbx[ib & 1][2], rbx[ib & 1][3]);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B0, aw[jb][ib], 0, 0, 0);
+          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B1, aw[jb][ib], 0, 0, 0);
+          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B0, aw[jb][ib], 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    {   // epilogue: dL/dy -> BatchNorm L-1 backward -> g_{L-1} (columns 128 hf + il .. + 3 of sample 16 sb + lm)
+      const int il = 16 * wv + 4 * kg;
+      const f32x4 cun = *reinterpret_cast<const f32x4*>(cst + 128 + il);
+      const f32x4 cgm = *reinterpret_cast<const f32x4*>(cst + 256 + il);
+      const f32x4 ckk = *reinterpret_cast<const f32x4*>(cst + 384 + il);
+      const f32x4 cis = *reinterpret_cast<const f32x4*>(cst + 512 + il);
+      const f32x4 cga = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+      const int i = 128 * hf + il;
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int sm = 16 * sb + lm;
+        const bool valid = (int64_t)tl * 32 + sm < n;
+        const int o = fb_off<FB_XP>(sm, il);
+        const f16x4 xh = *reinterpret_cast<const f16x4*>(xb + o);
+        const f16x4 xm = *reinterpret_cast<const f16x4*>(xb + FB_XPART + o);
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float d = ad[sb][q] * dun;
+          const float xc = ((float)xh[q] + (float)xm[q]) * cun[q];   // h - mean (hi + mid: 22 bits)
+          v[q] = valid ? ((d - cgm[q]) - xc * ckk[q]) * cis[q] * cga[q] : 0.0f;
+          gmo = fmaxf(gmo, fabsf(v[q]));
+        }
+        if constexpr (GOUT != 1) {
+          f32x4 vs;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) vs[q] = v[q] * gso;
+          s16x4 p0, p1;
+          split2_x4(vs, p0, p1);
+          char* gt = gout + (size_t)tl * GS_TILE + sm * FB_GP + 2 * i;
+          *reinterpret_cast<s16x4*>(gt) = p0;
+          *reinterpret_cast<s16x4*>(gt + FB_GPART) = p1;
+        }
+        if constexpr (GOUT != 0) {
+          f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tl * TILE_FLOATS) + (i >> 3) * 64 + sm +
+                       32 * ((i >> 2) & 1);
+          __builtin_nontemporal_store(v, dst);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs of tiles k + 1 / k + 2 (its stores may fly)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int k = 0; k < nk; ++k) tile(k);
+  gmo = wave_max_f(gmo);
+  if (lane == 0) atomicMax(gmax_out + ((bid * 8 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
+  float* pb = part + (size_t)pr * WgradCfg<LAY>::PART;
+#pragma unroll
+  for (int ib = 0; ib < 8; ++ib) {
+    const float cu = cst[128 + 16 * ib + lm] * gun;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pb[(size_t)(32 * wv + 16 * jb + 4 * kg + r) * C + COL + 128 * hf + 16 * ib + lm] = aw[jb][ib][r] * cu;
+  }
+  if (hf == 0) {
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      float d = dbacc[jb];
+      d += __shfl_xor(d, 16, 64);
+      d += __shfl_xor(d, 32, 64);
+      if (kg == 0) pb[(size_t)256 * C + 32 * wv + 16 * jb + lm] = d * gun;
+    }
+  }
+  __syncthreads();
+  if (red.mode != 0) fb_reduce_row(red, reinterpret_cast<double*>(fb), t);
+}
+
 struct GradTable {
   float* dst[34];
   int64_t off[34];
@@ -3527,6 +4056,9 @@ struct BwdWs {
   f16x8* wth16;       // W^T image of k_bwd_fused (7 layers)
   float* bnb;         // BatchNorm 0..6 backward constants of the chunk (k_fb_prep)
   float* ocst;        // occ_out / BatchNorm 7 backward constants of the chunk (k_fb_prep: [A | B | mean | K][256])
+  int* gexp;          // rematerialised backward: scale exponents of the pre-split g images, per layer
+  unsigned* gm7;      // rematerialised backward: |g_7| maximum slots (k_g7)
+  float* wcol;        // rematerialised backward: column abs sums of W_1..W_7 (k_wcol)
   size_t bytes;
 };
 
@@ -3556,6 +4088,8 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t opb = take(sizeof(unsigned));
   const size_t owt16 = take(7 * HW_H * sizeof(f16x8)), obnb = take(7 * 512 * sizeof(float));
   const size_t oocst = take(4 * 256 * sizeof(float));
+  const size_t ogexp = take(16 * sizeof(int)), ogm7 = take(GMAX_SLOTS * sizeof(unsigned));
+  const size_t owcol = take(7 * 256 * sizeof(float));
   char* b = (char*)base;
   BwdWs w;
   w.wth = (f16x8*)(b + owt);
@@ -3579,6 +4113,9 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.wth16 = (f16x8*)(b + owt16);
   w.bnb = (float*)(b + obnb);
   w.ocst = (float*)(b + oocst);
+  w.gexp = (int*)(b + ogexp);
+  w.gm7 = (unsigned*)(b + ogm7);
+  w.wcol = (float*)(b + owcol);
   w.bytes = off;
   return w;
 }
@@ -3715,6 +4252,153 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   hipLaunchKernelGGL(k_fb_reduce_tail, dim3(256, 3), dim3(1024), 0, s, pset[1], (const float*)ws.coef,
                      ws.gacc + G.w[1], ws.gacc + G.b[1], part_e0, ws.gacc + G.w[0], ws.gacc + G.b[0], part_e4,
                      ws.gacc + G.w[4], FB_PAIRS, (int)we);
+}
+
+// One chunk through the rematerialised backward (no activation store): max |dL/dlogit|, k_fb_prep on the fold's
+// statistics, the chunk's encoding image, g_7 (k_g7), layers 7..1 each in ONE k_bwd_remat launch, the encoding
+// columns of layers 0 and 4 (k_wgrad_b3 MODE 3 on g_0 and g_4 as fp32 tiles), the last partial sums.  g buffers:
+// pre-split images S0 / S1 alternate (g_7, g_5, g_3, g_1 in S0; g_6, g_4, g_2 in S1), g_4 also as fp32 tiles (F4)
+// and g_0 only as fp32 tiles (F0).
+static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs& ws, const FoldBnBwd& FB,
+                        const f16x8* pimg, const float* pscl, int64_t ci, int64_t c0, int64_t n, const float* rays,
+                        int ray_stride, const float* z, int n_samples, float eps, const float* grad, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)RB_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)RB_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat<0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)RB_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)RB_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
+    attr = true;
+  }
+  const double dn = (double)n;
+  const int64_t ntiles = (n + 31) / 32;
+  const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
+  {
+    // k_out_gabs reads 4 B per sample; k_fb_prep's traffic is per chunk (a few KB)
+    ProfScope ps(s, PT_BWD_MISC, 0.0, 4.0 * dn);
+    unsigned* gvmax = reinterpret_cast<unsigned*>(ws.ostat);
+    hipLaunchKernelGGL(k_out_gabs, dim3(eg < 256 ? eg : 256), dim3(256), 0, s, grad + c0, n, gvmax);
+    FbPrepOut po;
+    for (int L = 0; L < 8; ++L) po.g[L] = G.g[L];
+    po.d_beta7 = ws.gacc + G.be[7];
+    po.d_wout = ws.gacc + G.wo;
+    po.d_bout = ws.gacc + G.bo;
+    hipLaunchKernelGGL(k_fb_prep, dim3(8), dim3(256), 0, s, P, (const double*)nullptr, n, eps, ws.coef, FB, ci,
+                       ws.bnb, ws.gacc, po, FB.oacc + ci * 257, gvmax, ws.ocst, ws.gmax);
+  }
+  char* const encimg = reinterpret_cast<char*>(ws.enc);
+  const int64_t C = FB.C;
+  auto prow = [&](int L) { return pimg + ((size_t)L * C + ci) * 256 * 16; };
+  auto psrow = [&](int L) { return pscl + ((size_t)L * C + ci) * 256; };
+  char* const S[2] = {reinterpret_cast<char*>(ws.h[0]), reinterpret_cast<char*>(ws.h[1])};
+  float* const F4 = ws.h[2];
+  float* const F0 = ws.h[3];
+  {
+    // the encoding (30 sincosf per sample): 4 B of z in, 256 B of image out per sample
+    ProfScope ps(s, PT_BWD_REMAT, 0.0, (4.0 + 256.0) * dn);
+    hipLaunchKernelGGL(k_remat_enc, dim3((unsigned)((ntiles + RE_TILES - 1) / RE_TILES)), dim3(32 * RE_TILES), 0, s,
+                       rays, ray_stride, z, n_samples, c0, n, FB.eb + ci * 64, ws.pbound, encimg, ws.gm7);
+  }
+  {
+    // g_7: 2 x 256 x 64 fp32-FLOP per sample (h_7 - mean_7); 256 B of image + 4 B in, 1 KiB out
+    ProfScope ps(s, PT_BWD_REMAT, 2.0 * 256.0 * 64.0 * dn, (260.0 + 1024.0) * dn);
+    hipLaunchKernelGGL(k_g7, dim3((unsigned)std::min<int64_t>(ntiles, 256)), dim3(512), G7_LDS, s, encimg,
+                       grad + c0, n, prow(7), psrow(7), (const float*)ws.ocst, ws.gmax + 7 * GMAX_SLOTS, ws.gexp,
+                       ws.gm7, S[0]);
+  }
+  const unsigned fbg = (unsigned)(2 * FB_PAIRS);
+  float* const pset[2] = {ws.part, ws.part + (size_t)FB_PAIRS * WgradCfg<2>::PART};
+  for (int L = 7; L >= 1; --L) {
+    const float* coefp = ws.coef + 1024 * (L - 1);
+    FbRed red{nullptr, nullptr, nullptr, nullptr, 0};
+    if (L < 7)
+      red = FbRed{pset[(L + 1) & 1], ws.coef + 1024 * L, ws.gacc + G.w[L + 1], ws.gacc + G.b[L + 1], L + 1 == 4 ? 2 : 1};
+    const char* gin = S[(7 - L) & 1];
+    char* gout = S[(8 - L) & 1];
+    float* g32 = L == 5 ? F4 : L == 1 ? F0 : nullptr;
+    const unsigned* gmin = L == 7 ? ws.gm7 : ws.gmax + L * GMAX_SLOTS;
+    // algorithmic work: data and weight gradient (2 x 2 x 256 x 256) + the input's rematerialisation (2 x 256 x 64);
+    // bytes: g_L in (1 KiB), the encoding image (256 B), g_{L-1} out (1 KiB; 2 KiB for the layer writing both)
+    ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0 + 2.0 * 256.0 * 64.0) * dn,
+                 (1024.0 + 256.0 + (L == 5 ? 2048.0 : 1024.0)) * dn);
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), RB_LDS, s, gin, gout, g32, ws.wth16 + (size_t)(L - 1) * HW_H,
+                         (const int*)ws.sw, L, n, coefp, (const float*)(ws.bnb + 512 * (L - 1)), P.bn_w[L - 1],
+                         ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
+                         pset[L & 1], red, (const char*)encimg, prow(L - 1), psrow(L - 1));
+    };
+    if (L == 4) launch(k_bwd_remat<2, 0>);
+    else if (L == 5) launch(k_bwd_remat<0, 2>);
+    else if (L == 1) launch(k_bwd_remat<0, 1>);
+    else launch(k_bwd_remat<0, 0>);
+  }
+  const unsigned we = (unsigned)std::min<int64_t>(ntiles, WG_BLOCKS);
+  float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
+  float* const part_e4 = part_e0 + (size_t)WG_BLOCKS * WgradCfg<1>::PART;
+  {
+    ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 2.0 * 256.0 * 64 * dn, 2048.0 * dn);
+    launch_wgrad_b3_one<3, 1, true, 3>(we, s, rays, ray_stride, z, n_samples, c0, n, nullptr, F0, nullptr, nullptr,
+                                       ws.gmax + 0 * GMAX_SLOTS, part_e0, ws.pbound, F4, ws.gmax + 4 * GMAX_SLOTS,
+                                       part_e4);
+  }
+  // the partial sums read (k_fb_reduce_tail): layer 1's pair partials and the two encoding-column sets
+  ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0 + 2.0 * we * WgradCfg<1>::PART * 4.0);
+  hipLaunchKernelGGL(k_fb_reduce_tail, dim3(256, 3), dim3(1024), 0, s, pset[1], (const float*)ws.coef,
+                     ws.gacc + G.w[1], ws.gacc + G.b[1], part_e0, ws.gacc + G.w[0], ws.gacc + G.b[0], part_e4,
+                     ws.gacc + G.w[4], FB_PAIRS, (int)we);
+}
+
+static void emit_grads(const GaccLayout& G, const BwdWs& ws, const pcnerf_nof_grads* grads, hipStream_t s) {
+  GradTable T;
+  int k = 0;
+  for (int L = 0; L < 8; ++L) {
+    T.dst[k] = grads->lin_w[L], T.off[k] = G.w[L], T.len[k++] = 256 * in_features(L);
+    T.dst[k] = grads->lin_b[L], T.off[k] = G.b[L], T.len[k++] = 256;
+    T.dst[k] = grads->bn_w[L], T.off[k] = G.g[L], T.len[k++] = 256;
+    T.dst[k] = grads->bn_b[L], T.off[k] = G.be[L], T.len[k++] = 256;
+  }
+  T.dst[k] = grads->out_w, T.off[k] = G.wo, T.len[k++] = 256;
+  T.dst[k] = grads->out_b, T.off[k] = G.bo, T.len[k++] = 1;
+  hipLaunchKernelGGL(k_grad_emit, dim3((256 * 319 + 255) / 256, 34), dim3(256), 0, s, T, ws.gacc);
+}
+
+// The default training backward (train math f16x2_3 with the fused forward): every chunk through remat_chunk, on
+// the state the forward kept (pcnerf_nof_query_train_fused_state) -- no activation store, no recomputed forward, no
+// host synchronisation.
+static void backward_remat(const float* rays, int ray_stride, const float* z, int n_samples, int64_t total,
+                           int64_t chunk, const pcnerf_nof_params* params, float eps, const float* grad,
+                           void* workspace, size_t workspace_bytes, const pcnerf_nof_grads* grads, hipStream_t s,
+                           void* fstate, size_t fstate_bytes) {
+  PCN_CHECK(g_train_math == 1, "pcnerf_nof_query_train_backward_remat: needs train math 1 (f16x2_3)");
+  const BwdWs ws = carve_bwd(workspace, chunk);
+  PCN_CHECK(workspace_bytes >= ws.bytes, "pcnerf_nof_query_train_backward_remat: workspace too small");
+  NofParamsDev P;
+  PCN_CHECK(to_dev_params(params, eps, &P), "pcnerf_nof_query_train_backward_remat: null parameter pointer");
+  PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
+  const GaccLayout G = gacc_layout();
+  pos_bound_async(rays, ray_stride, z, n_samples, nullptr, total, ws.pbound, s);
+  hipLaunchKernelGGL(k_wscale, dim3(8), dim3(256), 0, s, P, ws.sw);
+  hipLaunchKernelGGL(k_pack_dgrad_h16, dim3((unsigned)((7 * HW_H + 255) / 256)), dim3(256), 0, s, P, ws.sw,
+                     ws.wth16);
+  hipLaunchKernelGGL(k_wcol, dim3(7), dim3(256), 0, s, P, ws.wcol);
+  PCN_HIP(hipMemsetAsync(ws.gacc, 0, (size_t)G.total * 8, s));
+  PCN_HIP(hipMemsetAsync(ws.ostat, 0, sizeof(unsigned), s));   // k_out_gabs's word (k_fb_prep re-zeroes it)
+  const FoldBnBwd FB = fold_bn_backward(rays, ray_stride, z, n_samples, total, chunk, P, grad, fstate, fstate_bytes, s);
+  // every chunk's P' images at once, into the Sigma products' space (free now)
+  f16x8* const pimg = static_cast<f16x8*>(FB.scratch);
+  float* const pscl = reinterpret_cast<float*>(pimg + (size_t)8 * FB.C * 256 * 16);
+  hipLaunchKernelGGL(k_remat_pimg, dim3(8, (unsigned)FB.C), dim3(256), 0, s, FB, ws.pbound, pimg, pscl);
+  for (int64_t c0 = 0; c0 < total; c0 += chunk) {
+    const int64_t n = total - c0 < chunk ? total - c0 : chunk;
+    remat_chunk(P, G, ws, FB, pimg, pscl, c0 / chunk, c0, n, rays, ray_stride, z, n_samples, eps, grad, s);
+  }
+  emit_grads(G, ws, grads, s);
+  PCN_LAUNCH_CHECK("pcnerf_nof_query_train_backward_remat");
 }
 
 static void backward_train(const float* rays, int ray_stride, const float* z, int n_samples, const float* ein,
@@ -3882,17 +4566,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
                          P.lin_w[0], (const float*)nullptr, ws.gacc + G.w[0], ws.gacc + G.b[0], (double*)nullptr, (int)wb0);
     }
   }
-  GradTable T;
-  int k = 0;
-  for (int L = 0; L < 8; ++L) {
-    T.dst[k] = grads->lin_w[L], T.off[k] = G.w[L], T.len[k++] = 256 * in_features(L);
-    T.dst[k] = grads->lin_b[L], T.off[k] = G.b[L], T.len[k++] = 256;
-    T.dst[k] = grads->bn_w[L], T.off[k] = G.g[L], T.len[k++] = 256;
-    T.dst[k] = grads->bn_b[L], T.off[k] = G.be[L], T.len[k++] = 256;
-  }
-  T.dst[k] = grads->out_w, T.off[k] = G.wo, T.len[k++] = 256;
-  T.dst[k] = grads->out_b, T.off[k] = G.bo, T.len[k++] = 1;
-  hipLaunchKernelGGL(k_grad_emit, dim3((256 * 319 + 255) / 256, 34), dim3(256), 0, s, T, ws.gacc);
+  emit_grads(G, ws, grads, s);
   PCN_LAUNCH_CHECK("pcnerf_nof_backward");
 }
 
@@ -3929,6 +4603,23 @@ extern "C" int pcnerf_nof_query_train_backward_fused(const float* rays, int64_t 
   backward_train(rays, ray_stride, z, n_samples, nullptr, n_rays * (int64_t)n_samples, chunk, params, eps,
                  grad_logit, nullptr, workspace, workspace_bytes, grads, (hipStream_t)stream, store, store_chunks,
                  state, state_bytes);
+  PCN_API_END
+}
+
+extern "C" int pcnerf_nof_query_train_backward_remat(const float* rays, int64_t n_rays, int ray_stride,
+                                                     const float* z, int n_samples, int64_t chunk,
+                                                     const pcnerf_nof_params* params, float eps,
+                                                     const float* grad_logit, void* state, size_t state_bytes,
+                                                     void* workspace, size_t workspace_bytes,
+                                                     const pcnerf_nof_grads* grads, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(rays && z && params && grad_logit && state && workspace && grads,
+            "pcnerf_nof_query_train_backward_remat: null argument");
+  PCN_CHECK(n_rays > 0 && n_samples > 0 && chunk > 0, "pcnerf_nof_query_train_backward_remat: empty input");
+  PCN_CHECK(ray_stride >= 6, "pcnerf_nof_query_train_backward_remat: ray_stride < 6");
+  const int64_t total = n_rays * (int64_t)n_samples;
+  backward_remat(rays, ray_stride, z, n_samples, total, std::min(chunk, total), params, eps, grad_logit, workspace,
+                 workspace_bytes, grads, (hipStream_t)stream, state, state_bytes);
   PCN_API_END
 }
 

@@ -53,6 +53,9 @@ struct FoldBnBwd {
   const double* sr;
   const double* oacc;
   int64_t C;
+  const double* pp;   // [8][C][256][64] P'_L (column 63: the pre-BatchNorm mean without the Linear bias)
+  const double* eb;   // [C][64] the chunks' encoding means
+  void* scratch;      // the layer maps' Sigma products (P'_L Sigma, 1 MiB per chunk): free once fold_bn_backward ran
 };
 FoldBnBwd fold_bn_backward(const float* rays, int stride, const float* z, int S, int64_t total, int64_t chunk,
                            const NofParamsDev& P, const float* g_logit, void* state, size_t state_bytes,

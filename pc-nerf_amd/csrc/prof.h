@@ -24,7 +24,8 @@ enum ProfTag {
   PT_FOLD_MOMENTS = 16,// train fold: k_tf_moments / k_tf_gmoments (per-sample encoding moments)
   PT_FOLD_ALGEBRA = 17,// train fold: the per-chunk float64 layer algebra (forward or backward)
   PT_TRAIN_QUERY = 18, // k_nof_eval_h3<true>: the fused train-mode query (per-chunk BatchNorm coefficients)
-  PT_BWD_FUSED = 19,   // k_bwd_fused: one layer's data + weight gradient in one pass (stored chunks)
+  PT_BWD_FUSED = 19,   // k_bwd_remat / k_bwd_fused: one layer's data + weight gradient in one pass
+  PT_BWD_REMAT = 20,   // the rematerialised backward's per-chunk operands: encoding image (k_remat_enc), g_7 (k_g7)
 };
 extern bool g_prof_on;
 class ProfScope {

@@ -22,10 +22,15 @@ class TrainPass(torch.autograd.Function):
     def forward(ctx, model, rays, z, noise, noise_std, eps, chunk, with_losses, sub_num, *params):
         # a chunk larger than the pass is the same single BatchNorm chunk: size workspaces and store by the pass
         chunk = max(1, min(int(chunk), z.numel()))
-        ctx.store = ctx.fold = None
+        ctx.store = ctx.fold = ctx.state = None
         if _ops.train_fold_enabled():   # opt-in exact affine fold: per-chunk moments + layer maps, no activations
             ctx.fold = _ops.fold_state(z.device, z.numel(), chunk)
             p = _ops.query(model, rays, z, chunk, fold=ctx.fold)
+        elif _ops.remat_enabled():
+            # default: no activations kept -- the fused query's state (moments + layer maps, ~3 MB per chunk) only;
+            # the backward rematerialises every layer input from the encoding
+            ctx.state = _ops.fold_state(z.device, z.numel(), chunk)
+            p = _ops.query(model, rays, z, chunk, keep=ctx.state)
         else:
             # keep the chunks' layer outputs for the backward in the HBM left after its workspace (+ 4 GiB margin)
             L = _ops.H.lib()
@@ -53,6 +58,9 @@ class TrainPass(torch.autograd.Function):
         if ctx.fold is not None:
             grads = _ops.nof_query_backward_fold(ctx.model, rays, z, ctx.chunk, g_logit, ctx.fold)
             ctx.fold = None
+        elif ctx.state is not None:
+            grads = _ops.nof_query_backward_remat(ctx.model, rays, z, ctx.chunk, g_logit, ctx.state)
+            ctx.state = None
         else:
             grads = _ops.nof_query_backward(ctx.model, rays, z, ctx.chunk, g_logit, ctx.store)
             ctx.store.release()

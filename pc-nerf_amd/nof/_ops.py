@@ -218,16 +218,49 @@ def _track_batches(model, n_chunks: int) -> None:
             bn.num_batches_tracked.add_(n_chunks)
 
 
-def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fold=None) -> torch.Tensor:
+# The training backward under the default train math ("f16x2_3_fused"): "remat" (default since round 5) keeps no
+# activations -- the forward keeps only its fold state and the backward rematerialises each layer's input per tile
+# from the chunk's encoding (pcnerf_nof_query_train_backward_remat); "store" is round 4's activation store (the
+# forward writes the layer outputs of the chunks its budget holds, the rest are recomputed layer by layer).
+_TRAIN_BACKWARD = os.environ.get("PCNERF_TRAIN_BACKWARD", "remat")
+
+
+def set_train_backward(mode: str) -> str:
+    """Select the default train math's backward ("remat" or "store"); returns the previous one."""
+    global _TRAIN_BACKWARD
+    if mode not in ("remat", "store"):
+        raise ValueError("train backward must be 'remat' or 'store'")
+    prev, _TRAIN_BACKWARD = _TRAIN_BACKWARD, mode
+    return prev
+
+
+def remat_enabled() -> bool:
+    """True when a train-mode render pass keeps no activations (default train math, remat backward)."""
+    return _TRAIN_FUSED and _TRAIN_BACKWARD == "remat" and not _TRAIN_FOLD
+
+
+def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fold=None, keep=None) -> torch.Tensor:
     """Occupancy p (R, S) of the samples o + d*z through Embedding + NOF (render.py:18-25 / 44-51).
     ``store`` (train mode): an ActivationStore whose chunks keep the layer outputs for the backward.
     ``fold`` (train mode): a fold_state buffer -- the query runs through the train fold and keeps its state there
-    (also taken, with a temporary buffer, when set_train_fold(True))."""
+    (also taken, with a temporary buffer, when set_train_fold(True)).
+    ``keep`` (train mode, default math): a fold_state buffer the fused query keeps its state in for
+    nof_query_backward_remat."""
     L = H.lib()
     R, S = z.shape
     p = torch.empty((R, S), dtype=torch.float32, device=z.device)
     st = _stream(z)
-    if model.training and (fold is not None or _TRAIN_FOLD):
+    if model.training and keep is not None:
+        if not _TRAIN_FUSED:
+            raise RuntimeError("query(keep=...) needs the default train math (f16x2_3_fused)")
+        chunk = max(1, min(int(chunk), R * S))
+        mom, eps = _bn_config(model)
+        s, keep_params = _params(model)
+        H.check(L.pcnerf_nof_query_train_fused_state(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                                     ctypes.byref(s), mom, eps, keep.data_ptr(), keep.numel(),
+                                                     p.data_ptr(), st))
+        _track_batches(model, -(-R * S // int(chunk)))
+    elif model.training and (fold is not None or _TRAIN_FOLD):
         chunk = max(1, min(int(chunk), R * S))
         mom, eps = _bn_config(model)
         s, keep = _params(model)
@@ -699,6 +732,23 @@ def nof_query_backward(model, rays, z, chunk: int, g_logit, store=None) -> list:
         H.check(L.pcnerf_nof_query_train_backward(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
                                                   ctypes.byref(s), eps, _f32(g_logit).data_ptr(), ws.data_ptr(),
                                                   ws.numel(), ctypes.byref(gs), _stream(z)))
+    return out
+
+
+def nof_query_backward_remat(model, rays, z, chunk: int, g_logit, state) -> list:
+    """Parameter gradients (grad_params order) of the default train-mode query whose forward kept ``state``
+    (query(..., keep=state)); the state is consumed."""
+    L = H.lib()
+    R, S = z.shape
+    chunk = max(1, min(int(chunk), R * S))
+    _, eps = _bn_config(model)
+    s, keep = _params(model)
+    gs, out = _grads_struct(model, z.device)
+    ws = _workspace(z.device, L.pcnerf_nof_backward_workspace_bytes(int(chunk)))
+    H.check(L.pcnerf_nof_query_train_backward_remat(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
+                                                    ctypes.byref(s), eps, _f32(g_logit).data_ptr(), state.data_ptr(),
+                                                    state.numel(), ws.data_ptr(), ws.numel(), ctypes.byref(gs),
+                                                    _stream(z)))
     return out
 
 

@@ -67,12 +67,17 @@ def named(m):
     return dict(m.named_parameters())
 
 
-@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused"])
+@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused", "f16x2_3_fused_store"])
 def train_math(request):
+    """The layered split math, fp32 MFMA, the default (fused forward + rematerialising backward) and the default
+    forward with round 4's activation-store backward."""
     from nof import _ops
-    prev = _ops.set_train_math(request.param)
-    yield request.param
+    mode = request.param
+    prev = _ops.set_train_math("f16x2_3_fused" if mode.startswith("f16x2_3_fused") else mode)
+    prevb = _ops.set_train_backward("store" if mode.endswith("_store") else "remat")
+    yield mode
     _ops.set_train_math(prev)
+    _ops.set_train_backward(prevb)
 
 
 @pytest.mark.parametrize("name", ["pcnerf", "divide", "original"])
