@@ -173,7 +173,12 @@ def pmc_traffic(kernel_name: str, line: str = None):
     except (OSError, ValueError):
         return None, None
     ks = d.get("kernels", d)
-    v = ks.get(f"{kernel_name}@{line}") or ks.get(kernel_name, {}) if line else ks.get(kernel_name, {})
+    # a line with its own name (train_step_refcfg, config3) takes only its own profile's entry; the mode-named lines
+    # the kernel's entry
+    if line in EXTRA_LINES and EXTRA_LINES[line].get("line") == line:
+        v = ks.get(f"{kernel_name}@{line}", {})
+    else:
+        v = ks.get(f"{kernel_name}@{line}") or ks.get(kernel_name, {}) if line else ks.get(kernel_name, {})
     meta = d.get("_meta", {})
     return v.get("hbm_bytes_per_launch"), ({"file": "profiles/pmc_traffic.json", "head": v.get("head", meta.get("head")),
                                             "profile": v.get("profile", meta.get("profile"))} if v else None)
@@ -242,7 +247,12 @@ def make_blocks(a, rank, world, dev, syn):
 # the reference's published 779 rays/s), render_rays_val and the two-step inference.
 EXTRA_LINES = {
     "train_step": dict(mode="train_step", rays=65536, samples=128, importance=256, cpu_rays=512),
-    "train_step_refcfg": dict(mode="train_step", rays=256, samples=768, importance=1536, cpu_rays=64),
+    "train_step_refcfg": dict(mode="train_step", rays=256, samples=768, importance=1536, cpu_rays=64,
+                              line="train_step_refcfg"),
+    # BASELINE config 3: one training step of 262,144 KITTI-fixture rays at 64/128 (train_kitti.py:117-155; 256
+    # BatchNorm chunks of 262,144 samples -- the reference's shell chunk)
+    "config3": dict(config=3, mode="train_step", rays=262144, samples=64, importance=128, cpu_rays=256,
+                    line="config3"),
     "val": dict(mode="val", rays=65536, samples=128, importance=256, cpu_rays=2048),
     "view": dict(mode="view", rays=16384, samples=128, importance=256, cpu_rays=512),
 }
@@ -345,8 +355,9 @@ def run_line(a, L, dev, rank, world):
             _ops.set_train_fold(True)
         else:
             _ops.set_eval_fold(True)
-    # this caller allocates nothing between forward and backward: let the store take the free HBM
-    prev_budget = _ops.set_activation_store_budget(1 << 62) if grad else None
+    # (the default training backward keeps no activation store; under set_train_backward("store") this caller, which
+    # allocates nothing between forward and backward, lets the store take the free HBM)
+    prev_budget = _ops.set_activation_store_budget(1 << 62) if grad and not _ops.remat_enabled() else None
     blocks = make_blocks(a, rank, world, dev, syn)
     for blk in blocks:
         blk["mc"] = syn.load_into(NOF_coarse(), syn.init_nof_params(blk["seeds"][0])).to(dev).train(train)
@@ -441,14 +452,14 @@ def run_line(a, L, dev, rank, world):
     elapsed, loss_val = timed(a.steps, a.warmup)
     log(f"{a.mode}: {1e3 * elapsed / a.steps:.2f} ms/step")
     kstep_ms = breakdown.get("ms", 0.0)
-    roof, kernels = kernel_report(L, a, train_math, eval_math)
+    roof, kernels = kernel_report(L, a, train_math, eval_math, getattr(a, "line", None) or a.mode)
 
     # the same workload with the MLP on the fp32 MFMA pipe (train / eval math "fp32"), for comparison
     fp32_line = None
     if train and train_math != "fp32" and not a.no_fp32_line and not a.fold:
         _ops.set_train_math("fp32")
         el32, _ = timed(a.steps, 1)
-        roof32, k32 = kernel_report(L, a, "fp32")
+        roof32, k32 = kernel_report(L, a, "fp32", line="fp32")
         _ops.set_train_math(train_math)
         fp32_line = {"value": None, "ms_per_step": round(1e3 * el32 / a.steps, 3), "roofline": roof32,
                      "kernels": {k: v for k, v in k32.items() if k.startswith("train")},
@@ -457,7 +468,7 @@ def run_line(a, L, dev, rank, world):
     if eval_math not in (None, "fp32") and not a.no_fp32_line:
         _ops.set_eval_math("fp32")
         el32, _ = timed(a.steps, 1)
-        roof32, k32 = kernel_report(L, a, None, "fp32")
+        roof32, k32 = kernel_report(L, a, None, "fp32", line="fp32")
         _ops.set_eval_math(eval_math)
         fp32_line = {"value": None, "ms_per_step": round(1e3 * el32 / a.steps, 3), "roofline": roof32,
                      "kernels": {k: v for k, v in k32.items() if k.startswith("eval")},
@@ -472,7 +483,7 @@ def run_line(a, L, dev, rank, world):
     del blocks, opt, step, block_step
     gc.collect()
     torch.cuda.empty_cache()
-    if grad:
+    if prev_budget is not None or (grad and not _ops.remat_enabled()):
         _ops.set_activation_store_budget(prev_budget)
     if a.fold:
         _ops.set_train_fold(False)
@@ -581,8 +592,12 @@ def dtype_label(train_math, eval_math, fold=False):
 FP16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense BF16/FP16 MFMA
 
 
-def kernel_report(L, a, train_math, eval_math=None):
-    """Kernel breakdown of the last timed step (library HIP events) and the dominant kernel's roofline."""
+def kernel_report(L, a, train_math, eval_math=None, line=None):
+    """Kernel breakdown of the last timed step (library HIP events) and the dominant kernel's roofline; ``line``
+    selects the PMC traffic entries (pmc_traffic)."""
+    from nof import _ops
+    line = line or a.mode
+    remat = a.mode == "train_step" and train_math == "f16x2_3_fused" and _ops.remat_enabled()
     split = train_math in ("f16x2_3", "f16x2_4", "f16x2_3_fused")
     esplit = eval_math == "f16x2_3"
     nterm = 3 if (train_math in ("f16x2_3", "f16x2_3_fused") or esplit) else 4
@@ -593,9 +608,9 @@ def kernel_report(L, a, train_math, eval_math=None):
               13: "k_nof_eval_fold", 14: f"k_wgrad_b3<1,0,0,true,{nterm}>", 15: f"k_train_h1<{nterm}>",
               16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw",
               # (the train query writing the activation store is its own instantiation)
-              18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" else "k_nof_eval_h3<true,false>",
-              19: "k_bwd_fused<0,false>"}
-    pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd"}
+              18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" and not remat else "k_nof_eval_h3<true,false>",
+              19: "k_bwd_remat<0,0>" if remat else "k_bwd_fused<0,false>"}
+    pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd", 20: "k_g7"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
     ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)
@@ -604,10 +619,10 @@ def kernel_report(L, a, train_math, eval_math=None):
                   (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
                   (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold"), (14, "wgrad_b3"),
                   (15, "train_h1"), (16, "fold_moments"), (17, "fold_algebra"), (18, "train_query"),
-                  (19, "bwd_fused")):
+                  (19, "bwd_fused"), (20, "bwd_remat_operands")):
         tm, n, f, b = prof_read(L, t)
         if n:
-            tr, src = pmc_traffic(pmc_names.get(t, ""), a.mode)
+            tr, src = pmc_traffic(pmc_names.get(t, ""), line)
             kernels[nm] = {"kernel": pmc_names.get(t), "ms_per_step": round(tm, 3), "launches_per_step": n,
                            "avg_us": round(1e3 * tm / n, 2),
                            "TFLOP/s": round(f / (tm * 1e-3) / 1e12, 2) if f else None,
@@ -617,7 +632,7 @@ def kernel_report(L, a, train_math, eval_math=None):
     avg_s = ktime_ms * 1e-3 / max(klaunch, 1)
     achieved = (kflops / max(klaunch, 1)) / avg_s / 1e12
     gbs = kbytes / max(klaunch, 1) / avg_s / 1e9
-    traffic, traffic_src = pmc_traffic(kname, a.mode)
+    traffic, traffic_src = pmc_traffic(kname, line)
     nprod = nterm   # k_wgrad_b3 too: f16x2 parts, nterm products (the six-product bf16x3 form is a build option)
     if a.fold:   # no MLP left: the query moves 8 B per sample (+ ray rows) and is bound by its sincos (VALU)
         roof = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

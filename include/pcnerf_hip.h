@@ -186,13 +186,14 @@ int pcnerf_nof_query_train_fused_store(const float* rays, int64_t n_rays, int ra
 /* The training backward after pcnerf_nof_query_train_fused_store (the autograd of render.py:47-50 / models.py:183-203
  * in train_kitti.py:155's loss.backward(), as pcnerf_nof_query_train_backward): `state` is that forward's state.
  * Each stored chunk's layers run ONE pass each (data gradient, BatchNorm backward and weight gradient together,
- * g_{L-1} written over h_{L-1} in the store, which the call consumes); the BatchNorm-backward statistics per chunk
+ * g_{L-1} written over h_{L-1} in the store, which the call CONSUMES: a second backward on the same store would read
+ * gradients as activations -- recompute instead); the BatchNorm-backward statistics per chunk
  * come from the state (the chunk's encoding and gradient moments, float64).  Chunks beyond store_chunks are
  * recomputed and take the two-pass backward.  Gradients are ADDED to `grads`. */
 int pcnerf_nof_query_train_backward_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z,
                                           int n_samples, int64_t chunk, const pcnerf_nof_params* params, float eps,
                                           const float* grad_logit, void* state, size_t state_bytes, void* workspace,
-                                          size_t workspace_bytes, const pcnerf_nof_grads* grads, const void* store,
+                                          size_t workspace_bytes, const pcnerf_nof_grads* grads, void* store,
                                           int64_t store_chunks, void* stream);
 /* The training step's forward and backward without any activation store (the default training path since round 5;
  * replaces the autograd of render.py:47-50 / models.py:183-203 that train_kitti.py:155's loss.backward() runs).

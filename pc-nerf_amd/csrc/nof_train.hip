@@ -2946,14 +2946,18 @@ constexpr size_t FB_LDS = 3 * (size_t)FB_BUF + 7 * 128 * sizeof(float);   // spl
 constexpr size_t FB_LDS_OUT = FB_LDS + (4 * 256 + 8 * 64) * sizeof(float);  // + occ_out / BatchNorm 7 constants,
                                                                             //   dL/dlogit slots
 
-// The rematerialised backward (k_bwd_remat, the default since round 5) moves g between layers PRE-SPLIT: a tile's
-// g as the split buffer's g half holds it ([part 2][sample 32][feature 256] fp16 at fb_off<FB_GP>, 32 KiB), scaled
-// by 2^gexp[L], so the consumer DMAs it straight into its split buffer; and the chunk's encoding image (FB_ENC bytes
-// per tile, k_remat_enc) the same way.  Encoding row r's 16-byte chunk ch sits at ch ^ ((r >> 1) & 7): the x
-// product's 16-byte B-operand reads (8 features of one sample, lanes = 16 samples x 4 chunks) are conflict-free.
+// The rematerialised backward (k_bwd_remat, the default since round 5) moves g between layers PRE-SPLIT, scaled by
+// 2^gexp[L], in the byte layout its consumer's LDS holds it, so it is DMA'd with no conversion: per 32-sample tile
+// [part 2][octet o 32][cell][8 fp16] (32 KiB), cell = sample ^ (12 (o & 1)) holding features 8 o .. 8 o + 7 of that
+// sample (gs_off).  That one layout makes the data gradient's 16-byte B-operand reads (16 samples of one octet per
+// lane group), the weight gradient's transposed reads (4 samples x 16 features per 16 lanes) and the producer's
+// 8-byte stores (16 samples x 2 halves: 256 contiguous bytes per octet) conflict-free / contiguous.  The chunk's
+// encoding image (FB_ENC bytes per tile, k_remat_enc) is DMA'd the same way: row r's 16-byte chunk ch sits at
+// ch ^ ((r >> 1) & 7) (conflict-free 16-byte B-operand reads, lanes = 16 samples x 4 chunks).
 constexpr int FB_ENC = 8192;
 constexpr int GS_TILE = 2 * FB_GPART;
 __device__ __forceinline__ int fb_eoff(int r, int ch) { return r * 128 + 16 * (ch ^ ((r >> 1) & 7)); }
+__device__ __forceinline__ int gs_off(int s, int o) { return (o * 32 + (s ^ (12 * (o & 1)))) * 16; }
 
 // 16-byte chunk c of row r sits at c ^ f(r), f(r) = 2 (r & 3 | b << 2) | p with p = bit 2 of r and b = bit 2 ^ bit 3:
 // sixteen distinct values over a row block of 16 (the split writes: 32 lanes = 16 rows x two 8-byte halves of one
@@ -3672,8 +3676,9 @@ __global__ __launch_bounds__(512, 1) void k_g7(const char* __restrict__ enc, con
         }
         s16x4 p0, p1;
         split2_x4(v, p0, p1);
-        *reinterpret_cast<s16x4*>(gt + sm * FB_GP + 2 * f) = p0;
-        *reinterpret_cast<s16x4*>(gt + FB_GPART + sm * FB_GP + 2 * f) = p1;
+        const int o = gs_off(sm, f >> 3) + 2 * (f & 7);
+        *reinterpret_cast<s16x4*>(gt + o) = p0;
+        *reinterpret_cast<s16x4*>(gt + FB_GPART + o) = p1;
       }
     }
     __builtin_amdgcn_s_waitcnt(fb_vmcnt(8));   // this wave's DMA of tile k + 1 (the 8 stores may still fly)
@@ -3769,18 +3774,15 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat(const char* __restrict__ g
   const int eo = tile_scale_exp(obm);
   const float gso = ldexpf(1.0f, eo);
   if (bid == 0 && t == 0) gexp[layer - 1] = eo;
-  // g_L of tile k (pre-split image, rows of 512 B per part) -> split buffer k & 1: wave w moves rows 4w .. 4w+3 of
-  // both parts, lane l of instruction m row 4 w + 2 (m & 1) + (l >> 5), LDS chunk l & 31 <- image chunk ^ fb_swz
+  // g_L of tile k (pre-split image) -> split buffer k & 1's g half: a linear copy, 4 KiB per wave
   auto dma_g = [&](int k) {
     const int tl = pr + k * npair;
     char* const sb = fb + (size_t)(k & 1) * FB_BUF;
     int ln = lane;
     asm volatile("" : "+v"(ln));   // lane addresses recomputed per tile: held across the loop they would spill
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int p = m >> 1, r0 = 4 * wv + 2 * (m & 1), r = r0 + (ln >> 5), c = (ln & 31) ^ fb_swz(r);
-      fb_glds16(gin + (size_t)tl * GS_TILE + p * FB_GPART + r * FB_GP + 16 * c, sb + p * FB_GPART + r0 * FB_GP);
-    }
+    for (int m = 0; m < 4; ++m)
+      fb_glds16(gin + (size_t)tl * GS_TILE + (4 * wv + m) * 1024 + 16 * ln, sb + (4 * wv + m) * 1024);
   };
   auto dma_enc = [&](int k) {   // tile k's encoding image -> slot k & 1 (1 KiB per wave)
     const int tl = pr + k * npair;
@@ -3858,7 +3860,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat(const char* __restrict__ g
     for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
-        const int o = fb_off<FB_GP>(16 * sb + lm, 32 * ks + 8 * kg);
+        const int o = gs_off(16 * sb + lm, 4 * ks + kg);
         const f16x8 bh = *reinterpret_cast<const f16x8*>(gb + o);
         const f16x8 bm = *reinterpret_cast<const f16x8*>(gb + FB_GPART + o);
         ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bh, ad[sb], 0, 0, 0);
@@ -3890,7 +3892,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat(const char* __restrict__ g
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
         const int col = 32 * wv + 16 * jb + 4 * trp;
-        ra[jb] = read8(ga + fb_off<FB_GP>(tr0, col), ga + fb_off<FB_GP>(tr1, col), QG{});
+        ra[jb] = read8(ga + gs_off(tr0, col >> 3) + 2 * (col & 7), ga + gs_off(tr1, col >> 3) + 2 * (col & 7), QG{});
       }
       rbx[0] = xrd(0);
       fb_lgkm<4>(ra);
@@ -3955,7 +3957,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat(const char* __restrict__ g
           for (int q = 0; q < 4; ++q) vs[q] = v[q] * gso;
           s16x4 p0, p1;
           split2_x4(vs, p0, p1);
-          char* gt = gout + (size_t)tl * GS_TILE + sm * FB_GP + 2 * i;
+          char* gt = gout + (size_t)tl * GS_TILE + gs_off(sm, i >> 3) + 2 * (i & 7);
           *reinterpret_cast<s16x4*>(gt) = p0;
           *reinterpret_cast<s16x4*>(gt + FB_GPART) = p1;
         }
@@ -4203,8 +4205,8 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
     // max |dL/dlogit| (into the first word of the output-statistics copies, which the one-pass backward does not
     // use: it takes those statistics from the fold; zero before the first chunk, re-zeroed by k_fb_prep), then
     // every constant of the chunk's layers in one launch (k_fb_prep); g_7 itself is made inside layer 7's
-    // k_bwd_fused
-    ProfScope ps(s, PT_BWD_MISC, 0.0, 2.0 * 1024.0 * dn);
+    // k_bwd_fused.  Bytes: k_out_gabs reads 4 B of dL/dlogit per sample; k_fb_prep's are per chunk (a few KB)
+    ProfScope ps(s, PT_BWD_MISC, 0.0, 4.0 * dn);
     unsigned* gvmax = reinterpret_cast<unsigned*>(ws.ostat);
     hipLaunchKernelGGL(k_out_gabs, dim3(eg < 256 ? eg : 256), dim3(256), 0, s, grad + c0, n, gvmax);
     FbPrepOut po;
@@ -4592,7 +4594,7 @@ extern "C" int pcnerf_nof_query_train_backward_fused(const float* rays, int64_t 
                                                      const pcnerf_nof_params* params, float eps,
                                                      const float* grad_logit, void* state, size_t state_bytes,
                                                      void* workspace, size_t workspace_bytes,
-                                                     const pcnerf_nof_grads* grads, const void* store,
+                                                     const pcnerf_nof_grads* grads, void* store,
                                                      int64_t store_chunks, void* stream) {
   PCN_API_BEGIN
   PCN_CHECK(rays && z && params && grad_logit && state && workspace && grads,

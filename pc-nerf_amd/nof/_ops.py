@@ -179,7 +179,11 @@ _depth2_order = "stable"
 
 
 def set_depth2_order(order: str) -> str:
-    """Select depth2's order of equal weights; returns the previous one."""
+    """Select depth2's order of equal weights; returns the previous one.  A process-wide setting (the library keeps
+    one static): every thread and stream of the process renders with it.  For rows of at most 32 samples torch's GPU
+    sort is a bitonic network, which does NOT keep equal keys in index order, so for S <= 32 neither setting is
+    the order a GPU run of the reference would give there: depth2's tie order is parity-unpinned for such rows
+    (no reference GPU output exists to pin either order; the goldens pin "cpu")."""
     global _depth2_order
     if order not in _DEPTH2_ORDER:
         raise ValueError(f"depth2 order must be one of {sorted(_DEPTH2_ORDER)}")
@@ -691,6 +695,12 @@ class ActivationStore:
         n_chunks = -(-int(total_samples) // int(chunk))
         self.budget = store_budget(device, reserve) if n_chunks > 0 else 0
         self.n_chunks = min(n_chunks, self.budget // self.per_chunk)
+        # the fused query addresses a stored layer with a 32-bit byte offset: a chunk whose layer region reaches 4 GiB
+        # (>= 4,194,304 samples) is not stored there, every chunk is recomputed instead (the layered maths' store
+        # has no such limit)
+        layer_bytes = (self.per_chunk - 8 * 512 * 8) // 8
+        if _TRAIN_FUSED and layer_bytes >= 1 << 32:
+            self.n_chunks = 0
         self.buf = None
         self.fstate = None   # the fused forward's state (query), read by the one-pass backward
         while self.n_chunks > 0:
@@ -723,6 +733,10 @@ def nof_query_backward(model, rays, z, chunk: int, g_logit, store=None) -> list:
                                                         fstate.data_ptr(), fstate.numel(), ws.data_ptr(), ws.numel(),
                                                         ctypes.byref(gs), store.buf.data_ptr(), store.n_chunks,
                                                         _stream(z)))
+        # that backward wrote g_{L-1} over the stored h_{L-1}: the store is consumed, so a second backward on it
+        # recomputes every chunk instead of reading gradients as activations
+        store.fstate = None
+        store.n_chunks = 0
     elif store is not None and store.n_chunks > 0:
         H.check(L.pcnerf_nof_query_train_backward_store(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S,
                                                         int(chunk), ctypes.byref(s), eps, _f32(g_logit).data_ptr(),
