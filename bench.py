@@ -127,7 +127,8 @@ def dry_run(a, world, rank):
     dist = world > 1
     if dist:
         tdist.init_process_group("gloo")
-    blocks = blocks_of_rank(rank, world, world if a.config in (2, 3) else {4: 4, 5: 8}[a.config])
+    blocks = (list(range(8)) if a.config == 5 else    # config 5: every block, a row-balanced share of each
+              blocks_of_rank(rank, world, world if a.config in (2, 3) else 4))
     x = torch.randn(256, 256)
 
     def step():
@@ -211,9 +212,19 @@ def kitti_fixture_rays(dev):
 
 
 def make_blocks(a, rank, world, dev, syn):
-    """This rank's work: a list of parent blocks, each {rays, other, gt, seeds, sub_num}."""
-    from nof.blocks import blocks_of_rank
+    """This rank's work: a list of parent blocks, each {rays, other, gt, seeds, sub_num}.  Config 5 (the two-step
+    inference over 8 parent blocks): every rank holds all 8 blocks' weights (replicated) and renders a row-balanced
+    share of WHOLE ray groups of each block (nof.blocks.split_groups), so no rank waits on a larger block."""
+    from nof.blocks import blocks_of_rank, split_groups
     out = []
+    if a.config == 5 and a.mode == "view":
+        for b in range(8):
+            vr, vo, vg = syn.make_view_rows(a.rays, n_children=32, seed=1000 * b)
+            s, e = split_groups(vr[:, 12], world)[rank]
+            out.append(dict(block=b, rays=torch.from_numpy(vr[s:e]).to(dev), other=torch.from_numpy(vo[s:e]).to(dev),
+                            gt=torch.from_numpy(vg[s:e]).to(dev), seeds=(1234 + b, 5678 + b), sub_num=32,
+                            groups=int((vr[s:e, 12] >= -0.5).sum())))
+        return out
     if a.config == 3:
         scene = kitti_fixture_rays(dev)
         gen = torch.Generator(device=dev).manual_seed(rank)
@@ -477,7 +488,8 @@ def run_line(a, L, dev, rank, world):
 
     # rays processed per step by the whole job (weak scaling: every rank its own blocks / batch)
     # (view: LiDAR rays = ray groups, a.rays per block; otherwise the rays of the block's batch)
-    n_local = a.rays * len(blocks) if view else sum(blk["rays"].shape[0] for blk in blocks)
+    n_local = (sum(blk.get("groups", a.rays) for blk in blocks) if view
+               else sum(blk["rays"].shape[0] for blk in blocks))
     blocks_rank0 = [blk["block"] for blk in blocks]
     sample = {k: blocks[0][k] for k in ("block", "rays", "seeds", "sub_num")}
     del blocks, opt, step, block_step

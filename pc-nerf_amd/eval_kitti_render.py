@@ -14,6 +14,12 @@ Per test frame ((j+1-3-data_start) % 5 == 0, eval_kitti_render.py:1025-1033):
      (or ``_one_step``), float32 xyz binary PCD like open3d writes.
 Rendering is per row in eval mode, so the batch size only bounds memory: results are identical for any
 ``batch_rows`` (tests/test_eval_driver.py checks this).
+
+Multi-GPU (torchrun, one process per GPU; the reference has no multi-GPU path): every rank holds the block's
+coarse/fine weights (replicated) and renders a contiguous share of WHOLE ray groups of the rows the reference renders
+(its batching rule decides which rows that is), shares cut by row count (nof.blocks.split_groups); the effective
+points are gathered to rank 0 in rank order (nof.blocks.gather_rows, RCCL over xGMI), which writes the same PCD a
+single process writes.  Rank 0 alone writes the row cache.
 """
 from __future__ import annotations
 
@@ -28,7 +34,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+import torch.distributed as dist  # noqa: E402
+
 from nof import dataset as D  # noqa: E402
+from nof.blocks import gather_rows, split_groups  # noqa: E402
 from nof import io as nio  # noqa: E402
 from nof.networks import Embedding, NOF_coarse, NOF_fine  # noqa: E402
 from nof.raytable import build_view_rows  # noqa: E402
@@ -76,6 +85,7 @@ def get_opts(argv=None):
     # this implementation only
     a('--device', type=str, default='cuda')
     a('--batch_rows', type=int, default=0, help="rows per render call (0: the reference's 4096 KITTI / 18432 MaiCity)")
+    a('--dist_backend', type=str, default='nccl', help="collective backend under torchrun (nccl = RCCL)")
     return p.parse_args(argv)
 
 
@@ -174,13 +184,33 @@ def cache_dir(h, f):
     return os.path.join(h.result_path, step, f"{f}pcd", "childnerf_ray_intersect")
 
 
-def render_frame(models, rows, other, h, batch_rows):
-    """Steps 2-3 for one frame -> (points (M,3) float32 of the effective rows, n_rows rendered)."""
+def group_batches(group_col, s0: int, e0: int, batch_rows: int):
+    """Rows [s0, e0) (whole groups) in batches of >= batch_rows rows that never end inside a group (the reference's
+    rule without its end-of-table quirks: a rank's share is not the table's end)."""
+    out, i = [], s0
+    while i < e0:
+        e = min(i + batch_rows, e0)
+        while e < e0 and group_col[e] < -0.5:
+            e += 1
+        out.append((i, e))
+        i = e
+    return out
+
+
+def render_frame(models, rows, other, h, batch_rows, rank=0, world=1):
+    """Steps 2-3 for one frame -> (points (M,3) float32 of the effective rows, n_rows rendered).  With world > 1
+    every rank renders its share of the rows the single-process run renders and rank 0 receives every rank's
+    points in rank order (others get None)."""
     mc, mf, emb = models
     col = rows[:, 12].cpu().numpy()
     pts, done = [], 0
+    slices = batch_slices(col, batch_rows)
+    if world > 1:
+        n_render = slices[-1][1] if slices else 0
+        s0, e0 = split_groups(col, world, 0, n_render)[rank]
+        slices = group_batches(col, s0, e0, batch_rows)
     with torch.no_grad():
-        for s, e in batch_slices(col, batch_rows):
+        for s, e in slices:
             r = render_rays_view_0525_2_2(mc, mf, emb, rows[s:e], other[s:e], N_samples=h.N_samples,
                                           N_importance=h.N_importance, use_disp=h.use_disp, perturb=h.perturb,
                                           noise_std=h.noise_std, chunk=h.chunk,
@@ -188,8 +218,12 @@ def render_frame(models, rows, other, h, batch_rows):
             m = r['rays_effective_flag_fine'].reshape(-1).bool()
             pts.append(r['points_inference_fine'][m])
             done += e - s
-    out = torch.cat(pts) if pts else torch.zeros((0, 3), device=rows.device)
-    return out.to(torch.float32), done
+    out = (torch.cat(pts) if pts else torch.zeros((0, 3), device=rows.device)).to(torch.float32)
+    if world > 1:
+        n = torch.tensor([done], dtype=torch.int64, device=rows.device)
+        dist.all_reduce(n)
+        return gather_rows(out.contiguous(), dst=0), int(n)
+    return out, done
 
 
 def load_models(h, device):
@@ -204,6 +238,24 @@ def load_models(h, device):
 
 def main(argv=None):
     h = get_opts(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    own_group = False
+    if world > 1 and not dist.is_initialized():
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if h.device == "cuda" and h.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            h.device = f"cuda:{local}"
+        dist.init_process_group(h.dist_backend)
+        own_group = True
+    try:
+        return _run(h, rank, world)
+    finally:
+        if own_group:
+            dist.destroy_process_group()
+
+
+def _run(h, rank, world):
     dev = torch.device(h.device)
     models = load_models(h, dev)
     batch_rows = h.batch_rows or (18432 if h.dataset == "maicity" else 4096)
@@ -215,18 +267,23 @@ def main(argv=None):
         if h.test_data_create:
             scene = scene or Scene(h, dev)
             rows, ranges, other, tin = scene.view_rows(f, h.depth_inference_method)
-            nio.save_view_rows(cdir, rows.cpu().numpy(), other.cpu().numpy(), ranges.cpu().numpy(), tin.cpu().numpy())
+            if rank == 0:
+                nio.save_view_rows(cdir, rows.cpu().numpy(), other.cpu().numpy(), ranges.cpu().numpy(),
+                                   tin.cpu().numpy())
         else:
             r, o, g, _ = nio.load_view_rows(cdir)
             rows, other = torch.from_numpy(r).to(dev), torch.from_numpy(o).to(dev)
-        pts, n = render_frame(models, rows, other, h, batch_rows)
+        pts, n = render_frame(models, rows, other, h, batch_rows, rank, world)
+        if rank != 0:
+            continue
         if h.pcd_path:
             os.makedirs(os.path.dirname(os.path.abspath(h.pcd_path + "x")), exist_ok=True)
             suffix = "_two_step.pcd" if h.depth_inference_method == 2 else "_one_step.pcd"
             nio.write_pcd(h.pcd_path + str(f) + suffix, pts.cpu().numpy())
         torch.cuda.synchronize(dev)
         report.append({"frame": f, "rows": n, "points": int(pts.shape[0]), "seconds": time.perf_counter() - t0})
-    print(json.dumps(report))
+    if rank == 0:
+        print(json.dumps(report))
     return report
 
 

@@ -8,6 +8,7 @@ MI355X and over gloo in the CPU tests.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -19,6 +20,28 @@ def blocks_of_rank(rank: int, world: int, n_blocks: int) -> list[int]:
     q, r = divmod(n_blocks, world)
     start = rank * q + min(rank, r)
     return list(range(start, start + q + (1 if rank < r else 0)))
+
+
+def split_groups(group_col, world: int, start: int = 0, end: int | None = None) -> list[tuple[int, int]]:
+    """Rows [start, end) of a two-step row table cut into ``world`` contiguous ranges of WHOLE ray groups with
+    near-equal row counts (by parent block, then by contiguous ray groups; a group is never split, as
+    in the reference's own batching, eval_kitti_render.py:1120-1130).  ``group_col``: column 12 of the rows (k-1 on
+    a group's first row, -1 on its continuation rows).  Cut r goes to the group start nearest r/world of the rows,
+    so no range is more than half a group (<= 14 rows on the reference's KITTI frames) off its share."""
+    col = np.asarray(group_col).reshape(-1)
+    end = col.shape[0] if end is None else int(end)
+    if world < 1 or not 0 <= start <= end <= col.shape[0]:
+        raise ValueError("bad world / row range")
+    starts = start + np.flatnonzero(col[start:end] >= -0.5)
+    bounds = [start]
+    for r in range(1, world):
+        target = start + r * (end - start) / world
+        j = int(np.searchsorted(starts, target))
+        cand = [c for c in (starts[j - 1] if j > 0 else start, starts[j] if j < starts.shape[0] else end)]
+        pick = int(min(cand, key=lambda c: abs(c - target)))
+        bounds.append(max(pick, bounds[-1]))
+    bounds.append(end)
+    return [(bounds[i], bounds[i + 1]) for i in range(world)]
 
 
 def gather_rows(local: torch.Tensor, dst: int = 0, group=None) -> torch.Tensor | None:

@@ -141,7 +141,114 @@ def test_bench_launcher_spawns_ranks():
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout          # rank 0 only
-    assert lines[0]["n_gpus"] == 2 and lines[0]["dry_run"] and lines[0]["rank0_blocks"] == [0, 1, 2, 3]
+    # config 5: every rank renders a row-balanced share of each of the 8 blocks
+    assert lines[0]["n_gpus"] == 2 and lines[0]["dry_run"] and lines[0]["rank0_blocks"] == list(range(8))
     bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--dry-run"],
                          capture_output=True, text=True, env={**env, "WORLD_SIZE": "2"}, timeout=120)
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
+
+
+def _col12(sizes):
+    """Column 12 of two-step rows with these ray-group sizes (k-1 on a group's first row, -1 on the others)."""
+    import numpy as np
+    col = np.full(int(np.sum(sizes)), -1.0, dtype=np.float32)
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    col[starts] = np.asarray(sizes, dtype=np.float32) - 1
+    return col
+
+
+def test_split_groups_reference_group_sizes():
+    """The row-balanced split of the eval driver on the reference's own two-step rows
+    (tests/golden/view_group_sizes.npz: KITTI frames 1153 / 1178, groups of 1-28 rows): whole groups only, every
+    row once, and the largest share within 2 % of the mean at 2, 4 and 8 ranks."""
+    import numpy as np
+    from conftest import golden
+    from nof.blocks import split_groups
+    g = golden("view_group_sizes")
+    for key in ("f1153", "f1178"):
+        col = _col12(g[key].astype(np.int64))
+        n = col.shape[0]
+        for world in (1, 2, 4, 8):
+            parts = split_groups(col, world)
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+            assert all(col[s] >= -0.5 for s, e in parts if s < n)            # each share starts a group
+            sizes = [e - s for s, e in parts]
+            assert max(sizes) / (n / world) <= 1.02, (key, world, sizes)
+        # a sub-range (the rows the reference's batching renders) splits the same way
+        parts = split_groups(col, 8, 0, n - 1 if col[n - 1] >= -0.5 else n)
+        assert sum(e - s for s, e in parts) in (n - 1, n)
+
+
+def test_group_batches_whole_groups():
+    import numpy as np
+    import eval_kitti_render as E
+    rng = np.random.default_rng(3)
+    col = _col12(rng.integers(1, 12, size=500))
+    for s0, e0 in ((0, col.shape[0]), (37 if col[37] >= -0.5 else 0, col.shape[0])):
+        for bs in (1, 16, 1000):
+            sl = E.group_batches(col, s0, e0, bs)
+            assert sl[0][0] == s0 and sl[-1][1] == e0
+            assert all(a[1] == b[0] for a, b in zip(sl, sl[1:]))
+            assert all(e == e0 or col[e] >= -0.5 for _, e in sl)
+
+
+def _fake_view_render(mc, mf, emb, rows, other, **kw):
+    """Per-row stand-in for render_rays_view_0525_2_2 (CPU): what render_frame's slicing must preserve."""
+    flag = (rows[:, 0] * 7 + rows[:, 1]).floor().remainder(3) != 0
+    return {"rays_effective_flag_fine": flag.reshape(-1, 1), "points_inference_fine": rows[:, :3] * 2 + rows[:, 12:13]}
+
+
+def _eval_worker(rank, world, port, q, rows, other, batch_rows):
+    import argparse
+    import eval_kitti_render as E
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        E.render_rays_view_0525_2_2 = _fake_view_render
+        h = argparse.Namespace(N_samples=8, N_importance=16, use_disp=False, perturb=0, noise_std=0, chunk=1024,
+                               depth_inference_method=2)
+        pts, n = E.render_frame((None, None, None), rows, other, h, batch_rows, rank, world)
+        q.put((rank, None if pts is None else pts.numpy(), n))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("tail", ["group", "lone_row"])
+def test_eval_render_frame_world2_matches_one_process(tail):
+    """render_frame over 2 gloo ranks (whole-group shares, points gathered to rank 0 in rank order) returns exactly
+    the single-process cloud and row count -- including the reference's dropped lone last row."""
+    import numpy as np
+    import eval_kitti_render as E
+    rng = np.random.default_rng(11)
+    sizes = list(rng.integers(1, 9, size=700)) + ([1] if tail == "lone_row" else [3])
+    col = _col12(sizes)
+    rows = torch.zeros((col.shape[0], 13))
+    rows[:, :3] = torch.from_numpy(rng.normal(size=(col.shape[0], 3)).astype(np.float32)) * 10
+    rows[:, 12] = torch.from_numpy(col)
+    other = torch.zeros(col.shape[0], dtype=torch.int64)
+    bs = 512 if tail == "group" else 16
+    E.render_rays_view_0525_2_2, keep = _fake_view_render, E.render_rays_view_0525_2_2
+    try:
+        want, n1 = E.render_frame((None, None, None), rows, other,
+                                  __import__("argparse").Namespace(N_samples=8, N_importance=16, use_disp=False,
+                                                                   perturb=0, noise_std=0, chunk=1024,
+                                                                   depth_inference_method=2), bs)
+    finally:
+        E.render_rays_view_0525_2_2 = keep
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_eval_worker, args=(r, 2, port, q, rows, other, bs)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, pts, n = q.get(timeout=90)
+        res[r] = (pts, n)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    assert res[1][0] is None and res[0][1] == res[1][1] == n1
+    np.testing.assert_array_equal(res[0][0], want.numpy())
