@@ -16,15 +16,15 @@
 //                  a shift against cancellation), fp16 hi/mid parts on the matrix pipe per 64-sample tile (three
 //                  exact products, fp32 accumulation), float64 across tiles
 //   k_tf_stats     ebar, Sigma per chunk (float64)
-//   k_tf_layer<L>  P'_L, Q_L = P'_L Sigma, var, s, the pre-BN mean (float64 GEMMs on v_mfma_f64_16x16x4_f64,
-//                  64-row tiles x chunks)
+//   k_tf_layer16<L> P'_L, Q_L = P'_L Sigma, var, s, the pre-BN mean (float64 GEMMs on v_mfma_f64_16x16x4_f64,
+//                  16-row tiles x chunks)
 //   k_tf_out       (a_c, c_c);  launch_fold_logits: p = sigmoid(a_c . e + c_c) per sample
 //   k_tf_running   running_mean / running_var, chunk by chunk in order (bn_coeffs' arithmetic)
 // Backward (dL/dlogit per sample):
 //   k_tf_gmoments  per chunk: abar = sum_s g_s (e_s - ebar), gbar = sum_s g_s
 //   k_tf_bwd_out   occ_out / beta_7 gradients, adjoint of P_7 -> through BatchNorm 7 to the adjoint A'_7 of P'_7
 //   per layer L = 7..0: k_tf_dw<L> (dW_L = sum_c A'_L P_{L-1}^T, chunk-group partials), k_tf_dw_reduce<L>,
-//                  k_tf_bwd_layer<L> (A_{L-1} = W_L^T A'_L, then BatchNorm L-1's backward:
+//                  k_tf_bwd_layer16<L> (A_{L-1} = W_L^T A'_L, then BatchNorm L-1's backward:
 //                  ds = A.p', dgamma += ds / sqrt(var+eps), dvar = -ds gamma / (2 (var+eps)^1.5),
 //                  A'_{L-1} = s A + 2 dvar Q_{L-1})
 //   k_tf_vec_reduce gamma / out gradients summed over chunks.
@@ -38,7 +38,8 @@
 
 namespace pcn {
 
-constexpr int TF_WPC_MAX = 16;   // moment workgroups per chunk
+constexpr int TF_WPC_MIN = 16;   // moment workgroups per chunk: at least this many (when the chunk has the tiles),
+constexpr int TF_WPC_MAX = 256;  //   enough for ~512 workgroups over all chunks when there are few, at most this
 constexpr int TF_G_MAX = 16;     // chunk groups of the weight-gradient partials
 
 struct FoldDev {   // device views of the fold state (float64 throughout)
@@ -76,7 +77,10 @@ static FoldLayout fold_layout(int64_t total, int64_t chunk, bool fwd_only = fals
   FoldLayout F{};
   F.C = (total + chunk - 1) / chunk;
   const int64_t tiles = (std::min(chunk, total) + 63) / 64;
-  F.wpc = (int)std::max<int64_t>(1, std::min<int64_t>(TF_WPC_MAX, tiles / 64));
+  // a few large chunks (the reference's shell setting: 1 coarse and 3 fine chunks) would leave most CUs idle at
+  // 16 workgroups per chunk: ~512 workgroups in all, each at least 4 tiles of 64 samples (one per wave)
+  const int64_t want = std::max<int64_t>(TF_WPC_MIN, (512 + F.C - 1) / F.C);
+  F.wpc = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(want, TF_WPC_MAX), tiles / 4));
   F.G = (int)std::min<int64_t>(F.C, TF_G_MAX);
   const size_t C = (size_t)F.C, wpc = (size_t)F.wpc, G = (size_t)F.G;
   const size_t b = fwd_only ? 0 : 1;
@@ -275,13 +279,19 @@ __global__ __launch_bounds__(256) void k_tf_moments(SampleSrc q, FoldDev F) {
   for (int k = tid; k < 4096; k += 256) out[k] = red[k];
 }
 
-// grid (16, C), 256 threads (wpc > 1): the moment partials of a chunk summed in a fixed order into partial 0.
+// grid (64, C), 256 threads (wpc > 1): the moment partials of a chunk summed in a fixed order into partial 0 --
+// thread group g (4 of 64 threads) adds partials g, g + 4, ... of entry 64 blockIdx.x + lane, then the four group
+// sums are added in order (the partials come from every XCD: 4 independent chains of loads in flight per entry)
 __global__ __launch_bounds__(256) void k_tf_msum(FoldDev F) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+  __shared__ double red[4][64];
+  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63, k = blockIdx.x * 64 + lane;
   double* m = F.mom + (int64_t)blockIdx.y * F.wpc * 4096 + k;
-  double s = m[0];
-  for (int w = 1; w < F.wpc; ++w) s += m[(int64_t)w * 4096];
-  m[0] = s;
+  double s = 0.0;
+#pragma unroll 8
+  for (int w = g; w < F.wpc; w += 4) s += m[(int64_t)w * 4096];
+  red[g][lane] = s;
+  __syncthreads();
+  if (g == 0) m[0] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 // grid C, 256 threads: n = sum d_63^2, dbar = sum d / n, Sigma = sum d d^T / n - dbar dbar^T, ebar = e0 + dbar.
@@ -334,49 +344,56 @@ __device__ __forceinline__ void mfma64_quad(const double* As, const double* Bs, 
 __device__ __forceinline__ int q_row(int R, int x, int r, int lane) { return R + 16 * x + (lane >> 4) + 4 * r; }
 __device__ __forceinline__ int q_col(int Cc, int y, int lane) { return Cc + 16 * y + (lane & 15); }
 
-// sum over the tile's 64 columns of v[x][y][r] for each of the wave's rows (16 lanes x 2 blocks x 2 waves):
-// red[2][64] in LDS receives the two column halves (the caller syncs and adds them).
-__device__ __forceinline__ void row_sum_to_lds(double (&v)[2][4], int R, int wave, int lane, double* red) {
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      double t = v[x][r];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
-      if ((lane & 15) == 0) red[(wave & 1) * 64 + q_row(R, x, r, lane)] = t;
-    }
+// ---- 16-row tiles (the layer algebra's kernels): wave w owns the tile's columns 16 w .. 16 w + 15, one 16 x 16
+// block on v_mfma_f64_16x16x4_f64: acc += A B over k in [0, 64) with A(r, k) = ATR ? As[k TP + r] : As[r TP + k]
+// (r < 16), B(k, col) = Bs[k TP + col].  Four times the workgroups of the 64-row form and a quarter of its MFMA
+// chain per wave: the reference's shell setting has 1-3 chunks, so the chain's latency was the cost.
+template <bool ATR>
+__device__ __forceinline__ void mfma16_rows(const double* As, const double* Bs, int wave, int lane, f64x4& acc) {
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < 64; k0 += 4) {
+    const int k = k0 + lk;
+    const double a = ATR ? As[k * TP + li] : As[li * TP + k];
+    const double b = Bs[k * TP + 16 * wave + li];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
 }
 
-// grid (4, C), 256 threads: rows R0..R0+63 of P'_L = W_L B for chunk c, where B's rows are [unit_k | ebar_k] for
-// the encoding inputs and [s_{L-1,k} P'_{L-1}[k] | beta_{L-1,k}] for the previous layer's features (64-deep k
-// slices staged in LDS); then Q = P' Sigma (P' and Sigma staged), var_i = Q_i . p'_i, s = gamma / sqrt(var + eps),
-// mean(h_L) = P'[:, 63] + b_L.
+// sum over the wave's 16 columns of v[r] (row (lane >> 4) + 4 r of the tile) into red[wave][row]
+__device__ __forceinline__ void row_sum16(const double (&v)[4], int wave, int lane, double (*red)[16]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double t = v[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+    if ((lane & 15) == 0) red[wave][(lane >> 4) + 4 * r] = t;
+  }
+}
+
+// k_tf_layer in 16-row tiles, grid (16, C): rows R0..R0+15 of P'_L, Q_L = P'_L Sigma, var, s, the pre-BN mean.
 template <int L>
-__global__ __launch_bounds__(256) void k_tf_layer(NofParamsDev P, FoldDev F, double eps) {
+__global__ __launch_bounds__(256) void k_tf_layer16(NofParamsDev P, FoldDev F, double eps) {
   constexpr int IN = L == 0 ? 63 : L == 4 ? 319 : 256;
   constexpr int KE = (L == 0 || L == 4) ? 63 : 0;
-  __shared__ double As[64 * TP];
+  __shared__ double As[16 * TP];
   __shared__ double Bs[64 * TP];
-  __shared__ double red[128];
+  __shared__ double red[4][16];
   const int64_t C = F.C;
-  const int c = blockIdx.y, R0 = blockIdx.x * 64, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int R = 32 * (wave >> 1), Cc = 32 * (wave & 1);
+  const int c = blockIdx.y, R0 = blockIdx.x * 16, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const float* __restrict__ W = P.lin_w[L];
   const double* eb = F.eb + (int64_t)c * 64;
   const double* pprev = F.pp + ((int64_t)(L > 0 ? L - 1 : 0) * C + c) * 256 * 64;
   const double* sprev = F.sr + ((int64_t)(L > 0 ? L - 1 : 0) * C + c) * 1024;
   const float* bprev = P.bn_b[L > 0 ? L - 1 : 0];
-  f64x4 acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+  f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
   for (int k0 = 0; k0 < IN; k0 += 64) {
-    for (int e = tid; e < 4096; e += 256) {
+    for (int e = tid; e < 1024; e += 256) {
       const int r = e >> 6, kk = e & 63, k = k0 + kk;
       As[r * TP + kk] = k < IN ? (double)W[(int64_t)(R0 + r) * IN + k] : 0.0;
-      const int col = kk, kr = k0 + r;   // B row kr, column col
+    }
+    for (int e = tid; e < 4096; e += 256) {
+      const int col = e & 63, kr = k0 + (e >> 6);   // B row kr, column col
       double v = 0.0;
       if (kr < KE) {
         v = col < 63 ? (kr == col ? 1.0 : 0.0) : eb[kr];
@@ -384,52 +401,39 @@ __global__ __launch_bounds__(256) void k_tf_layer(NofParamsDev P, FoldDev F, dou
         const int kh = kr - KE;
         v = col < 63 ? sprev[kh] * pprev[kh * 64 + col] : (double)bprev[kh];
       }
-      Bs[r * TP + col] = v;
+      Bs[(e >> 6) * TP + col] = v;
     }
     __syncthreads();
-    mfma64_quad<false, false>(As, Bs, R, Cc, lane, acc);
+    mfma16_rows<false>(As, Bs, wave, lane, acc);
     __syncthreads();
   }
+  const int col = 16 * wave + (lane & 15);
   const int64_t base = (((int64_t)L * C + c) * 256 + R0) * 64;
   double* pp = F.pp + base;
   double* qo = F.q + base;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = q_row(R, x, r, lane), col = q_col(Cc, y, lane);
-        pp[row * 64 + col] = acc[x][y][r];
-        As[row * TP + col] = acc[x][y][r];
-      }
+  for (int r = 0; r < 4; ++r) {
+    const int row = (lane >> 4) + 4 * r;
+    pp[row * 64 + col] = acc[r];
+    As[row * TP + col] = acc[r];
+  }
   const double* sg = F.sig + (int64_t)c * 4096;
   for (int e = tid; e < 4096; e += 256) Bs[(e >> 6) * TP + (e & 63)] = sg[e];
   __syncthreads();
-  f64x4 qa[2][2];
+  f64x4 qa = f64x4{0.0, 0.0, 0.0, 0.0};
+  mfma16_rows<false>(As, Bs, wave, lane, qa);
+  double v[4];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) qa[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
-  mfma64_quad<false, false>(As, Bs, R, Cc, lane, qa);
-  double v[2][4];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v[x][r] = 0.0;
-#pragma unroll
-      for (int y = 0; y < 2; ++y) {
-        const int row = q_row(R, x, r, lane), col = q_col(Cc, y, lane);
-        qo[row * 64 + col] = qa[x][y][r];
-        v[x][r] += qa[x][y][r] * acc[x][y][r];   // column 63: Sigma's row 63 is zero, so Q[:, 63] = 0
-      }
-    }
-  row_sum_to_lds(v, R, wave, lane, red);
+  for (int r = 0; r < 4; ++r) {
+    const int row = (lane >> 4) + 4 * r;
+    qo[row * 64 + col] = qa[r];
+    v[r] = qa[r] * acc[r];   // column 63: Sigma's row 63 is zero, so Q[:, 63] = 0
+  }
+  row_sum16(v, wave, lane, red);
   __syncthreads();
-  if (tid < 64) {
+  if (tid < 16) {
     const int row = R0 + tid;
-    double var = red[tid] + red[64 + tid];
+    double var = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
     if (var < 0.0) var = 0.0;
     const double rinv = 1.0 / sqrt(var + eps);
     double* sr = F.sr + ((int64_t)L * C + c) * 1024;
@@ -610,11 +614,17 @@ __global__ __launch_bounds__(256) void k_tf_bwd_out(NofParamsDev P, FoldDev F) {
   __shared__ double ab[64];
   __shared__ double dot[64], coef[64], dvv[64];
   __shared__ double gbar_s;
+  __shared__ double gred[4][64];
   const int c = blockIdx.y, I0 = blockIdx.x * 64, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t C = F.C;
-  if (wave == 0) {
+  {   // the gradient-moment partials: wave v adds partials v, v + 4, ..., then the four sums in order
     double G = 0.0;
-    for (int w = 0; w < F.wpc; ++w) G += F.gm[((int64_t)c * F.wpc + w) * 64 + lane];
+    for (int w = wave; w < F.wpc; w += 4) G += F.gm[((int64_t)c * F.wpc + w) * 64 + lane];
+    gred[wave][lane] = G;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const double G = (gred[0][lane] + gred[1][lane]) + (gred[2][lane] + gred[3][lane]);
     const double gb = __shfl(G, 63, 64);
     ab[lane] = lane < 63 ? G - gb * (F.eb[(int64_t)c * 64 + lane] - F.e0[(int64_t)c * 64 + lane]) : 0.0;
     if (lane == 0) gbar_s = gb;
@@ -651,73 +661,61 @@ __global__ __launch_bounds__(256) void k_tf_bwd_out(NofParamsDev P, FoldDev F) {
     out[(I0 + r) * 64 + lane] = lane < 63 ? coef[r] * ab[lane] + 2.0 * dvv[r] * q7[(I0 + r) * 64 + lane] : 0.0;
 }
 
-// grid (4, C), 256 threads: A_{L-1}[k][j] = sum_i W_L[i][OFF + k] A'_L[i][j] for rows k0..k0+63 (W staged as
-// [i][k], read transposed), then BatchNorm L-1's backward to A'_{L-1} (ab[(L-1)&1]) and dgamma_{L-1} per chunk.
+// k_tf_bwd_layer in 16-row tiles, grid (16, C): rows k0..k0+15 of A_{L-1} = W_L^T A'_L, BatchNorm L-1's backward
+// to A'_{L-1} and dgamma_{L-1} per chunk.
 template <int L>
-__global__ __launch_bounds__(256) void k_tf_bwd_layer(NofParamsDev P, FoldDev F) {
+__global__ __launch_bounds__(256) void k_tf_bwd_layer16(NofParamsDev P, FoldDev F) {
   constexpr int IN = L == 4 ? 319 : 256, OFF = L == 4 ? 63 : 0;
   constexpr int LP = L - 1;
-  __shared__ double As[64 * TP];
+  __shared__ double As[64 * TP];   // W_L[i][OFF + K0 + kk], kk < 16 (read transposed)
   __shared__ double Bs[64 * TP];
-  __shared__ double red[128];
+  __shared__ double red[4][16];
+  __shared__ double dsv[16];
   const int64_t C = F.C;
-  const int c = blockIdx.y, K0 = blockIdx.x * 64, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int R = 32 * (wave >> 1), Cc = 32 * (wave & 1);
+  const int c = blockIdx.y, K0 = blockIdx.x * 16, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const float* __restrict__ W = P.lin_w[L];
   const double* abin = F.ab + ((int64_t)(L & 1) * C + c) * 256 * 64;
-  f64x4 acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+  f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
   for (int i0 = 0; i0 < 256; i0 += 64) {
+    for (int e = tid; e < 1024; e += 256) {
+      const int ii = e >> 4, kk = e & 15;
+      As[ii * TP + kk] = (double)W[(int64_t)(i0 + ii) * IN + OFF + K0 + kk];
+    }
     for (int e = tid; e < 4096; e += 256) {
       const int ii = e >> 6, kk = e & 63;
-      As[ii * TP + kk] = (double)W[(int64_t)(i0 + ii) * IN + OFF + K0 + kk];
       Bs[ii * TP + kk] = abin[(i0 + ii) * 64 + kk];
     }
     __syncthreads();
-    mfma64_quad<true, false>(As, Bs, R, Cc, lane, acc);
+    mfma16_rows<true>(As, Bs, wave, lane, acc);
     __syncthreads();
   }
   const double* ppp = F.pp + ((int64_t)LP * C + c) * 256 * 64;
   const double* qq = F.q + ((int64_t)LP * C + c) * 256 * 64;
   const double* srp = F.sr + ((int64_t)LP * C + c) * 1024;
-  double v[2][4];
+  const int col = 16 * wave + (lane & 15);
+  double v[4];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v[x][r] = 0.0;
-#pragma unroll
-      for (int y = 0; y < 2; ++y) {
-        const int k = K0 + q_row(R, x, r, lane), col = q_col(Cc, y, lane);
-        if (col < 63) v[x][r] += acc[x][y][r] * ppp[k * 64 + col];
-      }
-    }
-  row_sum_to_lds(v, R, wave, lane, red);
+  for (int r = 0; r < 4; ++r) {
+    const int k = K0 + (lane >> 4) + 4 * r;
+    v[r] = col < 63 ? acc[r] * ppp[k * 64 + col] : 0.0;
+  }
+  row_sum16(v, wave, lane, red);
   __syncthreads();
-  if (tid < 64) {
+  if (tid < 16) {
     const int k = K0 + tid;
-    const double ds = red[tid] + red[64 + tid];
+    const double ds = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
     F.dg[((int64_t)LP * C + c) * 256 + k] = ds * srp[256 + k];
-    red[tid] = ds;   // this thread's own slot: no other thread reads it before the barrier
+    dsv[tid] = ds;
   }
   __syncthreads();
   double* out = F.ab + ((int64_t)(LP & 1) * C + c) * 256 * 64;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int kl = q_row(R, x, r, lane), k = K0 + kl;
-      const double s = srp[k], rinv = srp[256 + k], gam = (double)P.bn_w[LP][k];
-      const double dv = -0.5 * red[kl] * gam * rinv * rinv * rinv;
-#pragma unroll
-      for (int y = 0; y < 2; ++y) {
-        const int col = q_col(Cc, y, lane);
-        out[k * 64 + col] = col < 63 ? s * acc[x][y][r] + 2.0 * dv * qq[k * 64 + col] : 0.0;
-      }
-    }
+  for (int r = 0; r < 4; ++r) {
+    const int kl = (lane >> 4) + 4 * r, k = K0 + kl;
+    const double sk = srp[k], rinv = srp[256 + k], gam = (double)P.bn_w[LP][k];
+    const double dv = -0.5 * dsv[kl] * gam * rinv * rinv * rinv;
+    out[k * 64 + col] = col < 63 ? sk * acc[r] + 2.0 * dv * qq[k * 64 + col] : 0.0;
+  }
 }
 
 // grid (16, G), 256 threads: partial g of dW_L's h columns, sum over the group's chunks of
@@ -805,7 +803,7 @@ __global__ void k_tf_vec_reduce(FoldDev F, pcnerf_nof_grads G) {
 // ------------------------------------------------------------------------------------------------- host
 template <int L>
 static void launch_layer(const NofParamsDev& P, const FoldDev& F, double eps, hipStream_t s) {
-  hipLaunchKernelGGL(k_tf_layer<L>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F, eps);
+  hipLaunchKernelGGL(k_tf_layer16<L>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F, eps);
 }
 
 static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, float momentum, float eps,
@@ -827,7 +825,7 @@ static void fold_forward(const SampleSrc& q, const pcnerf_nof_params* params, fl
   }
   {
     ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
-    if (F.wpc > 1) hipLaunchKernelGGL(k_tf_msum, dim3(16, (unsigned)F.C), dim3(256), 0, s, F);
+    if (F.wpc > 1) hipLaunchKernelGGL(k_tf_msum, dim3(64, (unsigned)F.C), dim3(256), 0, s, F);
     hipLaunchKernelGGL(k_tf_stats, dim3((unsigned)F.C), dim3(256), 0, s, F);
     launch_layer<0>(P, F, ep, s);
     launch_layer<1>(P, F, ep, s);
@@ -870,7 +868,7 @@ static void fused_forward(const SampleSrc& q, const pcnerf_nof_params* params, f
   }
   {
     ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
-    if (F.wpc > 1) hipLaunchKernelGGL(k_tf_msum, dim3(16, (unsigned)F.C), dim3(256), 0, s, F);
+    if (F.wpc > 1) hipLaunchKernelGGL(k_tf_msum, dim3(64, (unsigned)F.C), dim3(256), 0, s, F);
     hipLaunchKernelGGL(k_tf_stats, dim3((unsigned)F.C), dim3(256), 0, s, F);
     launch_layer<0>(P, F, ep, s);
     launch_layer<1>(P, F, ep, s);
@@ -900,7 +898,7 @@ template <int L>
 static void backward_layer(const NofParamsDev& P, const FoldDev& F, const pcnerf_nof_grads* G, hipStream_t s) {
   if constexpr (L > 0) hipLaunchKernelGGL(k_tf_dw<L>, dim3(16, F.G), dim3(256), 0, s, F);
   if (G->lin_w[L]) hipLaunchKernelGGL(k_tf_dw_reduce<L>, dim3(256), dim3(320), 0, s, F, G->lin_w[L]);
-  if constexpr (L > 0) hipLaunchKernelGGL(k_tf_bwd_layer<L>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  if constexpr (L > 0) hipLaunchKernelGGL(k_tf_bwd_layer16<L>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F);
 }
 
 static void fold_backward(const SampleSrc& q, const pcnerf_nof_params* params, float eps, const float* g,
@@ -948,13 +946,13 @@ FoldBnBwd fold_bn_backward(const float* rays, int stride, const float* z, int S,
   }
   ProfScope ps(s, PT_FOLD_ALGEBRA, 0.0, 0.0);
   hipLaunchKernelGGL(k_tf_bwd_out, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
-  hipLaunchKernelGGL(k_tf_bwd_layer<7>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
-  hipLaunchKernelGGL(k_tf_bwd_layer<6>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
-  hipLaunchKernelGGL(k_tf_bwd_layer<5>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
-  hipLaunchKernelGGL(k_tf_bwd_layer<4>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
-  hipLaunchKernelGGL(k_tf_bwd_layer<3>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
-  hipLaunchKernelGGL(k_tf_bwd_layer<2>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
-  hipLaunchKernelGGL(k_tf_bwd_layer<1>, dim3(4, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer16<7>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer16<6>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer16<5>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer16<4>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer16<3>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer16<2>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F);
+  hipLaunchKernelGGL(k_tf_bwd_layer16<1>, dim3(16, (unsigned)F.C), dim3(256), 0, s, P, F);
   return FoldBnBwd{F.dg, F.sr, F.oacc, F.C, F.pp, F.eb, F.q};
 }
 

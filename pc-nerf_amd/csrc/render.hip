@@ -541,86 +541,161 @@ __global__ __launch_bounds__(256) void k_sample_pdf(const float* __restrict__ bi
   }
 }
 
-// render.py:371-412 + :463-467.  One wave per ray; per-wave LDS: z (S) | w (S) | bins (S) | cdf (S) | sort (P2).
-__global__ __launch_bounds__(256) void k_resample(const float* __restrict__ Z, const float* __restrict__ Wt,
-                                                  int64_t n_rays, int S, int I, int P2,
-                                                  const float* __restrict__ U, float* __restrict__ ZF) {
-  extern __shared__ float lds[];
+// float64 block sum / exclusive scan over NT threads (NT / 64 waves; sh holds NT / 64 doubles).  The pdf sums
+// they serve are exact in float64 (see pdf_samples), so the grouping does not change a bit of the result.
+template <int NT>
+__device__ __forceinline__ double blk_sum_d(double v, double* sh) {
+  v = wave_sum_d(v);
+  if constexpr (NT == 64) {
+    return v;
+  } else {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) sh[wid] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int i = 0; i < NT / 64; ++i) t += sh[i];
+    __syncthreads();
+    return t;
+  }
+}
+template <int NT>
+__device__ __forceinline__ double blk_excl_d(double v, double* sh) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
-  const int64_t ray0 = (int64_t)blockIdx.x * nw + wid;
-  const bool active = ray0 < n_rays;
-  const int64_t ray = active ? ray0 : n_rays - 1;
-  float* zs = lds + (size_t)wid * (4 * S + P2);
-  float* ws = zs + S;
-  float* bins = ws + S;
-  float* cdf = bins + S;
-  float* sb = cdf + S;
-  for (int i = lane; i < S; i += 64) {
-    zs[i] = Z[ray * S + i];
-    ws[i] = Wt[ray * S + i];
+  const double ex = wave_excl_sum(v, lane);
+  if constexpr (NT == 64) {
+    return ex;
+  } else {
+    const double wt = __shfl(ex + v, 63, 64);
+    if (lane == 0) sh[wid] = wt;
+    __syncthreads();
+    double base = 0.0;
+    for (int i = 0; i < wid; ++i) base += sh[i];
+    __syncthreads();
+    return base + ex;
   }
-  __syncthreads();
-  const int nbin = S - 1;
-  for (int i = lane; i < nbin; i += 64) bins[i] = 0.5f * (zs[i + 1] + zs[i]);
-  pdf_samples(bins, ws + 1, nbin, cdf, I, U ? U + ray * I : nullptr, sb + S, lane);
-  for (int i = lane; i < S; i += 64) sb[i] = zs[i];
-  for (int i = S + I + lane; i < P2; i += 64) sb[i] = __builtin_nanf("");   // pads sort last, with any NaN
-  __syncthreads();
-  // sort(cat(z, z_samples)) (render.py:463-467): both lists are (almost always) non-decreasing already, so the
-  // merged position of a coarse value is its index plus the fine values strictly below it, of a fine value its
-  // index plus the coarse values <= it (binary searches in LDS).  Any unsorted list in the block sends the whole
-  // block through the bitonic sort below (its barriers need every wave); the sorted values are the same.
-  // (a NaN compares false, so a list holding one is "unsorted" and goes to the NaN-aware bitonic sort)
-  bool mono = true;
-  for (int i = lane; i < S; i += 64) mono = mono && (sb[i] == sb[i]) && (i + 1 >= S || sb[i] <= sb[i + 1]);
-  for (int i = lane; i < I; i += 64)
-    mono = mono && (sb[S + i] == sb[S + i]) && (i + 1 >= I || sb[S + i] <= sb[S + i + 1]);
-  if (!__syncthreads_or(mono ? 0 : 1)) {
-    if (active) {
-      float* out = ZF + ray * (S + I);
-      for (int i = lane; i < S; i += 64) {
-        const float v = sb[i];
-        int lo = 0, hi = I;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (sb[S + mid] < v) lo = mid + 1; else hi = mid;
-        }
-        out[i + lo] = v;
-      }
-      for (int i = lane; i < I; i += 64) {
-        const float v = sb[S + i];
-        int lo = 0, hi = S;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (sb[mid] <= v) lo = mid + 1; else hi = mid;
-        }
-        out[i + lo] = v;
-      }
-    }
-    return;
-  }
-  // bitonic sort of P2 values (ascending); every wave of the block runs the same trip counts
-  for (int k = 2; k <= P2; k <<= 1) {
+}
+
+// ascending bitonic sort of a[0..n) in LDS (n a power of two) by NT threads, comparator c of each stage on the
+// pair (i, i | j) with i = c with a zero bit inserted at j; NaN sorts after every number (torch.sort's order)
+template <int NT>
+__device__ void blk_bitonic(float* a, int n) {
+  for (int k = 2; k <= n; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = lane; i < P2; i += 64) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const float a = sb[i], b = sb[ixj];
-          const bool up = (i & k) == 0;
-          const bool gt = (a == a) ? (a > b) : (b == b);   // NaN greater than every number (torch.sort order)
-          if (gt == up) {
-            sb[i] = b;
-            sb[ixj] = a;
-          }
+      for (int c = threadIdx.x; c < (n >> 1); c += NT) {
+        const int i = ((c & ~(j - 1)) << 1) | (c & (j - 1)), ixj = i | j;
+        const float x = a[i], y = a[ixj];
+        const bool up = (i & k) == 0;
+        const bool gt = (x == x) ? (x > y) : (y == y);
+        if (gt == up) {
+          a[i] = y;
+          a[ixj] = x;
         }
       }
       __syncthreads();
     }
   }
-  if (active) {
-    const int F = S + I;
-    for (int i = lane; i < F; i += 64) ZF[ray * F + i] = sb[i];
+}
+
+// render.py:371-412 + :463-467, one ray per workgroup of NT threads.  LDS: z (S) | w (S) | bins (S) | cdf (S) |
+// fine (PF = pow2 >= I) | full sort (P2 = pow2 >= S + I).  sample_pdf's draws are unsorted whenever the uniforms
+// are (perturb: torch.rand), so the fine list is bitonic-sorted on its own and merged with the coarse z (sorted by
+// construction, render.py:433-442) by binary search: a coarse value lands at its index plus the fine values
+// strictly below it, a fine value at its index plus the coarse values <= it.  A coarse list out of order or a NaN
+// anywhere sends the ray through the bitonic sort of the whole concatenation instead; the sorted values are the
+// same either way.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_resample(const float* __restrict__ Z, const float* __restrict__ Wt, int S,
+                                                 int I, int PF, int P2, const float* __restrict__ U,
+                                                 float* __restrict__ ZF) {
+  extern __shared__ float lds[];
+  __shared__ double sh[NT / 64];
+  const int tid = threadIdx.x;
+  const int64_t ray = blockIdx.x;
+  float* zs = lds;
+  float* ws = zs + S;
+  float* bins = ws + S;
+  float* cdf = bins + S;
+  float* fs = cdf + S;
+  float* sb = fs + PF;
+  for (int i = tid; i < S; i += NT) {
+    zs[i] = Z[ray * S + i];
+    ws[i] = Wt[ray * S + i];
+  }
+  __syncthreads();
+  const int nb = S - 1, npdf = nb - 1;   // bins = mid-points, weights w[1:-1] (render.py:456-458)
+  for (int i = tid; i < nb; i += NT) bins[i] = 0.5f * (zs[i + 1] + zs[i]);
+  const float* w = ws + 1;
+  const int B = (npdf + NT - 1) / NT, i0 = tid * B;
+  double ls = 0.0;
+  for (int j = 0; j < B; ++j) {
+    const int i = i0 + j;
+    if (i < npdf) ls += (double)(w[i] + 1e-5f);
+  }
+  const float tot = (float)blk_sum_d<NT>(ls, sh);
+  double lp = 0.0;
+  for (int j = 0; j < B; ++j) {
+    const int i = i0 + j;
+    if (i < npdf) lp += (double)((w[i] + 1e-5f) / tot);
+  }
+  double run = blk_excl_d<NT>(lp, sh);
+  if (tid == 0) cdf[0] = 0.0f;
+  for (int j = 0; j < B; ++j) {
+    const int i = i0 + j;
+    if (i < npdf) {
+      run += (double)((w[i] + 1e-5f) / tot);
+      cdf[i + 1] = (float)run;
+    }
+  }
+  __syncthreads();
+  const float* u_row = U ? U + ray * I : nullptr;
+  for (int k = tid; k < I; k += NT) {
+    const float u = u_row ? u_row[k] : linspace01(k, I);
+    int lo = 0, hi = nb;   // first index with cdf > u  (searchsorted right=True)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
+    }
+    const int below = max(lo - 1, 0), above = min(lo, nb - 1);
+    const float c0 = cdf[below], c1 = cdf[above];
+    float denom = c1 - c0;
+    if (denom < 1e-5f) denom = 1.0f;
+    const float t = (u - c0) / denom;
+    const float b0 = bins[below], b1 = bins[above];
+    fs[k] = b0 + t * (b1 - b0);
+  }
+  for (int k = I + tid; k < PF; k += NT) fs[k] = __builtin_nanf("");
+  bool ok = true;
+  for (int i = tid; i < S; i += NT) ok = ok && (zs[i] == zs[i]) && (i + 1 >= S || zs[i] <= zs[i + 1]);
+  __syncthreads();
+  for (int i = tid; i < I; i += NT) ok = ok && (fs[i] == fs[i]);
+  float* out = ZF + ray * (S + I);
+  if (__syncthreads_or(ok ? 0 : 1)) {
+    for (int i = tid; i < S; i += NT) sb[i] = zs[i];
+    for (int i = tid; i < I; i += NT) sb[S + i] = fs[i];
+    for (int i = S + I + tid; i < P2; i += NT) sb[i] = __builtin_nanf("");
+    __syncthreads();
+    blk_bitonic<NT>(sb, P2);
+    for (int i = tid; i < S + I; i += NT) out[i] = sb[i];
+    return;
+  }
+  blk_bitonic<NT>(fs, PF);
+  for (int i = tid; i < S; i += NT) {
+    const float v = zs[i];
+    int lo = 0, hi = I;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (fs[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    out[i + lo] = v;
+  }
+  for (int i = tid; i < I; i += NT) {
+    const float v = fs[i];
+    int lo = 0, hi = S;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (zs[mid] <= v) lo = mid + 1; else hi = mid;
+    }
+    out[i + lo] = v;
   }
 }
 
@@ -1063,22 +1138,30 @@ extern "C" int pcnerf_resample(const float* z, const float* weights, int64_t n_r
   PCN_API_BEGIN
   PCN_CHECK(z && weights && z_fine, "pcnerf_resample: null argument");
   PCN_CHECK(n_rays > 0 && n_samples >= 3 && n_importance > 0, "pcnerf_resample: need n_samples >= 3");
+  PCN_CHECK(n_rays <= 0x7fffffff, "pcnerf_resample: more than 2^31 - 1 rays in one call");
   const int F = n_samples + n_importance;
-  int P2 = 1;
+  int P2 = 1, PF = 1;
   while (P2 < F) P2 <<= 1;
-  const size_t per_wave = (size_t)(4 * n_samples + P2) * sizeof(float);
-  const size_t lds_max = 160 * 1024;
-  PCN_CHECK(per_wave <= lds_max, "pcnerf_resample: n_samples + n_importance too large for one wave's LDS");
-  int nw = (int)(lds_max / per_wave);
-  if (nw > 4) nw = 4;
-  if (nw > 1 && per_wave * nw > 64 * 1024) nw = (int)((64 * 1024) / per_wave) > 0 ? (int)((64 * 1024) / per_wave) : 1;
-  if (per_wave * nw > 64 * 1024)
-    PCN_HIP(hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(per_wave * nw)));
+  while (PF < n_importance) PF <<= 1;
+  const size_t lds = (size_t)(4 * n_samples + PF + P2) * sizeof(float);
+  PCN_CHECK(lds <= 160 * 1024, "pcnerf_resample: n_samples + n_importance too large for one workgroup's LDS");
+  // about four comparators per thread in each bitonic stage of the fine sort
+  const int nt = PF >= 2048 ? 512 : PF >= 1024 ? 256 : PF >= 512 ? 128 : 64;
   ProfScope ps((hipStream_t)stream, PT_RESAMPLE, 0.0,
                (double)n_rays * (8.0 * n_samples + 4.0 * F + (u ? 4.0 * n_importance : 0.0)));
-  hipLaunchKernelGGL(k_resample, dim3(nblk(n_rays, nw)), dim3(64 * nw), per_wave * nw, (hipStream_t)stream, z,
-                     weights, n_rays, n_samples, n_importance, P2, u, z_fine);
+#define PCN_RS(NT)                                                                                                \
+  do {                                                                                                            \
+    if (lds > 64 * 1024)                                                                                          \
+      PCN_HIP(hipFuncSetAttribute((const void*)k_resample<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                                  (int)lds));                                                                     \
+    hipLaunchKernelGGL(k_resample<NT>, dim3((unsigned)n_rays), dim3(NT), lds, (hipStream_t)stream, z, weights,   \
+                       n_samples, n_importance, PF, P2, u, z_fine);                                               \
+  } while (0)
+  if (nt == 512) PCN_RS(512);
+  else if (nt == 256) PCN_RS(256);
+  else if (nt == 128) PCN_RS(128);
+  else PCN_RS(64);
+#undef PCN_RS
   PCN_LAUNCH_CHECK("pcnerf_resample");
   PCN_API_END
 }

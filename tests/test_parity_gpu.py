@@ -379,16 +379,21 @@ def test_segmented_coarse_z_bitexact(ratio):
             assert torch.equal(got, want), (S, ratio)
 
 
-def test_resample_merge_exact():
+@pytest.mark.parametrize("R,S,I,sorted_u", [(256, 128, 256, True), (256, 128, 256, False), (64, 200, 500, False),
+                                             (32, 300, 1000, False), (16, 768, 1536, False)])
+def test_resample_merge_exact(R, S, I, sorted_u):
     """k_resample's sort(cat(z, z_samples)) (render.py:463-467): bit for bit the sort of the coarse z and the
-    fine samples the same pdf code draws (pcnerf_sample_pdf), for sorted coarse rows (binary-search merge) and with
-    every third row unsorted (the block falls back to the bitonic sort); and the fine samples against the oracle."""
+    fine samples the same pdf code draws (pcnerf_sample_pdf), for sorted coarse rows (fine sort + binary-search
+    merge) and with every third row unsorted (the ray falls back to the bitonic sort of the concatenation); sorted
+    (perturb=0) and unsorted (perturb: torch.rand) uniforms; workgroup sizes 64..512 (fine lists of 256..2048
+    slots, the reference shell's 768 / 1536 last); and the fine samples against the oracle."""
     from nof import _ops
     gen = torch.Generator().manual_seed(7)
-    R, S, I = 256, 128, 256
     z = torch.sort(torch.rand(R, S, generator=gen) * 30, -1)[0]
     w = torch.rand(R, S, generator=gen)
-    u = torch.sort(torch.rand(R, I, generator=gen), -1)[0]
+    u = torch.rand(R, I, generator=gen)
+    if sorted_u:
+        u = torch.sort(u, -1)[0]
     zr = z.clone()
     zr[::3, 40], zr[::3, 41] = z[::3, 41], z[::3, 40]
     for zz in (z, zr):
