@@ -47,6 +47,35 @@ __device__ __forceinline__ float wave_max_f(float v) {
   return v;
 }
 
+// max |alpha(n) W[n][k]| over one layer's out_f x in_f weights by the whole block of NT threads (eight independent
+// loads in flight per thread; fmaxf drops NaN weights, in any order)
+template <int NT, typename Alpha>
+__device__ __forceinline__ float block_layer_absmax(const float* __restrict__ w, int out_f, int in_f, Alpha alpha) {
+  const int total = out_f * in_f;
+  float m = 0.0f;
+  for (int i0 = threadIdx.x; i0 < total; i0 += NT * 8) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int i = i0 + NT * e;
+      v[e] = i < total ? w[i] : 0.0f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int i = i0 + NT * e;
+      if (i < total) m = fmaxf(m, fabsf(alpha(i / in_f) * v[e]));
+    }
+  }
+  m = wave_max_f(m);
+  __shared__ float red[NT / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float r = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+
 // torch sigmoid on CPU: 1 / (1 + exp(-x)).
 __device__ __forceinline__ float sigmoid_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
 

@@ -211,23 +211,12 @@ __global__ __launch_bounds__(256) void k_nof_eval(const float* __restrict__ rays
 // per-layer weight scale exponents of the BatchNorm-folded weights (RAW: of the raw weights, for the train-mode
 // query), stored in the image as int32
 template <bool RAW>
-__global__ __launch_bounds__(256) void k_eval_wscale(NofParamsDev P, float* __restrict__ out) {
+__global__ __launch_bounds__(1024) void k_eval_wscale(NofParamsDev P, float* __restrict__ out) {
   const int L = blockIdx.x;
-  const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
-  float m = 0.0f;
-  for (int i = threadIdx.x; i < 256 * in_f; i += 256) {
-    const int n = i / in_f;
-    const float alpha = RAW ? 1.0f : (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
-    m = fmaxf(m, fabsf(alpha * P.lin_w[L][i]));
-  }
-  m = wave_max_f(m);
-  __shared__ float red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    reinterpret_cast<int*>(out + OFF_EH_SW)[L] = m > 0.0f && m == m && m < 3.0e38f ? 14 - ilogbf(m) : 0;
-  }
+  const float m = block_layer_absmax<1024>(P.lin_w[L], 256, L == 0 ? 63 : L == 4 ? 319 : 256, [&](int n) {
+    return RAW ? 1.0f : (1.0f / sqrtf(P.bn_rv[L][n] + P.eps)) * P.bn_w[L][n];
+  });
+  if (threadIdx.x == 0) reinterpret_cast<int*>(out + OFF_EH_SW)[L] = m > 0.0f && m == m && m < 3.0e38f ? 14 - ilogbf(m) : 0;
 }
 
 typedef _Float16 eh_f16x8 __attribute__((ext_vector_type(8)));
@@ -933,7 +922,7 @@ size_t train_query_image_floats() { return EVAL_FLOATS; }
 
 void pack_train_query(const NofParamsDev& P, float* img, hipStream_t s) {
   hipLaunchKernelGGL(k_pack_eval_vectors<true>, dim3(1), dim3(256), 0, s, P, img);   // occ_out, raw biases
-  hipLaunchKernelGGL(k_eval_wscale<true>, dim3(8), dim3(256), 0, s, P, img);
+  hipLaunchKernelGGL(k_eval_wscale<true>, dim3(8), dim3(1024), 0, s, P, img);
   hipLaunchKernelGGL(k_pack_eval_h3<true>, dim3((unsigned)((EH_VECS + 255) / 256)),
                      dim3(256), 0, s, P, img);
 }
@@ -1038,7 +1027,7 @@ extern "C" int pcnerf_nof_pack_eval(const pcnerf_nof_params* params, float* pack
   const unsigned nb = (unsigned)((OFF_BIAS + 255) / 256);
   hipLaunchKernelGGL(k_pack_eval_weights, dim3(nb), dim3(256), 0, s, P, packed);
   hipLaunchKernelGGL(k_pack_eval_vectors<false>, dim3(1), dim3(256), 0, s, P, packed);
-  hipLaunchKernelGGL(k_eval_wscale<false>, dim3(8), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(k_eval_wscale<false>, dim3(8), dim3(1024), 0, s, P, packed);
   hipLaunchKernelGGL(k_pack_eval_h3<false>, dim3((unsigned)((EH_VECS + 255) / 256)),
                      dim3(256), 0, s, P, packed);
   PCN_LAUNCH_CHECK("pcnerf_nof_pack_eval");

@@ -54,7 +54,7 @@ struct FoldDev {   // device views of the fold state (float64 throughout)
   double* sr;      // [8][C][4][256] s, 1/sqrt(var+eps), mean(h_L), var(h_L)
   double* fold;    // [C][64] (a_c, c_c)
   double* gm;      // [C][wpc][64] backward moment partials
-  double* ab;      // [2][C][256][64] A'_L ping-pong
+  double* ab;      // [2][C][256][64] forward: P_L = s_L (.) P'_L | beta_L ping-pong; backward: A'_L ping-pong
   double* dg;      // [8][C][256] dgamma per chunk
   double* dw;      // [G][256][256] weight-gradient partials (h columns)
   double* vec;     // [C][576] d out_w (256), d beta_7 (256), d out_b (1)
@@ -71,8 +71,9 @@ struct FoldLayout {
   size_t doubles;
 };
 
-// fwd_only: the fused train query's state (pcnerf_nof_train_fused_bytes) -- the backward-only pieces (gm, ab, dg, dw,
-// vec: about 2.5 MB per chunk) and the fold's logits are empty, so its size does not grow with them
+// fwd_only: the fused train query's state (pcnerf_nof_train_fused_bytes) -- the backward-only pieces (gm, dg, dw, vec:
+// about 2.2 MB per chunk) and the fold's logits are empty, so its size does not grow with them; ab is kept (the
+// forward's P_L ping-pong, k_tf_layer16)
 static FoldLayout fold_layout(int64_t total, int64_t chunk, bool fwd_only = false) {
   FoldLayout F{};
   F.C = (total + chunk - 1) / chunk;
@@ -85,7 +86,7 @@ static FoldLayout fold_layout(int64_t total, int64_t chunk, bool fwd_only = fals
   const size_t C = (size_t)F.C, wpc = (size_t)F.wpc, G = (size_t)F.G;
   const size_t b = fwd_only ? 0 : 1;
   const size_t n[FOLD_PIECES] = {C * wpc * 4096, C * 4096, C * 64, C * 64, 8 * C * 256 * 64, 8 * C * 256 * 64,
-                                 8 * C * 1024, b * C * 64, b * C * wpc * 64, b * 2 * C * 256 * 64, b * 8 * C * 256,
+                                 8 * C * 1024, b * C * 64, b * C * wpc * 64, 2 * C * 256 * 64, b * 8 * C * 256,
                                  b * G * 256 * 256, b * C * 576, C * TQ_COEF_FLOATS / 2,
                                  (train_query_image_floats() + 1) / 2, b * C * 257};
   size_t o = 0;
@@ -371,7 +372,10 @@ __device__ __forceinline__ void row_sum16(const double (&v)[4], int wave, int la
   }
 }
 
-// k_tf_layer in 16-row tiles, grid (16, C): rows R0..R0+15 of P'_L, Q_L = P'_L Sigma, var, s, the pre-BN mean.
+// k_tf_layer in 16-row tiles, grid (16, C): rows R0..R0+15 of P'_L, Q_L = P'_L Sigma, var, s, the pre-BN mean, and
+// P_L = s_L (.) P'_L with beta_L in column 63 (F.ab[L & 1]: the next layer's B operand as a plain copy; the backward
+// reuses the buffer for its adjoints).  Thread t stages B rows k0 + (t >> 6) + 4 it, column t & 63, through
+// registers one K step ahead of the matrix products.
 template <int L>
 __global__ __launch_bounds__(256) void k_tf_layer16(NofParamsDev P, FoldDev F, double eps) {
   constexpr int IN = L == 0 ? 63 : L == 4 ? 319 : 256;
@@ -379,46 +383,60 @@ __global__ __launch_bounds__(256) void k_tf_layer16(NofParamsDev P, FoldDev F, d
   __shared__ double As[16 * TP];
   __shared__ double Bs[64 * TP];
   __shared__ double red[4][16];
+  __shared__ double sv[16];
   const int64_t C = F.C;
   const int c = blockIdx.y, R0 = blockIdx.x * 16, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int col = tid & 63, rr = tid >> 6;
   const float* __restrict__ W = P.lin_w[L];
   const double* eb = F.eb + (int64_t)c * 64;
-  const double* pprev = F.pp + ((int64_t)(L > 0 ? L - 1 : 0) * C + c) * 256 * 64;
-  const double* sprev = F.sr + ((int64_t)(L > 0 ? L - 1 : 0) * C + c) * 1024;
-  const float* bprev = P.bn_b[L > 0 ? L - 1 : 0];
+  const double* pbp = F.ab + ((int64_t)((L + 1) & 1) * C + c) * 256 * 64;   // P_{L-1} | beta_{L-1}
+  const double* sg = F.sig + (int64_t)c * 4096;
+  double bv[16];
+  float av[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int e = tid + 256 * it, k = k0 + (e & 63);
+      av[it] = k < IN ? W[(int64_t)(R0 + (e >> 6)) * IN + k] : 0.0f;
+    }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int kr = k0 + rr + 4 * it;
+      double x = 0.0;
+      if (kr < KE) x = col < 63 ? (kr == col ? 1.0 : 0.0) : eb[kr];
+      else if (kr < IN) x = pbp[(kr - KE) * 64 + col];
+      bv[it] = x;
+    }
+  };
+  load(0);
   f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
   for (int k0 = 0; k0 < IN; k0 += 64) {
-    for (int e = tid; e < 1024; e += 256) {
-      const int r = e >> 6, kk = e & 63, k = k0 + kk;
-      As[r * TP + kk] = k < IN ? (double)W[(int64_t)(R0 + r) * IN + k] : 0.0;
-    }
-    for (int e = tid; e < 4096; e += 256) {
-      const int col = e & 63, kr = k0 + (e >> 6);   // B row kr, column col
-      double v = 0.0;
-      if (kr < KE) {
-        v = col < 63 ? (kr == col ? 1.0 : 0.0) : eb[kr];
-      } else if (kr < IN) {
-        const int kh = kr - KE;
-        v = col < 63 ? sprev[kh] * pprev[kh * 64 + col] : (double)bprev[kh];
-      }
-      Bs[(e >> 6) * TP + col] = v;
-    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) As[(rr + 4 * it) * TP + col] = (double)av[it];
+#pragma unroll
+    for (int it = 0; it < 16; ++it) Bs[(rr + 4 * it) * TP + col] = bv[it];
     __syncthreads();
+    if (k0 + 64 < IN) {
+      load(k0 + 64);
+    } else {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) bv[it] = sg[(rr + 4 * it) * 64 + col];   // Sigma for Q_L
+    }
     mfma16_rows<false>(As, Bs, wave, lane, acc);
     __syncthreads();
   }
-  const int col = 16 * wave + (lane & 15);
+  const int ocol = 16 * wave + (lane & 15);
   const int64_t base = (((int64_t)L * C + c) * 256 + R0) * 64;
   double* pp = F.pp + base;
   double* qo = F.q + base;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = (lane >> 4) + 4 * r;
-    pp[row * 64 + col] = acc[r];
-    As[row * TP + col] = acc[r];
+    pp[row * 64 + ocol] = acc[r];
+    As[row * TP + ocol] = acc[r];
   }
-  const double* sg = F.sig + (int64_t)c * 4096;
-  for (int e = tid; e < 4096; e += 256) Bs[(e >> 6) * TP + (e & 63)] = sg[e];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) Bs[(rr + 4 * it) * TP + col] = bv[it];
   __syncthreads();
   f64x4 qa = f64x4{0.0, 0.0, 0.0, 0.0};
   mfma16_rows<false>(As, Bs, wave, lane, qa);
@@ -426,7 +444,7 @@ __global__ __launch_bounds__(256) void k_tf_layer16(NofParamsDev P, FoldDev F, d
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = (lane >> 4) + 4 * r;
-    qo[row * 64 + col] = qa[r];
+    qo[row * 64 + ocol] = qa[r];
     v[r] = qa[r] * acc[r];   // column 63: Sigma's row 63 is zero, so Q[:, 63] = 0
   }
   row_sum16(v, wave, lane, red);
@@ -436,11 +454,20 @@ __global__ __launch_bounds__(256) void k_tf_layer16(NofParamsDev P, FoldDev F, d
     double var = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
     if (var < 0.0) var = 0.0;
     const double rinv = 1.0 / sqrt(var + eps);
+    const double sc = (double)P.bn_w[L][row] * rinv;
     double* sr = F.sr + ((int64_t)L * C + c) * 1024;
-    sr[row] = (double)P.bn_w[L][row] * rinv;
+    sr[row] = sc;
     sr[256 + row] = rinv;
     sr[512 + row] = As[tid * TP + 63] + (double)P.lin_b[L][row];
     sr[768 + row] = var;
+    sv[tid] = sc;
+  }
+  __syncthreads();
+  double* pb = F.ab + ((int64_t)(L & 1) * C + c) * 256 * 64 + (int64_t)R0 * 64;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = (lane >> 4) + 4 * r;
+    pb[row * 64 + ocol] = ocol < 63 ? sv[row] * acc[r] : (double)P.bn_b[L][R0 + row];
   }
 }
 
@@ -662,7 +689,7 @@ __global__ __launch_bounds__(256) void k_tf_bwd_out(NofParamsDev P, FoldDev F) {
 }
 
 // k_tf_bwd_layer in 16-row tiles, grid (16, C): rows k0..k0+15 of A_{L-1} = W_L^T A'_L, BatchNorm L-1's backward
-// to A'_{L-1} and dgamma_{L-1} per chunk.
+// to A'_{L-1} and dgamma_{L-1} per chunk.  Staging through registers one K step ahead, as k_tf_layer16.
 template <int L>
 __global__ __launch_bounds__(256) void k_tf_bwd_layer16(NofParamsDev P, FoldDev F) {
   constexpr int IN = L == 4 ? 319 : 256, OFF = L == 4 ? 63 : 0;
@@ -673,32 +700,49 @@ __global__ __launch_bounds__(256) void k_tf_bwd_layer16(NofParamsDev P, FoldDev 
   __shared__ double dsv[16];
   const int64_t C = F.C;
   const int c = blockIdx.y, K0 = blockIdx.x * 16, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int col = tid & 63, rr = tid >> 6;
   const float* __restrict__ W = P.lin_w[L];
   const double* abin = F.ab + ((int64_t)(L & 1) * C + c) * 256 * 64;
-  f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
-  for (int i0 = 0; i0 < 256; i0 += 64) {
-    for (int e = tid; e < 1024; e += 256) {
-      const int ii = e >> 4, kk = e & 15;
-      As[ii * TP + kk] = (double)W[(int64_t)(i0 + ii) * IN + OFF + K0 + kk];
-    }
-    for (int e = tid; e < 4096; e += 256) {
-      const int ii = e >> 6, kk = e & 63;
-      Bs[ii * TP + kk] = abin[(i0 + ii) * 64 + kk];
-    }
-    __syncthreads();
-    mfma16_rows<true>(As, Bs, wave, lane, acc);
-    __syncthreads();
-  }
   const double* ppp = F.pp + ((int64_t)LP * C + c) * 256 * 64;
   const double* qq = F.q + ((int64_t)LP * C + c) * 256 * 64;
   const double* srp = F.sr + ((int64_t)LP * C + c) * 1024;
-  const int col = 16 * wave + (lane & 15);
-  double v[4];
+  const int ocol = 16 * wave + (lane & 15);
+  double pv[4], qv[4];   // the epilogue's operands, loaded while the products run
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int k = K0 + (lane >> 4) + 4 * r;
-    v[r] = col < 63 ? acc[r] * ppp[k * 64 + col] : 0.0;
+    pv[r] = ppp[k * 64 + ocol];
+    qv[r] = qq[k * 64 + ocol];
   }
+  double bv[16];
+  float av[4];
+  auto load = [&](int i0) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int e = tid + 256 * it;
+      av[it] = W[(int64_t)(i0 + (e >> 4)) * IN + OFF + K0 + (e & 15)];
+    }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) bv[it] = abin[(i0 + rr + 4 * it) * 64 + col];
+  };
+  load(0);
+  f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int i0 = 0; i0 < 256; i0 += 64) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int e = tid + 256 * it;
+      As[(e >> 4) * TP + (e & 15)] = (double)av[it];
+    }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) Bs[(rr + 4 * it) * TP + col] = bv[it];
+    __syncthreads();
+    if (i0 + 64 < 256) load(i0 + 64);
+    mfma16_rows<true>(As, Bs, wave, lane, acc);
+    __syncthreads();
+  }
+  double v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = ocol < 63 ? acc[r] * pv[r] : 0.0;
   row_sum16(v, wave, lane, red);
   __syncthreads();
   if (tid < 16) {
@@ -714,7 +758,7 @@ __global__ __launch_bounds__(256) void k_tf_bwd_layer16(NofParamsDev P, FoldDev 
     const int kl = (lane >> 4) + 4 * r, k = K0 + kl;
     const double sk = srp[k], rinv = srp[256 + k], gam = (double)P.bn_w[LP][k];
     const double dv = -0.5 * dsv[kl] * gam * rinv * rinv * rinv;
-    out[k * 64 + col] = col < 63 ? sk * acc[r] + 2.0 * dv * qq[k * 64 + col] : 0.0;
+    out[k * 64 + ocol] = ocol < 63 ? sk * acc[r] + 2.0 * dv * qv[r] : 0.0;
   }
 }
 

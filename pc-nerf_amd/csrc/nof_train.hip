@@ -433,21 +433,11 @@ __host__ __device__ constexpr size_t off_h(int layer, bool epart) {
 }
 constexpr size_t TRAIN_H_VECS = 2 * HW_E + 7 * HW_H;
 
-// per-layer weight scale exponents: sw[L] with max|W_L| 2^sw in [2^14, 2^15)
-__global__ __launch_bounds__(256) void k_wscale(NofParamsDev P, int* __restrict__ sw) {
+// per-layer weight scale exponents: sw[L] with max|W_L| 2^sw in [2^14, 2^15); grid 8, 1024 threads
+__global__ __launch_bounds__(1024) void k_wscale(NofParamsDev P, int* __restrict__ sw) {
   const int L = blockIdx.x;
-  const int in_f = L == 0 ? 63 : L == 4 ? 319 : 256;
-  const float* w = P.lin_w[L];
-  float m = 0.0f;
-  for (int i = threadIdx.x; i < 256 * in_f; i += 256) m = fmaxf(m, fabsf(w[i]));
-  m = wave_max_f(m);
-  __shared__ float red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    sw[L] = m > 0.0f && m == m && m < 3.0e38f ? 14 - ilogbf(m) : 0;
-  }
+  const float m = block_layer_absmax<1024>(P.lin_w[L], 256, L == 0 ? 63 : L == 4 ? 319 : 256, [](int) { return 1.0f; });
+  if (threadIdx.x == 0) sw[L] = m > 0.0f && m == m && m < 3.0e38f ? 14 - ilogbf(m) : 0;
 }
 
 __global__ void k_pack_train_h(NofParamsDev P, const int* __restrict__ sw, f16x8* __restrict__ out) {
@@ -1447,7 +1437,7 @@ static void pack_weights(const NofParamsDev& P, float* wp, f16x8* wh, int* sw, h
   if (g_train_math == 0) {
     hipLaunchKernelGGL(k_pack_train, dim3((unsigned)((TRAIN_W_FLOATS + 255) / 256)), dim3(256), 0, s, P, wp);
   } else {
-    hipLaunchKernelGGL(k_wscale, dim3(8), dim3(256), 0, s, P, sw);
+    hipLaunchKernelGGL(k_wscale, dim3(8), dim3(1024), 0, s, P, sw);
     hipLaunchKernelGGL(k_pack_train_h, dim3((unsigned)((TRAIN_H_VECS + 255) / 256)), dim3(256), 0, s, P, sw, wh);
   }
 }
@@ -1523,13 +1513,17 @@ __global__ __launch_bounds__(256) void k_pos_bound(const float* __restrict__ ray
     m = fmaxf(m, fmaxf(fabsf(p[0]), fmaxf(fabsf(p[1]), fabsf(p[2]))));   // fmaxf drops NaN positions
   }
   m = wave_max_f(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  // one atomic per workgroup (a few hundred in all: same-address atomics serialise at one L2 channel)
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 static void pos_bound_async(const float* rays, int stride, const float* z, int S, const float* ein, int64_t total,
                             unsigned* dev, hipStream_t s) {
   PCN_HIP(hipMemsetAsync(dev, 0, sizeof(unsigned), s));
-  const int64_t blocks = std::min<int64_t>(2048, (total + 255) / 256);
+  const int64_t blocks = std::min<int64_t>(512, (total + 255) / 256);
   hipLaunchKernelGGL(k_pos_bound, dim3((unsigned)blocks), dim3(256), 0, s, rays, stride, z, S, ein, total, dev);
 }
 
@@ -4752,7 +4746,7 @@ static void backward_remat(const float* rays, int ray_stride, const float* z, in
   PCN_CHECK(total % chunk != 1 && total != 1, "Expected more than 1 value per channel when training");
   const GaccLayout G = gacc_layout();
   pos_bound_async(rays, ray_stride, z, n_samples, nullptr, total, ws.pbound, s);
-  hipLaunchKernelGGL(k_wscale, dim3(8), dim3(256), 0, s, P, ws.sw);
+  hipLaunchKernelGGL(k_wscale, dim3(8), dim3(1024), 0, s, P, ws.sw);
   hipLaunchKernelGGL(k_pack_dgrad_h16, dim3((unsigned)((7 * HW_H + 255) / 256)), dim3(256), 0, s, P, ws.sw,
                      ws.wth16);
   hipLaunchKernelGGL(k_wcol, dim3(7), dim3(256), 0, s, P, ws.wcol);

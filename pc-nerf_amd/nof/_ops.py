@@ -605,7 +605,14 @@ def grad_params(model) -> list:
 
 
 def _grads_struct(model, device):
-    out = [torch.zeros_like(t, device=device) for t in grad_params(model)]
+    # one zeroed allocation for all 34 tensors (views at 256-byte aligned offsets): one fill kernel, not 34
+    ps = grad_params(model)
+    offs, o = [], 0
+    for t in ps:
+        offs.append(o)
+        o += (t.numel() + 63) & ~63
+    flat = torch.zeros(o, dtype=torch.float32, device=device)
+    out = [flat[a:a + t.numel()].view(t.shape) for a, t in zip(offs, ps)]
     s = H.NofGrads()
     for i in range(8):
         s.lin_w[i] = out[i].data_ptr()
