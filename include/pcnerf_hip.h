@@ -195,6 +195,18 @@ int pcnerf_nof_query_train_backward_fused(const float* rays, int64_t n_rays, int
                                           const float* grad_logit, void* state, size_t state_bytes, void* workspace,
                                           size_t workspace_bytes, const pcnerf_nof_grads* grads, void* store,
                                           int64_t store_chunks, void* stream);
+/* Data-parallel BatchNorm running statistics (replaces, for DP training, the per-process running-stat update of
+ * nn.BatchNorm1d in train mode, models.py:183-203 under render.py:47-50's chunk loop; Lightning's DDP leaves them
+ * per rank).  pcnerf_nof_train_bn_stats: each chunk's batch statistics of a fused / fold train query (or embedded
+ * forward) read from its `state` right after the forward -- out [C][8][2][256] doubles, C = ceil(total / chunk):
+ * the mean of h_L (bias included) and the biased variance.  pcnerf_bn_running_replay: running_mean / running_var of
+ * `params` advanced over `n_chunks` such records in order with the forward's own update arithmetic; `ns` (device,
+ * int64) holds each chunk's sample count.  nof/bn_sync.py gathers every rank's records and replays them in global
+ * chunk order, so every rank ends with the same statistics. */
+int pcnerf_nof_train_bn_stats(const void* state, size_t state_bytes, int64_t total_samples, int64_t chunk,
+                              double* out, void* stream);
+int pcnerf_bn_running_replay(const pcnerf_nof_params* params, float momentum, const double* stats, const int64_t* ns,
+                             int64_t n_chunks, void* stream);
 /* The training step's forward and backward without any activation store (the default training path since round 5;
  * replaces the autograd of render.py:47-50 / models.py:183-203 that train_kitti.py:155's loss.backward() runs).
  * pcnerf_nof_query_train_fused_state: the fused query above, keeping its `state` (pcnerf_nof_train_fold_bytes

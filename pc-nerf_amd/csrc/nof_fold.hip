@@ -572,6 +572,26 @@ __global__ void k_tf_running(NofParamsDev P, FoldDev F, SampleSrc q, double mom)
   P.bn_rv[L][k] = rv;
 }
 
+// grid 8, 256 threads: the running statistics after n chunks' batch statistics applied in order, k_tf_running's
+// arithmetic -- st [n][8][2][256] (mean of h_L with its bias, biased variance), ns [n] the chunks' sample counts.
+// The data-parallel BatchNorm sync (nof/bn_sync.py) replays every rank's chunks in global order with it.
+__global__ void k_bn_replay(NofParamsDev P, const double* __restrict__ st, const int64_t* __restrict__ ns, int64_t n,
+                            double mom) {
+  const int L = blockIdx.x, k = threadIdx.x;
+  if (!P.bn_rm[L]) return;
+  float rm = P.bn_rm[L][k], rv = P.bn_rv[L][k];
+#pragma unroll 8
+  for (int64_t c = 0; c < n; ++c) {
+    const double mean = st[(c * 8 + L) * 512 + k], var = st[(c * 8 + L) * 512 + 256 + k];
+    const int64_t m = ns[c];
+    rm = (float)(mom * mean + (1.0 - mom) * (double)rm);
+    const double unb = m > 1 ? var * (double)m / (double)(m - 1) : var;
+    rv = (float)(mom * unb + (1.0 - mom) * (double)rv);
+  }
+  P.bn_rm[L][k] = rm;
+  P.bn_rv[L][k] = rv;
+}
+
 // ------------------------------------------------------------------------------------------------- backward
 __device__ __forceinline__ float fold_logit_grad(const float* __restrict__ g, const float* __restrict__ p,
                                                  int64_t i) {
@@ -1012,6 +1032,41 @@ extern "C" size_t pcnerf_nof_train_fold_bytes(int64_t total_samples, int64_t chu
 extern "C" size_t pcnerf_nof_train_fused_bytes(int64_t total_samples, int64_t chunk) {
   if (total_samples <= 0 || chunk <= 0) return 0;
   return fold_layout(total_samples, std::min(chunk, total_samples), true).doubles * sizeof(double);
+}
+
+// Per-chunk BatchNorm batch statistics of a fused / fold train query (or embedded forward) from its state, while
+// the state is still the forward's (before any backward): out [C][8][2][256] doubles = each chunk's mean of h_L
+// (bias included) and biased variance -- what k_tf_running applied to running_mean / running_var.
+extern "C" int pcnerf_nof_train_bn_stats(const void* state, size_t state_bytes, int64_t total_samples, int64_t chunk,
+                                         double* out, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(state && out, "pcnerf_nof_train_bn_stats: null argument");
+  PCN_CHECK(total_samples > 0 && chunk > 0, "pcnerf_nof_train_bn_stats: empty input");
+  // the statistics' offset is the same in the forward-only and the full layout (pieces before it do not change)
+  const FoldLayout Lo = fold_layout(total_samples, std::min(chunk, total_samples), true);
+  PCN_CHECK(state_bytes >= Lo.doubles * sizeof(double), "pcnerf_nof_train_bn_stats: state buffer too small");
+  const double* sr = static_cast<const double*>(state) + Lo.off[6];
+  for (int L = 0; L < 8; ++L)
+    PCN_HIP(hipMemcpy2DAsync(out + L * 512, 8 * 512 * sizeof(double), sr + (size_t)L * Lo.C * 1024 + 512,
+                             1024 * sizeof(double), 512 * sizeof(double), (size_t)Lo.C, hipMemcpyDeviceToDevice,
+                             (hipStream_t)stream));
+  PCN_API_END
+}
+
+// running_mean / running_var of `params` advanced over n_chunks chunks' statistics in order (k_bn_replay):
+// stats [n_chunks][8][2][256] as pcnerf_nof_train_bn_stats writes them, ns [n_chunks] (device) their sample counts.
+extern "C" int pcnerf_bn_running_replay(const pcnerf_nof_params* params, float momentum, const double* stats,
+                                        const int64_t* ns, int64_t n_chunks, void* stream) {
+  PCN_API_BEGIN
+  PCN_CHECK(params && stats && ns, "pcnerf_bn_running_replay: null argument");
+  PCN_CHECK(n_chunks >= 0, "pcnerf_bn_running_replay: negative chunk count");
+  NofParamsDev P;
+  PCN_CHECK(to_dev_params(params, 1e-5f, &P), "pcnerf_bn_running_replay: null parameter pointer");
+  if (n_chunks > 0)
+    hipLaunchKernelGGL(k_bn_replay, dim3(8), dim3(256), 0, (hipStream_t)stream, P, stats, ns, n_chunks,
+                       (double)momentum);
+  PCN_LAUNCH_CHECK("pcnerf_bn_running_replay");
+  PCN_API_END
 }
 
 extern "C" int pcnerf_nof_query_train_fused(const float* rays, int64_t n_rays, int ray_stride, const float* z,

@@ -4219,7 +4219,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #if PCN_RB_NOSTORE
             if (cell[0] == 12345u && cell[3] == 4321u)
 #endif
-            *reinterpret_cast<u32x4*>(gt) = cell;
+            __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));   // streaming: keep L2 for the g / encoding tiles the other half re-reads
           }
           if constexpr (GOUT != 0) {
             f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tl * TILE_FLOATS) + (i >> 3) * 64 + sm +

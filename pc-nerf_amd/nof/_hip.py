@@ -102,6 +102,8 @@ _SIGS = {
     "pcnerf_nof_query_train_backward_remat": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams),
                                                       c_float, vp, vp, c_size, vp, c_size, ctypes.POINTER(NofGrads),
                                                       vp]),
+    "pcnerf_nof_train_bn_stats": (c_int, [vp, c_size, i64, i64, vp, vp]),
+    "pcnerf_bn_running_replay": (c_int, [ctypes.POINTER(NofParams), c_float, vp, vp, i64, vp]),
     "pcnerf_nof_train_fold_bytes": (c_size, [i64, i64]),
     "pcnerf_nof_train_fused_bytes": (c_size, [i64, i64]),
     "pcnerf_nof_query_train_fold": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams), c_float,

@@ -216,6 +216,52 @@ def fold_state(device, total_samples: int, chunk: int) -> torch.Tensor:
     return torch.empty((max(n, 1),), dtype=torch.uint8, device=device)
 
 
+# The active data-parallel BatchNorm recorder (nof.bn_sync.BnSync.record), or None: train-mode queries hand it their
+# per-chunk batch statistics.
+_BN_REC = None
+
+
+def _bn_before(model):
+    if _BN_REC is not None:
+        _BN_REC.before(model)
+
+
+def _bn_after(model, state: torch.Tensor, total: int, chunk: int):
+    if _BN_REC is not None:
+        _BN_REC.after(model, state, total, chunk)
+
+
+def _bn_unsupported():
+    if _BN_REC is not None:
+        raise NotImplementedError("data-parallel BatchNorm sync (nof.bn_sync) needs the default train math "
+                                  "(f16x2_3_fused) or the train fold: the layered train maths keep no per-chunk "
+                                  "statistics record")
+
+
+def bn_chunk_stats(state: torch.Tensor, total: int, chunk: int) -> torch.Tensor:
+    """(C, 8, 2, 256) float64: each BatchNorm chunk's mean of h_L (bias included) and biased variance, read from a
+    fused / fold train query's state right after its forward (pcnerf_nof_train_bn_stats)."""
+    chunk = max(1, min(int(chunk), int(total)))
+    C = -(-int(total) // chunk)
+    out = torch.empty((C, 8, 2, 256), dtype=torch.float64, device=state.device)
+    H.check(H.lib().pcnerf_nof_train_bn_stats(state.data_ptr(), state.numel(), int(total), chunk, out.data_ptr(),
+                                              _stream(state)))
+    return out
+
+
+def bn_running_replay(model, stats: torch.Tensor, ns: torch.Tensor) -> None:
+    """Advance the model's running_mean / running_var over the chunks' statistics ``stats`` (n, 8, 2, 256) float64
+    in order, ``ns`` (n,) int64 their sample counts (pcnerf_bn_running_replay: the forward's own arithmetic)."""
+    stats = stats.contiguous()
+    ns = ns.to(device=stats.device, dtype=torch.int64).contiguous()
+    if stats.dim() != 4 or tuple(stats.shape[1:]) != (8, 2, 256) or ns.numel() != stats.shape[0]:
+        raise ValueError("stats must be (n, 8, 2, 256) with one sample count per chunk")
+    mom, _ = _bn_config(model)
+    s, keep = _params(model)
+    H.check(H.lib().pcnerf_bn_running_replay(ctypes.byref(s), mom, stats.data_ptr(), ns.data_ptr(), stats.shape[0],
+                                             _stream(stats)))
+
+
 def _track_batches(model, n_chunks: int) -> None:
     for bn in model.norms():
         if bn.num_batches_tracked is not None:
@@ -260,9 +306,11 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
         chunk = max(1, min(int(chunk), R * S))
         mom, eps = _bn_config(model)
         s, keep_params = _params(model)
+        _bn_before(model)
         H.check(L.pcnerf_nof_query_train_fused_state(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
                                                      ctypes.byref(s), mom, eps, keep.data_ptr(), keep.numel(),
                                                      p.data_ptr(), st))
+        _bn_after(model, keep, R * S, chunk)
         _track_batches(model, -(-R * S // int(chunk)))
     elif model.training and (fold is not None or _TRAIN_FOLD):
         chunk = max(1, min(int(chunk), R * S))
@@ -270,9 +318,11 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
         s, keep = _params(model)
         if fold is None:
             fold = fold_state(z.device, R * S, chunk)
+        _bn_before(model)
         H.check(L.pcnerf_nof_query_train_fold(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
                                               ctypes.byref(s), mom, eps, fold.data_ptr(), fold.numel(),
                                               p.data_ptr(), st))
+        _bn_after(model, fold, R * S, chunk)
         _track_batches(model, -(-R * S // int(chunk)))
     elif model.training and _TRAIN_FUSED:
         # the network per sample in one fused kernel; with an activation store it also writes the stored chunks'
@@ -280,6 +330,7 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
         chunk = max(1, min(int(chunk), R * S))
         mom, eps = _bn_config(model)
         s, keep = _params(model)
+        _bn_before(model)
         if store is not None and store.n_chunks > 0:
             # the state (the chunks' encoding moments and layer maps) is the backward's too: kept with the store
             store.fstate = fold_state(z.device, R * S, chunk)
@@ -287,13 +338,16 @@ def query(model, rays: torch.Tensor, z: torch.Tensor, chunk: int, store=None, fo
                                                          int(chunk), ctypes.byref(s), mom, eps,
                                                          store.fstate.data_ptr(), store.fstate.numel(), p.data_ptr(),
                                                          store.buf.data_ptr(), store.n_chunks, st))
+            _bn_after(model, store.fstate, R * S, chunk)
         else:
             ws = _workspace(z.device, int(L.pcnerf_nof_train_fused_bytes(R * S, chunk)))
             H.check(L.pcnerf_nof_query_train_fused(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, int(chunk),
                                                    ctypes.byref(s), mom, eps, ws.data_ptr(), ws.numel(),
                                                    p.data_ptr(), st))
+            _bn_after(model, ws, R * S, chunk)
         _track_batches(model, -(-R * S // int(chunk)))
     elif model.training:
+        _bn_unsupported()
         chunk = max(1, min(int(chunk), R * S))   # a larger chunk is the same single BatchNorm chunk
         mom, eps = _bn_config(model)
         s, keep = _params(model)
@@ -335,8 +389,10 @@ def nof_forward_embedded(model, x: torch.Tensor, with_fold_state: bool = False):
         mom, eps = _bn_config(model)
         s, keep = _params(model)
         fold = fold_state(x.device, B, B)
+        _bn_before(model)
         H.check(L.pcnerf_nof_forward_train_fold(x.data_ptr(), B, ctypes.byref(s), mom, eps, fold.data_ptr(),
                                                 fold.numel(), out.data_ptr(), st))
+        _bn_after(model, fold, B, B)
         _track_batches(model, 1)
     elif model.training and _TRAIN_FUSED:
         if B <= 1:
@@ -344,12 +400,15 @@ def nof_forward_embedded(model, x: torch.Tensor, with_fold_state: bool = False):
         mom, eps = _bn_config(model)
         s, keep = _params(model)
         ws = _workspace(x.device, int(L.pcnerf_nof_train_fused_bytes(B, B)))
+        _bn_before(model)
         H.check(L.pcnerf_nof_forward_train_fused(x.data_ptr(), B, ctypes.byref(s), mom, eps, ws.data_ptr(),
                                                  ws.numel(), out.data_ptr(), st))
+        _bn_after(model, ws, B, B)
         _track_batches(model, 1)
     elif model.training:
         if B <= 1:
             raise ValueError("Expected more than 1 value per channel when training")
+        _bn_unsupported()
         mom, eps = _bn_config(model)
         s, keep = _params(model)
         ws = _workspace(x.device, L.pcnerf_nof_train_workspace_bytes(B))

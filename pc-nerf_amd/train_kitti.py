@@ -14,8 +14,10 @@ training / validation step arithmetic (train_kitti.py:20-245); what Lightning di
     best.ckpt on the lowest train/loss -- loadable by the reference's load_ckpt;
   * data parallel (one process per GPU, ``torchrun``): every rank takes its slice of each global batch of
     ``batch_size * world`` rays (DistributedSampler semantics), gradients are averaged with one all_reduce of a
-    flat bucket over RCCL (nof.blocks.allreduce_grads); BatchNorm statistics stay per rank (no sync_batchnorm,
-    as Lightning's DDP default).
+    flat bucket over RCCL (nof.blocks.allreduce_grads); each chunk is normalised by its own batch statistics on
+    its rank (no sync_batchnorm, as Lightning's DDP), while the BatchNorm RUNNING statistics are made
+    rank-independent (nof.bn_sync: every rank's chunk statistics replayed in global chunk order), so every rank's
+    checkpoint is the same.
 
 Usage (PC-NeRF KITTI-00 1151-1200, shells/pretraining/KITTI00_pcnerf_train.bash's options):
     python pc-nerf_amd/train_kitti.py --datasettype kitti_dataload --root_dir <pcd dir> --pose_path poses.txt \\
@@ -36,6 +38,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from torch.optim.lr_scheduler import MultiStepLR  # noqa: E402
 
 from nof.blocks import allreduce_grads, shard_batch  # noqa: E402
+from nof.bn_sync import BnSync  # noqa: E402
 from nof.criteria import child_range_loss, nof_loss  # noqa: E402
 from nof.criteria.metrics import abs_error, acc_thres, eval_points  # noqa: E402
 from nof.dataset import nof_dataset  # noqa: E402
@@ -214,6 +217,7 @@ def fit(system, max_steps=0, log_path=None, ckpt_dir=None):
     h = system.hparams
     ddp = dist.is_available() and dist.is_initialized()
     rank, world = (dist.get_rank(), dist.get_world_size()) if ddp else (0, 1)
+    bns = BnSync() if ddp else None
     system.prepare_data()
     opt, sched = system.configure_optimizers()
     params = system.parameters()
@@ -235,10 +239,15 @@ def fit(system, max_steps=0, log_path=None, ckpt_dir=None):
             if idx.numel() == 0:
                 continue
             opt.zero_grad(set_to_none=True)
-            loss, logs = system.training_step(system.train_dataset[idx], b)
+            if ddp:
+                with bns.record():
+                    loss, logs = system.training_step(system.train_dataset[idx], b)
+            else:
+                loss, logs = system.training_step(system.train_dataset[idx], b)
             loss.sum().backward()
             if ddp:
                 allreduce_grads(params)
+                bns.sync()
             opt.step()
             step += 1
             ep_loss.append(loss.detach())

@@ -3,6 +3,7 @@ max-over-ranks time used by bench.py."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -252,3 +253,70 @@ def test_eval_render_frame_world2_matches_one_process(tail):
         assert p.exitcode == 0
     assert res[1][0] is None and res[0][1] == res[1][1] == n1
     np.testing.assert_array_equal(res[0][0], want.numpy())
+
+
+def _bn_records(rank, seed):
+    """Rank ``rank``'s synthetic chunk-statistics records: (model index, stats, total, chunk), ragged per rank."""
+    g = torch.Generator().manual_seed(1000 * seed + rank)
+    out = []
+    for mi, total, chunk in ((0, 1000 + 300 * rank, 256), (1, 700 - 200 * rank, 128), (0, 513 + 7 * rank, 512)):
+        C = -(-total // chunk)
+        st = torch.empty((C, 8, 2, 256), dtype=torch.float64)
+        st[:, :, 0] = torch.randn((C, 8, 256), generator=g, dtype=torch.float64)
+        st[:, :, 1] = torch.rand((C, 8, 256), generator=g, dtype=torch.float64) * 2 + 0.01
+        out.append((mi, st, total, chunk))
+    return out
+
+
+def _bn_models():
+    from nof import synthetic as syn
+    from nof.networks import NOF_coarse, NOF_fine
+    return [syn.load_into(NOF_coarse(), syn.init_nof_params(11)), syn.load_into(NOF_fine(), syn.init_nof_params(12))]
+
+
+def _bn_worker(rank, world, port, q):
+    from bn_replay_ref import replay_reference
+    from nof.bn_sync import BnSync
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        models = _bn_models()
+        bns = BnSync()
+        for mi, st, total, chunk in _bn_records(rank, 3):
+            bns.add_record(models[mi], st, total, chunk)
+            for b in models[mi].norms():   # the rank's own forward moved its buffers (sync must start over)
+                b.running_mean.add_(rank + 1.0)
+                b.num_batches_tracked.add_(-(-total // chunk))
+        bns.sync(replay=replay_reference)
+        q.put((rank, [{k: v.numpy().copy() for k, v in m.state_dict().items()} for m in models]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bn_sync_world2_rank_independent_running_stats():
+    """nof.bn_sync under gloo world 2: every rank ends with the same BatchNorm running statistics, equal to one
+    process applying rank 0's then rank 1's chunks (per query, in call order) from the step's starting values, and
+    num_batches_tracked counting both ranks' chunks.  Ragged chunk counts per rank."""
+    from bn_replay_ref import replay_reference
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bn_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    models = _bn_models()
+    recs = [_bn_records(r, 3) for r in range(2)]
+    for i in range(3):
+        mi = recs[0][i][0]
+        st = torch.cat([recs[r][i][1] for r in range(2)], 0)
+        ns = [min(c, t - k * c) for r in range(2) for t, c in [recs[r][i][2:]] for k in range(-(-t // c))]
+        replay_reference(models[mi], st, torch.tensor(ns))
+        for b in models[mi].norms():
+            b.num_batches_tracked.add_(len(ns))
+    for m, s0, s1 in zip(models, got[0], got[1]):
+        for k, v in m.state_dict().items():
+            np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
+            np.testing.assert_array_equal(s0[k], v.numpy(), err_msg=k)

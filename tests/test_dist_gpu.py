@@ -111,3 +111,77 @@ def test_data_parallel_hip_gradients_two_ranks():
         np.testing.assert_array_equal(a, b)                       # every rank ends with the same gradients
         want = (x + y) / 2
         np.testing.assert_allclose(a, want, rtol=1e-6, atol=1e-6 * max(np.abs(want).max(), 1e-30))
+
+
+def _bn_step(models, rays, bns=None):
+    """One train_kitti.py:117-155 step's forward + backward on ``rays`` (recorded by ``bns`` when given)."""
+    from nof.criteria import nof_loss
+    from nof.networks import Embedding
+    from nof.render import render_rays_train
+    import contextlib
+    mc, mf = models
+    with (bns.record() if bns is not None else contextlib.nullcontext()):
+        res = render_rays_train(mc, mf, Embedding(3, 10), rays, **KW)
+    sl1 = nof_loss["smoothl1"]()
+    gt = rays[:, 14]
+    loss = 1e-1 * sl1(1e1 * res["depth"], 1e1 * gt) + 1e-1 * sl1(1e1 * res["depth_fine"], 1e1 * gt)
+    loss.backward()
+
+
+def _bn_models_gpu(chunk_seed=0):
+    from nof import synthetic as syn
+    from nof.networks import NOF_coarse, NOF_fine
+    return (syn.load_into(NOF_coarse(), syn.init_nof_params(1234)).cuda().train(),
+            syn.load_into(NOF_fine(), syn.init_nof_params(5678)).cuda().train())
+
+
+def _bn_rank(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "pc-nerf_amd"), here):
+        sys.path.insert(0, p)
+    from nof import synthetic as syn
+    from nof.blocks import allreduce_grads, shard_batch
+    from nof.bn_sync import BnSync
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        rays = torch.from_numpy(syn.make_rays(401, seed=43)).cuda()
+        idx = shard_batch(torch.arange(401, device="cuda"), rank, world)
+        models = _bn_models_gpu()
+        bns = BnSync()
+        _bn_step(models, rays[idx].contiguous(), bns)
+        allreduce_grads([p for m in models for p in m.parameters()])
+        bns.sync()
+        q.put((rank, [{k: v.cpu().numpy() for k, v in m.state_dict().items()} for m in models]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_data_parallel_batchnorm_running_stats_rank_independent():
+    """Data parallel over 2 gloo ranks sharing the GPU, the default train math: after nof.bn_sync every rank's
+    state_dict (weights' gradients aside: running_mean / running_var / num_batches_tracked included) is identical,
+    and the running statistics equal one process rendering rank 0's shard and then rank 1's (train mode, chunk
+    4096: 201 / 200 rays, so the ranks' tail chunks differ) -- bit for bit (the HIP replay of every chunk's recorded
+    statistics in global order, pcnerf_nof_train_bn_stats + pcnerf_bn_running_replay)."""
+    from nof import synthetic as syn
+    from nof.blocks import shard_batch
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_bn_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=200) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    rays = torch.from_numpy(syn.make_rays(401, seed=43)).cuda()
+    models = _bn_models_gpu()
+    for r in range(2):
+        _bn_step(models, rays[shard_batch(torch.arange(401, device="cuda"), r, 2)].contiguous())
+    for m, s0, s1 in zip(models, got[0], got[1]):
+        for k, v in m.state_dict().items():
+            np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
+            if "running" in k or "num_batches" in k:
+                np.testing.assert_array_equal(s0[k], v.cpu().numpy(), err_msg=k)
