@@ -528,7 +528,11 @@ def run_line(a, L, dev, rank, world):
     return {"value": value, "elapsed": elapsed, "rays_per_step": rays_per_step, "roofline": roof,
             "kernels": kernels, "kstep_ms": kstep_ms, "fp32_mfma": fp32_line, "cpu_baseline": cpu,
             "cd_vs_ref": cdref, "loss": loss_val, "train_math": train_math, "eval_math": eval_math,
-            "blocks_rank0": blocks_rank0}
+            "blocks_rank0": blocks_rank0,
+            "backward": (None if not grad else
+                         "remat: no activation store, no memory budget set -- the drop-in's default training path "
+                         "(nof._ops.set_train_backward)" if _ops.remat_enabled() else
+                         "store: activation store, budget free HBM - 4 GiB (opt-in)")}
 
 
 def line_json(a, world, ln):
@@ -573,7 +577,8 @@ def line_json(a, world, ln):
                    "batchnorm": "train (batch stats per chunk)" if train else "eval (folded)",
                    "network": "affine fold (sigmoid(a.e + c))" if a.fold else "9 Linear layers as written",
                    "segmented_ratio": 0.1 if train else None, "perturb": 1 if train else 0,
-                   "parallelism": (f"dp{world}" if a.config == 3 else f"blocks{world}"), "gather": bool(a.gather)},
+                   "parallelism": (f"dp{world}" if a.config == 3 else f"blocks{world}"), "gather": bool(a.gather),
+                   "backward": ln.get("backward")},
         "roofline": ln["roofline"],
         "train_math": ln["train_math"],
         "eval_math": ln["eval_math"],
