@@ -4061,6 +4061,17 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
   const int eo = tile_scale_exp(obm);
   const float gso = ldexpf(1.0f, eo);
   if (bid == 0 && t == 0) gexp[layer - 1] = eo;
+  // the epilogue's per-feature constants folded (read by the D waves after the barrier below):
+  //   2^eo g_{L-1} = (dy A - B) - (xh + xm) C,  A = dun invstd gamma 2^eo,  B = gm invstd gamma 2^eo,
+  //   C = 2^-e kk invstd gamma 2^eo   (slots 640 / 256 / 384; cun at 128 stays for the W waves)
+  const float dun = ldexpf(1.0f, -sw[layer]) * gun;
+  if (t < 128) {
+    const float sc = cst[512 + t] * cst[640 + t] * gso;
+    const float cb = cst[256 + t] * sc, cc = cst[128 + t] * cst[384 + t] * sc;
+    cst[640 + t] = dun * sc;
+    cst[256 + t] = cb;
+    cst[384 + t] = cc;
+  }
   auto dma_g = [&](int k) {
     const int tl = pr + k * npair;
     char* const sb = fb + (size_t)(k & 1) * FB_BUF;
@@ -4133,7 +4144,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
   __builtin_amdgcn_s_barrier();
   if (wv < 4) {
     // ---- D: data gradient of input features 128 hf + 32 rw + 16 rb + lm, epilogue, g_{L-1} stores
-    const float dun = ldexpf(1.0f, -sw[layer]) * gun;
+    const float gui = ldexpf(1.0f, -eo);
     f16x8 wr[8][2][2];
     {
       const f16x8* __restrict__ w8 = wt + lane;
@@ -4180,11 +4191,9 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
         const int il = 32 * rw + 16 * rb + 4 * kg;
-        const f32x4 cun = *reinterpret_cast<const f32x4*>(cst + 128 + il);
-        const f32x4 cgm = *reinterpret_cast<const f32x4*>(cst + 256 + il);
-        const f32x4 ckk = *reinterpret_cast<const f32x4*>(cst + 384 + il);
-        const f32x4 cis = *reinterpret_cast<const f32x4*>(cst + 512 + il);
-        const f32x4 cga = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+        const f32x4 cA = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+        const f32x4 cB = *reinterpret_cast<const f32x4*>(cst + 256 + il);
+        const f32x4 cC = *reinterpret_cast<const f32x4*>(cst + 384 + il);
         const int i = 128 * hf + il;
 #pragma unroll
         for (int sb = 0; sb < 2; ++sb) {
@@ -4193,18 +4202,14 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
           const int o = fb_off<FB_XP>(sm, il);
           const f16x4 xh = *reinterpret_cast<const f16x4*>(xb + o);
           const f16x4 xm = *reinterpret_cast<const f16x4*>(xb + FB_XPART + o);
-          f32x4 v;
+          f32x4 vs;   // 2^eo g_{L-1}
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float d = ad[rb][sb][q] * dun;
-            const float xc = ((float)xh[q] + (float)xm[q]) * cun[q];
-            v[q] = valid ? ((d - cgm[q]) - xc * ckk[q]) * cis[q] * cga[q] : 0.0f;
-            gmo = fmaxf(gmo, fabsf(v[q]));
+            const float xs = (float)xh[q] + (float)xm[q];   // exact: the split's two parts
+            vs[q] = valid ? fmaf(-xs, cC[q], fmaf(ad[rb][sb][q], cA[q], -cB[q])) : 0.0f;
+            gmo = fmaxf(gmo, fabsf(vs[q]));
           }
           if constexpr (GOUT != 1) {
-            f32x4 vs;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) vs[q] = v[q] * gso;
             s16x4 p0, p1;
             split2_x4(vs, p0, p1);
             // one 16-byte cell per lane: the lanes of 16-lane rows 2r / 2r+1 (kg even / odd: features i .. i+3 and
@@ -4222,6 +4227,9 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
             __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));   // streaming: keep L2 for the g / encoding tiles the other half re-reads
           }
           if constexpr (GOUT != 0) {
+            f32x4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = vs[q] * gui;   // exact: a power of two
             f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tl * TILE_FLOATS) + (i >> 3) * 64 + sm +
                          32 * ((i >> 2) & 1);
             __builtin_nontemporal_store(v, dst);
@@ -4234,7 +4242,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_s_barrier();
     }
-    gmo = wave_max_f(gmo);
+    gmo = wave_max_f(gmo) * gui;
     if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rw) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
   } else {
     // ---- W: x of tile k + 1, weight gradient rows j = 64 rw + 16 jb + lm (4 blocks) x the half's 128 columns
