@@ -2498,22 +2498,36 @@ __device__ __forceinline__ void split3_x4(const f32x4& v, s16x4& p0, s16x4& p1, 
   }
 }
 
+// hi = fp16(v), mid = fp16(v - hi) for a pair of values: the pair's hi parts by one packed conversion, each mid by
+// ONE mixed-precision fma (v_fma_mix{lo,hi}_f16 with the f16 hi operand selected by op_sel): v - hi is exact in
+// fp32, so this is the same single rounding as converting the fp32 difference, bit for bit (nof_eval.hip's
+// eh_split8; scripts/micro/split_mix.hip checked it over 67M values) -- 3 instructions a pair instead of ~10
+__device__ __forceinline__ void split2_pair(float a, float b, unsigned& hb, unsigned& mb) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  h2 hp;
+  hp[0] = (_Float16)a;
+  hp[1] = (_Float16)b;
+  hb = __builtin_bit_cast(unsigned, hp);
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(mb) : "v"(hb), "v"(a));
+  asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(mb) : "v"(hb), "v"(b));
+}
+
 __device__ __forceinline__ void split2_x4(const f32x4& v, s16x4& p0, s16x4& p1) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const _Float16 a = (_Float16)v[q];
-    p0[q] = __builtin_bit_cast(short, a);
-    p1[q] = __builtin_bit_cast(short, (_Float16)(v[q] - (float)a));
-  }
+  typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+  unsigned h0, m0, h1, m1;
+  split2_pair(v[0], v[1], h0, m0);
+  split2_pair(v[2], v[3], h1, m1);
+  p0 = __builtin_bit_cast(s16x4, u32x2_{h0, h1});
+  p1 = __builtin_bit_cast(s16x4, u32x2_{m0, m1});
 }
 
 __device__ __forceinline__ void split2_f16(const float (&v)[8], f16x8& hi, f16x8& mid) {
+  typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+  unsigned h[4], m[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const _Float16 a = (_Float16)v[j];
-    hi[j] = a;
-    mid[j] = (_Float16)(v[j] - (float)a);
-  }
+  for (int p = 0; p < 4; ++p) split2_pair(v[2 * p], v[2 * p + 1], h[p], m[p]);
+  hi = __builtin_bit_cast(f16x8, u32x4_{h[0], h[1], h[2], h[3]});
+  mid = __builtin_bit_cast(f16x8, u32x4_{m[0], m[1], m[2], m[3]});
 }
 
 // byte offset of features f .. f+3 (f % 4 == 0) of row r (sample within the half tile) in one x part
