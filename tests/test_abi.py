@@ -78,6 +78,28 @@ def test_math_switches_without_gpu():
     assert _ops.get_eval_math() == "f16x2_3"
 
 
+def test_activation_store_skips_chunks_beyond_32bit_layer_offsets(monkeypatch):
+    """the fused query addresses a stored layer with a 32-bit byte offset, so under the default
+    train math a chunk whose layer region reaches 4 GiB (>= 4,194,304 samples) is not stored -- the store holds no
+    chunk and every chunk is recomputed -- instead of the forward failing, however large the budget."""
+    import torch
+    from nof import _ops
+    gib = 1 << 30
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (280 * gib, 288 * gib))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda dev=None: 0)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda dev=None: 0)
+    monkeypatch.delenv("PCNERF_ACT_STORE", raising=False)
+    prev = _ops.set_activation_store_budget(1 << 62)
+    prev_math = _ops.set_train_math("f16x2_3_fused")
+    try:
+        big = 1 << 22
+        st = _ops.ActivationStore("cuda:0", 2 * big, big, 0)
+        assert st.n_chunks == 0 and st.buf is None
+    finally:
+        _ops.set_activation_store_budget(prev)
+        _ops.set_train_math(prev_math)
+
+
 def test_activation_store_default_is_bounded(monkeypatch):
     """The drop-in's default activation-store budget is DEFAULT_STORE_CAP (32 GiB) however much HBM is free, at most
     half of what is free, and callers opt into more (set_activation_store_budget / PCNERF_ACT_STORE_GB)."""
