@@ -626,9 +626,7 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
               16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw",
               # (the train query writing the activation store is its own instantiation)
               18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" and not remat else "k_nof_eval_h3<true,false>",
-              # the default role-split kernel (PCNERF_BWD_KERNEL=1 selects the lockstep k_bwd_remat for A/Bs)
-              19: (("k_bwd_remat<0,0>" if os.environ.get("PCNERF_BWD_KERNEL") == "1" else "k_bwd_remat2<0,0>")
-                   if remat else "k_bwd_fused<0,false>")}
+              19: "k_bwd_remat2<0,0>" if remat else "k_bwd_fused<0,false>"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd", 20: "k_g7"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]

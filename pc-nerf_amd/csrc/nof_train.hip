@@ -3698,8 +3698,9 @@ __global__ __launch_bounds__(512, 1) void k_g7(const char* __restrict__ enc, con
 }
 constexpr size_t G7_LDS = 2 * FB_ENC + 1024 * sizeof(float);
 
-// k_bwd_remat<LAY, GOUT>: one layer's backward over a chunk in one pass, as k_bwd_fused (a pair of workgroups per
-// tile, halves of the input features, 8 waves; W_L^T rows in registers; one barrier a tile), with
+// The rematerialised layer launch (k_bwd_remat2 below): one layer's backward over a chunk in one pass, as k_bwd_fused
+// (a pair of workgroups per tile, halves of the input features, 8 waves; W_L^T rows in registers; one barrier a
+// tile), with
 //   * g_L arriving PRE-SPLIT by LDS-DMA straight into the tile's split buffer (no raw buffer, no conversion: its
 //     producer wrote it at 2^gexp[L]), one tile ahead;
 //   * the layer input x = h_{L-1} - mean made on the matrix pipe from the encoding image (two LDS slots, one tile
@@ -3711,303 +3712,8 @@ constexpr size_t G7_LDS = 2 * FB_ENC + 1024 * sizeof(float);
 // HBM per sample: 1 KiB of g_L, 256 B of encoding in, 1 KiB of g_{L-1} out (2.25 KiB; the store path moved 3).
 constexpr size_t RB_PX = 128 * 256;   // the half's P' rows (128 x 16 f16x8), slot q of row r at q ^ (r & 15)
 constexpr size_t RB_LDS = 2 * (size_t)FB_BUF + 2 * FB_ENC + RB_PX + 8 * 128 * sizeof(float);
-static_assert(RB_LDS <= 160 * 1024, "k_bwd_remat LDS");
-template <int LAY, int GOUT>
-__global__ __launch_bounds__(512, 1) void k_bwd_remat(const char* __restrict__ gin, char* __restrict__ gout,
-                                                       float* __restrict__ gout32, const f16x8* __restrict__ wt,
-                                                       const int* __restrict__ sw, int layer, int64_t n,
-                                                       const float* __restrict__ coefp, const float* __restrict__ bnb,
-                                                       const float* __restrict__ gamma, int* __restrict__ gexp,
-                                                       const float* __restrict__ wcol,
-                                                       const unsigned* __restrict__ gmax_in,
-                                                       unsigned* __restrict__ gmax_out, float* __restrict__ part,
-                                                       FbRed red, const char* __restrict__ enc,
-                                                       const f16x8* __restrict__ px, const float* __restrict__ pxs) {
-  constexpr int C = WgradCfg<LAY>::C, COL = LAY == 2 ? 64 : 0;
-  constexpr int NST = (GOUT != 1 ? 4 : 0) + (GOUT != 0 ? 2 : 0);   // global stores per wave and tile
-  extern __shared__ __attribute__((aligned(16))) char fb[];
-  char* const enb = fb + 2 * FB_BUF;
-  char* const pxl = enb + 2 * FB_ENC;
-  float* const cst = reinterpret_cast<float*>(pxl + RB_PX);   // [csc | cun | gm | kk | invstd | gamma | xs | bound]
-  const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int bid = (int)blockIdx.x, hf = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
-  const int npair = (int)gridDim.x >> 1;
-  const int nt = (int)((n + 31) / 32);
-  const int nk = pr < nt ? (nt - 1 - pr) / npair + 1 : 0;   // this pair's tiles: pr + k npair, k < nk
-  const float rn = sqrtf((float)n);
-  if (t < 128) {
-    const int c = 128 * hf + t;
-    const float invstd = coefp[256 + c];
-    const float bnd = rn / invstd;   // Samuelson: |h - mean| <= sqrt(n) sigma
-    int e = (bnd > 0.0f && bnd < 3.0e38f) ? 14 - ilogbf(bnd) : 0;
-    e = e < -60 ? -60 : e > 60 ? 60 : e;
-    cst[t] = ldexpf(1.0f, e);
-    cst[128 + t] = ldexpf(1.0f, -e);
-    cst[256 + t] = bnb[c];
-    cst[384 + t] = bnb[256 + c];
-    cst[512 + t] = invstd;
-    cst[640 + t] = gamma[c];
-    cst[768 + t] = ldexpf(pxs[c], e);   // x accumulator (P' rows at 2^t_i) -> x at its split scale
-  }
-  unsigned gmx = 0;
-  for (int i = 0; i < GMAX_SLOTS; ++i) gmx = max(gmx, gmax_in[i]);   // (uniform loads)
-  {   // the bound on |g_{L-1}| over all 256 columns (every workgroup computes the same value)
-    const int c = t & 255;
-    const float invstd = coefp[256 + c];
-    float ob = ((wcol[c] * __uint_as_float(gmx) + fabsf(bnb[c])) + rn / invstd * fabsf(bnb[256 + c])) * invstd *
-               fabsf(gamma[c]) * 1.01f;
-    ob = wave_max_f(ob);
-    if (lane == 0) cst[896 + wv] = ob;
-  }
-  for (int j = t; j < 128 * 16; j += 512) {   // the half's P' rows, slot-swizzled by row
-    const int r = j >> 4, q = j & 15;
-    *reinterpret_cast<f16x8*>(pxl + r * 256 + 16 * (q ^ (r & 15))) = px[(size_t)(128 * hf + r) * 16 + q];
-  }
-  const int eg = gexp[layer];
-  const float gun = ldexpf(1.0f, -eg);
-  const float dun = ldexpf(1.0f, -sw[layer]) * gun;   // data-gradient accumulator -> dL/dy
-  f16x8 wr[8][2];
-  {
-    const f16x8* __restrict__ w8 = wt + lane;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) wr[ks][p] = w8[((ks * 16 + 8 * hf + wv) * 2 + p) * 64];
-  }
-  __syncthreads();
-  float obm = cst[896];
-#pragma unroll
-  for (int i = 1; i < 8; ++i) obm = fmaxf(obm, cst[896 + i]);
-  const int eo = tile_scale_exp(obm);
-  const float gso = ldexpf(1.0f, eo);
-  if (bid == 0 && t == 0) gexp[layer - 1] = eo;
-  // g_L of tile k (pre-split image) -> split buffer k & 1's g half: a linear copy, 4 KiB per wave
-  auto dma_g = [&](int k) {
-    const int tl = pr + k * npair;
-    char* const sb = fb + (size_t)(k & 1) * FB_BUF;
-    int ln = lane;
-    asm volatile("" : "+v"(ln));   // lane addresses recomputed per tile: held across the loop they would spill
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-      fb_glds16(gin + (size_t)tl * GS_TILE + (4 * wv + m) * 1024 + 16 * ln, sb + (4 * wv + m) * 1024);
-  };
-  auto dma_enc = [&](int k) {   // tile k's encoding image -> slot k & 1 (1 KiB per wave)
-    const int tl = pr + k * npair;
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    fb_glds16(enc + (size_t)tl * FB_ENC + wv * 1024 + ln * 16, enb + (k & 1) * FB_ENC + wv * 1024);
-  };
-  // x of tile k (this wave's 16 columns il .. il + 15 of the half) from slot k & 1 -> split buffer k & 1's x half
-  auto remat_x = [&](int k) {
-    const char* eb = enb + (k & 1) * FB_ENC;
-    char* const xb = fb + (size_t)(k & 1) * FB_BUF + 2 * FB_GPART;
-    const int r = 16 * wv + lm;
-    f16x8 pa[2][2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const int q = (2 * ks + p) * 4 + kg;
-        pa[ks][p] = *reinterpret_cast<const f16x8*>(pxl + r * 256 + 16 * (q ^ (r & 15)));
-      }
-    f32x4 ax[2] = {f32x4{}, f32x4{}};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        const int o = fb_eoff(16 * sb + lm, 4 * ks + kg);
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(eb + o);
-        const f16x8 bm = *reinterpret_cast<const f16x8*>(eb + FB_ENC / 2 + o);
-        ax[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[ks][0], bh, ax[sb], 0, 0, 0);
-        ax[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[ks][0], bm, ax[sb], 0, 0, 0);
-        ax[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[ks][1], bh, ax[sb], 0, 0, 0);
-      }
-    const int il = 16 * wv + 4 * kg;
-    const f32x4 xs = *reinterpret_cast<const f32x4*>(cst + 768 + il);
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-      f32x4 v;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = ax[sb][q] * xs[q];   // (the image is zero past the chunk)
-      s16x4 p0, p1;
-      split2_x4(v, p0, p1);
-      const int o = fb_off<FB_XP>(16 * sb + lm, il);
-      *reinterpret_cast<s16x4*>(xb + o) = p0;
-      *reinterpret_cast<s16x4*>(xb + FB_XPART + o) = p1;
-    }
-  };
-  f32x4 aw[2][8];
-#pragma unroll
-  for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-    for (int ib = 0; ib < 8; ++ib) aw[jb][ib] = f32x4{};
-  float dbacc[2] = {0.0f, 0.0f};
-  float gmo = 0.0f;
-  const int trq = lm >> 2, trp = lm & 3;   // transposed reads: lane lm = 4 q + pp of 16-lane group kg
-  if (nk > 0) {
-    dma_g(0);
-    dma_enc(0);
-    if (nk > 1) dma_enc(1);
-    __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
-    __builtin_amdgcn_s_barrier();   // every wave's part of tile 0's encoding (and the P' rows, constants)
-    remat_x(0);
-  }
-  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-  __builtin_amdgcn_s_barrier();
-  auto tile = [&](int k) {
-    const int tl = pr + k * npair;
-    if (k + 1 < nk) dma_g(k + 1);     // into split buffer (k + 1) & 1, free since the last barrier
-    if (k + 2 < nk) dma_enc(k + 2);   // into slot k & 1, read by remat_x(k) before the last barrier
-    const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
-    const char* gb = sp;
-    const char* xb = sp + 2 * FB_GPART;
-    f32x4 ad[2] = {f32x4{}, f32x4{}};
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        const int o = gs_off(16 * sb + lm, 4 * ks + kg);
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(gb + o);
-        const f16x8 bm = *reinterpret_cast<const f16x8*>(gb + FB_GPART + o);
-        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bh, ad[sb], 0, 0, 0);
-        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][0], bm, ad[sb], 0, 0, 0);
-        ad[sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][1], bh, ad[sb], 0, 0, 0);
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    if (k + 1 < nk) remat_x(k + 1);   // slot (k + 1) & 1: DMA'd a tile ago, every wave's part waited before the barrier
-    __builtin_amdgcn_s_setprio(1);
-    {   // weight gradient (k_bwd_fused's: transposed operand reads, next column block's read under the current)
-      auto read8 = [&](unsigned a0, unsigned a1, auto partc) {
-        constexpr int Q = decltype(partc)::value;
-        const s16x4 h0 = fb_tr<0>(a0), h1 = fb_tr<0>(a1), m0 = fb_tr<Q>(a0), m1 = fb_tr<Q>(a1);
-        return std::array<s16x4, 4>{h0, h1, m0, m1};
-      };
-      auto join = [](const s16x4& a, const s16x4& b) {
-        return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
-      };
-      using QG = std::integral_constant<int, FB_GPART>;
-      using QX = std::integral_constant<int, FB_XPART>;
-      const unsigned ga = fb_lds_addr(gb), xa = fb_lds_addr(xb);
-      const int tr0 = 8 * kg + trq, tr1 = tr0 + 4;
-      auto xrd = [&](int ib) {
-        const int col = 16 * ib + 4 * trp;
-        return read8(xa + fb_off<FB_XP>(tr0, col), xa + fb_off<FB_XP>(tr1, col), QX{});
-      };
-      std::array<s16x4, 4> ra[2], rbx[2];
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        const int col = 32 * wv + 16 * jb + 4 * trp;
-        ra[jb] = read8(ga + gs_off(tr0, col >> 3) + 2 * (col & 7), ga + gs_off(tr1, col >> 3) + 2 * (col & 7), QG{});
-      }
-      rbx[0] = xrd(0);
-      fb_lgkm<4>(ra);
-      f16x8 A[2][2];
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        A[jb][0] = join(ra[jb][0], ra[jb][1]);
-        A[jb][1] = join(ra[jb][2], ra[jb][3]);
-      }
-      if (hf == 0) {
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) dbacc[jb] += (float)A[jb][0][e] + (float)A[jb][1][e];
-      }
-#pragma unroll
-      for (int ib = 0; ib < 8; ++ib) {
-        std::array<s16x4, 4> cur[1] = {rbx[ib & 1]};
-        if (ib + 1 < 8) {
-          rbx[(ib + 1) & 1] = xrd(ib + 1);
-          fb_lgkm<4>(cur);
-        } else {
-          fb_lgkm<0>(cur);
-        }
-        rbx[ib & 1] = cur[0];
-        const f16x8 B0 = join(rbx[ib & 1][0], rbx[ib & 1][1]), B1 = join(rbx[ib & 1][2], rbx[ib & 1][3]);
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B0, aw[jb][ib], 0, 0, 0);
-          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][0], B1, aw[jb][ib], 0, 0, 0);
-          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[jb][1], B0, aw[jb][ib], 0, 0, 0);
-        }
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    {   // epilogue: dL/dy -> BatchNorm L-1 backward -> g_{L-1} (columns 128 hf + il .. + 3 of sample 16 sb + lm)
-      const int il = 16 * wv + 4 * kg;
-      const f32x4 cun = *reinterpret_cast<const f32x4*>(cst + 128 + il);
-      const f32x4 cgm = *reinterpret_cast<const f32x4*>(cst + 256 + il);
-      const f32x4 ckk = *reinterpret_cast<const f32x4*>(cst + 384 + il);
-      const f32x4 cis = *reinterpret_cast<const f32x4*>(cst + 512 + il);
-      const f32x4 cga = *reinterpret_cast<const f32x4*>(cst + 640 + il);
-      const int i = 128 * hf + il;
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        const int sm = 16 * sb + lm;
-        const bool valid = (int64_t)tl * 32 + sm < n;
-        const int o = fb_off<FB_XP>(sm, il);
-        const f16x4 xh = *reinterpret_cast<const f16x4*>(xb + o);
-        const f16x4 xm = *reinterpret_cast<const f16x4*>(xb + FB_XPART + o);
-        f32x4 v;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float d = ad[sb][q] * dun;
-          const float xc = ((float)xh[q] + (float)xm[q]) * cun[q];   // h - mean (hi + mid: 22 bits)
-          v[q] = valid ? ((d - cgm[q]) - xc * ckk[q]) * cis[q] * cga[q] : 0.0f;
-          gmo = fmaxf(gmo, fabsf(v[q]));
-        }
-        if constexpr (GOUT != 1) {
-          f32x4 vs;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) vs[q] = v[q] * gso;
-          s16x4 p0, p1;
-          split2_x4(vs, p0, p1);
-          char* gt = gout + (size_t)tl * GS_TILE + gs_off(sm, i >> 3) + 2 * (i & 7);
-          *reinterpret_cast<s16x4*>(gt) = p0;
-          *reinterpret_cast<s16x4*>(gt + FB_GPART) = p1;
-        }
-        if constexpr (GOUT != 0) {
-          f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tl * TILE_FLOATS) + (i >> 3) * 64 + sm +
-                       32 * ((i >> 2) & 1);
-          __builtin_nontemporal_store(v, dst);
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs of tiles k + 1 / k + 2 (its stores may fly)
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-  };
-  for (int k = 0; k < nk; ++k) tile(k);
-  gmo = wave_max_f(gmo);
-  if (lane == 0) atomicMax(gmax_out + ((bid * 8 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
-  float* pb = part + (size_t)pr * WgradCfg<LAY>::PART;
-#pragma unroll
-  for (int ib = 0; ib < 8; ++ib) {
-    const float cu = cst[128 + 16 * ib + lm] * gun;
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        pb[(size_t)(32 * wv + 16 * jb + 4 * kg + r) * C + COL + 128 * hf + 16 * ib + lm] = aw[jb][ib][r] * cu;
-  }
-  if (hf == 0) {
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb) {
-      float d = dbacc[jb];
-      d += __shfl_xor(d, 16, 64);
-      d += __shfl_xor(d, 32, 64);
-      if (kg == 0) pb[(size_t)256 * C + 32 * wv + 16 * jb + lm] = d * gun;
-    }
-  }
-  __syncthreads();
-  if (red.mode != 0) fb_reduce_row(red, reinterpret_cast<double*>(fb), t);
-}
-
-// k_bwd_remat2<LAY, GOUT>: k_bwd_remat's work (same operands, layouts, scales and outputs) split by ROLE between the
-// two waves of each SIMD (waves w and w + 4 share a SIMD): waves 0-3 ("D") the data gradient of 32 input features
+static_assert(RB_LDS <= 160 * 1024, "k_bwd_remat2 LDS");
+// k_bwd_remat2<LAY, GOUT>: that work split by ROLE between the two waves of each SIMD (waves w and w + 4 share a SIMD): waves 0-3 ("D") the data gradient of 32 input features
 // each (W_L^T rows in registers: 2 row blocks, so every 16-byte g read feeds 6 MFMAs instead of 3) and the BatchNorm
 // backward epilogue with the g_{L-1} stores; waves 4-7 ("W") the rematerialisation of 32 x columns each and the
 // weight gradient of 64 neuron rows each (G's 64 x 128 slice in 128 registers).  Per tile a D wave runs MFMAs then
@@ -4623,14 +4329,6 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                         int ray_stride, const float* z, int n_samples, float eps, const float* grad, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)RB_LDS));
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)RB_LDS));
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat<0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)RB_LDS));
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4642,9 +4340,6 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
     PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
     attr = true;
   }
-  // the role-split kernel (k_bwd_remat2) unless PCNERF_BWD_KERNEL=1 asks for the lockstep one (A/B)
-  const char* bk = getenv("PCNERF_BWD_KERNEL");
-  const bool split_roles = !(bk && bk[0] == '1');
   const double dn = (double)n;
   const int64_t ntiles = (n + 31) / 32;
   const unsigned eg = (unsigned)((ntiles + 3) / 4 < 1024 ? (ntiles + 3) / 4 : 1024);
@@ -4702,17 +4397,10 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                          ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
                          pset[L & 1], red, (const char*)encimg, prow(L - 1), psrow(L - 1));
     };
-    if (split_roles) {
-      if (L == 4) launch(k_bwd_remat2<2, 0>);
-      else if (L == 5) launch(k_bwd_remat2<0, 2>);
-      else if (L == 1) launch(k_bwd_remat2<0, 1>);
-      else launch(k_bwd_remat2<0, 0>);
-    } else {
-      if (L == 4) launch(k_bwd_remat<2, 0>);
-      else if (L == 5) launch(k_bwd_remat<0, 2>);
-      else if (L == 1) launch(k_bwd_remat<0, 1>);
-      else launch(k_bwd_remat<0, 0>);
-    }
+    if (L == 4) launch(k_bwd_remat2<2, 0>);
+    else if (L == 5) launch(k_bwd_remat2<0, 2>);
+    else if (L == 1) launch(k_bwd_remat2<0, 1>);
+    else launch(k_bwd_remat2<0, 0>);
   }
   const unsigned we = (unsigned)std::min<int64_t>(ntiles, WG_BLOCKS);
   float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;

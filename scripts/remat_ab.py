@@ -63,10 +63,8 @@ for n, x, y in zip(names, grads["store"], grads["remat"]):
         worst = max(worst, d)
     print(f"  {n:24s} max|store|={sc:.3e}  max|diff|/max={d:.2e}")
 print(f"worst weight-matrix rel diff {worst:.2e}", flush=True)
-# "remat" = the default kernel (the role-split k_bwd_remat2); "remat1" = the lockstep k_bwd_remat
-for mode in ("store", "remat1", "remat", "store", "remat1", "remat"):
-    os.environ["PCNERF_BWD_KERNEL"] = "1" if mode == "remat1" else "2"
-    _ops.set_train_backward("store" if mode == "store" else "remat")
+for mode in ("store", "remat", "store", "remat"):
+    _ops.set_train_backward(mode)
     mc, mf = models()
     step(mc, mf, 1)
     torch.cuda.synchronize()
