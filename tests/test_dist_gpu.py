@@ -185,3 +185,67 @@ def test_data_parallel_batchnorm_running_stats_rank_independent():
             np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
             if "running" in k or "num_batches" in k:
                 np.testing.assert_array_equal(s0[k], v.cpu().numpy(), err_msg=k)
+
+
+def _fit_rank(rank, world, port, tmp, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "pc-nerf_amd"), here):
+        sys.path.insert(0, p)
+    import train_kitti as T
+    from nof.nof_utils import get_opts
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        root, pose_path = os.path.join(tmp, "pcd"), os.path.join(tmp, "poses.txt")
+        out = os.path.join(tmp, f"run{rank}")
+        args = f"""--datasettype kitti_dataload --root_dir {root} --pose_path {pose_path} --data_start 1150
+         --data_end 1155 --re_loaddata 1 --result_path {out} --N_samples 32 --N_importance 64 --perturb 1
+         --noise_std 0 --chunk 4096 --batch_size 96 --batch_size_val 64 --cloud_size_val 128 --num_epochs 1
+         --optimizer adam --lr 5e-4 --weight_decay 1e-3 --decay_gamma 0.2 --use_child_nerf_divide 0
+         --use_child_nerf_loss 1 --use_segmentated_sample 1 --segmentated_child_nerf_ratio 0.1 --lambda_loss 1
+         --lambda_loss_fine 1 --lambda_child_free_loss 1000000 --lambda_child_depth_loss 100000 --range_delete_x 3
+         --range_delete_y 2 --range_delete_z 1.25 --surface_expand 0.05 --interest_x 20 --interest_y 20
+         --visualize 0 --seed 42"""
+        h = get_opts(args.split())
+        torch.manual_seed(0)
+        system = T.NOFSystem(h)
+        system.prepare_data()
+        h.sub_nerf_test_num = system.train_dataset.sub_nerf_test_num
+        res = T.fit(system, max_steps=3)
+        q.put((rank, res["steps"], [{k: v.cpu().numpy() for k, v in m.state_dict().items()}
+                                    for m in (system.nof_coarse, system.nof_fine)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(280)
+def test_fit_data_parallel_checkpoints_rank_independent(tmp_path):
+    """train_kitti.fit() data parallel over 2 gloo ranks sharing the GPU (3 steps on the KITTI fixture scene, each
+    rank its half of every global batch, BatchNorm chunks of 4096 samples): both ranks end with the same state_dict
+    -- weights (one all_reduce of the gradients, the same Adam step) AND running_mean / running_var /
+    num_batches_tracked (nof.bn_sync replaying both ranks' chunk statistics in global order), so the checkpoint does
+    not depend on which rank writes it."""
+    from test_dataset import write_scene
+    root, pose_path, _ = write_scene(str(tmp_path))
+    assert os.path.samefile(root, os.path.join(str(tmp_path), "pcd"))
+    assert os.path.samefile(pose_path, os.path.join(str(tmp_path), "poses.txt"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_fit_rank, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, steps, sd = q.get(timeout=250)
+        got[r] = (steps, sd)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert got[0][0] == got[1][0] == 3
+    for s0, s1 in zip(got[0][1], got[1][1]):
+        assert s0.keys() == s1.keys()
+        for k in s0:
+            np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
+        nbt = [k for k in s0 if k.endswith("num_batches_tracked")]
+        assert nbt and all(int(s0[k]) > 3 for k in nbt)   # every rank's chunks counted
