@@ -235,9 +235,10 @@ def fit(system, max_steps=0, log_path=None, ckpt_dir=None):
         gb = h.batch_size * world
         ep_loss = []
         for b, s in enumerate(range(0, n, gb)):
-            idx = shard_batch(perm[s:s + gb], rank, world)
-            if idx.numel() == 0:
+            glob = perm[s:s + gb]
+            if glob.numel() < world:   # a rank's shard would be empty: every rank skips it (the collectives below)
                 continue
+            idx = shard_batch(glob, rank, world)
             opt.zero_grad(set_to_none=True)
             if ddp:
                 with bns.record():
