@@ -3881,8 +3881,33 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
     for (int ks = 0; ks < 8; ++ks)
       asm volatile("" ::"v"(wr[ks][0][0]), "v"(wr[ks][0][1]), "v"(wr[ks][1][0]), "v"(wr[ks][1][1]));
     float gmo = 0.0f;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 pcell[2][2] = {{u32x4{}, u32x4{}}, {u32x4{}, u32x4{}}};
+    f32x4 pv32[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+    // a cell's g_{L-1} stores (tile tq): the split pair as one 16-byte cell, and / or the fp32 value
+    auto store_cell = [&](int rb, int sb, int tq, const u32x4& cell, const f32x4& v) {
+      const int il = 32 * rw + 16 * rb + 4 * kg, i = 128 * hf + il, sm = 16 * sb + lm;
+      if constexpr (GOUT != 1) {
+        char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
+#if PCN_RB_NOSTORE
+        if (cell[0] == 12345u && cell[3] == 4321u)
+#endif
+        __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));   // streaming: keep L2 for the g / encoding tiles the other half re-reads
+      }
+      if constexpr (GOUT != 0) {
+        f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tq * TILE_FLOATS) + (i >> 3) * 64 + sm +
+                     32 * ((i >> 2) & 1);
+        __builtin_nontemporal_store(v, dst);
+      }
+    };
+    // tile k's g_{L-1} cells are stored during tile k + 1's data-gradient MFMAs, one cell after every second k-step
+    // (pinned there by scheduling barriers: left to the scheduler they sink to the phase's end), so the D waves'
+    // stores do not meet every CU's at the epilogue: -1.6 % per launch (profiles/r05_variants_remat2_defer.txt)
+    // (tile 0: zero cells to tile 0's own slots, rewritten by this wave's later stores of its real cells -- same
+    // addresses, program order; they also keep NST stores behind every tile's DMAs for the vmcnt(NST) below)
     for (int k = 0; k < nk; ++k) {
       const int tl = pr + k * npair;
+      const int ptl = k > 0 ? tl - npair : tl;
 #if !PCN_RB_NODMA
       if (k + 1 < nk) dma_g(k + 1);
       if (k + 2 < nk) dma_enc(k + 2);
@@ -3907,6 +3932,11 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
             ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][1], bh, ad[rb][sb], 0, 0, 0);
 #endif
           }
+          if ((ks & 1) && sb == 1) {
+            store_cell((ks >> 2) & 1, (ks >> 1) & 1, ptl, pcell[(ks >> 2) & 1][(ks >> 1) & 1],
+                       pv32[(ks >> 2) & 1][(ks >> 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
@@ -3914,7 +3944,6 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
         const f32x4 cA = *reinterpret_cast<const f32x4*>(cst + 640 + il);
         const f32x4 cB = *reinterpret_cast<const f32x4*>(cst + 256 + il);
         const f32x4 cC = *reinterpret_cast<const f32x4*>(cst + 384 + il);
-        const int i = 128 * hf + il;
 #pragma unroll
         for (int sb = 0; sb < 2; ++sb) {
           const int sm = 16 * sb + lm;
@@ -3929,6 +3958,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
             vs[q] = valid ? fmaf(-xs, cC[q], fmaf(ad[rb][sb][q], cA[q], -cB[q])) : 0.0f;
             gmo = fmaxf(gmo, fabsf(vs[q]));
           }
+          u32x4 cell = {};
           if constexpr (GOUT != 1) {
             s16x4 p0, p1;
             split2_x4(vs, p0, p1);
@@ -3938,22 +3968,15 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
             const fb_i32x2 hv = __builtin_bit_cast(fb_i32x2, p0), mv = __builtin_bit_cast(fb_i32x2, p1);
             const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
             const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
-            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 cell = {s0[0], s1[0], s0[1], s1[1]};
-            char* gt = gout + (size_t)tl * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
-#if PCN_RB_NOSTORE
-            if (cell[0] == 12345u && cell[3] == 4321u)
-#endif
-            __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));   // streaming: keep L2 for the g / encoding tiles the other half re-reads
+            cell = u32x4{s0[0], s1[0], s0[1], s1[1]};
           }
+          f32x4 v = {};
           if constexpr (GOUT != 0) {
-            f32x4 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = vs[q] * gui;   // exact: a power of two
-            f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tl * TILE_FLOATS) + (i >> 3) * 64 + sm +
-                         32 * ((i >> 2) & 1);
-            __builtin_nontemporal_store(v, dst);
           }
+          pcell[rb][sb] = cell;
+          pv32[rb][sb] = v;
         }
       }
 #if !PCN_RB_NOWAIT
@@ -3961,6 +3984,12 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #endif
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_s_barrier();
+    }
+    if (nk > 0) {   // the last tile's cells
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) store_cell(rb, sb, pr + (nk - 1) * npair, pcell[rb][sb], pv32[rb][sb]);
     }
     gmo = wave_max_f(gmo) * gui;
     if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rw) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
