@@ -40,6 +40,17 @@ constexpr int H1_XD = H_XD;      // k_train_h1's B-operand read ring depth
 // blocks later), the block of the first staging piece, the blocks between staging pieces
 constexpr int WB3_AREAD = 3, WB3_STAGE = 0, WB3_SPACE = 2;
 
+#ifndef PCN_RB_CLK
+#define PCN_RB_CLK 0   // diagnostic builds: per-wave shader cycles of the layer-2 launch's phases (pcnerf_debug_rbclk)
+#endif
+#if PCN_RB_CLK
+// [block * 8 + wave]: cycles summed over the tiles of: phase A (D: data-gradient MFMAs; W: remat), phase B (D:
+// epilogue; W: weight-gradient MFMAs), the end-of-tile wait + barrier; the loop; the tile count
+__device__ unsigned long long g_rbclk[4096][5];
+#define RB_T(v) do { __builtin_amdgcn_sched_barrier(0); v = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define RB_T(v) do { } while (0)
+#endif
 #ifndef PCN_CLOCK_STAMP
 #define PCN_CLOCK_STAMP 0  // diagnostic builds only: phase stamps of 1 k_train_ws, 2 k_wgrad (pcnerf_debug_clock)
 #endif
@@ -1442,6 +1453,12 @@ static void pack_weights(const NofParamsDev& P, float* wp, f16x8* wh, int* sw, h
   }
 }
 }  // namespace pcn
+
+#if PCN_RB_CLK
+extern "C" int pcnerf_debug_rbclk(unsigned long long* out) {   // out: [4096][5] (g_rbclk)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pcn::g_rbclk), sizeof(pcn::g_rbclk)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 #if PCN_CLOCK_STAMP
 // diagnostic builds: median over workgroups of the last hidden-layer launch's in-kernel clock (MHz) and cycles
@@ -3905,9 +3922,12 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
     // stores do not meet every CU's at the epilogue: -1.6 % per launch (profiles/r05_variants_remat2_defer.txt)
     // (tile 0: zero cells to tile 0's own slots, rewritten by this wave's later stores of its real cells -- same
     // addresses, program order; they also keep NST stores behind every tile's DMAs for the vmcnt(NST) below)
+    [[maybe_unused]] unsigned long long ck0 = 0, ck1 = 0, ck2 = 0, ck3 = 0, cA = 0, cB = 0, cW = 0, cL0 = 0, cL1 = 0;
+    RB_T(cL0);
     for (int k = 0; k < nk; ++k) {
       const int tl = pr + k * npair;
       const int ptl = k > 0 ? tl - npair : tl;
+      RB_T(ck0);
 #if !PCN_RB_NODMA
       if (k + 1 < nk) dma_g(k + 1);
       if (k + 2 < nk) dma_enc(k + 2);
@@ -3938,6 +3958,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
             __builtin_amdgcn_sched_barrier(0);
           }
         }
+      RB_T(ck1);
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
         const int il = 32 * rw + 16 * rb + 4 * kg;
@@ -3979,12 +4000,24 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
           pv32[rb][sb] = v;
         }
       }
+      RB_T(ck2);
 #if !PCN_RB_NOWAIT
       __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs (its stores may fly)
 #endif
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_s_barrier();
+      RB_T(ck3);
+      cA += ck1 - ck0;
+      cB += ck2 - ck1;
+      cW += ck3 - ck2;
     }
+    RB_T(cL1);
+#if PCN_RB_CLK
+    if (layer == 2 && lane == 0 && bid < 512) {
+      unsigned long long* g = g_rbclk[bid * 8 + wv];
+      g[0] = cA; g[1] = cB; g[2] = cW; g[3] = cL1 - cL0; g[4] = (unsigned long long)nk;
+    }
+#endif
     if (nk > 0) {   // the last tile's cells
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
@@ -4001,7 +4034,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #pragma unroll
       for (int ib = 0; ib < 8; ++ib) aw[jb][ib] = f32x4{};
     const int trq = lm >> 2, trp = lm & 3;
+    [[maybe_unused]] unsigned long long ck0 = 0, ck1 = 0, ck2 = 0, ck3 = 0, cA = 0, cB = 0, cW = 0, cL0 = 0, cL1 = 0;
+    RB_T(cL0);
     for (int k = 0; k < nk; ++k) {
+      RB_T(ck0);
 #if !PCN_RB_NODMA
       if (k + 1 < nk) dma_g(k + 1);
       if (k + 2 < nk) dma_enc(k + 2);
@@ -4009,6 +4045,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #if !PCN_RB_NORM
       if (k + 1 < nk) remat_x(k + 1);
 #endif
+      RB_T(ck1);
       const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
       auto read8 = [&](unsigned a0, unsigned a1, auto partc) {
         constexpr int Q = decltype(partc)::value;
@@ -4062,12 +4099,24 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #endif
         }
       }
+      RB_T(ck2);
 #if !PCN_RB_NOWAIT
       __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
 #endif
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_s_barrier();
+      RB_T(ck3);
+      cA += ck1 - ck0;
+      cB += ck2 - ck1;
+      cW += ck3 - ck2;
     }
+    RB_T(cL1);
+#if PCN_RB_CLK
+    if (layer == 2 && lane == 0 && bid < 512) {
+      unsigned long long* g = g_rbclk[bid * 8 + wv];
+      g[0] = cA; g[1] = cB; g[2] = cW; g[3] = cL1 - cL0; g[4] = (unsigned long long)nk;
+    }
+#endif
     float* pb = part + (size_t)pr * WgradCfg<LAY>::PART;
 #pragma unroll
     for (int ib = 0; ib < 8; ++ib) {
