@@ -24,8 +24,11 @@ static hipEvent_t get_event() {
     g_pool.pop_back();
     return e;
   }
+  // timing-only events (read by hipEventElapsedTime after a device synchronise): no system-scope fence, whose L2
+  // writeback + invalidate at every record put ~10 us between the instrumented step's kernels (and a cold L2 in
+  // front of each), where the uninstrumented steps run them back to back
   hipEvent_t e;
-  PCN_HIP(hipEventCreate(&e));
+  PCN_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   return e;
 }
 
