@@ -622,10 +622,11 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
     knames = {0: "k_nof_eval_h3<false,false>" if esplit else "k_nof_eval", 1: hid, 2: f"k_train_h<8,false,{nterm}>" if split else "k_train_ws<8,false>",
               3: f"k_train_h<8,true,{nterm}>" if split else "k_train_ws<8,true>",
               10: "k_wgrad<2>+k_wgrad<1>" if split else "k_wgrad<0>", 11: f"k_dgrad_h<{nterm}>" if split else "k_dgrad_ws",
-              # (the fused / remat backward: MODE 3, the encoding columns of layers 0 and 4 in one pass; the layered
-              # split backward launches several modes, named by its hidden-layer one)
+              # (the encoding columns of layers 0 and 4: k_wgrad_enc in the remat backward, k_wgrad_b3 MODE 3 in the
+              # store backward; the layered split backward launches several modes, named by its hidden-layer one)
               13: "k_nof_eval_fold", 15: f"k_train_h1<{nterm}>",
-              14: f"k_wgrad_b3<1,3,1,true,{nterm}>" if train_math == "f16x2_3_fused" else f"k_wgrad_b3<1,0,0,true,{nterm}>",
+              14: ("k_wgrad_enc" if remat else f"k_wgrad_b3<1,3,1,true,{nterm}>") if train_math == "f16x2_3_fused"
+              else f"k_wgrad_b3<1,0,0,true,{nterm}>",
               16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw",
               # (the train query writing the activation store is its own instantiation)
               18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" and not remat else "k_nof_eval_h3<true,false>",

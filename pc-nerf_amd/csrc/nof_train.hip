@@ -40,6 +40,12 @@ constexpr int H1_XD = H_XD;      // k_train_h1's B-operand read ring depth
 // blocks later), the block of the first staging piece, the blocks between staging pieces
 constexpr int WB3_AREAD = 3, WB3_STAGE = 0, WB3_SPACE = 2;
 
+#ifndef PCN_RB_DEPI
+#define PCN_RB_DEPI 0   // A/B switch: the D waves' epilogue of tile k runs between tile k + 1's data-gradient MFMAs
+#endif
+#ifndef PCN_RB_RPRIO
+#define PCN_RB_RPRIO 0   // A/B switch: the W waves' remat phase at raised wave priority
+#endif
 #ifndef PCN_RB_CLK
 #define PCN_RB_CLK 0   // diagnostic builds: per-wave shader cycles of the layer-2 launch's phases (pcnerf_debug_rbclk)
 #endif
@@ -3899,8 +3905,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
       asm volatile("" ::"v"(wr[ks][0][0]), "v"(wr[ks][0][1]), "v"(wr[ks][1][0]), "v"(wr[ks][1][1]));
     float gmo = 0.0f;
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#if !PCN_RB_DEPI
     u32x4 pcell[2][2] = {{u32x4{}, u32x4{}}, {u32x4{}, u32x4{}}};
     f32x4 pv32[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+#endif
     // a cell's g_{L-1} stores (tile tq): the split pair as one 16-byte cell, and / or the fp32 value
     auto store_cell = [&](int rb, int sb, int tq, const u32x4& cell, const f32x4& v) {
       const int il = 32 * rw + 16 * rb + 4 * kg, i = 128 * hf + il, sm = 16 * sb + lm;
@@ -3924,6 +3932,111 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
     // addresses, program order; they also keep NST stores behind every tile's DMAs for the vmcnt(NST) below)
     [[maybe_unused]] unsigned long long ck0 = 0, ck1 = 0, ck2 = 0, ck3 = 0, cA = 0, cB = 0, cW = 0, cL0 = 0, cL1 = 0;
     RB_T(cL0);
+#if PCN_RB_DEPI
+    // tile k's BatchNorm-backward epilogue runs between tile k + 1's data-gradient MFMAs, one cell after every
+    // second k-step (pinned by scheduling barriers), from its accumulators and x values kept in registers across
+    // the barrier (x: the buffer is rewritten by the W waves' remat of tile k + 2 during tile k + 1); tile 0's pass
+    // stores zero cells (no valid sample) to tile 0's own slots, rewritten in program order by its real cells --
+    // and keeps NST stores behind every tile's DMAs for the vmcnt(NST) below
+    f32x4 adp[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+    f16x4 xhp[2][2] = {}, xmp[2][2] = {};
+    auto epi_cell = [&](int rb, int sb, int tq, bool have) {
+      const int il = 32 * rw + 16 * rb + 4 * kg, sm = 16 * sb + lm;
+      const f32x4 cA = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+      const f32x4 cB = *reinterpret_cast<const f32x4*>(cst + 256 + il);
+      const f32x4 cC = *reinterpret_cast<const f32x4*>(cst + 384 + il);
+      const bool valid = have && (int64_t)tq * 32 + sm < n;
+      f32x4 vs;   // 2^eo g_{L-1}
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float xs = (float)xhp[rb][sb][q] + (float)xmp[rb][sb][q];   // exact: the split's two parts
+        vs[q] = valid ? fmaf(-xs, cC[q], fmaf(adp[rb][sb][q], cA[q], -cB[q])) : 0.0f;
+        gmo = fmaxf(gmo, fabsf(vs[q]));
+      }
+      const int i = 128 * hf + il;
+      if constexpr (GOUT != 1) {
+        s16x4 p0, p1;
+        split2_x4(vs, p0, p1);
+        const fb_i32x2 hv = __builtin_bit_cast(fb_i32x2, p0), mv = __builtin_bit_cast(fb_i32x2, p1);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
+        const u32x4 cell = {s0[0], s1[0], s0[1], s1[1]};
+        char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
+        __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));
+      }
+      if constexpr (GOUT != 0) {
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = vs[q] * gui;   // exact: a power of two
+        f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tq * TILE_FLOATS) + (i >> 3) * 64 + sm +
+                     32 * ((i >> 2) & 1);
+        __builtin_nontemporal_store(v, dst);
+      }
+    };
+    for (int k = 0; k < nk; ++k) {
+      const int tl = pr + k * npair;
+      const int ptl = k > 0 ? tl - npair : tl;
+      RB_T(ck0);
+#if !PCN_RB_NODMA
+      if (k + 1 < nk) dma_g(k + 1);
+      if (k + 2 < nk) dma_enc(k + 2);
+#endif
+      const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
+      const char* xb = sp + 2 * FB_GPART;
+      f32x4 ad[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) {
+          const int o = gs_off(16 * sb + lm, 4 * ks + kg);
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(sp + o);
+          const f16x8 bm = *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bh, ad[rb][sb], 0, 0, 0);
+            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bm, ad[rb][sb], 0, 0, 0);
+            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][1], bh, ad[rb][sb], 0, 0, 0);
+          }
+          if ((ks & 1) && sb == 1) {
+            epi_cell((ks >> 2) & 1, (ks >> 1) & 1, ptl, k > 0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      RB_T(ck1);
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) {
+          const int o = fb_off<FB_XP>(16 * sb + lm, 32 * rw + 16 * rb + 4 * kg);
+          xhp[rb][sb] = *reinterpret_cast<const f16x4*>(xb + o);
+          xmp[rb][sb] = *reinterpret_cast<const f16x4*>(xb + FB_XPART + o);
+          adp[rb][sb] = ad[rb][sb];
+        }
+      RB_T(ck2);
+#if !PCN_RB_NOWAIT
+      __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs (its stores may fly)
+#endif
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+      RB_T(ck3);
+      cA += ck1 - ck0;
+      cB += ck2 - ck1;
+      cW += ck3 - ck2;
+    }
+    RB_T(cL1);
+#if PCN_RB_CLK
+    if (layer == 2 && lane == 0 && bid < 512) {
+      unsigned long long* g = g_rbclk[bid * 8 + wv];
+      g[0] = cA; g[1] = cB; g[2] = cW; g[3] = cL1 - cL0; g[4] = (unsigned long long)nk;
+    }
+#endif
+    if (nk > 0) {   // the last tile's epilogue
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) epi_cell(rb, sb, pr + (nk - 1) * npair, true);
+    }
+#else
     for (int k = 0; k < nk; ++k) {
       const int tl = pr + k * npair;
       const int ptl = k > 0 ? tl - npair : tl;
@@ -4024,6 +4137,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #pragma unroll
         for (int sb = 0; sb < 2; ++sb) store_cell(rb, sb, pr + (nk - 1) * npair, pcell[rb][sb], pv32[rb][sb]);
     }
+#endif
     gmo = wave_max_f(gmo) * gui;
     if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rw) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
   } else {
@@ -4042,9 +4156,11 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
       if (k + 1 < nk) dma_g(k + 1);
       if (k + 2 < nk) dma_enc(k + 2);
 #endif
+      if (PCN_RB_RPRIO) __builtin_amdgcn_s_setprio(PCN_RB_RPRIO);
 #if !PCN_RB_NORM
       if (k + 1 < nk) remat_x(k + 1);
 #endif
+      if (PCN_RB_RPRIO) __builtin_amdgcn_s_setprio(0);
       RB_T(ck1);
       const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
       auto read8 = [&](unsigned a0, unsigned a1, auto partc) {
@@ -4137,6 +4253,108 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
   }
   __syncthreads();
   if (red.mode != 0) fb_reduce_row(red, reinterpret_cast<double*>(fb), t);
+}
+
+// k_wgrad_enc: the encoding columns of dW_0 and of the skip layer's dW_4, G = sum_s g (x) d, from the PRE-SPLIT g_0 and
+// g_4 images (k_bwd_remat2's output layout, gs_off) and the chunk's encoding image (k_remat_enc: d = e - ebar, fb_eoff),
+// all three DMA'd straight into LDS (72 KiB per tile, double-buffered) -- no sincos, no conversion.  d in place of e:
+// sum_s g_L = 0 exactly (BatchNorm follows both Linears), so sum g (x) e = sum g (x) d; the layer-0 bias gradient
+// sum_s g_0 is that exact 0.  8 waves: 0-3 on g_0, 4-7 on g_4, each 64 rows (4 x 16) x the 64 columns (4 x 16) in
+// 64 registers; per tile and wave 32 transposed reads (ds_read_b64_tr_b16) and 48 v_mfma_f32_16x16x32_f16 (hi.hi +
+// hi.mid + mid.hi).  Partials per workgroup in k_wgrad<1>'s layout, unscaled (2^-gexp of the image, 2^-s of the
+// column), summed by k_fb_reduce_tail.  HBM per sample: 2 KiB of g + 256 B of encoding.
+constexpr size_t WE_BUF = 2 * (size_t)GS_TILE + FB_ENC;
+constexpr size_t WE_LDS = 2 * WE_BUF;
+static_assert(WE_LDS <= 160 * 1024, "k_wgrad_enc LDS");
+__global__ __launch_bounds__(512, 1) void k_wgrad_enc(const char* __restrict__ g0, const char* __restrict__ g4,
+                                                      const char* __restrict__ enc, int64_t n,
+                                                      const int* __restrict__ gexp, const unsigned* __restrict__ pbound,
+                                                      float* __restrict__ part0, float* __restrict__ part4) {
+  extern __shared__ __attribute__((aligned(16))) char wel[];
+  const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6), src = wv >> 2, rw = wv & 3;
+  const int nt = (int)((n + 31) / 32), blk = (int)blockIdx.x, gstride = (int)gridDim.x;
+  const int nk = blk < nt ? (nt - 1 - blk) / gstride + 1 : 0;
+  // one tile: 72 pieces of 1 KiB (g_0 0..31, g_4 32..63, encoding 64..71), 9 per wave, into buffer k & 1
+  auto dma = [&](int k) {
+    const size_t tl = (size_t)(blk + k * gstride);
+    char* const b = wel + (size_t)(k & 1) * WE_BUF;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int p = 9 * wv + i;
+      const char* gsrc = p < 32 ? g0 + tl * GS_TILE + p * 1024
+                         : p < 64 ? g4 + tl * GS_TILE + (p - 32) * 1024
+                                  : enc + tl * FB_ENC + (p - 64) * 1024;
+      fb_glds16(gsrc + 16 * ln, b + p * 1024);
+    }
+  };
+  // the encoding image's element (sample r, column c): row r, 16-byte chunk (c >> 3) ^ ((r >> 1) & 7)
+  auto eoff = [](int r, int c) { return r * 128 + 16 * ((c >> 3) ^ ((r >> 1) & 7)) + 2 * (c & 7); };
+  auto join = [](const s16x4& a, const s16x4& b) {
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  f32x4 aw[4][4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib) aw[jb][ib] = f32x4{};
+  const int trq = lm >> 2, trp = lm & 3, tr0 = 8 * kg + trq, tr1 = tr0 + 4;
+  if (nk > 0) dma(0);
+  __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+  __builtin_amdgcn_s_barrier();
+  for (int k = 0; k < nk; ++k) {
+    if (k + 1 < nk) dma(k + 1);
+    const char* const b = wel + (size_t)(k & 1) * WE_BUF;
+    const unsigned ga = fb_lds_addr(b + src * GS_TILE), ea = fb_lds_addr(b + 2 * GS_TILE);
+    std::array<s16x4, 4> ra[4], rx[4];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      const int col = 64 * rw + 16 * jb + 4 * trp;
+      const unsigned a0 = ga + gs_off(tr0, col >> 3) + 2 * (col & 7), a1 = ga + gs_off(tr1, col >> 3) + 2 * (col & 7);
+      ra[jb] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_GPART>(a0), fb_tr<FB_GPART>(a1)};
+    }
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib) {
+      const int c = 16 * ib + 4 * trp;
+      const unsigned a0 = ea + eoff(tr0, c), a1 = ea + eoff(tr1, c);
+      rx[ib] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_ENC / 2>(a0), fb_tr<FB_ENC / 2>(a1)};
+    }
+    fb_lgkm<0>(ra);
+    fb_lgkm<0>(rx);
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib) {
+      const f16x8 B0 = join(rx[ib][0], rx[ib][1]), B1 = join(rx[ib][2], rx[ib][3]);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const f16x8 A0 = join(ra[jb][0], ra[jb][1]), A1 = join(ra[jb][2], ra[jb][3]);
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0, aw[jb][ib], 0, 0, 0);
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1, aw[jb][ib], 0, 0, 0);
+        aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0, aw[jb][ib], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));   // this wave's DMA of tile k + 1
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();              // every wave's DMA landed; buffer k & 1 read by all
+  }
+  constexpr int C = WgradCfg<1>::C;
+  float* const pb = (src == 0 ? part0 : part4) + (size_t)blk * WgradCfg<1>::PART;
+  const float gu = ldexpf(1.0f, -gexp[src == 0 ? 0 : 4]);
+  const int sxyz = remat_sx(0, __uint_as_float(*pbound));
+#pragma unroll
+  for (int ib = 0; ib < 4; ++ib) {
+    const int col = 16 * ib + lm;
+    const float cu = ldexpf(gu, -(col < 3 ? sxyz : 13));
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pb[(size_t)(64 * rw + 16 * jb + 4 * kg + r) * C + col] = aw[jb][ib][r] * cu;
+  }
+  if (kg == 0) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) pb[(size_t)256 * C + 64 * rw + 16 * jb + lm] = 0.0f;
+  }
 }
 
 struct GradTable {
@@ -4398,10 +4616,10 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
 }
 
 // One chunk through the rematerialised backward (no activation store): max |dL/dlogit|, k_fb_prep on the fold's
-// statistics, the chunk's encoding image, g_7 (k_g7), layers 7..1 each in ONE k_bwd_remat launch, the encoding
-// columns of layers 0 and 4 (k_wgrad_b3 MODE 3 on g_0 and g_4 as fp32 tiles), the last partial sums.  g buffers:
-// pre-split images S0 / S1 alternate (g_7, g_5, g_3, g_1 in S0; g_6, g_4, g_2 in S1), g_4 also as fp32 tiles (F4)
-// and g_0 only as fp32 tiles (F0).
+// statistics, the chunk's encoding image, g_7 (k_g7), layers 7..1 each in ONE k_bwd_remat2 launch, the encoding
+// columns of layers 0 and 4 (k_wgrad_enc on the pre-split g_0 and g_4 and the encoding image), the last partial sums.
+// g buffers, all pre-split: S0 / S1 alternate (g_7, g_5, g_3, g_1 in S0; g_6, g_2, g_0 in S1), g_4 in S2 (kept to
+// the end for k_wgrad_enc).
 static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs& ws, const FoldBnBwd& FB,
                         const f16x8* pimg, const float* pscl, int64_t ci, int64_t c0, int64_t n, const float* rays,
                         int ray_stride, const float* z, int n_samples, float eps, const float* grad, hipStream_t s) {
@@ -4409,13 +4627,10 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   if (!attr) {
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)RB_LDS));
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_enc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WE_LDS));
     attr = true;
   }
   const double dn = (double)n;
@@ -4439,8 +4654,7 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   auto prow = [&](int L) { return pimg + ((size_t)L * C + ci) * 256 * 16; };
   auto psrow = [&](int L) { return pscl + ((size_t)L * C + ci) * 256; };
   char* const S[2] = {reinterpret_cast<char*>(ws.h[0]), reinterpret_cast<char*>(ws.h[1])};
-  float* const F4 = ws.h[2];
-  float* const F0 = ws.h[3];
+  char* const S2 = reinterpret_cast<char*>(ws.h[2]);
   {
     // the encoding (30 sincosf per sample): 4 B of z in, 256 B of image out per sample
     ProfScope ps(s, PT_BWD_REMAT, 0.0, (4.0 + 256.0) * dn);
@@ -4461,33 +4675,29 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
     FbRed red{nullptr, nullptr, nullptr, nullptr, 0};
     if (L < 7)
       red = FbRed{pset[(L + 1) & 1], ws.coef + 1024 * L, ws.gacc + G.w[L + 1], ws.gacc + G.b[L + 1], L + 1 == 4 ? 2 : 1};
-    const char* gin = S[(7 - L) & 1];
-    char* gout = S[(8 - L) & 1];
-    float* g32 = L == 5 ? F4 : L == 1 ? F0 : nullptr;
+    const char* gin = L == 4 ? S2 : S[(7 - L) & 1];
+    char* gout = L == 5 ? S2 : S[(8 - L) & 1];
     const unsigned* gmin = L == 7 ? ws.gm7 : ws.gmax + L * GMAX_SLOTS;
     // algorithmic work: data and weight gradient (2 x 2 x 256 x 256) + the input's rematerialisation (2 x 256 x 64);
-    // bytes: g_L in (1 KiB), the encoding image (256 B), g_{L-1} out (1 KiB; 2 KiB for the layer writing both)
-    ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0 + 2.0 * 256.0 * 64.0) * dn,
-                 (1024.0 + 256.0 + (L == 5 ? 2048.0 : 1024.0)) * dn);
+    // bytes: g_L in (1 KiB), the encoding image (256 B), g_{L-1} out (1 KiB)
+    ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0 + 2.0 * 256.0 * 64.0) * dn, (1024.0 + 256.0 + 1024.0) * dn);
     auto launch = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), RB_LDS, s, gin, gout, g32, ws.wth16 + (size_t)(L - 1) * HW_H,
+      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), RB_LDS, s, gin, gout, (float*)nullptr, ws.wth16 + (size_t)(L - 1) * HW_H,
                          (const int*)ws.sw, L, n, coefp, (const float*)(ws.bnb + 512 * (L - 1)), P.bn_w[L - 1],
                          ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
                          pset[L & 1], red, (const char*)encimg, prow(L - 1), psrow(L - 1));
     };
     if (L == 4) launch(k_bwd_remat2<2, 0>);
-    else if (L == 5) launch(k_bwd_remat2<0, 2>);
-    else if (L == 1) launch(k_bwd_remat2<0, 1>);
     else launch(k_bwd_remat2<0, 0>);
   }
   const unsigned we = (unsigned)std::min<int64_t>(ntiles, WG_BLOCKS);
   float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
   float* const part_e4 = part_e0 + (size_t)WG_BLOCKS * WgradCfg<1>::PART;
   {
-    ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 2.0 * 256.0 * 64 * dn, 2048.0 * dn);
-    launch_wgrad_b3_one<3, 1, true, 3>(we, s, rays, ray_stride, z, n_samples, c0, n, nullptr, F0, nullptr, nullptr,
-                                       ws.gmax + 0 * GMAX_SLOTS, part_e0, ws.pbound, F4, ws.gmax + 4 * GMAX_SLOTS,
-                                       part_e4);
+    // 2 x 2 x 256 x 64 fp32-FLOP per sample; 2 KiB of g + 256 B of encoding in
+    ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 2.0 * 256.0 * 64 * dn, (2048.0 + 256.0) * dn);
+    hipLaunchKernelGGL(k_wgrad_enc, dim3(we), dim3(512), WE_LDS, s, (const char*)S[1], (const char*)S2,
+                       (const char*)encimg, n, (const int*)ws.gexp, (const unsigned*)ws.pbound, part_e0, part_e4);
   }
   // the partial sums read (k_fb_reduce_tail): layer 1's pair partials and the two encoding-column sets
   ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0 + 2.0 * we * WgradCfg<1>::PART * 4.0);
