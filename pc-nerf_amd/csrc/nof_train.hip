@@ -4257,61 +4257,74 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 
 // k_wgrad_enc: the encoding columns of dW_0 and of the skip layer's dW_4, G = sum_s g (x) d, from the PRE-SPLIT g_0 and
 // g_4 images (k_bwd_remat2's output layout, gs_off) and the chunk's encoding image (k_remat_enc: d = e - ebar, fb_eoff),
-// all three DMA'd straight into LDS (72 KiB per tile, double-buffered) -- no sincos, no conversion.  d in place of e:
-// sum_s g_L = 0 exactly (BatchNorm follows both Linears), so sum g (x) e = sum g (x) d; the layer-0 bias gradient
-// sum_s g_0 is that exact 0.  8 waves: 0-3 on g_0, 4-7 on g_4, each 64 rows (4 x 16) x the 64 columns (4 x 16) in
-// 64 registers; per tile and wave 32 transposed reads (ds_read_b64_tr_b16) and 48 v_mfma_f32_16x16x32_f16 (hi.hi +
-// hi.mid + mid.hi).  Partials per workgroup in k_wgrad<1>'s layout, unscaled (2^-gexp of the image, 2^-s of the
-// column), summed by k_fb_reduce_tail.  HBM per sample: 2 KiB of g + 256 B of encoding.
-constexpr size_t WE_BUF = 2 * (size_t)GS_TILE + FB_ENC;
-constexpr size_t WE_LDS = 2 * WE_BUF;
+// DMA'd straight into LDS -- no sincos, no conversion.  d in place of e: sum_s g_L = 0 exactly (BatchNorm follows
+// both Linears), so sum g (x) e = sum g (x) d; the layer-0 bias gradient sum_s g_0 is that exact 0.  The two sources
+// split between the workgroups of a pair (blocks b and b + 8: the same XCD, so the encoding tile's second read is an
+// L2 hit): 40 KiB per tile (one g image + the encoding), a ring of three slots, DMA two tiles ahead (-5 % against
+// one workgroup taking both sources at 72 KiB per tile, double-buffered; four slots: no change;
+// profiles/r05_wgrad_enc_ab.txt).  8 waves x 32 rows (2 x 16) x the 64 columns in 32 registers; per tile and wave
+// 24 transposed reads (ds_read_b64_tr_b16) and 24 v_mfma_f32_16x16x32_f16 (hi.hi + hi.mid + mid.hi).  Partials in
+// k_wgrad<1>'s layout, one set per pair and source, unscaled (2^-gexp of the image, 2^-s of the column), summed by
+// k_fb_reduce_tail.  HBM per sample: 2 KiB of g + 256 B of encoding.
+constexpr int WE_SLOTS = 3, WE_AHEAD = WE_SLOTS - 1;
+constexpr size_t WE_BUF = (size_t)GS_TILE + FB_ENC;
+constexpr size_t WE_LDS = WE_SLOTS * WE_BUF;
 static_assert(WE_LDS <= 160 * 1024, "k_wgrad_enc LDS");
 __global__ __launch_bounds__(512, 1) void k_wgrad_enc(const char* __restrict__ g0, const char* __restrict__ g4,
-                                                      const char* __restrict__ enc, int64_t n,
-                                                      const int* __restrict__ gexp, const unsigned* __restrict__ pbound,
-                                                      float* __restrict__ part0, float* __restrict__ part4) {
+                                                       const char* __restrict__ enc, int64_t n,
+                                                       const int* __restrict__ gexp, const unsigned* __restrict__ pbound,
+                                                       float* __restrict__ part0, float* __restrict__ part4) {
   extern __shared__ __attribute__((aligned(16))) char wel[];
   const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6), src = wv >> 2, rw = wv & 3;
-  const int nt = (int)((n + 31) / 32), blk = (int)blockIdx.x, gstride = (int)gridDim.x;
-  const int nk = blk < nt ? (nt - 1 - blk) / gstride + 1 : 0;
-  // one tile: 72 pieces of 1 KiB (g_0 0..31, g_4 32..63, encoding 64..71), 9 per wave, into buffer k & 1
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int bid = (int)blockIdx.x, src = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
+  const int npair = (int)gridDim.x >> 1;
+  const int nt = (int)((n + 31) / 32);
+  const int nk = pr < nt ? (nt - 1 - pr) / npair + 1 : 0;
+  const char* const gsrc = src == 0 ? g0 : g4;
+  // one tile: 40 pieces of 1 KiB (g 0..31, encoding 32..39), 5 per wave, into slot k % 3
   auto dma = [&](int k) {
-    const size_t tl = (size_t)(blk + k * gstride);
-    char* const b = wel + (size_t)(k & 1) * WE_BUF;
+    const size_t tl = (size_t)(pr + k * npair);
+    char* const b = wel + (size_t)(k % WE_SLOTS) * WE_BUF;
     int ln = lane;
     asm volatile("" : "+v"(ln));
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int p = 9 * wv + i;
-      const char* gsrc = p < 32 ? g0 + tl * GS_TILE + p * 1024
-                         : p < 64 ? g4 + tl * GS_TILE + (p - 32) * 1024
-                                  : enc + tl * FB_ENC + (p - 64) * 1024;
-      fb_glds16(gsrc + 16 * ln, b + p * 1024);
+    for (int i = 0; i < 5; ++i) {
+      const int p = 5 * wv + i;
+      const char* a = p < 32 ? gsrc + tl * GS_TILE + p * 1024 : enc + tl * FB_ENC + (p - 32) * 1024;
+      fb_glds16(a + 16 * ln, b + p * 1024);
     }
   };
-  // the encoding image's element (sample r, column c): row r, 16-byte chunk (c >> 3) ^ ((r >> 1) & 7)
   auto eoff = [](int r, int c) { return r * 128 + 16 * ((c >> 3) ^ ((r >> 1) & 7)) + 2 * (c & 7); };
   auto join = [](const s16x4& a, const s16x4& b) {
     return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
   };
-  f32x4 aw[4][4];
+  f32x4 aw[2][4];
 #pragma unroll
-  for (int jb = 0; jb < 4; ++jb)
+  for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
     for (int ib = 0; ib < 4; ++ib) aw[jb][ib] = f32x4{};
   const int trq = lm >> 2, trp = lm & 3, tr0 = 8 * kg + trq, tr1 = tr0 + 4;
-  if (nk > 0) dma(0);
-  __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+  // this wave's DMAs done but for the last m tiles' (5 each)
+  auto wait_ahead = [](int m) {
+    if (m >= 2) __builtin_amdgcn_s_waitcnt(fb_vmcnt(10));
+    else if (m == 1) __builtin_amdgcn_s_waitcnt(fb_vmcnt(5));
+    else __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+  };
+  static_assert(WE_AHEAD <= 3, "wait_ahead");
+#pragma unroll
+  for (int j = 0; j < WE_AHEAD; ++j)
+    if (j < nk) dma(j);
+  wait_ahead(min(WE_AHEAD - 1, nk - 1));
   __builtin_amdgcn_s_barrier();
   for (int k = 0; k < nk; ++k) {
-    if (k + 1 < nk) dma(k + 1);
-    const char* const b = wel + (size_t)(k & 1) * WE_BUF;
-    const unsigned ga = fb_lds_addr(b + src * GS_TILE), ea = fb_lds_addr(b + 2 * GS_TILE);
-    std::array<s16x4, 4> ra[4], rx[4];
+    if (k + WE_AHEAD < nk) dma(k + WE_AHEAD);
+    const char* const b = wel + (size_t)(k % WE_SLOTS) * WE_BUF;
+    const unsigned ga = fb_lds_addr(b), ea = fb_lds_addr(b + GS_TILE);
+    std::array<s16x4, 4> ra[2], rx[4];
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) {
-      const int col = 64 * rw + 16 * jb + 4 * trp;
+    for (int jb = 0; jb < 2; ++jb) {
+      const int col = 32 * wv + 16 * jb + 4 * trp;
       const unsigned a0 = ga + gs_off(tr0, col >> 3) + 2 * (col & 7), a1 = ga + gs_off(tr1, col >> 3) + 2 * (col & 7);
       ra[jb] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_GPART>(a0), fb_tr<FB_GPART>(a1)};
     }
@@ -4327,19 +4340,19 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_enc(const char* __restrict__ g
     for (int ib = 0; ib < 4; ++ib) {
       const f16x8 B0 = join(rx[ib][0], rx[ib][1]), B1 = join(rx[ib][2], rx[ib][3]);
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb) {
+      for (int jb = 0; jb < 2; ++jb) {
         const f16x8 A0 = join(ra[jb][0], ra[jb][1]), A1 = join(ra[jb][2], ra[jb][3]);
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0, aw[jb][ib], 0, 0, 0);
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1, aw[jb][ib], 0, 0, 0);
         aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0, aw[jb][ib], 0, 0, 0);
       }
     }
-    __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));   // this wave's DMA of tile k + 1
+    wait_ahead(max(0, min(k + WE_AHEAD, nk - 1) - (k + 1)));   // tile k + 1's DMA landed (later tiles' may fly)
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();              // every wave's DMA landed; buffer k & 1 read by all
+    __builtin_amdgcn_s_barrier();
   }
   constexpr int C = WgradCfg<1>::C;
-  float* const pb = (src == 0 ? part0 : part4) + (size_t)blk * WgradCfg<1>::PART;
+  float* const pb = (src == 0 ? part0 : part4) + (size_t)pr * WgradCfg<1>::PART;
   const float gu = ldexpf(1.0f, -gexp[src == 0 ? 0 : 4]);
   const int sxyz = remat_sx(0, __uint_as_float(*pbound));
 #pragma unroll
@@ -4347,13 +4360,13 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_enc(const char* __restrict__ g
     const int col = 16 * ib + lm;
     const float cu = ldexpf(gu, -(col < 3 ? sxyz : 13));
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
+    for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pb[(size_t)(64 * rw + 16 * jb + 4 * kg + r) * C + col] = aw[jb][ib][r] * cu;
+      for (int r = 0; r < 4; ++r) pb[(size_t)(32 * wv + 16 * jb + 4 * kg + r) * C + col] = aw[jb][ib][r] * cu;
   }
   if (kg == 0) {
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) pb[(size_t)256 * C + 64 * rw + 16 * jb + lm] = 0.0f;
+    for (int jb = 0; jb < 2; ++jb) pb[(size_t)256 * C + 32 * wv + 16 * jb + lm] = 0.0f;
   }
 }
 
@@ -4696,14 +4709,14 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   {
     // 2 x 2 x 256 x 64 fp32-FLOP per sample; 2 KiB of g + 256 B of encoding in
     ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 2.0 * 256.0 * 64 * dn, (2048.0 + 256.0) * dn);
-    hipLaunchKernelGGL(k_wgrad_enc, dim3(we), dim3(512), WE_LDS, s, (const char*)S[1], (const char*)S2,
+    hipLaunchKernelGGL(k_wgrad_enc, dim3(2 * FB_PAIRS), dim3(512), WE_LDS, s, (const char*)S[1], (const char*)S2,
                        (const char*)encimg, n, (const int*)ws.gexp, (const unsigned*)ws.pbound, part_e0, part_e4);
   }
   // the partial sums read (k_fb_reduce_tail): layer 1's pair partials and the two encoding-column sets
   ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0 + 2.0 * we * WgradCfg<1>::PART * 4.0);
   hipLaunchKernelGGL(k_fb_reduce_tail, dim3(256, 3), dim3(1024), 0, s, pset[1], (const float*)ws.coef,
                      ws.gacc + G.w[1], ws.gacc + G.b[1], part_e0, ws.gacc + G.w[0], ws.gacc + G.b[0], part_e4,
-                     ws.gacc + G.w[4], FB_PAIRS, (int)we);
+                     ws.gacc + G.w[4], FB_PAIRS, (int)std::min<int64_t>(ntiles, FB_PAIRS));
 }
 
 static void emit_grads(const GaccLayout& G, const BwdWs& ws, const pcnerf_nof_grads* grads, hipStream_t s) {
