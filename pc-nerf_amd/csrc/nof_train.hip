@@ -4703,7 +4703,7 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
     if (L == 4) launch(k_bwd_remat2<2, 0>);
     else launch(k_bwd_remat2<0, 0>);
   }
-  const unsigned we = (unsigned)std::min<int64_t>(ntiles, WG_BLOCKS);
+  const int ne = (int)std::min<int64_t>(ntiles, FB_PAIRS);   // encoding-column partial sets (one per pair)
   float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
   float* const part_e4 = part_e0 + (size_t)WG_BLOCKS * WgradCfg<1>::PART;
   {
@@ -4713,10 +4713,10 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                        (const char*)encimg, n, (const int*)ws.gexp, (const unsigned*)ws.pbound, part_e0, part_e4);
   }
   // the partial sums read (k_fb_reduce_tail): layer 1's pair partials and the two encoding-column sets
-  ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0 + 2.0 * we * WgradCfg<1>::PART * 4.0);
+  ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * WgradCfg<0>::PART * 4.0 + 2.0 * ne * WgradCfg<1>::PART * 4.0);
   hipLaunchKernelGGL(k_fb_reduce_tail, dim3(256, 3), dim3(1024), 0, s, pset[1], (const float*)ws.coef,
                      ws.gacc + G.w[1], ws.gacc + G.b[1], part_e0, ws.gacc + G.w[0], ws.gacc + G.b[0], part_e4,
-                     ws.gacc + G.w[4], FB_PAIRS, (int)std::min<int64_t>(ntiles, FB_PAIRS));
+                     ws.gacc + G.w[4], FB_PAIRS, ne);
 }
 
 static void emit_grads(const GaccLayout& G, const BwdWs& ws, const pcnerf_nof_grads* grads, hipStream_t s) {
