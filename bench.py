@@ -630,7 +630,7 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
               16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw",
               # (the train query writing the activation store is its own instantiation)
               18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" and not remat else "k_nof_eval_h3<true,false>",
-              19: "k_bwd_remat2<0,0>" if remat else "k_bwd_fused<0,false>"}
+              19: "k_bwd_remat2<0>" if remat else "k_bwd_fused<0,false>"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd", 20: "k_g7"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
@@ -686,12 +686,12 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                 "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1)}
     if tag == 19 and remat:
-        # one launch per layer and chunk (<0,0> for layers 7, 6, 3, 2; <0,2>, <2,0>, <0,1> for 5, 4, 1): the
+        # one launch per layer and chunk (<0> for layers 7, 6, 5, 3, 2, 1; <2> for the skip layer 4): the
         # per-sample bytes (g_L + encoding in, g_{L-1} out) are the algorithmic count; each launch also writes its 128
         # pair partials of the weight gradient (the split-K over tiles) and reads the previous layer's
         per_launch = kbytes / max(klaunch, 1)
         partials = 2.0 * 128 * (256 * 256 + 256) * 4
-        roof["note"] = ("layer launches k_bwd_remat2<0,0|0,1|0,2|2,0> averaged; traffic = <0,0>'s PMC bytes; the "
+        roof["note"] = ("layer launches k_bwd_remat2<0|2> averaged; traffic = <0>'s PMC bytes; the "
                         "weight-gradient partial round trip (2 x 128 pairs x 256 KiB) is outside the algorithmic bytes")
         roof["partials_bytes_per_launch"] = partials
         if traffic:

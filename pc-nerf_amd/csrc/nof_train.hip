@@ -40,12 +40,6 @@ constexpr int H1_XD = H_XD;      // k_train_h1's B-operand read ring depth
 // blocks later), the block of the first staging piece, the blocks between staging pieces
 constexpr int WB3_AREAD = 3, WB3_STAGE = 0, WB3_SPACE = 2;
 
-#ifndef PCN_RB_DEPI
-#define PCN_RB_DEPI 0   // A/B switch: the D waves' epilogue of tile k runs between tile k + 1's data-gradient MFMAs
-#endif
-#ifndef PCN_RB_RPRIO
-#define PCN_RB_RPRIO 0   // A/B switch: the W waves' remat phase at raised wave priority
-#endif
 #ifndef PCN_RB_CLK
 #define PCN_RB_CLK 0   // diagnostic builds: per-wave shader cycles of the layer-2 launch's phases (pcnerf_debug_rbclk)
 #endif
@@ -3729,22 +3723,21 @@ constexpr size_t G7_LDS = 2 * FB_ENC + 1024 * sizeof(float);
 //   * the layer input x = h_{L-1} - mean made on the matrix pipe from the encoding image (two LDS slots, one tile
 //     deeper) and the half's P'_{L-1} rows (LDS, staged once: 12 MFMAs per wave and tile), split into the x half of
 //     the next tile's buffer between the data- and weight-gradient MFMAs;
-//   * g_{L-1} = ((dy - gm) - x kk) invstd gamma written pre-split (GOUT 0), as fp32 tiles (1: g_0, read by the
-//     encoding-column launch), or both (2: g_4), at 2^gexp[L-1] from a bound fixed in the prologue:
+//   * g_{L-1} = ((dy - gm) - x kk) invstd gamma written pre-split at 2^gexp[L-1] from a bound fixed in the prologue:
 //     |g_{L-1,i}| <= (sum_j |W_L[j][i]| max|g_L| + |gm_i| + sqrt(n) sigma_i |kk_i|) invstd_i |gamma_i|.
 // HBM per sample: 1 KiB of g_L, 256 B of encoding in, 1 KiB of g_{L-1} out (2.25 KiB; the store path moved 3).
 constexpr size_t RB_PX = 128 * 256;   // the half's P' rows (128 x 16 f16x8), slot q of row r at q ^ (r & 15)
 constexpr size_t RB_LDS = 2 * (size_t)FB_BUF + 2 * FB_ENC + RB_PX + 8 * 128 * sizeof(float);
 static_assert(RB_LDS <= 160 * 1024, "k_bwd_remat2 LDS");
-// k_bwd_remat2<LAY, GOUT>: that work split by ROLE between the two waves of each SIMD (waves w and w + 4 share a SIMD): waves 0-3 ("D") the data gradient of 32 input features
+// k_bwd_remat2<LAY>: that work split by ROLE between the two waves of each SIMD (waves w and w + 4 share a SIMD): waves 0-3 ("D") the data gradient of 32 input features
 // each (W_L^T rows in registers: 2 row blocks, so every 16-byte g read feeds 6 MFMAs instead of 3) and the BatchNorm
 // backward epilogue with the g_{L-1} stores; waves 4-7 ("W") the rematerialisation of 32 x columns each and the
 // weight gradient of 64 neuron rows each (G's 64 x 128 slice in 128 registers).  Per tile a D wave runs MFMAs then
 // VALU (dgrad, epilogue), a W wave VALU-heavy then MFMAs (remat, wgrad), so each SIMD's two waves are in
 // complementary phases between the tile's barriers; the g / encoding DMAs stay spread over all eight waves.
-template <int LAY, int GOUT>
+template <int LAY>
 __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ gin, char* __restrict__ gout,
-                                                        float* __restrict__ gout32, const f16x8* __restrict__ wt,
+                                                        const f16x8* __restrict__ wt,
                                                         const int* __restrict__ sw, int layer, int64_t n,
                                                         const float* __restrict__ coefp, const float* __restrict__ bnb,
                                                         const float* __restrict__ gamma, int* __restrict__ gexp,
@@ -3754,7 +3747,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
                                                         FbRed red, const char* __restrict__ enc,
                                                         const f16x8* __restrict__ px, const float* __restrict__ pxs) {
   constexpr int C = WgradCfg<LAY>::C, COL = LAY == 2 ? 64 : 0;
-  constexpr int NST = 4 * ((GOUT != 1 ? 1 : 0) + (GOUT != 0 ? 1 : 0));   // a D wave's global stores per tile
+  constexpr int NST = 4;   // a D wave's global stores per tile
   extern __shared__ __attribute__((aligned(16))) char fb[];
   char* const enb = fb + 2 * FB_BUF;
   char* const pxl = enb + 2 * FB_ENC;
@@ -3905,25 +3898,15 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
       asm volatile("" ::"v"(wr[ks][0][0]), "v"(wr[ks][0][1]), "v"(wr[ks][1][0]), "v"(wr[ks][1][1]));
     float gmo = 0.0f;
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#if !PCN_RB_DEPI
     u32x4 pcell[2][2] = {{u32x4{}, u32x4{}}, {u32x4{}, u32x4{}}};
-    f32x4 pv32[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
-#endif
-    // a cell's g_{L-1} stores (tile tq): the split pair as one 16-byte cell, and / or the fp32 value
-    auto store_cell = [&](int rb, int sb, int tq, const u32x4& cell, const f32x4& v) {
-      const int il = 32 * rw + 16 * rb + 4 * kg, i = 128 * hf + il, sm = 16 * sb + lm;
-      if constexpr (GOUT != 1) {
-        char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
+    // a cell's g_{L-1} store (tile tq): the split pair as one 16-byte cell
+    auto store_cell = [&](int rb, int sb, int tq, const u32x4& cell) {
+      const int i = 128 * hf + 32 * rw + 16 * rb + 4 * kg, sm = 16 * sb + lm;
+      char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
 #if PCN_RB_NOSTORE
-        if (cell[0] == 12345u && cell[3] == 4321u)
+      if (cell[0] == 12345u && cell[3] == 4321u)
 #endif
-        __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));   // streaming: keep L2 for the g / encoding tiles the other half re-reads
-      }
-      if constexpr (GOUT != 0) {
-        f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tq * TILE_FLOATS) + (i >> 3) * 64 + sm +
-                     32 * ((i >> 2) & 1);
-        __builtin_nontemporal_store(v, dst);
-      }
+      __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));   // streaming: keep L2 for the g / encoding tiles the other half re-reads
     };
     // tile k's g_{L-1} cells are stored during tile k + 1's data-gradient MFMAs, one cell after every second k-step
     // (pinned there by scheduling barriers: left to the scheduler they sink to the phase's end), so the D waves'
@@ -3932,111 +3915,6 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
     // addresses, program order; they also keep NST stores behind every tile's DMAs for the vmcnt(NST) below)
     [[maybe_unused]] unsigned long long ck0 = 0, ck1 = 0, ck2 = 0, ck3 = 0, cA = 0, cB = 0, cW = 0, cL0 = 0, cL1 = 0;
     RB_T(cL0);
-#if PCN_RB_DEPI
-    // tile k's BatchNorm-backward epilogue runs between tile k + 1's data-gradient MFMAs, one cell after every
-    // second k-step (pinned by scheduling barriers), from its accumulators and x values kept in registers across
-    // the barrier (x: the buffer is rewritten by the W waves' remat of tile k + 2 during tile k + 1); tile 0's pass
-    // stores zero cells (no valid sample) to tile 0's own slots, rewritten in program order by its real cells --
-    // and keeps NST stores behind every tile's DMAs for the vmcnt(NST) below
-    f32x4 adp[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
-    f16x4 xhp[2][2] = {}, xmp[2][2] = {};
-    auto epi_cell = [&](int rb, int sb, int tq, bool have) {
-      const int il = 32 * rw + 16 * rb + 4 * kg, sm = 16 * sb + lm;
-      const f32x4 cA = *reinterpret_cast<const f32x4*>(cst + 640 + il);
-      const f32x4 cB = *reinterpret_cast<const f32x4*>(cst + 256 + il);
-      const f32x4 cC = *reinterpret_cast<const f32x4*>(cst + 384 + il);
-      const bool valid = have && (int64_t)tq * 32 + sm < n;
-      f32x4 vs;   // 2^eo g_{L-1}
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float xs = (float)xhp[rb][sb][q] + (float)xmp[rb][sb][q];   // exact: the split's two parts
-        vs[q] = valid ? fmaf(-xs, cC[q], fmaf(adp[rb][sb][q], cA[q], -cB[q])) : 0.0f;
-        gmo = fmaxf(gmo, fabsf(vs[q]));
-      }
-      const int i = 128 * hf + il;
-      if constexpr (GOUT != 1) {
-        s16x4 p0, p1;
-        split2_x4(vs, p0, p1);
-        const fb_i32x2 hv = __builtin_bit_cast(fb_i32x2, p0), mv = __builtin_bit_cast(fb_i32x2, p1);
-        const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
-        const u32x4 cell = {s0[0], s1[0], s0[1], s1[1]};
-        char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
-        __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));
-      }
-      if constexpr (GOUT != 0) {
-        f32x4 v;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = vs[q] * gui;   // exact: a power of two
-        f32x4* dst = reinterpret_cast<f32x4*>(gout32 + (size_t)tq * TILE_FLOATS) + (i >> 3) * 64 + sm +
-                     32 * ((i >> 2) & 1);
-        __builtin_nontemporal_store(v, dst);
-      }
-    };
-    for (int k = 0; k < nk; ++k) {
-      const int tl = pr + k * npair;
-      const int ptl = k > 0 ? tl - npair : tl;
-      RB_T(ck0);
-#if !PCN_RB_NODMA
-      if (k + 1 < nk) dma_g(k + 1);
-      if (k + 2 < nk) dma_enc(k + 2);
-#endif
-      const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
-      const char* xb = sp + 2 * FB_GPART;
-      f32x4 ad[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb) {
-          const int o = gs_off(16 * sb + lm, 4 * ks + kg);
-          const f16x8 bh = *reinterpret_cast<const f16x8*>(sp + o);
-          const f16x8 bm = *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb) {
-            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bh, ad[rb][sb], 0, 0, 0);
-            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bm, ad[rb][sb], 0, 0, 0);
-            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][1], bh, ad[rb][sb], 0, 0, 0);
-          }
-          if ((ks & 1) && sb == 1) {
-            epi_cell((ks >> 2) & 1, (ks >> 1) & 1, ptl, k > 0);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      RB_T(ck1);
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb) {
-          const int o = fb_off<FB_XP>(16 * sb + lm, 32 * rw + 16 * rb + 4 * kg);
-          xhp[rb][sb] = *reinterpret_cast<const f16x4*>(xb + o);
-          xmp[rb][sb] = *reinterpret_cast<const f16x4*>(xb + FB_XPART + o);
-          adp[rb][sb] = ad[rb][sb];
-        }
-      RB_T(ck2);
-#if !PCN_RB_NOWAIT
-      __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs (its stores may fly)
-#endif
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      __builtin_amdgcn_s_barrier();
-      RB_T(ck3);
-      cA += ck1 - ck0;
-      cB += ck2 - ck1;
-      cW += ck3 - ck2;
-    }
-    RB_T(cL1);
-#if PCN_RB_CLK
-    if (layer == 2 && lane == 0 && bid < 512) {
-      unsigned long long* g = g_rbclk[bid * 8 + wv];
-      g[0] = cA; g[1] = cB; g[2] = cW; g[3] = cL1 - cL0; g[4] = (unsigned long long)nk;
-    }
-#endif
-    if (nk > 0) {   // the last tile's epilogue
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb) epi_cell(rb, sb, pr + (nk - 1) * npair, true);
-    }
-#else
     for (int k = 0; k < nk; ++k) {
       const int tl = pr + k * npair;
       const int ptl = k > 0 ? tl - npair : tl;
@@ -4066,8 +3944,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #endif
           }
           if ((ks & 1) && sb == 1) {
-            store_cell((ks >> 2) & 1, (ks >> 1) & 1, ptl, pcell[(ks >> 2) & 1][(ks >> 1) & 1],
-                       pv32[(ks >> 2) & 1][(ks >> 1) & 1]);
+            store_cell((ks >> 2) & 1, (ks >> 1) & 1, ptl, pcell[(ks >> 2) & 1][(ks >> 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -4092,25 +3969,15 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
             vs[q] = valid ? fmaf(-xs, cC[q], fmaf(ad[rb][sb][q], cA[q], -cB[q])) : 0.0f;
             gmo = fmaxf(gmo, fabsf(vs[q]));
           }
-          u32x4 cell = {};
-          if constexpr (GOUT != 1) {
-            s16x4 p0, p1;
-            split2_x4(vs, p0, p1);
-            // one 16-byte cell per lane: the lanes of 16-lane rows 2r / 2r+1 (kg even / odd: features i .. i+3 and
-            // i+4 .. i+7 of one octet) swap halves (v_permlane16_swap: the odd row's first operand <-> the even
-            // row's second), so the even row stores the octet's hi part and the odd row its mid part
-            const fb_i32x2 hv = __builtin_bit_cast(fb_i32x2, p0), mv = __builtin_bit_cast(fb_i32x2, p1);
-            const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
-            const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
-            cell = u32x4{s0[0], s1[0], s0[1], s1[1]};
-          }
-          f32x4 v = {};
-          if constexpr (GOUT != 0) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = vs[q] * gui;   // exact: a power of two
-          }
-          pcell[rb][sb] = cell;
-          pv32[rb][sb] = v;
+          s16x4 p0, p1;
+          split2_x4(vs, p0, p1);
+          // one 16-byte cell per lane: the lanes of 16-lane rows 2r / 2r+1 (kg even / odd: features i .. i+3 and
+          // i+4 .. i+7 of one octet) swap halves (v_permlane16_swap: the odd row's first operand <-> the even
+          // row's second), so the even row stores the octet's hi part and the odd row its mid part
+          const fb_i32x2 hv = __builtin_bit_cast(fb_i32x2, p0), mv = __builtin_bit_cast(fb_i32x2, p1);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
+          pcell[rb][sb] = u32x4{s0[0], s1[0], s0[1], s1[1]};
         }
       }
       RB_T(ck2);
@@ -4135,9 +4002,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-        for (int sb = 0; sb < 2; ++sb) store_cell(rb, sb, pr + (nk - 1) * npair, pcell[rb][sb], pv32[rb][sb]);
+        for (int sb = 0; sb < 2; ++sb) store_cell(rb, sb, pr + (nk - 1) * npair, pcell[rb][sb]);
     }
-#endif
     gmo = wave_max_f(gmo) * gui;
     if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rw) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
   } else {
@@ -4156,11 +4022,9 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
       if (k + 1 < nk) dma_g(k + 1);
       if (k + 2 < nk) dma_enc(k + 2);
 #endif
-      if (PCN_RB_RPRIO) __builtin_amdgcn_s_setprio(PCN_RB_RPRIO);
 #if !PCN_RB_NORM
       if (k + 1 < nk) remat_x(k + 1);
 #endif
-      if (PCN_RB_RPRIO) __builtin_amdgcn_s_setprio(0);
       RB_T(ck1);
       const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
       auto read8 = [&](unsigned a0, unsigned a1, auto partc) {
@@ -4638,9 +4502,9 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                         int ray_stride, const float* z, int n_samples, float eps, const float* grad, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_enc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WE_LDS));
@@ -4695,13 +4559,13 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
     // bytes: g_L in (1 KiB), the encoding image (256 B), g_{L-1} out (1 KiB)
     ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0 + 2.0 * 256.0 * 64.0) * dn, (1024.0 + 256.0 + 1024.0) * dn);
     auto launch = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), RB_LDS, s, gin, gout, (float*)nullptr, ws.wth16 + (size_t)(L - 1) * HW_H,
+      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), RB_LDS, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,
                          (const int*)ws.sw, L, n, coefp, (const float*)(ws.bnb + 512 * (L - 1)), P.bn_w[L - 1],
                          ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
                          pset[L & 1], red, (const char*)encimg, prow(L - 1), psrow(L - 1));
     };
-    if (L == 4) launch(k_bwd_remat2<2, 0>);
-    else launch(k_bwd_remat2<0, 0>);
+    if (L == 4) launch(k_bwd_remat2<2>);
+    else launch(k_bwd_remat2<0>);
   }
   const int ne = (int)std::min<int64_t>(ntiles, FB_PAIRS);   // encoding-column partial sets (one per pair)
   float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
