@@ -3701,12 +3701,17 @@ __global__ __launch_bounds__(512, 1) void k_g7(const char* __restrict__ enc, con
         }
         s16x4 p0, p1;
         split2_x4(v, p0, p1);
-        const int o = gs_off(sm, f >> 3) + 2 * (f & 7);
-        *reinterpret_cast<s16x4*>(gt + o) = p0;
-        *reinterpret_cast<s16x4*>(gt + FB_GPART + o) = p1;
+        // one 16-byte cell per lane, as k_bwd_remat2's epilogue: kg even / odd (features f .. f+3, f+4 .. f+7 of
+        // one octet) swap halves, the even row storing the octet's hi part and the odd row its mid part
+        const fb_i32x2 hv = __builtin_bit_cast(fb_i32x2, p0), mv = __builtin_bit_cast(fb_i32x2, p1);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 cell = {s0[0], s1[0], s0[1], s1[1]};
+        __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt + (kg & 1) * FB_GPART + gs_off(sm, f >> 3)));
       }
     }
-    __builtin_amdgcn_s_waitcnt(fb_vmcnt(8));   // this wave's DMA of tile k + 1 (the 8 stores may still fly)
+    __builtin_amdgcn_s_waitcnt(fb_vmcnt(4));   // this wave's DMA of tile k + 1 (the 4 stores may still fly)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
   }
@@ -3714,6 +3719,9 @@ __global__ __launch_bounds__(512, 1) void k_g7(const char* __restrict__ enc, con
   if (lane == 0) atomicMax(gm7 + ((bid * 8 + wv) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
 }
 constexpr size_t G7_LDS = 2 * FB_ENC + 1024 * sizeof(float);
+// k_g7's grid: two workgroups per CU (96 VGPRs, 20 KiB of LDS each) -- -6 % against one (256), 1024 no better
+// (profiles/r05_g7_ab.txt)
+constexpr int G7_BLOCKS = 512;
 
 // The rematerialised layer launch (k_bwd_remat2 below): one layer's backward over a chunk in one pass, as k_bwd_fused
 // (a pair of workgroups per tile, halves of the input features, 8 waves; W_L^T rows in registers; one barrier a
@@ -4541,7 +4549,7 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   {
     // g_7: 2 x 256 x 64 fp32-FLOP per sample (h_7 - mean_7); 256 B of image + 4 B in, 1 KiB out
     ProfScope ps(s, PT_BWD_REMAT, 2.0 * 256.0 * 64.0 * dn, (260.0 + 1024.0) * dn);
-    hipLaunchKernelGGL(k_g7, dim3((unsigned)std::min<int64_t>(ntiles, 256)), dim3(512), G7_LDS, s, encimg,
+    hipLaunchKernelGGL(k_g7, dim3((unsigned)std::min<int64_t>(ntiles, G7_BLOCKS)), dim3(512), G7_LDS, s, encimg,
                        grad + c0, n, prow(7), psrow(7), (const float*)ws.ocst, ws.gmax + 7 * GMAX_SLOTS, ws.gexp,
                        ws.gm7, S[0]);
   }
