@@ -27,7 +27,8 @@ launcher and the distributed timing on CPU (gloo), with no GPU.
 The default run (N=1, config 2, train_fwd) also times, in the same process and as extra keys of its one line, the
 training step (``train_step``: config 2 with backward + Adam), the reference's own shell setting of it
 (``train_step_refcfg``: 256 rays at 768 + 1536 samples, chunk 262,144, shells/pretraining/KITTI00_pcnerf_train.bash),
-``val`` and the two-step ``view``, each with its own ms_per_step, roofline, cpu_baseline and cd_vs_ref (--no-extra
+BASELINE configs 3 (``config3``) and 4 (``config4``, all four MaiCity blocks on the one GPU), ``val`` and the
+two-step ``view``, each with its own ms_per_step, roofline, cpu_baseline and cd_vs_ref (--no-extra
 skips them), and measures what the fp16 matrix pipe sustains on the board (``mfma_ceiling_measured``, 1 s).
 
 Prints ONE JSON line (rank 0) with the throughput, the dominant kernel's roofline (HIP events over the timed
@@ -264,6 +265,10 @@ EXTRA_LINES = {
     # BatchNorm chunks of 262,144 samples -- the reference's shell chunk)
     "config3": dict(config=3, mode="train_step", rays=262144, samples=64, importance=128, cpu_rays=256,
                     line="config3"),
+    # BASELINE config 4: the MaiCity-00 split, 4 parent blocks with their own weights, 262,144 rays each at 128/256,
+    # train_fwd -- on one GPU all four blocks, 1,048,576 rays per step
+    "config4": dict(config=4, mode="train_fwd", rays=262144, samples=128, importance=256, cpu_rays=256,
+                    line="config4"),
     "val": dict(mode="val", rays=65536, samples=128, importance=256, cpu_rays=2048),
     "view": dict(mode="view", rays=16384, samples=128, importance=256, cpu_rays=512),
 }
