@@ -2046,17 +2046,12 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part
   constexpr int SPLIT = Cfg::SPLIT;
   const int in_f = ldw > 0 ? ldw : MODE == 0 ? 256 : MODE == 1 ? 63 : 319;
   constexpr int wcol_h = MODE == 2 ? 63 : 0, col_h = Cfg::EX ? 64 : 0;
+  static_assert(C * SPLIT % 64 == 0, "whole waves");
   __shared__ double red[C * SPLIT];
+  __shared__ double redw[C * SPLIT / 64];
   const int m = blockIdx.x, tt = threadIdx.x, t = tt % C, sl = tt / C;
-  double d = 0.0;
-  for (int b = tt; b < nblk; b += C * SPLIT) d += (double)part[(size_t)b * Cfg::PART + (size_t)256 * C + m];
-  red[tt] = d;
-  __syncthreads();
-  double dbm = 0.0;
-  const int nred = nblk < C * SPLIT ? nblk : C * SPLIT;   // only the first nblk threads summed anything
-  for (int i = 0; i < nred; ++i) dbm += red[i];
-  __syncthreads();
-  // 32 loads per thread in flight at once (the sum is latency-bound otherwise)
+  // the column sums first (32 loads per thread in flight at once: the sum is latency-bound otherwise), then the bias
+  // row, reduced by wave shuffles -- one barrier
   double Gp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   const float* pc = part + (size_t)m * C + t;
   const int nbc = (Cfg::EX && t < 64) ? nblk_e : nblk;   // the encoding columns' own partial count (MODE 2)
@@ -2075,9 +2070,17 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part
   }
   for (; b < b1; ++b) Gp[0] += (double)pc[(size_t)b * Cfg::PART];
   double G = ((Gp[0] + Gp[1]) + (Gp[2] + Gp[3])) + ((Gp[4] + Gp[5]) + (Gp[6] + Gp[7]));
+  double d = 0.0;
+  for (int bb = tt; bb < nblk; bb += C * SPLIT) d += (double)part[(size_t)bb * Cfg::PART + (size_t)256 * C + m];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+  if ((tt & 63) == 0) redw[tt >> 6] = d;
+  if (SPLIT > 1) red[tt] = G;
+  __syncthreads();
+  double dbm = 0.0;
+#pragma unroll
+  for (int i = 0; i < C * SPLIT / 64; ++i) dbm += redw[i];
   if (SPLIT > 1) {
-    red[tt] = G;
-    __syncthreads();
     if (sl != 0) return;
     for (int k = 1; k < SPLIT; ++k) G += red[t + C * k];
   }
