@@ -47,25 +47,31 @@ __device__ __forceinline__ float wave_max_f(float v) {
   return v;
 }
 
-// max |alpha(n) W[n][k]| over one layer's out_f x in_f weights by the whole block of NT threads (eight independent
-// loads in flight per thread; fmaxf drops NaN weights, in any order)
+// max |alpha(n) W[n][k]| over one layer's out_f x in_f weights by the whole block of NT threads (16-byte loads, eight
+// in flight per thread: two or three rounds for a 256 x 256..319 layer; fmaxf drops NaN weights, in any order)
 template <int NT, typename Alpha>
 __device__ __forceinline__ float block_layer_absmax(const float* __restrict__ w, int out_f, int in_f, Alpha alpha) {
   const int total = out_f * in_f;
   float m = 0.0f;
-  for (int i0 = threadIdx.x; i0 < total; i0 += NT * 8) {
-    float v[8];
+  const int n4 = ((uintptr_t)w & 15) == 0 ? total >> 2 : 0;   // (an unaligned layer takes the scalar loop)
+  const f32x4* __restrict__ w4 = reinterpret_cast<const f32x4*>(w);
+  for (int i0 = threadIdx.x; i0 < n4; i0 += NT * 8) {
+    f32x4 v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int i = i0 + NT * e;
-      v[e] = i < total ? w[i] : 0.0f;
+      v[e] = i < n4 ? w4[i] : f32x4{};
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int i = i0 + NT * e;
-      if (i < total) m = fmaxf(m, fabsf(alpha(i / in_f) * v[e]));
+      if (i < n4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m = fmaxf(m, fabsf(alpha((4 * i + q) / in_f) * v[e][q]));
+      }
     }
   }
+  for (int i = 4 * n4 + (int)threadIdx.x; i < total; i += NT) m = fmaxf(m, fabsf(alpha(i / in_f) * w[i]));
   m = wave_max_f(m);
   __shared__ float red[NT / 64];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
