@@ -614,6 +614,14 @@ def dtype_label(train_math, eval_math, fold=False):
 FP16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense BF16/FP16 MFMA
 
 
+def split_layer_bound(bytes_per_launch, flop_per_launch, products):
+    """The roof of a split-fp16 layer kernel: the one whose floor for the launch's algorithmic work is longer --
+    ``products`` fp16 MFMA products per fp32 FLOP against the dense fp16 peak, or the bytes against HBM."""
+    t_mfma = products * flop_per_launch / (FP16_MFMA_PEAK_TFLOPS * 1e12)
+    t_hbm = bytes_per_launch / (HBM_PEAK_GBS * 1e9)
+    return "mfma" if t_mfma > t_hbm else "hbm"
+
+
 def kernel_report(L, a, train_math, eval_math=None, line=None):
     """Kernel breakdown of the last timed step (library HIP events) and the dominant kernel's roofline; ``line``
     selects the PMC traffic entries (pmc_traffic)."""
@@ -680,7 +688,7 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
         # floor for the launch's algorithmic work: the layered kernels' 2 KiB/sample stream outlasts their MFMA
         # work (hbm); the rematerialised layer's 3 x 294,912 fp16 FLOP/sample outlast its 2.25 KiB (mfma)
         per_b, per_f = kbytes / max(klaunch, 1), kflops / max(klaunch, 1)
-        mfma_bound = nprod * per_f / (FP16_MFMA_PEAK_TFLOPS * 1e12) > per_b / (HBM_PEAK_GBS * 1e9)
+        mfma_bound = split_layer_bound(per_b, per_f, nprod) == "mfma"
         hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
         mf = {"achieved": round(nprod * achieved, 1), "peak": FP16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
               "frac": round(nprod * achieved / FP16_MFMA_PEAK_TFLOPS, 4)}
