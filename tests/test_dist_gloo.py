@@ -144,6 +144,13 @@ def test_bench_launcher_spawns_ranks():
     assert len(lines) == 1, out.stdout          # rank 0 only
     # config 5: every rank renders a row-balanced share of each of the 8 blocks
     assert lines[0]["n_gpus"] == 2 and lines[0]["dry_run"] and lines[0]["rank0_blocks"] == list(range(8))
+    # the self-proving N-rank record: backend, ranks seen, per-rank rays / ms / collective ms
+    d = lines[0]["dist"]
+    assert d["backend"] == "gloo" and d["ranks_seen"] == 2
+    for k in ("rays_per_rank", "ms_per_step_per_rank", "collective_ms_per_step_per_rank"):
+        assert len(d[k]) == 2 and all(v >= 0 for v in d[k])
+    assert d["rays_per_rank"] == [2048, 2048]
+    assert all(c <= m for c, m in zip(d["collective_ms_per_step_per_rank"], d["ms_per_step_per_rank"]))
     bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--dry-run"],
                          capture_output=True, text=True, env={**env, "WORLD_SIZE": "2"}, timeout=120)
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
