@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #define PCN_WAVE 64
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -92,3 +94,17 @@ __device__ __forceinline__ float smooth_l1(float a, float b) {
 }
 
 }  // namespace pcn
+
+// hipFuncSetAttribute (the dynamic-LDS cap) is per DEVICE: a launcher sets it the first time it runs on each device
+// of the process, tracked by a bit per device id (a per-process flag left a second device's launches at
+// the default cap).
+inline bool pcn_attr_needed(const std::atomic<uint64_t>& mask) {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return !(mask.load(std::memory_order_acquire) & (1ull << (d & 63)));
+}
+inline void pcn_attr_done(std::atomic<uint64_t>& mask) {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  mask.fetch_or(1ull << (d & 63), std::memory_order_release);
+}

@@ -4373,11 +4373,11 @@ template <int MODE>
 static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                          int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
                          const float* mu, float* part) {
-  static bool attr = false;
+  static std::atomic<uint64_t> attr{0};
   const size_t lds = WgradCfg<MODE>::LDS_BYTES;
-  if (!attr) {
+  if (pcn_attr_needed(attr)) {
     PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
+    pcn_attr_done(attr);
   }
   hipLaunchKernelGGL(k_wgrad<MODE>, dim3(blocks), dim3(512), lds, s, rays, stride, z, S, c0, n, ein, gin, hprev,
                      mu, part);
@@ -4393,11 +4393,11 @@ static void launch_wgrad_b3_one(unsigned blocks, hipStream_t s, const float* ray
   using Cfg = Wb3Cfg<MODE, H2>;
   constexpr size_t lds = 3 * Cfg::BUF + (H2 ? 2 * Cfg::NBLK * 32 * sizeof(float) : 0);
   static_assert(lds <= 160 * 1024, "LDS");
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<uint64_t> attr{0};
+  if (pcn_attr_needed(attr)) {
     PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_b3<RB, MODE, LAY, H2, NTP>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
+    pcn_attr_done(attr);
   }
   hipLaunchKernelGGL((k_wgrad_b3<RB, MODE, LAY, H2, NTP>), dim3(blocks), dim3(512 / RB), lds, s, rays, stride, z, S,
                      c0, ein, gin, hprev, mu, n, gmax, part, pbound, gin2, gmax2, part2);
@@ -4435,15 +4435,15 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                         int64_t c0, int64_t n, const double* stats, float* const (&hh)[8], const float* rays,
                         int ray_stride, const float* z, int n_samples, const float* ein, float eps, const float* grad,
                         hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<uint64_t> attr{0};
+  if (pcn_attr_needed(attr)) {
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)FB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)FB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_fused<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)FB_LDS_OUT));
-    attr = true;
+    pcn_attr_done(attr);
   }
   const double dn = (double)n;
   const int64_t ntiles = (n + 31) / 32;
@@ -4511,15 +4511,15 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
 static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs& ws, const FoldBnBwd& FB,
                         const f16x8* pimg, const float* pscl, int64_t ci, int64_t c0, int64_t n, const float* rays,
                         int ray_stride, const float* z, int n_samples, float eps, const float* grad, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<uint64_t> attr{0};
+  if (pcn_attr_needed(attr)) {
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_enc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WE_LDS));
-    attr = true;
+    pcn_attr_done(attr);
   }
   const double dn = (double)n;
   const int64_t ntiles = (n + 31) / 32;

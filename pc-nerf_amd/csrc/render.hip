@@ -596,8 +596,9 @@ __device__ void blk_bitonic(float* a, int n) {
   }
 }
 
-// render.py:371-412 + :463-467, one ray per workgroup of NT threads.  LDS: z (S) | w (S) | bins (S) | cdf (S) |
-// fine (PF = pow2 >= I) | full sort (P2 = pow2 >= S + I).  sample_pdf's draws are unsorted whenever the uniforms
+// render.py:371-412 + :463-467, one ray per workgroup of NT threads.  LDS: z (S) | fine (PF = pow2 >= I) | w (S) |
+// bins (S) | cdf (S), the full-sort buffer (P2 = pow2 >= S + I) aliasing w / bins / cdf, which are dead once the
+// fine values are drawn: (S + PF + max(3S, P2)) floats, 112 KiB at the reference eval shells' 4096 + 8192.  sample_pdf's draws are unsorted whenever the uniforms
 // are (perturb: torch.rand), so the fine list is bitonic-sorted on its own and merged with the coarse z (sorted by
 // construction, render.py:433-442) by binary search: a coarse value lands at its index plus the fine values
 // strictly below it, a fine value at its index plus the coarse values <= it.  A coarse list out of order or a NaN
@@ -612,11 +613,11 @@ __global__ __launch_bounds__(NT) void k_resample(const float* __restrict__ Z, co
   const int tid = threadIdx.x;
   const int64_t ray = blockIdx.x;
   float* zs = lds;
-  float* ws = zs + S;
+  float* fs = zs + S;
+  float* ws = fs + PF;
   float* bins = ws + S;
   float* cdf = bins + S;
-  float* fs = cdf + S;
-  float* sb = fs + PF;
+  float* sb = ws;   // (after the draws: the barrier below orders the last cdf / bins read before its first write)
   for (int i = tid; i < S; i += NT) {
     zs[i] = Z[ray * S + i];
     ws[i] = Wt[ray * S + i];
@@ -1143,10 +1144,12 @@ extern "C" int pcnerf_resample(const float* z, const float* weights, int64_t n_r
   int P2 = 1, PF = 1;
   while (P2 < F) P2 <<= 1;
   while (PF < n_importance) PF <<= 1;
-  const size_t lds = (size_t)(4 * n_samples + PF + P2) * sizeof(float);
-  PCN_CHECK(lds <= 160 * 1024, "pcnerf_resample: n_samples + n_importance too large for one workgroup's LDS");
+  const size_t lds = (size_t)(n_samples + PF + std::max(3 * n_samples, P2)) * sizeof(float);
   // about four comparators per thread in each bitonic stage of the fine sort
   const int nt = PF >= 2048 ? 512 : PF >= 1024 ? 256 : PF >= 512 ? 128 : 64;
+  // (+ the static float64 block-scan slots, NT / 64 of them)
+  PCN_CHECK(lds + (size_t)(nt / 64) * sizeof(double) <= 160 * 1024,
+            "pcnerf_resample: n_samples + n_importance too large for one workgroup's LDS");
   ProfScope ps((hipStream_t)stream, PT_RESAMPLE, 0.0,
                (double)n_rays * (8.0 * n_samples + 4.0 * F + (u ? 4.0 * n_importance : 0.0)));
 #define PCN_RS(NT)                                                                                                \

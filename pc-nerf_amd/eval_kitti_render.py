@@ -241,11 +241,13 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     own_group = False
-    if world > 1 and not dist.is_initialized():
+    if world > 1 and h.device == "cuda":
+        # one GPU per rank whatever the backend and whoever made the group (a gloo group left every rank
+        # on cuda:0); ranks that are meant to share a GPU say so through LOCAL_RANK (the 2-rank test: both 0)
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        if h.device == "cuda" and h.dist_backend == "nccl":
-            torch.cuda.set_device(local)
-            h.device = f"cuda:{local}"
+        torch.cuda.set_device(local)
+        h.device = f"cuda:{local}"
+    if world > 1 and not dist.is_initialized():
         dist.init_process_group(h.dist_backend)
         own_group = True
     try:

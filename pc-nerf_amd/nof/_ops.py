@@ -232,10 +232,11 @@ def _bn_after(model, state: torch.Tensor, total: int, chunk: int):
 
 
 def _bn_unsupported():
+    """A train-mode query under a layered train math (f16x2_3, f16x2_4, fp32): it keeps no per-chunk statistics
+    record, so the active recorder is told, and its sync() leaves every rank's running statistics as that rank's own
+    forward set them (the per-rank behaviour of Lightning's DDP without sync_batchnorm), with a one-time warning."""
     if _BN_REC is not None:
-        raise NotImplementedError("data-parallel BatchNorm sync (nof.bn_sync) needs the default train math "
-                                  "(f16x2_3_fused) or the train fold: the layered train maths keep no per-chunk "
-                                  "statistics record")
+        _BN_REC.mark_unsupported()
 
 
 def bn_chunk_stats(state: torch.Tensor, total: int, chunk: int) -> torch.Tensor:

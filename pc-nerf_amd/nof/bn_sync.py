@@ -16,10 +16,20 @@ gets by running the ranks' slices one after another, and num_batches_tracked cou
 
 The batch statistics themselves (what normalises each chunk) stay per rank, as the reference computes them per
 chunk of its own batch: only the running buffers -- what a checkpoint carries into eval mode -- are synchronised.
+
+What the synchronised statistics equal, and what they do not: they are the ranks' slices run back to back, chunked
+per rank.  They equal neither the reference's Lightning DDP checkpoint (rank 0's own statistics) nor a single process
+running the GLOBAL batch, whose chunking differs whenever a rank's sample count is not a multiple of chunk (the
+reference shell's 256 rays x 768 samples = 196,608 < 262,144 per rank: each rank one partial chunk, one process
+262,144 + 131,072).  No reference run pins them: they are rank-independent by construction, parity-unpinned.
+
+Under a layered train math (f16x2_3, f16x2_4, fp32) the queries keep no per-chunk record: sync() then warns once
+and leaves each rank's running statistics as its own forward set them (per-rank, as before this module existed).
 """
 from __future__ import annotations
 
 import contextlib
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -35,9 +45,15 @@ class BnSync:
     """Record one step's BatchNorm chunk statistics (``with sync.record(): forward``) and make the running
     statistics rank-independent (``sync.sync()`` after the forward, on every rank)."""
 
+    _warned = False
+
     def __init__(self):
         self._snap = {}    # id(model) -> (model, running_mean clones, running_var clones, num_batches_tracked clones)
         self._recs = []    # (model, stats (C, 8, 2, 256) float64, total samples, chunk)
+        self._unsupported = False   # a query of this step kept no record (layered train math)
+
+    def mark_unsupported(self) -> None:
+        self._unsupported = True
 
     # -- hooks called by nof._ops around every train-mode query
     def before(self, model) -> None:
@@ -72,21 +88,30 @@ class BnSync:
         every rank calls it after the same sequence of queries).  ``replay(model, stats, ns)``: the update
         (default nof._ops.bn_running_replay, the HIP kernel).  Single-process: the forward's own update already is
         the sequential one; the records are dropped."""
-        recs, snap = self._recs, self._snap
-        self._recs, self._snap = [], {}
+        recs, snap, unsupported = self._recs, self._snap, self._unsupported
+        self._recs, self._snap, self._unsupported = [], {}, False
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
             return
         replay = replay or _ops.bn_running_replay
         world = dist.get_world_size(group)
         cpu_comm = dist.get_backend(group) == "gloo"
-        dev = recs[0][1].device if recs else torch.device("cpu")
+        dev = recs[0][1].device if recs else (torch.device("cuda", torch.cuda.current_device())
+                                              if not cpu_comm and torch.cuda.is_available() else torch.device("cpu"))
         comm_dev = torch.device("cpu") if cpu_comm else dev
-        # the ranks must have made the same queries (same models in the same order): the counts are checked first
-        n = torch.tensor([len(recs)], dtype=torch.int64, device=comm_dev)
+        # the ranks must have made the same queries (same models in the same order): the counts are checked first,
+        # with whether any rank's step had a query that kept no record
+        n = torch.tensor([len(recs), int(unsupported)], dtype=torch.int64, device=comm_dev)
         ns = [torch.zeros_like(n) for _ in range(world)]
         dist.all_gather(ns, n, group=group)
-        if any(int(x) != len(recs) for x in ns):
-            raise RuntimeError(f"BnSync.sync: ranks recorded different numbers of queries {[int(x) for x in ns]}")
+        if any(int(x[1]) for x in ns):
+            if not BnSync._warned:
+                warnings.warn("nof.bn_sync: a layered train math keeps no per-chunk BatchNorm statistics; the "
+                              "running statistics stay per rank (select the default train math f16x2_3_fused for "
+                              "rank-independent ones)", RuntimeWarning, stacklevel=2)
+                BnSync._warned = True
+            return
+        if any(int(x[0]) != len(recs) for x in ns):
+            raise RuntimeError(f"BnSync.sync: ranks recorded different numbers of queries {[int(x[0]) for x in ns]}")
         if not recs:
             return
         meta = torch.tensor([[t, c] for (_, _, t, c) in recs], dtype=torch.int64, device=comm_dev)

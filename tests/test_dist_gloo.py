@@ -327,3 +327,48 @@ def test_bn_sync_world2_rank_independent_running_stats():
         for k, v in m.state_dict().items():
             np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
             np.testing.assert_array_equal(s0[k], v.numpy(), err_msg=k)
+
+
+def _bn_unsup_worker(rank, world, port, q):
+    import warnings
+    from nof import _ops
+    from nof.bn_sync import BnSync
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        models = _bn_models()
+        bns = BnSync()
+        with bns.record():
+            bns.before(models[0])
+            for b in models[0].norms():   # the rank's own (layered-math) forward moved its buffers
+                b.running_mean.add_(rank + 1.0)
+            if rank == 1:                 # one rank's query kept no record: every rank must skip the replay
+                _ops._bn_unsupported()
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            bns.sync()
+        q.put((rank, [b.running_mean.numpy().copy() for b in models[0].norms()],
+               any(issubclass(x.category, RuntimeWarning) for x in w)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bn_sync_layered_math_keeps_per_rank_stats():
+    """a train-mode query under a layered train math (no per-chunk record) inside BnSync.record() no
+    longer raises; sync() warns and leaves each rank's running statistics as its own forward set them, on every rank
+    (the flag is all-gathered, so the ranks agree on skipping)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bn_unsup_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {r: (m, w) for r, m, w in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    base = _bn_models()[0]
+    for r in range(2):
+        means, _ = got[r]
+        for m, b in zip(means, base.norms()):
+            np.testing.assert_array_equal(m, b.running_mean.numpy() + (r + 1.0))
+    assert got[0][1] or got[1][1]   # warned (once per process)

@@ -135,12 +135,15 @@ def _bn_models_gpu(chunk_seed=0):
             syn.load_into(NOF_fine(), syn.init_nof_params(5678)).cuda().train())
 
 
-def _bn_rank(rank, world, port, q):
+def _bn_rank(rank, world, port, q, math=None):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "pc-nerf_amd"), here):
         sys.path.insert(0, p)
+    from nof import _ops
     from nof import synthetic as syn
+    if math is not None:
+        _ops.set_train_math(math)
     from nof.blocks import allreduce_grads, shard_batch
     from nof.bn_sync import BnSync
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -185,6 +188,38 @@ def test_data_parallel_batchnorm_running_stats_rank_independent():
             np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
             if "running" in k or "num_batches" in k:
                 np.testing.assert_array_equal(s0[k], v.cpu().numpy(), err_msg=k)
+
+
+@pytest.mark.timeout(240)
+def test_data_parallel_layered_math_bn_per_rank():
+    """data-parallel training under a layered train math (f16x2_3: no per-chunk statistics record) no
+    longer raises inside BnSync.record(); each rank keeps the running statistics its own forward set (equal to one
+    process rendering that rank's shard), with a warning."""
+    from nof import _ops
+    from nof import synthetic as syn
+    from nof.blocks import shard_batch
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_bn_rank, args=(r, 2, port, q, "f16x2_3")) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=200) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    prev = _ops.set_train_math("f16x2_3")
+    try:
+        rays = torch.from_numpy(syn.make_rays(401, seed=43)).cuda()
+        for r in range(2):
+            models = _bn_models_gpu()
+            _bn_step(models, rays[shard_batch(torch.arange(401, device="cuda"), r, 2)].contiguous())
+            for m, s in zip(models, got[r]):
+                for k, v in m.state_dict().items():
+                    if "running" in k or "num_batches" in k:
+                        np.testing.assert_array_equal(s[k], v.cpu().numpy(), err_msg=k)
+    finally:
+        _ops.set_train_math(prev)
 
 
 def _fit_rank(rank, world, port, tmp, q):

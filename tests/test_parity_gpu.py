@@ -380,7 +380,8 @@ def test_segmented_coarse_z_bitexact(ratio):
 
 
 @pytest.mark.parametrize("R,S,I,sorted_u", [(256, 128, 256, True), (256, 128, 256, False), (64, 200, 500, False),
-                                             (32, 300, 1000, False), (16, 768, 1536, False)])
+                                             (32, 300, 1000, False), (16, 768, 1536, False),
+                                             (4, 4096, 8192, True), (4, 4096, 8192, False)])
 def test_resample_merge_exact(R, S, I, sorted_u):
     """k_resample's sort(cat(z, z_samples)) (render.py:463-467): bit for bit the sort of the coarse z and the
     fine samples the same pdf code draws (pcnerf_sample_pdf), for sorted coarse rows (fine sort + binary-search
@@ -402,6 +403,21 @@ def test_resample_merge_exact(R, S, I, sorted_u):
         fine = _ops.sample_pdf_standalone(mid.to(DEV), w[:, 1:-1].to(DEV), I, False, u.to(DEV)).cpu()
         assert torch.equal(got, torch.sort(torch.cat([zz, fine], -1), -1)[0])
         close(fine, O.sample_pdf(mid, w[:, 1:-1], I, False, u).numpy(), 1e-5, 1e-6, "fine samples")
+
+
+def test_render_val_eval_shell_setting():
+    """The reference eval shells' sampling (shells/pretraining/*_eval.bash: N_samples 4096, N_importance 8192, chunk
+    184320): k_resample's largest fine list (8,192 draws, 12,288-value merge) fits one workgroup's LDS and the
+    rendered depths match the oracle (the launch used to exceed the 160 KiB cap)."""
+    rays = syn.make_rays(6, seed=29)
+    emb, mc, mf = models(False)
+    kw = dict(N_samples=4096, N_importance=8192, perturb=0, noise_std=0, chunk=184320)
+    with torch.no_grad():
+        res = R.render_rays_val(mc, mf, emb, torch.from_numpy(rays).to(DEV), **kw)
+    Pc, Pf = O.params_from_numpy(syn.init_nof_params(SEED_C)), O.params_from_numpy(syn.init_nof_params(SEED_F))
+    ref = O.render_rays_val(Pc, Pf, torch.from_numpy(rays), **kw)
+    for k in ("depth", "depth_fine"):
+        close(res[k], ref[k].numpy(), RTOL, 1e-9, k)
 
 
 def test_empty_rays_raise_like_the_reference():
