@@ -746,6 +746,7 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
     from nof import _ops
     line = line or a.mode
     remat = a.mode == "train_step" and train_math == "f16x2_3_fused" and _ops.remat_enabled()
+    rver = _ops.get_remat_version() if remat else None
     split = train_math in ("f16x2_3", "f16x2_4", "f16x2_3_fused")
     esplit = eval_math == "f16x2_3"
     nterm = 3 if (train_math in ("f16x2_3", "f16x2_3_fused") or esplit) else 4
@@ -761,7 +762,7 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
               16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw",
               # (the train query writing the activation store is its own instantiation)
               18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" and not remat else "k_nof_eval_h3<true,false>",
-              19: "k_bwd_remat2<0>" if remat else "k_bwd_fused<0,false>"}
+              19: ("k_bwd_remat3" if rver == 3 else "k_bwd_remat2<0>") if remat else "k_bwd_fused<0,false>"}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd", 20: "k_g7"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
@@ -786,6 +787,10 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
     gbs = kbytes / max(klaunch, 1) / avg_s / 1e9
     traffic, traffic_src = pmc_traffic(kname, line)
     nprod = nterm   # k_wgrad_b3 too: f16x2 parts, nterm products (the six-product bf16x3 form is a build option)
+    if tag == 19 and rver == 3:
+        # k_bwd_remat3 issues 3 products of (2.256.256 + 2.256.64 + 2.256.64) per sample against the algorithmic
+        # 2.2.256.256 (its weight gradient contracts the 64 encoding columns; the rematerialised x is extra work)
+        nprod = 3.0 * (131072 + 32768 + 32768) / 262144
     if a.fold:   # no MLP left: the query moves 8 B per sample (+ ray rows) and is bound by its sincos (VALU)
         roof = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -825,13 +830,14 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                 "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_flop_per_launch": kflops / max(klaunch, 1)}
     if tag == 19 and remat:
-        # one launch per layer and chunk (<0> for layers 7, 6, 5, 3, 2, 1; <2> for the skip layer 4): the
-        # per-sample bytes (g_L + encoding in, g_{L-1} out) are the algorithmic count; each launch also writes its 128
-        # pair partials of the weight gradient (the split-K over tiles) and reads the previous layer's
+        # one launch per layer and chunk: the per-sample bytes (g_L + encoding in, g_{L-1} out) are the algorithmic
+        # count; each launch also writes its 128 pair partials of the weight gradient (the split-K over tiles) and
+        # reads the previous layer's
         per_launch = kbytes / max(klaunch, 1)
-        partials = 2.0 * 128 * (256 * 256 + 256) * 4
-        roof["note"] = ("layer launches k_bwd_remat2<0|2> averaged; traffic = <0>'s PMC bytes; the "
-                        "weight-gradient partial round trip (2 x 128 pairs x 256 KiB) is outside the algorithmic bytes")
+        partials = 2.0 * 128 * (256 * (64 if rver == 3 else 256) + 256) * 4
+        roof["note"] = (("k_bwd_remat3 (weight gradient over the 64 encoding columns, projected by P'^T per chunk)"
+                         if rver == 3 else "layer launches k_bwd_remat2<0|2> averaged") +
+                        "; the weight-gradient partial round trip is outside the algorithmic bytes")
         roof["partials_bytes_per_launch"] = partials
         if traffic:
             roof["traffic_over_algorithmic"] = round(traffic / per_launch, 3)

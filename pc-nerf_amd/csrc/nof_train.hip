@@ -1361,6 +1361,14 @@ struct TrainWs {
 // products (k_train_h).  Process-wide; pcnerf_set_train_math.  Mode 1 renders config 2 within 1.9e-5 of a float64
 // evaluation of the same rays (fp32 MFMA: 2.2e-5; the reference itself: 1.1e-4) at 1.9x the speed.
 static int g_train_math = 1;
+// The rematerialised backward's layer kernel: 3 = k_bwd_remat3 (default: weight gradient over the encoding columns,
+// projected by P'^T per chunk), 2 = k_bwd_remat2 (round 5's: over the rematerialised x columns).  PCNERF_REMAT_VER
+// selects it at load time (A/B measurements).
+static int remat_ver_env() {
+  const char* v = getenv("PCNERF_REMAT_VER");
+  return (v && v[0] == '2') ? 2 : 3;
+}
+static int g_remat_ver = remat_ver_env();
 
 static TrainWs carve(void* base, int64_t chunk) {
   const size_t tiles = (size_t)((chunk + 31) / 32);
@@ -1403,6 +1411,16 @@ extern "C" int pcnerf_set_train_math(int mode) {
   }
   const int prev = pcn::g_train_math;
   pcn::g_train_math = mode;
+  return prev;
+}
+
+extern "C" int pcnerf_set_remat_version(int version) {
+  if (version != 2 && version != 3) {
+    pcn::set_error("pcnerf_set_remat_version: version must be 2 (k_bwd_remat2) or 3 (k_bwd_remat3)");
+    return -1;
+  }
+  const int prev = pcn::g_remat_ver;
+  pcn::g_remat_ver = version;
   return prev;
 }
 
@@ -1899,7 +1917,7 @@ struct WgradCfg {
   static constexpr int C = (EX ? 64 : 0) + (HX ? 256 : 0);
   static constexpr int GS = 32 * LDS_ROW;
   static constexpr int BUF = GS + (HX ? GS : 0) + (EX ? 32 * ES_ROW : 0);
-  static constexpr size_t LDS_BYTES = (size_t)(2 * BUF + 256) * sizeof(float);
+  static constexpr size_t LDS_BYTES = (size_t)(2 * BUF + 256 + 64) * sizeof(float);   // + mu, + encoding shift
   static constexpr size_t PART = (size_t)256 * C + 256;
   // k_wgrad_reduce: SPLIT slices of the partial list per column, RT threads per block
   static constexpr int SPLIT = C >= 1024 ? 1 : 1024 / C;
@@ -1918,8 +1936,30 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
   CLK_ENTRY
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* mus = lds + 2 * BUF;
+  // the encoding columns are contracted as g (x) (e - e(c0)), e(c0) the chunk's first sample's encoding: sum_s g = 0
+  // exactly (BatchNorm follows the Linear), so the sum is the same, while the rounding noise of sum_s g no longer
+  // multiplies |e| (positions far from the origin) but only the chunk's spread around one of its own samples
+  float* esh = mus + 256;
   const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31, wv = t >> 6;
   if (HX && t < 256) mus[t] = mu[t];
+  if (EX && t < 64) {
+    if (ein) {
+      esh[t] = t < 63 ? ein[c0 * 63 + t] : 0.0f;
+    } else {
+      float p[3];
+      sample_point(rays + ray_of(c0, S) * stride, z[c0], p);
+      float v = 0.0f;
+      if (t < 3) {
+        v = p[t];
+      } else if (t < 63) {
+        const int q = t - 3, k = q / 6, r = q - 6 * k, m = r % 3;
+        float sv, cv;
+        sincosf((float)(1 << k) * p[m], &sv, &cv);   // encode_half's arithmetic
+        v = r < 3 ? sv : cv;
+      }
+      esh[t] = v;
+    }
+  }
   __syncthreads();
   const int64_t ntiles = (n + 31) / 32;
   f32x16 ah[8], ae[2];
@@ -1963,22 +2003,22 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays
       const int64_t gi = c0 + sl;
       if (ein) {
         const float* er = ein + gi * 63;
-        for (int f = jj; f < 64; f += 16) row[f] = f < 63 ? er[f] : 0.0f;
+        for (int f = jj; f < 64; f += 16) row[f] = f < 63 ? er[f] - esh[f] : 0.0f;
       } else {
         float p[3];
         sample_point(rays + ray_of(gi, S) * stride, z[gi], p);
         if (jj == 0) {
-          row[0] = p[0];
-          row[1] = p[1];
-          row[2] = p[2];
+          row[0] = p[0] - esh[0];
+          row[1] = p[1] - esh[1];
+          row[2] = p[2] - esh[2];
           row[63] = 0.0f;
         }
         for (int q = jj; q < 30; q += 16) {
           const int k = q / 3, m = q - 3 * k;
           float sv, cv;
           sincosf((float)(1 << k) * p[m], &sv, &cv);  // encode_half's arithmetic
-          row[3 + 6 * k + m] = sv;
-          row[6 + 6 * k + m] = cv;
+          row[3 + 6 * k + m] = sv - esh[3 + 6 * k + m];
+          row[6 + 6 * k + m] = cv - esh[6 + 6 * k + m];
         }
       }
     }
@@ -4130,6 +4170,398 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
   if (red.mode != 0) fb_reduce_row(red, reinterpret_cast<double*>(fb), t);
 }
 
+// ---- k_bwd_remat3: the rematerialised layer launch with the weight gradient taken over the ENCODING columns
+// (VERDICT r5 item 2).  Inside a chunk every layer input is x = h_{L-1} - mean_{L-1} = P'_{L-1} d (d = e - ebar, the
+// identity-activation premise the remat already rests on) and sum_s g_L = 0 (BatchNorm L's backward), so
+//   G_L = sum_s g_L (x) x = (sum_s g_L (x) d) P'_{L-1}^T :
+// the tile loop contracts g_L with the 64 encoding columns (24 MFMAs per W wave and tile instead of 96 over the 256
+// x columns) and k_gd_proj applies P'_{L-1}^T in float64 once per chunk and layer (256 x 64 x 256).  x itself is
+// still made per tile (the BatchNorm backward's x kk term), but only as that term: the W waves write
+// xc = x (kk invstd gamma 2^eo) + gm invstd gamma 2^eo in fp32 (no hi / mid split: x is no longer an MFMA operand),
+// and the D waves' epilogue is one fma, 2^eo g_{L-1} = dy A - xc.  Per SIMD and tile the matrix pipe carries 96 + 24
+// + 24 MFMA groups instead of 96 + 24 + 96.  The weight-gradient partials (per pair: 256 rows x the half's 32 encoding
+// columns, in k_wgrad_enc's 64-column layout) are 4x smaller; the next launch's tail sums them per row into the
+// chunk's float64 G_d (gd_reduce_row), k_gd_tail sums layer 1's.  The skip layer's encoding columns ARE its G_d, so
+// k_wgrad_enc is left with g_0 alone.
+constexpr int R3_XC = 32 * 128 * 4;                      // xc: [32 samples][32 chunks of 4 features] fp32
+static_assert(2 * FB_GPART + R3_XC == FB_BUF, "remat3 keeps k_bwd_remat2's tile buffer size");
+constexpr int R3_ENC_SLOTS = 3;                          // remat of tile k + 1 and wgrad of tile k, DMA of k + 2
+constexpr size_t R3_LDS = 2 * (size_t)FB_BUF + R3_ENC_SLOTS * FB_ENC + RB_PX + 8 * 128 * sizeof(float);
+static_assert(R3_LDS <= 160 * 1024, "k_bwd_remat3 LDS");
+constexpr size_t GD_PART = WgradCfg<1>::PART;            // 256 x 64 + 256 floats per pair
+constexpr int GD_LAYER = 256 * 64;                       // doubles of one layer's G_d
+// 16-byte chunk c4 (features 4 c4 .. 4 c4 + 3) of sample s: 16 lanes of one k-group (16 samples) on 16 distinct bank
+// groups for the W waves' stores and the D waves' reads alike
+__device__ __forceinline__ int r3_xoff(int s, int c4) { return s * 512 + 16 * (c4 ^ (s & 15)); }
+
+// Row m = blockIdx.x of a layer's G_d over np pair partials (WgradCfg<1> layout), float64, by NT threads: column
+// t & 63, NT / 64 slices of the pairs; red: NT doubles of LDS
+template <int NT>
+__device__ __forceinline__ void gd_reduce_row(const float* __restrict__ part, int np, double* __restrict__ gd,
+                                              double* red, int t) {
+  constexpr int NS = NT / 64;
+  const int m = (int)blockIdx.x, c = t & 63, sl = t >> 6;
+  const int per = (np + NS - 1) / NS, b0 = sl * per, b1 = min(np, b0 + per);
+  const float* pc = part + (size_t)m * 64 + c;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  int b = b0;
+  for (; b + 16 <= b1; b += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = pc[(size_t)(b + j) * GD_PART];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j & 3] += (double)v[j];
+  }
+  for (; b < b1; ++b) a[0] += (double)pc[(size_t)b * GD_PART];
+  red[t] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (t < 64) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) s += red[64 * i + t];
+    gd[(size_t)m * 64 + t] = s;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ gin, char* __restrict__ gout,
+                                                        const f16x8* __restrict__ wt,
+                                                        const int* __restrict__ sw, int layer, int64_t n,
+                                                        const float* __restrict__ coefp, const float* __restrict__ bnb,
+                                                        const float* __restrict__ gamma, int* __restrict__ gexp,
+                                                        const float* __restrict__ wcol,
+                                                        const unsigned* __restrict__ gmax_in,
+                                                        unsigned* __restrict__ gmax_out, float* __restrict__ part,
+                                                        const float* __restrict__ rpart, double* __restrict__ rgd,
+                                                        const char* __restrict__ enc,
+                                                        const f16x8* __restrict__ px, const float* __restrict__ pxs,
+                                                        const unsigned* __restrict__ pbound) {
+  constexpr int NST = 4;   // a D wave's global stores per tile
+  extern __shared__ __attribute__((aligned(16))) char fb[];
+  char* const enb = fb + 2 * FB_BUF;
+  char* const pxl = enb + R3_ENC_SLOTS * FB_ENC;
+  float* const cst = reinterpret_cast<float*>(pxl + RB_PX);   // [. | 2^-e | B | . | invstd | A | x scale | bound]
+  const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int rw = wv & 3;   // index within the role
+  const int bid = (int)blockIdx.x, hf = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
+  const int npair = (int)gridDim.x >> 1;
+  const int nt = (int)((n + 31) / 32);
+  const int nk = pr < nt ? (nt - 1 - pr) / npair + 1 : 0;
+  const float rn = sqrtf((float)n);
+  if (t < 128) {
+    const int c = 128 * hf + t;
+    const float invstd = coefp[256 + c];
+    const float bnd = rn / invstd;   // Samuelson: |h - mean| <= sqrt(n) sigma
+    int e = (bnd > 0.0f && bnd < 3.0e38f) ? 14 - ilogbf(bnd) : 0;
+    e = e < -60 ? -60 : e > 60 ? 60 : e;
+    cst[128 + t] = ldexpf(1.0f, -e);
+    cst[256 + t] = bnb[c];
+    cst[384 + t] = bnb[256 + c];
+    cst[512 + t] = invstd;
+    cst[640 + t] = gamma[c];
+    cst[768 + t] = ldexpf(pxs[c], e);
+  }
+  unsigned gmx = 0;
+  for (int i = 0; i < GMAX_SLOTS; ++i) gmx = max(gmx, gmax_in[i]);
+  {
+    const int c = t & 255;
+    const float invstd = coefp[256 + c];
+    float ob = ((wcol[c] * __uint_as_float(gmx) + fabsf(bnb[c])) + rn / invstd * fabsf(bnb[256 + c])) * invstd *
+               fabsf(gamma[c]) * 1.01f;
+    ob = wave_max_f(ob);
+    if (lane == 0) cst[896 + wv] = ob;
+  }
+  for (int j = t; j < 128 * 16; j += 512) {
+    const int r = j >> 4, q = j & 15;
+    *reinterpret_cast<f16x8*>(pxl + r * 256 + 16 * (q ^ (r & 15))) = px[(size_t)(128 * hf + r) * 16 + q];
+  }
+  const int eg = gexp[layer];
+  const float gun = ldexpf(1.0f, -eg);
+  __syncthreads();
+  float obm = cst[896];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) obm = fmaxf(obm, cst[896 + i]);
+  const int eo = tile_scale_exp(obm);
+  const float gso = ldexpf(1.0f, eo);
+  if (bid == 0 && t == 0) gexp[layer - 1] = eo;
+  // the epilogue's per-feature constants folded:
+  //   2^eo g_{L-1} = dy A - xc,  A = dun invstd gamma 2^eo  (slot 640),
+  //   xc = m X + B,  m = the remat MFMA's output,  X = x scale 2^-e kk invstd gamma 2^eo (slot 768),
+  //   B = gm invstd gamma 2^eo (slot 256)
+  const float dun = ldexpf(1.0f, -sw[layer]) * gun;
+  if (t < 128) {
+    const float sc = cst[512 + t] * cst[640 + t] * gso;
+    const float cb = cst[256 + t] * sc, cc = cst[128 + t] * cst[384 + t] * sc;
+    cst[640 + t] = dun * sc;
+    cst[256 + t] = cb;
+    cst[768 + t] = cst[768 + t] * cc;   // (a power of two times cc: exact)
+  }
+  auto dma_g = [&](int k) {
+    const int tl = pr + k * npair;
+    char* const sb = fb + (size_t)(k & 1) * FB_BUF;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      fb_glds16(gin + (size_t)tl * GS_TILE + (4 * wv + m) * 1024 + 16 * ln, sb + (4 * wv + m) * 1024);
+  };
+  auto dma_enc = [&](int k) {
+    const int tl = pr + k * npair;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    fb_glds16(enc + (size_t)tl * FB_ENC + wv * 1024 + ln * 16, enb + (k % R3_ENC_SLOTS) * FB_ENC + wv * 1024);
+  };
+  // W waves: xc of tile k, features 32 rw .. 32 rw + 31 of the half (2 row blocks of P'), enc slot k % 3 -> buffer k & 1
+  auto remat_xc = [&](int k) {
+    const char* eb = enb + (k % R3_ENC_SLOTS) * FB_ENC;
+    char* const xb = fb + (size_t)(k & 1) * FB_BUF + 2 * FB_GPART;
+    f32x4 ax[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 pa[2][2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int r = 32 * rw + 16 * rb + lm, q = (2 * ks + p) * 4 + kg;
+          pa[rb][p] = *reinterpret_cast<const f16x8*>(pxl + r * 256 + 16 * (q ^ (r & 15)));
+        }
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int o = fb_eoff(16 * sb + lm, 4 * ks + kg);
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(eb + o);
+        const f16x8 bm = *reinterpret_cast<const f16x8*>(eb + FB_ENC / 2 + o);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][0], bh, ax[rb][sb], 0, 0, 0);
+          ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][0], bm, ax[rb][sb], 0, 0, 0);
+          ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][1], bh, ax[rb][sb], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int il = 32 * rw + 16 * rb + 4 * kg;
+      const f32x4 X = *reinterpret_cast<const f32x4*>(cst + 768 + il);
+      const f32x4 B = *reinterpret_cast<const f32x4*>(cst + 256 + il);
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaf(ax[rb][sb][q], X[q], B[q]);
+        *reinterpret_cast<f32x4*>(xb + r3_xoff(16 * sb + lm, il >> 2)) = v;
+      }
+    }
+  };
+  if (nk > 0) {
+    dma_g(0);
+    dma_enc(0);
+    if (nk > 1) dma_enc(1);
+    __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+    __builtin_amdgcn_s_barrier();
+    if (wv >= 4) remat_xc(0);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  if (wv < 4) {
+    // ---- D: data gradient of input features 128 hf + 32 rw + 16 rb + lm, epilogue, g_{L-1} stores
+    const float gui = ldexpf(1.0f, -eo);
+    f16x8 wr[8][2][2];
+    {
+      const f16x8* __restrict__ w8 = wt + lane;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int p = 0; p < 2; ++p) wr[ks][rb][p] = w8[((ks * 16 + 8 * hf + 2 * rw + rb) * 2 + p) * 64];
+    }
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      asm volatile("" ::"v"(wr[ks][0][0]), "v"(wr[ks][0][1]), "v"(wr[ks][1][0]), "v"(wr[ks][1][1]));
+    float gmo = 0.0f;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 pcell[2][2] = {{u32x4{}, u32x4{}}, {u32x4{}, u32x4{}}};
+    auto store_cell = [&](int rb, int sb, int tq, const u32x4& cell) {
+      const int i = 128 * hf + 32 * rw + 16 * rb + 4 * kg, sm = 16 * sb + lm;
+      char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
+      __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));
+    };
+    // tile k's g_{L-1} cells are stored during tile k + 1's data-gradient MFMAs (k_bwd_remat2's schedule)
+    for (int k = 0; k < nk; ++k) {
+      const int tl = pr + k * npair;
+      const int ptl = k > 0 ? tl - npair : tl;
+      if (k + 1 < nk) dma_g(k + 1);
+      if (k + 2 < nk) dma_enc(k + 2);
+      const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
+      const char* xb = sp + 2 * FB_GPART;
+      f32x4 ad[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) {
+          const int o = gs_off(16 * sb + lm, 4 * ks + kg);
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(sp + o);
+          const f16x8 bm = *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bh, ad[rb][sb], 0, 0, 0);
+            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bm, ad[rb][sb], 0, 0, 0);
+            ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][1], bh, ad[rb][sb], 0, 0, 0);
+          }
+          if ((ks & 1) && sb == 1) {
+            store_cell((ks >> 2) & 1, (ks >> 1) & 1, ptl, pcell[(ks >> 2) & 1][(ks >> 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int il = 32 * rw + 16 * rb + 4 * kg;
+        const f32x4 cA = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) {
+          const int sm = 16 * sb + lm;
+          const bool valid = (int64_t)tl * 32 + sm < n;
+          const f32x4 xc = *reinterpret_cast<const f32x4*>(xb + r3_xoff(sm, il >> 2));
+          f32x4 vs;   // 2^eo g_{L-1}
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            vs[q] = valid ? fmaf(ad[rb][sb][q], cA[q], -xc[q]) : 0.0f;
+            gmo = fmaxf(gmo, fabsf(vs[q]));
+          }
+          s16x4 p0, p1;
+          split2_x4(vs, p0, p1);
+          const fb_i32x2 hv = __builtin_bit_cast(fb_i32x2, p0), mv = __builtin_bit_cast(fb_i32x2, p1);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
+          pcell[rb][sb] = u32x4{s0[0], s1[0], s0[1], s1[1]};
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs (its stores may fly)
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+    }
+    if (nk > 0) {   // the last tile's cells
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) store_cell(rb, sb, pr + (nk - 1) * npair, pcell[rb][sb]);
+    }
+    gmo = wave_max_f(gmo) * gui;
+    if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rw) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
+  } else {
+    // ---- W: xc of tile k + 1; G_d rows j = 64 rw + 16 jb + lm (4 blocks) x the half's 32 encoding columns
+    f32x4 aw[4][2];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) aw[jb][ib] = f32x4{};
+    const int trq = lm >> 2, trp = lm & 3, tr0 = 8 * kg + trq, tr1 = tr0 + 4;
+    auto join = [](const s16x4& a, const s16x4& b) {
+      return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    auto eoff = [](int r, int c) { return r * 128 + 16 * ((c >> 3) ^ ((r >> 1) & 7)) + 2 * (c & 7); };
+    for (int k = 0; k < nk; ++k) {
+      if (k + 1 < nk) dma_g(k + 1);
+      if (k + 2 < nk) dma_enc(k + 2);
+      if (k + 1 < nk) remat_xc(k + 1);
+      const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
+      const unsigned ga = fb_lds_addr(sp), ea = fb_lds_addr(enb + (k % R3_ENC_SLOTS) * FB_ENC);
+      std::array<s16x4, 4> ra[4], rx[2];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const int col = 64 * rw + 16 * jb + 4 * trp;
+        const unsigned a0 = ga + gs_off(tr0, col >> 3) + 2 * (col & 7), a1 = ga + gs_off(tr1, col >> 3) + 2 * (col & 7);
+        ra[jb] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_GPART>(a0), fb_tr<FB_GPART>(a1)};
+      }
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) {
+        const int c = 32 * hf + 16 * ib + 4 * trp;
+        const unsigned a0 = ea + eoff(tr0, c), a1 = ea + eoff(tr1, c);
+        rx[ib] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_ENC / 2>(a0), fb_tr<FB_ENC / 2>(a1)};
+      }
+      fb_lgkm<0>(ra);
+      fb_lgkm<0>(rx);
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) {
+        const f16x8 B0 = join(rx[ib][0], rx[ib][1]), B1 = join(rx[ib][2], rx[ib][3]);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          const f16x8 A0 = join(ra[jb][0], ra[jb][1]), A1 = join(ra[jb][2], ra[jb][3]);
+          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0, aw[jb][ib], 0, 0, 0);
+          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1, aw[jb][ib], 0, 0, 0);
+          aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0, aw[jb][ib], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+    }
+    // this pair's G_d partial, unscaled (2^-gexp[L] of g_L, 2^-s_k of the column): Sigma_s g_L d_k
+    float* const pb = part + (size_t)pr * GD_PART;
+    const int sxyz = remat_sx(0, __uint_as_float(*pbound));
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      const int col = 32 * hf + 16 * ib + lm;
+      const float cu = ldexpf(gun, -(col < 3 ? sxyz : 13));
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pb[(size_t)(64 * rw + 16 * jb + 4 * kg + r) * 64 + col] = aw[jb][ib][r] * cu;
+    }
+  }
+  // the previous layer's G_d partials, one row per workgroup (LDS as scratch)
+  __syncthreads();
+  if (rpart) gd_reduce_row<512>(rpart, FB_PAIRS, rgd, reinterpret_cast<double*>(fb), t);
+}
+
+// after layer 1's launch: layer 1's G_d (grid.y 0) and layer 0's encoding columns from k_wgrad_enc's g_0 sets
+// (grid.y 1: dW_0, db_0), one row per block of 1024
+__global__ __launch_bounds__(1024) void k_gd_tail(const float* __restrict__ part1, double* __restrict__ gd1,
+                                                  const float* __restrict__ pe0, double* __restrict__ dW0,
+                                                  double* __restrict__ db0, int we) {
+  __shared__ double red[1024];
+  if (blockIdx.y == 0) gd_reduce_row<1024>(part1, FB_PAIRS, gd1, red, threadIdx.x);
+  else wgrad_reduce_body<1>(pe0, we, nullptr, nullptr, dW0, db0, nullptr, we, 0);
+}
+
+// dW_L[j][i] += alpha_i sum_k G_d[L][j][k] P'_{L-1}[i][k] for the chunk (float64; alpha = invstd gamma of BatchNorm
+// L-1, the Linear's input scale), L = 1..7; the skip layer also takes its encoding columns dW_4[j][k] += G_d[4][j][k]
+// (its input there is e itself).  grid (16 row blocks, 7 layers), 256 threads (column i).
+struct GdProj {
+  double* dW[8];
+  const float* coef;   // ws.coef: layer L's BatchNorm constants at 1024 L (alpha at 512)
+  const double* gd;    // [8][256][64]
+  const double* pp;    // the fold's P' maps [8][C][256][64]
+  int64_t C, ci;
+};
+__global__ __launch_bounds__(256) void k_gd_proj(GdProj g) {
+  __shared__ double gs[16][64];
+  const int L = 1 + (int)blockIdx.y, j0 = 16 * (int)blockIdx.x, i = threadIdx.x;
+  for (int idx = i; idx < 16 * 64; idx += 256)
+    gs[idx >> 6][idx & 63] = g.gd[(size_t)L * GD_LAYER + (size_t)(j0 + (idx >> 6)) * 64 + (idx & 63)];
+  __syncthreads();
+  const double* prow = g.pp + (((size_t)(L - 1) * g.C + g.ci) * 256 + i) * 64;
+  double acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+  for (int k = 0; k < 63; ++k) {
+    const double p = prow[k];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = fma(gs[j][k], p, acc[j]);
+  }
+  const double alpha = (double)g.coef[1024 * (L - 1) + 512 + i];
+  const int in_f = in_features(L), wc = L == 4 ? 63 : 0;
+  double* const dW = g.dW[L];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dW[(size_t)(j0 + j) * in_f + wc + i] += alpha * acc[j];
+  if (L == 4 && i < 63) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dW[(size_t)(j0 + j) * in_f + i] += gs[j][i];
+  }
+}
+
 // k_wgrad_enc: the encoding columns of dW_0 and of the skip layer's dW_4, G = sum_s g (x) d, from the PRE-SPLIT g_0 and
 // g_4 images (k_bwd_remat2's output layout, gs_off) and the chunk's encoding image (k_remat_enc: d = e - ebar, fb_eoff),
 // DMA'd straight into LDS -- no sincos, no conversion.  d in place of e: sum_s g_L = 0 exactly (BatchNorm follows
@@ -4152,8 +4584,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_enc(const char* __restrict__ g
   extern __shared__ __attribute__((aligned(16))) char wel[];
   const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int bid = (int)blockIdx.x, src = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
-  const int npair = (int)gridDim.x >> 1;
+  // g4 null (the default, k_bwd_remat3 takes the skip layer's encoding columns): every workgroup its own tiles of
+  // g_0 and its own partial set; otherwise the pairs split by source
+  const bool one = g4 == nullptr;
+  const int bid = (int)blockIdx.x, src = one ? 0 : (bid >> 3) & 1;
+  const int pr = one ? bid : ((bid >> 4) << 3) | (bid & 7);
+  const int npair = one ? (int)gridDim.x : (int)gridDim.x >> 1;
   const int nt = (int)((n + 31) / 32);
   const int nk = pr < nt ? (nt - 1 - pr) / npair + 1 : 0;
   const char* const gsrc = src == 0 ? g0 : g4;
@@ -4308,6 +4744,7 @@ struct BwdWs {
   int* gexp;          // rematerialised backward: scale exponents of the pre-split g images, per layer
   unsigned* gm7;      // rematerialised backward: |g_7| maximum slots (k_g7)
   float* wcol;        // rematerialised backward: column abs sums of W_1..W_7 (k_wcol)
+  double* gd;         // k_bwd_remat3: the chunk's G_d = sum_s g_L (x) d per layer [8][256][64]
   size_t bytes;
 };
 
@@ -4339,6 +4776,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   const size_t oocst = take(4 * 256 * sizeof(float));
   const size_t ogexp = take(16 * sizeof(int)), ogm7 = take(GMAX_SLOTS * sizeof(unsigned));
   const size_t owcol = take(7 * 256 * sizeof(float));
+  const size_t ogd = take(8 * (size_t)GD_LAYER * sizeof(double));
   char* b = (char*)base;
   BwdWs w;
   w.wth = (f16x8*)(b + owt);
@@ -4365,6 +4803,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
   w.gexp = (int*)(b + ogexp);
   w.gm7 = (unsigned*)(b + ogm7);
   w.wcol = (float*)(b + owcol);
+  w.gd = (double*)(b + ogd);
   w.bytes = off;
   return w;
 }
@@ -4503,6 +4942,56 @@ static void fused_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                      ws.gacc + G.w[4], FB_PAIRS, (int)we);
 }
 
+// k_bwd_remat3's layers of one chunk (after k_g7): layers 7..1 (each launch's tail sums the previous layer's G_d
+// partials into ws.gd), k_wgrad_enc on g_0 alone, k_gd_tail (layer 1's G_d, dW_0), k_gd_proj (every layer's
+// dW_L += alpha (G_d P'^T), and the skip layer's encoding columns)
+template <class PR, class PS>
+static void remat3_layers(const NofParamsDev& P, const GaccLayout& G, const BwdWs& ws, const FoldBnBwd& FB, const f16x8*,
+                          const float*, int64_t ci, int64_t n, const float*, hipStream_t s, char* encimg,
+                          const PR& prow, const PS& psrow, char* const (&S)[2], char* S2, float* const (&pset)[2]) {
+  const double dn = (double)n;
+  const int64_t ntiles = (n + 31) / 32;
+  const unsigned fbg = (unsigned)(2 * FB_PAIRS);
+  for (int L = 7; L >= 1; --L) {
+    const float* coefp = ws.coef + 1024 * (L - 1);
+    const char* gin = L == 4 ? S2 : S[(7 - L) & 1];
+    char* gout = L == 5 ? S2 : S[(8 - L) & 1];
+    const unsigned* gmin = L == 7 ? ws.gm7 : ws.gmax + L * GMAX_SLOTS;
+    const float* rpart = L < 7 ? pset[(L + 1) & 1] : nullptr;
+    double* rgd = ws.gd + (size_t)(L + 1) * GD_LAYER;
+    // algorithmic work: the layer's backward as written, data gradient (2 x 256 x 256) + weight gradient
+    // (2 x 256 x 256: G_L = sum g (x) x, formed here as (sum g (x) d) P'^T); issued on the matrix pipe per sample:
+    // 2 x 256 x 256 + 2 x 256 x 64 (G_d) + 2 x 256 x 64 (x), x 3 products.  Bytes: g_L in (1 KiB), the encoding
+    // image (256 B), g_{L-1} out (1 KiB)
+    ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0) * dn, (1024.0 + 256.0 + 1024.0) * dn);
+    hipLaunchKernelGGL(k_bwd_remat3, dim3(fbg), dim3(512), R3_LDS, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,
+                       (const int*)ws.sw, L, n, coefp, (const float*)(ws.bnb + 512 * (L - 1)), P.bn_w[L - 1],
+                       ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
+                       pset[L & 1], rpart, rgd, (const char*)encimg, prow(L - 1), psrow(L - 1),
+                       (const unsigned*)ws.pbound);
+  }
+  const int ne = (int)std::min<int64_t>(ntiles, 2 * FB_PAIRS);   // g_0's partial sets (one per workgroup)
+  float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
+  {
+    // 2 x 256 x 64 fp32-FLOP per sample; 1 KiB of g + 256 B of encoding in
+    ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, (1024.0 + 256.0) * dn);
+    hipLaunchKernelGGL(k_wgrad_enc, dim3(2 * FB_PAIRS), dim3(512), WE_LDS, s, (const char*)S[1], (const char*)nullptr,
+                       (const char*)encimg, n, (const int*)ws.gexp, (const unsigned*)ws.pbound, part_e0,
+                       (float*)nullptr);
+  }
+  ProfScope ps(s, PT_BWD_MISC, 0.0, (double)FB_PAIRS * GD_PART * 4.0 + ne * WgradCfg<1>::PART * 4.0);
+  hipLaunchKernelGGL(k_gd_tail, dim3(256, 2), dim3(1024), 0, s, (const float*)pset[1], ws.gd + GD_LAYER,
+                     (const float*)part_e0, ws.gacc + G.w[0], ws.gacc + G.b[0], ne);
+  GdProj gp;
+  for (int L = 0; L < 8; ++L) gp.dW[L] = ws.gacc + G.w[L];
+  gp.coef = ws.coef;
+  gp.gd = ws.gd;
+  gp.pp = FB.pp;
+  gp.C = FB.C;
+  gp.ci = ci;
+  hipLaunchKernelGGL(k_gd_proj, dim3(16, 7), dim3(256), 0, s, gp);
+}
+
 // One chunk through the rematerialised backward (no activation store): max |dL/dlogit|, k_fb_prep on the fold's
 // statistics, the chunk's encoding image, g_7 (k_g7), layers 7..1 each in ONE k_bwd_remat2 launch, the encoding
 // columns of layers 0 and 4 (k_wgrad_enc on the pre-split g_0 and g_4 and the encoding image), the last partial sums.
@@ -4517,6 +5006,8 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                                 (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat3, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)R3_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_enc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WE_LDS));
     pcn_attr_done(attr);
@@ -4558,6 +5049,10 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   }
   const unsigned fbg = (unsigned)(2 * FB_PAIRS);
   float* const pset[2] = {ws.part, ws.part + (size_t)FB_PAIRS * WgradCfg<2>::PART};
+  if (g_remat_ver == 3) {
+    remat3_layers(P, G, ws, FB, pimg, pscl, ci, n, grad, s, encimg, prow, psrow, S, S2, pset);
+    return;
+  }
   for (int L = 7; L >= 1; --L) {
     const float* coefp = ws.coef + 1024 * (L - 1);
     FbRed red{nullptr, nullptr, nullptr, nullptr, 0};

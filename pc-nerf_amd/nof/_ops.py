@@ -122,6 +122,21 @@ TRAIN_MATH = {"fp32": 0, "f16x2_3": 1, "f16x2_4": 2, "f16x2_3_fused": 1}
 _TRAIN_FUSED = True   # the library's own default is mode 1 (f16x2_3)
 
 
+def set_remat_version(version: int) -> int:
+    """Select the default training backward's layer kernel (3: k_bwd_remat3, the default; 2: k_bwd_remat2); returns
+    the previous one (pcnerf_set_remat_version)."""
+    prev = H.lib().pcnerf_set_remat_version(int(version))
+    if prev < 0:
+        raise RuntimeError(H.lib().pcnerf_last_error().decode())
+    return prev
+
+
+def get_remat_version() -> int:
+    v = set_remat_version(3)
+    set_remat_version(v)
+    return v
+
+
 def set_train_math(mode: str) -> str:
     """Select the train-mode layer arithmetic; returns the previous mode's name."""
     global _TRAIN_FUSED

@@ -67,17 +67,20 @@ def named(m):
     return dict(m.named_parameters())
 
 
-@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused", "f16x2_3_fused_store"])
+@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused", "f16x2_3_fused_remat2", "f16x2_3_fused_store"])
 def train_math(request):
-    """The layered split math, fp32 MFMA, the default (fused forward + rematerialising backward) and the default
-    forward with round 4's activation-store backward."""
+    """The layered split math, fp32 MFMA, the default (fused forward + rematerialising backward, k_bwd_remat3), the
+    same with round 5's layer kernel (k_bwd_remat2) and the default forward with round 4's activation-store
+    backward."""
     from nof import _ops
     mode = request.param
     prev = _ops.set_train_math("f16x2_3_fused" if mode.startswith("f16x2_3_fused") else mode)
     prevb = _ops.set_train_backward("store" if mode.endswith("_store") else "remat")
+    prevr = _ops.set_remat_version(2 if mode.endswith("_remat2") else 3)
     yield mode
     _ops.set_train_math(prev)
     _ops.set_train_backward(prevb)
+    _ops.set_remat_version(prevr)
 
 
 @pytest.mark.parametrize("name", ["pcnerf", "divide", "original"])
@@ -338,15 +341,9 @@ def test_train_grads_vs_oracle_small_chunks(train_math):
     lr, lrf = range_losses(res["depth"], res["depth_fine"], rays[:, 14], rays, 0, 32)
     total(res, lr, lrf).sum().backward()
     pc, pf = named(mc), named(mf)
-    try:
-        check_grads_elem(lambda k: pc[k].grad.cpu().numpy(), list(pc), gc, "", f"oracle_chunk1000_{train_math}",
-                         noise=NOISE)
-        check_grads_elem(lambda k: pf[k].grad.cpu().numpy(), list(pf), gf, "", f"oracle_chunk1000_{train_math}",
-                         noise=NOISE)
-    except AssertionError:
-        if train_math != "fp32":
-            raise
-        # worst error / tolerance measured: remat 0.70, store 0.71, layered split 0.82, fp32 MFMA 1.20
-        pytest.xfail("fp32 MFMA layered math: dW_0 contracted over the uncentered encoding, so the rounding noise "
-                     "of sum_s g_0 (exactly 0) times the encoding mean reaches it; at 1,000-sample chunks 2 of 2,048 "
-                     "sampled entries sit at 1.2 x the float32 oracle's envelope around float64")
+    # (no xfail branch: the fp32 MFMA layered math contracts the encoding columns around the chunk's first sample,
+    # k_wgrad, so the rounding noise of sum_s g_0 -- exactly 0 -- no longer multiplies the encoding's magnitude)
+    check_grads_elem(lambda k: pc[k].grad.cpu().numpy(), list(pc), gc, "", f"oracle_chunk1000_{train_math}",
+                     noise=NOISE)
+    check_grads_elem(lambda k: pf[k].grad.cpu().numpy(), list(pf), gf, "", f"oracle_chunk1000_{train_math}",
+                     noise=NOISE)
