@@ -11,8 +11,8 @@ the reference's optimizer step (Adam lr 5e-4, eps 1e-8, weight_decay 1e-3 over b
 13-column rows grouped per LiDAR ray; value counts LiDAR rays (groups).
 
 The other BASELINE configs (--config):
-  3  KITTI-00 training loop: train_step at 262,144 rays/iter and 64/128 samples on the KITTI-00 fixture scene's
-     rays (nof.dataset on tests/golden/kitti_frames.npz, batch drawn with replacement); with N GPUs each rank takes
+  3  KITTI-00 training loop: train_step at 262,144 rays/iter and 64/128 samples on frames 1151-1200 at 50 % frame
+     sparsity (nof.dataset on tests/golden/kitti_frames_full.npz, batch drawn with replacement); with N GPUs each rank takes
      262,144 rays of a data-parallel step and the gradients are averaged over RCCL (nof.blocks.allreduce_grads);
   4  MaiCity-00 bounds split into 4 parent blocks (own weights, 262,144 rays each, 128/256 samples), train_fwd,
      blocks dealt over the ranks, every block's depths gathered to rank 0 over RCCL (strong scaling: 1M rays/iter);
@@ -209,12 +209,14 @@ def pmc_traffic(kernel_name: str, line: str = None):
 
 # ----------------------------------------------------------------------------------------------- workloads
 def kitti_fixture_rays(dev):
-    """The KITTI-00 fixture scene's train rays (tests/golden/kitti_frames.npz: scans 1151..1156, every 40th point),
-    built on the GPU by nof.dataset exactly as the parity tests build them."""
+    """BASELINE config 3's scene: KITTI-00 scans 1151..1200 (tests/golden/kitti_frames_full.npz, every 16th point)
+    at the 50 % frame-sparsity rule (25 train frames, 157,108 rows), its train rays built on the GPU by nof.dataset
+    exactly as the parity test builds them (tests/golden/make_config3_full.py)."""
     import tempfile
     from nof import dataset as D
     from nof import io as nio
-    g = dict(np.load(os.path.join(HERE, "tests", "golden", "kitti_frames.npz"), allow_pickle=False))
+    g = dict(np.load(os.path.join(HERE, "tests", "golden", "kitti_frames_full.npz"), allow_pickle=False))
+    sc = dict(np.load(os.path.join(HERE, "tests", "golden", "config3_full_scene.npz"), allow_pickle=False))
     with tempfile.TemporaryDirectory() as tmp:
         os.makedirs(os.path.join(tmp, "pcd"))
         for k, v in g.items():
@@ -225,12 +227,13 @@ def kitti_fixture_rays(dev):
                 fh.write("1 0 0 0 0 1 0 0 0 0 1 0\n")
             for row in g["poses"]:
                 fh.write(" ".join(repr(float(v)) for v in row) + "\n")
-        ds = D.kitti_dataload(os.path.join(tmp, "pcd"), split="train", data_start=1150, data_end=1155,
-                              cloud_size_val=64, range_delete_x=3, range_delete_y=2, range_delete_z=1.25,
-                              sub_nerf_test_num=0, surface_expand=0.05, over_height=0.168, over_low=-2.0,
-                              interest_x=20.0, interest_y=20.0, pose_path=os.path.join(tmp, "poses.txt"),
-                              re_loaddata=1, result_path=os.path.join(tmp, "out"), device=dev)
-    return ds.rays
+        ds = D.kitti_dataload(os.path.join(tmp, "pcd"), split="train", data_start=int(sc["data_start"]),
+                              data_end=int(sc["data_end"]), cloud_size_val=64, range_delete_x=3, range_delete_y=2,
+                              range_delete_z=1.25, sub_nerf_test_num=0, surface_expand=0.05, over_height=0.168,
+                              over_low=-2.0, interest_x=20.0, interest_y=20.0, pose_path=os.path.join(tmp, "poses.txt"),
+                              re_loaddata=1, result_path=os.path.join(tmp, "out"), device=dev,
+                              sparsity=int(sc["sparsity"]))
+    return ds.rays, int(sc["children"])
 
 
 def make_blocks(a, rank, world, dev, syn):
@@ -248,12 +251,12 @@ def make_blocks(a, rank, world, dev, syn):
                             groups=int((vr[s:e, 12] >= -0.5).sum())))
         return out
     if a.config == 3:
-        scene = kitti_fixture_rays(dev)
+        scene, n_child = kitti_fixture_rays(dev)
         gen = torch.Generator(device=dev).manual_seed(rank)
         idx = torch.randint(0, scene.shape[0], (a.rays,), device=dev, generator=gen)
         rays = scene[idx].contiguous()
         return [dict(block=0, rays=rays, other=None, gt=rays[:, 14].contiguous(), seeds=(1234, 5678),
-                     sub_num=1171, scene=scene)]
+                     sub_num=n_child, scene=scene)]
     n_blocks = {2: world, 4: 4, 5: 8}[a.config]
     for b in blocks_of_rank(rank, world, n_blocks):
         seeds = (1234 + b, 5678 + b)
@@ -676,8 +679,8 @@ def line_json(a, world, ln):
         # every tensor and every accumulation is fp32; the Linear layers' products as the selected math forms them
         "dtype": dtype_label(ln["train_math"], ln["eval_math"], a.fold),
         "data": {2: "synthetic (config-2 parent block, 32 child AABBs; seeded NOF weights -- checkpoints absent)",
-                 3: "KITTI-00 fixture scene (scans 1151-1156, every 40th point) rays built by nof.dataset, "
-                    "262,144-ray batches drawn with replacement; seeded NOF weights",
+                 3: "KITTI-00 frames 1151-1200 at 50% frame sparsity (every 16th point) rays built by "
+                    "nof.dataset, 262,144-ray batches drawn with replacement; seeded NOF weights",
                  4: "synthetic MaiCity-00 parent blocks (x-split of [-12,61]x[-12,12]x[-2,0.5], 256 child AABBs "
                     "each); seeded per-block NOF weights",
                  5: "synthetic two-step rows (group-size histogram of the reference's KITTI test frames), 8 "

@@ -250,6 +250,12 @@ int pcnerf_sample_coarse(const float* rays, int64_t n_rays, int ray_stride, int 
 int pcnerf_perturb(const float* z, int64_t n_rays, int n_samples, float perturb, const float* rand, float* z_out,
                    void* stream);
 
+/* The compositing kernels' ray group, process-wide; returns the previous setting, or -1 for an invalid one.
+ * 0 (default): a whole 256-thread workgroup per ray when the batch has fewer than 2,048 rays of >= 512 samples (the
+ * reference shell's 256 rays x 2,304 fine samples: all CUs busy, 9 samples per thread), one wave per ray otherwise;
+ * 64 / 256 force either (A/B, tests).  Same results: every sum and scan runs in float64 and rounds once. */
+int pcnerf_set_composite_group(int group);
+
 /* ---------------------------------------------------------------- compositing + child losses
  * (render.py:51-61 and :75-159).  Per ray: w = p * cumprod(1-p) (+ noise_std*noise if noise != NULL),
  * w /= sum(w) + eps; depth = sum(w z).  If `rays` != NULL, also the child masks (inclusive, expansion

@@ -149,10 +149,97 @@ __device__ __forceinline__ double wave_excl_sum(double v, int lane) {
   return lane == 0 ? 0.0 : ex;
 }
 
+// A ray's compositing group: one wave (G = 64, four rays per 256-thread workgroup: the many-ray batches) or one
+// whole workgroup (G = 256: batches of a few hundred long rays, e.g. the reference shell's 256 rays x 2,304 fine
+// samples, where a wave per ray kept 64 of 256 CUs busy and 36 samples per lane spilled).  Thread t of the group
+// holds samples t B .. t B + B - 1; the group primitives below combine the per-thread values -- wave shuffles, and
+// for G = 256 the four waves' partials through LDS (sh: 8 doubles).
+template <int G>
+struct Grp {
+  static_assert(G == 64 || G == 256, "one wave or one 256-thread workgroup per ray");
+  static constexpr int NW = G / 64;
+  __device__ static int tid() { return G == 64 ? (int)(threadIdx.x & 63) : (int)threadIdx.x; }
+  __device__ static int64_t ray() {
+    return G == 64 ? (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
+  }
+  __device__ static double sum(double v, double* sh) {
+    v = wave_sum_d(v);
+    if constexpr (G == 64) {
+      return v;
+    } else {
+      if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+      __syncthreads();
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) t += sh[i];
+      __syncthreads();
+      return t;
+    }
+  }
+  // exclusive product over the group's threads in order
+  __device__ static double excl_prod(double v, double* sh) {
+    const int lane = threadIdx.x & 63;
+    const double ex = wave_excl_prod(v, lane);
+    if constexpr (G == 64) {
+      return ex;
+    } else {
+      const int w = threadIdx.x >> 6;
+      const double tot = __shfl(ex * v, 63, 64);
+      if (lane == 0) sh[w] = tot;
+      __syncthreads();
+      double base = 1.0;
+      for (int i = 0; i < w; ++i) base *= sh[i];
+      __syncthreads();
+      return base * ex;
+    }
+  }
+  __device__ static bool any(bool b) {
+    if constexpr (G == 64) return __any(b);
+    else return __syncthreads_or(b ? 1 : 0) != 0;
+  }
+  __device__ static float bcast(float v, int src, double* sh) {
+    if constexpr (G == 64) {
+      return __shfl(v, src, 64);
+    } else {
+      if ((int)threadIdx.x == src) sh[0] = (double)v;
+      __syncthreads();
+      const float r = (float)sh[0];
+      __syncthreads();
+      return r;
+    }
+  }
+  // U entering each thread's block from above: the composition of threads t + 1 .. G - 1's affine maps
+  // (Y = A + Bm Y_next) applied to 0
+  __device__ static double suffix_affine(double A, double Bm, double* sh) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double An = __shfl_down(A, o, 64), Bn = __shfl_down(Bm, o, 64);
+      if (lane + o < 64) {
+        A = A + Bm * An;
+        Bm = Bm * Bn;
+      }
+    }
+    double Y = 0.0;   // entering this wave's last lane
+    if constexpr (G == 256) {
+      const int w = threadIdx.x >> 6;
+      if (lane == 0) {
+        sh[w] = A;
+        sh[4 + w] = Bm;
+      }
+      __syncthreads();
+      for (int i = NW - 1; i > w; --i) Y = sh[i] + sh[4 + i] * Y;
+      __syncthreads();
+    }
+    const double An1 = __shfl_down(A, 1, 64), Bn1 = __shfl_down(Bm, 1, 64);
+    return lane == 63 ? Y : An1 + Bn1 * Y;
+  }
+};
+
 // Smallest thr = thr0 + k*0.01 (Python float64 accumulation) for which a sample of the ray lies in
 // [fl32(near - fl32(thr)), fl32(far + fl32(thr))] (inclusive: render.py:80-84,94-97) or the open interval
 // (strict: render.py:255-263).  Returns fl32 bounds.
-template <bool STRICT, int MAXB>
+template <bool STRICT, int MAXB, int G = 64>
 __device__ __forceinline__ void expand_bounds(const float (&zv)[MAXB], int nb, float near, float far, double thr0,
                                               float& lo, float& hi, int* err) {
   double thr = thr0;
@@ -164,7 +251,7 @@ __device__ __forceinline__ void expand_bounds(const float (&zv)[MAXB], int nb, f
 #pragma unroll
     for (int j = 0; j < MAXB; ++j)
       if (j < nb) any |= STRICT ? (lo < zv[j] && zv[j] < hi) : (lo <= zv[j] && zv[j] <= hi);
-    if (__any(any)) return;
+    if (Grp<G>::any(any)) return;
     thr = thr + 0.01;
   }
   if (err) *err = 1;
@@ -345,7 +432,7 @@ __global__ __launch_bounds__(256) void k_depth2_ties(const float* __restrict__ W
   }
 }
 
-template <int MAXB>
+template <int MAXB, int G>
 __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, const float* __restrict__ Z,
                                                    int64_t n_rays, int S, const float* __restrict__ noise,
                                                    float noise_std, float eps, const float* __restrict__ rays,
@@ -354,10 +441,12 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
                                                    float* __restrict__ free_ray, float* __restrict__ sl1_ray,
                                                    double* __restrict__ opac_row, float* __restrict__ depth2,
                                                    int* __restrict__ err) {
-  const int lane = threadIdx.x & 63;
-  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (ray >= n_rays) return;
-  const int B = (S + 63) / 64;
+  using Gp = Grp<G>;
+  __shared__ double gsh[8];
+  const int lane = Gp::tid();
+  const int64_t ray = Gp::ray();
+  if (ray >= n_rays) return;   // (G = 256: one workgroup per ray, never taken)
+  const int B = (S + G - 1) / G;
   const int i0 = lane * B;
   const int nb = max(0, min(B, S - i0));
   const float* pr = P + ray * S + i0;
@@ -376,7 +465,7 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
     }
   }
   // transmittance: cumprod of [1, 1-p] in float64, each prefix rounded to fp32 (render.py:52-55)
-  double T = wave_excl_prod(loc, lane);
+  double T = Gp::excl_prod(loc, gsh);
   double sw = 0.0;
 #pragma unroll
   for (int j = 0; j < MAXB; ++j) {
@@ -390,7 +479,7 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
       wv[j] = 0.0f;
     }
   }
-  const float den = (float)wave_sum_d(sw) + eps;  // render.py:60
+  const float den = (float)Gp::sum(sw, gsh) + eps;  // render.py:60
   double sd = 0.0;
 #pragma unroll
   for (int j = 0; j < MAXB; ++j) {
@@ -399,7 +488,7 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
       sd += (double)(wv[j] * zv[j]);
     }
   }
-  const float d = (float)wave_sum_d(sd);
+  const float d = (float)Gp::sum(sd, gsh);
   if (Wout) {
     float* wr = Wout + ray * S + i0;
 #pragma unroll
@@ -412,7 +501,7 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
 #pragma unroll
     for (int j = 0; j < MAXB; ++j)
       if (j < nb) op += (double)((logf(0.1f + pv[j]) + logf(0.1f + (1.0f - pv[j]))) + 2.20727f);
-    op = wave_sum_d(op);
+    op = Gp::sum(op, gsh);
     if (lane == 0) opac_row[ray] = op;
   }
   if (depth2) {  // render.py:598-600: z at the position of sample S-1 in argsort(w, descending=True)
@@ -425,13 +514,12 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
 #pragma unroll
     for (int j = 0; j < MAXB; ++j)
       if (j == last_j) wl = wv[j];
-    wl = __shfl(wl, last_lane, 64);
+    wl = Gp::bcast(wl, last_lane, gsh);
     int cnt = 0;
 #pragma unroll
     for (int j = 0; j < MAXB; ++j)
       if (j < nb && i0 + j < S - 1) cnt += kv_desc(wv[j], wl) || !kv_desc(wl, wv[j]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    cnt = (int)Gp::sum((double)cnt, gsh);
     if (lane == 0) depth2[ray] = Z[ray * S + cnt];
   }
   if (!rays) return;
@@ -440,8 +528,8 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
   const float* r = rays + ray * stride;
   const float cn = r[cn_col], cf = r[cf_col], rg = r[rg_col];
   float lo0, hi0, lo2, hi2;
-  expand_bounds<false, MAXB>(zv, nb, cn, cf, 0.0, lo0, hi0, err);
-  expand_bounds<false, MAXB>(zv, nb, cn, cf, 2.0, lo2, hi2, err);
+  expand_bounds<false, MAXB, G>(zv, nb, cn, cf, 0.0, lo0, hi0, err);
+  expand_bounds<false, MAXB, G>(zv, nb, cn, cf, 2.0, lo2, hi2, err);
   double fr = 0.0, sc = 0.0;
 #pragma unroll
   for (int j = 0; j < MAXB; ++j) {
@@ -453,7 +541,7 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
       sc += (double)(wv[j] * (m2 ? 1.0f : 0.0f));
     }
   }
-  const float denc = (float)wave_sum_d(sc) + eps;  // render.py:129
+  const float denc = (float)Gp::sum(sc, gsh) + eps;  // render.py:129
   double dcs = 0.0;
 #pragma unroll
   for (int j = 0; j < MAXB; ++j) {
@@ -463,8 +551,8 @@ __global__ __launch_bounds__(256) void k_composite(const float* __restrict__ P, 
       dcs += (double)(wc * (zv[j] * m2));
     }
   }
-  const float dc = (float)wave_sum_d(dcs);
-  const float frs = (float)wave_sum_d(fr);
+  const float dc = (float)Gp::sum(dcs, gsh);
+  const float frs = (float)Gp::sum(fr, gsh);
   if (lane == 0) {
     free_ray[ray] = frs;
     sl1_ray[ray] = smooth_l1(10.0f * dc, 10.0f * rg);
@@ -890,17 +978,19 @@ __global__ void k_pointwise_loss_bwd(const float* __restrict__ a, const float* _
 // p saturates at 1): each lane composes the map over its block, a wave suffix scan composes the lanes.
 // Child terms: free = sum (w*!M0)^2 / R (or per child / count), depth loss c * mean SL1(10 dc, 10 range),
 // dc = sum_j w_j M2_j z_j / (sum w M2 + eps).
-template <int MAXB>
+template <int MAXB, int G>
 __global__ __launch_bounds__(256) void k_composite_bwd(
     const float* __restrict__ P, const float* __restrict__ Z, int64_t n_rays, int S, const float* __restrict__ noise,
     float noise_std, float eps, const float* __restrict__ rays, int stride, int cn_col, int cf_col, int rg_col,
     int cid_col, int n_child, const double* __restrict__ counts, const float* __restrict__ g_depth,
     const float* __restrict__ g_free, const float* __restrict__ g_dl, float* __restrict__ g_logit,
     int* __restrict__ err) {
-  const int lane = threadIdx.x & 63;
-  const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (ray >= n_rays) return;
-  const int B = (S + 63) / 64;
+  using Gp = Grp<G>;
+  __shared__ double gsh[8];
+  const int lane = Gp::tid();
+  const int64_t ray = Gp::ray();
+  if (ray >= n_rays) return;   // (G = 256: one workgroup per ray, never taken)
+  const int B = (S + G - 1) / G;
   const int i0 = lane * B;
   const int nb = max(0, min(B, S - i0));
   const float* pr = P + ray * S + i0;
@@ -918,7 +1008,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
       zv[j] = 0.0f;
     }
   }
-  double T = wave_excl_prod(loc, lane);
+  double T = Gp::excl_prod(loc, gsh);
   double sw = 0.0;
 #pragma unroll
   for (int j = 0; j < MAXB; ++j) {
@@ -933,7 +1023,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
       T *= (double)(1.0f - pv[j]);
     }
   }
-  const float den = (float)wave_sum_d(sw) + eps;
+  const float den = (float)Gp::sum(sw, gsh) + eps;
 #pragma unroll
   for (int j = 0; j < MAXB; ++j)
     if (j < nb) wv[j] = wv[j] / den;
@@ -961,8 +1051,8 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
       }
     }
     float lo0, hi0, lo2, hi2;
-    expand_bounds<false, MAXB>(zv, nb, cn, cf, 0.0, lo0, hi0, err);
-    expand_bounds<false, MAXB>(zv, nb, cn, cf, 2.0, lo2, hi2, err);
+    expand_bounds<false, MAXB, G>(zv, nb, cn, cf, 0.0, lo0, hi0, err);
+    expand_bounds<false, MAXB, G>(zv, nb, cn, cf, 2.0, lo2, hi2, err);
     double sc = 0.0;
 #pragma unroll
     for (int j = 0; j < MAXB; ++j) {
@@ -971,7 +1061,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
         sc += (double)(wv[j] * (m2 ? 1.0f : 0.0f));
       }
     }
-    const float denc = (float)wave_sum_d(sc) + eps;
+    const float denc = (float)Gp::sum(sc, gsh) + eps;
     double dcs = 0.0;
 #pragma unroll
     for (int j = 0; j < MAXB; ++j) {
@@ -981,7 +1071,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
         dcs += (double)(wc * (zv[j] * m2));
       }
     }
-    const float dc = (float)wave_sum_d(dcs);
+    const float dc = (float)Gp::sum(dcs, gsh);
     const float x = 10.0f * dc - 10.0f * rg;
     const double sl1g = fabsf(x) < 1.0f ? (double)x : (x > 0.0f ? 1.0 : -1.0);  // SmoothL1 (beta 1) derivative
     const double gdc = kd * sl1g;
@@ -1000,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
 #pragma unroll
   for (int j = 0; j < MAXB; ++j)
     if (j < nb) dot += gw[j] * (double)wv[j];
-  dot = wave_sum_d(dot);
+  dot = Gp::sum(dot, gsh);
   const double rden = 1.0 / (double)den;
 #pragma unroll
   for (int j = 0; j < MAXB; ++j) gw[j] = (gw[j] - dot) * rden;  // now dL/dw~
@@ -1014,17 +1104,8 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
       Bm = b * Bm;
     }
   }
-  // suffix composition over lanes: Y_L = A_L + B_L * Y_{L+1}
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double An = __shfl_down(A, o, 64), Bn = __shfl_down(Bm, o, 64);
-    if (lane + o < 64) {
-      A = A + Bm * An;
-      Bm = Bm * Bn;
-    }
-  }
-  double U = __shfl_down(A, 1, 64);
-  if (lane == 63) U = 0.0;
+  // suffix composition over the group's threads: Y_t = A_t + B_t Y_{t+1}
+  double U = Gp::suffix_affine(A, Bm, gsh);
   float* go = g_logit + ray * S + i0;
 #pragma unroll
   for (int j = MAXB - 1; j >= 0; --j) {
@@ -1055,6 +1136,25 @@ extern "C" int pcnerf_abi_version(void) { return PCNERF_ABI_VERSION; }
 extern "C" const char* pcnerf_last_error(void) { return g_last_error.c_str(); }
 
 static inline unsigned nblk(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+// a workgroup per ray (Grp<256>) when a wave per ray would leave most CUs idle: fewer rays than two 4-ray workgroups
+// per CU (2048), with rows long enough (>= 512 samples) that 256 threads each hold >= 2 of them.  Override for
+// A/B: pcnerf_set_composite_group(64 | 256 | 0 = this rule).
+static int g_comp_group = 0;
+static inline bool composite_block_per_ray(int64_t n_rays, int n_samples) {
+  if (g_comp_group == 64) return false;
+  if (g_comp_group == 256) return true;
+  return n_rays < 2048 && n_samples >= 512;
+}
+extern "C" int pcnerf_set_composite_group(int g) {
+  if (g != 0 && g != 64 && g != 256) {
+    pcn::set_error("pcnerf_set_composite_group: 0 (automatic), 64 (a wave per ray) or 256 (a workgroup per ray)");
+    return -1;
+  }
+  const int prev = g_comp_group;
+  g_comp_group = g;
+  return prev;
+}
 
 extern "C" int pcnerf_sample_coarse(const float* rays, int64_t n_rays, int ray_stride, int near_col, int far_col,
                                     int child_near_col, int child_far_col, int n_samples, int n_parent,
@@ -1112,24 +1212,36 @@ extern "C" int pcnerf_composite(const float* p, const float* z, int64_t n_rays, 
   PCN_CHECK(!depth2 || g_depth2_order == 0 || n_samples <= 2048,
             "pcnerf_composite: depth2 in torch CPU's tie order (pcnerf_set_depth2_order(1)) supports at most 2048 "
             "samples per ray");
-  const int B = (n_samples + 63) / 64;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 g(nblk(n_rays, 4)), b(256);
+  const dim3 b(256);
   const double ns = (double)n_rays * n_samples;
   ProfScope ps(s, PT_COMPOSITE, 0.0, ns * (weights ? 12.0 : 8.0) + (rays ? 60.0 * n_rays : 0.0) + 12.0 * n_rays);
-#define PCN_COMP(MB)                                                                                          \
-  hipLaunchKernelGGL(k_composite<MB>, g, b, 0, s, p, z, n_rays, n_samples, noise, noise_std, eps, rays,      \
-                     ray_stride, child_near_col, child_far_col, range_col, weights, depth, free_ray, sl1_ray, \
-                     opac_row, depth2, (int*)nullptr)
-  if (B <= 2) PCN_COMP(2);
-  else if (B <= 6) PCN_COMP(6);
-  else if (B <= 16) PCN_COMP(16);
-  else if (B <= 64) PCN_COMP(64);
-  else if (B <= 256) PCN_COMP(256);
-  else PCN_CHECK(false, "pcnerf_composite: more than 16384 samples per ray");
+#define PCN_COMP(MB, G, GRID)                                                                                 \
+  hipLaunchKernelGGL((k_composite<MB, G>), GRID, b, 0, s, p, z, n_rays, n_samples, noise, noise_std, eps,     \
+                     rays, ray_stride, child_near_col, child_far_col, range_col, weights, depth, free_ray,    \
+                     sl1_ray, opac_row, depth2, (int*)nullptr)
+  if (composite_block_per_ray(n_rays, n_samples)) {
+    const int B = (n_samples + 255) / 256;
+    const dim3 g((unsigned)n_rays);
+    if (B <= 2) PCN_COMP(2, 256, g);
+    else if (B <= 6) PCN_COMP(6, 256, g);
+    else if (B <= 16) PCN_COMP(16, 256, g);
+    else if (B <= 64) PCN_COMP(64, 256, g);
+    else PCN_CHECK(false, "pcnerf_composite: more than 16384 samples per ray");
+  } else {
+    const int B = (n_samples + 63) / 64;
+    const dim3 g(nblk(n_rays, 4));
+    if (B <= 2) PCN_COMP(2, 64, g);
+    else if (B <= 6) PCN_COMP(6, 64, g);
+    else if (B <= 16) PCN_COMP(16, 64, g);
+    else if (B <= 64) PCN_COMP(64, 64, g);
+    else if (B <= 256) PCN_COMP(256, 64, g);
+    else PCN_CHECK(false, "pcnerf_composite: more than 16384 samples per ray");
+  }
 #undef PCN_COMP
   if (depth2 && g_depth2_order == 1)   // rows whose w[S-1] ties: torch CPU's order of equal keys
-    hipLaunchKernelGGL(k_depth2_ties, g, b, (size_t)8 * 4 * n_samples, s, weights, z, n_rays, n_samples, depth2);
+    hipLaunchKernelGGL(k_depth2_ties, dim3(nblk(n_rays, 4)), b, (size_t)8 * 4 * n_samples, s, weights, z, n_rays,
+                       n_samples, depth2);
   PCN_LAUNCH_CHECK("pcnerf_composite");
   PCN_API_END
 }
@@ -1284,19 +1396,29 @@ extern "C" int pcnerf_composite_backward(const float* p, const float* z, int64_t
                        n_rays, sub_nerf_test_num, (double*)workspace);
     counts = (const double*)workspace;
   }
-  const int B = (n_samples + 63) / 64;
-  const dim3 g(nblk(n_rays, 4)), b(256);
+  const dim3 b(256);
   ProfScope ps(s, PT_COMPOSITE_BWD, 0.0, (double)n_rays * n_samples * (12.0 + (noise ? 4.0 : 0.0)));
-#define PCN_CB(MB)                                                                                           \
-  hipLaunchKernelGGL(k_composite_bwd<MB>, g, b, 0, s, p, z, n_rays, n_samples, noise, noise_std, eps, rays,  \
-                     ray_stride, child_near_col, child_far_col, range_col, child_id_col,                    \
-                     rays ? sub_nerf_test_num : 0, counts, grad_depth, grad_free_loss, grad_depth_loss,      \
+#define PCN_CB(MB, G, GRID)                                                                                   \
+  hipLaunchKernelGGL((k_composite_bwd<MB, G>), GRID, b, 0, s, p, z, n_rays, n_samples, noise, noise_std, eps, \
+                     rays, ray_stride, child_near_col, child_far_col, range_col, child_id_col,               \
+                     rays ? sub_nerf_test_num : 0, counts, grad_depth, grad_free_loss, grad_depth_loss,       \
                      grad_logit, (int*)nullptr)
-  if (B <= 2) PCN_CB(2);
-  else if (B <= 6) PCN_CB(6);
-  else if (B <= 16) PCN_CB(16);
-  else if (B <= 64) PCN_CB(64);
-  else PCN_CHECK(false, "pcnerf_composite_backward: more than 4096 samples per ray");
+  if (composite_block_per_ray(n_rays, n_samples)) {
+    const int B = (n_samples + 255) / 256;
+    const dim3 g((unsigned)n_rays);
+    if (B <= 2) PCN_CB(2, 256, g);
+    else if (B <= 6) PCN_CB(6, 256, g);
+    else if (B <= 16) PCN_CB(16, 256, g);
+    else PCN_CHECK(false, "pcnerf_composite_backward: more than 4096 samples per ray");
+  } else {
+    const int B = (n_samples + 63) / 64;
+    const dim3 g(nblk(n_rays, 4));
+    if (B <= 2) PCN_CB(2, 64, g);
+    else if (B <= 6) PCN_CB(6, 64, g);
+    else if (B <= 16) PCN_CB(16, 64, g);
+    else if (B <= 64) PCN_CB(64, 64, g);
+    else PCN_CHECK(false, "pcnerf_composite_backward: more than 4096 samples per ray");
+  }
 #undef PCN_CB
   PCN_LAUNCH_CHECK("pcnerf_composite_backward");
   PCN_API_END

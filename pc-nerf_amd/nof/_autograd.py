@@ -87,22 +87,6 @@ class NofForward(torch.autograd.Function):
         return (None, None) + tuple(grads)
 
 
-class PointwiseLoss(torch.autograd.Function):
-    """mean(loss(pred, target)) of nof/criteria/loss.py with d/dpred (targets are measured ranges)."""
-
-    @staticmethod
-    def forward(ctx, pred, target, kind, valid_mask):
-        ctx.kind = kind
-        ctx.save_for_backward(pred, target, valid_mask)
-        return _ops.pointwise_loss(pred, target, kind, valid_mask)
-
-    @staticmethod
-    def backward(ctx, g):
-        pred, target, m = ctx.saved_tensors
-        gp = _ops.pointwise_loss_backward(pred, target, ctx.kind, m, g.contiguous())
-        return gp.reshape(pred.shape), None, None, None
-
-
 class ChildRangeLoss(torch.autograd.Function):
     """Per-child range loss of train_kitti.py:125-142 (divide branch) with d/dpred."""
 

@@ -44,6 +44,7 @@ _SIGS = {
     "pcnerf_nof_train_workspace_bytes": (c_size, [i64]),
     "pcnerf_set_train_math": (c_int, [c_int]),
     "pcnerf_set_remat_version": (c_int, [c_int]),
+    "pcnerf_set_composite_group": (c_int, [c_int]),
     "pcnerf_set_eval_math": (c_int, [c_int]),
     "pcnerf_nof_query_train": (c_int, [vp, i64, c_int, vp, c_int, i64, ctypes.POINTER(NofParams), c_float, c_float,
                                        vp, c_size, vp, vp]),

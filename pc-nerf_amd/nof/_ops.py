@@ -137,6 +137,15 @@ def get_remat_version() -> int:
     return v
 
 
+def set_composite_group(group: int) -> int:
+    """The compositing kernels' ray group: 0 automatic (default), 64 a wave per ray, 256 a workgroup per ray
+    (pcnerf_set_composite_group); returns the previous setting."""
+    prev = H.lib().pcnerf_set_composite_group(int(group))
+    if prev < 0:
+        raise RuntimeError(H.lib().pcnerf_last_error().decode())
+    return prev
+
+
 def set_train_math(mode: str) -> str:
     """Select the train-mode layer arithmetic; returns the previous mode's name."""
     global _TRAIN_FUSED

@@ -8,7 +8,7 @@ from torch import nn
 
 import torch
 
-from .. import _autograd, _ops
+from .. import _autograd, _ops, _torch_ops  # noqa: F401  (_torch_ops registers torch.ops.pcnerf)
 
 __all__ = ["NOFLoss", "NOFMSELoss", "NOFL1Loss", "NOFSmoothL1Loss", "child_range_loss"]
 
@@ -20,9 +20,8 @@ class NOFLoss(nn.Module):
         super().__init__()
 
     def forward(self, pred, target, valid_mask=None):
-        if torch.is_grad_enabled() and pred.requires_grad:
-            return _autograd.PointwiseLoss.apply(pred, target, self.kind, valid_mask)
-        return _ops.pointwise_loss(pred, target, self.kind, valid_mask)
+        # pcnerf::pointwise_loss: its backward (pcnerf::pointwise_loss_backward) is registered with the operator
+        return torch.ops.pcnerf.pointwise_loss(pred, target, self.kind, valid_mask)
 
 
 class NOFMSELoss(NOFLoss):

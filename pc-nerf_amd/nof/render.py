@@ -26,11 +26,25 @@ import numpy as np
 import torch
 
 from . import _autograd, _ops
+from . import _torch_ops
 from .networks import NOF, Embedding, NOF_coarse, NOF_fine, NOF_plusfine  # noqa: F401  (reference exports)
 
 __all__ = ['render_rays']
 
 EPSILON = 1e-10  # render.py:456, :514, :656
+# the tensor-level stages go through the registered operators (nof._torch_ops): torch's dispatcher, FakeTensor
+# tracing and torch.compile see them as graph nodes
+P = torch.ops.pcnerf
+
+
+def _query(model, rays, z, chunk):
+    """The NOF query of one pass: eval mode through pcnerf::pack_eval + pcnerf::query_eval (the module's tensors
+    are operator inputs); train mode and the opt-in eval fold through nof._ops.query (module-level state: BatchNorm
+    running statistics, chunk moments)."""
+    if not model.training and not _ops.eval_fold_enabled():
+        _ops._bn_config(model)
+        return P.query_eval(rays, z, P.pack_eval(_torch_ops.eval_params(model)))
+    return _ops.query(model, rays, z, chunk)
 
 
 def _check_inputs(model, model_fine, embedding_xy, rays, n_cols, differentiable=False):
@@ -63,9 +77,9 @@ def _coarse(rays, N_samples, segmented, ratio, perturb, rng):
     """render.py:429-454."""
     R = rays.shape[0]
     n_parent = int(N_samples * (1 - ratio)) if segmented else N_samples
-    z = _ops.sample_coarse(rays, N_samples, n_parent, 6, 7, 10, 11)
+    z = P.sample_coarse(rays, N_samples, n_parent, 6, 7, 10, 11, False)
     if perturb > 0:
-        z = _ops.perturb(z, perturb, _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
+        z = P.perturb(z, float(perturb), _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
     return z
 
 
@@ -95,7 +109,7 @@ def sample_pdf(bins, weights, N_samples, det=False, pytest=False, *, u=None):
             hu = np.random.rand(R, N_samples)
         u = torch.from_numpy(np.ascontiguousarray(hu, dtype=np.float32)).to(bins.device)
         det = False   # the uploaded draws are used as given (the linspace is numpy's, float64 rounded to float32)
-    return _ops.sample_pdf_standalone(bins, weights, N_samples, det, u)
+    return P.sample_pdf(bins, weights, int(N_samples), bool(det), u)
 
 
 def render_rays_train(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: torch.Tensor, sub_nerf_test_num=4,
@@ -118,18 +132,18 @@ def render_rays_train(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays
             if not with_losses:
                 free, dl = torch.tensor(0.0), torch.tensor(0.0)
             return w, depth, free, dl
-        p = _ops.query(m, rays, z, chunk)
-        w, depth, fr, sl = _ops.composite(p, z, _noise(rng, noise_key, z, noise_std), noise_std, EPSILON,
-                                          rays if with_losses else None)
+        p = _query(m, rays, z, chunk)
+        w, depth, fr, sl = P.composite(p, z, _noise(rng, noise_key, z, noise_std), float(noise_std), EPSILON,
+                                       rays if with_losses else None, 10, 11, 14, True)
         if with_losses:
-            free, dl = _ops.child_losses(fr, sl, rays, use_child_nerf_divide == 1, sub_nerf_test_num)
+            free, dl = P.child_losses(fr, sl, rays, use_child_nerf_divide == 1, int(sub_nerf_test_num))
         else:
             free, dl = torch.tensor(0.0), torch.tensor(0.0)   # render.py:123-125, 157-159 (CPU scalars)
         return w, depth, free, dl
 
     w, depth, free, dl = one_pass(model, z, "noise")
     u = None if perturb == 0 else _draw(rng, "u", (R, N_importance), rays.device, torch.rand)
-    zf = _ops.resample(z, w, N_importance, u)
+    zf = P.resample(z, w, int(N_importance), u)
     _, depth_f, free_f, dl_f = one_pass(model_fine, zf, "noise_fine")
     return {'child_free_loss_fine': free_f, 'child_depth_loss_fine': dl_f, "depth_fine": depth_f,
             'child_free_loss': free, 'child_depth_loss': dl, 'depth': depth}
@@ -142,13 +156,14 @@ def render_rays_val(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: 
     rays = _check_inputs(model, model_fine, embedding_xy, rays, 8)
     R = rays.shape[0]
     z = _coarse(rays, N_samples, False, 0.0, perturb, rng)
-    p = _ops.query(model, rays, z, chunk)
-    w, depth, _, _ = _ops.composite(p, z, _noise(rng, "noise", z, noise_std), noise_std, EPSILON)
+    p = _query(model, rays, z, chunk)
+    w, depth, _, _ = P.composite(p, z, _noise(rng, "noise", z, noise_std), float(noise_std), EPSILON, None, 10, 11,
+                                 14, True)
     u = None if perturb == 0 else _draw(rng, "u", (R, N_importance), rays.device, torch.rand)
-    zf = _ops.resample(z, w, N_importance, u)
-    pf = _ops.query(model_fine, rays, zf, chunk)
-    _, depth_f, _, _ = _ops.composite(pf, zf, _noise(rng, "noise_fine", zf, noise_std), noise_std, EPSILON,
-                                      want_weights=False)
+    zf = P.resample(z, w, int(N_importance), u)
+    pf = _query(model_fine, rays, zf, chunk)
+    _, depth_f, _, _ = P.composite(pf, zf, _noise(rng, "noise_fine", zf, noise_std), float(noise_std), EPSILON,
+                                   None, 10, 11, 14, False)
     return {"depth_fine": depth_f, 'depth': depth}
 
 
@@ -161,17 +176,17 @@ def render_rays(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: torc
     the last sample falls in the descending weight order (render.py:598-600; ties broken stably)."""
     rays = _check_inputs(model, model_fine, embedding_xy, rays, 8)
     R = rays.shape[0]
-    z = _ops.sample_coarse(rays, N_samples, N_samples, 6, 7, disparity=use_disp)
+    z = P.sample_coarse(rays, N_samples, N_samples, 6, 7, 0, 0, bool(use_disp))
     if perturb > 0:
-        z = _ops.perturb(z, perturb, _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
+        z = P.perturb(z, float(perturb), _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
     eps = float(isval)
-    p = _ops.query(model, rays, z, chunk)
-    w, depth, _, _, opac, _ = _ops.composite(p, z, _noise(rng, "noise", z, noise_std), noise_std, eps, extras=True)
+    p = _query(model, rays, z, chunk)
+    w, depth, opac, _ = P.composite_extras(p, z, _noise(rng, "noise", z, noise_std), float(noise_std), eps)
     u = None if perturb == 0 else _draw(rng, "u", (R, N_importance), rays.device, torch.rand)
-    zf = _ops.resample(z, w, N_importance, u)
-    pf = _ops.query(model_fine, rays, zf, chunk)
-    wf, depth_f, _, _, opac_f, depth2 = _ops.composite(pf, zf, _noise(rng, "noise_fine", zf, noise_std), noise_std,
-                                                       eps, extras=True)
+    zf = P.resample(z, w, int(N_importance), u)
+    pf = _query(model_fine, rays, zf, chunk)
+    wf, depth_f, opac_f, depth2 = P.composite_extras(pf, zf, _noise(rng, "noise_fine", zf, noise_std),
+                                                     float(noise_std), eps)
     return {'depth_fine': depth_f, 'weights': wf, 'opacity': opac, 'z_vals': zf, "depth": depth, "depth2": depth2,
             "opacity_fine": opac_f}
 
@@ -179,9 +194,9 @@ def render_rays(model: NOF, model_fine: NOF, embedding_xy: Embedding, rays: torc
 def _inference_view(model, rays, z, other, chunk, method):
     """inference_0525_2 (render.py:229-368) on the HIP kernels: query, per-row compositing / peak / child sums,
     then the ray-group walk."""
-    p = _ops.query(model, rays, z, chunk)
-    w, depth, at_peak, csum, opac_row, pts = _ops.view_rows(p, z, rays, method, EPSILON)
-    flags, opacity = _ops.view_walk(other, at_peak, csum, opac_row, z.shape[1])
+    p = _query(model, rays, z, chunk)
+    w, depth, at_peak, csum, opac_row, pts = P.view_rows(p, z, rays, int(method), EPSILON)
+    flags, opacity = P.view_walk(other, at_peak, csum, opac_row, int(z.shape[1]))
     return depth, w, opacity, flags, pts
 
 
@@ -198,13 +213,13 @@ def render_rays_view_0525_2_2(model: NOF, model_fine: NOF, embedding_xy: Embeddi
         other = torch.as_tensor(other)
     other = other.to(rays.device)
     R = rays.shape[0]
-    z = _ops.sample_coarse(rays, N_samples, N_samples, 9, 10)   # parent bounds, render.py:622-628
+    z = P.sample_coarse(rays, N_samples, N_samples, 9, 10, 0, 0, False)   # parent bounds, render.py:622-628
     if perturb > 0:
-        z = _ops.perturb(z, perturb, _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
+        z = P.perturb(z, float(perturb), _draw(rng, "perturb_rand", (R, N_samples), rays.device, torch.rand))
     method = int(depth_inference_method)
     depth, w, opacity, flags, pts = _inference_view(model, rays, z, other, chunk, method)
     u = None if perturb == 0 else _draw(rng, "u", (R, N_importance), rays.device, torch.rand)
-    zf = _ops.resample(z, w, N_importance, u)
+    zf = P.resample(z, w, int(N_importance), u)
     depth_f, wf, opacity_f, flags_f, pts_f = _inference_view(model_fine, rays, zf, other, chunk, method)
     return {'depth_fine': depth_f, 'weights': wf, 'opacity': opacity, 'z_vals': zf, "depth": depth,
             "opacity_fine": opacity_f, "points_inference_fine": pts_f, "points_inference": pts,

@@ -13,7 +13,7 @@ HIP depth_fine to 1e-4 of this float64 evaluation, and to the reference within t
     python tests/golden/make_f64.py config1 [--save]   (KITTI-00 4,096-ray batch, 64/128)
     python tests/golden/make_f64.py config4 [--save]   (MaiCity blocks, 128/256)
     python tests/golden/make_f64.py config2 [--save]   (65,536 rays, 128/256; ~10 minutes on 8 cores)
-    python tests/golden/make_f64.py config3 [--save]   (262,144 KITTI rays, 64/128; ~20 minutes on 8 cores)
+    (config 3's float64 evaluation: tests/golden/make_config3_full.py f64)
     python tests/golden/make_f64.py grads [--save]     (float64 gradients of the 96-ray gradient goldens)
 Optional: --hip <npz with depth, depth_fine> compares a HIP run too.
 Test infrastructure (imports the oracle)."""
@@ -117,7 +117,7 @@ def main():
         grads64("--save" in sys.argv)
         return
     ap = argparse.ArgumentParser()
-    ap.add_argument("config", choices=["config1", "config2", "config3", "config4"])
+    ap.add_argument("config", choices=["config1", "config2", "config4"])
     ap.add_argument("--hip", default=None)
     ap.add_argument("--save", action="store_true", help=f"write tests/golden/<config>_f64.npz")
     a = ap.parse_args()
@@ -130,11 +130,6 @@ def main():
         sc, g = golden("scene_rays"), golden("config4_maicity")
         for b in range(4):
             cases.append((f"b{b}_", torch.from_numpy(sc[f"maicity_b{b}"]), 1234 + b, 5678 + b, 128, 256, g))
-    elif a.config == "config3":
-        sc, g = golden("scene_rays"), golden("config3_kitti")
-        rows = sc["kitti_train_all"]
-        idx = np.random.default_rng(int(g["seed"])).integers(0, rows.shape[0], int(g["n_rays"]))
-        cases.append(("", torch.from_numpy(rows[idx]), 1234, 5678, 64, 128, g))
     else:
         g = golden("config2_full")
         cases.append(("", torch.from_numpy(syn.make_rays(65536, seed=0)), 1234, 5678, 128, 256, g))
@@ -158,8 +153,7 @@ def main():
                 stats(f"{a.config} {pre}hip depth_fine", hip[pre + "depth_fine"], df64)
                 stats(f"{a.config} {pre}hip vs ref depth_fine", hip[pre + "depth_fine"], g[pre + "depth_fine"])
     if a.save:
-        name = {"config1": "config1_kitti", "config2": "config2_full", "config3": "config3_kitti",
-                "config4": "config4_maicity"}[a.config]
+        name = {"config1": "config1_kitti", "config2": "config2_full", "config4": "config4_maicity"}[a.config]
         path = os.path.join(HERE, name + "_f64.npz")
         np.savez_compressed(path, **saved)
         print("wrote", path)

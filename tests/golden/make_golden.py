@@ -555,40 +555,8 @@ def gen_config1_kitti(threads=1, name="config1_kitti"):
     torch.set_num_threads(1)
 
 
-CONFIG3_SEED = 3
-
-
-def config3_batch(n=262144):
-    """BASELINE config 3's batch: 262,144 rays drawn with replacement (numpy seed CONFIG3_SEED) from the KITTI-00
-    fixture scene's whole train split (scene_rays.npz kitti_train_all); the GPU test rebuilds the split with
-    nof.dataset, checks it bit for bit and draws the same indices."""
-    sc = scene_rays()
-    rows = sc["kitti_train_all"]
-    idx = np.random.default_rng(CONFIG3_SEED).integers(0, rows.shape[0], n)
-    return rows[idx], int(sc["kitti_children"])
-
-
-def gen_config3_kitti(threads=None, name="config3_kitti"):
-    """BASELINE config 3 at full size: the KITTI training step's forward on 262,144 rays at 64/128 samples with the
-    PC-NeRF KITTI shell's settings (chunk 262,144: 64 coarse + 192 fine BatchNorm chunks; perturb 0), train mode:
-    depths, child and range losses, the total, running statistics after the step."""
-    import time
-    torch.set_num_threads(threads or os.cpu_count() or 1)
-    rays, n_child = config3_batch()
-    emb, mc, mf = models(train=True)
-    t0 = time.perf_counter()
-    with torch.no_grad():
-        res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays), sub_nerf_test_num=n_child, N_samples=64,
-                                  N_importance=128, **PCNERF_TRAIN)
-    print(name, time.perf_counter() - t0, "s")
-    save(name, n_rays=rays.shape[0], seed=CONFIG3_SEED, N_samples=64, N_importance=128, sub_nerf_test_num=n_child,
-         threads=torch.get_num_threads(), **train_outputs(res, rays, mc, mf))
-    torch.set_num_threads(1)
-
-
-def gen_config3_alt():
-    """config 3 rerun with another thread count (the reference's own spread; see gen_self_spread)."""
-    gen_config3_kitti(threads=3, name="config3_kitti_alt")
+# BASELINE config 3 (KITTI-00 frames 1151-1200 at 50 % frame sparsity, 262,144 rays): tests/golden/make_config3_full.py
+# (its ``ref`` step imports this module for the reference's render_rays_train and these helpers)
 
 
 def gen_config4_maicity(threads=1, name="config4_maicity"):
@@ -623,7 +591,7 @@ def gen_self_spread():
 
 GENERATORS = [gen_maicity_frames, gen_kitti_frames, gen_metrics, gen_grads, gen_aabb, gen_render_rays, gen_nof,
               gen_pdf, gen_val, gen_train, gen_view, gen_pdf_pytest, gen_config1_kitti, gen_config4_maicity,
-              gen_config2_full, gen_self_spread, gen_grads_chunk, gen_view_kitti, gen_config3_kitti, gen_config3_alt]
+              gen_config2_full, gen_self_spread, gen_grads_chunk, gen_view_kitti]
 
 if __name__ == "__main__":
     # python make_golden.py [name ...]  (names without the gen_ prefix; default: all)

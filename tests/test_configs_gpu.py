@@ -6,7 +6,7 @@
   config 2  the headline workload at FULL size: 65,536 rays, 128/256 samples, chunk 262,144 (32 coarse + 96 fine
             BatchNorm chunks), child losses, against the reference run on the same rays (config2_full.npz);
   config 3  the KITTI training loop at 262,144 rays/iter (64/128 samples): the full-size step's forward against the
-            reference run on the same rays (config3_kitti.npz), then forward, losses, backward, Adam, properties;
+            reference run on the same rays (config3_full.npz: frames 1151-1200 at 50 % sparsity), then forward, losses, backward, Adam, properties;
   config 4  MaiCity-00 in 4 parent blocks, each with its own weights (config4_maicity.npz);
   the training driver: k steps of Adam + MultiStepLR through train_kitti.fit() against the oracle's autograd +
             torch.optim.Adam (parameters and per-step losses), once with BatchNorm inputs whose |mean|/std >> 1.
@@ -228,19 +228,39 @@ def test_config4_maicity_blocks(tmp_path):
 
 
 # ----------------------------------------------------------------------------------------------- config 3
+def kitti_scene_full(tmp_path):
+    """BASELINE config 3's scene: KITTI-00 scans 1151..1200 (tests/golden/kitti_frames_full.npz, every 16th point)
+    at the 50 % frame-sparsity rule (ipb2dmapping.py:647-660: 25 train frames), built on the GPU by nof.dataset."""
+    from test_dataset import INTEREST, write_scene
+    from nof import dataset as D
+    sc = golden("config3_full_scene")
+    root, pose_path, _ = write_scene(str(tmp_path), "kitti_frames_full")
+    return D.kitti_dataload(root, split="train", data_start=int(sc["data_start"]), data_end=int(sc["data_end"]),
+                            cloud_size_val=64, range_delete_x=3, range_delete_y=2, range_delete_z=1.25,
+                            sub_nerf_test_num=0, surface_expand=0.05, over_height=0.168, over_low=-2.0,
+                            interest_x=INTEREST, interest_y=INTEREST, pose_path=pose_path, re_loaddata=1,
+                            result_path=str(tmp_path / "out"), device=DEV, sparsity=int(sc["sparsity"])), sc
+
+
 def test_config3_training_step_262144_rays(tmp_path):
     """The KITTI training loop's step at 262,144 rays/iter (64/128 samples, chunk 262,144: 64 coarse + 192 fine
-    BatchNorm chunks, more than the default activation store holds, so the backward recomputes part of the
-    forward): a batch drawn (with replacement, numpy seed 3) from the KITTI fixture scene's whole train split, rebuilt
-    on the GPU and checked bit for bit against tests/golden/scene_rays.npz.  The first step's forward (depths, child
-    and range losses, total, running statistics) against the reference run on the same 262,144 rays
-    (config3_kitti.npz, make_golden.gen_config3_kitti) with check_train's tolerances -- depth_fine against the float64
-    evaluation and the reference's own spread (config3_kitti_f64.npz, _alt.npz); then three steps of forward,
-    losses, backward, Adam: finite losses that decrease on the repeated batch, finite non-zero gradients on both
-    networks, running statistics and parameters updated."""
-    tr, _ = kitti_scene(tmp_path)
-    sc, g3 = golden("scene_rays"), golden("config3_kitti")
-    np.testing.assert_array_equal(tr.rays.cpu().numpy(), sc["kitti_train_all"])
+    BatchNorm chunks) on BASELINE config 3's scene -- KITTI-00 frames 1151-1200 at 50 % frame sparsity (25 train
+    frames, 157,108 rows, 3,362 child cells; tests/golden/make_config3_full.py): the train split rebuilt on the GPU
+    by nof.dataset and checked bit for bit against the CPU restatement's (sha256 of all rows, the first 4,096 rows),
+    a batch drawn from it with replacement (numpy seed 3).  The first step's forward (depths, child and range losses,
+    total, running statistics) against the reference run on the same 262,144 rays (config3_full.npz) with
+    check_train's tolerances -- depth_fine against the float64 evaluation and the reference's own spread
+    (config3_full_f64.npz, _alt.npz); then three steps of forward, losses, backward, Adam: finite losses that
+    decrease on the repeated batch, finite non-zero gradients on both networks, running statistics and parameters
+    updated."""
+    import hashlib
+    tr, sc = kitti_scene_full(tmp_path)
+    g3 = golden("config3_full")
+    got = tr.rays.cpu().numpy()
+    assert got.shape[0] == int(sc["n_rows"])
+    np.testing.assert_array_equal(got[:4096], sc["head"])
+    assert hashlib.sha256(np.ascontiguousarray(got, dtype=np.float32).tobytes()).hexdigest() == str(sc["sha256"])
+    assert int(g3["sub_nerf_test_num"]) == int(sc["children"])
     idx = np.random.default_rng(int(g3["seed"])).integers(0, tr.rays.shape[0], int(g3["n_rays"]))
     rays = tr.rays[torch.from_numpy(idx).to(DEV)].contiguous()
     emb, mc, mf = models(True)
@@ -256,8 +276,8 @@ def test_config3_training_step_262144_rays(tmp_path):
         for k in ("depth", "depth_fine"):
             assert torch.isfinite(res[k]).all()
         if not losses:   # the first step's forward against the reference
-            check_train({k: v.detach() for k, v in res.items()}, g3, rays, mc, mf, name="config3_kitti",
-                        f64=golden("config3_kitti_f64"), alt=golden("config3_kitti_alt"))
+            check_train({k: v.detach() for k, v in res.items()}, g3, rays, mc, mf, name="config3_full",
+                        f64=golden("config3_full_f64"), alt=golden("config3_full_alt"))
         gt = rays[:, 14]
         loss = (1e-1 * loss_fn(1e1 * res["depth"], 1e1 * gt) + 1e-1 * loss_fn(1e1 * res["depth_fine"], 1e1 * gt)
                 + 1e6 * (res["child_free_loss"] + res["child_free_loss_fine"])

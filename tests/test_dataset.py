@@ -23,9 +23,10 @@ KW = dict(range_delete=(3.0, 2.0, 1.25), over_height=0.168, over_low=-2.0)
 INTEREST = 20.0
 
 
-def write_scene(tmp):
-    """The fixture as the reference's inputs: <tmp>/pcd/<n>.pcd and a poses.txt whose rows 1150..1156 are real."""
-    g = golden("kitti_frames")
+def write_scene(tmp, name="kitti_frames"):
+    """The fixture as the reference's inputs: <tmp>/pcd/<n>.pcd and a poses.txt whose rows 1150..1156 are real
+    (``kitti_frames_full``: scans 1151..1200, rows 1150..1200)."""
+    g = golden(name)
     os.makedirs(os.path.join(tmp, "pcd"), exist_ok=True)
     for k, v in g.items():
         if k.startswith("f"):

@@ -587,3 +587,38 @@ def test_nan_bounds_sort_like_torch():
     mid = 0.5 * (z[:, 1:] + z[:, :-1])
     fine = _ops.sample_pdf_standalone(mid.to(DEV), w[:, 1:-1].contiguous().to(DEV), I, False, u.to(DEV)).cpu()
     np.testing.assert_array_equal(zf.numpy(), torch.sort(torch.cat([z, fine], -1), -1)[0].numpy())
+
+
+@pytest.mark.parametrize("R_,S", [(256, 768), (256, 2304), (40, 4096)])
+def test_composite_workgroup_per_ray(R_, S):
+    """The reference shell's shape (256 rays x 768 coarse / 2,304 fine samples) and 4,096-sample rows: k_composite /
+    k_composite_bwd with a 256-thread workgroup per ray (Grp<256>, the automatic choice here) against a wave per ray
+    (Grp<64>) on the same inputs -- weights, depth, child-loss terms, opacity sums, depth2 and dL/dlogit -- and
+    the forward against the oracle's compositing (render.py:51-61; depth rtol 1e-5).  Every sum and scan is float64
+    rounded once, so the two groupings agree to float64 association noise."""
+    from nof import _ops
+    gen = torch.Generator().manual_seed(S)
+    rays = torch.from_numpy(syn.make_rays(R_, seed=S))
+    z = torch.sort(rays[:, 6:7] + (rays[:, 7:8] - rays[:, 6:7]) * torch.rand(R_, S, generator=gen), -1)[0]
+    p = torch.rand(R_, S, generator=gen) ** 8   # mostly transparent, a few occupied samples per ray
+    rd, zd, pd = rays.to(DEV), z.to(DEV), p.to(DEV)
+    gdep = torch.randn(R_, generator=gen).to(DEV)
+    gfree, gdl = torch.tensor(0.3, device=DEV), torch.tensor(-0.7, device=DEV)
+    outs = {}
+    prev = _ops.set_composite_group(0)
+    try:
+        for grp in (64, 256):
+            _ops.set_composite_group(grp)
+            w, d, fr, sl = _ops.composite(pd, zd, None, 0.0, 1e-10, rd)
+            w2, d2, _, _, om, dep2 = _ops.composite(pd, zd, None, 0.0, 1e-10, extras=True)
+            g = _ops.composite_backward(pd, zd, None, 0.0, 1e-10, rd, 0, gdep, gfree, gdl)
+            outs[grp] = [t.cpu().double() for t in (w, d, fr, sl, om, dep2, g)]
+    finally:
+        _ops.set_composite_group(prev)
+    names = ("weights", "depth", "free_ray", "sl1_ray", "opacity", "depth2", "g_logit")
+    for n, a, b in zip(names, outs[64], outs[256]):
+        scale = float(b.abs().max()) or 1.0
+        assert float((a - b).abs().max()) <= 2e-6 * scale, n
+    wr, dr = O.composite(p, z)
+    close(outs[256][1], dr.numpy(), 1e-5, 1e-6, "depth vs oracle")
+    close(outs[256][0], wr.numpy(), 1e-5, 1e-7, "weights vs oracle")
