@@ -765,7 +765,8 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
               16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw",
               # (the train query writing the activation store is its own instantiation)
               18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" and not remat else "k_nof_eval_h3<true,false>",
-              19: ("k_bwd_remat3" if rver == 3 else "k_bwd_remat2<0>") if remat else "k_bwd_fused<0,false>"}
+              19: ({3: "k_bwd_remat3<false>", 4: "k_bwd_remat3<true>"}.get(rver, "k_bwd_remat2<0>") if remat
+                   else "k_bwd_fused<0,false>")}
     pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd", 20: "k_g7"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
@@ -790,7 +791,7 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
     gbs = kbytes / max(klaunch, 1) / avg_s / 1e9
     traffic, traffic_src = pmc_traffic(kname, line)
     nprod = nterm   # k_wgrad_b3 too: f16x2 parts, nterm products (the six-product bf16x3 form is a build option)
-    if tag == 19 and rver == 3:
+    if tag == 19 and rver in (3, 4):
         # k_bwd_remat3 issues 3 products of (2.256.256 + 2.256.64 + 2.256.64) per sample against the algorithmic
         # 2.2.256.256 (its weight gradient contracts the 64 encoding columns; the rematerialised x is extra work)
         nprod = 3.0 * (131072 + 32768 + 32768) / 262144
@@ -837,9 +838,9 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
         # count; each launch also writes its 128 pair partials of the weight gradient (the split-K over tiles) and
         # reads the previous layer's
         per_launch = kbytes / max(klaunch, 1)
-        partials = 2.0 * 128 * (256 * (64 if rver == 3 else 256) + 256) * 4
+        partials = 2.0 * 128 * (256 * (64 if rver in (3, 4) else 256) + 256) * 4
         roof["note"] = (("k_bwd_remat3 (weight gradient over the 64 encoding columns, projected by P'^T per chunk)"
-                         if rver == 3 else "layer launches k_bwd_remat2<0|2> averaged") +
+                         if rver in (3, 4) else "layer launches k_bwd_remat2<0|2> averaged") +
                         "; the weight-gradient partial round trip is outside the algorithmic bytes")
         roof["partials_bytes_per_launch"] = partials
         if traffic:

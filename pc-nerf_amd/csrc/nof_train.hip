@@ -1366,7 +1366,7 @@ static int g_train_math = 1;
 // selects it at load time (A/B measurements).
 static int remat_ver_env() {
   const char* v = getenv("PCNERF_REMAT_VER");
-  return (v && v[0] == '2') ? 2 : 3;
+  return (v && v[0] == '2') ? 2 : (v && v[0] == '4') ? 4 : 3;
 }
 static int g_remat_ver = remat_ver_env();
 
@@ -1415,8 +1415,9 @@ extern "C" int pcnerf_set_train_math(int mode) {
 }
 
 extern "C" int pcnerf_set_remat_version(int version) {
-  if (version != 2 && version != 3) {
-    pcn::set_error("pcnerf_set_remat_version: version must be 2 (k_bwd_remat2) or 3 (k_bwd_remat3)");
+  if (version < 2 || version > 4) {
+    pcn::set_error("pcnerf_set_remat_version: version must be 2 (k_bwd_remat2), 3 (k_bwd_remat3) or 4 "
+                   "(k_bwd_remat3 with the epilogue on the W waves)");
     return -1;
   }
   const int prev = pcn::g_remat_ver;
@@ -1924,42 +1925,59 @@ struct WgradCfg {
   static constexpr int RT = C * SPLIT;
 };
 
+// the chunk's encoding mean as float64 column sums (atomics into a zeroed acc[64]): k_wgrad's centring constant
+__global__ __launch_bounds__(256) void k_enc_mean(const float* __restrict__ rays, int stride,
+                                                  const float* __restrict__ z, int S, int64_t c0, int64_t n,
+                                                  const float* __restrict__ ein, double* __restrict__ acc) {
+  __shared__ double sh[4][64];
+  double a[63];
+#pragma unroll
+  for (int k = 0; k < 63; ++k) a[k] = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float f[64];
+    if (ein) {
+#pragma unroll
+      for (int k = 0; k < 63; ++k) f[k] = ein[(c0 + i) * 63 + k];
+    } else {
+      float p[3];
+      sample_point(rays + ray_of(c0 + i, S) * stride, z[c0 + i], p);
+      encode_full(p, f);
+    }
+#pragma unroll
+    for (int k = 0; k < 63; ++k) a[k] += (double)f[k];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 63; ++k) {
+    const double v = wave_sum_d(a[k]);
+    if (lane == 0) sh[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 63) {
+    const int k = threadIdx.x;
+    atomicAdd(acc + k, ((sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k])));
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(512, 1) void k_wgrad(const float* __restrict__ rays, int stride,
                                                   const float* __restrict__ z, int S, int64_t c0, int64_t n,
                                                   const float* __restrict__ ein, const float* __restrict__ gin,
                                                   const float* __restrict__ hprev, const float* __restrict__ mu,
-                                                  float* __restrict__ part) {
+                                                  float* __restrict__ part, const double* __restrict__ esum) {
   using Cfg = WgradCfg<MODE>;
   constexpr bool HX = Cfg::HX, EX = Cfg::EX;
   constexpr int GS = Cfg::GS, BUF = Cfg::BUF, C = Cfg::C;
   CLK_ENTRY
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* mus = lds + 2 * BUF;
-  // the encoding columns are contracted as g (x) (e - e(c0)), e(c0) the chunk's first sample's encoding: sum_s g = 0
-  // exactly (BatchNorm follows the Linear), so the sum is the same, while the rounding noise of sum_s g no longer
-  // multiplies |e| (positions far from the origin) but only the chunk's spread around one of its own samples
+  // the encoding columns are contracted as g (x) (e - ebar), ebar the chunk's encoding mean (k_enc_mean; esum null:
+  // 0): sum_s g = 0 exactly (BatchNorm follows the Linear), so the sum is the same, while a constant offset in g (the
+  // fp32 rounding of its chunk mean) no longer multiplies n ebar -- it cancels, as in the fused paths' G = g (x) d
   float* esh = mus + 256;
   const int t = threadIdx.x, lane = t & 63, h = lane >> 5, li = lane & 31, wv = t >> 6;
   if (HX && t < 256) mus[t] = mu[t];
-  if (EX && t < 64) {
-    if (ein) {
-      esh[t] = t < 63 ? ein[c0 * 63 + t] : 0.0f;
-    } else {
-      float p[3];
-      sample_point(rays + ray_of(c0, S) * stride, z[c0], p);
-      float v = 0.0f;
-      if (t < 3) {
-        v = p[t];
-      } else if (t < 63) {
-        const int q = t - 3, k = q / 6, r = q - 6 * k, m = r % 3;
-        float sv, cv;
-        sincosf((float)(1 << k) * p[m], &sv, &cv);   // encode_half's arithmetic
-        v = r < 3 ? sv : cv;
-      }
-      esh[t] = v;
-    }
-  }
+  if (EX && t < 64) esh[t] = (esum && t < 63) ? (float)(esum[t] / (double)n) : 0.0f;
   __syncthreads();
   const int64_t ntiles = (n + 31) / 32;
   f32x16 ah[8], ae[2];
@@ -4186,7 +4204,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat2(const char* __restrict__ 
 constexpr int R3_XC = 32 * 128 * 4;                      // xc: [32 samples][32 chunks of 4 features] fp32
 static_assert(2 * FB_GPART + R3_XC == FB_BUF, "remat3 keeps k_bwd_remat2's tile buffer size");
 constexpr int R3_ENC_SLOTS = 3;                          // remat of tile k + 1 and wgrad of tile k, DMA of k + 2
-constexpr size_t R3_LDS = 2 * (size_t)FB_BUF + R3_ENC_SLOTS * FB_ENC + RB_PX + 8 * 128 * sizeof(float);
+constexpr size_t R3_LDS = 2 * (size_t)FB_BUF + R3_ENC_SLOTS * FB_ENC + 8 * 128 * sizeof(float);
 static_assert(R3_LDS <= 160 * 1024, "k_bwd_remat3 LDS");
 constexpr size_t GD_PART = WgradCfg<1>::PART;            // 256 x 64 + 256 floats per pair
 constexpr int GD_LAYER = 256 * 64;                       // doubles of one layer's G_d
@@ -4224,6 +4242,12 @@ __device__ __forceinline__ void gd_reduce_row(const float* __restrict__ part, in
   __syncthreads();
 }
 
+// WEPI (version 4): the BatchNorm-backward epilogue and the g_{L-1} stores move from the D to the W waves, which
+// hold x in registers from their own rematerialisation: a D wave runs only the 96 data-gradient MFMAs of a tile and
+// writes its fp32 accumulators to LDS (the xc slot's 16 KiB), a W wave takes tile k - 1's accumulators there after
+// the barrier, finishes g_{L-1} = dy A - (x X + B) and stores it, then makes x of tile k and G_d of tile k (48 MFMAs):
+// per SIMD 96 MFMAs against 48 + the epilogue's VALU, instead of 96 + epilogue against 48.
+template <bool WEPI>
 __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ gin, char* __restrict__ gout,
                                                         const f16x8* __restrict__ wt,
                                                         const int* __restrict__ sw, int layer, int64_t n,
@@ -4239,8 +4263,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
   constexpr int NST = 4;   // a D wave's global stores per tile
   extern __shared__ __attribute__((aligned(16))) char fb[];
   char* const enb = fb + 2 * FB_BUF;
-  char* const pxl = enb + R3_ENC_SLOTS * FB_ENC;
-  float* const cst = reinterpret_cast<float*>(pxl + RB_PX);   // [. | 2^-e | B | . | invstd | A | x scale | bound]
+  float* const cst = reinterpret_cast<float*>(enb + R3_ENC_SLOTS * FB_ENC);   // [. | 2^-e | B | . | invstd | A | X | bound]
   const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int rw = wv & 3;   // index within the role
@@ -4272,9 +4295,17 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
     ob = wave_max_f(ob);
     if (lane == 0) cst[896 + wv] = ob;
   }
-  for (int j = t; j < 128 * 16; j += 512) {
-    const int r = j >> 4, q = j & 15;
-    *reinterpret_cast<f16x8*>(pxl + r * 256 + 16 * (q ^ (r & 15))) = px[(size_t)(128 * hf + r) * 16 + q];
+  // W waves: their P' rows (features 32 rw .. 32 rw + 31 of the half, 64 columns, hi / mid) in registers for the
+  // whole launch -- the same 8 f16x8 every tile (the LDS copy cost 8 KiB of reads per wave and tile)
+  f16x8 pa_r[2][2][2];   // [ks][rb][part]
+  if (wv >= 4) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          pa_r[ks][rb][p] = px[(size_t)(128 * hf + 32 * rw + 16 * rb + lm) * 16 + (2 * ks + p) * 4 + kg];
   }
   const int eg = gexp[layer];
   const float gun = ldexpf(1.0f, -eg);
@@ -4319,14 +4350,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
     f32x4 ax[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      f16x8 pa[2][2];
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const int r = 32 * rw + 16 * rb + lm, q = (2 * ks + p) * 4 + kg;
-          pa[rb][p] = *reinterpret_cast<const f16x8*>(pxl + r * 256 + 16 * (q ^ (r & 15)));
-        }
+      const auto& pa = pa_r[ks];
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
         const int o = fb_eoff(16 * sb + lm, 4 * ks + kg);
@@ -4360,11 +4384,185 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
     if (nk > 1) dma_enc(1);
     __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
     __builtin_amdgcn_s_barrier();
-    if (wv >= 4) remat_xc(0);
+    if (!WEPI && wv >= 4) remat_xc(0);
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
-  if (wv < 4) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  if constexpr (WEPI) {
+    if (wv < 4) {
+      // ---- D: the data-gradient MFMAs of features 128 hf + 32 rw + 16 rb + lm; accumulators to LDS
+      f16x8 wr[8][2][2];
+      {
+        const f16x8* __restrict__ w8 = wt + lane;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) wr[ks][rb][p] = w8[((ks * 16 + 8 * hf + 2 * rw + rb) * 2 + p) * 64];
+      }
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        asm volatile("" ::"v"(wr[ks][0][0]), "v"(wr[ks][0][1]), "v"(wr[ks][1][0]), "v"(wr[ks][1][1]));
+      for (int k = 0; k < nk; ++k) {
+        if (k + 1 < nk) dma_g(k + 1);
+        if (k + 2 < nk) dma_enc(k + 2);
+        char* const sp = fb + (size_t)(k & 1) * FB_BUF;
+        f32x4 ad[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb) {
+            const int o = gs_off(16 * sb + lm, 4 * ks + kg);
+            const f16x8 bh = *reinterpret_cast<const f16x8*>(sp + o);
+            const f16x8 bm = *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+              ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bh, ad[rb][sb], 0, 0, 0);
+              ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bm, ad[rb][sb], 0, 0, 0);
+              ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][1], bh, ad[rb][sb], 0, 0, 0);
+            }
+          }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb)
+            *reinterpret_cast<f32x4*>(sp + 2 * FB_GPART + r3_xoff(16 * sb + lm, (32 * rw + 16 * rb + 4 * kg) >> 2)) =
+                ad[rb][sb];
+        __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+      }
+    } else {
+      // ---- W: epilogue + stores of tile k - 1, x of tile k (registers), G_d of tile k
+      const float gui = ldexpf(1.0f, -eo);
+      float gmo = 0.0f;
+      f32x4 xr[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};   // x X + B of the previous tile
+      f32x4 aw[4][2];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) aw[jb][ib] = f32x4{};
+      const int trq = lm >> 2, trp = lm & 3, tr0 = 8 * kg + trq, tr1 = tr0 + 4;
+      auto join = [](const s16x4& a, const s16x4& b) {
+        return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      auto eoff = [](int r, int c) { return r * 128 + 16 * ((c >> 3) ^ ((r >> 1) & 7)) + 2 * (c & 7); };
+      // tile kq's g_{L-1}: its accumulators (LDS) and xr; kq < 0: zero cells to tile 0's own slots (rewritten by
+      // this wave's later stores -- same addresses, program order), so every tile has NST stores behind its DMAs
+      auto epilogue = [&](int kq) {
+        const int tq = pr + (kq < 0 ? 0 : kq) * npair;
+        const char* adb = fb + (size_t)((kq < 0 ? 0 : kq) & 1) * FB_BUF + 2 * FB_GPART;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const int il = 32 * rw + 16 * rb + 4 * kg, i = 128 * hf + il;
+          const f32x4 cA = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb) {
+            const int sm = 16 * sb + lm;
+            const bool valid = kq >= 0 && (int64_t)tq * 32 + sm < n;
+            const f32x4 ad = *reinterpret_cast<const f32x4*>(adb + r3_xoff(sm, il >> 2));
+            f32x4 vs;   // 2^eo g_{L-1}
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              vs[q] = valid ? fmaf(ad[q], cA[q], -xr[rb][sb][q]) : 0.0f;
+              gmo = fmaxf(gmo, fabsf(vs[q]));
+            }
+            s16x4 p0, p1;
+            split2_x4(vs, p0, p1);
+            const fb_i32x2 hv = __builtin_bit_cast(fb_i32x2, p0), mv = __builtin_bit_cast(fb_i32x2, p1);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
+            const u32x4 cell = {s0[0], s1[0], s0[1], s1[1]};
+            char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
+            __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));
+          }
+        }
+      };
+      auto remat_reg = [&](int k) {
+        const char* eb = enb + (k % R3_ENC_SLOTS) * FB_ENC;
+        f32x4 ax[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const auto& pa = pa_r[ks];
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb) {
+            const int o = fb_eoff(16 * sb + lm, 4 * ks + kg);
+            const f16x8 bh = *reinterpret_cast<const f16x8*>(eb + o);
+            const f16x8 bm = *reinterpret_cast<const f16x8*>(eb + FB_ENC / 2 + o);
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+              ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][0], bh, ax[rb][sb], 0, 0, 0);
+              ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][0], bm, ax[rb][sb], 0, 0, 0);
+              ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][1], bh, ax[rb][sb], 0, 0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const int il = 32 * rw + 16 * rb + 4 * kg;
+          const f32x4 X = *reinterpret_cast<const f32x4*>(cst + 768 + il);
+          const f32x4 B = *reinterpret_cast<const f32x4*>(cst + 256 + il);
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xr[rb][sb][q] = fmaf(ax[rb][sb][q], X[q], B[q]);
+        }
+      };
+      for (int k = 0; k < nk; ++k) {
+        if (k + 1 < nk) dma_g(k + 1);
+        if (k + 2 < nk) dma_enc(k + 2);
+        epilogue(k - 1);
+        remat_reg(k);
+        const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
+        const unsigned ga = fb_lds_addr(sp), ea = fb_lds_addr(enb + (k % R3_ENC_SLOTS) * FB_ENC);
+        std::array<s16x4, 4> ra[4], rx[2];
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          const int col = 64 * rw + 16 * jb + 4 * trp;
+          const unsigned a0 = ga + gs_off(tr0, col >> 3) + 2 * (col & 7), a1 = ga + gs_off(tr1, col >> 3) + 2 * (col & 7);
+          ra[jb] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_GPART>(a0), fb_tr<FB_GPART>(a1)};
+        }
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+          const int c = 32 * hf + 16 * ib + 4 * trp;
+          const unsigned a0 = ea + eoff(tr0, c), a1 = ea + eoff(tr1, c);
+          rx[ib] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_ENC / 2>(a0), fb_tr<FB_ENC / 2>(a1)};
+        }
+        fb_lgkm<0>(ra);
+        fb_lgkm<0>(rx);
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+          const f16x8 B0 = join(rx[ib][0], rx[ib][1]), B1 = join(rx[ib][2], rx[ib][3]);
+#pragma unroll
+          for (int jb = 0; jb < 4; ++jb) {
+            const f16x8 A0 = join(ra[jb][0], ra[jb][1]), A1 = join(ra[jb][2], ra[jb][3]);
+            aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0, aw[jb][ib], 0, 0, 0);
+            aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1, aw[jb][ib], 0, 0, 0);
+            aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0, aw[jb][ib], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs (its stores may fly)
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+      }
+      if (nk > 0) epilogue(nk - 1);   // (the loop's last barrier: D's accumulators of tile nk - 1 are in LDS)
+      gmo = wave_max_f(gmo) * gui;
+      if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rw) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
+      float* const pb = part + (size_t)pr * GD_PART;
+      const int sxyz = remat_sx(0, __uint_as_float(*pbound));
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) {
+        const int col = 32 * hf + 16 * ib + lm;
+        const float cu = ldexpf(gun, -(col < 3 ? sxyz : 13));
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pb[(size_t)(64 * rw + 16 * jb + 4 * kg + r) * 64 + col] = aw[jb][ib][r] * cu;
+      }
+    }
+  } else if (wv < 4) {
     // ---- D: data gradient of input features 128 hf + 32 rw + 16 rb + lm, epilogue, g_{L-1} stores
     const float gui = ldexpf(1.0f, -eo);
     f16x8 wr[8][2][2];
@@ -4528,7 +4726,7 @@ __global__ __launch_bounds__(1024) void k_gd_tail(const float* __restrict__ part
 
 // dW_L[j][i] += alpha_i sum_k G_d[L][j][k] P'_{L-1}[i][k] for the chunk (float64; alpha = invstd gamma of BatchNorm
 // L-1, the Linear's input scale), L = 1..7; the skip layer also takes its encoding columns dW_4[j][k] += G_d[4][j][k]
-// (its input there is e itself).  grid (16 row blocks, 7 layers), 256 threads (column i).
+// (its input there is e itself).
 struct GdProj {
   double* dW[8];
   const float* coef;   // ws.coef: layer L's BatchNorm constants at 1024 L (alpha at 512)
@@ -4537,28 +4735,37 @@ struct GdProj {
   int64_t C, ci;
 };
 __global__ __launch_bounds__(256) void k_gd_proj(GdProj g) {
-  __shared__ double gs[16][64];
-  const int L = 1 + (int)blockIdx.y, j0 = 16 * (int)blockIdx.x, i = threadIdx.x;
-  for (int idx = i; idx < 16 * 64; idx += 256)
-    gs[idx >> 6][idx & 63] = g.gd[(size_t)L * GD_LAYER + (size_t)(j0 + (idx >> 6)) * 64 + (idx & 63)];
+  // one 64 x 64 block of dW_L per workgroup: grid (16 = 4 row blocks x 4 column blocks, 7 layers); P'_{L-1} rows
+  // i0..i0+63 and G_d rows j0..j0+63 staged in LDS with coalesced loads, 16 outputs (63-term float64 dots) a thread
+  __shared__ double gs[64][65];
+  __shared__ double ps[64][65];
+  const int L = 1 + (int)blockIdx.y, j0 = 64 * ((int)blockIdx.x >> 2), i0 = 64 * ((int)blockIdx.x & 3);
+  const int t = threadIdx.x;
+  const double* gdl = g.gd + (size_t)L * GD_LAYER;
+  const double* pp = g.pp + (((size_t)(L - 1) * g.C + g.ci) * 256) * 64;
+  for (int idx = t; idx < 64 * 64; idx += 256) {
+    const int r = idx >> 6, c = idx & 63;
+    gs[r][c] = gdl[(size_t)(j0 + r) * 64 + c];
+    ps[r][c] = c < 63 ? pp[(size_t)(i0 + r) * 64 + c] : 0.0;
+  }
   __syncthreads();
-  const double* prow = g.pp + (((size_t)(L - 1) * g.C + g.ci) * 256 + i) * 64;
+  const int ti = t & 63, tj = t >> 6;   // column i0 + ti, rows j0 + tj + 4 m
   double acc[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+  for (int m = 0; m < 16; ++m) acc[m] = 0.0;
   for (int k = 0; k < 63; ++k) {
-    const double p = prow[k];
+    const double p = ps[ti][k];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = fma(gs[j][k], p, acc[j]);
+    for (int m = 0; m < 16; ++m) acc[m] = fma(gs[tj + 4 * m][k], p, acc[m]);
   }
-  const double alpha = (double)g.coef[1024 * (L - 1) + 512 + i];
+  const double alpha = (double)g.coef[1024 * (L - 1) + 512 + i0 + ti];
   const int in_f = in_features(L), wc = L == 4 ? 63 : 0;
   double* const dW = g.dW[L];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) dW[(size_t)(j0 + j) * in_f + wc + i] += alpha * acc[j];
-  if (L == 4 && i < 63) {
+  for (int m = 0; m < 16; ++m) dW[(size_t)(j0 + tj + 4 * m) * in_f + wc + i0 + ti] += alpha * acc[m];
+  if (L == 4 && i0 == 0 && ti < 63) {   // the skip layer's encoding columns: its input there is e itself
 #pragma unroll
-    for (int j = 0; j < 16; ++j) dW[(size_t)(j0 + j) * in_f + i] += gs[j][i];
+    for (int m = 0; m < 16; ++m) dW[(size_t)(j0 + tj + 4 * m) * in_f + ti] += gs[tj + 4 * m][ti];
   }
 }
 
@@ -4811,7 +5018,7 @@ static BwdWs carve_bwd(void* base, int64_t chunk) {
 template <int MODE>
 static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int stride, const float* z, int S,
                          int64_t c0, int64_t n, const float* ein, const float* gin, const float* hprev,
-                         const float* mu, float* part) {
+                         const float* mu, float* part, const double* esum = nullptr) {
   static std::atomic<uint64_t> attr{0};
   const size_t lds = WgradCfg<MODE>::LDS_BYTES;
   if (pcn_attr_needed(attr)) {
@@ -4819,7 +5026,7 @@ static void launch_wgrad(unsigned blocks, hipStream_t s, const float* rays, int 
     pcn_attr_done(attr);
   }
   hipLaunchKernelGGL(k_wgrad<MODE>, dim3(blocks), dim3(512), lds, s, rays, stride, z, S, c0, n, ein, gin, hprev,
-                     mu, part);
+                     mu, part, esum);
 }
 
 template <int MODE, int LAY, bool H2, int NTP>
@@ -4964,11 +5171,15 @@ static void remat3_layers(const NofParamsDev& P, const GaccLayout& G, const BwdW
     // 2 x 256 x 256 + 2 x 256 x 64 (G_d) + 2 x 256 x 64 (x), x 3 products.  Bytes: g_L in (1 KiB), the encoding
     // image (256 B), g_{L-1} out (1 KiB)
     ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0) * dn, (1024.0 + 256.0 + 1024.0) * dn);
-    hipLaunchKernelGGL(k_bwd_remat3, dim3(fbg), dim3(512), R3_LDS, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,
-                       (const int*)ws.sw, L, n, coefp, (const float*)(ws.bnb + 512 * (L - 1)), P.bn_w[L - 1],
-                       ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
-                       pset[L & 1], rpart, rgd, (const char*)encimg, prow(L - 1), psrow(L - 1),
-                       (const unsigned*)ws.pbound);
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), R3_LDS, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,
+                         (const int*)ws.sw, L, n, coefp, (const float*)(ws.bnb + 512 * (L - 1)), P.bn_w[L - 1],
+                         ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
+                         pset[L & 1], rpart, rgd, (const char*)encimg, prow(L - 1), psrow(L - 1),
+                         (const unsigned*)ws.pbound);
+    };
+    if (g_remat_ver == 4) launch(k_bwd_remat3<true>);
+    else launch(k_bwd_remat3<false>);
   }
   const int ne = (int)std::min<int64_t>(ntiles, 2 * FB_PAIRS);   // g_0's partial sets (one per workgroup)
   float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
@@ -5006,7 +5217,9 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                                 (int)RB_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat2<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RB_LDS));
-    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat3, hipFuncAttributeMaxDynamicSharedMemorySize,
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat3<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)R3_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat3<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)R3_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_enc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WE_LDS));
@@ -5049,7 +5262,7 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
   }
   const unsigned fbg = (unsigned)(2 * FB_PAIRS);
   float* const pset[2] = {ws.part, ws.part + (size_t)FB_PAIRS * WgradCfg<2>::PART};
-  if (g_remat_ver == 3) {
+  if (g_remat_ver >= 3) {
     remat3_layers(P, G, ws, FB, pimg, pscl, ci, n, grad, s, encimg, prow, psrow, S, S2, pset);
     return;
   }
@@ -5234,6 +5447,14 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
                          ws.gacc + G.wo, ws.gacc + G.bo, ws.g[0], split ? ws.tmax[0] : nullptr,
                          split ? ws.gmax + 7 * GMAX_SLOTS : nullptr, OSTAT_COPIES);
     }
+    // the chunk's encoding mean (fp32 MFMA math: k_wgrad's centring of the encoding columns of layers 0 and 4)
+    const double* emean = nullptr;
+    if (!split) {
+      PCN_HIP(hipMemsetAsync(ws.gd, 0, 64 * sizeof(double), s));
+      hipLaunchKernelGGL(k_enc_mean, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 256)), dim3(256), 0, s, rays,
+                         ray_stride, z, n_samples, c0, n, ein, ws.gd);
+      emean = ws.gd;
+    }
     // 3. layers 7..1
     int cur = 0;
     for (int L = 7; L >= 1; --L) {
@@ -5248,7 +5469,8 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
           launch_wgrad_b3<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
                              ws.gmax + L * GMAX_SLOTS, ws.part, ws.pbound);
         else if (L == 4)
-          launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part);
+          launch_wgrad<2>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[3], coefp, ws.part,
+                          emean);
         else
           launch_wgrad<0>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], hh[L - 1], coefp,
                           ws.part);
@@ -5294,7 +5516,7 @@ static void backward_train(const float* rays, int ray_stride, const float* z, in
                            ws.gmax + 0 * GMAX_SLOTS, ws.part, ws.pbound);
       else
         launch_wgrad<1>(wblocks, s, rays, ray_stride, z, n_samples, c0, n, ein, ws.g[cur], nullptr, nullptr,
-                        ws.part);
+                        ws.part, emean);
     }
     {
       ProfScope ps(s, PT_BWD_MISC, 0.0, (double)wb0 * WgradCfg<1>::PART * 4.0);

@@ -123,8 +123,8 @@ _TRAIN_FUSED = True   # the library's own default is mode 1 (f16x2_3)
 
 
 def set_remat_version(version: int) -> int:
-    """Select the default training backward's layer kernel (3: k_bwd_remat3, the default; 2: k_bwd_remat2); returns
-    the previous one (pcnerf_set_remat_version)."""
+    """Select the default training backward's layer kernel (3: k_bwd_remat3, the default; 4: k_bwd_remat3 with the
+    epilogue on the W waves; 2: k_bwd_remat2); returns the previous one (pcnerf_set_remat_version)."""
     prev = H.lib().pcnerf_set_remat_version(int(version))
     if prev < 0:
         raise RuntimeError(H.lib().pcnerf_last_error().decode())
