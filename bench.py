@@ -208,25 +208,72 @@ def pmc_traffic(kernel_name: str, line: str = None):
 
 
 # ----------------------------------------------------------------------------------------------- workloads
+def write_kitti_fixture(tmp):
+    """tests/golden/kitti_frames_full.npz (KITTI-00 scans 1151..1200, every 16th point, and their poses) as the
+    reference's on-disk layout under ``tmp``: pcd/<frame>.pcd and poses.txt (identity rows before frame 1150)."""
+    from nof import io as nio
+    g = dict(np.load(os.path.join(HERE, "tests", "golden", "kitti_frames_full.npz"), allow_pickle=False))
+    os.makedirs(os.path.join(tmp, "pcd"), exist_ok=True)
+    for k, v in g.items():
+        if k.startswith("f"):
+            nio.write_pcd(os.path.join(tmp, "pcd", f"{k[1:]}.pcd"), v)
+    with open(os.path.join(tmp, "poses.txt"), "w") as fh:
+        for _ in range(int(g["pose_first"])):
+            fh.write("1 0 0 0 0 1 0 0 0 0 1 0\n")
+        for row in g["poses"]:
+            fh.write(" ".join(repr(float(v)) for v in row) + "\n")
+    return os.path.join(tmp, "pcd"), os.path.join(tmp, "poses.txt")
+
+
+# BASELINE config 5: KITTI-00 frames 1150..1198 as 8 contiguous parent blocks of 6 frames (the fixture holds one
+# 50-frame sequence), each with its own parent box and child boxes; the held-out frames at 80 % frame sparsity
+# (eval_kitti_render.py:1060) rendered by the two-step path
+C5_START, C5_FRAMES, C5_BLOCKS, C5_SPARSITY = 1150, 6, 8, 80
+
+
+def eval_opts(root, pose_path, ds, de, samples=128, importance=256, chunk=262144, extra=""):
+    """eval_kitti_render.get_opts with the KITTI eval shell's settings (shells/pretraining/KITTI00_pcnerf_eval.bash:
+    range_delete 2/1/0.5, over_height 0.168, over_low -2, interest 20 x 20, skip connection, method 2)."""
+    import eval_kitti_render as E
+    return E.get_opts(f"""--dataset kitti --root_dir {root} --pose_path {pose_path} --data_start {ds} --data_end {de}
+        --depth_inference_method 2 --test_data_create 1 --N_samples {samples} --N_importance {importance}
+        --chunk {chunk} --range_delete_x 2 --range_delete_y 1 --range_delete_z 0.5 --over_height 0.168
+        --over_low -2 --interest_x 20 --interest_y 20 --use_skip {extra}""".split())
+
+
+def kitti_view_blocks(dev, blocks=None):
+    """Config 5's rows: for each parent block b (frames C5_START + 6 b + 1 .. + 6) the eval driver's scene (parent
+    cloud of the block's frames, its child boxes, eval_kitti_render.Scene) and the two-step rows (method 2) of the
+    block's held-out frames at 80 % sparsity, built on the GPU (nof.raytable) and concatenated frame after frame
+    (whole ray groups).  -> [{block, rows, other, ranges, frames, groups}]."""
+    import tempfile
+    import eval_kitti_render as E
+    out = []
+    with tempfile.TemporaryDirectory() as tmp:
+        root, poses = write_kitti_fixture(tmp)
+        for b in (range(C5_BLOCKS) if blocks is None else blocks):
+            ds = C5_START + C5_FRAMES * b
+            h = eval_opts(root, poses, ds, ds + C5_FRAMES)
+            scene = E.Scene(h, dev)
+            frames = E.test_frame_ids(ds, ds + C5_FRAMES, C5_SPARSITY)
+            parts = [scene.view_rows(f, 2) for f in frames]
+            rows = torch.cat([p[0] for p in parts])
+            out.append(dict(block=b, rows=rows, ranges=torch.cat([p[1] for p in parts]),
+                            other=torch.cat([p[2] for p in parts]), frames=frames,
+                            groups=int((rows[:, 12] >= -0.5).sum()), children=int(scene.bounds6.shape[0]),
+                            parent6=scene.parent6))
+    return out
+
+
 def kitti_fixture_rays(dev):
     """BASELINE config 3's scene: KITTI-00 scans 1151..1200 (tests/golden/kitti_frames_full.npz, every 16th point)
     at the 50 % frame-sparsity rule (25 train frames, 157,108 rows), its train rays built on the GPU by nof.dataset
     exactly as the parity test builds them (tests/golden/make_config3_full.py)."""
     import tempfile
     from nof import dataset as D
-    from nof import io as nio
-    g = dict(np.load(os.path.join(HERE, "tests", "golden", "kitti_frames_full.npz"), allow_pickle=False))
     sc = dict(np.load(os.path.join(HERE, "tests", "golden", "config3_full_scene.npz"), allow_pickle=False))
     with tempfile.TemporaryDirectory() as tmp:
-        os.makedirs(os.path.join(tmp, "pcd"))
-        for k, v in g.items():
-            if k.startswith("f"):
-                nio.write_pcd(os.path.join(tmp, "pcd", f"{k[1:]}.pcd"), v)
-        with open(os.path.join(tmp, "poses.txt"), "w") as fh:
-            for _ in range(int(g["pose_first"])):
-                fh.write("1 0 0 0 0 1 0 0 0 0 1 0\n")
-            for row in g["poses"]:
-                fh.write(" ".join(repr(float(v)) for v in row) + "\n")
+        write_kitti_fixture(tmp)
         ds = D.kitti_dataload(os.path.join(tmp, "pcd"), split="train", data_start=int(sc["data_start"]),
                               data_end=int(sc["data_end"]), cloud_size_val=64, range_delete_x=3, range_delete_y=2,
                               range_delete_z=1.25, sub_nerf_test_num=0, surface_expand=0.05, over_height=0.168,
@@ -243,12 +290,12 @@ def make_blocks(a, rank, world, dev, syn):
     from nof.blocks import blocks_of_rank, split_groups
     out = []
     if a.config == 5 and a.mode == "view":
-        for b in range(8):
-            vr, vo, vg = syn.make_view_rows(a.rays, n_children=32, seed=1000 * b)
-            s, e = split_groups(vr[:, 12], world)[rank]
-            out.append(dict(block=b, rays=torch.from_numpy(vr[s:e]).to(dev), other=torch.from_numpy(vo[s:e]).to(dev),
-                            gt=torch.from_numpy(vg[s:e]).to(dev), seeds=(1234 + b, 5678 + b), sub_num=32,
-                            groups=int((vr[s:e, 12] >= -0.5).sum())))
+        for kb in kitti_view_blocks(dev):
+            b, vr = kb["block"], kb["rows"]
+            s, e = split_groups(vr[:, 12].cpu().numpy(), world)[rank]
+            out.append(dict(block=b, rays=vr[s:e].contiguous(), other=kb["other"][s:e].contiguous(),
+                            gt=kb["ranges"][s:e].contiguous(), seeds=(1234 + b, 5678 + b),
+                            sub_num=kb["children"], groups=int((vr[s:e, 12] >= -0.5).sum()), frames=kb["frames"]))
         return out
     if a.config == 3:
         scene, n_child = kitti_fixture_rays(dev)
@@ -293,6 +340,9 @@ EXTRA_LINES = {
     # train_fwd -- on one GPU all four blocks, 1,048,576 rays per step
     "config4": dict(config=4, mode="train_fwd", rays=262144, samples=128, importance=256, cpu_rays=None,
                     line="config4"),
+    # BASELINE config 5: the two-step inference of 8 KITTI parent blocks' held-out frames (80 % frame sparsity), all
+    # eight on the one GPU (kitti_view_blocks)
+    "config5": dict(config=5, mode="view", rays=16384, samples=128, importance=256, cpu_rays=None, line="config5"),
     "val": dict(mode="val", rays=65536, samples=128, importance=256, cpu_rays=None),
     "view": dict(mode="view", rays=16384, samples=128, importance=256, cpu_rays=None),
 }
@@ -603,7 +653,7 @@ def run_line(a, L, dev, rank, world):
     n_local = (sum(blk.get("groups", a.rays) for blk in blocks) if view
                else sum(blk["rays"].shape[0] for blk in blocks))
     blocks_rank0 = [blk["block"] for blk in blocks]
-    sample = {k: blocks[0][k] for k in ("block", "rays", "seeds", "sub_num")}
+    sample = {k: blocks[0][k] for k in ("block", "rays", "seeds", "sub_num", "other") if k in blocks[0]}
     del blocks, opt, step, block_step
     gc.collect()
     torch.cuda.empty_cache()
@@ -683,8 +733,9 @@ def line_json(a, world, ln):
                     "nof.dataset, 262,144-ray batches drawn with replacement; seeded NOF weights",
                  4: "synthetic MaiCity-00 parent blocks (x-split of [-12,61]x[-12,12]x[-2,0.5], 256 child AABBs "
                     "each); seeded per-block NOF weights",
-                 5: "synthetic two-step rows (group-size histogram of the reference's KITTI test frames), 8 "
-                    "parent blocks; seeded per-block NOF weights"}[a.config]
+                 5: "KITTI-00 frames 1151-1198 (every 16th point) as 8 contiguous 6-frame parent blocks, two-step "
+                    "rows of each block's held-out frames at 80% frame sparsity built by nof.raytable; seeded "
+                    "per-block NOF weights"}[a.config]
                 + ("; ray groups with the group-size histogram of the reference's KITTI test frames"
                    if view and a.config == 2 else ""),
         "config": {"workload": {"train_fwd": "render_rays_train fwd + range/child losses",
@@ -695,7 +746,8 @@ def line_json(a, world, ln):
                                               "(opt-in)" if train else " -- exact affine fold of the eval network "
                                               "(opt-in)") if a.fold else ""),
                    "baseline_config": a.config,
-                   "rays_per_step": int(ln["rays_per_step"]), "rays_per_block": a.rays,
+                   "rays_per_step": int(ln["rays_per_step"]),
+                   "rays_per_block": None if (view and a.config == 5) else a.rays,
                    "blocks_rank0": ln["blocks_rank0"],
                    "N_samples": a.samples, "N_importance": a.importance,
                    "mlp_samples_per_ray": a.samples + a.samples + a.importance, "chunk": a.chunk,
@@ -943,8 +995,14 @@ def cpu_baseline(a, syn, blk):
 
 def cpu_baseline_view(a, syn, O, threads, blk):
     """Two-step inference (render.py:614-699 restated in oracle/ref_cpu.py) on ``--cpu-rays`` ray groups."""
-    vr, vo, _ = syn.make_view_rows(a.cpu_rays, n_children=32, seed=1000 * blk["block"])
-    rows, other = torch.from_numpy(vr), torch.from_numpy(vo)
+    if blk.get("other") is not None and a.config == 5:   # the first --cpu-rays ray groups of the block's own rows
+        starts = torch.nonzero(blk["rays"][:, 12] >= -0.5).reshape(-1).cpu()
+        end = int(starts[a.cpu_rays]) if a.cpu_rays < starts.numel() else int(blk["rays"].shape[0])
+        rows, other = blk["rays"][:end].cpu(), blk["other"][:end].cpu()
+        a.cpu_rays = min(a.cpu_rays, int(starts.numel()))
+    else:
+        vr, vo, _ = syn.make_view_rows(a.cpu_rays, n_children=32, seed=1000 * blk["block"])
+        rows, other = torch.from_numpy(vr), torch.from_numpy(vo)
     Pc = O.params_from_numpy(syn.init_nof_params(blk["seeds"][0]))
     Pf = O.params_from_numpy(syn.init_nof_params(blk["seeds"][1]))
     with torch.no_grad():

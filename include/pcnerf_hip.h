@@ -100,10 +100,10 @@ int pcnerf_nof_query_train(const float* rays, int64_t n_rays, int ray_stride, co
 int pcnerf_set_train_math(int mode);
 
 /* The default training backward's layer kernel, process-wide; returns the previous one, or -1 for an invalid one.
- * 3 (default): k_bwd_remat3 -- each hidden layer's weight gradient contracted over the 64 encoding columns,
+ * 4 (default): k_bwd_remat3<true> -- each hidden layer's weight gradient contracted over the 64 encoding columns,
  * (sum_s g_L (x) (e - ebar)) P'_{L-1}^T, with P'_{L-1} the chunk's float64 layer map (x = h_{L-1} - mean = P' (e - ebar)
- * under identity activations, models.py:72) applied once per chunk.  4: the same with the BatchNorm-backward epilogue
- * and the g stores on the weight-gradient waves.  2: k_bwd_remat2 (round 5: over the 256 rematerialised input
+ * under identity activations, models.py:72) applied once per chunk; the BatchNorm-backward epilogue and the g stores
+ * on the weight-gradient waves.  3: the same with the epilogue on the data-gradient waves.  2: k_bwd_remat2 (round 5: over the 256 rematerialised input
  * columns).  Same gradients within the parity envelope (tests/test_backward_gpu.py). */
 int pcnerf_set_remat_version(int version);
 

@@ -315,35 +315,7 @@ __global__ __launch_bounds__(256) void k_tf_stats(FoldDev F) {
   if (tid < 64) F.eb[(int64_t)c * 64 + tid] = tid < 63 ? F.e0[(int64_t)c * 64 + tid] + G[tid * 64 + 63] / n : 0.0;
 }
 
-// ---- float64 64 x 64 tiles on v_mfma_f64_16x16x4_f64 (A[l&15][k=l>>4], B[k=l>>4][l&15], D[(l>>4)+4r][l&15]).
-// Four waves per workgroup, wave w owns the 32 x 32 quadrant (rows 32(w>>1), columns 32(w&1)) as 2 x 2 blocks.
-typedef double f64x4 __attribute__((ext_vector_type(4)));
-constexpr int TP = 65;   // LDS pitch (doubles) of a 64-wide tile: odd, so 16 lanes' 8-byte reads are conflict-free
-
-// acc += A B over k in [0, 64): A(r, k) = ATR ? As[k TP + r] : As[r TP + k], B(k, c) = BTR ? Bs[c TP + k] : Bs[k TP + c]
-template <bool ATR, bool BTR>
-__device__ __forceinline__ void mfma64_quad(const double* As, const double* Bs, int R, int Cc, int lane,
-                                            f64x4 (&acc)[2][2]) {
-  const int li = lane & 15, lk = lane >> 4;
-#pragma unroll 4
-  for (int k0 = 0; k0 < 64; k0 += 4) {
-    const int k = k0 + lk;
-    double a[2], b[2];
-#pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      const int r = R + 16 * x + li, c = Cc + 16 * x + li;
-      a[x] = ATR ? As[k * TP + r] : As[r * TP + k];
-      b[x] = BTR ? Bs[c * TP + k] : Bs[k * TP + c];
-    }
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y) acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[y], acc[x][y], 0, 0, 0);
-  }
-}
-
-__device__ __forceinline__ int q_row(int R, int x, int r, int lane) { return R + 16 * x + (lane >> 4) + 4 * r; }
-__device__ __forceinline__ int q_col(int Cc, int y, int lane) { return Cc + 16 * y + (lane & 15); }
+// (float64 64 x 64 tiles on v_mfma_f64_16x16x4_f64: mfma64_quad, common.h)
 
 // ---- 16-row tiles (the layer algebra's kernels): wave w owns the tile's columns 16 w .. 16 w + 15, one 16 x 16
 // block on v_mfma_f64_16x16x4_f64: acc += A B over k in [0, 64) with A(r, k) = ATR ? As[k TP + r] : As[r TP + k]

@@ -1361,14 +1361,21 @@ struct TrainWs {
 // products (k_train_h).  Process-wide; pcnerf_set_train_math.  Mode 1 renders config 2 within 1.9e-5 of a float64
 // evaluation of the same rays (fp32 MFMA: 2.2e-5; the reference itself: 1.1e-4) at 1.9x the speed.
 static int g_train_math = 1;
-// The rematerialised backward's layer kernel: 3 = k_bwd_remat3 (default: weight gradient over the encoding columns,
-// projected by P'^T per chunk), 2 = k_bwd_remat2 (round 5's: over the rematerialised x columns).  PCNERF_REMAT_VER
+// The rematerialised backward's layer kernel: 4 = k_bwd_remat3<true> (default: weight gradient over the encoding
+// columns, projected by P'^T per chunk; BatchNorm-backward epilogue on the W waves), 3 = k_bwd_remat3<false> (the
+// epilogue on the D waves), 2 = k_bwd_remat2 (round 5's: over the rematerialised x columns).  PCNERF_REMAT_VER
 // selects it at load time (A/B measurements).
 static int remat_ver_env() {
   const char* v = getenv("PCNERF_REMAT_VER");
-  return (v && v[0] == '2') ? 2 : (v && v[0] == '4') ? 4 : 3;
+  return (v && v[0] == '2') ? 2 : (v && v[0] == '3') ? 3 : 4;
 }
 static int g_remat_ver = remat_ver_env();
+// version 4's layer-1 launch forms dW_0's encoding columns itself (k_bwd_remat3<true, true>; default); 0 keeps
+// k_wgrad_enc on the stored g_0 (PCNERF_REMAT_FUSE0=0 / pcnerf_set_remat_fuse0, A/B)
+static int g_remat_fuse0 = [] {
+  const char* v = getenv("PCNERF_REMAT_FUSE0");
+  return (v && v[0] == '0') ? 0 : 1;
+}();
 
 static TrainWs carve(void* base, int64_t chunk) {
   const size_t tiles = (size_t)((chunk + 31) / 32);
@@ -4206,6 +4213,11 @@ static_assert(2 * FB_GPART + R3_XC == FB_BUF, "remat3 keeps k_bwd_remat2's tile 
 constexpr int R3_ENC_SLOTS = 3;                          // remat of tile k + 1 and wgrad of tile k, DMA of k + 2
 constexpr size_t R3_LDS = 2 * (size_t)FB_BUF + R3_ENC_SLOTS * FB_ENC + 8 * 128 * sizeof(float);
 static_assert(R3_LDS <= 160 * 1024, "k_bwd_remat3 LDS");
+// layer 1's launch with dW_0's encoding columns fused (LAST): a fourth encoding slot (tile k - 1's image stays until
+// its G_0 is formed) and the half's g_0 tile, split, in the g layout (2 parts x 16 octets x 32 cells x 16 B)
+constexpr int R3_G0 = 2 * 16 * 32 * 16;
+constexpr size_t R3L_LDS = 2 * (size_t)FB_BUF + 4 * FB_ENC + 8 * 128 * sizeof(float) + R3_G0;
+static_assert(R3L_LDS <= 160 * 1024, "k_bwd_remat3<true, true> LDS");
 constexpr size_t GD_PART = WgradCfg<1>::PART;            // 256 x 64 + 256 floats per pair
 constexpr int GD_LAYER = 256 * 64;                       // doubles of one layer's G_d
 // 16-byte chunk c4 (features 4 c4 .. 4 c4 + 3) of sample s: 16 lanes of one k-group (16 samples) on 16 distinct bank
@@ -4247,7 +4259,12 @@ __device__ __forceinline__ void gd_reduce_row(const float* __restrict__ part, in
 // writes its fp32 accumulators to LDS (the xc slot's 16 KiB), a W wave takes tile k - 1's accumulators there after
 // the barrier, finishes g_{L-1} = dy A - (x X + B) and stores it, then makes x of tile k and G_d of tile k (48 MFMAs):
 // per SIMD 96 MFMAs against 48 + the epilogue's VALU, instead of 96 + epilogue against 48.
-template <bool WEPI>
+//
+// LAST (layer 1, with WEPI): g_0 is consumed in the launch that makes it -- its only use is dW_0's encoding columns
+// G_0 = sum_s g_0 (x) d -- so the W waves write their g_0 cells of tile k - 1 to the LDS g_0 tile instead of HBM and
+// form G_0 there (24 more MFMAs: their 32 rows x the 64 encoding columns), one partial set per pair in
+// k_wgrad_enc's layout (part0): k_wgrad_enc and g_0's 1 KiB/sample round trip through HBM are gone.
+template <bool WEPI, bool LAST = false>
 __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ gin, char* __restrict__ gout,
                                                         const f16x8* __restrict__ wt,
                                                         const int* __restrict__ sw, int layer, int64_t n,
@@ -4259,11 +4276,14 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
                                                         const float* __restrict__ rpart, double* __restrict__ rgd,
                                                         const char* __restrict__ enc,
                                                         const f16x8* __restrict__ px, const float* __restrict__ pxs,
-                                                        const unsigned* __restrict__ pbound) {
-  constexpr int NST = 4;   // a D wave's global stores per tile
+                                                        const unsigned* __restrict__ pbound, float* __restrict__ part0) {
+  static_assert(!LAST || WEPI, "the fused layer-0 columns need the W-wave epilogue");
+  constexpr int NST = LAST ? 0 : 4;   // a g-storing wave's global stores per tile
+  constexpr int NS = LAST ? 4 : R3_ENC_SLOTS;   // encoding slots
   extern __shared__ __attribute__((aligned(16))) char fb[];
   char* const enb = fb + 2 * FB_BUF;
-  float* const cst = reinterpret_cast<float*>(enb + R3_ENC_SLOTS * FB_ENC);   // [. | 2^-e | B | . | invstd | A | X | bound]
+  float* const cst = reinterpret_cast<float*>(enb + NS * FB_ENC);   // [. | 2^-e | B | . | invstd | A | X | bound]
+  char* const g0i = enb + NS * FB_ENC + 8 * 128 * sizeof(float);   // LAST: the half's g_0 tile
   const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int rw = wv & 3;   // index within the role
@@ -4341,11 +4361,11 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
     const int tl = pr + k * npair;
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    fb_glds16(enc + (size_t)tl * FB_ENC + wv * 1024 + ln * 16, enb + (k % R3_ENC_SLOTS) * FB_ENC + wv * 1024);
+    fb_glds16(enc + (size_t)tl * FB_ENC + wv * 1024 + ln * 16, enb + (k % NS) * FB_ENC + wv * 1024);
   };
   // W waves: xc of tile k, features 32 rw .. 32 rw + 31 of the half (2 row blocks of P'), enc slot k % 3 -> buffer k & 1
   auto remat_xc = [&](int k) {
-    const char* eb = enb + (k % R3_ENC_SLOTS) * FB_ENC;
+    const char* eb = enb + (k % NS) * FB_ENC;
     char* const xb = fb + (size_t)(k & 1) * FB_BUF + 2 * FB_GPART;
     f32x4 ax[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
 #pragma unroll
@@ -4452,6 +4472,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
       // tile kq's g_{L-1}: its accumulators (LDS) and xr; kq < 0: zero cells to tile 0's own slots (rewritten by
       // this wave's later stores -- same addresses, program order), so every tile has NST stores behind its DMAs
       auto epilogue = [&](int kq) {
+        if (LAST && kq < 0) return;
         const int tq = pr + (kq < 0 ? 0 : kq) * npair;
         const char* adb = fb + (size_t)((kq < 0 ? 0 : kq) & 1) * FB_BUF + 2 * FB_GPART;
 #pragma unroll
@@ -4475,13 +4496,55 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
             const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], mv[0], false, false);
             const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], mv[1], false, false);
             const u32x4 cell = {s0[0], s1[0], s0[1], s1[1]};
-            char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
-            __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));
+            if constexpr (LAST) {
+              *reinterpret_cast<u32x4*>(g0i + (kg & 1) * (R3_G0 / 2) + gs_off(sm, il >> 3)) = cell;
+            } else {
+              char* gt = gout + (size_t)tq * GS_TILE + (kg & 1) * FB_GPART + gs_off(sm, i >> 3);
+              __builtin_nontemporal_store(cell, reinterpret_cast<u32x4*>(gt));
+            }
           }
         }
       };
+      // LAST: G_0 of tile kq, rows 32 rw + 16 jb + 4 kg + r of the half's g_0 (this wave's own epilogue rows, read
+      // back transposed from the g_0 tile) x the 64 encoding columns of tile kq's image (slot kq % 4)
+      f32x4 a0w[2][4];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) a0w[jb][ib] = f32x4{};
+      auto gd0 = [&](int kq) {
+        asm volatile("" ::: "memory");   // the g_0 cell stores above, before the transposed reads
+        const unsigned g0a = fb_lds_addr(g0i), ea = fb_lds_addr(enb + (kq % NS) * FB_ENC);
+        std::array<s16x4, 4> ra[2], rx[4];
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          const int col = 32 * rw + 16 * jb + 4 * trp;
+          const unsigned a0 = g0a + gs_off(tr0, col >> 3) + 2 * (col & 7), a1 = g0a + gs_off(tr1, col >> 3) + 2 * (col & 7);
+          ra[jb] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<R3_G0 / 2>(a0), fb_tr<R3_G0 / 2>(a1)};
+        }
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+          const int c = 16 * ib + 4 * trp;
+          const unsigned a0 = ea + eoff(tr0, c), a1 = ea + eoff(tr1, c);
+          rx[ib] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_ENC / 2>(a0), fb_tr<FB_ENC / 2>(a1)};
+        }
+        fb_lgkm<0>(ra);
+        fb_lgkm<0>(rx);
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+          const f16x8 B0 = join(rx[ib][0], rx[ib][1]), B1 = join(rx[ib][2], rx[ib][3]);
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb) {
+            const f16x8 A0 = join(ra[jb][0], ra[jb][1]), A1 = join(ra[jb][2], ra[jb][3]);
+            a0w[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0, a0w[jb][ib], 0, 0, 0);
+            a0w[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1, a0w[jb][ib], 0, 0, 0);
+            a0w[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0, a0w[jb][ib], 0, 0, 0);
+          }
+        }
+        asm volatile("" ::: "memory");   // the reads above, before the next tile's cell stores
+      };
       auto remat_reg = [&](int k) {
-        const char* eb = enb + (k % R3_ENC_SLOTS) * FB_ENC;
+        const char* eb = enb + (k % NS) * FB_ENC;
         f32x4 ax[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -4514,9 +4577,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
         if (k + 1 < nk) dma_g(k + 1);
         if (k + 2 < nk) dma_enc(k + 2);
         epilogue(k - 1);
+        if (LAST && k > 0) gd0(k - 1);
         remat_reg(k);
         const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
-        const unsigned ga = fb_lds_addr(sp), ea = fb_lds_addr(enb + (k % R3_ENC_SLOTS) * FB_ENC);
+        const unsigned ga = fb_lds_addr(sp), ea = fb_lds_addr(enb + (k % NS) * FB_ENC);
         std::array<s16x4, 4> ra[4], rx[2];
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) {
@@ -4548,6 +4612,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
         __builtin_amdgcn_s_barrier();
       }
       if (nk > 0) epilogue(nk - 1);   // (the loop's last barrier: D's accumulators of tile nk - 1 are in LDS)
+      if (LAST && nk > 0) gd0(nk - 1);
       gmo = wave_max_f(gmo) * gui;
       if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rw) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
       float* const pb = part + (size_t)pr * GD_PART;
@@ -4560,6 +4625,20 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
         for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) pb[(size_t)(64 * rw + 16 * jb + 4 * kg + r) * 64 + col] = aw[jb][ib][r] * cu;
+      }
+      if constexpr (LAST) {   // G_0, unscaled (2^-eo of the g_0 tile, 2^-s of the column); the bias row: exact 0
+        float* const p0 = part0 + (size_t)pr * GD_PART;
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+          const int col = 16 * ib + lm;
+          const float cu = ldexpf(gui, -(col < 3 ? sxyz : 13));
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              p0[(size_t)(128 * hf + 32 * rw + 16 * jb + 4 * kg + r) * 64 + col] = a0w[jb][ib][r] * cu;
+        }
+        if (lane < 32) p0[(size_t)256 * 64 + 128 * hf + 32 * rw + lane] = 0.0f;
       }
     }
   } else if (wv < 4) {
@@ -4665,7 +4744,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
       if (k + 2 < nk) dma_enc(k + 2);
       if (k + 1 < nk) remat_xc(k + 1);
       const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
-      const unsigned ga = fb_lds_addr(sp), ea = fb_lds_addr(enb + (k % R3_ENC_SLOTS) * FB_ENC);
+      const unsigned ga = fb_lds_addr(sp), ea = fb_lds_addr(enb + (k % NS) * FB_ENC);
       std::array<s16x4, 4> ra[4], rx[2];
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
@@ -4735,37 +4814,55 @@ struct GdProj {
   int64_t C, ci;
 };
 __global__ __launch_bounds__(256) void k_gd_proj(GdProj g) {
-  // one 64 x 64 block of dW_L per workgroup: grid (16 = 4 row blocks x 4 column blocks, 7 layers); P'_{L-1} rows
-  // i0..i0+63 and G_d rows j0..j0+63 staged in LDS with coalesced loads, 16 outputs (63-term float64 dots) a thread
-  __shared__ double gs[64][65];
-  __shared__ double ps[64][65];
+  // one 64 x 64 block of dW_L per workgroup: grid (16 = 4 row blocks x 4 column blocks, 7 layers).  G_d rows
+  // j0..j0+63 and P'_{L-1} rows i0..i0+63 (64 encoding columns, the 64th zero) staged in LDS -- every thread's 32
+  // loads issued before its first LDS store -- then the 64 x 64 x 64 product on v_mfma_f64_16x16x4_f64, a 32 x 32
+  // quadrant per wave (mfma64_quad; the VALU form's 1,008 dependent fma per thread and 16 serialised load rounds
+  // took 39 us per chunk)
+  __shared__ double gs[64 * TP];
+  __shared__ double ps[64 * TP];
   const int L = 1 + (int)blockIdx.y, j0 = 64 * ((int)blockIdx.x >> 2), i0 = 64 * ((int)blockIdx.x & 3);
-  const int t = threadIdx.x;
-  const double* gdl = g.gd + (size_t)L * GD_LAYER;
-  const double* pp = g.pp + (((size_t)(L - 1) * g.C + g.ci) * 256) * 64;
-  for (int idx = t; idx < 64 * 64; idx += 256) {
-    const int r = idx >> 6, c = idx & 63;
-    gs[r][c] = gdl[(size_t)(j0 + r) * 64 + c];
-    ps[r][c] = c < 63 ? pp[(size_t)(i0 + r) * 64 + c] : 0.0;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const double* gdl = g.gd + (size_t)L * GD_LAYER + (size_t)j0 * 64;
+  const double* pp = g.pp + (((size_t)(L - 1) * g.C + g.ci) * 256 + i0) * 64;
+  double vg[16], vp[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int idx = t + 256 * q;
+    vg[q] = gdl[idx];
+    vp[q] = (idx & 63) < 63 ? pp[idx] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int idx = t + 256 * q, r = idx >> 6, c = idx & 63;
+    gs[r * TP + c] = vg[q];
+    ps[r * TP + c] = vp[q];
   }
   __syncthreads();
-  const int ti = t & 63, tj = t >> 6;   // column i0 + ti, rows j0 + tj + 4 m
-  double acc[16];
+  const int R = 32 * (w >> 1), Cc = 32 * (w & 1);
+  f64x4 acc[2][2];
 #pragma unroll
-  for (int m = 0; m < 16; ++m) acc[m] = 0.0;
-  for (int k = 0; k < 63; ++k) {
-    const double p = ps[ti][k];
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int m = 0; m < 16; ++m) acc[m] = fma(gs[tj + 4 * m][k], p, acc[m]);
-  }
-  const double alpha = (double)g.coef[1024 * (L - 1) + 512 + i0 + ti];
+    for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // acc(r, c) = sum_k G_d[j0 + r][k] P'[i0 + c][k]
+  mfma64_quad<false, true>(gs, ps, R, Cc, lane, acc);
   const int in_f = in_features(L), wc = L == 4 ? 63 : 0;
   double* const dW = g.dW[L];
 #pragma unroll
-  for (int m = 0; m < 16; ++m) dW[(size_t)(j0 + tj + 4 * m) * in_f + wc + i0 + ti] += alpha * acc[m];
-  if (L == 4 && i0 == 0 && ti < 63) {   // the skip layer's encoding columns: its input there is e itself
+  for (int y = 0; y < 2; ++y) {
+    const int i = i0 + q_col(Cc, y, lane);
+    const double alpha = (double)g.coef[1024 * (L - 1) + 512 + i];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) dW[(size_t)(j0 + tj + 4 * m) * in_f + ti] += gs[tj + 4 * m][ti];
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dW[(size_t)(j0 + q_row(R, x, r, lane)) * in_f + wc + i] += alpha * acc[x][y][r];
+  }
+  if (L == 4 && i0 == 0) {   // the skip layer's encoding columns: its input there is e itself
+    for (int idx = t; idx < 64 * 63; idx += 256) {
+      const int r = idx / 63, c = idx - 63 * r;
+      dW[(size_t)(j0 + r) * in_f + c] += gs[r * TP + c];
+    }
   }
 }
 
@@ -5159,6 +5256,8 @@ static void remat3_layers(const NofParamsDev& P, const GaccLayout& G, const BwdW
   const double dn = (double)n;
   const int64_t ntiles = (n + 31) / 32;
   const unsigned fbg = (unsigned)(2 * FB_PAIRS);
+  float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
+  const bool fuse0 = g_remat_ver == 4 && g_remat_fuse0;   // layer 1's launch forms dW_0's encoding columns
   for (int L = 7; L >= 1; --L) {
     const float* coefp = ws.coef + 1024 * (L - 1);
     const char* gin = L == 4 ? S2 : S[(7 - L) & 1];
@@ -5170,20 +5269,24 @@ static void remat3_layers(const NofParamsDev& P, const GaccLayout& G, const BwdW
     // (2 x 256 x 256: G_L = sum g (x) x, formed here as (sum g (x) d) P'^T); issued on the matrix pipe per sample:
     // 2 x 256 x 256 + 2 x 256 x 64 (G_d) + 2 x 256 x 64 (x), x 3 products.  Bytes: g_L in (1 KiB), the encoding
     // image (256 B), g_{L-1} out (1 KiB)
-    ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0) * dn, (1024.0 + 256.0 + 1024.0) * dn);
-    auto launch = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), R3_LDS, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,
+    // (layer 1 fused: + 2 x 256 x 64 of dW_0's encoding columns; g_0 stays in LDS: 1 KiB less out)
+    const bool last = fuse0 && L == 1;
+    ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0 + (last ? 2.0 * 256.0 * 64.0 : 0.0)) * dn,
+                 (1024.0 + 256.0 + (last ? 0.0 : 1024.0)) * dn);
+    auto launch = [&](auto kern, size_t lds) {
+      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), lds, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,
                          (const int*)ws.sw, L, n, coefp, (const float*)(ws.bnb + 512 * (L - 1)), P.bn_w[L - 1],
                          ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
                          pset[L & 1], rpart, rgd, (const char*)encimg, prow(L - 1), psrow(L - 1),
-                         (const unsigned*)ws.pbound);
+                         (const unsigned*)ws.pbound, last ? part_e0 : (float*)nullptr);
     };
-    if (g_remat_ver == 4) launch(k_bwd_remat3<true>);
-    else launch(k_bwd_remat3<false>);
+    if (last) launch(k_bwd_remat3<true, true>, R3L_LDS);
+    else if (g_remat_ver == 4) launch(k_bwd_remat3<true>, R3_LDS);
+    else launch(k_bwd_remat3<false>, R3_LDS);
   }
-  const int ne = (int)std::min<int64_t>(ntiles, 2 * FB_PAIRS);   // g_0's partial sets (one per workgroup)
-  float* const part_e0 = ws.part + 2 * (size_t)FB_PAIRS * WgradCfg<2>::PART;
-  {
+  // g_0's partial sets: one per pair from the fused layer-1 launch, else one per workgroup of k_wgrad_enc
+  const int ne = fuse0 ? FB_PAIRS : (int)std::min<int64_t>(ntiles, 2 * FB_PAIRS);
+  if (!fuse0) {
     // 2 x 256 x 64 fp32-FLOP per sample; 1 KiB of g + 256 B of encoding in
     ProfScope ps(s, PT_BWD_WGRAD_H, 2.0 * 256.0 * 64 * dn, (1024.0 + 256.0) * dn);
     hipLaunchKernelGGL(k_wgrad_enc, dim3(2 * FB_PAIRS), dim3(512), WE_LDS, s, (const char*)S[1], (const char*)nullptr,
@@ -5221,6 +5324,8 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                                 (int)R3_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat3<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)R3_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat3<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)R3L_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_enc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WE_LDS));
     pcn_attr_done(attr);

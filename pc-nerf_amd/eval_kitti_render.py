@@ -86,12 +86,31 @@ def get_opts(argv=None):
     a('--device', type=str, default='cuda')
     a('--batch_rows', type=int, default=0, help="rows per render call (0: the reference's 4096 KITTI / 18432 MaiCity)")
     a('--dist_backend', type=str, default='nccl', help="collective backend under torchrun (nccl = RCCL)")
+    a('--frame_sparsity', type=int, default=20,
+      help="held-out frame rule of eval_kitti_render.py:1054-1062 (percent; 20 is the reference's active one)")
     return p.parse_args(argv)
 
 
-def test_frame_ids(data_start, data_end):
-    """eval_kitti_render.py:1025-1026 (frame sparsity 20 %): the held-out frames."""
-    return [j + 1 for j in range(data_start, data_end) if (j + 1 - 3 - data_start) % 5 == 0]
+# the rendered (held-out) frames per frame sparsity (%), eval_kitti_render.py:1054-1062 (20 % active, the others in
+# its comments): frame j + 1 is rendered when rule(j + 1 - data_start) holds
+EVAL_SPARSITY_RULES = {
+    20: lambda k: (k - 3) % 5 == 0,
+    25: lambda k: k % 4 == 0,
+    33: lambda k: k % 3 == 0,
+    50: lambda k: k % 2 == 0,
+    67: lambda k: (k - 1) % 3 != 0,
+    75: lambda k: (k - 1) % 4 != 0,
+    80: lambda k: (k - 3) % 5 != 0,
+    90: lambda k: (k - 5) % 10 != 0,
+}
+
+
+def test_frame_ids(data_start, data_end, sparsity=20):
+    """eval_kitti_render.py:1053-1062: the held-out frames at a frame sparsity (20 %: the active rule)."""
+    if int(sparsity) not in EVAL_SPARSITY_RULES:
+        raise ValueError(f"frame sparsity {sparsity}: one of {sorted(EVAL_SPARSITY_RULES)}")
+    rule = EVAL_SPARSITY_RULES[int(sparsity)]
+    return [j + 1 for j in range(data_start, data_end) if rule(j + 1 - data_start)]
 
 
 def batch_slices(group_col: np.ndarray, batch_rows: int):
@@ -263,7 +282,7 @@ def _run(h, rank, world):
     batch_rows = h.batch_rows or (18432 if h.dataset == "maicity" else 4096)
     scene = None
     report = []
-    for f in test_frame_ids(h.data_start, h.data_end):
+    for f in test_frame_ids(h.data_start, h.data_end, h.frame_sparsity):
         t0 = time.perf_counter()
         cdir = cache_dir(h, f)
         if h.test_data_create:

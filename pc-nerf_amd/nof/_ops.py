@@ -123,8 +123,9 @@ _TRAIN_FUSED = True   # the library's own default is mode 1 (f16x2_3)
 
 
 def set_remat_version(version: int) -> int:
-    """Select the default training backward's layer kernel (3: k_bwd_remat3, the default; 4: k_bwd_remat3 with the
-    epilogue on the W waves; 2: k_bwd_remat2); returns the previous one (pcnerf_set_remat_version)."""
+    """Select the default training backward's layer kernel (4: k_bwd_remat3 with the BatchNorm-backward epilogue on
+    the W waves, the default; 3: k_bwd_remat3 with it on the D waves; 2: k_bwd_remat2); returns the previous one
+    (pcnerf_set_remat_version)."""
     prev = H.lib().pcnerf_set_remat_version(int(version))
     if prev < 0:
         raise RuntimeError(H.lib().pcnerf_last_error().decode())
@@ -132,7 +133,7 @@ def set_remat_version(version: int) -> int:
 
 
 def get_remat_version() -> int:
-    v = set_remat_version(3)
+    v = set_remat_version(4)
     set_remat_version(v)
     return v
 

@@ -67,17 +67,17 @@ def named(m):
     return dict(m.named_parameters())
 
 
-@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused", "f16x2_3_fused_remat2", "f16x2_3_fused_remat4",
+@pytest.fixture(params=["f16x2_3", "fp32", "f16x2_3_fused", "f16x2_3_fused_remat2", "f16x2_3_fused_remat3",
                         "f16x2_3_fused_store"])
 def train_math(request):
-    """The layered split math, fp32 MFMA, the default (fused forward + rematerialising backward, k_bwd_remat3), the
-    same with round 5's layer kernel (k_bwd_remat2) and with the W-wave epilogue (k_bwd_remat3<true>, version 4),
-    and the default forward with round 4's activation-store backward."""
+    """The layered split math, fp32 MFMA, the default (fused forward + rematerialising backward, k_bwd_remat3<true>:
+    the W-wave epilogue, version 4), the same with round 5's layer kernel (k_bwd_remat2) and with the D-wave
+    epilogue (k_bwd_remat3<false>, version 3), and the default forward with round 4's activation-store backward."""
     from nof import _ops
     mode = request.param
     prev = _ops.set_train_math("f16x2_3_fused" if mode.startswith("f16x2_3_fused") else mode)
     prevb = _ops.set_train_backward("store" if mode.endswith("_store") else "remat")
-    prevr = _ops.set_remat_version(2 if mode.endswith("_remat2") else 4 if mode.endswith("_remat4") else 3)
+    prevr = _ops.set_remat_version(2 if mode.endswith("_remat2") else 3 if mode.endswith("_remat3") else 4)
     yield mode
     _ops.set_train_math(prev)
     _ops.set_train_backward(prevb)

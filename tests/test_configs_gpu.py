@@ -227,6 +227,79 @@ def test_config4_maicity_blocks(tmp_path):
                     f64=golden("config4_maicity_f64"), alt=golden("config4_maicity_alt"))
 
 
+# ----------------------------------------------------------------------------------------------- config 5
+def test_config5_kitti_blocks_two_step(tmp_path):
+    """BASELINE config 5 at its shape on the fixture's one sequence: KITTI-00 frames 1150..1198 as 8 contiguous
+    6-frame parent blocks (bench.kitti_view_blocks: each block's own parent cloud and child boxes, eval_kitti_render
+    .Scene), the two-step rows of every block's held-out frames at 80 % frame sparsity (eval_kitti_render.py:1060).
+    Per block: the rows of its first held-out frame bit for bit against the oracle's row builder (oracle/rays_cpu.py:
+    the scan filter, block transform and interest region of eval_kitti_render.py:621-660 on the oracle's float32
+    relative poses; child boxes from the same parent cloud), the row table's group structure, and a 256-group slice
+    rendered two-step (render.py:614-699) against the oracle on the same rows and weights: effective flags equal,
+    depths / points within 1e-4."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import eval_kitti_render as E
+    import nof.dataset as D
+    from test_dataset import oracle_poses_from
+    from oracle import dataset_cpu as OD, ref_cpu as O, rays_cpu as RC
+    from nof.render import render_rays_view_0525_2_2
+    blocks = bench.kitti_view_blocks(DEV)
+    assert [b["block"] for b in blocks] == list(range(8))
+    g = golden("kitti_frames_full")
+    root, pose_path = bench.write_kitti_fixture(str(tmp_path))
+    rd, interest = (2.0, 1.0, 0.5), 20.0
+    for kb in blocks:
+        ds = bench.C5_START + bench.C5_FRAMES * kb["block"]
+        de = ds + bench.C5_FRAMES
+        assert kb["frames"] == [ds + k for k in range(1, bench.C5_FRAMES + 1) if (k - 3) % 5 != 0]   # 80 %: 5 of 6
+        rows = kb["rows"].cpu().numpy()
+        starts = np.nonzero(rows[:, 12] >= -0.5)[0]
+        assert kb["groups"] == len(starts) > 1000 and starts[0] == 0
+        # a group's head row carries its row count - 1, its continuation rows -1
+        assert np.array_equal(np.diff(np.append(starts, len(rows))) - 1, rows[starts, 12].astype(np.int64))
+        # the first held-out frame's rows vs the oracle
+        f = kb["frames"][0]
+        P = oracle_poses_from(g, pose_path, ds)
+        positions = np.stack([P[k + 1][:3, 3] for k in range(ds, de)])
+        pts = OD.filter_scan(g[f"f{f}"], rd, 0.168, -2.0, strict_range=True)
+        w = OD.interest_filter(D.to_block(torch.from_numpy(pts), torch.from_numpy(P[f])).numpy(), positions,
+                               interest, interest)
+        parent = D.fuse_frames(root, D.relative_poses(D.read_poses(pose_path), ds), ds, de, "cpu", rd, 0.168, -2.0,
+                               interest, interest)
+        cells = OD.split_children(parent.numpy())
+        b6 = np.concatenate([np.stack([a for a, _ in cells]), np.stack([b for _, b in cells])], 1)
+        p6 = kb["parent6"].cpu().numpy()
+        orows, orng, ooth, _ = RC.build_view_rows(w, P[f][:3, 3].astype(np.float64), b6, p6[:3], p6[3:], 2)
+        n0 = orows.shape[0]
+        assert kb["children"] == b6.shape[0]
+        np.testing.assert_array_equal(rows[:n0], orows, err_msg=f"block {kb['block']} frame {f}")
+        np.testing.assert_array_equal(kb["other"][:n0].cpu().numpy(), ooth)
+        np.testing.assert_array_equal(kb["ranges"][:n0].cpu().numpy(), orng)
+        report(f"config5_kitti_b{kb['block']}_rows", frames=len(kb["frames"]), rows=len(rows), groups=kb["groups"],
+               children=kb["children"])
+    # two-step render of block 3's first 256 groups vs the oracle (seeded block weights, as the bench)
+    kb = blocks[3]
+    starts = torch.nonzero(kb["rows"][:, 12] >= -0.5).reshape(-1)
+    end = int(starts[256])
+    rows, other = kb["rows"][:end], kb["other"][:end]
+    seeds = (1234 + 3, 5678 + 3)
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(seeds[0])).to(DEV).eval()
+    mf = syn.load_into(NOF_fine(), syn.init_nof_params(seeds[1])).to(DEV).eval()
+    with torch.no_grad():
+        res = render_rays_view_0525_2_2(mc, mf, Embedding(3, 10), rows, other, N_samples=128, N_importance=256,
+                                        perturb=0, noise_std=0, chunk=262144, depth_inference_method=2)
+        ref = O.render_rays_view(O.params_from_numpy(syn.init_nof_params(seeds[0])),
+                                 O.params_from_numpy(syn.init_nof_params(seeds[1])), rows.cpu(), other.cpu(), 128,
+                                 256, 262144, method=2)
+    for k in ("rays_effective_flag", "rays_effective_flag_fine"):
+        assert torch.equal(res[k].reshape(-1).cpu().bool(), ref[k].reshape(-1).bool()), k
+    for k in ("depth", "depth_fine", "points_inference", "points_inference_fine"):
+        close(res[k].cpu(), ref[k], what=k)
+    report("config5_kitti_b3_render", rows=end, depth_fine_max_rel=max_rel(res["depth_fine"].cpu(), ref["depth_fine"]))
+
+
 # ----------------------------------------------------------------------------------------------- config 3
 def kitti_scene_full(tmp_path):
     """BASELINE config 3's scene: KITTI-00 scans 1151..1200 (tests/golden/kitti_frames_full.npz, every 16th point)

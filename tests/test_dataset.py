@@ -44,9 +44,14 @@ def write_scene(tmp, name="kitti_frames"):
 def oracle_poses(g, pose_path):
     """ipb2dmapping.py:566-584 restated: every row of the file, then one batched float32 T_start^-1 @ poses (the
     batched product's rounding depends on the batch, so the whole file goes through it, as in the reference)."""
+    return oracle_poses_from(g, pose_path, DS)
+
+
+def oracle_poses_from(g, pose_path, data_start):
+    """oracle_poses relative to frame ``data_start`` + 1 (another block's start)."""
     P = np.asarray([np.vstack([np.loadtxt([ln]).reshape(3, 4), [[0, 0, 0, 1.0]]]) @ D.T_VELO2CAM
                     for ln in open(pose_path).read().splitlines()])
-    rel = (torch.from_numpy(np.linalg.inv(P[DS + 1])).float() @ torch.tensor(P, dtype=torch.float32)).numpy()
+    rel = (torch.from_numpy(np.linalg.inv(P[data_start + 1])).float() @ torch.tensor(P, dtype=torch.float32)).numpy()
     return {int(g["pose_first"]) + i: rel[int(g["pose_first"]) + i] for i in range(len(g["poses"]))}
 
 

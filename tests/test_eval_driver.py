@@ -14,6 +14,14 @@ from oracle import dataset_cpu as OD
 def test_test_frames():
     assert E.test_frame_ids(1150, 1200) == [1153 + 5 * i for i in range(10)]
     assert E.test_frame_ids(0, 50)[:2] == [3, 8]
+    # the commented rules of eval_kitti_render.py:1055-1062; 80 % renders exactly the frames 20 % trains on less
+    t20, t80 = set(E.test_frame_ids(1150, 1200)), set(E.test_frame_ids(1150, 1200, 80))
+    assert len(t80) == 40 and not t20 & t80 and t20 | t80 == set(range(1151, 1201))
+    for sp, n in ((25, 12), (33, 16), (50, 25), (67, 33), (75, 37), (90, 45)):
+        assert len(E.test_frame_ids(1150, 1200, sp)) == n, sp
+    assert E.test_frame_ids(1150, 1156, 80) == [1151, 1152, 1154, 1155, 1156]   # config 5's 6-frame block
+    with pytest.raises(ValueError):
+        E.test_frame_ids(0, 10, 40)
 
 
 def _groups(sizes):
