@@ -79,7 +79,7 @@ def parse(argv=None):
     ap.add_argument("--chunk", type=int, default=262144)
     ap.add_argument("--cpu-rays", type=int, default=None,
                     help="bounded CPU-baseline sample (rays; default %d on every line, or the whole line when "
-                         "smaller; 512 ray groups for view)" % CPU_SAMPLE_RAYS)
+                         "smaller; ray groups for view)" % CPU_SAMPLE_RAYS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32-line", action="store_true",
                     help="skip the comparison run of the train lines under the fp32 MFMA train math (profiling)")
@@ -666,7 +666,7 @@ def run_line(a, L, dev, rank, world):
     cpu = cdref = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline belongs to the N=1 line only
         if a.cpu_rays is None:
-            a.cpu_rays = 512 if view else min(CPU_SAMPLE_RAYS, a.rays)
+            a.cpu_rays = min(CPU_SAMPLE_RAYS, a.rays)
         if a.fold:
             (_ops.set_train_fold if train else _ops.set_eval_fold)(True)
         log(f"{a.mode}: CPU baseline on {a.cpu_rays} rays")
