@@ -4264,6 +4264,9 @@ __device__ __forceinline__ void gd_reduce_row(const float* __restrict__ part, in
 // G_0 = sum_s g_0 (x) d -- so the W waves write their g_0 cells of tile k - 1 to the LDS g_0 tile instead of HBM and
 // form G_0 there (24 more MFMAs: their 32 rows x the 64 encoding columns), one partial set per pair in
 // k_wgrad_enc's layout (part0): k_wgrad_enc and g_0's 1 KiB/sample round trip through HBM are gone.
+#ifndef PCN_R3_KREG
+#define PCN_R3_KREG 1   // the W waves' per-feature epilogue / remat constants in registers (0: read from LDS, A/B)
+#endif
 template <bool WEPI, bool LAST = false>
 __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ gin, char* __restrict__ gout,
                                                         const f16x8* __restrict__ wt,
@@ -4469,6 +4472,21 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
         return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
       };
       auto eoff = [](int r, int c) { return r * 128 + 16 * ((c >> 3) ^ ((r >> 1) & 7)) + 2 * (c & 7); };
+      // the epilogue's and the remat's per-feature constants A, X, B of this wave's 2 x 4 features: in registers
+      // for the launch (24 VGPRs; 6 KiB of LDS reads per wave and tile saved), except in layer 1's fused launch,
+      // whose G_0 accumulators take those registers
+      f32x4 kA[2], kX[2], kB[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int il = 32 * rw + 16 * rb + 4 * kg;
+        kA[rb] = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+        kX[rb] = *reinterpret_cast<const f32x4*>(cst + 768 + il);
+        kB[rb] = *reinterpret_cast<const f32x4*>(cst + 256 + il);
+      }
+      constexpr bool KREG = PCN_R3_KREG && !LAST;
+      auto cA_of = [&](int rb, int il) { return KREG ? kA[rb] : *reinterpret_cast<const f32x4*>(cst + 640 + il); };
+      auto cX_of = [&](int rb, int il) { return KREG ? kX[rb] : *reinterpret_cast<const f32x4*>(cst + 768 + il); };
+      auto cB_of = [&](int rb, int il) { return KREG ? kB[rb] : *reinterpret_cast<const f32x4*>(cst + 256 + il); };
       // tile kq's g_{L-1}: its accumulators (LDS) and xr; kq < 0: zero cells to tile 0's own slots (rewritten by
       // this wave's later stores -- same addresses, program order), so every tile has NST stores behind its DMAs
       auto epilogue = [&](int kq) {
@@ -4478,7 +4496,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           const int il = 32 * rw + 16 * rb + 4 * kg, i = 128 * hf + il;
-          const f32x4 cA = *reinterpret_cast<const f32x4*>(cst + 640 + il);
+          const f32x4 cA = cA_of(rb, il);
 #pragma unroll
           for (int sb = 0; sb < 2; ++sb) {
             const int sm = 16 * sb + lm;
@@ -4565,8 +4583,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           const int il = 32 * rw + 16 * rb + 4 * kg;
-          const f32x4 X = *reinterpret_cast<const f32x4*>(cst + 768 + il);
-          const f32x4 B = *reinterpret_cast<const f32x4*>(cst + 256 + il);
+          const f32x4 X = cX_of(rb, il), B = cB_of(rb, il);
 #pragma unroll
           for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
