@@ -4866,6 +4866,25 @@ __global__ __launch_bounds__(256) void k_gd_proj(GdProj g) {
   mfma64_quad<false, true>(gs, ps, R, Cc, lane, acc);
   const int in_f = in_features(L), wc = L == 4 ? 63 : 0;
   double* const dW = g.dW[L];
+  // the read-modify-writes of the float64 accumulators: every load issued before the first store (the compiler
+  // cannot tell the addresses apart, so interleaved += serialised 16 round trips: 20 us per launch)
+  double old[2][2][4];
+#pragma unroll
+  for (int y = 0; y < 2; ++y)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        old[x][y][r] = dW[(size_t)(j0 + q_row(R, x, r, lane)) * in_f + wc + i0 + q_col(Cc, y, lane)];
+  double ek[16];
+  const bool skip = L == 4 && i0 == 0;   // the skip layer's encoding columns: its input there is e itself
+  if (skip) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int idx = t + 256 * q, r = idx / 63, c = idx - 63 * r;
+      ek[q] = idx < 64 * 63 ? dW[(size_t)(j0 + r) * in_f + c] : 0.0;
+    }
+  }
 #pragma unroll
   for (int y = 0; y < 2; ++y) {
     const int i = i0 + q_col(Cc, y, lane);
@@ -4873,12 +4892,14 @@ __global__ __launch_bounds__(256) void k_gd_proj(GdProj g) {
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dW[(size_t)(j0 + q_row(R, x, r, lane)) * in_f + wc + i] += alpha * acc[x][y][r];
+      for (int r = 0; r < 4; ++r)
+        dW[(size_t)(j0 + q_row(R, x, r, lane)) * in_f + wc + i] = old[x][y][r] + alpha * acc[x][y][r];
   }
-  if (L == 4 && i0 == 0) {   // the skip layer's encoding columns: its input there is e itself
-    for (int idx = t; idx < 64 * 63; idx += 256) {
-      const int r = idx / 63, c = idx - 63 * r;
-      dW[(size_t)(j0 + r) * in_f + c] += gs[r * TP + c];
+  if (skip) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int idx = t + 256 * q, r = idx / 63, c = idx - 63 * r;
+      if (idx < 64 * 63) dW[(size_t)(j0 + r) * in_f + c] = ek[q] + gs[r * TP + c];
     }
   }
 }

@@ -9,5 +9,5 @@ if [ "$TESTS" != "0" ]; then
   rc=$?; tail -2 gpurun_out/smoke.log; echo "smoke rc=$rc"; [ $rc -ne 0 ] && exit $rc
 fi
 s=$(date +%s)
-timeout -k 10 600 python3 bench.py ${BENCH_ARGS} > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err
+timeout -k 10 600 python3 bench.py ${BENCH_ARGS} --detail gpurun_out/bench_default_detail.json > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err
 rc=$?; echo "bench rc=$rc wall=$(( $(date +%s) - s ))s"; exit $rc

@@ -14,7 +14,7 @@ HB=$!
 trap "kill $HB 2>/dev/null" EXIT
 echo "python3 bench.py --no-cpu-baseline --no-fp32-line $*" > $OUT/command.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
-  python3 bench.py --no-cpu-baseline --no-fp32-line "$@" > $OUT/stats_bench.json 2> $OUT/stats.err
+  python3 bench.py --no-cpu-baseline --no-fp32-line --detail $OUT/stats_detail.json "$@" > $OUT/stats_bench.json 2> $OUT/stats.err
 rc=$?; echo "stats rc=$rc"; [ $rc -ne 0 ] && exit $rc
 rm -f $OUT/stats/*kernel_trace.csv   # per-dispatch trace: the stats file carries the averages
 for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
@@ -22,7 +22,7 @@ for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_A
          "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
   N=$(echo $C | tr ' ' '_' | cut -c1-40)
   timeout -s KILL 400 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_$N -o run -- \
-    python3 bench.py --no-cpu-baseline --no-fp32-line "$@" --steps 1 --warmup 0 > $OUT/pmc_$N.json 2> $OUT/pmc_$N.err
+    python3 bench.py --no-cpu-baseline --no-fp32-line --detail "" "$@" --steps 1 --warmup 0 > $OUT/pmc_$N.json 2> $OUT/pmc_$N.err
   rc=$?; echo "pmc $N rc=$rc"; [ $rc -ne 0 ] && exit $rc
   python3 scripts/compact_pmc.py $OUT/pmc_$N
 done
