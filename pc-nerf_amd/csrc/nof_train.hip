@@ -4264,6 +4264,10 @@ __device__ __forceinline__ void gd_reduce_row(const float* __restrict__ part, in
 // G_0 = sum_s g_0 (x) d -- so the W waves write their g_0 cells of tile k - 1 to the LDS g_0 tile instead of HBM and
 // form G_0 there (24 more MFMAs: their 32 rows x the 64 encoding columns), one partial set per pair in
 // k_wgrad_enc's layout (part0): k_wgrad_enc and g_0's 1 KiB/sample round trip through HBM are gone.
+#ifndef PCN_R3_ABL
+#define PCN_R3_ABL 0    // timing-only ablations of k_bwd_remat3<true> (wrong results): 1 W waves idle, 2 D waves
+                        // without MFMAs, 3 D waves' B operands from registers instead of LDS
+#endif
 #ifndef PCN_R3_KREG
 #define PCN_R3_KREG 1   // the W waves' per-feature epilogue / remat constants in registers (0: read from LDS, A/B)
 #endif
@@ -4428,18 +4432,19 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks)
         asm volatile("" ::"v"(wr[ks][0][0]), "v"(wr[ks][0][1]), "v"(wr[ks][1][0]), "v"(wr[ks][1][1]));
+      constexpr int ABL = LAST ? 0 : PCN_R3_ABL;
       for (int k = 0; k < nk; ++k) {
         if (k + 1 < nk) dma_g(k + 1);
         if (k + 2 < nk) dma_enc(k + 2);
         char* const sp = fb + (size_t)(k & 1) * FB_BUF;
         f32x4 ad[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
+        for (int ks = 0; ks < (ABL == 2 ? 0 : 8); ++ks)
 #pragma unroll
           for (int sb = 0; sb < 2; ++sb) {
             const int o = gs_off(16 * sb + lm, 4 * ks + kg);
-            const f16x8 bh = *reinterpret_cast<const f16x8*>(sp + o);
-            const f16x8 bm = *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
+            const f16x8 bh = ABL == 3 ? wr[(ks + 1) & 7][sb][0] : *reinterpret_cast<const f16x8*>(sp + o);
+            const f16x8 bm = ABL == 3 ? wr[(ks + 2) & 7][sb][1] : *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
               ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bh, ad[rb][sb], 0, 0, 0);
@@ -4590,9 +4595,16 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
             for (int q = 0; q < 4; ++q) xr[rb][sb][q] = fmaf(ax[rb][sb][q], X[q], B[q]);
         }
       };
+      constexpr int ABLW = LAST ? 0 : PCN_R3_ABL;
       for (int k = 0; k < nk; ++k) {
         if (k + 1 < nk) dma_g(k + 1);
         if (k + 2 < nk) dma_enc(k + 2);
+        if (ABLW == 1) {
+          __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_s_barrier();
+          continue;
+        }
         epilogue(k - 1);
         if (LAST && k > 0) gd0(k - 1);
         remat_reg(k);
