@@ -1372,6 +1372,15 @@ static int remat_ver_env() {
 static int g_remat_ver = remat_ver_env();
 // version 4's layer-1 launch forms dW_0's encoding columns itself (k_bwd_remat3<true, true>; default); 0 keeps
 // k_wgrad_enc on the stored g_0 (PCNERF_REMAT_FUSE0=0 / pcnerf_set_remat_fuse0, A/B)
+// version 4's hidden layers with eight W waves (three waves per SIMD: each W wave half the epilogue / remat / G_d
+// rows); PCNERF_REMAT_W8=1 (A/B)
+#ifndef PCN_R3_W8_DEFAULT
+#define PCN_R3_W8_DEFAULT 0
+#endif
+static int g_remat_w8 = [] {
+  const char* v = getenv("PCNERF_REMAT_W8");
+  return v ? (v[0] == '1' ? 1 : 0) : PCN_R3_W8_DEFAULT;
+}();
 static int g_remat_fuse0 = [] {
   const char* v = getenv("PCNERF_REMAT_FUSE0");
   return (v && v[0] == '0') ? 0 : 1;
@@ -4266,13 +4275,19 @@ __device__ __forceinline__ void gd_reduce_row(const float* __restrict__ part, in
 // k_wgrad_enc's layout (part0): k_wgrad_enc and g_0's 1 KiB/sample round trip through HBM are gone.
 #ifndef PCN_R3_ABL
 #define PCN_R3_ABL 0    // timing-only ablations of k_bwd_remat3<true> (wrong results): 1 W waves idle, 2 D waves
-                        // without MFMAs, 3 D waves' B operands from registers instead of LDS
+                        // without MFMAs, 3 D waves' B operands from registers instead of LDS, 4 no DMA waits
+#endif
+#ifndef PCN_R3_WORDER
+#define PCN_R3_WORDER 2   // W waves: G_d's transposed reads issued 1 after the epilogue / 2 before it (0: after remat)
+#endif
+#ifndef PCN_R3_DPF
+#define PCN_R3_DPF 0      // D waves: the next k-step's B operands read one k-step ahead into registers
 #endif
 #ifndef PCN_R3_KREG
 #define PCN_R3_KREG 1   // the W waves' per-feature epilogue / remat constants in registers (0: read from LDS, A/B)
 #endif
-template <bool WEPI, bool LAST = false>
-__global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ gin, char* __restrict__ gout,
+template <bool WEPI, bool LAST = false, int NW = 4>
+__global__ __launch_bounds__(64 * (4 + NW), 1) void k_bwd_remat3(const char* __restrict__ gin, char* __restrict__ gout,
                                                         const f16x8* __restrict__ wt,
                                                         const int* __restrict__ sw, int layer, int64_t n,
                                                         const float* __restrict__ coefp, const float* __restrict__ bnb,
@@ -4285,7 +4300,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
                                                         const f16x8* __restrict__ px, const float* __restrict__ pxs,
                                                         const unsigned* __restrict__ pbound, float* __restrict__ part0) {
   static_assert(!LAST || WEPI, "the fused layer-0 columns need the W-wave epilogue");
-  constexpr int NST = LAST ? 0 : 4;   // a g-storing wave's global stores per tile
+  static_assert(NW == 4 || (NW == 8 && WEPI && !LAST), "eight W waves: the W-wave epilogue, hidden layers");
+  // NW W waves: FW features of the half each (RBW row blocks of 16) and GR rows of G_d (JBW blocks of 16)
+  constexpr int FW = 128 / NW, RBW = FW / 16, GR = 256 / NW, JBW = GR / 16;
+  constexpr int NST = LAST ? 0 : 2 * RBW;   // a g-storing wave's global stores per tile
   constexpr int NS = LAST ? 4 : R3_ENC_SLOTS;   // encoding slots
   extern __shared__ __attribute__((aligned(16))) char fb[];
   char* const enb = fb + 2 * FB_BUF;
@@ -4293,7 +4311,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
   char* const g0i = enb + NS * FB_ENC + 8 * 128 * sizeof(float);   // LAST: the half's g_0 tile
   const int t = threadIdx.x, lane = t & 63, kg = lane >> 4, lm = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int rw = wv & 3;   // index within the role
+  const int rw = wv & 3;   // index within the role (D waves)
+  const int rwW = wv - 4;  // index within the W role
   const int bid = (int)blockIdx.x, hf = (bid >> 3) & 1, pr = ((bid >> 4) << 3) | (bid & 7);
   const int npair = (int)gridDim.x >> 1;
   const int nt = (int)((n + 31) / 32);
@@ -4324,22 +4343,22 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
   }
   // W waves: their P' rows (features 32 rw .. 32 rw + 31 of the half, 64 columns, hi / mid) in registers for the
   // whole launch -- the same 8 f16x8 every tile (the LDS copy cost 8 KiB of reads per wave and tile)
-  f16x8 pa_r[2][2][2];   // [ks][rb][part]
+  f16x8 pa_r[2][RBW][2];   // [ks][rb][part]
   if (wv >= 4) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
         for (int p = 0; p < 2; ++p)
-          pa_r[ks][rb][p] = px[(size_t)(128 * hf + 32 * rw + 16 * rb + lm) * 16 + (2 * ks + p) * 4 + kg];
+          pa_r[ks][rb][p] = px[(size_t)(128 * hf + FW * rwW + 16 * rb + lm) * 16 + (2 * ks + p) * 4 + kg];
   }
   const int eg = gexp[layer];
   const float gun = ldexpf(1.0f, -eg);
   __syncthreads();
   float obm = cst[896];
 #pragma unroll
-  for (int i = 1; i < 8; ++i) obm = fmaxf(obm, cst[896 + i]);
+  for (int i = 1; i < 4 + NW; ++i) obm = fmaxf(obm, cst[896 + i]);
   const int eo = tile_scale_exp(obm);
   const float gso = ldexpf(1.0f, eo);
   if (bid == 0 && t == 0) gexp[layer - 1] = eo;
@@ -4374,7 +4393,9 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
   auto remat_xc = [&](int k) {
     const char* eb = enb + (k % NS) * FB_ENC;
     char* const xb = fb + (size_t)(k & 1) * FB_BUF + 2 * FB_GPART;
-    f32x4 ax[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+    f32x4 ax[RBW][2];
+#pragma unroll
+    for (int rb = 0; rb < RBW; ++rb) ax[rb][0] = ax[rb][1] = f32x4{};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const auto& pa = pa_r[ks];
@@ -4384,7 +4405,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
         const f16x8 bh = *reinterpret_cast<const f16x8*>(eb + o);
         const f16x8 bm = *reinterpret_cast<const f16x8*>(eb + FB_ENC / 2 + o);
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
+        for (int rb = 0; rb < RBW; ++rb) {
           ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][0], bh, ax[rb][sb], 0, 0, 0);
           ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][0], bm, ax[rb][sb], 0, 0, 0);
           ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][1], bh, ax[rb][sb], 0, 0, 0);
@@ -4392,8 +4413,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
       }
     }
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      const int il = 32 * rw + 16 * rb + 4 * kg;
+    for (int rb = 0; rb < RBW; ++rb) {
+      const int il = FW * rwW + 16 * rb + 4 * kg;
       const f32x4 X = *reinterpret_cast<const f32x4*>(cst + 768 + il);
       const f32x4 B = *reinterpret_cast<const f32x4*>(cst + 256 + il);
 #pragma unroll
@@ -4406,9 +4427,11 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
     }
   };
   if (nk > 0) {
-    dma_g(0);
-    dma_enc(0);
-    if (nk > 1) dma_enc(1);
+    if (wv < 8) {   // (waves 8.. of the eight-W-wave form issue no DMA)
+      dma_g(0);
+      dma_enc(0);
+      if (nk > 1) dma_enc(1);
+    }
     __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
     __builtin_amdgcn_s_barrier();
     if (!WEPI && wv >= 4) remat_xc(0);
@@ -4438,13 +4461,27 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
         if (k + 2 < nk) dma_enc(k + 2);
         char* const sp = fb + (size_t)(k & 1) * FB_BUF;
         f32x4 ad[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
-#pragma unroll
-        for (int ks = 0; ks < (ABL == 2 ? 0 : 8); ++ks)
+        constexpr bool DPF = !LAST && PCN_R3_DPF;
+        f16x8 bq[2][2][2];   // DPF: [k-step parity][sb][part], the next k-step's operands read ahead
+        auto bload = [&](int ks) {
 #pragma unroll
           for (int sb = 0; sb < 2; ++sb) {
             const int o = gs_off(16 * sb + lm, 4 * ks + kg);
-            const f16x8 bh = ABL == 3 ? wr[(ks + 1) & 7][sb][0] : *reinterpret_cast<const f16x8*>(sp + o);
-            const f16x8 bm = ABL == 3 ? wr[(ks + 2) & 7][sb][1] : *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
+            bq[ks & 1][sb][0] = *reinterpret_cast<const f16x8*>(sp + o);
+            bq[ks & 1][sb][1] = *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
+          }
+        };
+        if (DPF) bload(0);
+#pragma unroll
+        for (int ks = 0; ks < (ABL == 2 ? 0 : 8); ++ks) {
+          if (DPF && ks + 1 < 8) bload(ks + 1);
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb) {
+            const int o = gs_off(16 * sb + lm, 4 * ks + kg);
+            const f16x8 bh = DPF ? bq[ks & 1][sb][0] : ABL == 3 ? wr[(ks + 1) & 7][sb][0]
+                                                               : *reinterpret_cast<const f16x8*>(sp + o);
+            const f16x8 bm = DPF ? bq[ks & 1][sb][1] : ABL == 3 ? wr[(ks + 2) & 7][sb][1]
+                                                               : *reinterpret_cast<const f16x8*>(sp + FB_GPART + o);
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
               ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][0], bh, ad[rb][sb], 0, 0, 0);
@@ -4452,13 +4489,14 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
               ad[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[ks][rb][1], bh, ad[rb][sb], 0, 0, 0);
             }
           }
+        }
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
           for (int sb = 0; sb < 2; ++sb)
             *reinterpret_cast<f32x4*>(sp + 2 * FB_GPART + r3_xoff(16 * sb + lm, (32 * rw + 16 * rb + 4 * kg) >> 2)) =
                 ad[rb][sb];
-        __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
+        if (ABL != 4) __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_s_barrier();
       }
@@ -4466,10 +4504,12 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
       // ---- W: epilogue + stores of tile k - 1, x of tile k (registers), G_d of tile k
       const float gui = ldexpf(1.0f, -eo);
       float gmo = 0.0f;
-      f32x4 xr[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};   // x X + B of the previous tile
-      f32x4 aw[4][2];
+      f32x4 xr[RBW][2];   // x X + B of the previous tile
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
+      for (int rb = 0; rb < RBW; ++rb) xr[rb][0] = xr[rb][1] = f32x4{};
+      f32x4 aw[JBW][2];
+#pragma unroll
+      for (int jb = 0; jb < JBW; ++jb)
 #pragma unroll
         for (int ib = 0; ib < 2; ++ib) aw[jb][ib] = f32x4{};
       const int trq = lm >> 2, trp = lm & 3, tr0 = 8 * kg + trq, tr1 = tr0 + 4;
@@ -4480,10 +4520,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
       // the epilogue's and the remat's per-feature constants A, X, B of this wave's 2 x 4 features: in registers
       // for the launch (24 VGPRs; 6 KiB of LDS reads per wave and tile saved), except in layer 1's fused launch,
       // whose G_0 accumulators take those registers
-      f32x4 kA[2], kX[2], kB[2];
+      f32x4 kA[RBW], kX[RBW], kB[RBW];
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const int il = 32 * rw + 16 * rb + 4 * kg;
+      for (int rb = 0; rb < RBW; ++rb) {
+        const int il = FW * rwW + 16 * rb + 4 * kg;
         kA[rb] = *reinterpret_cast<const f32x4*>(cst + 640 + il);
         kX[rb] = *reinterpret_cast<const f32x4*>(cst + 768 + il);
         kB[rb] = *reinterpret_cast<const f32x4*>(cst + 256 + il);
@@ -4499,8 +4539,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
         const int tq = pr + (kq < 0 ? 0 : kq) * npair;
         const char* adb = fb + (size_t)((kq < 0 ? 0 : kq) & 1) * FB_BUF + 2 * FB_GPART;
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          const int il = 32 * rw + 16 * rb + 4 * kg, i = 128 * hf + il;
+        for (int rb = 0; rb < RBW; ++rb) {
+          const int il = FW * rwW + 16 * rb + 4 * kg, i = 128 * hf + il;
           const f32x4 cA = cA_of(rb, il);
 #pragma unroll
           for (int sb = 0; sb < 2; ++sb) {
@@ -4568,7 +4608,9 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
       };
       auto remat_reg = [&](int k) {
         const char* eb = enb + (k % NS) * FB_ENC;
-        f32x4 ax[2][2] = {{f32x4{}, f32x4{}}, {f32x4{}, f32x4{}}};
+        f32x4 ax[RBW][2];
+#pragma unroll
+        for (int rb = 0; rb < RBW; ++rb) ax[rb][0] = ax[rb][1] = f32x4{};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const auto& pa = pa_r[ks];
@@ -4578,7 +4620,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
             const f16x8 bh = *reinterpret_cast<const f16x8*>(eb + o);
             const f16x8 bm = *reinterpret_cast<const f16x8*>(eb + FB_ENC / 2 + o);
 #pragma unroll
-            for (int rb = 0; rb < 2; ++rb) {
+            for (int rb = 0; rb < RBW; ++rb) {
               ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][0], bh, ax[rb][sb], 0, 0, 0);
               ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][0], bm, ax[rb][sb], 0, 0, 0);
               ax[rb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[rb][1], bh, ax[rb][sb], 0, 0, 0);
@@ -4586,8 +4628,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
           }
         }
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          const int il = 32 * rw + 16 * rb + 4 * kg;
+        for (int rb = 0; rb < RBW; ++rb) {
+          const int il = FW * rwW + 16 * rb + 4 * kg;
           const f32x4 X = cX_of(rb, il), B = cB_of(rb, il);
 #pragma unroll
           for (int sb = 0; sb < 2; ++sb)
@@ -4597,53 +4639,60 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
       };
       constexpr int ABLW = LAST ? 0 : PCN_R3_ABL;
       for (int k = 0; k < nk; ++k) {
-        if (k + 1 < nk) dma_g(k + 1);
-        if (k + 2 < nk) dma_enc(k + 2);
+        if (wv < 8 && k + 1 < nk) dma_g(k + 1);
+        if (wv < 8 && k + 2 < nk) dma_enc(k + 2);
         if (ABLW == 1) {
           __builtin_amdgcn_s_waitcnt(fb_vmcnt(0));
           __builtin_amdgcn_s_waitcnt(0xC07F);
           __builtin_amdgcn_s_barrier();
           continue;
         }
-        epilogue(k - 1);
-        if (LAST && k > 0) gd0(k - 1);
-        remat_reg(k);
         const char* const sp = fb + (size_t)(k & 1) * FB_BUF;
         const unsigned ga = fb_lds_addr(sp), ea = fb_lds_addr(enb + (k % NS) * FB_ENC);
-        std::array<s16x4, 4> ra[4], rx[2];
+        std::array<s16x4, 4> ra[JBW], rx[2];
+        auto gd_reads = [&]() {
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) {
-          const int col = 64 * rw + 16 * jb + 4 * trp;
-          const unsigned a0 = ga + gs_off(tr0, col >> 3) + 2 * (col & 7), a1 = ga + gs_off(tr1, col >> 3) + 2 * (col & 7);
-          ra[jb] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_GPART>(a0), fb_tr<FB_GPART>(a1)};
-        }
+          for (int jb = 0; jb < JBW; ++jb) {
+            const int col = GR * rwW + 16 * jb + 4 * trp;
+            const unsigned a0 = ga + gs_off(tr0, col >> 3) + 2 * (col & 7), a1 = ga + gs_off(tr1, col >> 3) + 2 * (col & 7);
+            ra[jb] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_GPART>(a0), fb_tr<FB_GPART>(a1)};
+          }
 #pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-          const int c = 32 * hf + 16 * ib + 4 * trp;
-          const unsigned a0 = ea + eoff(tr0, c), a1 = ea + eoff(tr1, c);
-          rx[ib] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_ENC / 2>(a0), fb_tr<FB_ENC / 2>(a1)};
-        }
+          for (int ib = 0; ib < 2; ++ib) {
+            const int c = 32 * hf + 16 * ib + 4 * trp;
+            const unsigned a0 = ea + eoff(tr0, c), a1 = ea + eoff(tr1, c);
+            rx[ib] = std::array<s16x4, 4>{fb_tr<0>(a0), fb_tr<0>(a1), fb_tr<FB_ENC / 2>(a0), fb_tr<FB_ENC / 2>(a1)};
+          }
+          asm volatile("" ::: "memory");   // (issued before the LDS reads that follow)
+        };
+        constexpr int WO = LAST ? 0 : PCN_R3_WORDER;
+        if (WO == 2) gd_reads();
+        epilogue(k - 1);
+        if (LAST && k > 0) gd0(k - 1);
+        if (WO == 1) gd_reads();
+        remat_reg(k);
+        if (WO == 0) gd_reads();
         fb_lgkm<0>(ra);
         fb_lgkm<0>(rx);
 #pragma unroll
         for (int ib = 0; ib < 2; ++ib) {
           const f16x8 B0 = join(rx[ib][0], rx[ib][1]), B1 = join(rx[ib][2], rx[ib][3]);
 #pragma unroll
-          for (int jb = 0; jb < 4; ++jb) {
+          for (int jb = 0; jb < JBW; ++jb) {
             const f16x8 A0 = join(ra[jb][0], ra[jb][1]), A1 = join(ra[jb][2], ra[jb][3]);
             aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0, aw[jb][ib], 0, 0, 0);
             aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1, aw[jb][ib], 0, 0, 0);
             aw[jb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0, aw[jb][ib], 0, 0, 0);
           }
         }
-        __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs (its stores may fly)
+        if (ABLW != 4) __builtin_amdgcn_s_waitcnt(fb_vmcnt(NST));   // this wave's DMAs (its stores may fly)
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_s_barrier();
       }
       if (nk > 0) epilogue(nk - 1);   // (the loop's last barrier: D's accumulators of tile nk - 1 are in LDS)
       if (LAST && nk > 0) gd0(nk - 1);
       gmo = wave_max_f(gmo) * gui;
-      if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rw) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
+      if (lane == 0) atomicMax(gmax_out + ((bid * 4 + rwW) & (GMAX_SLOTS - 1)), __float_as_uint(gmo));
       float* const pb = part + (size_t)pr * GD_PART;
       const int sxyz = remat_sx(0, __uint_as_float(*pbound));
 #pragma unroll
@@ -4651,9 +4700,9 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
         const int col = 32 * hf + 16 * ib + lm;
         const float cu = ldexpf(gun, -(col < 3 ? sxyz : 13));
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
+        for (int jb = 0; jb < JBW; ++jb)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) pb[(size_t)(64 * rw + 16 * jb + 4 * kg + r) * 64 + col] = aw[jb][ib][r] * cu;
+          for (int r = 0; r < 4; ++r) pb[(size_t)(GR * rwW + 16 * jb + 4 * kg + r) * 64 + col] = aw[jb][ib][r] * cu;
       }
       if constexpr (LAST) {   // G_0, unscaled (2^-eo of the g_0 tile, 2^-s of the column); the bias row: exact 0
         float* const p0 = part0 + (size_t)pr * GD_PART;
@@ -4819,7 +4868,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_remat3(const char* __restrict__ 
   }
   // the previous layer's G_d partials, one row per workgroup (LDS as scratch)
   __syncthreads();
-  if (rpart) gd_reduce_row<512>(rpart, FB_PAIRS, rgd, reinterpret_cast<double*>(fb), t);
+  if (rpart) gd_reduce_row<64 * (4 + NW)>(rpart, FB_PAIRS, rgd, reinterpret_cast<double*>(fb), t);
 }
 
 // after layer 1's launch: layer 1's G_d (grid.y 0) and layer 0's encoding columns from k_wgrad_enc's g_0 sets
@@ -5323,14 +5372,15 @@ static void remat3_layers(const NofParamsDev& P, const GaccLayout& G, const BwdW
     const bool last = fuse0 && L == 1;
     ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0 + (last ? 2.0 * 256.0 * 64.0 : 0.0)) * dn,
                  (1024.0 + 256.0 + (last ? 0.0 : 1024.0)) * dn);
-    auto launch = [&](auto kern, size_t lds) {
-      hipLaunchKernelGGL(kern, dim3(fbg), dim3(512), lds, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,
+    auto launch = [&](auto kern, size_t lds, unsigned threads = 512) {
+      hipLaunchKernelGGL(kern, dim3(fbg), dim3(threads), lds, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,
                          (const int*)ws.sw, L, n, coefp, (const float*)(ws.bnb + 512 * (L - 1)), P.bn_w[L - 1],
                          ws.gexp, (const float*)(ws.wcol + (L - 1) * 256), gmin, ws.gmax + (L - 1) * GMAX_SLOTS,
                          pset[L & 1], rpart, rgd, (const char*)encimg, prow(L - 1), psrow(L - 1),
                          (const unsigned*)ws.pbound, last ? part_e0 : (float*)nullptr);
     };
     if (last) launch(k_bwd_remat3<true, true>, R3L_LDS);
+    else if (g_remat_ver == 4 && g_remat_w8) launch(k_bwd_remat3<true, false, 8>, R3_LDS, 768);
     else if (g_remat_ver == 4) launch(k_bwd_remat3<true>, R3_LDS);
     else launch(k_bwd_remat3<false>, R3_LDS);
   }
@@ -5376,6 +5426,8 @@ static void remat_chunk(const NofParamsDev& P, const GaccLayout& G, const BwdWs&
                                 (int)R3_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat3<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)R3L_LDS));
+    PCN_HIP(hipFuncSetAttribute((const void*)k_bwd_remat3<true, false, 8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)R3_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_g7, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G7_LDS));
     PCN_HIP(hipFuncSetAttribute((const void*)k_wgrad_enc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WE_LDS));
     pcn_attr_done(attr);

@@ -4,5 +4,5 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 600 python3 scripts/lib_ab.py abl0 abl1 abl2 abl3 --steps 5 --rounds 2 > gpurun_out/r6f_abl.txt 2>&1
+timeout -k 10 600 python3 scripts/lib_ab.py ${ABL_NAMES:-abl0 abl1 abl2 abl3} --steps 5 --rounds 2 > gpurun_out/r6f_abl.txt 2>&1
 rc=$?; cat gpurun_out/r6f_abl.txt; exit $rc
