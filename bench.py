@@ -817,9 +817,10 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
               16: "k_tf_moments", 17: "k_tf_layer+k_tf_bwd_layer+k_tf_dw",
               # (the train query writing the activation store is its own instantiation)
               18: "k_nof_eval_h3<true,true>" if a.mode == "train_step" and not remat else "k_nof_eval_h3<true,false>",
-              19: ({3: "k_bwd_remat3<false>", 4: "k_bwd_remat3<true>"}.get(rver, "k_bwd_remat2<0>") if remat
+              19: ({3: "k_bwd_remat3<false,false,4>", 4: "k_bwd_remat3<true,false,4>"}.get(rver, "k_bwd_remat2<0>") if remat
                    else "k_bwd_fused<0,false>")}
-    pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd", 20: "k_g7"}
+    pmc_names = {**knames, 4: "k_train_out", 7: "k_resample", 9: "k_composite_bwd", 20: "k_g7",
+                 21: "k_bwd_remat3<true,true,4>"}
     tag = max(knames, key=lambda t: prof_read(L, t)[0])
     kname = knames[tag]
     ktime_ms, klaunch, kflops, kbytes = prof_read(L, tag)
@@ -828,7 +829,7 @@ def kernel_report(L, a, train_math, eval_math=None, line=None):
                   (5, "bn_fold"), (6, "composite"), (7, "resample"), (8, "sample"), (9, "composite_bwd"),
                   (10, "wgrad"), (11, "dgrad"), (12, "bwd_other"), (13, "eval_fold"), (14, "wgrad_b3"),
                   (15, "train_h1"), (16, "fold_moments"), (17, "fold_algebra"), (18, "train_query"),
-                  (19, "bwd_fused"), (20, "bwd_remat_operands")):
+                  (19, "bwd_fused"), (20, "bwd_remat_operands"), (21, "bwd_fused_layer1")):
         tm, n, f, b = prof_read(L, t)
         if n:
             tr, src = pmc_traffic(pmc_names.get(t, ""), line)

@@ -5370,7 +5370,8 @@ static void remat3_layers(const NofParamsDev& P, const GaccLayout& G, const BwdW
     // image (256 B), g_{L-1} out (1 KiB)
     // (layer 1 fused: + 2 x 256 x 64 of dW_0's encoding columns; g_0 stays in LDS: 1 KiB less out)
     const bool last = fuse0 && L == 1;
-    ProfScope ps(s, PT_BWD_FUSED, (2.0 * 2.0 * 256.0 * 256.0 + (last ? 2.0 * 256.0 * 64.0 : 0.0)) * dn,
+    ProfScope ps(s, last ? PT_BWD_FUSED_L1 : PT_BWD_FUSED,
+                 (2.0 * 2.0 * 256.0 * 256.0 + (last ? 2.0 * 256.0 * 64.0 : 0.0)) * dn,
                  (1024.0 + 256.0 + (last ? 0.0 : 1024.0)) * dn);
     auto launch = [&](auto kern, size_t lds, unsigned threads = 512) {
       hipLaunchKernelGGL(kern, dim3(fbg), dim3(threads), lds, s, gin, gout, ws.wth16 + (size_t)(L - 1) * HW_H,

@@ -26,6 +26,7 @@ enum ProfTag {
   PT_TRAIN_QUERY = 18, // k_nof_eval_h3<true>: the fused train-mode query (per-chunk BatchNorm coefficients)
   PT_BWD_FUSED = 19,   // k_bwd_remat / k_bwd_fused: one layer's data + weight gradient in one pass
   PT_BWD_REMAT = 20,   // the rematerialised backward's per-chunk operands: encoding image (k_remat_enc), g_7 (k_g7)
+  PT_BWD_FUSED_L1 = 21,// k_bwd_remat3<true, true>: layer 1 with dW_0's encoding columns formed in LDS
 };
 extern bool g_prof_on;
 class ProfScope {
