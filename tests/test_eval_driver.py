@@ -223,3 +223,27 @@ def test_eval_driver_two_ranks_writes_the_same_pcd(tmp_path):
         a = open(f"{tmp_path}/pcd/w1_{r['frame']}_two_step.pcd", "rb").read()
         b = open(f"{tmp_path}/pcd/w2_{r['frame']}_two_step.pcd", "rb").read()
         assert r["points"] > 0 and a == b
+
+
+@pytest.mark.gpu
+def test_eval_driver_frame_sparsity_80(tmp_path):
+    """--frame_sparsity 80 (eval_kitti_render.py:1060, BASELINE config 5's rule): main() renders exactly the frames
+    the 80 % rule holds out -- the complement of the 20 % rule's -- and each frame's rendered row count is the one its
+    two-step rows give (the reference's batching rule: all rows but a lone last one)."""
+    from test_dataset import write_scene, DS, DE, INTEREST
+    root, pose_path, g = write_scene(str(tmp_path))
+    base = f"""--dataset kitti --root_dir {root} --pose_path {pose_path} --data_start {DS} --data_end {DE}
+     --test_data_create 1 --depth_inference_method 2 --N_samples 32 --N_importance 64 --chunk 8192
+     --range_delete_x 3 --range_delete_y 2 --range_delete_z 1.25 --over_height 0.168 --over_low -2.0
+     --interest_x {INTEREST} --interest_y {INTEREST} --use_skip --result_path {tmp_path}/res
+     --pcd_path {tmp_path}/pcd/s80_ --frame_sparsity 80"""
+    rep = E.main(base.split())
+    frames = [r["frame"] for r in rep]
+    assert frames == E.test_frame_ids(DS, DE, 80) == [f for f in range(DS + 1, DE + 1)
+                                                      if f not in E.test_frame_ids(DS, DE)]
+    h = E.get_opts(base.split())
+    scene = E.Scene(h, "cuda")
+    for r in rep:
+        rows, _, _, _ = scene.view_rows(r["frame"], 2)
+        assert r["rows"] == sum(e - s for s, e in E.batch_slices(rows[:, 12].cpu().numpy(), 4096)) > 0
+        assert os.path.exists(f"{tmp_path}/pcd/s80_{r['frame']}_two_step.pcd")
