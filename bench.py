@@ -362,10 +362,18 @@ def main(argv=None):
     if a.dry_run:
         return dry_run(a, world, rank)
     dist = world > 1
+    # test-only: PCNERF_BENCH_SHARE_GPU=1 puts every rank on cuda:0 with the gloo backend (RCCL needs one GPU per
+    # rank), so the N-rank path runs on a one-GPU box (tests/test_dist_gpu.py); the driver's runs never set it
+    share = os.environ.get("PCNERF_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            tdist.init_process_group("gloo")
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     from nof import _hip
     L = _hip.lib()

@@ -284,3 +284,35 @@ def test_fit_data_parallel_checkpoints_rank_independent(tmp_path):
             np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
         nbt = [k for k in s0 if k.endswith("num_batches_tracked")]
         assert nbt and all(int(s0[k]) > 3 for k in nbt)   # every rank's chunks counted
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_on_one_gpu(cfg, tmp_path):
+    """bench.py --gpus 2 end to end -- launcher, one process per rank, the config's sharding (2: a block per rank;
+    3: a data-parallel batch with the gradient all-reduce; 4: blocks dealt and depths gathered; 5: every block's
+    whole ray groups split and gathered), barrier-bracketed timing, max over ranks, rank 0's line with the rank
+    report -- with both ranks on the one GPU of this box over gloo (PCNERF_BENCH_SHARE_GPU: RCCL needs a GPU per
+    rank; the driver's N-GPU runs take the same code with nccl)."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PCNERF_BENCH_SHARE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(os.path.dirname(here), "bench.py"), "--gpus", "2", "--config", str(cfg),
+           "--steps", "2", "--warmup", "1", "--samples", "32", "--importance", "64", "--no-ceiling",
+           "--detail", str(tmp_path / "detail.json")] + ([] if cfg == 5 else ["--rays", "4096"])
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    d = line["dist"]
+    assert line["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["backend"] == "gloo"
+    assert len(d["rays_per_rank"]) == 2 and min(d["rays_per_rank"]) > 0 and line["value"] > 0
+    assert line["config"]["rays_per_step"] == sum(d["rays_per_rank"])
+    if cfg in (2, 3):   # weak scaling: every rank its own 4,096 rays
+        assert d["rays_per_rank"] == [4096, 4096]
+    if cfg == 5:        # whole ray groups of every block, shares within a few percent
+        assert max(d["rays_per_rank"]) <= 1.1 * min(d["rays_per_rank"])
+    assert line["cpu_baseline"] is None   # the CPU baseline belongs to the N = 1 line
