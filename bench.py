@@ -361,7 +361,7 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.dry_run:
         return dry_run(a, world, rank)
-    dist = world > 1
+    dist = dist_on(world)
     # test-only: PCNERF_BENCH_SHARE_GPU=1 puts every rank on cuda:0 with the gloo backend (RCCL needs one GPU per
     # rank), so the N-rank path runs on a one-GPU box (tests/test_dist_gpu.py); the driver's runs never set it
     share = os.environ.get("PCNERF_BENCH_SHARE_GPU") == "1"
@@ -498,6 +498,13 @@ def add_ceiling(roof, ceiling):
         roof["frac_of_measured_ceiling"] = round(roof["issued_TFLOPs"] / ceiling["TFLOPs"], 4)
 
 
+def dist_on(world):
+    """Whether this run goes through torch.distributed: N > 1, or (test-only, PCNERF_BENCH_FORCE_DIST=1 under a
+    one-process torchrun) N = 1 over a one-rank RCCL group, so every collective of the N-rank path runs through RCCL
+    on a one-GPU box (tests/test_dist_gpu.py); the driver's runs never set it."""
+    return world > 1 or os.environ.get("PCNERF_BENCH_FORCE_DIST") == "1"
+
+
 def run_line(a, L, dev, rank, world):
     """One bench line: ``a.warmup`` untimed + ``a.steps`` timed steps of ``a.mode`` on this rank's blocks, the
     kernel breakdown / roofline of the last step, the fp32-MFMA comparison and (rank 0, N=1) the CPU baseline."""
@@ -507,7 +514,7 @@ def run_line(a, L, dev, rank, world):
     from nof.criteria import nof_loss
     from nof.networks import Embedding, NOF_coarse, NOF_fine
     from nof.render import render_rays_train, render_rays_val, render_rays_view_0525_2_2
-    dist = world > 1
+    dist = dist_on(world)
     if dist:
         import torch.distributed as tdist
 

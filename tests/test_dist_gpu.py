@@ -316,3 +316,36 @@ def test_bench_two_ranks_on_one_gpu(cfg, tmp_path):
     if cfg == 5:        # whole ray groups of every block, shares within a few percent
         assert max(d["rays_per_rank"]) <= 1.1 * min(d["rays_per_rank"])
     assert line["cpu_baseline"] is None   # the CPU baseline belongs to the N = 1 line
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+@pytest.mark.timeout(300)
+def test_bench_one_rank_rccl(cfg, tmp_path):
+    """bench.py under torch.distributed.run with one process and PCNERF_BENCH_FORCE_DIST=1: the N-rank code path
+    (barriers, max over ranks, the config's gather / gradient all-reduce, the rank report) over a one-rank RCCL
+    group, so every collective the driver's N-GPU runs issue executes through RCCL on this box's one GPU."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PCNERF_BENCH_FORCE_DIST="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "PCNERF_BENCH_SHARE_GPU"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(os.path.dirname(here), "bench.py"), "--gpus", "1", "--config", str(cfg),
+           "--steps", "2", "--warmup", "1", "--samples", "32", "--importance", "64", "--no-ceiling",
+           "--no-cpu-baseline", "--no-extra", "--detail", str(tmp_path / "detail.json")] + \
+        ([] if cfg == 5 else ["--rays", "4096"])
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    d = line["dist"]
+    assert line["n_gpus"] == 1 and d["ranks_seen"] == 1 and d["backend"] == "nccl"
+    assert d["rays_per_rank"] == [line["config"]["rays_per_step"]] and line["value"] > 0
+    if cfg in (3, 4, 5):   # the step's collective ran (gradient all-reduce / depth gather) and was timed
+        assert d["collective_ms_per_step_per_rank"][0] > 0
