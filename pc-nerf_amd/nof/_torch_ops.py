@@ -29,6 +29,26 @@ def _packed_floats() -> int:
     return _PACKED[0]
 
 
+def _need(op: str, name: str, t: Optional[Tensor], shape: tuple, dtype=torch.float32) -> None:
+    """Host-side check of one operand against the layout its kernel's grid and reads assume: a contiguous ``dtype``
+    device tensor of ``shape`` (None: any size, ``('min', k)``: at least k)."""
+    if t is None:
+        return
+    H.require_device(t)
+    if t.dtype != dtype or not t.is_contiguous():
+        raise RuntimeError(f"pcnerf::{op}: {name} must be a contiguous {dtype} device tensor")
+    ok = t.dim() == len(shape)
+    for have, want in zip(t.shape, shape):
+        if want is None:
+            continue
+        if isinstance(want, tuple):
+            ok = ok and have >= want[1]
+        else:
+            ok = ok and have == want
+    if not ok:
+        raise RuntimeError(f"pcnerf::{op}: {name} has shape {tuple(t.shape)}, expected {shape}")
+
+
 # ----------------------------------------------------------------------------------------------- embedding
 @torch.library.custom_op(f"{NS}::embed", mutates_args=())
 def embed(x: Tensor) -> Tensor:
@@ -46,6 +66,7 @@ def _(x):
 def sample_coarse(rays: Tensor, n_samples: int, n_parent: int, near_col: int, far_col: int, cn_col: int,
                   cf_col: int, disparity: bool) -> Tensor:
     """Coarse z (render.py:429-442; the segmented merge when n_parent < n_samples)."""
+    _need("sample_coarse", "rays", rays, (None, None))
     return _ops.sample_coarse(rays, n_samples, n_parent, near_col, far_col, cn_col, cf_col, disparity)
 
 
@@ -57,6 +78,8 @@ def _(rays, n_samples, n_parent, near_col, far_col, cn_col, cf_col, disparity):
 @torch.library.custom_op(f"{NS}::perturb", mutates_args=())
 def perturb(z: Tensor, amount: float, rand: Tensor) -> Tensor:
     """Stratified perturbation (render.py:449-454)."""
+    _need("perturb", "z", z, (None, None))
+    _need("perturb", "rand", rand, tuple(z.shape))
     return _ops.perturb(z, amount, rand)
 
 
@@ -68,6 +91,8 @@ def _(z, amount, rand):
 @torch.library.custom_op(f"{NS}::resample", mutates_args=())
 def resample(z: Tensor, w: Tensor, n_importance: int, u: Optional[Tensor]) -> Tensor:
     """sample_pdf + sort(cat(z, samples)) (render.py:371-412, 463-467)."""
+    _need("resample", "z", z, (None, None))
+    _need("resample", "w", w, tuple(z.shape))
     return _ops.resample(z, w, n_importance, u)
 
 
@@ -88,6 +113,31 @@ def _(bins, weights, n_samples, det, u):
 
 
 # ----------------------------------------------------------------------------------------------- network (eval)
+# pcnerf_nof_params' tensor shapes (models.py: 4 + 4 Linear/BatchNorm1d layers of 256, the skip layer's input
+# [x, h_3] 63 + 256 wide, occ_out 256 -> 1): the kernels index them at these sizes, so the operator checks them
+_LIN_IN = (63, 256, 256, 256, 319, 256, 256, 256)
+
+
+def _param_shapes() -> list:
+    return ([(256, k) for k in _LIN_IN] + [(256,)] * 40 + [(1, 256), (1,)])
+
+
+def _check_query(rays: Tensor, z: Tensor, packed: Tensor) -> None:
+    """The host-side checks before pcnerf_nof_query_eval's launch: its grid and reads assume these layouts."""
+    H.require_device(rays, z, packed)
+    for name, t in (("rays", rays), ("z", z), ("packed", packed)):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError(f"pcnerf::query_eval: {name} must be a contiguous float32 device tensor")
+    if z.dim() != 2 or rays.dim() != 2 or rays.shape[0] != z.shape[0] or rays.shape[1] < 6:
+        raise RuntimeError(f"pcnerf::query_eval: rays (R, >=6) and z (R, S) expected, got {tuple(rays.shape)} and "
+                           f"{tuple(z.shape)}")
+    if packed.numel() != _packed_floats():
+        raise RuntimeError(f"pcnerf::query_eval: packed must be pcnerf::pack_eval's image ({_packed_floats()} floats), "
+                           f"got {packed.numel()}")
+    if not (rays.device == z.device == packed.device):
+        raise RuntimeError("pcnerf::query_eval: rays, z and packed must be on one device")
+
+
 @torch.library.custom_op(f"{NS}::pack_eval", mutates_args=())
 def pack_eval(params: list[Tensor]) -> Tensor:
     """The eval network image (BatchNorm folded, MFMA operand order) from the module's 50 tensors in
@@ -95,10 +145,13 @@ def pack_eval(params: list[Tensor]) -> Tensor:
     if len(params) != 50:
         raise RuntimeError(f"pcnerf::pack_eval takes 50 parameter tensors, got {len(params)}")
     s = H.NofParams()
-    for t in params:
+    for i, (t, shp) in enumerate(zip(params, _param_shapes())):
         H.require_device(t)
         if t.dtype != torch.float32 or not t.is_contiguous():
             raise RuntimeError("NOF parameters must be contiguous float32 device tensors")
+        if tuple(t.shape) != shp:
+            raise RuntimeError(f"pcnerf::pack_eval: parameter {i} has shape {tuple(t.shape)}, expected {shp} "
+                               "(NOF(feature_size=256, in_channels_xy=63, use_skip=True))")
     for i in range(8):
         s.lin_w[i], s.lin_b[i] = params[i].data_ptr(), params[8 + i].data_ptr()
         s.bn_w[i], s.bn_b[i] = params[16 + i].data_ptr(), params[24 + i].data_ptr()
@@ -126,6 +179,7 @@ def eval_params(model) -> list:
 @torch.library.custom_op(f"{NS}::query_eval", mutates_args=())
 def query_eval(rays: Tensor, z: Tensor, packed: Tensor) -> Tensor:
     """Eval-mode occupancy p (R, S) of o + d z through Embedding + NOF (render.py:18-25, models.py:183-203)."""
+    _check_query(rays, z, packed)
     R, S = z.shape
     p = torch.empty((R, S), dtype=torch.float32, device=z.device)
     H.check(H.lib().pcnerf_nof_query_eval(rays.data_ptr(), R, rays.shape[1], z.data_ptr(), S, packed.data_ptr(),
@@ -143,6 +197,9 @@ def _(rays, z, packed):
 def composite(p: Tensor, z: Tensor, noise: Optional[Tensor], noise_std: float, eps: float, rays: Optional[Tensor],
               cn_col: int, cf_col: int, range_col: int, want_weights: bool) -> tuple[Tensor, Tensor, Tensor, Tensor]:
     """(weights (R,S) or (0,), depth (R,), free_ray (R,) or (0,), sl1_ray (R,) or (0,)): render.py:51-61, 75-159."""
+    _need("composite", "z", z, (None, None))
+    _need("composite", "p", p, tuple(z.shape))
+    _need("composite", "rays", rays, (z.shape[0], None))
     w, d, fr, sl = _ops.composite(p, z, noise, noise_std, eps, rays, cn_col, cf_col, range_col, want_weights)
     e = z.new_empty((0,))
     return (w if w is not None else e), d, (fr if fr is not None else e.clone()), (sl if sl is not None else e.clone())
@@ -160,6 +217,8 @@ def _(p, z, noise, noise_std, eps, rays, cn_col, cf_col, range_col, want_weights
 def composite_extras(p: Tensor, z: Tensor, noise: Optional[Tensor], noise_std: float,
                      eps: float) -> tuple[Tensor, Tensor, Tensor, Tensor]:
     """render_rays's compositing (render.py:538-611): (weights, depth, opacity mean (), depth2 (R,))."""
+    _need("composite_extras", "z", z, (None, None))
+    _need("composite_extras", "p", p, tuple(z.shape))
     w, d, _, _, om, d2 = _ops.composite(p, z, noise, noise_std, eps, extras=True)
     return w, d, om, d2
 
@@ -174,6 +233,9 @@ def _(p, z, noise, noise_std, eps):
 def child_losses(free_ray: Tensor, sl1_ray: Tensor, rays: Tensor, divide: bool,
                  sub_nerf_test_num: int) -> tuple[Tensor, Tensor]:
     """(child_free_loss, child_depth_loss): (1,) each in the divide branch, () otherwise (render.py:102-159)."""
+    _need("child_losses", "free_ray", free_ray, (None,))
+    _need("child_losses", "sl1_ray", sl1_ray, tuple(free_ray.shape))
+    _need("child_losses", "rays", rays, (free_ray.shape[0], ("min", 10)))
     a, b = _ops.child_losses(free_ray, sl1_ray, rays, divide, sub_nerf_test_num)
     return a.clone(), b.clone()
 
@@ -190,6 +252,9 @@ def view_rows(p: Tensor, z: Tensor, rows: Tensor, method: int,
               eps: float) -> tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
     """inference_0525_2's per-row stage (render.py:229-330): weights, depth, at_peak (uint8), child sum, per-row
     opacity terms (float64), points (R, 3)."""
+    _need("view_rows", "z", z, (None, None))
+    _need("view_rows", "p", p, tuple(z.shape))
+    _need("view_rows", "rows", rows, (z.shape[0], ("min", 8)))
     return _ops.view_rows(p, z, rows, method, eps)
 
 

@@ -89,3 +89,61 @@ def test_torch_compile_render_rays_val():
         assert torch.equal(got[k], want[k]), k
     for op in ("sample_coarse", "pack_eval", "query_eval", "composite", "resample"):
         assert any(f"pcnerf.{op}" in s for s in seen), (op, sorted(set(seen)))
+
+
+def test_param_shapes_match_module():
+    """pcnerf::pack_eval's shape check is the module's own layout (models.py), tensor for tensor."""
+    from nof.networks import NOF_coarse
+    got = [tuple(t.shape) for t in T.eval_params(NOF_coarse())]
+    assert got == T._param_shapes() and len(got) == 50
+
+
+@pytest.mark.gpu
+def test_operators_reject_bad_layouts():
+    """The public operators check on the host what their kernels' grids and reads assume: wrong shapes, strides,
+    dtypes or image sizes raise before any launch."""
+    from nof import synthetic as syn
+    from nof.networks import NOF_coarse
+    P = torch.ops.pcnerf
+    mc = syn.load_into(NOF_coarse(), syn.init_nof_params(7)).cuda().eval()
+    params = T.eval_params(mc)
+    packed = P.pack_eval(params)
+    rays = torch.from_numpy(syn.make_rays(64, seed=3)).cuda()
+    z = torch.linspace(1, 20, 32, device="cuda").expand(64, 32).contiguous()
+    assert P.query_eval(rays, z, packed).shape == (64, 32)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        P.query_eval(rays, z.t().contiguous().t(), packed)
+    with pytest.raises(RuntimeError, match="expected"):
+        P.query_eval(rays[:63].contiguous(), z, packed)
+    with pytest.raises(RuntimeError, match="pack_eval's image"):
+        P.query_eval(rays, z, packed[:-1].contiguous())
+    bad = list(params)
+    bad[4] = torch.zeros(256, 256, device="cuda")   # the skip layer takes 319 inputs
+    with pytest.raises(RuntimeError, match="expected"):
+        P.pack_eval(bad)
+
+
+@pytest.mark.gpu
+def test_tensor_operators_reject_mismatched_operands():
+    """Each tensor-level operator checks its operands' rows / shapes / contiguity on the host before the launch."""
+    P = torch.ops.pcnerf
+    dev = "cuda"
+    rays = torch.rand(32, 15, device=dev) + 1.0
+    z = torch.sort(torch.rand(32, 16, device=dev) * 10 + 1, dim=1).values.contiguous()
+    p = torch.rand(32, 16, device=dev)
+    with pytest.raises(RuntimeError, match="expected"):
+        P.perturb(z, 1.0, torch.rand(32, 15, device=dev))
+    with pytest.raises(RuntimeError, match="expected"):
+        P.resample(z, p[:, :15].contiguous(), 8, None)
+    with pytest.raises(RuntimeError, match="expected"):
+        P.composite(p[:31].contiguous(), z, None, 0.0, 1e-10, rays, 10, 11, 14, True)
+    with pytest.raises(RuntimeError, match="expected"):
+        P.composite(p, z, None, 0.0, 1e-10, rays[:31].contiguous(), 10, 11, 14, True)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        P.composite(p.t().contiguous().t(), z, None, 0.0, 1e-10, rays, 10, 11, 14, True)
+    with pytest.raises(RuntimeError, match="expected"):
+        P.view_rows(p, z, rays[:, :7].contiguous(), 2, 1e-10)
+    w, d, fr, sl = P.composite(p, z, None, 0.0, 1e-10, rays, 10, 11, 14, True)
+    with pytest.raises(RuntimeError, match="expected"):
+        P.child_losses(fr, sl[:31].contiguous(), rays, False, 4)
+    assert P.resample(z, w, 8, None).shape == (32, 24)
