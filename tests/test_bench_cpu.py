@@ -120,3 +120,12 @@ def test_cpu_baseline_sample_is_fixed(bench):
         return t[0]
     best, out, n = bench._best_of(fn, reps=3, long_s=1e9)
     assert n == 3 and out == 3
+
+
+def test_dist_on_only_for_n_ranks_or_the_test_switch(bench, monkeypatch):
+    """The N-rank path runs for world > 1, and at world 1 only under the test-only PCNERF_BENCH_FORCE_DIST=1 (the
+    one-rank RCCL test); the driver's default N = 1 run never initialises a process group."""
+    monkeypatch.delenv("PCNERF_BENCH_FORCE_DIST", raising=False)
+    assert not bench.dist_on(1) and bench.dist_on(2) and bench.dist_on(8)
+    monkeypatch.setenv("PCNERF_BENCH_FORCE_DIST", "1")
+    assert bench.dist_on(1)
