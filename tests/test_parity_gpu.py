@@ -420,6 +420,32 @@ def test_render_val_eval_shell_setting():
         close(res[k], ref[k].numpy(), RTOL, 1e-9, k)
 
 
+@pytest.mark.parametrize("method", [1, 2])
+def test_render_view_eval_shell_setting(method):
+    """The two-step inference at the reference eval shells' sampling (N_samples 4096, N_importance 8192, chunk
+    184320; eval_kitti_render.py renders through render_rays_view_0525_2_2 at exactly this): 12,288 fine samples per
+    row -- k_view_rows' largest per-row buffers (48 KiB, one wave per workgroup) and its widest template -- and the
+    ray-group walk, against the oracle on a few synthetic groups."""
+    rows, other, _ = syn.make_view_rows(5, seed=41)
+    # occupancy bias -9: per-sample occupancy ~1e-4, so transmittance survives 12,288 samples and the depths land
+    # inside the rays (at the default -4 a random net's weights pile up in the first few hundred samples)
+    pc_np, pf_np = syn.init_nof_params(SEED_C, occ_bias=-9.0), syn.init_nof_params(SEED_F, occ_bias=-9.0)
+    mc = syn.load_into(NOF_coarse(), pc_np).to(DEV).eval()
+    mf = syn.load_into(NOF_fine(), pf_np).to(DEV).eval()
+    emb = Embedding(3, 10)
+    kw = dict(N_samples=4096, N_importance=8192, perturb=0, noise_std=0, chunk=184320)
+    with torch.no_grad():
+        res = R.render_rays_view_0525_2_2(mc, mf, emb, torch.from_numpy(rows).to(DEV), torch.from_numpy(other).to(DEV),
+                                          depth_inference_method=method, **kw)
+    Pc, Pf = O.params_from_numpy(pc_np), O.params_from_numpy(pf_np)
+    ref = O.render_rays_view(Pc, Pf, torch.from_numpy(rows), torch.from_numpy(other), N_samples=4096,
+                             N_importance=8192, chunk=184320, method=method)
+    for k in ("rays_effective_flag", "rays_effective_flag_fine"):
+        assert np.array_equal(res[k].cpu().numpy(), ref[k].numpy().reshape(res[k].shape)), k
+    for k in ("depth", "depth_fine", "points_inference", "points_inference_fine"):
+        close(res[k], ref[k].numpy(), RTOL, 1e-6, k)
+
+
 def test_empty_rays_raise_like_the_reference():
     """Zero rays: the reference's chunk loop collects nothing and torch.cat([]) raises (render.py:18-25, 44-51);
     the HIP path refuses the empty input with an exception too, never a silent empty result."""
