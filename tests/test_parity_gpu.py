@@ -478,6 +478,32 @@ def test_render_train_vs_oracle_config2_subset(train_math):
         close(res[k], ref[k].numpy(), RTOL, 1e-9, k)
 
 
+def test_render_train_reference_shell_setting():
+    """The reference's training shells' sampling (shells/pretraining/*_train.bash: 256 rays, N_samples 768,
+    N_importance 1536, chunk 262144, segmented 0.1, child losses): one coarse BatchNorm chunk of 196,608 samples and
+    fine chunks of 262,144 + 262,144 + 65,536, against the CPU oracle -- depths, the four child losses and both
+    networks' running statistics after every chunk's update (default train math).  Occupancy bias -7.5: with
+    768 + 2304 samples per ray the default -4 puts every ray's weight in its first samples."""
+    rays = syn.make_rays(256, seed=13)
+    pc_np, pf_np = syn.init_nof_params(SEED_C, occ_bias=-7.5), syn.init_nof_params(SEED_F, occ_bias=-7.5)
+    mc = syn.load_into(NOF_coarse(), pc_np).to(DEV).train(True)
+    mf = syn.load_into(NOF_fine(), pf_np).to(DEV).train(True)
+    emb = Embedding(3, 10)
+    kw = dict(sub_nerf_test_num=32, N_samples=768, N_importance=1536, perturb=0, noise_std=0, chunk=262144,
+              issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0, use_child_nerf_loss=1)
+    with torch.no_grad():
+        res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays).to(DEV), **kw)
+    Pc, Pf = O.params_from_numpy(pc_np), O.params_from_numpy(pf_np)
+    with torch.no_grad():
+        ref = O.render_rays_train(Pc, Pf, torch.from_numpy(rays), **kw)
+    for k in ("depth", "depth_fine", "child_free_loss", "child_depth_loss", "child_free_loss_fine",
+              "child_depth_loss_fine"):
+        close(res[k], ref[k].numpy(), RTOL, 1e-9, k)
+    for m, P in ((mc, Pc), (mf, Pf)):
+        want = np.stack([np.stack([P[b + ".running_mean"].numpy(), P[b + ".running_var"].numpy()]) for b in O.BN])
+        close(running(m), want, RTOL, 1e-7, "running stats")
+
+
 @pytest.mark.parametrize("chunk", [50, 1000, 262144])
 def test_render_train_tiny_and_odd_chunks(chunk, train_math):
     """BatchNorm chunks of 50 samples (two 32-sample tiles, the second partial: a 2-workgroup grid), 1000 and one
