@@ -481,9 +481,11 @@ def test_render_train_vs_oracle_config2_subset(train_math):
 def test_render_train_reference_shell_setting():
     """The reference's training shells' sampling (shells/pretraining/*_train.bash: 256 rays, N_samples 768,
     N_importance 1536, chunk 262144, segmented 0.1, child losses): one coarse BatchNorm chunk of 196,608 samples and
-    fine chunks of 262,144 + 262,144 + 65,536, against the CPU oracle -- depths, the four child losses and both
-    networks' running statistics after every chunk's update (default train math).  Occupancy bias -7.5: with
-    768 + 2304 samples per ray the default -4 puts every ray's weight in its first samples."""
+    fine chunks of 262,144 + 262,144 + 65,536 (default train math).  At 2,304 samples per ray the float32 oracle's
+    own rounding moves depth_fine by ~2e-4 with its thread count, so the reference value is the oracle's float64
+    evaluation (make_f64.py's): every entry within 1e-4 of it, or within 1.5 x the float32 oracle's own largest
+    error; the running statistics of both networks after every chunk's update within 1e-4.  Occupancy bias -7.5:
+    with 768 + 2304 samples per ray the default -4 puts every ray's weight in its first samples."""
     rays = syn.make_rays(256, seed=13)
     pc_np, pf_np = syn.init_nof_params(SEED_C, occ_bias=-7.5), syn.init_nof_params(SEED_F, occ_bias=-7.5)
     mc = syn.load_into(NOF_coarse(), pc_np).to(DEV).train(True)
@@ -493,13 +495,19 @@ def test_render_train_reference_shell_setting():
               issegmentated=1, childnerf_ratio=0.1, use_child_nerf_divide=0, use_child_nerf_loss=1)
     with torch.no_grad():
         res = R.render_rays_train(mc, mf, emb, torch.from_numpy(rays).to(DEV), **kw)
-    Pc, Pf = O.params_from_numpy(pc_np), O.params_from_numpy(pf_np)
-    with torch.no_grad():
-        ref = O.render_rays_train(Pc, Pf, torch.from_numpy(rays), **kw)
+        ref = O.render_rays_train(O.params_from_numpy(pc_np), O.params_from_numpy(pf_np), torch.from_numpy(rays),
+                                  **kw)
+        P64 = [{k: (v.double() if v.is_floating_point() else v) for k, v in O.params_from_numpy(q).items()}
+               for q in (pc_np, pf_np)]
+        r64 = O.render_rays_train(P64[0], P64[1], torch.from_numpy(rays), **kw, f64=True)
     for k in ("depth", "depth_fine", "child_free_loss", "child_depth_loss", "child_free_loss_fine",
               "child_depth_loss_fine"):
-        close(res[k], ref[k].numpy(), RTOL, 1e-9, k)
-    for m, P in ((mc, Pc), (mf, Pf)):
+        want = r64[k].numpy().astype(np.float64)
+        e_hip = np.abs(res[k].cpu().numpy().astype(np.float64) - want) / np.maximum(np.abs(want), 1e-30)
+        e_ref = np.abs(ref[k].numpy().astype(np.float64) - want) / np.maximum(np.abs(want), 1e-30)
+        _report({"case": f"train_shell_{k}", "vs_f64_max": float(e_hip.max()), "ref_vs_f64_max": float(e_ref.max())})
+        assert e_hip.max() <= max(RTOL, 1.5 * e_ref.max()), (k, float(e_hip.max()), float(e_ref.max()))
+    for m, P in ((mc, P64[0]), (mf, P64[1])):
         want = np.stack([np.stack([P[b + ".running_mean"].numpy(), P[b + ".running_var"].numpy()]) for b in O.BN])
         close(running(m), want, RTOL, 1e-7, "running stats")
 
